@@ -1,0 +1,205 @@
+/*
+ * yoda.h — C-ABI of libyoda, the MI355X-native Yoda Filter/Score hot path.
+ *
+ * This is the drop-in boundary a Go kube-scheduler plugin binds through cgo (see
+ * INTEGRATION.md).  It replaces the per-pair Go calls the scheduler framework makes into
+ * the reference plugin with one call per pod batch:
+ *
+ *   reference (Mr-LvGJ/kubernetes-scheduler)            replaced by
+ *   ---------------------------------------------       -----------------------------------
+ *   filter.PodFitsNumber/Memory/Clock                   yoda_run  (K1: feasibility sweep)
+ *     pkg/yoda/filter/filter.go:11-58
+ *   collection.CollectMaxValues (PreScore)              yoda_run  (K1: per-pod maxima)
+ *     pkg/yoda/collection/collection.go:30-76
+ *   score.CalculateBasicScore/Card/Allocate/Actual      yoda_run  (K2: integer card score)
+ *     pkg/yoda/score/algorithm.go:96,264-310
+ *   score.BalancedCpuDiskIOPriority (live Mode B)       yoda_run  (mode YODA_MODE_DISKIO)
+ *     pkg/yoda/score/algorithm.go:99-119
+ *   Yoda.Score + filter.Uint64ToInt64                   yoda_run  (K2)
+ *     pkg/yoda/scheduler.go:116-156, filter.go:84-86
+ *   Yoda.NormalizeScore + k8s v1.22.3 selectHost        yoda_run  (K2 argmax + finalize)
+ *     pkg/yoda/scheduler.go:158-183
+ *   sort.Less / GetPodPriority (greedy batch order)     yoda_greedy
+ *     pkg/yoda/sort/sort.go:8-18
+ *
+ * Conventions:
+ *   - every entry point returns int: YODA_OK (0) or a negative YODA_ERR_* code; the
+ *     message of the last failure is in yoda_last_error();
+ *   - no C++ exception crosses the boundary; all buffers are caller-owned;
+ *   - a handle is NOT thread-safe: one handle per goroutine, or guard it;
+ *   - "d_" pointer arguments are device pointers (HIP global memory on the handle's
+ *     device); everything else is host memory.
+ *
+ * Integer widths follow the reference on GOARCH=amd64 (Makefile:4): Go `uint` is 64-bit.
+ */
+#ifndef YODA_H_
+#define YODA_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YODA_ABI_VERSION 1
+
+/* Maximum card slots per node (SCV Status.CardList length). */
+#define YODA_MAX_CARDS 16
+
+/* ---- status codes ------------------------------------------------------------------ */
+#define YODA_OK 0
+#define YODA_ERR_INVALID_ARG -1   /* NULL handle/pointer, bad size, bad mode            */
+#define YODA_ERR_HIP -2           /* a HIP runtime call failed                          */
+#define YODA_ERR_NO_NODES -3      /* yoda_run/yoda_eval before yoda_upload_nodes        */
+#define YODA_ERR_NO_PODS -4       /* yoda_run before yoda_upload_pods                   */
+#define YODA_ERR_RANGE -5         /* input outside what the library can represent       */
+#define YODA_ERR_NO_DEVICE -6     /* no HIP device / bad device ordinal                 */
+#define YODA_ERR_STATE -7         /* call out of sequence (e.g. phase2 before phase1)   */
+
+/* ---- scoring modes ----------------------------------------------------------------- */
+/* Mode A: the SCV GPU path (filter.go + collection.go + algorithm.go:264-310 composed as
+ * algorithm.go:96).  Mode B: the score the shipped binary computes
+ * (BalancedCpuDiskIOPriority, algorithm.go:99-119; Filter is a pass-through). */
+#define YODA_MODE_SCV 0
+#define YODA_MODE_DISKIO 1
+
+/* ---- per-pod outcome (the framework Status the reference would produce) ------------ */
+#define YODA_PICK_NONE (-1)  /* no feasible node: Unschedulable                          */
+#define YODA_PICK_ERROR (-2) /* framework Error (see status)                             */
+
+#define YODA_STATUS_OK 0             /* pick is a node index                              */
+#define YODA_STATUS_UNSCHEDULABLE 1  /* no node passed Filter                              */
+#define YODA_STATUS_DIV_ZERO 2       /* a scored node has TotalMemorySum == 0: the
+                                        reference panics (algorithm.go:294 / :309)        */
+#define YODA_STATUS_SCORE_RANGE 3    /* NormalizeScore produced a score outside [0,100]
+                                        (int64 overflow at scheduler.go:178); k8s rejects */
+
+/* Node snapshot, struct-of-arrays.  Node i's card slot j lives at [i * max_cards + j];
+ * slots j >= card_count[i] are ignored.  Mirrors the SCV CRD Status
+ * (github.com/NJUPT-ISL/SCV api/v1 @46b36eeed646, types pinned by use: filter.go:13,22,53,57,
+ * collection.go:14-20, algorithm.go:294,305-309). */
+typedef struct yoda_node_soa {
+  uint32_t n_nodes;
+  uint32_t max_cards;                /* stride of the card arrays, 1..YODA_MAX_CARDS        */
+  const uint64_t* card_number;       /* [N] Status.CardNumber                              */
+  const uint32_t* card_count;        /* [N] len(Status.CardList), <= max_cards             */
+  const uint64_t* free_memory_sum;   /* [N] Status.FreeMemorySum                           */
+  const uint64_t* total_memory_sum;  /* [N] Status.TotalMemorySum                          */
+  const uint64_t* alloc_memory;      /* [N] sum of scv/memory labels of pods already bound
+                                        to the node (algorithm.go:299-303); may be NULL=0   */
+  const uint64_t* card_free_memory;  /* [N*K] Card.FreeMemory                              */
+  const uint64_t* card_total_memory; /* [N*K] Card.TotalMemory                             */
+  const uint64_t* card_clock;        /* [N*K] Card.Clock                                   */
+  const uint64_t* card_bandwidth;    /* [N*K] Card.Bandwidth                               */
+  const uint64_t* card_core;         /* [N*K] Card.Core                                    */
+  const uint64_t* card_power;        /* [N*K] Card.Power                                   */
+  const uint8_t* card_healthy;       /* [N*K] Card.Health == "Healthy"                     */
+  /* Mode B inputs: advisor.NodeInfo (advisor.go:26-32).  May be NULL for Mode A. */
+  const double* cpu;                 /* [N] NodeInfo.Cpu   (percent)                       */
+  const double* disk_io;             /* [N] NodeInfo.DiskIO (MB/s)                         */
+} yoda_node_soa;
+
+/* Pod requests, struct-of-arrays, already parsed from labels with the reference's Go
+ * semantics (strconv.Atoi; negative values wrap to uint64 — filter.go:60-74). */
+typedef struct yoda_pod_soa {
+  uint32_t n_pods;
+  const uint8_t* has_number;   /* [P] label scv/number present (filter.go:12)               */
+  const uint64_t* number;      /* [P] strToUint(scv/number)                                */
+  const uint8_t* has_memory;   /* [P] label scv/memory present (filter.go:19)               */
+  const uint64_t* memory;      /* [P] StrToUint64(scv/memory)                              */
+  const uint8_t* has_clock;    /* [P] label scv/clock present (filter.go:36)                */
+  const uint64_t* clock;       /* [P] strToUint(scv/clock)                                 */
+  const int64_t* priority;     /* [P] Atoi(scv/priority) (sort.go:12-18); may be NULL = 0   */
+  /* Mode B: may be NULL for Mode A. */
+  const double* rio;           /* [P] ParseFloat(annotations["diskIO"], 32) (algorithm.go:103) */
+  const int64_t* rcpu;         /* [P] CalculatePodResourceRequest(cpu) millicores (:104,238) */
+} yoda_pod_soa;
+
+/* Per-pod outputs of yoda_eval / yoda_download.  Any pointer may be NULL. */
+typedef struct yoda_eval_out {
+  int32_t* pick;         /* [P] node index (global), YODA_PICK_NONE or YODA_PICK_ERROR     */
+  int32_t* status;       /* [P] YODA_STATUS_*                                              */
+  uint32_t* n_feasible;  /* [P] nodes that passed Filter                                   */
+  uint32_t* n_ties;      /* [P] nodes sharing the top normalized score (the set k8s
+                            selectHost draws from at random)                              */
+  int64_t* top_score;    /* [P] raw Score (after Uint64ToInt64) of the picked node         */
+  uint64_t* maxima;      /* [P*6] Mode A PreScore maxima in MaxValue order (collection.go:
+                            14-21): Bandwidth, Clock, Core, FreeMemory, Power, TotalMemory */
+} yoda_eval_out;
+
+typedef struct yoda_handle yoda_t;
+
+/* ---- lifecycle ---------------------------------------------------------------------- */
+int yoda_abi_version(void);
+/* One handle drives one GPU (device ordinal).  Multi-GPU: one handle per GPU, each holding
+ * a node shard, merged by the caller's collectives through the yoda_shard_* entry points. */
+int yoda_create(int device, yoda_t** out);
+int yoda_destroy(yoda_t* h);
+const char* yoda_last_error(const yoda_t* h);
+/* Launch all work on this HIP stream (hipStream_t passed as void*); NULL = the handle's own. */
+int yoda_set_stream(yoda_t* h, void* hip_stream);
+int yoda_synchronize(yoda_t* h);
+
+/* ---- node snapshot ------------------------------------------------------------------ */
+/* Upload a node snapshot (or a shard of one).  node_offset is the global index of this
+ * shard's first node: picks are reported as node_offset + local index.  Replaces the
+ * previous snapshot.  Chooses the exact-f64 fast path or the exact-u64 generic path from
+ * the value ranges; flags: YODA_UPLOAD_FORCE_GENERIC. */
+#define YODA_UPLOAD_FORCE_GENERIC 1u
+int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nodes, uint32_t node_offset,
+                      uint32_t flags);
+/* 1 if the uploaded snapshot runs on the generic (u64) path, 0 on the fast path. */
+int yoda_uses_generic_path(const yoda_t* h);
+/* Replace alloc_memory (the Allocate-score input) without re-uploading the cards. */
+int yoda_update_alloc(yoda_t* h, const uint64_t* alloc_memory);
+
+/* ---- one-shot evaluation ------------------------------------------------------------ */
+/* Schedule every pod independently against the uploaded snapshot (each pod sees the same
+ * snapshot: a batch of independent scheduling cycles).  Equivalent to
+ * yoda_upload_pods + yoda_run + yoda_download. */
+int yoda_eval(yoda_t* h, const yoda_pod_soa* pods, int mode, yoda_eval_out* out);
+
+/* ---- split evaluation (device-resident timing, multi-GPU) --------------------------- */
+int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pods);
+/* Run filter+prescore+score+normalize+select for the uploaded pods; results stay on the
+ * device until yoda_download.  Asynchronous on the handle's stream. */
+#define YODA_RUN_BITMASK 1u /* also materialise the feasibility bitmask for download      */
+int yoda_run(yoda_t* h, int mode, uint32_t flags);
+int yoda_download(yoda_t* h, yoda_eval_out* out);
+/* Feasibility bitmask of the last yoda_run with YODA_RUN_BITMASK: bit (n & 31) of
+ * words[p * ((N + 31) / 32) + n / 32] is set iff node n (local) passed Filter for pod p. */
+int yoda_download_bitmask(yoda_t* h, uint32_t* words, uint64_t n_words);
+
+/* Sharded evaluation.  Each rank holds a node shard; between phases the caller reduces
+ * the exchange buffers across ranks (RCCL all-reduce) with the op named per buffer.
+ *   phase1 -> d_maxima [6*P] u64 (MAX), d_counts [2*P] u32 (SUM: n_feasible, n_zero_total)
+ *   phase2 (reads reduced maxima/counts) -> d_best [P] i64 (MAX), d_idx [P] u32, d_ties [P]
+ *            u32, d_lowest [P] i64 (MIN)
+ *   prepare_merge (reads reduced d_best) -> masks d_idx (MIN) and d_ties (SUM) in place
+ *   finalize (reads reduced buffers) -> picks into the handle, then yoda_download. */
+int yoda_shard_phase1(yoda_t* h, int mode, uint64_t* d_maxima, uint32_t* d_counts);
+int yoda_shard_phase2(yoda_t* h, int mode, const uint64_t* d_maxima, const uint32_t* d_counts,
+                      int64_t* d_best, uint32_t* d_idx, uint32_t* d_ties, int64_t* d_lowest);
+int yoda_shard_prepare_merge(yoda_t* h, const int64_t* d_best_global, const int64_t* d_best_local,
+                             uint32_t* d_idx, uint32_t* d_ties);
+int yoda_shard_finalize(yoda_t* h, int mode, const uint32_t* d_counts, const int64_t* d_best,
+                        const uint32_t* d_idx, const uint32_t* d_ties, const int64_t* d_lowest);
+/* Generic path only: pods whose NormalizeScore can overflow int64 are re-evaluated with
+ * the exact normalize (scheduler.go:176-179).  Returns the number of such pods in *n_pods. */
+int yoda_shard_overflow_count(yoda_t* h, uint32_t* n_pods);
+
+/* ---- greedy batch ------------------------------------------------------------------- */
+/* Schedule the pods one after another in queue order (sort.go:8-10: scv/priority
+ * descending, then input index), each pick feeding the next cycle through the node's
+ * Allocate score (alloc_memory += scv/memory, algorithm.go:299-303; the scheduler-cache
+ * "assume" of SURVEY §3.4).  YODA_GREEDY_CARD_CAPACITY additionally decrements the picked
+ * node's CardNumber by the pod's number (saturating at 0): a build-defined extension.
+ * The uploaded snapshot is left unchanged. */
+#define YODA_GREEDY_CARD_CAPACITY 1u
+int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, int32_t* pick);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* YODA_H_ */
