@@ -1,0 +1,205 @@
+#!/usr/bin/env python3
+"""bench.py — pod-node pair evals/s of the Yoda Filter/Score/select hot path on MI355X.
+
+Metric (BASELINE.json): pod-node pair evals/sec (filter+score+select) at 100k x 100k,
+bit-exact picks.  One step = feasibility + PreScore maxima + score + NormalizeScore/select of
+ALL P pods over ALL N nodes (percentageOfNodesToScore 100), node snapshot and pods already
+resident in HBM, picks left in device memory.  Workload: BASELINE config 3 (100k pods x 100k
+nodes, K=8, seed 7; synthetic data), nodes sharded across ranks for --gpus N (strong
+scaling: total work fixed), merged by RCCL all-reduces (yoda_amd/dist.py).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  Besides the contract fields it carries `roofline` (dominant
+kernel: algorithmic bytes / HIP-event-timed launch duration vs 8 TB/s) and `cpu_baseline`
+(the C oracle, reference-shaped, on a bounded pod sample, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "kubernetes-scheduler_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from yoda_amd import synth  # noqa: E402
+from yoda_amd.capi import Yoda  # noqa: E402
+from yoda_amd.soa import MODE_DISKIO, MODE_SCV  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def bytes_per_pair(k: int, mode: int) -> int:
+    """SURVEY.md §8d / BASELINE.md: one consult of the compact node record,
+    B_node = 32*K + 40 B (Mode B: 16 B)."""
+    return 16 if mode == MODE_DISKIO else 32 * k + 40
+
+
+def cpu_baseline(nodes, pods, mode, target_s: float, threads: int, gpu_res):
+    """Time the C oracle (scalar, reference-shaped) on a bounded pod sample; also checks the
+    sample's picks against the GPU's (the oracle is the checker here)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # noqa: E402  (cpu_baseline leg only)
+    oracle.lib()
+    probe = min(pods.n_pods, 4 * threads)
+    t0 = time.perf_counter()
+    oracle.schedule(nodes, pods.slice(0, probe), mode, threads=threads)
+    rate = probe * nodes.n_nodes / (time.perf_counter() - t0)
+    sample = int(max(probe, min(pods.n_pods, rate * target_s / nodes.n_nodes)))
+    sub = pods.slice(0, sample)
+    t0 = time.perf_counter()
+    want = oracle.schedule(nodes, sub, mode, threads=threads)
+    dt = time.perf_counter() - t0
+    parity = bool(np.array_equal(want.pick, gpu_res.pick[:sample]) and
+                  np.array_equal(want.status, gpu_res.status[:sample]))
+    return {"value": sample * nodes.n_nodes / dt, "unit": "pairs/s", "cores": threads,
+            "kind": "port",
+            "sample": f"first {sample} pods x all {nodes.n_nodes} nodes of the same workload, "
+                      f"C oracle (yoda_oracle.c, reference-shaped: per pod filter, "
+                      f"CollectMaxValues, score, normalize, select), OpenMP {threads} threads, "
+                      f"{dt:.1f} s",
+            "sample_picks_match_gpu": parity}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--pods", type=int, default=None)
+    ap.add_argument("--nodes", type=int, default=None)
+    ap.add_argument("--mode", choices=["scv", "diskio"], default="scv")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    mode = MODE_SCV if args.mode == "scv" else MODE_DISKIO
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+
+    nodes, pods = synth.make_config(args.config, pods=args.pods, nodes=args.nodes)
+    P, N = pods.n_pods, nodes.n_nodes
+    from yoda_amd.dist import ShardExchange, shard_bounds
+    b = shard_bounds(N, world)
+    lo, hi = int(b[rank]), int(b[rank + 1])
+    y = Yoda(local_rank)
+    y.upload_nodes(nodes.slice(lo, hi), node_offset=lo)
+    y.upload_pods(pods)
+    y.set_stream(torch.cuda.current_stream(device).cuda_stream)
+    k_slots = int(nodes.card_count.max()) if N else 1
+    k_slots = 1 << max(0, (k_slots - 1).bit_length())
+
+    if world > 1:
+        ex = ShardExchange.distributed(y, device)
+        step = lambda: ex.step(mode)  # noqa: E731
+    else:
+        step = lambda: y.run(mode)  # noqa: E731
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize(device)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    y.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    y.profile(False)
+    k1_ms, k2_ms, launches = y.profile_read()
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # End-to-end (pod H2D + kernels + picks D2H), single GPU only: reported, never `value`.
+    e2e_ms = None
+    if world == 1:
+        t0 = time.perf_counter()
+        res = y.eval(pods, mode)
+        e2e_ms = (time.perf_counter() - t0) * 1e3
+    else:
+        res = y.download()
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = P * N / (elapsed / args.steps)
+    n_local = hi - lo
+    # dominant kernel of this rank: K2 (score) unless K1 takes longer
+    k1_avg = k1_ms / max(launches, 1)
+    k2_avg = k2_ms / max(launches, 1)
+    dom, dom_ms = ("k2_score", k2_avg) if k2_avg >= k1_avg else ("k1_filter_maxima", k1_avg)
+    algo_bytes = P * n_local * bytes_per_pair(k_slots, mode)
+    achieved = algo_bytes / (dom_ms / 1e3) / 1e9 if dom_ms > 0 else 0.0
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "pmc_latest.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": "pod-node pair evals/sec (filter+score+select) at 100k×100k; bit-exact picks",
+        "value": value,
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64" if mode == MODE_SCV and not y.generic else ("int64" if mode == MODE_SCV
+                                                                   else "f64"),
+        "data": "synthetic (seeded SCV node records and pod requests, yoda_amd/synth.py)",
+        "config": {"workload": f"config{args.config}: {P} pods x {N} nodes, "
+                               f"{'Mode A SCV GPU score' if mode == MODE_SCV else 'Mode B diskIO'}"
+                               f", K={k_slots} card slots",
+                   "pods": P, "nodes": N, "mode": args.mode,
+                   "path": "generic-u64" if y.generic else "fast-f64",
+                   "parallelism": f"node-shard x{world}" + (" (RCCL all-reduce merge)"
+                                                            if world > 1 else "")},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "avg_launch_ms": dom_ms, "k1_avg_ms": k1_avg, "k2_avg_ms": k2_avg,
+                     "bytes_per_pair": bytes_per_pair(k_slots, mode),
+                     "pairs_per_launch": P * n_local},
+        "e2e_ms": e2e_ms,
+        "status_counts": {str(s): int((res.status == s).sum()) for s in np.unique(res.status)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(nodes, pods, mode, args.cpu_seconds,
+                                           args.cpu_threads, res)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    y.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -136,8 +136,11 @@ int yoda_abi_version(void);
 int yoda_create(int device, yoda_t** out);
 int yoda_destroy(yoda_t* h);
 const char* yoda_last_error(const yoda_t* h);
-/* Launch all work on this HIP stream (hipStream_t passed as void*); NULL = the handle's own. */
+/* Launch all work on this HIP stream (hipStream_t passed as void*; NULL = the HIP null
+ * stream, e.g. PyTorch's default stream).  Until called, the handle uses a non-blocking
+ * stream of its own; yoda_use_own_stream switches back to it. */
 int yoda_set_stream(yoda_t* h, void* hip_stream);
+int yoda_use_own_stream(yoda_t* h);
 int yoda_synchronize(yoda_t* h);
 
 /* ---- node snapshot ------------------------------------------------------------------ */
@@ -187,6 +190,13 @@ int yoda_shard_finalize(yoda_t* h, int mode, const uint32_t* d_counts, const int
 /* Generic path only: pods whose NormalizeScore can overflow int64 are re-evaluated with
  * the exact normalize (scheduler.go:176-179).  Returns the number of such pods in *n_pods. */
 int yoda_shard_overflow_count(yoda_t* h, uint32_t* n_pods);
+
+/* ---- kernel timing ----------------------------------------------------------------- */
+/* enable != 0: every subsequent K1 / K2 launch is bracketed by HIP events recorded on the
+ * launch stream.  yoda_profile_read synchronizes, returns the summed K1 and K2 durations
+ * (ms) and launch count since the last read, and clears them. */
+int yoda_profile(yoda_t* h, int enable);
+int yoda_profile_read(yoda_t* h, double* k1_ms, double* k2_ms, uint32_t* n_launches);
 
 /* ---- greedy batch ------------------------------------------------------------------- */
 /* Schedule the pods one after another in queue order (sort.go:8-10: scv/priority

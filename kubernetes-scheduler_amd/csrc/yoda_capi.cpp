@@ -1,0 +1,869 @@
+// yoda_capi.cpp — host side of libyoda: the C-ABI of include/yoda.h.
+//
+// Packs the node snapshot and pod requests into the device layout of yoda_layout.h, picks
+// the exact-f64 fast path or the exact-u64 generic path, and sequences the kernels of
+// yoda_kernels.hip on the handle's stream.  No exception crosses the C boundary.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/yoda.h"
+#include "yoda_layout.h"
+
+namespace yoda {
+// launchers (yoda_kernels.hip)
+hipError_t launch_k1(int K, bool fast, const unsigned char* nodes, uint32_t n_nodes,
+                     uint32_t chunk_nodes, uint32_t C, const PodParams& pp, uint32_t n_pods,
+                     const Partials& part, uint32_t* bitmask, hipStream_t s);
+hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool fast,
+                          uint64_t* maxima, uint32_t* counts, hipStream_t s);
+hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, hipStream_t s);
+hipError_t launch_k2(int K, bool fast, const unsigned char* nodes, uint32_t n_nodes,
+                     uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
+                     const double* rcp, uint32_t n_pods, const uint32_t* bitmask,
+                     const Partials& part, hipStream_t s);
+hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
+                            uint32_t C, const PodParams& pp, uint32_t n_pods, const Partials& part,
+                            hipStream_t s);
+hipError_t launch_reduce2(const Partials& part, uint32_t C, uint32_t n_pods, bool is_f64,
+                          uint32_t node_offset, int64_t* best, uint32_t* idx, uint32_t* ties,
+                          int64_t* low, hipStream_t s);
+hipError_t launch_merge_prepare(const int64_t* best_global, const int64_t* best_local,
+                                uint32_t n_pods, uint32_t* idx, uint32_t* ties, hipStream_t s);
+hipError_t launch_fill_diskio_state(uint32_t n_pods, uint32_t n_nodes, uint64_t* maxima,
+                                    uint32_t* counts, hipStream_t s);
+hipError_t launch_finalize(const uint32_t* counts, const int64_t* best, const uint32_t* idx,
+                           const uint32_t* ties_in, const int64_t* lowest, uint32_t n_pods,
+                           bool generic, int32_t* pick, int32_t* status, uint32_t* ties_out,
+                           uint32_t* flagged, uint32_t* n_flagged, hipStream_t s);
+hipError_t launch_k3(int K, const unsigned char* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
+                     uint32_t C, const PodParams& pp, const uint64_t* maxima, uint32_t n_pods,
+                     const uint32_t* bitmask, const uint32_t* flagged, const uint32_t* n_flagged,
+                     const int64_t* best, const int64_t* low, const Partials& part,
+                     uint32_t max_flagged, hipStream_t s);
+hipError_t launch_reduce3(const Partials& part, uint32_t C, const uint32_t* flagged,
+                          const uint32_t* n_flagged, uint32_t max_flagged, uint32_t node_offset,
+                          int32_t* pick, int32_t* status, uint32_t* ties, hipStream_t s);
+hipError_t launch_bitmask_transpose(const uint32_t* in, uint32_t W, uint32_t n_pods,
+                                    uint32_t* out, hipStream_t s);
+}  // namespace yoda
+
+using namespace yoda;
+
+namespace {
+
+struct Status {
+  int code;
+  std::string msg;
+};
+
+// Grow-only device buffer.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= bytes) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    const size_t alloc = std::max<size_t>(n, 256);
+    hipError_t e = hipMalloc(&p, alloc);
+    if (e == hipSuccess) bytes = alloc;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+}  // namespace
+
+struct yoda_handle {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t own_stream = nullptr;
+  std::string last_error;
+
+  // node snapshot
+  bool has_nodes = false;
+  bool generic = false;
+  bool nodes_diskio = false;  // node cpu/disk_io present
+  bool pods_diskio = false;   // pod rio/rcpu present
+  int K = 1;
+  uint32_t n_nodes = 0, node_offset = 0;
+  DevBuf nodes;     // fast or generic records
+  DevBuf nodes_b;   // Mode B records
+  std::vector<unsigned char> host_records;  // kept for alloc updates (greedy)
+  std::vector<uint64_t> h_total_sum, h_free_sum;
+
+  // pods
+  bool has_pods = false;
+  uint32_t n_pods = 0;
+  std::vector<uint64_t> h_pod_mem;      // scv/memory (0 if absent) for greedy alloc
+  std::vector<uint8_t> h_pod_has_mem;
+  std::vector<uint64_t> h_pod_number;   // PodFitsNumber operand
+  DevBuf pod_m_f, pod_c_f, pod_m_u, pod_c_u, pod_number, pod_need_mem, pod_need_clk, pod_alpha,
+      pod_beta;
+
+  // state
+  DevBuf maxima, counts, rcp, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
+  DevBuf bitmask, bitmask_t;
+  DevBuf p_max_f, p_max_u, p_cnt, p_best_f, p_best_i, p_idx, p_ties, p_low_f, p_low_i, p_err;
+  uint32_t C = 1, chunk_nodes = 32;
+  int last_mode = -1;
+  bool ran = false;
+  bool ran_bitmask = false;
+  bool phase1_done = false;
+
+  // profiling: event pairs around K1 / K2
+  bool profiling = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_k1, ev_k2;
+  size_t ev_used = 0;
+
+  hipEvent_t next_event() {
+    if (ev_used == ev_pool.size()) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      ev_pool.push_back(e);
+    }
+    return ev_pool[ev_used++];
+  }
+
+  ~yoda_handle() {
+    for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
+    DevBuf* all[] = {&nodes, &nodes_b, &pod_m_f, &pod_c_f, &pod_m_u, &pod_c_u, &pod_number,
+                     &pod_need_mem, &pod_need_clk, &pod_alpha, &pod_beta, &maxima, &counts, &rcp,
+                     &best, &idx, &ties, &lowest, &pick, &status, &ties_out, &flagged, &n_flagged,
+                     &bitmask, &bitmask_t, &p_max_f, &p_max_u, &p_cnt, &p_best_f, &p_best_i,
+                     &p_idx, &p_ties, &p_low_f, &p_low_i, &p_err};
+    for (DevBuf* b : all) b->release();
+    if (own_stream) (void)hipStreamDestroy(own_stream);
+  }
+};
+
+namespace {
+
+int fail(yoda_t* h, int code, const std::string& msg) {
+  if (h) h->last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(h, expr)                                                                \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(h, YODA_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+int pow2_cards(uint32_t kmax) {
+  int k = 1;
+  while ((uint32_t)k < kmax) k <<= 1;
+  return k;
+}
+
+// CalculateAllocateScore + CalculateActualScore (algorithm.go:293-310), uint64 wrap.
+// zero_total: TotalMemorySum == 0, where the reference divides by zero.
+uint64_t static_score(uint64_t free_sum, uint64_t total_sum, uint64_t alloc, bool* zero_total) {
+  *zero_total = total_sum == 0;
+  if (total_sum == 0) return 0;
+  const uint64_t allocate = total_sum < alloc ? 0 : (total_sum - alloc) * 100u / total_sum * 3u;
+  const uint64_t actual = (free_sum * 100u / total_sum) * 2u;
+  return allocate + actual;
+}
+
+// Pick chunking: enough workgroups to fill 256 CUs several times over.
+void plan_chunks(yoda_t* h, uint32_t n_pods, uint32_t n_nodes) {
+  const uint32_t pod_blocks = std::max<uint32_t>(1, (n_pods + kBlock - 1) / kBlock);
+  const uint32_t max_chunks = std::max<uint32_t>(1, (n_nodes + kChunkAlign - 1) / kChunkAlign);
+  uint32_t C = std::min(max_chunks, std::max<uint32_t>(1, (2048 + pod_blocks - 1) / pod_blocks));
+  uint32_t chunk = (n_nodes + C - 1) / C;
+  chunk = std::max<uint32_t>(kChunkAlign, (chunk + kChunkAlign - 1) / kChunkAlign * kChunkAlign);
+  h->chunk_nodes = chunk;
+  h->C = std::max<uint32_t>(1, (n_nodes + chunk - 1) / chunk);
+}
+
+int ensure_state(yoda_t* h, uint32_t P) {
+  const size_t CP = (size_t)h->C * P;
+  const size_t W = (h->n_nodes + 31) / 32;
+  HIP_TRY(h, h->maxima.ensure(6 * (size_t)P * 8));
+  HIP_TRY(h, h->counts.ensure(2 * (size_t)P * 4));
+  HIP_TRY(h, h->rcp.ensure(5 * (size_t)P * 8));
+  HIP_TRY(h, h->best.ensure((size_t)P * 8));
+  HIP_TRY(h, h->idx.ensure((size_t)P * 4));
+  HIP_TRY(h, h->ties.ensure((size_t)P * 4));
+  HIP_TRY(h, h->lowest.ensure((size_t)P * 8));
+  HIP_TRY(h, h->pick.ensure((size_t)P * 4));
+  HIP_TRY(h, h->status.ensure((size_t)P * 4));
+  HIP_TRY(h, h->ties_out.ensure((size_t)P * 4));
+  HIP_TRY(h, h->flagged.ensure((size_t)P * 4));
+  HIP_TRY(h, h->n_flagged.ensure(16));
+  HIP_TRY(h, h->bitmask.ensure(W * P * 4));
+  if (h->generic) {
+    HIP_TRY(h, h->p_max_u.ensure(6 * CP * 8));
+    HIP_TRY(h, h->p_best_i.ensure(CP * 8));
+    HIP_TRY(h, h->p_low_i.ensure(CP * 8));
+    HIP_TRY(h, h->p_err.ensure(CP * 4));
+  } else {
+    HIP_TRY(h, h->p_max_f.ensure(6 * CP * 8));
+  }
+  HIP_TRY(h, h->p_best_f.ensure(CP * 8));
+  HIP_TRY(h, h->p_low_f.ensure(CP * 8));
+  HIP_TRY(h, h->p_cnt.ensure(2 * CP * 4));
+  HIP_TRY(h, h->p_idx.ensure(CP * 4));
+  HIP_TRY(h, h->p_ties.ensure(CP * 4));
+  return YODA_OK;
+}
+
+PodParams pod_params(yoda_t* h) {
+  PodParams pp;
+  pp.m_f = h->pod_m_f.as<double>();
+  pp.c_f = h->pod_c_f.as<double>();
+  pp.m_u = h->pod_m_u.as<uint64_t>();
+  pp.c_u = h->pod_c_u.as<uint64_t>();
+  pp.number = h->pod_number.as<uint64_t>();
+  pp.need_mem = h->pod_need_mem.as<uint32_t>();
+  pp.need_clk = h->pod_need_clk.as<uint32_t>();
+  pp.alpha = h->pod_alpha.as<double>();
+  pp.beta = h->pod_beta.as<double>();
+  return pp;
+}
+
+Partials partials(yoda_t* h) {
+  Partials p;
+  p.max_f = h->p_max_f.as<double>();
+  p.max_u = h->p_max_u.as<uint64_t>();
+  p.cnt = h->p_cnt.as<uint32_t>();
+  p.best_f = h->p_best_f.as<double>();
+  p.best_i = h->p_best_i.as<int64_t>();
+  p.idx = h->p_idx.as<uint32_t>();
+  p.ties = h->p_ties.as<uint32_t>();
+  p.low_f = h->p_low_f.as<double>();
+  p.low_i = h->p_low_i.as<int64_t>();
+  p.err = h->p_err.as<uint32_t>();
+  return p;
+}
+
+int check_ready(yoda_t* h, int mode) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  if (mode != YODA_MODE_SCV && mode != YODA_MODE_DISKIO)
+    return fail(h, YODA_ERR_INVALID_ARG, "mode must be YODA_MODE_SCV or YODA_MODE_DISKIO");
+  if (!h->has_nodes) return fail(h, YODA_ERR_NO_NODES, "no node snapshot uploaded");
+  if (!h->has_pods) return fail(h, YODA_ERR_NO_PODS, "no pods uploaded");
+  if (mode == YODA_MODE_DISKIO && !(h->nodes_diskio && h->pods_diskio))
+    return fail(h, YODA_ERR_INVALID_ARG, "Mode B needs node cpu/disk_io and pod rio/rcpu");
+  HIP_TRY(h, hipSetDevice(h->device));
+  return YODA_OK;
+}
+
+// Phase 1: Filter + PreScore maxima (Mode A), or the all-feasible state (Mode B).
+int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts) {
+  const uint32_t P = h->n_pods;
+  if (P == 0) return YODA_OK;
+  if (mode == YODA_MODE_DISKIO) {
+    HIP_TRY(h, launch_fill_diskio_state(P, h->n_nodes, maxima, counts, h->stream));
+    return YODA_OK;
+  }
+  if (h->n_nodes == 0) {
+    HIP_TRY(h, hipMemsetAsync(counts, 0, 2 * (size_t)P * 4, h->stream));
+    std::vector<uint64_t> ones(6 * (size_t)P, 1);
+    HIP_TRY(h, hipMemcpyAsync(maxima, ones.data(), ones.size() * 8, hipMemcpyHostToDevice,
+                              h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    return YODA_OK;
+  }
+  Partials part = partials(h);
+  hipEvent_t e0 = h->profiling ? h->next_event() : nullptr;
+  hipEvent_t e1 = h->profiling ? h->next_event() : nullptr;
+  if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
+  HIP_TRY(h, launch_k1(h->K, !h->generic, h->nodes.as<unsigned char>(), h->n_nodes, h->chunk_nodes,
+                       h->C, pod_params(h), P, part, h->bitmask.as<uint32_t>(), h->stream));
+  if (e1) {
+    HIP_TRY(h, hipEventRecord(e1, h->stream));
+    h->ev_k1.emplace_back(e0, e1);
+  }
+  HIP_TRY(h, launch_reduce1(part, h->C, P, !h->generic, maxima, counts, h->stream));
+  return YODA_OK;
+}
+
+// Phase 2: Score over the feasible nodes with the (globally reduced) maxima.
+int phase2(yoda_t* h, int mode, const uint64_t* maxima, int64_t* best, uint32_t* idx,
+           uint32_t* ties, int64_t* low) {
+  const uint32_t P = h->n_pods;
+  if (P == 0) return YODA_OK;
+  if (h->n_nodes == 0) {
+    std::vector<int64_t> neg(P, -1), big(P, INT64_MAX);
+    std::vector<uint32_t> none(P, 0xffffffffu);
+    HIP_TRY(h, hipMemcpyAsync(best, neg.data(), (size_t)P * 8, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(low, big.data(), (size_t)P * 8, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(idx, none.data(), (size_t)P * 4, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(h, hipMemsetAsync(ties, 0, (size_t)P * 4, h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    return YODA_OK;
+  }
+  Partials part = partials(h);
+  bool is_f64 = true;
+  hipEvent_t e0 = h->profiling ? h->next_event() : nullptr;
+  hipEvent_t e1 = h->profiling ? h->next_event() : nullptr;
+  if (mode == YODA_MODE_SCV && !h->generic)
+    HIP_TRY(h, launch_prep2(maxima, P, h->rcp.as<double>(), h->stream));
+  if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
+  if (mode == YODA_MODE_DISKIO) {
+    HIP_TRY(h, launch_k2_diskio(h->nodes_b.as<NodeRecB>(), h->n_nodes, h->chunk_nodes, h->C,
+                                pod_params(h), P, part, h->stream));
+  } else {
+    HIP_TRY(h, launch_k2(h->K, !h->generic, h->nodes.as<unsigned char>(), h->n_nodes,
+                         h->chunk_nodes, h->C, pod_params(h), maxima, h->rcp.as<double>(), P,
+                         h->bitmask.as<uint32_t>(), part, h->stream));
+    is_f64 = !h->generic;
+  }
+  if (e1) {
+    HIP_TRY(h, hipEventRecord(e1, h->stream));
+    h->ev_k2.emplace_back(e0, e1);
+  }
+  HIP_TRY(h, launch_reduce2(part, h->C, P, is_f64, h->node_offset, best, idx, ties, low,
+                            h->stream));
+  return YODA_OK;
+}
+
+// Finalize into the handle's pick/status/ties; runs K3 for generic-path overflow pods.
+int finalize(yoda_t* h, int mode, const uint32_t* counts, const int64_t* best,
+             const uint32_t* idx, const uint32_t* ties, const int64_t* low, bool sharded) {
+  const uint32_t P = h->n_pods;
+  if (P == 0) return YODA_OK;
+  const bool generic = h->generic && mode == YODA_MODE_SCV;
+  HIP_TRY(h, hipMemsetAsync(h->n_flagged.p, 0, 4, h->stream));
+  HIP_TRY(h, launch_finalize(counts, best, idx, ties, low, P, generic, h->pick.as<int32_t>(),
+                             h->status.as<int32_t>(), h->ties_out.as<uint32_t>(),
+                             h->flagged.as<uint32_t>(), h->n_flagged.as<uint32_t>(), h->stream));
+  if (generic) {
+    uint32_t nfl = 0;
+    HIP_TRY(h, hipMemcpyAsync(&nfl, h->n_flagged.p, 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    if (nfl > 0) {
+      if (sharded)
+        return fail(h, YODA_ERR_STATE,
+                    "exact-normalize pods (int64 overflow in NormalizeScore) are not supported "
+                    "on the sharded path yet; evaluate on a single handle");
+      Partials part = partials(h);
+      HIP_TRY(h, launch_k3(h->K, h->nodes.as<unsigned char>(), h->n_nodes, h->chunk_nodes, h->C,
+                           pod_params(h), h->maxima.as<uint64_t>(), P, h->bitmask.as<uint32_t>(),
+                           h->flagged.as<uint32_t>(), h->n_flagged.as<uint32_t>(), best, low,
+                           part, nfl, h->stream));
+      HIP_TRY(h, launch_reduce3(part, h->C, h->flagged.as<uint32_t>(), h->n_flagged.as<uint32_t>(),
+                                nfl, h->node_offset, h->pick.as<int32_t>(), h->status.as<int32_t>(),
+                                h->ties_out.as<uint32_t>(), h->stream));
+    }
+  }
+  return YODA_OK;
+}
+
+bool is_pow2_le16(uint32_t k) { return k == 1 || k == 2 || k == 4 || k == 8 || k == 16; }
+
+}  // namespace
+
+// ======================================================================================
+extern "C" {
+
+int yoda_abi_version(void) { return YODA_ABI_VERSION; }
+
+int yoda_create(int device, yoda_t** out) {
+  if (!out) return YODA_ERR_INVALID_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return YODA_ERR_NO_DEVICE;
+  if (device < 0 || device >= n) return YODA_ERR_NO_DEVICE;
+  yoda_t* h = new (std::nothrow) yoda_t();
+  if (!h) return YODA_ERR_INVALID_ARG;
+  h->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return YODA_ERR_HIP;
+  }
+  h->stream = h->own_stream;
+  *out = h;
+  return YODA_OK;
+}
+
+int yoda_destroy(yoda_t* h) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  delete h;
+  return YODA_OK;
+}
+
+const char* yoda_last_error(const yoda_t* h) {
+  return h ? h->last_error.c_str() : "null handle";
+}
+
+int yoda_set_stream(yoda_t* h, void* hip_stream) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  h->stream = static_cast<hipStream_t>(hip_stream);
+  return YODA_OK;
+}
+
+int yoda_use_own_stream(yoda_t* h) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  h->stream = h->own_stream;
+  return YODA_OK;
+}
+
+int yoda_synchronize(yoda_t* h) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return YODA_OK;
+}
+
+int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, uint32_t flags) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  try {
+    if (!nd) return fail(h, YODA_ERR_INVALID_ARG, "nodes is NULL");
+    const uint32_t N = nd->n_nodes, KS = nd->max_cards;
+    if (KS < 1 || KS > YODA_MAX_CARDS)
+      return fail(h, YODA_ERR_INVALID_ARG, "max_cards must be in 1..16");
+    if (N > 0 && (!nd->card_number || !nd->card_count || !nd->free_memory_sum ||
+                  !nd->total_memory_sum || !nd->card_free_memory || !nd->card_total_memory ||
+                  !nd->card_clock || !nd->card_bandwidth || !nd->card_core || !nd->card_power ||
+                  !nd->card_healthy))
+      return fail(h, YODA_ERR_INVALID_ARG, "a required node array is NULL");
+    if ((uint64_t)node_offset + N > 0x7fffffffull)
+      return fail(h, YODA_ERR_RANGE, "node index exceeds int32");
+    HIP_TRY(h, hipSetDevice(h->device));
+    uint32_t kmax = 1;
+    for (uint32_t i = 0; i < N; ++i) {
+      if (nd->card_count[i] > KS) return fail(h, YODA_ERR_INVALID_ARG, "card_count > max_cards");
+      kmax = std::max(kmax, nd->card_count[i]);
+    }
+    const int K = pow2_cards(kmax);
+    // Exactness check for the f64 fast path.
+    bool fast = !(flags & YODA_UPLOAD_FORCE_GENERIC);
+    std::vector<uint64_t> stat(N);
+    std::vector<uint8_t> zt(N);
+    uint64_t max_clock = 0, max_static = 0;
+    for (uint32_t i = 0; i < N && true; ++i) {
+      bool z = false;
+      const uint64_t alloc = nd->alloc_memory ? nd->alloc_memory[i] : 0;
+      stat[i] = static_score(nd->free_memory_sum[i], nd->total_memory_sum[i], alloc, &z);
+      zt[i] = z;
+      max_static = std::max(max_static, stat[i]);
+      for (uint32_t j = 0; j < nd->card_count[i]; ++j) {
+        const size_t k = (size_t)i * KS + j;
+        const uint64_t v[6] = {nd->card_free_memory[k], nd->card_total_memory[k],
+                               nd->card_clock[k],       nd->card_bandwidth[k],
+                               nd->card_core[k],        nd->card_power[k]};
+        for (uint64_t x : v)
+          if (x > kFastFieldMax) fast = false;
+        max_clock = std::max(max_clock, nd->card_clock[k]);
+      }
+    }
+    if (fast) {
+      // per-card score <= 800 + 100*clock (5 quotients <= 100, clock/MaxBandwidth <= 100*clock)
+      const long double bound = (long double)K * (800.0L + 100.0L * (long double)max_clock) +
+                                (long double)max_static;
+      if (bound >= (long double)kFastScoreMax) fast = false;
+    }
+    // Build records.
+    const size_t stride = node_stride(K);
+    std::vector<unsigned char> rec((size_t)std::max<uint32_t>(N, 1) * stride, 0);
+    for (uint32_t i = 0; i < N; ++i) {
+      unsigned char* r = rec.data() + (size_t)i * stride;
+      uint32_t hm = 0;
+      for (uint32_t j = 0; j < nd->card_count[i]; ++j)
+        if (nd->card_healthy[(size_t)i * KS + j]) hm |= 1u << j;
+      if (fast) {
+        NodeHdrF hd{};
+        hd.static_score = (double)stat[i];
+        hd.card_number = nd->card_number[i];
+        hd.healthy_mask = hm;
+        hd.zero_total = zt[i];
+        std::memcpy(r, &hd, sizeof(hd));
+        double* f = reinterpret_cast<double*>(r + sizeof(hd));
+        for (uint32_t j = 0; j < nd->card_count[i]; ++j) {
+          const size_t k = (size_t)i * KS + j;
+          f[kFree * K + j] = (double)nd->card_free_memory[k];
+          f[kClock * K + j] = (double)nd->card_clock[k];
+          f[kTotal * K + j] = (double)nd->card_total_memory[k];
+          f[kBandwidth * K + j] = (double)nd->card_bandwidth[k];
+          f[kCore * K + j] = (double)nd->card_core[k];
+          f[kPower * K + j] = (double)nd->card_power[k];
+        }
+      } else {
+        NodeHdrG hd{};
+        hd.static_score = stat[i];
+        hd.card_number = nd->card_number[i];
+        hd.healthy_mask = hm;
+        hd.zero_total = zt[i];
+        std::memcpy(r, &hd, sizeof(hd));
+        uint64_t* f = reinterpret_cast<uint64_t*>(r + sizeof(hd));
+        for (uint32_t j = 0; j < nd->card_count[i]; ++j) {
+          const size_t k = (size_t)i * KS + j;
+          f[kFree * K + j] = nd->card_free_memory[k];
+          f[kClock * K + j] = nd->card_clock[k];
+          f[kTotal * K + j] = nd->card_total_memory[k];
+          f[kBandwidth * K + j] = nd->card_bandwidth[k];
+          f[kCore * K + j] = nd->card_core[k];
+          f[kPower * K + j] = nd->card_power[k];
+        }
+      }
+    }
+    HIP_TRY(h, h->nodes.ensure(rec.size()));
+    HIP_TRY(h, hipMemcpyAsync(h->nodes.p, rec.data(), rec.size(), hipMemcpyHostToDevice,
+                              h->stream));
+    const bool diskio = nd->cpu && nd->disk_io;
+    if (diskio && N > 0) {
+      std::vector<NodeRecB> rb(N);
+      for (uint32_t i = 0; i < N; ++i) {
+        rb[i].v = nd->cpu[i] / 100.0;     // algorithm.go:73
+        rb[i].u = nd->disk_io[i] / 50.0;  // algorithm.go:71
+      }
+      HIP_TRY(h, h->nodes_b.ensure((size_t)N * sizeof(NodeRecB)));
+      HIP_TRY(h, hipMemcpyAsync(h->nodes_b.p, rb.data(), (size_t)N * sizeof(NodeRecB),
+                                hipMemcpyHostToDevice, h->stream));
+    }
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    h->host_records.swap(rec);
+    h->h_total_sum.assign(nd->total_memory_sum, nd->total_memory_sum + N);
+    h->h_free_sum.assign(nd->free_memory_sum, nd->free_memory_sum + N);
+    h->nodes_diskio = diskio;
+    h->n_nodes = N;
+    h->node_offset = node_offset;
+    h->K = K;
+    h->generic = !fast;
+    h->has_nodes = true;
+    h->ran = false;
+    h->phase1_done = false;
+    if (!is_pow2_le16((uint32_t)K)) return fail(h, YODA_ERR_INVALID_ARG, "bad K");
+    return YODA_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(h, YODA_ERR_INVALID_ARG, "host allocation failed");
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
+int yoda_uses_generic_path(const yoda_t* h) { return h ? (h->generic ? 1 : 0) : -1; }
+
+int yoda_update_alloc(yoda_t* h, const uint64_t* alloc) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  if (!h->has_nodes) return fail(h, YODA_ERR_NO_NODES, "no node snapshot uploaded");
+  if (!alloc && h->n_nodes) return fail(h, YODA_ERR_INVALID_ARG, "alloc is NULL");
+  try {
+    HIP_TRY(h, hipSetDevice(h->device));
+    const size_t stride = node_stride(h->K);
+    uint64_t max_static = 0;
+    for (uint32_t i = 0; i < h->n_nodes; ++i) {
+      bool z = false;
+      const uint64_t s = static_score(h->h_free_sum[i], h->h_total_sum[i], alloc[i], &z);
+      unsigned char* r = h->host_records.data() + (size_t)i * stride;
+      if (h->generic) {
+        reinterpret_cast<NodeHdrG*>(r)->static_score = s;
+      } else {
+        reinterpret_cast<NodeHdrF*>(r)->static_score = (double)s;
+        max_static = std::max(max_static, s);
+      }
+    }
+    if (!h->generic && max_static >= (1ull << 51))
+      return fail(h, YODA_ERR_RANGE, "static score leaves the fast path; re-upload the nodes");
+    HIP_TRY(h, hipMemcpyAsync(h->nodes.p, h->host_records.data(), h->host_records.size(),
+                              hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    return YODA_OK;
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
+int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  try {
+    if (!pd) return fail(h, YODA_ERR_INVALID_ARG, "pods is NULL");
+    const uint32_t P = pd->n_pods;
+    if (P > 0 && (!pd->has_number || !pd->number || !pd->has_memory || !pd->memory ||
+                  !pd->has_clock || !pd->clock))
+      return fail(h, YODA_ERR_INVALID_ARG, "a required pod array is NULL");
+    HIP_TRY(h, hipSetDevice(h->device));
+    const uint64_t kClamp = 1ull << 53;  // > every fast-path card field (<= 2^44)
+    std::vector<double> mf(P), cf(P), al(P), be(P);
+    std::vector<uint64_t> mu(P), cu(P), num(P);
+    std::vector<uint32_t> nm(P), nc(P);
+    h->h_pod_mem.assign(P, 0);
+    h->h_pod_has_mem.assign(P, 0);
+    h->h_pod_number.assign(P, 1);
+    for (uint32_t p = 0; p < P; ++p) {
+      const uint64_t number = pd->has_number[p] ? pd->number[p] : 1;  // filter.go:12-15
+      const uint64_t m = pd->has_memory[p] ? pd->memory[p] : 0;       // filter.go:19,32
+      const uint64_t c = pd->has_clock[p] ? pd->clock[p] : 0;         // filter.go:36,49
+      const uint32_t need = number > 0xffffffffull ? 0xffffffffu : (uint32_t)number;
+      num[p] = number;
+      nm[p] = pd->has_memory[p] ? need : 0;
+      nc[p] = pd->has_clock[p] ? need : 0;
+      mu[p] = m;
+      cu[p] = c;
+      mf[p] = (double)std::min(m, kClamp);
+      cf[p] = (double)std::min(c, kClamp);
+      h->h_pod_mem[p] = pd->memory[p];
+      h->h_pod_has_mem[p] = pd->has_memory[p];
+      h->h_pod_number[p] = number;
+      if (pd->rio && pd->rcpu) {  // algorithm.go:105-106
+        const double beta = 1.0 / (1.0 + (double)pd->rcpu[p] / pd->rio[p]);
+        be[p] = beta;
+        al[p] = 1 - beta;
+      }
+    }
+    auto up = [&](DevBuf& b, const void* src, size_t bytes) -> int {
+      HIP_TRY(h, b.ensure(bytes));
+      if (bytes) HIP_TRY(h, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, h->stream));
+      return YODA_OK;
+    };
+    int rc;
+    if ((rc = up(h->pod_m_f, mf.data(), P * 8ull)) ||
+        (rc = up(h->pod_c_f, cf.data(), P * 8ull)) ||
+        (rc = up(h->pod_m_u, mu.data(), P * 8ull)) ||
+        (rc = up(h->pod_c_u, cu.data(), P * 8ull)) ||
+        (rc = up(h->pod_number, num.data(), P * 8ull)) ||
+        (rc = up(h->pod_need_mem, nm.data(), P * 4ull)) ||
+        (rc = up(h->pod_need_clk, nc.data(), P * 4ull)) ||
+        (rc = up(h->pod_alpha, al.data(), P * 8ull)) || (rc = up(h->pod_beta, be.data(), P * 8ull)))
+      return rc;
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    h->n_pods = P;
+    h->has_pods = true;
+    h->ran = false;
+    h->phase1_done = false;
+    h->pods_diskio = pd->rio != nullptr && pd->rcpu != nullptr;
+    return YODA_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(h, YODA_ERR_INVALID_ARG, "host allocation failed");
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
+static int prepare_run(yoda_t* h, int mode) {
+  int rc = check_ready(h, mode);
+  if (rc) return rc;
+  plan_chunks(h, h->n_pods, h->n_nodes);
+  return ensure_state(h, std::max<uint32_t>(h->n_pods, 1));
+}
+
+int yoda_run(yoda_t* h, int mode, uint32_t flags) {
+  int rc = prepare_run(h, mode);
+  if (rc) return rc;
+  try {
+    if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>()))) return rc;
+    if ((rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->best.as<int64_t>(),
+                     h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>())))
+      return rc;
+    if ((rc = finalize(h, mode, h->counts.as<uint32_t>(), h->best.as<int64_t>(),
+                       h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(),
+                       false)))
+      return rc;
+    h->ran = true;
+    h->ran_bitmask = mode == YODA_MODE_SCV && (flags & YODA_RUN_BITMASK);
+    h->last_mode = mode;
+    return YODA_OK;
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
+int yoda_download(yoda_t* h, yoda_eval_out* out) {
+  if (!h || !out) return YODA_ERR_INVALID_ARG;
+  if (!h->ran) return fail(h, YODA_ERR_STATE, "yoda_download before yoda_run/finalize");
+  try {
+    HIP_TRY(h, hipSetDevice(h->device));
+    const uint32_t P = h->n_pods;
+    if (P == 0) return YODA_OK;
+    hipStream_t s = h->stream;
+    if (out->pick)
+      HIP_TRY(h, hipMemcpyAsync(out->pick, h->pick.p, P * 4ull, hipMemcpyDeviceToHost, s));
+    if (out->status)
+      HIP_TRY(h, hipMemcpyAsync(out->status, h->status.p, P * 4ull, hipMemcpyDeviceToHost, s));
+    if (out->n_feasible)
+      HIP_TRY(h, hipMemcpyAsync(out->n_feasible, h->counts.p, P * 4ull, hipMemcpyDeviceToHost, s));
+    if (out->n_ties)
+      HIP_TRY(h, hipMemcpyAsync(out->n_ties, h->ties_out.p, P * 4ull, hipMemcpyDeviceToHost, s));
+    std::vector<int64_t> top;
+    std::vector<int32_t> st;
+    if (out->top_score) {
+      top.resize(P);
+      st.resize(P);
+      HIP_TRY(h, hipMemcpyAsync(top.data(), h->best.p, P * 8ull, hipMemcpyDeviceToHost, s));
+      HIP_TRY(h, hipMemcpyAsync(st.data(), h->status.p, P * 4ull, hipMemcpyDeviceToHost, s));
+    }
+    std::vector<uint64_t> mx;
+    if (out->maxima) {
+      mx.resize(6 * (size_t)P);
+      HIP_TRY(h, hipMemcpyAsync(mx.data(), h->maxima.p, mx.size() * 8, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(h, hipStreamSynchronize(s));
+    if (out->top_score)
+      for (uint32_t p = 0; p < P; ++p) out->top_score[p] = st[p] == YODA_STATUS_OK ? top[p] : 0;
+    if (out->maxima)
+      for (uint32_t p = 0; p < P; ++p)
+        for (int f = 0; f < 6; ++f) out->maxima[(size_t)p * 6 + f] = mx[(size_t)f * P + p];
+    return YODA_OK;
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
+int yoda_download_bitmask(yoda_t* h, uint32_t* words, uint64_t n_words) {
+  if (!h || !words) return YODA_ERR_INVALID_ARG;
+  if (!h->ran_bitmask)
+    return fail(h, YODA_ERR_STATE, "no bitmask: run Mode A with YODA_RUN_BITMASK first");
+  const uint32_t W = (h->n_nodes + 31) / 32;
+  const uint64_t need = (uint64_t)W * h->n_pods;
+  if (n_words < need) return fail(h, YODA_ERR_INVALID_ARG, "bitmask buffer too small");
+  if (need == 0) return YODA_OK;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, h->bitmask_t.ensure(need * 4));
+  HIP_TRY(h, launch_bitmask_transpose(h->bitmask.as<uint32_t>(), W, h->n_pods,
+                                      h->bitmask_t.as<uint32_t>(), h->stream));
+  HIP_TRY(h, hipMemcpyAsync(words, h->bitmask_t.p, need * 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return YODA_OK;
+}
+
+int yoda_eval(yoda_t* h, const yoda_pod_soa* pods, int mode, yoda_eval_out* out) {
+  int rc = yoda_upload_pods(h, pods);
+  if (rc) return rc;
+  if ((rc = yoda_run(h, mode, 0))) return rc;
+  return yoda_download(h, out);
+}
+
+// ---- sharded entry points -------------------------------------------------------------
+int yoda_shard_phase1(yoda_t* h, int mode, uint64_t* d_maxima, uint32_t* d_counts) {
+  int rc = prepare_run(h, mode);
+  if (rc) return rc;
+  if (!d_maxima || !d_counts) return fail(h, YODA_ERR_INVALID_ARG, "NULL exchange buffer");
+  try {
+    if ((rc = phase1(h, mode, d_maxima, d_counts))) return rc;
+    h->phase1_done = true;
+    h->ran = false;
+    return YODA_OK;
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
+int yoda_shard_phase2(yoda_t* h, int mode, const uint64_t* d_maxima, const uint32_t* d_counts,
+                      int64_t* d_best, uint32_t* d_idx, uint32_t* d_ties, int64_t* d_lowest) {
+  int rc = check_ready(h, mode);
+  if (rc) return rc;
+  if (!h->phase1_done) return fail(h, YODA_ERR_STATE, "yoda_shard_phase2 before phase1");
+  if (!d_maxima || !d_counts || !d_best || !d_idx || !d_ties || !d_lowest)
+    return fail(h, YODA_ERR_INVALID_ARG, "NULL exchange buffer");
+  try {
+    const uint32_t P = h->n_pods;
+    // keep the reduced maxima for download and the generic exact-normalize pass
+    if (P) HIP_TRY(h, hipMemcpyAsync(h->maxima.p, d_maxima, 6ull * P * 8, hipMemcpyDeviceToDevice,
+                                     h->stream));
+    (void)d_counts;
+    return phase2(h, mode, h->maxima.as<uint64_t>(), d_best, d_idx, d_ties, d_lowest);
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
+int yoda_shard_prepare_merge(yoda_t* h, const int64_t* d_best_global, const int64_t* d_best_local,
+                             uint32_t* d_idx, uint32_t* d_ties) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  if (!d_best_global || !d_best_local || !d_idx || !d_ties)
+    return fail(h, YODA_ERR_INVALID_ARG, "NULL exchange buffer");
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (h->n_pods == 0) return YODA_OK;
+  HIP_TRY(h, launch_merge_prepare(d_best_global, d_best_local, h->n_pods, d_idx, d_ties,
+                                  h->stream));
+  return YODA_OK;
+}
+
+int yoda_shard_finalize(yoda_t* h, int mode, const uint32_t* d_counts, const int64_t* d_best,
+                        const uint32_t* d_idx, const uint32_t* d_ties, const int64_t* d_lowest) {
+  int rc = check_ready(h, mode);
+  if (rc) return rc;
+  if (!d_counts || !d_best || !d_idx || !d_ties || !d_lowest)
+    return fail(h, YODA_ERR_INVALID_ARG, "NULL exchange buffer");
+  try {
+    const uint32_t P = h->n_pods;
+    if (P) {
+      HIP_TRY(h, hipMemcpyAsync(h->counts.p, d_counts, 2ull * P * 4, hipMemcpyDeviceToDevice,
+                                h->stream));
+      HIP_TRY(h, hipMemcpyAsync(h->best.p, d_best, P * 8ull, hipMemcpyDeviceToDevice, h->stream));
+    }
+    if ((rc = finalize(h, mode, h->counts.as<uint32_t>(), h->best.as<int64_t>(), d_idx, d_ties,
+                       d_lowest, true)))
+      return rc;
+    h->ran = true;
+    h->ran_bitmask = false;
+    h->last_mode = mode;
+    return YODA_OK;
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
+int yoda_shard_overflow_count(yoda_t* h, uint32_t* n_pods) {
+  if (!h || !n_pods) return YODA_ERR_INVALID_ARG;
+  *n_pods = 0;
+  if (!h->generic || !h->n_flagged.p) return YODA_OK;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipMemcpyAsync(n_pods, h->n_flagged.p, 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return YODA_OK;
+}
+
+int yoda_profile(yoda_t* h, int enable) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  h->profiling = enable != 0;
+  return YODA_OK;
+}
+
+int yoda_profile_read(yoda_t* h, double* k1_ms, double* k2_ms, uint32_t* n_launches) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  double t1 = 0, t2 = 0;
+  for (auto& pr : h->ev_k1) {
+    float ms = 0;
+    HIP_TRY(h, hipEventElapsedTime(&ms, pr.first, pr.second));
+    t1 += ms;
+  }
+  for (auto& pr : h->ev_k2) {
+    float ms = 0;
+    HIP_TRY(h, hipEventElapsedTime(&ms, pr.first, pr.second));
+    t2 += ms;
+  }
+  if (k1_ms) *k1_ms = t1;
+  if (k2_ms) *k2_ms = t2;
+  if (n_launches) *n_launches = (uint32_t)h->ev_k2.size();
+  h->ev_k1.clear();
+  h->ev_k2.clear();
+  h->ev_used = 0;
+  return YODA_OK;
+}
+
+int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, int32_t* pick) {
+  (void)pods;
+  (void)mode;
+  (void)flags;
+  (void)pick;
+  return fail(h, YODA_ERR_STATE, "yoda_greedy: not implemented yet");
+}
+
+}  // extern "C"

@@ -1,0 +1,100 @@
+// yoda_layout.h — device-resident data layout shared by the HIP kernels and the host side
+// of libyoda.  See DESIGN.md §Data layout in HBM.
+//
+// Node records are array-of-structs, one record per node, because every wavefront walks
+// the nodes in lock-step and reads a node's record through the SCALAR path (s_load into
+// SGPRs, broadcast to all 64 lanes = 64 pods).  Inside a record the card fields are
+// grouped field-major so the feasibility sweep touches only the first two groups.
+#pragma once
+#include <stdint.h>
+
+namespace yoda {
+
+constexpr int kBlock = 256;             // threads per workgroup = 4 waves = 256 pods
+constexpr int kWave = 64;
+constexpr uint32_t kChunkAlign = 32;    // node-chunk granularity (one bitmask word)
+
+// Fast path: every card field <= kFastFieldMax and every score provably < 2^52, so the
+// whole score runs exactly in f64.
+constexpr uint64_t kFastFieldMax = 1ull << 44;
+constexpr uint64_t kFastScoreMax = 1ull << 52;
+
+// Record header of the fast path (32 B).  Cards follow: 6 groups of K doubles:
+//   free[K], clock[K], total[K], bandwidth[K], core[K], power[K].
+struct alignas(16) NodeHdrF {
+  double static_score;    // CalculateAllocateScore + CalculateActualScore (exact)
+  uint64_t card_number;   // Status.CardNumber
+  uint32_t healthy_mask;  // bit j: card j Healthy
+  uint32_t zero_total;    // Status.TotalMemorySum == 0 (reference panics if scored)
+  uint32_t pad0, pad1;
+};
+static_assert(sizeof(NodeHdrF) == 32, "NodeHdrF layout");
+
+// Generic (exact uint64) path: same shape with uint64 card fields.
+struct alignas(16) NodeHdrG {
+  uint64_t static_score;  // (Allocate + Actual) mod 2^64
+  uint64_t card_number;
+  uint32_t healthy_mask;
+  uint32_t zero_total;
+  uint32_t pad0, pad1;
+};
+static_assert(sizeof(NodeHdrG) == 32, "NodeHdrG layout");
+
+enum CardField { kFree = 0, kClock = 1, kTotal = 2, kBandwidth = 3, kCore = 4, kPower = 5 };
+constexpr int kCardFields = 6;
+
+__host__ __device__ constexpr uint32_t node_stride(int k) { return 32u + 48u * (uint32_t)k; }
+
+// Mode B node record: V = Cpu/100, U = DiskIO/50 (algorithm.go:71,73).
+struct alignas(16) NodeRecB {
+  double v, u;
+};
+
+// Per-pod device parameters (struct of arrays, length P each).
+struct PodParams {
+  // Filter / card predicate thresholds
+  double* m_f;         // fast: scv/memory clamped to 2^53 (0 if absent)
+  double* c_f;         // fast: scv/clock clamped to 2^53 (0 if absent)
+  uint64_t* m_u;       // generic: scv/memory (0 if absent)
+  uint64_t* c_u;       // generic: scv/clock  (0 if absent)
+  uint64_t* number;    // PodFitsNumber operand: label value or 1
+  uint32_t* need_mem;  // healthy cards with free >= m required (0 if label absent)
+  uint32_t* need_clk;  // healthy cards with clock == c required (0 if label absent)
+  // Mode B
+  double* alpha;
+  double* beta;
+};
+
+// Per-pod state produced between kernels (length P each unless noted).
+struct PodState {
+  uint64_t* maxima;    // [6][P] MaxValue in collection.go field order (see kMax* below)
+  uint32_t* counts;    // [2][P] n_feasible, n_zero_total
+  double* rcp;         // [5][P] RU(100 / M) for bw, core, power, free, total (fast path)
+  int64_t* best;       // [P] highest raw score over feasible nodes (-1: none)
+  uint32_t* idx;       // [P] lowest global node index reaching it
+  uint32_t* ties;      // [P] nodes reaching it
+  int64_t* lowest;     // [P] lowest raw score over feasible nodes (INT64_MAX: none)
+  int32_t* pick;       // [P]
+  int32_t* status;     // [P]
+  uint32_t* flagged;   // [P] generic path: pods needing the exact normalize
+  uint32_t* n_flagged; // [1]
+};
+
+// MaxValue field order (collection.go:14-21) used for the [6][P] maxima buffer.
+enum MaxField { kMaxBw = 0, kMaxClock = 1, kMaxCore = 2, kMaxFree = 3, kMaxPower = 4, kMaxTotal = 5 };
+
+// Chunk partials: [field][chunk][P].
+struct Partials {
+  double* max_f;       // [6][C][P] fast
+  uint64_t* max_u;     // [6][C][P] generic
+  uint32_t* cnt;       // [2][C][P]
+  double* best_f;      // [C][P]
+  int64_t* best_i;     // [C][P] (generic; also used for exact normalize)
+  uint32_t* idx;       // [C][P]
+  uint32_t* ties;      // [C][P]
+  double* low_f;       // [C][P]
+  int64_t* low_i;      // [C][P]
+  uint32_t* err;       // [C][P] exact normalize: score out of range seen
+};
+
+}  // namespace yoda

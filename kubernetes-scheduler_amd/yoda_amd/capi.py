@@ -1,0 +1,228 @@
+"""ctypes binding of libyoda (include/yoda.h) — the product path.
+
+Loads the in-tree libyoda.so built by `make -C kubernetes-scheduler_amd/csrc` (or
+__graft_entry__.build()).  There is no CPU fallback: if the library or a GPU is missing,
+every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+from .soa import CEvalOut, CNodeSoA, CPodSoA, EvalResult, NodeSoA, PodSoA
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libyoda.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "yoda.h")
+
+ERRORS = {
+    -1: "YODA_ERR_INVALID_ARG", -2: "YODA_ERR_HIP", -3: "YODA_ERR_NO_NODES",
+    -4: "YODA_ERR_NO_PODS", -5: "YODA_ERR_RANGE", -6: "YODA_ERR_NO_DEVICE", -7: "YODA_ERR_STATE",
+}
+
+_lib = None
+
+_vp = C.c_void_p
+_u32 = C.c_uint32
+_SIGS = {
+    "yoda_abi_version": ([], C.c_int),
+    "yoda_create": ([C.c_int, C.POINTER(_vp)], C.c_int),
+    "yoda_destroy": ([_vp], C.c_int),
+    "yoda_last_error": ([_vp], C.c_char_p),
+    "yoda_set_stream": ([_vp, _vp], C.c_int),
+    "yoda_use_own_stream": ([_vp], C.c_int),
+    "yoda_synchronize": ([_vp], C.c_int),
+    "yoda_upload_nodes": ([_vp, C.POINTER(CNodeSoA), _u32, _u32], C.c_int),
+    "yoda_uses_generic_path": ([_vp], C.c_int),
+    "yoda_update_alloc": ([_vp, C.POINTER(C.c_uint64)], C.c_int),
+    "yoda_eval": ([_vp, C.POINTER(CPodSoA), C.c_int, C.POINTER(CEvalOut)], C.c_int),
+    "yoda_upload_pods": ([_vp, C.POINTER(CPodSoA)], C.c_int),
+    "yoda_run": ([_vp, C.c_int, _u32], C.c_int),
+    "yoda_download": ([_vp, C.POINTER(CEvalOut)], C.c_int),
+    "yoda_download_bitmask": ([_vp, C.POINTER(C.c_uint32), C.c_uint64], C.c_int),
+    "yoda_shard_phase1": ([_vp, C.c_int, _vp, _vp], C.c_int),
+    "yoda_shard_phase2": ([_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "yoda_shard_prepare_merge": ([_vp, _vp, _vp, _vp, _vp], C.c_int),
+    "yoda_shard_finalize": ([_vp, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "yoda_shard_overflow_count": ([_vp, C.POINTER(C.c_uint32)], C.c_int),
+    "yoda_profile": ([_vp, C.c_int], C.c_int),
+    "yoda_profile_read": ([_vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                           C.POINTER(C.c_uint32)], C.c_int),
+    "yoda_greedy": ([_vp, C.POINTER(CPodSoA), C.c_int, _u32, C.POINTER(C.c_int32)], C.c_int),
+}
+
+
+class YodaError(RuntimeError):
+    pass
+
+
+def _share_torch_hip_runtime():
+    """One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64.so.7.  If
+    libyoda.so loaded first it would pull /opt/rocm's copy and torch would then fail to
+    initialise ("No HIP GPUs are available").  Pre-loading torch's copy (same SONAME) makes
+    libyoda bind to it.  The C library itself has no torch dependency (Go/cgo callers use the
+    system runtime).  YODA_HIP_RUNTIME=system disables this."""
+    if os.environ.get("YODA_HIP_RUNTIME", "") == "system":
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    hip = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(hip):
+        C.CDLL(hip, mode=C.RTLD_GLOBAL)
+
+
+def lib():
+    """Load libyoda.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        _share_torch_hip_runtime()
+        if not os.path.exists(LIB_PATH):
+            raise YodaError(f"libyoda not built: {LIB_PATH} missing (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+class Yoda:
+    """One libyoda handle = one GPU holding one node snapshot (or shard)."""
+
+    def __init__(self, device: int = 0):
+        self._h = _vp()
+        rc = lib().yoda_create(device, C.byref(self._h))
+        if rc != 0:
+            raise YodaError(f"yoda_create(device={device}) failed: {ERRORS.get(rc, rc)}")
+        self.device = device
+        self._nodes: Optional[NodeSoA] = None
+        self._pods: Optional[PodSoA] = None
+        self.n_nodes = 0
+        self.n_pods = 0
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            msg = lib().yoda_last_error(self._h)
+            raise YodaError(f"{what}: {ERRORS.get(rc, rc)}: {msg.decode() if msg else ''}")
+
+    def close(self):
+        if self._h:
+            lib().yoda_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- snapshot / pods ---------------------------------------------------------------
+    def set_stream(self, stream_ptr: int):
+        self._check(lib().yoda_set_stream(self._h, _vp(stream_ptr)), "yoda_set_stream")
+
+    def synchronize(self):
+        self._check(lib().yoda_synchronize(self._h), "yoda_synchronize")
+
+    def upload_nodes(self, nodes: NodeSoA, node_offset: int = 0, force_generic: bool = False):
+        self._nodes = nodes.normalized()
+        cn = self._nodes.c()
+        self._check(lib().yoda_upload_nodes(self._h, C.byref(cn), node_offset,
+                                            1 if force_generic else 0), "yoda_upload_nodes")
+        self.n_nodes = self._nodes.n_nodes
+        self.node_offset = node_offset
+
+    @property
+    def generic(self) -> bool:
+        return lib().yoda_uses_generic_path(self._h) == 1
+
+    def update_alloc(self, alloc: np.ndarray):
+        a = np.ascontiguousarray(alloc, dtype=np.uint64)
+        self._check(lib().yoda_update_alloc(self._h, a.ctypes.data_as(C.POINTER(C.c_uint64))),
+                    "yoda_update_alloc")
+
+    def upload_pods(self, pods: PodSoA):
+        self._pods = pods.normalized()
+        cp = self._pods.c()
+        self._check(lib().yoda_upload_pods(self._h, C.byref(cp)), "yoda_upload_pods")
+        self.n_pods = self._pods.n_pods
+
+    # ---- evaluation --------------------------------------------------------------------
+    def run(self, mode: int = 0, bitmask: bool = False):
+        self._check(lib().yoda_run(self._h, mode, 1 if bitmask else 0), "yoda_run")
+
+    def download(self) -> EvalResult:
+        res = EvalResult.empty(self.n_pods)
+        co = res.c()
+        self._check(lib().yoda_download(self._h, C.byref(co)), "yoda_download")
+        return res
+
+    def download_bitmask(self) -> np.ndarray:
+        w = (self.n_nodes + 31) // 32
+        words = np.zeros((self.n_pods, w), np.uint32)
+        self._check(lib().yoda_download_bitmask(
+            self._h, words.ctypes.data_as(C.POINTER(C.c_uint32)), words.size),
+            "yoda_download_bitmask")
+        return words
+
+    def eval(self, pods: PodSoA, mode: int = 0) -> EvalResult:
+        self.upload_pods(pods)
+        self.run(mode)
+        return self.download()
+
+    def greedy(self, pods: PodSoA, mode: int = 0, flags: int = 0) -> np.ndarray:
+        p = pods.normalized()
+        cp = p.c()
+        pick = np.full(p.n_pods, -3, np.int32)
+        self._check(lib().yoda_greedy(self._h, C.byref(cp), mode, flags,
+                                      pick.ctypes.data_as(C.POINTER(C.c_int32))), "yoda_greedy")
+        return pick
+
+    def profile(self, enable: bool = True):
+        self._check(lib().yoda_profile(self._h, 1 if enable else 0), "yoda_profile")
+
+    def profile_read(self):
+        """(k1_ms_total, k2_ms_total, n_launches) since the last read."""
+        k1, k2, n = C.c_double(), C.c_double(), C.c_uint32()
+        self._check(lib().yoda_profile_read(self._h, C.byref(k1), C.byref(k2), C.byref(n)),
+                    "yoda_profile_read")
+        return k1.value, k2.value, n.value
+
+    # ---- sharded (device pointers as ints) ---------------------------------------------
+    def shard_phase1(self, mode: int, d_maxima: int, d_counts: int):
+        self._check(lib().yoda_shard_phase1(self._h, mode, _vp(d_maxima), _vp(d_counts)),
+                    "yoda_shard_phase1")
+
+    def shard_phase2(self, mode, d_maxima, d_counts, d_best, d_idx, d_ties, d_lowest):
+        self._check(lib().yoda_shard_phase2(self._h, mode, _vp(d_maxima), _vp(d_counts),
+                                            _vp(d_best), _vp(d_idx), _vp(d_ties), _vp(d_lowest)),
+                    "yoda_shard_phase2")
+
+    def shard_prepare_merge(self, d_best_global, d_best_local, d_idx, d_ties):
+        self._check(lib().yoda_shard_prepare_merge(self._h, _vp(d_best_global),
+                                                   _vp(d_best_local), _vp(d_idx), _vp(d_ties)),
+                    "yoda_shard_prepare_merge")
+
+    def shard_finalize(self, mode, d_counts, d_best, d_idx, d_ties, d_lowest):
+        self._check(lib().yoda_shard_finalize(self._h, mode, _vp(d_counts), _vp(d_best),
+                                              _vp(d_idx), _vp(d_ties), _vp(d_lowest)),
+                    "yoda_shard_finalize")
+
+
+def header_symbols(path: str = HEADER_PATH):
+    """Entry points declared in include/yoda.h."""
+    import re
+    text = open(path).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(yoda_[a-z0-9_]+)\s*\(", text,
+                                 re.M)))

@@ -1,0 +1,53 @@
+"""CPU checks of the C-ABI boundary: libyoda loads and exports every entry point that
+include/yoda.h declares (no compute: there is no GPU here)."""
+import ctypes as C
+import re
+
+from yoda_amd import capi
+
+
+def test_header_declares_entry_points():
+    syms = capi.header_symbols()
+    for s in ("yoda_create", "yoda_destroy", "yoda_upload_nodes", "yoda_eval", "yoda_greedy",
+              "yoda_last_error", "yoda_shard_phase1", "yoda_shard_finalize"):
+        assert s in syms
+
+
+def test_library_exports_every_header_symbol():
+    lib = C.CDLL(capi.LIB_PATH)
+    missing = [s for s in capi.header_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_binding_covers_header():
+    assert set(capi.header_symbols()) == set(capi._SIGS), \
+        set(capi.header_symbols()) ^ set(capi._SIGS)
+
+
+def test_abi_version_and_null_handles():
+    L = capi.lib()
+    assert L.yoda_abi_version() == 1
+    # NULL handle / pointers are rejected without touching a GPU
+    assert L.yoda_destroy(None) == -1
+    assert L.yoda_run(None, 0, 0) == -1
+    assert L.yoda_download(None, None) == -1
+    assert L.yoda_create(0, None) == -1
+    assert L.yoda_last_error(None) == b"null handle"
+
+
+def test_create_without_gpu_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        return
+    h = C.c_void_p()
+    rc = capi.lib().yoda_create(0, C.byref(h))
+    assert rc == -6 and not h.value  # YODA_ERR_NO_DEVICE
+
+
+def test_struct_layouts_match_header():
+    text = open(capi.HEADER_PATH).read()
+    for cname, pystruct in (("yoda_node_soa", capi.CNodeSoA), ("yoda_pod_soa", capi.CPodSoA),
+                            ("yoda_eval_out", capi.CEvalOut)):
+        body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), text, re.S).group(1)
+        fields = re.findall(r"^\s*(?:const\s+)?[a-z0-9_]+\*?\s*\*?\s*([a-z_0-9]+);", body, re.M)
+        assert fields == [f for f, _ in pystruct._fields_], cname

@@ -1,0 +1,133 @@
+"""N>1 path on CPU: two gloo ranks, each holding a node shard, merge their exchange buffers
+with the collectives of yoda_amd/dist.py.  The per-shard buffers are what libyoda's
+yoda_shard_phase1/phase2 produce (computed here from the oracle, which has global
+knowledge); after the merge every rank must hold the single-shard (whole cluster) values."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from yoda_amd import synth
+from yoda_amd.dist import Reducer, ShardBuffers, merge_phase1, merge_phase2, shard_bounds
+from yoda_amd.soa import MODE_SCV
+
+P, N = 24, 90
+
+
+def _cluster():
+    nodes = synth.make_nodes(N, seed=314)
+    pods = synth.make_pods(P, seed=271)
+    # unsigned values above 2^63 exercise the sign-flip MAX
+    nodes.card_bandwidth[5, :] = np.uint64((1 << 64) - 3)
+    nodes.total_memory_sum[7] = 0
+    return nodes.normalized(), pods
+
+
+def _expected(nodes, pods):
+    """Per-pod global exchange values over the whole cluster."""
+    res = oracle.schedule(nodes, pods, MODE_SCV)
+    exp = {"maxima": res.maxima.T.copy(), "nf": res.n_feasible.astype(np.int64)}
+    best, idx, ties, low, nz = [], [], [], [], []
+    for p in range(P):
+        _, feas, raw, _ = oracle.pod_detail(nodes, pods, p)
+        f = np.nonzero(feas)[0]
+        nz.append(int((nodes.total_memory_sum[f] == 0).sum()))
+        if f.size == 0:
+            best.append(-1), idx.append(0xFFFFFFFF), ties.append(0), low.append((1 << 63) - 1)
+            continue
+        b = raw[f].max()
+        best.append(int(b)), idx.append(int(f[raw[f] == b][0]))
+        ties.append(int((raw[f] == b).sum())), low.append(int(raw[f].min()))
+    exp.update(best=np.array(best), idx=np.array(idx, np.uint64), ties=np.array(ties),
+               low=np.array(low), nz=np.array(nz))
+    return exp
+
+
+def _shard_buffers(nodes, pods, lo, hi):
+    """What yoda_shard_phase1/phase2 would write for nodes [lo, hi)."""
+    shard = nodes.slice(lo, hi)
+    res = oracle.schedule(shard, pods, MODE_SCV)
+    b = ShardBuffers(P, torch.device("cpu"))
+    b.maxima.copy_(torch.from_numpy(res.maxima.T.copy().reshape(-1).view(np.int64)))
+    nz = []
+    best, idx, ties, low = [], [], [], []
+    for p in range(P):
+        _, feas, raw, _ = oracle.pod_detail(nodes, pods, p)  # raw uses GLOBAL maxima
+        f = np.nonzero(feas[lo:hi])[0] + lo
+        nz.append(int((nodes.total_memory_sum[f] == 0).sum()))
+        if f.size == 0:
+            best.append(-1), idx.append(-1), ties.append(0), low.append((1 << 63) - 1)
+            continue
+        bb = raw[f].max()
+        best.append(int(bb)), idx.append(int(f[raw[f] == bb][0]))
+        ties.append(int((raw[f] == bb).sum())), low.append(int(raw[f].min()))
+    b.counts.copy_(torch.tensor(list(res.n_feasible.astype(np.int64)) + nz, dtype=torch.int32))
+    b.best.copy_(torch.tensor(best))
+    b.idx.copy_(torch.tensor(idx, dtype=torch.int32))   # u32 0xFFFFFFFF viewed as int32 -1
+    b.ties.copy_(torch.tensor(ties, dtype=torch.int32))
+    b.lowest.copy_(torch.tensor(low))
+    return b
+
+
+def _prepare_cpu(b: ShardBuffers):
+    """CPU stand-in of libyoda's k_merge_prepare."""
+    keep = (b.best == b.best_g) & (b.best_g >= 0)
+    b.idx.copy_(torch.where(keep, b.idx, torch.full_like(b.idx, -1)))
+    b.ties.copy_(torch.where(keep, b.ties, torch.zeros_like(b.ties)))
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        nodes, pods = _cluster()
+        bnd = shard_bounds(N, world)
+        b = _shard_buffers(nodes, pods, int(bnd[rank]), int(bnd[rank + 1]))
+        red = Reducer()
+        merge_phase1(red, [b])
+        merge_phase2(red, [b], _prepare_cpu)
+        q.put((rank, b.maxima.numpy().view(np.uint64).copy(), b.counts.numpy().copy(),
+               b.best_g.numpy().copy(), b.idx.numpy().view(np.uint32).copy(),
+               b.ties.numpy().copy(), b.lowest.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_shard_merge(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, PORTS[world],
+                                                q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nodes, pods = _cluster()
+    exp = _expected(nodes, pods)
+    for rank, mx, cnt, best, idx, ties, low in outs:
+        np.testing.assert_array_equal(mx.reshape(6, P), exp["maxima"], err_msg=f"rank {rank}")
+        np.testing.assert_array_equal(cnt[:P], exp["nf"])
+        np.testing.assert_array_equal(cnt[P:], exp["nz"])
+        np.testing.assert_array_equal(best, exp["best"])
+        np.testing.assert_array_equal(idx, exp["idx"])
+        np.testing.assert_array_equal(ties, exp["ties"])
+        np.testing.assert_array_equal(low, exp["low"])
+
+
+PORTS = {2: _free_port(), 3: _free_port()}

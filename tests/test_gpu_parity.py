@@ -1,0 +1,243 @@
+"""GPU parity: libyoda (HIP, gfx950) against the C oracle on identical seeded inputs.
+
+Bar: bit-exact picks, statuses, feasible counts, tie counts, top scores and PreScore maxima
+(integer work; the Mode-B float math is compared through its integer scores).  Ties are
+broken by lowest node index in both, and the tie count is the size of the set k8s
+selectHost would draw from."""
+import numpy as np
+import pytest
+
+import oracle
+import pyoracle as po
+from yoda_amd import synth
+from yoda_amd.capi import Yoda
+from yoda_amd.soa import MODE_DISKIO, MODE_SCV, NodeSoA
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    y = Yoda(0)
+    yield y
+    y.close()
+
+
+def assert_same(got, want, mode=MODE_SCV, pods=None):
+    sel = slice(None) if pods is None else pods
+    np.testing.assert_array_equal(got.status[sel], want.status[sel], err_msg="status")
+    np.testing.assert_array_equal(got.pick[sel], want.pick[sel], err_msg="pick")
+    np.testing.assert_array_equal(got.n_feasible[sel], want.n_feasible[sel], err_msg="n_feasible")
+    ok = want.status[sel] == 0
+    np.testing.assert_array_equal(got.n_ties[sel][ok], want.n_ties[sel][ok], err_msg="n_ties")
+    np.testing.assert_array_equal(got.top_score[sel][ok], want.top_score[sel][ok],
+                                  err_msg="top_score")
+    if mode == MODE_SCV:
+        np.testing.assert_array_equal(got.maxima[sel], want.maxima[sel], err_msg="maxima")
+
+
+def run_both(dev, nodes, pods, mode=MODE_SCV, force_generic=False, threads=8):
+    dev.upload_nodes(nodes, force_generic=force_generic)
+    got = dev.eval(pods, mode)
+    want = oracle.schedule(nodes, pods, mode, threads=threads)
+    return got, want
+
+
+def test_kat1(dev):
+    from test_oracle import kat1_cluster
+    scvs, pod = kat1_cluster()
+    nodes, pods = oracle.from_py(scvs, [pod])
+    for generic in (False, True):
+        got, want = run_both(dev, nodes, pods, force_generic=generic)
+        assert int(got.pick[0]) == 1 and int(got.top_score[0]) == 4061
+        assert list(map(int, got.maxima[0])) == [1200, 1500, 108, 16000, 400, 32000]
+        assert_same(got, want)
+
+
+@pytest.mark.parametrize("mode", [MODE_SCV, MODE_DISKIO])
+def test_config1(dev, mode):
+    nodes, pods = synth.make_config(1)
+    got, want = run_both(dev, nodes, pods, mode)
+    assert_same(got, want, mode)
+
+
+@pytest.mark.parametrize("mode", [MODE_SCV, MODE_DISKIO])
+def test_config2_full(dev, mode):
+    nodes, pods = synth.make_config(2)   # 1k pods x 5k nodes, seed 42
+    got, want = run_both(dev, nodes, pods, mode)
+    assert not dev.generic
+    assert_same(got, want, mode)
+    assert (got.status == 0).mean() > 0.5
+
+
+@pytest.mark.parametrize("mode", [MODE_SCV, MODE_DISKIO])
+def test_config4_heterogeneous(dev, mode):
+    nodes, pods = synth.make_config(4, pods=2000, nodes=6000)
+    got, want = run_both(dev, nodes, pods, mode)
+    assert_same(got, want, mode)
+    if mode == MODE_SCV:
+        # >= 90% of pairs infeasible
+        frac = want.n_feasible.astype(np.float64).sum() / (2000 * 6000)
+        assert frac < 0.10
+
+
+def test_generic_path_matches_fast(dev):
+    nodes, pods = synth.make_config(2, pods=300, nodes=2000)
+    got_f, want = run_both(dev, nodes, pods)
+    assert not dev.generic
+    got_g, _ = run_both(dev, nodes, pods, force_generic=True)
+    assert dev.generic
+    assert_same(got_f, want)
+    assert_same(got_g, want)
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 16])
+def test_card_slot_variants(dev, k):
+    nodes = synth.make_nodes(700, seed=100 + k, cards=k)
+    pods = synth.make_pods(200, seed=200 + k)
+    got, want = run_both(dev, nodes, pods)
+    assert_same(got, want)
+
+
+def _edge_cluster(rng, n, k):
+    nodes = synth.make_nodes(n, int(rng.integers(1 << 30)), cards=k)
+    nodes.card_number[rng.random(n) < 0.1] = 0
+    nodes.card_clock[rng.random(nodes.card_clock.shape) < 0.2] = 1500
+    nodes.card_count[rng.random(n) < 0.1] = rng.integers(0, k + 1)
+    return nodes.normalized()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_randomized_edges(dev, seed):
+    rng = np.random.default_rng(1000 + seed)
+    nodes = _edge_cluster(rng, 1500, 8)
+    pods = synth.make_pods(400, int(rng.integers(1 << 30)))
+    pods.number[rng.random(400) < 0.05] = np.uint64((1 << 64) - 1)
+    pods.number[rng.random(400) < 0.05] = 0
+    pods.memory[rng.random(400) < 0.05] = np.uint64((1 << 64) - 5)
+    pods.clock[rng.random(400) < 0.05] = np.uint64(1 << 60)
+    for generic in (False, True):
+        got, want = run_both(dev, nodes, pods, force_generic=generic)
+        assert_same(got, want)
+
+
+def test_tie_heavy(dev):
+    # identical nodes: every feasible node ties; lowest index wins, tie count = n_feasible
+    base = synth.make_nodes(1, seed=5)
+    n = 3000
+    nodes = NodeSoA(**{f: np.repeat(getattr(base, f), n, axis=0)
+                       for f in base.__dataclass_fields__})
+    pods = synth.make_pods(300, seed=6)
+    got, want = run_both(dev, nodes, pods)
+    assert_same(got, want)
+    ok = want.status == 0
+    assert (got.n_ties[ok] == got.n_feasible[ok]).all()
+
+
+def test_empty_inputs(dev):
+    nodes, pods = synth.make_config(2, pods=10, nodes=100)
+    zero_nodes = nodes.slice(0, 0)
+    got, want = run_both(dev, zero_nodes, pods)
+    assert (got.pick == -1).all() and (got.status == 1).all()
+    assert_same(got, want)
+    dev.upload_nodes(nodes)
+    r = dev.eval(pods.slice(0, 0))
+    assert r.pick.size == 0
+
+
+def test_div_zero_and_single_feasible(dev):
+    from test_oracle import H
+    n0 = po.Scv(card_number=1, card_list=[H(5000)], free_memory_sum=5000, total_memory_sum=0)
+    n1 = po.Scv(card_number=1, card_list=[H(5000)], free_memory_sum=5000, total_memory_sum=100)
+    n2 = po.Scv(card_number=0, card_list=[], free_memory_sum=0, total_memory_sum=100)
+    for scvs in ([n0, n1], [n0, n2], [n2, n2]):
+        nodes, pods = oracle.from_py(scvs, [po.Pod(), po.Pod(number=1)], max_cards=2)
+        got, want = run_both(dev, nodes, pods)
+        assert_same(got, want)
+
+
+@pytest.mark.parametrize("clock0", [10 ** 15 + 1, (1 << 62) // 100])
+def test_normalize_overflow_generic_path(dev, clock0):
+    from test_oracle import _overflow_pair
+    nodes, pods = oracle.from_py(_overflow_pair(clock0), [po.Pod()])
+    got, want = run_both(dev, nodes, pods)
+    assert dev.generic  # clock > 2^44 leaves the fast path
+    assert_same(got, want)
+
+
+def test_huge_values_generic(dev):
+    rng = np.random.default_rng(77)
+    nodes = synth.make_nodes(500, seed=78)
+    big = rng.integers(0, 1 << 63, size=nodes.card_free_memory.shape, dtype=np.int64)
+    nodes.card_free_memory[:] = big.astype(np.uint64)
+    nodes.card_total_memory[:] = (big.astype(np.uint64) * np.uint64(3))
+    nodes.total_memory_sum[:] = rng.integers(1, 1 << 62, size=500).astype(np.uint64)
+    nodes = nodes.normalized()
+    pods = synth.make_pods(100, seed=79)
+    got, want = run_both(dev, nodes, pods)
+    assert dev.generic
+    assert_same(got, want)
+
+
+def test_bitmask_matches_oracle(dev):
+    nodes, pods = synth.make_config(2, pods=64, nodes=1000)
+    dev.upload_nodes(nodes)
+    dev.upload_pods(pods)
+    dev.run(MODE_SCV, bitmask=True)
+    words = dev.download_bitmask()
+    bits = np.unpackbits(words.view(np.uint8), bitorder="little", axis=1)[:, :1000].astype(bool)
+    for p in range(0, 64, 7):
+        _, feas, _, _ = oracle.pod_detail(nodes, pods, p)
+        np.testing.assert_array_equal(bits[p], feas)
+
+
+def test_mode_b_kats(dev):
+    from test_oracle import KAT2
+    pod = po.Pod(rio=10.0, rcpu=100)
+    scvs = [po.Scv(card_number=0, card_list=[], free_memory_sum=0, total_memory_sum=1,
+                   cpu=float(c), disk_io=float(d)) for (c, d), _ in KAT2]
+    nodes, pods = oracle.from_py(scvs, [pod], max_cards=1)
+    got, want = run_both(dev, nodes, pods, MODE_DISKIO)
+    assert int(got.pick[0]) == 4 and int(got.top_score[0]) == 10
+    assert_same(got, want, MODE_DISKIO)
+
+
+def test_sharded_merge_on_one_gpu(dev):
+    """Simulate G node shards with G handles and the exchange done by torch on the device."""
+    import torch
+    from yoda_amd.dist import ShardExchange
+    nodes, pods = synth.make_config(2, pods=500, nodes=3000)
+    want = oracle.schedule(nodes, pods, MODE_SCV, threads=8)
+    for G in (2, 3):
+        bounds = np.linspace(0, nodes.n_nodes, G + 1).astype(int)
+        handles = []
+        for g in range(G):
+            y = Yoda(0)
+            y.upload_nodes(nodes.slice(bounds[g], bounds[g + 1]), node_offset=int(bounds[g]))
+            y.upload_pods(pods)
+            handles.append(y)
+        ex = ShardExchange.local(handles, torch.device("cuda:0"))
+        for mode in (MODE_SCV, MODE_DISKIO):
+            res = ex.run(mode)
+            w = want if mode == MODE_SCV else oracle.schedule(nodes, pods, mode, threads=8)
+            assert_same(res, w, mode)
+        for y in handles:
+            y.close()
+
+
+def test_full_size_config3_sampled(dev):
+    """100k pods x 100k nodes on one GPU; exact check of a pod sample against the oracle plus
+    size-independent invariants for every pod."""
+    nodes, pods = synth.make_config(3)
+    dev.upload_nodes(nodes)
+    got = dev.eval(pods, MODE_SCV)
+    rng = np.random.default_rng(3)
+    sample = np.sort(rng.choice(pods.n_pods, size=48, replace=False))
+    want = oracle.schedule(nodes, pods.take(sample), MODE_SCV, threads=8)
+    sub = type(got)(**{f: getattr(got, f)[sample] for f in got.__dataclass_fields__})
+    assert_same(sub, want)
+    ok = got.status == 0
+    assert ((got.pick >= 0) == ok).all()
+    assert (got.pick[ok] < nodes.n_nodes).all()
+    assert (got.n_ties[ok] >= 1).all() and (got.n_ties[ok] <= got.n_feasible[ok]).all()
+    assert (got.n_feasible[got.status == 1] == 0).all()
