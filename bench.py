@@ -172,14 +172,15 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f64" if mode == MODE_SCV and not y.generic else ("int64" if mode == MODE_SCV
-                                                                   else "f64"),
+        # arithmetic of the dominant kernel: N32 = u32 compares/sums + f32/f64 quotients
+        "dtype": {"n32": "u32+f32+f64", "f64": "f64", "u64": "u64"}[y.path]
+        if mode == MODE_SCV else "f64",
         "data": "synthetic (seeded SCV node records and pod requests, yoda_amd/synth.py)",
         "config": {"workload": f"config{args.config}: {P} pods x {N} nodes, "
                                f"{'Mode A SCV GPU score' if mode == MODE_SCV else 'Mode B diskIO'}"
                                f", K={k_slots} card slots",
                    "pods": P, "nodes": N, "mode": args.mode,
-                   "path": "generic-u64" if y.generic else "fast-f64",
+                   "path": y.path,
                    "parallelism": f"node-shard x{world}" + (" (RCCL all-reduce merge)"
                                                             if world > 1 else "")},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,

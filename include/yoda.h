@@ -146,13 +146,20 @@ int yoda_synchronize(yoda_t* h);
 /* ---- node snapshot ------------------------------------------------------------------ */
 /* Upload a node snapshot (or a shard of one).  node_offset is the global index of this
  * shard's first node: picks are reported as node_offset + local index.  Replaces the
- * previous snapshot.  Chooses the exact-f64 fast path or the exact-u64 generic path from
- * the value ranges; flags: YODA_UPLOAD_FORCE_GENERIC. */
-#define YODA_UPLOAD_FORCE_GENERIC 1u
+ * previous snapshot.  Chooses the narrowest exact record format the value ranges allow
+ * (DESIGN.md §Exactness). */
+#define YODA_UPLOAD_FORCE_GENERIC 1u /* always the exact-u64 path                     */
+#define YODA_UPLOAD_FORCE_F64 2u     /* never the narrow path (tests)                 */
 int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nodes, uint32_t node_offset,
                       uint32_t flags);
-/* 1 if the uploaded snapshot runs on the generic (u64) path, 0 on the fast path. */
+/* 1 if the uploaded snapshot runs on the generic (u64) path, 0 on a fast path. */
 int yoda_uses_generic_path(const yoda_t* h);
+/* Record format of the uploaded snapshot: YODA_PATH_N32 (u32/f32 fields + f64 memory
+ * quotients), YODA_PATH_F64 (exact f64) or YODA_PATH_U64 (exact uint64 wrap-around). */
+#define YODA_PATH_N32 0
+#define YODA_PATH_F64 1
+#define YODA_PATH_U64 2
+int yoda_record_path(const yoda_t* h);
 /* Replace alloc_memory (the Allocate-score input) without re-uploading the cards. */
 int yoda_update_alloc(yoda_t* h, const uint64_t* alloc_memory);
 

@@ -18,16 +18,17 @@
 
 namespace yoda {
 // launchers (yoda_kernels.hip)
-hipError_t launch_k1(int K, bool fast, const unsigned char* nodes, uint32_t n_nodes,
+hipError_t launch_k1(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, uint32_t n_pods,
                      const Partials& part, uint32_t* bitmask, hipStream_t s);
-hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool fast,
-                          uint64_t* maxima, uint32_t* counts, hipStream_t s);
-hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, hipStream_t s);
-hipError_t launch_k2(int K, bool fast, const unsigned char* nodes, uint32_t n_nodes,
+hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uint64_t* maxima,
+                          uint32_t* counts, hipStream_t s);
+hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
+                        hipStream_t s);
+hipError_t launch_k2(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
-                     const double* rcp, uint32_t n_pods, const uint32_t* bitmask,
-                     const Partials& part, hipStream_t s);
+                     const double* rcp, const float* rcp32, uint32_t n_pods,
+                     const uint32_t* bitmask, const Partials& part, hipStream_t s);
 hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
                             uint32_t C, const PodParams& pp, uint32_t n_pods, const Partials& part,
                             hipStream_t s);
@@ -98,7 +99,8 @@ struct yoda_handle {
 
   // node snapshot
   bool has_nodes = false;
-  bool generic = false;
+  bool generic = false;  // path == Path::U64
+  Path path = Path::N32;
   bool nodes_diskio = false;  // node cpu/disk_io present
   bool pods_diskio = false;   // pod rio/rcpu present
   int K = 1;
@@ -114,13 +116,13 @@ struct yoda_handle {
   std::vector<uint64_t> h_pod_mem;      // scv/memory (0 if absent) for greedy alloc
   std::vector<uint8_t> h_pod_has_mem;
   std::vector<uint64_t> h_pod_number;   // PodFitsNumber operand
-  DevBuf pod_m_f, pod_c_f, pod_m_u, pod_c_u, pod_number, pod_need_mem, pod_need_clk, pod_alpha,
+  DevBuf pod_m_f, pod_c_f, pod_m_u, pod_c_u, pod_m_32, pod_c_32, pod_number, pod_need_mem, pod_need_clk, pod_alpha,
       pod_beta;
 
   // state
-  DevBuf maxima, counts, rcp, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
+  DevBuf maxima, counts, rcp, rcp32, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
   DevBuf bitmask, bitmask_t;
-  DevBuf p_max_f, p_max_u, p_cnt, p_best_f, p_best_i, p_idx, p_ties, p_low_f, p_low_i, p_err;
+  DevBuf p_max_u, p_cnt, p_best_f, p_best_i, p_idx, p_ties, p_low_f, p_low_i, p_err;
   uint32_t C = 1, chunk_nodes = 32;
   int last_mode = -1;
   bool ran = false;
@@ -144,11 +146,14 @@ struct yoda_handle {
 
   ~yoda_handle() {
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&nodes, &nodes_b, &pod_m_f, &pod_c_f, &pod_m_u, &pod_c_u, &pod_number,
-                     &pod_need_mem, &pod_need_clk, &pod_alpha, &pod_beta, &maxima, &counts, &rcp,
-                     &best, &idx, &ties, &lowest, &pick, &status, &ties_out, &flagged, &n_flagged,
-                     &bitmask, &bitmask_t, &p_max_f, &p_max_u, &p_cnt, &p_best_f, &p_best_i,
-                     &p_idx, &p_ties, &p_low_f, &p_low_i, &p_err};
+    DevBuf* all[] = {&nodes,     &nodes_b,   &pod_m_f,    &pod_c_f,      &pod_m_u,
+                     &pod_c_u,   &pod_m_32,  &pod_c_32,   &pod_number,   &pod_need_mem,
+                     &pod_need_clk, &pod_alpha, &pod_beta, &maxima,      &counts,
+                     &rcp,       &rcp32,     &best,       &idx,          &ties,
+                     &lowest,    &pick,      &status,     &ties_out,     &flagged,
+                     &n_flagged, &bitmask,   &bitmask_t,  &p_max_u,      &p_cnt,
+                     &p_best_f,  &p_best_i,  &p_idx,      &p_ties,       &p_low_f,
+                     &p_low_i,   &p_err};
     for (DevBuf* b : all) b->release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
@@ -201,6 +206,7 @@ int ensure_state(yoda_t* h, uint32_t P) {
   HIP_TRY(h, h->maxima.ensure(6 * (size_t)P * 8));
   HIP_TRY(h, h->counts.ensure(2 * (size_t)P * 4));
   HIP_TRY(h, h->rcp.ensure(5 * (size_t)P * 8));
+  HIP_TRY(h, h->rcp32.ensure(3 * (size_t)P * 4));
   HIP_TRY(h, h->best.ensure((size_t)P * 8));
   HIP_TRY(h, h->idx.ensure((size_t)P * 4));
   HIP_TRY(h, h->ties.ensure((size_t)P * 4));
@@ -211,13 +217,11 @@ int ensure_state(yoda_t* h, uint32_t P) {
   HIP_TRY(h, h->flagged.ensure((size_t)P * 4));
   HIP_TRY(h, h->n_flagged.ensure(16));
   HIP_TRY(h, h->bitmask.ensure(W * P * 4));
+  HIP_TRY(h, h->p_max_u.ensure(6 * CP * 8));
   if (h->generic) {
-    HIP_TRY(h, h->p_max_u.ensure(6 * CP * 8));
     HIP_TRY(h, h->p_best_i.ensure(CP * 8));
     HIP_TRY(h, h->p_low_i.ensure(CP * 8));
     HIP_TRY(h, h->p_err.ensure(CP * 4));
-  } else {
-    HIP_TRY(h, h->p_max_f.ensure(6 * CP * 8));
   }
   HIP_TRY(h, h->p_best_f.ensure(CP * 8));
   HIP_TRY(h, h->p_low_f.ensure(CP * 8));
@@ -233,6 +237,8 @@ PodParams pod_params(yoda_t* h) {
   pp.c_f = h->pod_c_f.as<double>();
   pp.m_u = h->pod_m_u.as<uint64_t>();
   pp.c_u = h->pod_c_u.as<uint64_t>();
+  pp.m_32 = h->pod_m_32.as<uint32_t>();
+  pp.c_32 = h->pod_c_32.as<uint32_t>();
   pp.number = h->pod_number.as<uint64_t>();
   pp.need_mem = h->pod_need_mem.as<uint32_t>();
   pp.need_clk = h->pod_need_clk.as<uint32_t>();
@@ -243,7 +249,6 @@ PodParams pod_params(yoda_t* h) {
 
 Partials partials(yoda_t* h) {
   Partials p;
-  p.max_f = h->p_max_f.as<double>();
   p.max_u = h->p_max_u.as<uint64_t>();
   p.cnt = h->p_cnt.as<uint32_t>();
   p.best_f = h->p_best_f.as<double>();
@@ -288,13 +293,13 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts) {
   hipEvent_t e0 = h->profiling ? h->next_event() : nullptr;
   hipEvent_t e1 = h->profiling ? h->next_event() : nullptr;
   if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
-  HIP_TRY(h, launch_k1(h->K, !h->generic, h->nodes.as<unsigned char>(), h->n_nodes, h->chunk_nodes,
+  HIP_TRY(h, launch_k1(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes, h->chunk_nodes,
                        h->C, pod_params(h), P, part, h->bitmask.as<uint32_t>(), h->stream));
   if (e1) {
     HIP_TRY(h, hipEventRecord(e1, h->stream));
     h->ev_k1.emplace_back(e0, e1);
   }
-  HIP_TRY(h, launch_reduce1(part, h->C, P, !h->generic, maxima, counts, h->stream));
+  HIP_TRY(h, launch_reduce1(part, h->C, P, maxima, counts, h->stream));
   return YODA_OK;
 }
 
@@ -318,15 +323,15 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, int64_t* best, uint32_t*
   hipEvent_t e0 = h->profiling ? h->next_event() : nullptr;
   hipEvent_t e1 = h->profiling ? h->next_event() : nullptr;
   if (mode == YODA_MODE_SCV && !h->generic)
-    HIP_TRY(h, launch_prep2(maxima, P, h->rcp.as<double>(), h->stream));
+    HIP_TRY(h, launch_prep2(maxima, P, h->rcp.as<double>(), h->rcp32.as<float>(), h->stream));
   if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
   if (mode == YODA_MODE_DISKIO) {
     HIP_TRY(h, launch_k2_diskio(h->nodes_b.as<NodeRecB>(), h->n_nodes, h->chunk_nodes, h->C,
                                 pod_params(h), P, part, h->stream));
   } else {
-    HIP_TRY(h, launch_k2(h->K, !h->generic, h->nodes.as<unsigned char>(), h->n_nodes,
-                         h->chunk_nodes, h->C, pod_params(h), maxima, h->rcp.as<double>(), P,
-                         h->bitmask.as<uint32_t>(), part, h->stream));
+    HIP_TRY(h, launch_k2(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes,
+                         h->chunk_nodes, h->C, pod_params(h), maxima, h->rcp.as<double>(),
+                         h->rcp32.as<float>(), P, h->bitmask.as<uint32_t>(), part, h->stream));
     is_f64 = !h->generic;
   }
   if (e1) {
@@ -450,12 +455,11 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
       kmax = std::max(kmax, nd->card_count[i]);
     }
     const int K = pow2_cards(kmax);
-    // Exactness check for the f64 fast path.
-    bool fast = !(flags & YODA_UPLOAD_FORCE_GENERIC);
+    // Record format: the narrowest exact one.
     std::vector<uint64_t> stat(N);
     std::vector<uint8_t> zt(N);
-    uint64_t max_clock = 0, max_static = 0;
-    for (uint32_t i = 0; i < N && true; ++i) {
+    uint64_t max_field = 0, max_small = 0, max_clock = 0, max_bw = 0, max_static = 0;
+    for (uint32_t i = 0; i < N; ++i) {
       bool z = false;
       const uint64_t alloc = nd->alloc_memory ? nd->alloc_memory[i] : 0;
       stat[i] = static_score(nd->free_memory_sum[i], nd->total_memory_sum[i], alloc, &z);
@@ -463,61 +467,65 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
       max_static = std::max(max_static, stat[i]);
       for (uint32_t j = 0; j < nd->card_count[i]; ++j) {
         const size_t k = (size_t)i * KS + j;
-        const uint64_t v[6] = {nd->card_free_memory[k], nd->card_total_memory[k],
-                               nd->card_clock[k],       nd->card_bandwidth[k],
-                               nd->card_core[k],        nd->card_power[k]};
-        for (uint64_t x : v)
-          if (x > kFastFieldMax) fast = false;
+        max_field = std::max({max_field, nd->card_free_memory[k], nd->card_total_memory[k],
+                              nd->card_clock[k], nd->card_bandwidth[k], nd->card_core[k],
+                              nd->card_power[k]});
+        max_small = std::max({max_small, nd->card_bandwidth[k], nd->card_core[k],
+                              nd->card_power[k]});
         max_clock = std::max(max_clock, nd->card_clock[k]);
+        max_bw = std::max(max_bw, nd->card_bandwidth[k]);
       }
     }
-    if (fast) {
-      // per-card score <= 800 + 100*clock (5 quotients <= 100, clock/MaxBandwidth <= 100*clock)
-      const long double bound = (long double)K * (800.0L + 100.0L * (long double)max_clock) +
-                                (long double)max_static;
-      if (bound >= (long double)kFastScoreMax) fast = false;
-    }
+    // per-card score <= 800 + 100*clock (five quotients <= 100, clock/MaxBandwidth <= 100*clock)
+    const long double score_bound =
+        (long double)K * (800.0L + 100.0L * (long double)max_clock) + (long double)max_static;
+    const bool f64_ok = max_field <= kFastFieldMax && score_bound < (long double)kFastScoreMax;
+    const bool n32_ok = f64_ok && max_field <= kN32FieldMax && max_small <= kN32SmallFieldMax &&
+                        300.0L * max_clock + max_bw < (long double)(1u << 24);
+    Path path = n32_ok ? Path::N32 : (f64_ok ? Path::F64 : Path::U64);
+    if ((flags & YODA_UPLOAD_FORCE_F64) && path == Path::N32) path = Path::F64;
+    if (flags & YODA_UPLOAD_FORCE_GENERIC) path = Path::U64;
     // Build records.
-    const size_t stride = node_stride(K);
+    const size_t stride = path == Path::N32 ? n32_stride(K) : node_stride(K);
     std::vector<unsigned char> rec((size_t)std::max<uint32_t>(N, 1) * stride, 0);
     for (uint32_t i = 0; i < N; ++i) {
       unsigned char* r = rec.data() + (size_t)i * stride;
       uint32_t hm = 0;
       for (uint32_t j = 0; j < nd->card_count[i]; ++j)
         if (nd->card_healthy[(size_t)i * KS + j]) hm |= 1u << j;
-      if (fast) {
-        NodeHdrF hd{};
-        hd.static_score = (double)stat[i];
-        hd.card_number = nd->card_number[i];
-        hd.healthy_mask = hm;
-        hd.zero_total = zt[i];
-        std::memcpy(r, &hd, sizeof(hd));
-        double* f = reinterpret_cast<double*>(r + sizeof(hd));
-        for (uint32_t j = 0; j < nd->card_count[i]; ++j) {
-          const size_t k = (size_t)i * KS + j;
-          f[kFree * K + j] = (double)nd->card_free_memory[k];
-          f[kClock * K + j] = (double)nd->card_clock[k];
-          f[kTotal * K + j] = (double)nd->card_total_memory[k];
-          f[kBandwidth * K + j] = (double)nd->card_bandwidth[k];
-          f[kCore * K + j] = (double)nd->card_core[k];
-          f[kPower * K + j] = (double)nd->card_power[k];
-        }
-      } else {
-        NodeHdrG hd{};
+      NodeHdrG hd{};  // NodeHdrF has the same layout; static_score's bits set below
+      hd.card_number = nd->card_number[i];
+      hd.healthy_mask = hm;
+      hd.zero_total = zt[i];
+      if (path == Path::U64) {
         hd.static_score = stat[i];
-        hd.card_number = nd->card_number[i];
-        hd.healthy_mask = hm;
-        hd.zero_total = zt[i];
-        std::memcpy(r, &hd, sizeof(hd));
-        uint64_t* f = reinterpret_cast<uint64_t*>(r + sizeof(hd));
-        for (uint32_t j = 0; j < nd->card_count[i]; ++j) {
-          const size_t k = (size_t)i * KS + j;
-          f[kFree * K + j] = nd->card_free_memory[k];
-          f[kClock * K + j] = nd->card_clock[k];
-          f[kTotal * K + j] = nd->card_total_memory[k];
-          f[kBandwidth * K + j] = nd->card_bandwidth[k];
-          f[kCore * K + j] = nd->card_core[k];
-          f[kPower * K + j] = nd->card_power[k];
+      } else {
+        const double sd = (double)stat[i];
+        std::memcpy(&hd.static_score, &sd, 8);
+      }
+      std::memcpy(r, &hd, sizeof(hd));
+      for (uint32_t j = 0; j < nd->card_count[i]; ++j) {
+        const size_t k = (size_t)i * KS + j;
+        const uint64_t v[6] = {nd->card_free_memory[k], nd->card_clock[k],
+                               nd->card_total_memory[k], nd->card_bandwidth[k],
+                               nd->card_core[k], nd->card_power[k]};  // CardField order
+        if (path == Path::N32) {
+          uint32_t* u = reinterpret_cast<uint32_t*>(r + 32);
+          for (int f = 0; f < kCardFields; ++f) u[f * K + j] = (uint32_t)v[f];
+          float* g = reinterpret_cast<float*>(r + n32_f32_off(0, K));
+          g[kF32Bandwidth * K + j] = (float)v[kBandwidth];
+          g[kF32Clock * K + j] = (float)v[kClock];
+          g[kF32Core * K + j] = (float)v[kCore];
+          g[kF32Power * K + j] = (float)v[kPower];
+          double* d = reinterpret_cast<double*>(r + n32_f64_off(0, K));
+          d[kF64Free * K + j] = (double)v[kFree];
+          d[kF64Total * K + j] = (double)v[kTotal];
+        } else if (path == Path::F64) {
+          double* d = reinterpret_cast<double*>(r + 32);
+          for (int f = 0; f < kCardFields; ++f) d[f * K + j] = (double)v[f];
+        } else {
+          uint64_t* u = reinterpret_cast<uint64_t*>(r + 32);
+          for (int f = 0; f < kCardFields; ++f) u[f * K + j] = v[f];
         }
       }
     }
@@ -543,7 +551,8 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     h->n_nodes = N;
     h->node_offset = node_offset;
     h->K = K;
-    h->generic = !fast;
+    h->path = path;
+    h->generic = path == Path::U64;
     h->has_nodes = true;
     h->ran = false;
     h->phase1_done = false;
@@ -558,13 +567,15 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
 
 int yoda_uses_generic_path(const yoda_t* h) { return h ? (h->generic ? 1 : 0) : -1; }
 
+int yoda_record_path(const yoda_t* h) { return h ? (int)h->path : -1; }
+
 int yoda_update_alloc(yoda_t* h, const uint64_t* alloc) {
   if (!h) return YODA_ERR_INVALID_ARG;
   if (!h->has_nodes) return fail(h, YODA_ERR_NO_NODES, "no node snapshot uploaded");
   if (!alloc && h->n_nodes) return fail(h, YODA_ERR_INVALID_ARG, "alloc is NULL");
   try {
     HIP_TRY(h, hipSetDevice(h->device));
-    const size_t stride = node_stride(h->K);
+    const size_t stride = h->path == Path::N32 ? n32_stride(h->K) : node_stride(h->K);
     uint64_t max_static = 0;
     for (uint32_t i = 0; i < h->n_nodes; ++i) {
       bool z = false;
@@ -600,7 +611,7 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     const uint64_t kClamp = 1ull << 53;  // > every fast-path card field (<= 2^44)
     std::vector<double> mf(P), cf(P), al(P), be(P);
     std::vector<uint64_t> mu(P), cu(P), num(P);
-    std::vector<uint32_t> nm(P), nc(P);
+    std::vector<uint32_t> nm(P), nc(P), m32(P), c32(P);
     h->h_pod_mem.assign(P, 0);
     h->h_pod_has_mem.assign(P, 0);
     h->h_pod_number.assign(P, 1);
@@ -616,6 +627,8 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
       cu[p] = c;
       mf[p] = (double)std::min(m, kClamp);
       cf[p] = (double)std::min(c, kClamp);
+      m32[p] = (uint32_t)std::min<uint64_t>(m, 0xffffffffull);  // > every N32 field
+      c32[p] = (uint32_t)std::min<uint64_t>(c, 0xffffffffull);
       h->h_pod_mem[p] = pd->memory[p];
       h->h_pod_has_mem[p] = pd->has_memory[p];
       h->h_pod_number[p] = number;
@@ -635,6 +648,8 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
         (rc = up(h->pod_c_f, cf.data(), P * 8ull)) ||
         (rc = up(h->pod_m_u, mu.data(), P * 8ull)) ||
         (rc = up(h->pod_c_u, cu.data(), P * 8ull)) ||
+        (rc = up(h->pod_m_32, m32.data(), P * 4ull)) ||
+        (rc = up(h->pod_c_32, c32.data(), P * 4ull)) ||
         (rc = up(h->pod_number, num.data(), P * 8ull)) ||
         (rc = up(h->pod_need_mem, nm.data(), P * 4ull)) ||
         (rc = up(h->pod_need_clk, nc.data(), P * 4ull)) ||

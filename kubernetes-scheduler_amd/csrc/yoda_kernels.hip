@@ -24,35 +24,68 @@ namespace yoda {
 
 constexpr int64_t kI64Max = 0x7fffffffffffffffll;
 
-template <bool Fast>
-struct Num;
+// Record policies (yoda_layout.h): field type of the K1 sweep and where its groups live.
+template <Path P>
+struct Rec;
 template <>
-struct Num<true> {
-  using T = double;
-  using Hdr = NodeHdrF;
+struct Rec<Path::N32> {
+  using T = uint32_t;
+  static constexpr uint32_t stride(int k) { return n32_stride(k); }
+  static constexpr uint32_t off(int field, int k) { return n32_u32_off(field, k); }
 };
 template <>
-struct Num<false> {
+struct Rec<Path::F64> {
+  using T = double;
+  static constexpr uint32_t stride(int k) { return node_stride(k); }
+  static constexpr uint32_t off(int field, int k) { return 32u + 8u * (uint32_t)(field * k); }
+};
+template <>
+struct Rec<Path::U64> {
   using T = uint64_t;
-  using Hdr = NodeHdrG;
+  static constexpr uint32_t stride(int k) { return node_stride(k); }
+  static constexpr uint32_t off(int field, int k) { return 32u + 8u * (uint32_t)(field * k); }
 };
 
+// K values of one card-field group, read with ONE wide scalar load (the address is
+// wave-uniform), so a node costs a handful of s_load_dwordx8/x16 and one wait.
+template <class T, int K>
+struct alignas(sizeof(T) >= 4 ? sizeof(T) : 4) Group {
+  T v[K];
+};
+template <class T, int K>
+__device__ __forceinline__ Group<T, K> load_group(const unsigned char* p) {
+  return *reinterpret_cast<const Group<T, K>*>(p);
+}
+
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
+// max of two non-NaN doubles in ONE v_max_f64.  fmax() under the default IEEE mode first
+// canonicalizes both operands (two extra v_max_f64 per call); card fields and maxima are
+// exact non-negative integers, never NaN, so the canonicalization is dead work.
+// x must be wave-uniform (a node-record field read through the scalar path).
+__device__ __forceinline__ double dmax(double acc, double x) {
+  double r;
+  asm volatile("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(acc), "s"(x));  // x: uniform (SGPR)
+  return r;
+}
+__device__ __forceinline__ uint32_t fmax_t(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ double fmax_t(double a, double b) { return dmax(a, b); }
+__device__ __forceinline__ uint64_t fmax_t(uint64_t a, uint64_t b) { return umax64(a, b); }
 
 // ---------------------------------------------------------------------------------------
 // K1: Filter (PodFitsNumber ∧ PodFitsMemory ∧ PodFitsClock, collection.go:41-44) and the
 // PreScore maxima (CollectMaxValues).  Writes the feasibility bitmask [W][P] and per-chunk
-// partials.
-template <int K, bool Fast>
+// partials.  Branch-free in the card loop: a short-circuit `healthy && free >= m` would
+// make every field load conditional and serialise one scalar-load round trip per card.
+template <int K, Path PATH>
 __global__ __launch_bounds__(kBlock) void k1_filter_maxima(
     const unsigned char* __restrict__ nodes, uint32_t n_nodes, uint32_t chunk_nodes,
-    const double* __restrict__ m_f, const double* __restrict__ c_f,
-    const uint64_t* __restrict__ m_u, const uint64_t* __restrict__ c_u,
+    const typename Rec<PATH>::T* __restrict__ m_in, const typename Rec<PATH>::T* __restrict__ c_in,
     const uint64_t* __restrict__ number_in, const uint32_t* __restrict__ need_mem_in,
-    const uint32_t* __restrict__ need_clk_in, uint32_t n_pods, double* __restrict__ pmax_f,
-    uint64_t* __restrict__ pmax_u, uint32_t* __restrict__ pcnt, uint32_t* __restrict__ bitmask) {
-  using T = typename Num<Fast>::T;
-  using Hdr = typename Num<Fast>::Hdr;
+    const uint32_t* __restrict__ need_clk_in, uint32_t n_pods, uint64_t* __restrict__ pmax,
+    uint32_t* __restrict__ pcnt, uint32_t* __restrict__ bitmask) {
+  using R = Rec<PATH>;
+  using T = typename R::T;
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t chunk = blockIdx.y, C = gridDim.y;
   const uint32_t n0 = chunk * chunk_nodes;
@@ -63,13 +96,8 @@ __global__ __launch_bounds__(kBlock) void k1_filter_maxima(
   uint64_t number = ~0ull;  // padding lanes never fit
   uint32_t need_mem = 0, need_clk = 0;
   if (live) {
-    if constexpr (Fast) {
-      m = m_f[p];
-      c = c_f[p];
-    } else {
-      m = m_u[p];
-      c = c_u[p];
-    }
+    m = m_in[p];
+    c = c_in[p];
     number = number_in[p];
     need_mem = need_mem_in[p];
     need_clk = need_clk_in[p];
@@ -80,41 +108,35 @@ __global__ __launch_bounds__(kBlock) void k1_filter_maxima(
   uint32_t nf = 0, nz = 0, bits = 0;
 
   for (uint32_t n = n0; n < n1; ++n) {
-    const unsigned char* rec = nodes + (size_t)n * node_stride(K);
-    const Hdr* h = reinterpret_cast<const Hdr*>(rec);
-    const T* fld = reinterpret_cast<const T*>(rec + sizeof(Hdr));
-    const uint32_t hm = h->healthy_mask;
+    const unsigned char* rec = nodes + (size_t)n * R::stride(K);
+    const NodeHdrG hd = *reinterpret_cast<const NodeHdrG*>(rec);
+    const Group<T, K> fr = load_group<T, K>(rec + R::off(kFree, K));
+    const Group<T, K> ck = load_group<T, K>(rec + R::off(kClock, K));
     uint32_t cm = 0, cc = 0;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      const bool hj = (hm >> j) & 1u;
-      cm += (hj && fld[kFree * K + j] >= m) ? 1u : 0u;   // CardFitsMemory (filter.go:52-54)
-      cc += (hj && fld[kClock * K + j] == c) ? 1u : 0u;  // CardFitsClock  (filter.go:56-58)
+      const uint32_t hj = (hd.healthy_mask >> j) & 1u;
+      cm += (uint32_t)(fr.v[j] >= m) & hj;   // CardFitsMemory (filter.go:52-54)
+      cc += (uint32_t)(ck.v[j] == c) & hj;   // CardFitsClock  (filter.go:56-58)
     }
-    const bool feas = (number <= h->card_number) && cm >= need_mem && cc >= need_clk;
+    const bool feas = (number <= hd.card_number) & (cm >= need_mem) & (cc >= need_clk);
     bits |= (uint32_t)feas << (n & 31u);
     if (feas) {
       ++nf;
-      nz += h->zero_total;
+      nz += hd.zero_total;
+      const Group<T, K> bw = load_group<T, K>(rec + R::off(kBandwidth, K));
+      const Group<T, K> co = load_group<T, K>(rec + R::off(kCore, K));
+      const Group<T, K> pw = load_group<T, K>(rec + R::off(kPower, K));
+      const Group<T, K> to = load_group<T, K>(rec + R::off(kTotal, K));
 #pragma unroll
       for (int j = 0; j < K; ++j) {
-        const T fr = fld[kFree * K + j], ck = fld[kClock * K + j];
-        if (fr >= m && ck >= c) {  // collection.go:46: no health check, >= clock
-          if constexpr (Fast) {
-            mx[kMaxBw] = fmax(mx[kMaxBw], fld[kBandwidth * K + j]);
-            mx[kMaxClock] = fmax(mx[kMaxClock], ck);
-            mx[kMaxCore] = fmax(mx[kMaxCore], fld[kCore * K + j]);
-            mx[kMaxFree] = fmax(mx[kMaxFree], fr);
-            mx[kMaxPower] = fmax(mx[kMaxPower], fld[kPower * K + j]);
-            mx[kMaxTotal] = fmax(mx[kMaxTotal], fld[kTotal * K + j]);
-          } else {
-            mx[kMaxBw] = umax64(mx[kMaxBw], fld[kBandwidth * K + j]);
-            mx[kMaxClock] = umax64(mx[kMaxClock], ck);
-            mx[kMaxCore] = umax64(mx[kMaxCore], fld[kCore * K + j]);
-            mx[kMaxFree] = umax64(mx[kMaxFree], fr);
-            mx[kMaxPower] = umax64(mx[kMaxPower], fld[kPower * K + j]);
-            mx[kMaxTotal] = umax64(mx[kMaxTotal], fld[kTotal * K + j]);
-          }
+        if ((fr.v[j] >= m) & (ck.v[j] >= c)) {  // collection.go:46: no health check, >= clock
+          mx[kMaxBw] = fmax_t(mx[kMaxBw], bw.v[j]);
+          mx[kMaxClock] = fmax_t(mx[kMaxClock], ck.v[j]);
+          mx[kMaxCore] = fmax_t(mx[kMaxCore], co.v[j]);
+          mx[kMaxFree] = fmax_t(mx[kMaxFree], fr.v[j]);
+          mx[kMaxPower] = fmax_t(mx[kMaxPower], pw.v[j]);
+          mx[kMaxTotal] = fmax_t(mx[kMaxTotal], to.v[j]);
         }
       }
     }
@@ -125,32 +147,22 @@ __global__ __launch_bounds__(kBlock) void k1_filter_maxima(
   }
   if (!live) return;
 #pragma unroll
-  for (int f = 0; f < 6; ++f) {
-    const size_t o = ((size_t)f * C + chunk) * n_pods + p;
-    if constexpr (Fast)
-      pmax_f[o] = mx[f];
-    else
-      pmax_u[o] = mx[f];
-  }
+  for (int f = 0; f < 6; ++f) pmax[((size_t)f * C + chunk) * n_pods + p] = (uint64_t)mx[f];
   pcnt[((size_t)0 * C + chunk) * n_pods + p] = nf;
   pcnt[((size_t)1 * C + chunk) * n_pods + p] = nz;
 }
 
-// Per-pod merge of K1 chunk partials -> maxima [6][P] (u64) and counts [2][P].
-__global__ __launch_bounds__(kBlock) void k_reduce1(const double* __restrict__ pmax_f,
-                                                    const uint64_t* __restrict__ pmax_u,
+// Per-pod merge of K1 chunk partials -> maxima [6][P] and counts [2][P].
+__global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__ pmax,
                                                     const uint32_t* __restrict__ pcnt, uint32_t C,
-                                                    uint32_t n_pods, int fast,
+                                                    uint32_t n_pods,
                                                     uint64_t* __restrict__ maxima,
                                                     uint32_t* __restrict__ counts) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (p >= n_pods) return;
   for (int f = 0; f < 6; ++f) {
     uint64_t mx = 1;
-    for (uint32_t c = 0; c < C; ++c) {
-      const size_t o = ((size_t)f * C + c) * n_pods + p;
-      mx = umax64(mx, fast ? (uint64_t)pmax_f[o] : pmax_u[o]);
-    }
+    for (uint32_t c = 0; c < C; ++c) mx = umax64(mx, pmax[((size_t)f * C + c) * n_pods + p]);
     maxima[(size_t)f * n_pods + p] = mx;
   }
   for (int f = 0; f < 2; ++f) {
@@ -169,19 +181,33 @@ __device__ __forceinline__ double ru_100_over(double M) {
   return r;
 }
 
-// Fast path: per-pod reciprocals of the (all-reduced) maxima.
+// RU32(100 / M): the smallest float >= 100/M (M < 2^24, so (double)f * M is exact and the
+// fma's sign is exact).  floor(fl32(x * RU32(100/M))) == floor(100 x / M) whenever
+// 300 x + M < 2^24 (tools/check_div_lemma.c).
+__device__ __forceinline__ float ru32_100_over(double M) {
+  float f = (float)(100.0 / M);
+  if (__builtin_fma((double)f, M, -100.0) < 0.0) f = __int_as_float(__float_as_int(f) + 1);
+  return f;
+}
+
+// Per-pod reciprocals of the (all-reduced) maxima: f64 for all five divisors, f32 for the
+// small-field ones (bandwidth, core, power) used by the N32 path.
 __global__ __launch_bounds__(kBlock) void k_prep2(const uint64_t* __restrict__ maxima,
-                                                  uint32_t n_pods, double* __restrict__ rcp) {
+                                                  uint32_t n_pods, double* __restrict__ rcp,
+                                                  float* __restrict__ rcp32) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (p >= n_pods) return;
   const int src[5] = {kMaxBw, kMaxCore, kMaxPower, kMaxFree, kMaxTotal};
 #pragma unroll
-  for (int k = 0; k < 5; ++k)
-    rcp[(size_t)k * n_pods + p] = ru_100_over((double)maxima[(size_t)src[k] * n_pods + p]);
+  for (int k = 0; k < 5; ++k) {
+    const double M = (double)maxima[(size_t)src[k] * n_pods + p];
+    rcp[(size_t)k * n_pods + p] = ru_100_over(M);
+    if (k < 3) rcp32[(size_t)k * n_pods + p] = ru32_100_over(M);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
-// K2 fast path: CalculateBasicScore + Allocate + Actual in exact f64, running argmax with
+// K2 (F64 path): CalculateBasicScore + Allocate + Actual in exact f64, running argmax with
 // lowest-index ties, tie count and min over the feasible nodes of the chunk.
 template <int K>
 __global__ __launch_bounds__(kBlock) void k2_score_fast(
@@ -190,6 +216,7 @@ __global__ __launch_bounds__(kBlock) void k2_score_fast(
     const double* __restrict__ rcp, uint32_t n_pods, const uint32_t* __restrict__ bitmask,
     double* __restrict__ pbest, uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties,
     double* __restrict__ plow) {
+  using R = Rec<Path::F64>;
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t chunk = blockIdx.y;
   const uint32_t n0 = chunk * chunk_nodes;
@@ -211,26 +238,99 @@ __global__ __launch_bounds__(kBlock) void k2_score_fast(
     if ((n & 31u) == 0u) word = live ? bitmask[(size_t)(n >> 5) * n_pods + p] : 0u;
     const bool feas = (word >> (n & 31u)) & 1u;
     if (feas) {
-      const unsigned char* rec = nodes + (size_t)n * node_stride(K);
-      const NodeHdrF* h = reinterpret_cast<const NodeHdrF*>(rec);
-      const double* fld = reinterpret_cast<const double*>(rec + sizeof(NodeHdrF));
+      const unsigned char* rec = nodes + (size_t)n * R::stride(K);
+      const double stat = reinterpret_cast<const NodeHdrF*>(rec)->static_score;
+      const Group<double, K> fr = load_group<double, K>(rec + R::off(kFree, K));
+      const Group<double, K> ck = load_group<double, K>(rec + R::off(kClock, K));
+      const Group<double, K> bw = load_group<double, K>(rec + R::off(kBandwidth, K));
+      const Group<double, K> co = load_group<double, K>(rec + R::off(kCore, K));
+      const Group<double, K> pw = load_group<double, K>(rec + R::off(kPower, K));
+      const Group<double, K> to = load_group<double, K>(rec + R::off(kTotal, K));
       double basic = 0.0;
 #pragma unroll
       for (int j = 0; j < K; ++j) {
-        const double fr = fld[kFree * K + j], ck = fld[kClock * K + j];
-        if (fr >= m && ck >= c) {  // algorithm.go:271
-          // CalculateCardScore (algorithm.go:280-291): each quotient truncates before its
-          // weight; clock is divided by MaxBandwidth (:283).
-          double s = __builtin_trunc(fld[kBandwidth * K + j] * r_bw);
-          s += __builtin_trunc(ck * r_bw);
-          s += 2.0 * __builtin_trunc(fld[kCore * K + j] * r_core);
-          s += __builtin_trunc(fld[kPower * K + j] * r_pow);
-          s += 3.0 * __builtin_trunc(fr * r_free);
-          s += __builtin_trunc(fld[kTotal * K + j] * r_tot);
-          basic += s;
-        }
+        // CalculateCardScore (algorithm.go:280-291): each quotient truncates before its
+        // weight; clock is divided by MaxBandwidth (:283).  Every term is an exact integer
+        // < 2^52, so the sum is exact in any order and the weights fold into FMAs.
+        double s = __builtin_trunc(bw.v[j] * r_bw);
+        s += __builtin_trunc(ck.v[j] * r_bw);
+        s = __builtin_fma(__builtin_trunc(co.v[j] * r_core), 2.0, s);
+        s += __builtin_trunc(pw.v[j] * r_pow);
+        s = __builtin_fma(__builtin_trunc(fr.v[j] * r_free), 3.0, s);
+        s += __builtin_trunc(to.v[j] * r_tot);
+        basic += ((fr.v[j] >= m) & (ck.v[j] >= c)) ? s : 0.0;  // algorithm.go:271
       }
-      const double raw = basic + h->static_score;  // algorithm.go:96
+      const double raw = basic + stat;  // algorithm.go:96
+      if (raw > best) {
+        best = raw;
+        idx = n;
+        ties = 1;
+      } else if (raw == best) {
+        ++ties;
+      }
+      low = fmin(low, raw);
+    }
+  }
+  if (!live) return;
+  const size_t o = (size_t)chunk * n_pods + p;
+  pbest[o] = best;
+  pidx[o] = idx;
+  pties[o] = ties;
+  plow[o] = low;
+}
+
+// K2 (N32 path): same score; the four small-field quotients in f32 (exact under the N32
+// bounds), the two memory quotients in f64, the card score summed in u32 (< 2^27).
+template <int K>
+__global__ __launch_bounds__(kBlock) void k2_score_n32(
+    const unsigned char* __restrict__ nodes, uint32_t n_nodes, uint32_t chunk_nodes,
+    const uint32_t* __restrict__ m_32, const uint32_t* __restrict__ c_32,
+    const double* __restrict__ rcp, const float* __restrict__ rcp32, uint32_t n_pods,
+    const uint32_t* __restrict__ bitmask, double* __restrict__ pbest,
+    uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties, double* __restrict__ plow) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t chunk = blockIdx.y;
+  const uint32_t n0 = chunk * chunk_nodes;
+  const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
+  const bool live = p < n_pods;
+  uint32_t m = 0, c = 0;
+  float r_bw = 0, r_core = 0, r_pow = 0;
+  double r_free = 0, r_tot = 0;
+  if (live) {
+    m = m_32[p];
+    c = c_32[p];
+    r_bw = rcp32[0 * (size_t)n_pods + p];
+    r_core = rcp32[1 * (size_t)n_pods + p];
+    r_pow = rcp32[2 * (size_t)n_pods + p];
+    r_free = rcp[3 * (size_t)n_pods + p];
+    r_tot = rcp[4 * (size_t)n_pods + p];
+  }
+  double best = -1.0, low = 1.0e300;
+  uint32_t idx = 0xffffffffu, ties = 0, word = 0;
+  for (uint32_t n = n0; n < n1; ++n) {
+    if ((n & 31u) == 0u) word = live ? bitmask[(size_t)(n >> 5) * n_pods + p] : 0u;
+    const bool feas = (word >> (n & 31u)) & 1u;
+    if (feas) {
+      const unsigned char* rec = nodes + (size_t)n * n32_stride(K);
+      const double stat = reinterpret_cast<const NodeHdrF*>(rec)->static_score;
+      const Group<uint32_t, K> fr = load_group<uint32_t, K>(rec + n32_u32_off(kFree, K));
+      const Group<uint32_t, K> ck = load_group<uint32_t, K>(rec + n32_u32_off(kClock, K));
+      const Group<float, K> bwf = load_group<float, K>(rec + n32_f32_off(kF32Bandwidth, K));
+      const Group<float, K> ckf = load_group<float, K>(rec + n32_f32_off(kF32Clock, K));
+      const Group<float, K> cof = load_group<float, K>(rec + n32_f32_off(kF32Core, K));
+      const Group<float, K> pwf = load_group<float, K>(rec + n32_f32_off(kF32Power, K));
+      const Group<double, K> frd = load_group<double, K>(rec + n32_f64_off(kF64Free, K));
+      const Group<double, K> tod = load_group<double, K>(rec + n32_f64_off(kF64Total, K));
+      uint32_t basic = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        // CalculateCardScore (algorithm.go:280-291); clock / MaxBandwidth (:283)
+        uint32_t s = (uint32_t)(bwf.v[j] * r_bw) + (uint32_t)(ckf.v[j] * r_bw) +
+                     (uint32_t)(pwf.v[j] * r_pow) + (uint32_t)(tod.v[j] * r_tot);
+        s += 2u * (uint32_t)(cof.v[j] * r_core) + 3u * (uint32_t)(frd.v[j] * r_free);
+        basic += ((fr.v[j] >= m) & (ck.v[j] >= c)) ? s : 0u;  // algorithm.go:271
+      }
+      const double raw = (double)basic + stat;  // algorithm.go:96
       if (raw > best) {
         best = raw;
         idx = n;
@@ -599,49 +699,68 @@ __global__ __launch_bounds__(kBlock) void k_bitmask_transpose(const uint32_t* __
 
 static inline dim3 pod_grid(uint32_t n) { return dim3((n + kBlock - 1) / kBlock); }
 
-hipError_t launch_k1(int K, bool fast, const unsigned char* nodes, uint32_t n_nodes,
+hipError_t launch_k1(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, uint32_t n_pods,
                      const Partials& part, uint32_t* bitmask, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
-  if (fast) {
-    YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_filter_maxima<KK, true>), grid, dim3(kBlock), 0, s,
-                                        nodes, n_nodes, chunk_nodes, pp.m_f, pp.c_f, pp.m_u,
-                                        pp.c_u, pp.number, pp.need_mem, pp.need_clk, n_pods,
-                                        part.max_f, part.max_u, part.cnt, bitmask));
-  } else {
-    YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_filter_maxima<KK, false>), grid, dim3(kBlock), 0, s,
-                                        nodes, n_nodes, chunk_nodes, pp.m_f, pp.c_f, pp.m_u,
-                                        pp.c_u, pp.number, pp.need_mem, pp.need_clk, n_pods,
-                                        part.max_f, part.max_u, part.cnt, bitmask));
+  switch (path) {
+    case Path::N32:
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_filter_maxima<KK, Path::N32>), grid, dim3(kBlock), 0,
+                                          s, nodes, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
+                                          pp.number, pp.need_mem, pp.need_clk, n_pods, part.max_u,
+                                          part.cnt, bitmask));
+      break;
+    case Path::F64:
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_filter_maxima<KK, Path::F64>), grid, dim3(kBlock), 0,
+                                          s, nodes, n_nodes, chunk_nodes, pp.m_f, pp.c_f,
+                                          pp.number, pp.need_mem, pp.need_clk, n_pods, part.max_u,
+                                          part.cnt, bitmask));
+      break;
+    case Path::U64:
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_filter_maxima<KK, Path::U64>), grid, dim3(kBlock), 0,
+                                          s, nodes, n_nodes, chunk_nodes, pp.m_u, pp.c_u,
+                                          pp.number, pp.need_mem, pp.need_clk, n_pods, part.max_u,
+                                          part.cnt, bitmask));
+      break;
   }
   return hipGetLastError();
 }
 
-hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool fast,
-                          uint64_t* maxima, uint32_t* counts, hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce1, pod_grid(n_pods), dim3(kBlock), 0, s, part.max_f, part.max_u,
-                     part.cnt, C, n_pods, fast ? 1 : 0, maxima, counts);
+hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uint64_t* maxima,
+                          uint32_t* counts, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce1, pod_grid(n_pods), dim3(kBlock), 0, s, part.max_u, part.cnt, C,
+                     n_pods, maxima, counts);
   return hipGetLastError();
 }
 
-hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, hipStream_t s) {
-  hipLaunchKernelGGL(k_prep2, pod_grid(n_pods), dim3(kBlock), 0, s, maxima, n_pods, rcp);
+hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(k_prep2, pod_grid(n_pods), dim3(kBlock), 0, s, maxima, n_pods, rcp, rcp32);
   return hipGetLastError();
 }
 
-hipError_t launch_k2(int K, bool fast, const unsigned char* nodes, uint32_t n_nodes,
+hipError_t launch_k2(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
-                     const double* rcp, uint32_t n_pods, const uint32_t* bitmask,
-                     const Partials& part, hipStream_t s) {
+                     const double* rcp, const float* rcp32, uint32_t n_pods,
+                     const uint32_t* bitmask, const Partials& part, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
-  if (fast) {
-    YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_fast<KK>), grid, dim3(kBlock), 0, s, nodes,
-                                        n_nodes, chunk_nodes, pp.m_f, pp.c_f, rcp, n_pods,
-                                        bitmask, part.best_f, part.idx, part.ties, part.low_f));
-  } else {
-    YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_generic<KK>), grid, dim3(kBlock), 0, s, nodes,
-                                        n_nodes, chunk_nodes, pp.m_u, pp.c_u, maxima, n_pods,
-                                        bitmask, part.best_i, part.idx, part.ties, part.low_i));
+  switch (path) {
+    case Path::N32:
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_n32<KK>), grid, dim3(kBlock), 0, s, nodes,
+                                          n_nodes, chunk_nodes, pp.m_32, pp.c_32, rcp, rcp32,
+                                          n_pods, bitmask, part.best_f, part.idx, part.ties,
+                                          part.low_f));
+      break;
+    case Path::F64:
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_fast<KK>), grid, dim3(kBlock), 0, s, nodes,
+                                          n_nodes, chunk_nodes, pp.m_f, pp.c_f, rcp, n_pods,
+                                          bitmask, part.best_f, part.idx, part.ties, part.low_f));
+      break;
+    case Path::U64:
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_generic<KK>), grid, dim3(kBlock), 0, s, nodes,
+                                          n_nodes, chunk_nodes, pp.m_u, pp.c_u, maxima, n_pods,
+                                          bitmask, part.best_i, part.idx, part.ties, part.low_i));
+      break;
   }
   return hipGetLastError();
 }

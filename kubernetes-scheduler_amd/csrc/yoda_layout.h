@@ -14,10 +14,18 @@ constexpr int kBlock = 256;             // threads per workgroup = 4 waves = 256
 constexpr int kWave = 64;
 constexpr uint32_t kChunkAlign = 32;    // node-chunk granularity (one bitmask word)
 
-// Fast path: every card field <= kFastFieldMax and every score provably < 2^52, so the
-// whole score runs exactly in f64.
+// Three exact record formats, chosen per snapshot by the host:
+//   N32  every card field <= 0xFFFFFFFE, bandwidth/core/power <= 55738 and
+//        300*max_clock + max_bandwidth < 2^24: K1 runs on u32, K2's bandwidth/clock/core/
+//        power quotients in f32 (proof + exhaustive check: tools/check_div_lemma.c), the
+//        memory quotients in f64, the card score accumulates in u32.
+//   F64  every card field <= 2^44 and every score < 2^52: everything in exact f64.
+//   U64  anything else: Go's uint64 wrap-around arithmetic verbatim.
+enum class Path : int { N32 = 0, F64 = 1, U64 = 2 };
 constexpr uint64_t kFastFieldMax = 1ull << 44;
 constexpr uint64_t kFastScoreMax = 1ull << 52;
+constexpr uint64_t kN32FieldMax = 0xFFFFFFFEull;
+constexpr uint64_t kN32SmallFieldMax = 55738;  // 301 * x < 2^24
 
 // Record header of the fast path (32 B).  Cards follow: 6 groups of K doubles:
 //   free[K], clock[K], total[K], bandwidth[K], core[K], power[K].
@@ -43,7 +51,24 @@ static_assert(sizeof(NodeHdrG) == 32, "NodeHdrG layout");
 enum CardField { kFree = 0, kClock = 1, kTotal = 2, kBandwidth = 3, kCore = 4, kPower = 5 };
 constexpr int kCardFields = 6;
 
+// F64 / U64 record: header + 6 groups of K 8-byte fields in CardField order.
 __host__ __device__ constexpr uint32_t node_stride(int k) { return 32u + 48u * (uint32_t)k; }
+
+// N32 record: header (NodeHdrF) + 6 groups of K u32 in CardField order (K1 + the K2 card
+// predicate) + 4 groups of K f32 {bandwidth, clock, core, power} + 2 groups of K f64
+// {free, total} (K2 quotients).
+__host__ __device__ constexpr uint32_t n32_stride(int k) { return 32u + 56u * (uint32_t)k; }
+__host__ __device__ constexpr uint32_t n32_u32_off(int field, int k) {
+  return 32u + 4u * (uint32_t)(field * k);
+}
+enum N32F32 { kF32Bandwidth = 0, kF32Clock = 1, kF32Core = 2, kF32Power = 3 };
+__host__ __device__ constexpr uint32_t n32_f32_off(int g, int k) {
+  return 32u + 24u * (uint32_t)k + 4u * (uint32_t)(g * k);
+}
+enum N32F64 { kF64Free = 0, kF64Total = 1 };
+__host__ __device__ constexpr uint32_t n32_f64_off(int g, int k) {
+  return 32u + 40u * (uint32_t)k + 8u * (uint32_t)(g * k);
+}
 
 // Mode B node record: V = Cpu/100, U = DiskIO/50 (algorithm.go:71,73).
 struct alignas(16) NodeRecB {
@@ -57,6 +82,8 @@ struct PodParams {
   double* c_f;         // fast: scv/clock clamped to 2^53 (0 if absent)
   uint64_t* m_u;       // generic: scv/memory (0 if absent)
   uint64_t* c_u;       // generic: scv/clock  (0 if absent)
+  uint32_t* m_32;      // narrow: scv/memory clamped to 0xFFFFFFFF
+  uint32_t* c_32;      // narrow: scv/clock clamped to 0xFFFFFFFF
   uint64_t* number;    // PodFitsNumber operand: label value or 1
   uint32_t* need_mem;  // healthy cards with free >= m required (0 if label absent)
   uint32_t* need_clk;  // healthy cards with clock == c required (0 if label absent)
@@ -69,7 +96,8 @@ struct PodParams {
 struct PodState {
   uint64_t* maxima;    // [6][P] MaxValue in collection.go field order (see kMax* below)
   uint32_t* counts;    // [2][P] n_feasible, n_zero_total
-  double* rcp;         // [5][P] RU(100 / M) for bw, core, power, free, total (fast path)
+  double* rcp;         // [5][P] RU(100 / M) for bw, core, power, free, total (f64)
+  float* rcp32;        // [3][P] RU32(100 / M) for bw, core, power (narrow path)
   int64_t* best;       // [P] highest raw score over feasible nodes (-1: none)
   uint32_t* idx;       // [P] lowest global node index reaching it
   uint32_t* ties;      // [P] nodes reaching it
@@ -85,8 +113,7 @@ enum MaxField { kMaxBw = 0, kMaxClock = 1, kMaxCore = 2, kMaxFree = 3, kMaxPower
 
 // Chunk partials: [field][chunk][P].
 struct Partials {
-  double* max_f;       // [6][C][P] fast
-  uint64_t* max_u;     // [6][C][P] generic
+  uint64_t* max_u;     // [6][C][P]
   uint32_t* cnt;       // [2][C][P]
   double* best_f;      // [C][P]
   int64_t* best_i;     // [C][P] (generic; also used for exact normalize)

@@ -37,6 +37,7 @@ _SIGS = {
     "yoda_synchronize": ([_vp], C.c_int),
     "yoda_upload_nodes": ([_vp, C.POINTER(CNodeSoA), _u32, _u32], C.c_int),
     "yoda_uses_generic_path": ([_vp], C.c_int),
+    "yoda_record_path": ([_vp], C.c_int),
     "yoda_update_alloc": ([_vp, C.POINTER(C.c_uint64)], C.c_int),
     "yoda_eval": ([_vp, C.POINTER(CPodSoA), C.c_int, C.POINTER(CEvalOut)], C.c_int),
     "yoda_upload_pods": ([_vp, C.POINTER(CPodSoA)], C.c_int),
@@ -135,17 +136,23 @@ class Yoda:
     def synchronize(self):
         self._check(lib().yoda_synchronize(self._h), "yoda_synchronize")
 
-    def upload_nodes(self, nodes: NodeSoA, node_offset: int = 0, force_generic: bool = False):
+    def upload_nodes(self, nodes: NodeSoA, node_offset: int = 0, force_generic: bool = False,
+                     force_f64: bool = False):
         self._nodes = nodes.normalized()
         cn = self._nodes.c()
-        self._check(lib().yoda_upload_nodes(self._h, C.byref(cn), node_offset,
-                                            1 if force_generic else 0), "yoda_upload_nodes")
+        flags = (1 if force_generic else 0) | (2 if force_f64 else 0)
+        self._check(lib().yoda_upload_nodes(self._h, C.byref(cn), node_offset, flags),
+                    "yoda_upload_nodes")
         self.n_nodes = self._nodes.n_nodes
         self.node_offset = node_offset
 
     @property
     def generic(self) -> bool:
         return lib().yoda_uses_generic_path(self._h) == 1
+
+    @property
+    def path(self) -> str:
+        return {0: "n32", 1: "f64", 2: "u64"}[lib().yoda_record_path(self._h)]
 
     def update_alloc(self, alloc: np.ndarray):
         a = np.ascontiguousarray(alloc, dtype=np.uint64)

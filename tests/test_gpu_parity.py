@@ -36,8 +36,8 @@ def assert_same(got, want, mode=MODE_SCV, pods=None):
         np.testing.assert_array_equal(got.maxima[sel], want.maxima[sel], err_msg="maxima")
 
 
-def run_both(dev, nodes, pods, mode=MODE_SCV, force_generic=False, threads=8):
-    dev.upload_nodes(nodes, force_generic=force_generic)
+def run_both(dev, nodes, pods, mode=MODE_SCV, force_generic=False, threads=8, force_f64=False):
+    dev.upload_nodes(nodes, force_generic=force_generic, force_f64=force_f64)
     got = dev.eval(pods, mode)
     want = oracle.schedule(nodes, pods, mode, threads=threads)
     return got, want
@@ -65,7 +65,7 @@ def test_config1(dev, mode):
 def test_config2_full(dev, mode):
     nodes, pods = synth.make_config(2)   # 1k pods x 5k nodes, seed 42
     got, want = run_both(dev, nodes, pods, mode)
-    assert not dev.generic
+    assert dev.path == "n32"
     assert_same(got, want, mode)
     assert (got.status == 0).mean() > 0.5
 
@@ -81,14 +81,23 @@ def test_config4_heterogeneous(dev, mode):
         assert frac < 0.10
 
 
-def test_generic_path_matches_fast(dev):
+@pytest.mark.parametrize("path", ["n32", "f64", "u64"])
+def test_every_record_path(dev, path):
     nodes, pods = synth.make_config(2, pods=300, nodes=2000)
-    got_f, want = run_both(dev, nodes, pods)
-    assert not dev.generic
-    got_g, _ = run_both(dev, nodes, pods, force_generic=True)
-    assert dev.generic
-    assert_same(got_f, want)
-    assert_same(got_g, want)
+    got, want = run_both(dev, nodes, pods, force_generic=path == "u64", force_f64=path == "f64")
+    assert dev.path == path
+    assert_same(got, want)
+
+
+def test_f64_path_chosen_for_wide_fields(dev):
+    # free memory in bytes (> 2^32) leaves the narrow path but stays exact in f64
+    nodes, pods = synth.make_config(2, pods=200, nodes=1500)
+    nodes.card_free_memory[:] *= np.uint64(1 << 20)
+    nodes.card_total_memory[:] *= np.uint64(1 << 20)
+    pods.memory[:] *= np.uint64(1 << 20)
+    got, want = run_both(dev, nodes, pods)
+    assert dev.path == "f64"
+    assert_same(got, want)
 
 
 @pytest.mark.parametrize("k", [1, 2, 4, 8, 16])
@@ -116,8 +125,10 @@ def test_randomized_edges(dev, seed):
     pods.number[rng.random(400) < 0.05] = 0
     pods.memory[rng.random(400) < 0.05] = np.uint64((1 << 64) - 5)
     pods.clock[rng.random(400) < 0.05] = np.uint64(1 << 60)
-    for generic in (False, True):
-        got, want = run_both(dev, nodes, pods, force_generic=generic)
+    for path in ("n32", "f64", "u64"):
+        got, want = run_both(dev, nodes, pods, force_generic=path == "u64",
+                             force_f64=path == "f64")
+        assert dev.path == path
         assert_same(got, want)
 
 
