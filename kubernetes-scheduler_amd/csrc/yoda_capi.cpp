@@ -53,6 +53,7 @@ hipError_t launch_reduce3(const Partials& part, uint32_t C, const uint32_t* flag
                           int32_t* pick, int32_t* status, uint32_t* ties, hipStream_t s);
 hipError_t launch_bitmask_transpose(const uint32_t* in, uint32_t W, uint32_t n_pods,
                                     uint32_t* out, hipStream_t s);
+int kernel_capacity(int K, Path path, int which, int mode_diskio);
 }  // namespace yoda
 
 using namespace yoda;
@@ -123,7 +124,9 @@ struct yoda_handle {
   DevBuf maxima, counts, rcp, rcp32, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
   DevBuf bitmask, bitmask_t;
   DevBuf p_max_u, p_cnt, p_best_f, p_best_i, p_idx, p_ties, p_low_f, p_low_i, p_err;
-  uint32_t C = 1, chunk_nodes = 32;
+  uint32_t C1 = 1, chunk1 = 32;  // K1 node chunking
+  uint32_t C2 = 1, chunk2 = 32;  // K2 / K3 node chunking
+  int cap[2][3][2] = {};         // resident workgroups per (kernel, path, mode), cached
   int last_mode = -1;
   bool ran = false;
   bool ran_bitmask = false;
@@ -189,19 +192,36 @@ uint64_t static_score(uint64_t free_sum, uint64_t total_sum, uint64_t alloc, boo
   return allocate + actual;
 }
 
-// Pick chunking: enough workgroups to fill 256 CUs several times over.
-void plan_chunks(yoda_t* h, uint32_t n_pods, uint32_t n_nodes) {
+// Node chunking of one kernel: C chunks x ceil(P/256) pod blocks = B workgroups.  B is sized
+// to ~6 full "rounds" of the kernel's resident capacity (occupancy API), so the last round is
+// nearly full (efficiency >= 1 - pod_blocks / (6 cap)) and chunks stay small enough to
+// balance data-dependent work (K2 skips infeasible nodes).
+void plan_chunks_for(uint32_t cap, uint32_t n_pods, uint32_t n_nodes, uint32_t* C_out,
+                     uint32_t* chunk_out) {
   const uint32_t pod_blocks = std::max<uint32_t>(1, (n_pods + kBlock - 1) / kBlock);
   const uint32_t max_chunks = std::max<uint32_t>(1, (n_nodes + kChunkAlign - 1) / kChunkAlign);
-  uint32_t C = std::min(max_chunks, std::max<uint32_t>(1, (2048 + pod_blocks - 1) / pod_blocks));
+  if (cap == 0) cap = 2048;
+  uint32_t C = std::max<uint32_t>(1, (uint32_t)((6ull * cap) / pod_blocks));
+  C = std::min(C, max_chunks);
   uint32_t chunk = (n_nodes + C - 1) / C;
   chunk = std::max<uint32_t>(kChunkAlign, (chunk + kChunkAlign - 1) / kChunkAlign * kChunkAlign);
-  h->chunk_nodes = chunk;
-  h->C = std::max<uint32_t>(1, (n_nodes + chunk - 1) / chunk);
+  *chunk_out = chunk;
+  *C_out = std::max<uint32_t>(1, (n_nodes + chunk - 1) / chunk);
+}
+
+int capacity(yoda_t* h, int which, int mode) {
+  int& c = h->cap[which - 1][(int)h->path][mode == YODA_MODE_DISKIO ? 1 : 0];
+  if (c == 0) c = kernel_capacity(h->K, h->path, which, mode == YODA_MODE_DISKIO);
+  return c;
+}
+
+void plan_chunks(yoda_t* h, int mode, uint32_t n_pods, uint32_t n_nodes) {
+  plan_chunks_for((uint32_t)capacity(h, 1, mode), n_pods, n_nodes, &h->C1, &h->chunk1);
+  plan_chunks_for((uint32_t)capacity(h, 2, mode), n_pods, n_nodes, &h->C2, &h->chunk2);
 }
 
 int ensure_state(yoda_t* h, uint32_t P) {
-  const size_t CP = (size_t)h->C * P;
+  const size_t CP = (size_t)std::max(h->C1, h->C2) * P;
   const size_t W = (h->n_nodes + 31) / 32;
   HIP_TRY(h, h->maxima.ensure(6 * (size_t)P * 8));
   HIP_TRY(h, h->counts.ensure(2 * (size_t)P * 4));
@@ -293,13 +313,13 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts) {
   hipEvent_t e0 = h->profiling ? h->next_event() : nullptr;
   hipEvent_t e1 = h->profiling ? h->next_event() : nullptr;
   if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
-  HIP_TRY(h, launch_k1(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes, h->chunk_nodes,
-                       h->C, pod_params(h), P, part, h->bitmask.as<uint32_t>(), h->stream));
+  HIP_TRY(h, launch_k1(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes, h->chunk1,
+                       h->C1, pod_params(h), P, part, h->bitmask.as<uint32_t>(), h->stream));
   if (e1) {
     HIP_TRY(h, hipEventRecord(e1, h->stream));
     h->ev_k1.emplace_back(e0, e1);
   }
-  HIP_TRY(h, launch_reduce1(part, h->C, P, maxima, counts, h->stream));
+  HIP_TRY(h, launch_reduce1(part, h->C1, P, maxima, counts, h->stream));
   return YODA_OK;
 }
 
@@ -326,11 +346,11 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, int64_t* best, uint32_t*
     HIP_TRY(h, launch_prep2(maxima, P, h->rcp.as<double>(), h->rcp32.as<float>(), h->stream));
   if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
   if (mode == YODA_MODE_DISKIO) {
-    HIP_TRY(h, launch_k2_diskio(h->nodes_b.as<NodeRecB>(), h->n_nodes, h->chunk_nodes, h->C,
+    HIP_TRY(h, launch_k2_diskio(h->nodes_b.as<NodeRecB>(), h->n_nodes, h->chunk2, h->C2,
                                 pod_params(h), P, part, h->stream));
   } else {
     HIP_TRY(h, launch_k2(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes,
-                         h->chunk_nodes, h->C, pod_params(h), maxima, h->rcp.as<double>(),
+                         h->chunk2, h->C2, pod_params(h), maxima, h->rcp.as<double>(),
                          h->rcp32.as<float>(), P, h->bitmask.as<uint32_t>(), part, h->stream));
     is_f64 = !h->generic;
   }
@@ -338,7 +358,7 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, int64_t* best, uint32_t*
     HIP_TRY(h, hipEventRecord(e1, h->stream));
     h->ev_k2.emplace_back(e0, e1);
   }
-  HIP_TRY(h, launch_reduce2(part, h->C, P, is_f64, h->node_offset, best, idx, ties, low,
+  HIP_TRY(h, launch_reduce2(part, h->C2, P, is_f64, h->node_offset, best, idx, ties, low,
                             h->stream));
   return YODA_OK;
 }
@@ -363,11 +383,11 @@ int finalize(yoda_t* h, int mode, const uint32_t* counts, const int64_t* best,
                     "exact-normalize pods (int64 overflow in NormalizeScore) are not supported "
                     "on the sharded path yet; evaluate on a single handle");
       Partials part = partials(h);
-      HIP_TRY(h, launch_k3(h->K, h->nodes.as<unsigned char>(), h->n_nodes, h->chunk_nodes, h->C,
+      HIP_TRY(h, launch_k3(h->K, h->nodes.as<unsigned char>(), h->n_nodes, h->chunk2, h->C2,
                            pod_params(h), h->maxima.as<uint64_t>(), P, h->bitmask.as<uint32_t>(),
                            h->flagged.as<uint32_t>(), h->n_flagged.as<uint32_t>(), best, low,
                            part, nfl, h->stream));
-      HIP_TRY(h, launch_reduce3(part, h->C, h->flagged.as<uint32_t>(), h->n_flagged.as<uint32_t>(),
+      HIP_TRY(h, launch_reduce3(part, h->C2, h->flagged.as<uint32_t>(), h->n_flagged.as<uint32_t>(),
                                 nfl, h->node_offset, h->pick.as<int32_t>(), h->status.as<int32_t>(),
                                 h->ties_out.as<uint32_t>(), h->stream));
     }
@@ -458,7 +478,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     // Record format: the narrowest exact one.
     std::vector<uint64_t> stat(N);
     std::vector<uint8_t> zt(N);
-    uint64_t max_field = 0, max_small = 0, max_clock = 0, max_bw = 0, max_static = 0;
+    uint64_t max_field = 0, max_small = 0, max_clock = 0, max_static = 0;
     for (uint32_t i = 0; i < N; ++i) {
       bool z = false;
       const uint64_t alloc = nd->alloc_memory ? nd->alloc_memory[i] : 0;
@@ -471,17 +491,17 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
                               nd->card_clock[k], nd->card_bandwidth[k], nd->card_core[k],
                               nd->card_power[k]});
         max_small = std::max({max_small, nd->card_bandwidth[k], nd->card_core[k],
-                              nd->card_power[k]});
+                              nd->card_power[k], nd->card_clock[k]});
         max_clock = std::max(max_clock, nd->card_clock[k]);
-        max_bw = std::max(max_bw, nd->card_bandwidth[k]);
       }
     }
     // per-card score <= 800 + 100*clock (five quotients <= 100, clock/MaxBandwidth <= 100*clock)
     const long double score_bound =
         (long double)K * (800.0L + 100.0L * (long double)max_clock) + (long double)max_static;
     const bool f64_ok = max_field <= kFastFieldMax && score_bound < (long double)kFastScoreMax;
-    const bool n32_ok = f64_ok && max_field <= kN32FieldMax && max_small <= kN32SmallFieldMax &&
-                        300.0L * max_clock + max_bw < (long double)(1u << 24);
+    // bandwidth, clock, core and power <= 55738 on EVERY shard keeps 300 x + M < 2^24 for
+    // any maxima another shard contributes (all shards run one path: yoda_amd/dist.py).
+    const bool n32_ok = f64_ok && max_field <= kN32FieldMax && max_small <= kN32SmallFieldMax;
     Path path = n32_ok ? Path::N32 : (f64_ok ? Path::F64 : Path::U64);
     if ((flags & YODA_UPLOAD_FORCE_F64) && path == Path::N32) path = Path::F64;
     if (flags & YODA_UPLOAD_FORCE_GENERIC) path = Path::U64;
@@ -550,6 +570,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     h->nodes_diskio = diskio;
     h->n_nodes = N;
     h->node_offset = node_offset;
+    if (h->K != K || h->path != path) std::memset(h->cap, 0, sizeof(h->cap));
     h->K = K;
     h->path = path;
     h->generic = path == Path::U64;
@@ -672,7 +693,7 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
 static int prepare_run(yoda_t* h, int mode) {
   int rc = check_ready(h, mode);
   if (rc) return rc;
-  plan_chunks(h, h->n_pods, h->n_nodes);
+  plan_chunks(h, mode, h->n_pods, h->n_nodes);
   return ensure_state(h, std::max<uint32_t>(h->n_pods, 1));
 }
 

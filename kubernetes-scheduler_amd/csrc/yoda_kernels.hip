@@ -726,6 +726,35 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, uint32_t n_no
   return hipGetLastError();
 }
 
+// Resident 256-thread workgroups of one K1 / K2 instantiation on the whole device (occupancy
+// API x CUs), for grid sizing.  which: 1 = K1, 2 = K2.
+int kernel_capacity(int K, Path path, int which, int mode_diskio) {
+  int dev = 0, cus = 0, nb = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  const void* fn = nullptr;
+#define YODA_FN(expr) fn = reinterpret_cast<const void*>(expr)
+  if (mode_diskio) {
+    YODA_FN(&k2_diskio);
+  } else if (which == 1) {
+    switch (path) {
+      case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k1_filter_maxima<KK, Path::N32>))); break;
+      case Path::F64: YODA_K_SWITCH(K, YODA_FN((&k1_filter_maxima<KK, Path::F64>))); break;
+      case Path::U64: YODA_K_SWITCH(K, YODA_FN((&k1_filter_maxima<KK, Path::U64>))); break;
+    }
+  } else {
+    switch (path) {
+      case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k2_score_n32<KK>))); break;
+      case Path::F64: YODA_K_SWITCH(K, YODA_FN((&k2_score_fast<KK>))); break;
+      case Path::U64: YODA_K_SWITCH(K, YODA_FN((&k2_score_generic<KK>))); break;
+    }
+  }
+#undef YODA_FN
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kBlock, 0) != hipSuccess) return 0;
+  return nb * cus;
+}
+
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uint64_t* maxima,
                           uint32_t* counts, hipStream_t s) {
   hipLaunchKernelGGL(k_reduce1, pod_grid(n_pods), dim3(kBlock), 0, s, part.max_u, part.cnt, C,

@@ -15,8 +15,8 @@ constexpr int kWave = 64;
 constexpr uint32_t kChunkAlign = 32;    // node-chunk granularity (one bitmask word)
 
 // Three exact record formats, chosen per snapshot by the host:
-//   N32  every card field <= 0xFFFFFFFE, bandwidth/core/power <= 55738 and
-//        300*max_clock + max_bandwidth < 2^24: K1 runs on u32, K2's bandwidth/clock/core/
+//   N32  every card field <= 0xFFFFFFFE and bandwidth/clock/core/power <= 55738
+//        (so 300 x + M < 2^24 for every f32 quotient): K1 runs on u32, K2's bandwidth/clock/core/
 //        power quotients in f32 (proof + exhaustive check: tools/check_div_lemma.c), the
 //        memory quotients in f64, the card score accumulates in u32.
 //   F64  every card field <= 2^44 and every score < 2^52: everything in exact f64.
@@ -25,7 +25,7 @@ enum class Path : int { N32 = 0, F64 = 1, U64 = 2 };
 constexpr uint64_t kFastFieldMax = 1ull << 44;
 constexpr uint64_t kFastScoreMax = 1ull << 52;
 constexpr uint64_t kN32FieldMax = 0xFFFFFFFEull;
-constexpr uint64_t kN32SmallFieldMax = 55738;  // 301 * x < 2^24
+constexpr uint64_t kN32SmallFieldMax = 55738;  // 301 * 55738 < 2^24
 
 // Record header of the fast path (32 B).  Cards follow: 6 groups of K doubles:
 //   free[K], clock[K], total[K], bandwidth[K], core[K], power[K].

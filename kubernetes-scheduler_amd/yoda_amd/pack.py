@@ -1,0 +1,187 @@
+"""Host packers: k8s / SCV / advisor objects -> the SoA buffers of include/yoda.h.
+
+Inputs are plain dicts shaped like the API objects (JSON/YAML-decoded), so snapshots can be
+files instead of live Prometheus / API-server reads:
+
+  pod          k8s core/v1 Pod: metadata.labels scv/number|memory|clock|priority,
+               metadata.annotations diskIO, spec.containers/initContainers/overhead cpu
+  scv          NJUPT-ISL/SCV api/v1 Scv (go.mod:6, not vendored — JSON field names assumed
+               lowerCamelCase as kubebuilder emits them): status.cardNumber, cardList[{health,
+               freeMemory, totalMemory, clock, bandwidth, core, power}], freeMemorySum,
+               totalMemorySum
+  advisor      advisor.Result.Info (advisor.go:22-32): {node name: {Cpu, Memory, DiskIO, ...}}
+"""
+from __future__ import annotations
+
+import math
+import re
+from fractions import Fraction
+from typing import Dict, Iterable, List, Mapping, Optional, Sequence
+
+import numpy as np
+
+from .gostrconv import parse_float, pod_priority, str_to_uint
+from .soa import MAX_CARDS, NodeSoA, PodSoA
+
+# ---- k8s resource.Quantity (apimachinery) -------------------------------------------------
+_BIN = {"Ki": 2 ** 10, "Mi": 2 ** 20, "Gi": 2 ** 30, "Ti": 2 ** 40, "Pi": 2 ** 50, "Ei": 2 ** 60}
+_DEC = {"n": Fraction(1, 10 ** 9), "u": Fraction(1, 10 ** 6), "m": Fraction(1, 1000), "": 1,
+        "k": 10 ** 3, "M": 10 ** 6, "G": 10 ** 9, "T": 10 ** 12, "P": 10 ** 15, "E": 10 ** 18}
+_QTY = re.compile(r"^([+-]?)([0-9]*)(?:\.([0-9]*))?(.*)$")
+
+
+def parse_quantity(s: str) -> Fraction:
+    """resource.ParseQuantity value as an exact rational (raises ValueError if invalid)."""
+    s = str(s).strip()
+    m = _QTY.match(s)
+    if not m or not (m.group(2) or m.group(3)):
+        raise ValueError(f"invalid quantity {s!r}")
+    sign, ip, fp, suf = m.group(1), m.group(2) or "", m.group(3) or "", m.group(4)
+    v = Fraction(int(ip + fp) if (ip + fp) else 0, 10 ** len(fp))
+    if suf in _BIN:
+        v *= _BIN[suf]
+    elif suf in _DEC:
+        v *= _DEC[suf]
+    elif re.fullmatch(r"[eE][+-]?[0-9]+", suf):
+        v *= Fraction(10) ** int(suf[1:])
+    else:
+        raise ValueError(f"invalid quantity suffix {s!r}")
+    return -v if sign == "-" else v
+
+
+def milli_value(s: str) -> int:
+    """Quantity.MilliValue(): ceil(q * 1000)."""
+    return math.ceil(parse_quantity(s) * 1000)
+
+
+def value(s: str) -> int:
+    """Quantity.Value(): ceil(q)."""
+    return math.ceil(parse_quantity(s))
+
+
+DEFAULT_MILLI_CPU_REQUEST = 100  # k8s v1.22.3 pkg/scheduler/util/non_zero.go
+
+
+def nonzero_cpu_request(requests: Optional[Mapping[str, str]]) -> int:
+    """schedutil.GetNonzeroRequestForResource(cpu): 100m when unset (not when zero)."""
+    if not requests or "cpu" not in requests:
+        return DEFAULT_MILLI_CPU_REQUEST
+    return milli_value(requests["cpu"])
+
+
+def pod_cpu_request(pod: Mapping) -> int:
+    """score.CalculatePodResourceRequest(pod, cpu, true) (algorithm.go:238-262): sum of
+    containers, max'd with each init container, + overhead (Quantity.Value(), as the
+    reference writes it — cores, not millicores)."""
+    spec = pod.get("spec", {}) or {}
+    req = 0
+    for c in spec.get("containers", []) or []:
+        req += nonzero_cpu_request(((c.get("resources") or {}).get("requests")))
+    for c in spec.get("initContainers", []) or []:
+        v = nonzero_cpu_request(((c.get("resources") or {}).get("requests")))
+        req = max(req, v)
+    over = spec.get("overhead")
+    if over and "cpu" in over:
+        req += value(over["cpu"])
+    return req
+
+
+# ---- pods ----------------------------------------------------------------------------------
+def pack_pods(pods: Sequence[Mapping]) -> PodSoA:
+    P = len(pods)
+    out = {k: np.zeros(P, dt) for k, dt in (
+        ("has_number", np.uint8), ("number", np.uint64), ("has_memory", np.uint8),
+        ("memory", np.uint64), ("has_clock", np.uint8), ("clock", np.uint64),
+        ("priority", np.int64), ("rio", np.float64), ("rcpu", np.int64))}
+    for i, pod in enumerate(pods):
+        meta = pod.get("metadata", {}) or {}
+        labels = meta.get("labels", {}) or {}
+        ann = meta.get("annotations", {}) or {}
+        for key, has, val in (("scv/number", "has_number", "number"),
+                              ("scv/memory", "has_memory", "memory"),
+                              ("scv/clock", "has_clock", "clock")):
+            if key in labels:                       # filter.go:12,19,36
+                out[has][i] = 1
+                out[val][i] = str_to_uint(str(labels[key]))
+        if "scv/priority" in labels:                # sort.go:13
+            out["priority"][i] = pod_priority(str(labels["scv/priority"]))
+        # algorithm.go:103: Rio, _ := strconv.ParseFloat(pod.Annotations["diskIO"], 32)
+        out["rio"][i] = parse_float(str(ann.get("diskIO", "")), 32)[0]
+        out["rcpu"][i] = pod_cpu_request(pod)
+    return PodSoA(**out).normalized()
+
+
+# ---- nodes ---------------------------------------------------------------------------------
+def node_alloc_memory(node_names: Sequence[str], bound_pods: Iterable[Mapping]) -> np.ndarray:
+    """Σ scv/memory of the pods already on each node (algorithm.go:299-303), uint64 wrap."""
+    idx = {n: i for i, n in enumerate(node_names)}
+    alloc = [0] * len(node_names)
+    for pod in bound_pods:
+        node = (pod.get("spec", {}) or {}).get("nodeName")
+        labels = (pod.get("metadata", {}) or {}).get("labels", {}) or {}
+        if node in idx and "scv/memory" in labels:
+            alloc[idx[node]] = (alloc[idx[node]] + str_to_uint(str(labels["scv/memory"]))) \
+                & ((1 << 64) - 1)
+    return np.array(alloc, dtype=np.uint64)
+
+
+def pack_scvs(scvs: Sequence[Mapping], bound_pods: Iterable[Mapping] = (),
+              advisor: Optional[Mapping[str, Mapping]] = None,
+              max_cards: Optional[int] = None) -> NodeSoA:
+    """SCV CRD objects (one per node, in node order) -> NodeSoA.  `advisor` (Mode B) maps
+    node name -> advisor.NodeInfo fields {"Cpu", "DiskIO", ...}; a node missing from it
+    makes the reference panic (algorithm.go:70,73), so it is an error here."""
+    names = [(s.get("metadata", {}) or {}).get("name", str(i)) for i, s in enumerate(scvs)]
+    cards = [((s.get("status", {}) or {}).get("cardList") or []) for s in scvs]
+    k = max_cards or max([len(c) for c in cards] + [1])
+    if k > MAX_CARDS or any(len(c) > k for c in cards):
+        raise ValueError(f"more than {min(k, MAX_CARDS)} cards on a node")
+    N = len(scvs)
+    z = lambda dt: np.zeros((N, k), dt)  # noqa: E731
+    f, t, ck, bw, co, pw, h = (z(np.uint64), z(np.uint64), z(np.uint64), z(np.uint64),
+                               z(np.uint64), z(np.uint64), z(np.uint8))
+    for i, cl in enumerate(cards):
+        for j, c in enumerate(cl):
+            f[i, j] = int(c.get("freeMemory", 0))
+            t[i, j] = int(c.get("totalMemory", 0))
+            ck[i, j] = int(c.get("clock", 0))
+            bw[i, j] = int(c.get("bandwidth", 0))
+            co[i, j] = int(c.get("core", 0))
+            pw[i, j] = int(c.get("power", 0))
+            h[i, j] = c.get("health") == "Healthy"   # filter.go:53,57
+    st = [(s.get("status", {}) or {}) for s in scvs]
+    cpu = np.zeros(N)
+    disk = np.zeros(N)
+    if advisor is not None:
+        for i, n in enumerate(names):
+            if n not in advisor:
+                raise KeyError(f"node {n!r} missing from the advisor snapshot")
+            cpu[i] = float(advisor[n].get("Cpu", 0.0))
+            disk[i] = float(advisor[n].get("DiskIO", 0.0))
+    return NodeSoA(
+        card_number=np.array([int(x.get("cardNumber", 0)) for x in st], np.uint64),
+        card_count=np.array([len(c) for c in cards], np.uint32),
+        free_memory_sum=np.array([int(x.get("freeMemorySum", 0)) for x in st], np.uint64),
+        total_memory_sum=np.array([int(x.get("totalMemorySum", 0)) for x in st], np.uint64),
+        alloc_memory=node_alloc_memory(names, bound_pods),
+        card_free_memory=f, card_total_memory=t, card_clock=ck, card_bandwidth=bw,
+        card_core=co, card_power=pw, card_healthy=h, cpu=cpu, disk_io=disk).normalized()
+
+
+def scvs_from_soa(nodes: NodeSoA, prefix: str = "node-") -> List[Dict]:
+    """Inverse of pack_scvs (for fixtures and examples)."""
+    out = []
+    for i in range(nodes.n_nodes):
+        cl = [{"health": "Healthy" if nodes.card_healthy[i, j] else "Unhealthy",
+               "freeMemory": int(nodes.card_free_memory[i, j]),
+               "totalMemory": int(nodes.card_total_memory[i, j]),
+               "clock": int(nodes.card_clock[i, j]),
+               "bandwidth": int(nodes.card_bandwidth[i, j]),
+               "core": int(nodes.card_core[i, j]), "power": int(nodes.card_power[i, j])}
+              for j in range(int(nodes.card_count[i]))]
+        out.append({"apiVersion": "core.run-linux.com/v1", "kind": "Scv",
+                    "metadata": {"name": f"{prefix}{i}"},
+                    "status": {"cardNumber": int(nodes.card_number[i]), "cardList": cl,
+                               "freeMemorySum": int(nodes.free_memory_sum[i]),
+                               "totalMemorySum": int(nodes.total_memory_sum[i])}})
+    return out

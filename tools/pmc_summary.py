@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Summarise tools/profile.sh output: per kernel, average duration (kernel trace) and the
+average per-launch value of every PMC counter collected (one row per dispatch/counter)."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    n = name.split("(")[0]
+    for k in ("k1_filter_maxima", "k2_score", "k2_diskio", "k_reduce1", "k_reduce2",
+              "k_prep2", "k_finalize", "k3_exact_normalize"):
+        if k in n:
+            return k + (n[n.index("<"):] if "<" in n else "")
+    return n
+
+
+def main(out):
+    res = defaultdict(dict)
+    stats = glob.glob(os.path.join(out, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    for path in stats:
+        for r in csv.DictReader(open(path)):
+            res[short(r["Name"])]["avg_ns"] = float(r["AverageNs"])
+            res[short(r["Name"])]["calls"] = int(r["Calls"])
+    for path in glob.glob(os.path.join(out, "*", "**", "*counter_collection.csv"), recursive=True):
+        acc = defaultdict(lambda: defaultdict(list))
+        for r in csv.DictReader(open(path)):
+            acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, d in acc.items():
+            for c, v in d.items():
+                # rows are per dispatch (summed over dimensions already by rocprofv3)
+                res[k][c] = sum(v) / len(v)
+    for k, d in res.items():
+        if "FETCH_SIZE" in d:
+            # FETCH_SIZE / WRITE_SIZE are in KiB; gfx950 FETCH_SIZE under-counts wide streaming
+            # reads by 2x (MI355X_MICROARCH.md §HBM); both figures are reported.
+            d["hbm_read_bytes_raw"] = d["FETCH_SIZE"] * 1024
+            d["hbm_read_bytes_corrected_x2"] = d["FETCH_SIZE"] * 2048
+        if "WRITE_SIZE" in d:
+            d["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            d["hbm_bytes_per_launch"] = d["hbm_read_bytes_corrected_x2"] + d["hbm_write_bytes"]
+    json.dump(res, sys.stdout, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
