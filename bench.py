@@ -100,14 +100,15 @@ def main():
     b = shard_bounds(N, world)
     lo, hi = int(b[rank]), int(b[rank + 1])
     y = Yoda(local_rank)
-    y.upload_nodes(nodes.slice(lo, hi), node_offset=lo)
+    shard = nodes.slice(lo, hi)
+    y.upload_nodes(shard, node_offset=lo)
     y.upload_pods(pods)
     y.set_stream(torch.cuda.current_stream(device).cuda_stream)
     k_slots = int(nodes.card_count.max()) if N else 1
     k_slots = 1 << max(0, (k_slots - 1).bit_length())
 
     if world > 1:
-        ex = ShardExchange.distributed(y, device)
+        ex = ShardExchange.distributed(y, device, shard=shard, offset=lo)
         step = lambda: ex.step(mode)  # noqa: E731
     else:
         step = lambda: y.run(mode)  # noqa: E731

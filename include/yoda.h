@@ -180,6 +180,15 @@ int yoda_download(yoda_t* h, yoda_eval_out* out);
  * words[p * ((N + 31) / 32) + n / 32] is set iff node n (local) passed Filter for pod p. */
 int yoda_download_bitmask(yoda_t* h, uint32_t* words, uint64_t n_words);
 
+/* Framework-plugin row mode: for the uploaded pods (a handful — one per
+ * scheduling cycle), return the Filter result and the raw Score of EVERY node, so the
+ * plugin's Filter and Score become lookups and NormalizeScore/selectHost stay the
+ * reference's code.  bitmask: [P][ceil(N/32)] as yoda_download_bitmask; scores: [P][N]
+ * int64, the value Yoda.Score returns (after Uint64ToInt64), -1 where Filter fails.
+ * Also leaves the picks for yoda_download.  Either output may be NULL. */
+int yoda_score_rows(yoda_t* h, int mode, uint32_t* bitmask, uint64_t n_bitmask_words,
+                    int64_t* scores, uint64_t n_scores);
+
 /* Sharded evaluation.  Each rank holds a node shard; between phases the caller reduces
  * the exchange buffers across ranks (RCCL all-reduce) with the op named per buffer.
  *   phase1 -> d_maxima [6*P] u64 (MAX), d_counts [2*P] u32 (SUM: n_feasible, n_zero_total)

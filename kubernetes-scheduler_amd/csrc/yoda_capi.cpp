@@ -28,10 +28,13 @@ hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, fl
 hipError_t launch_k2(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
                      const double* rcp, const float* rcp32, uint32_t n_pods,
-                     const uint32_t* bitmask, const Partials& part, hipStream_t s);
+                     const uint32_t* bitmask, const Partials& part, int64_t* rows,
+                     hipStream_t s);
 hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
                             uint32_t C, const PodParams& pp, uint32_t n_pods, const Partials& part,
-                            hipStream_t s);
+                            int64_t* rows, hipStream_t s);
+hipError_t launch_rows_transpose(const int64_t* in, uint32_t n_nodes, uint32_t n_pods,
+                                 int64_t* out, hipStream_t s);
 hipError_t launch_reduce2(const Partials& part, uint32_t C, uint32_t n_pods, bool is_f64,
                           uint32_t node_offset, int64_t* best, uint32_t* idx, uint32_t* ties,
                           int64_t* low, hipStream_t s);
@@ -122,7 +125,7 @@ struct yoda_handle {
 
   // state
   DevBuf maxima, counts, rcp, rcp32, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
-  DevBuf bitmask, bitmask_t;
+  DevBuf bitmask, bitmask_t, rows, rows_t;
   DevBuf p_max_u, p_cnt, p_best_f, p_best_i, p_idx, p_ties, p_low_f, p_low_i, p_err;
   uint32_t C1 = 1, chunk1 = 32;  // K1 node chunking
   uint32_t C2 = 1, chunk2 = 32;  // K2 / K3 node chunking
@@ -155,6 +158,7 @@ struct yoda_handle {
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
                      &n_flagged, &bitmask,   &bitmask_t,  &p_max_u,      &p_cnt,
+                     &rows,      &rows_t,
                      &p_best_f,  &p_best_i,  &p_idx,      &p_ties,       &p_low_f,
                      &p_low_i,   &p_err};
     for (DevBuf* b : all) b->release();
@@ -325,7 +329,7 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts) {
 
 // Phase 2: Score over the feasible nodes with the (globally reduced) maxima.
 int phase2(yoda_t* h, int mode, const uint64_t* maxima, int64_t* best, uint32_t* idx,
-           uint32_t* ties, int64_t* low) {
+           uint32_t* ties, int64_t* low, int64_t* rows = nullptr) {
   const uint32_t P = h->n_pods;
   if (P == 0) return YODA_OK;
   if (h->n_nodes == 0) {
@@ -347,11 +351,12 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, int64_t* best, uint32_t*
   if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
   if (mode == YODA_MODE_DISKIO) {
     HIP_TRY(h, launch_k2_diskio(h->nodes_b.as<NodeRecB>(), h->n_nodes, h->chunk2, h->C2,
-                                pod_params(h), P, part, h->stream));
+                                pod_params(h), P, part, rows, h->stream));
   } else {
     HIP_TRY(h, launch_k2(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes,
                          h->chunk2, h->C2, pod_params(h), maxima, h->rcp.as<double>(),
-                         h->rcp32.as<float>(), P, h->bitmask.as<uint32_t>(), part, h->stream));
+                         h->rcp32.as<float>(), P, h->bitmask.as<uint32_t>(), part, rows,
+                         h->stream));
     is_f64 = !h->generic;
   }
   if (e1) {
@@ -774,6 +779,61 @@ int yoda_download_bitmask(yoda_t* h, uint32_t* words, uint64_t n_words) {
   HIP_TRY(h, hipMemcpyAsync(words, h->bitmask_t.p, need * 4, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
   return YODA_OK;
+}
+
+int yoda_score_rows(yoda_t* h, int mode, uint32_t* bitmask_out, uint64_t n_bitmask_words,
+                    int64_t* scores_out, uint64_t n_scores) {
+  int rc = prepare_run(h, mode);
+  if (rc) return rc;
+  try {
+    const uint32_t P = h->n_pods, N = h->n_nodes;
+    const uint64_t W = (N + 31) / 32;
+    if (bitmask_out && n_bitmask_words < W * P)
+      return fail(h, YODA_ERR_INVALID_ARG, "bitmask buffer too small");
+    if (scores_out && n_scores < (uint64_t)N * P)
+      return fail(h, YODA_ERR_INVALID_ARG, "scores buffer too small");
+    if ((uint64_t)N * P > (1ull << 31))
+      return fail(h, YODA_ERR_RANGE, "yoda_score_rows is for small pod batches (P*N <= 2^31)");
+    int64_t* rows = nullptr;
+    if (scores_out && (uint64_t)N * P > 0) {
+      HIP_TRY(h, h->rows.ensure((size_t)N * P * 8));
+      HIP_TRY(h, h->rows_t.ensure((size_t)N * P * 8));
+      HIP_TRY(h, hipMemsetAsync(h->rows.p, 0xff, (size_t)N * P * 8, h->stream));  // -1
+      rows = h->rows.as<int64_t>();
+    }
+    if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>()))) return rc;
+    if ((rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->best.as<int64_t>(),
+                     h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(),
+                     rows)))
+      return rc;
+    if ((rc = finalize(h, mode, h->counts.as<uint32_t>(), h->best.as<int64_t>(),
+                       h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(),
+                       false)))
+      return rc;
+    h->ran = true;
+    h->ran_bitmask = mode == YODA_MODE_SCV;
+    h->last_mode = mode;
+    if (rows) {
+      HIP_TRY(h, launch_rows_transpose(rows, N, P, h->rows_t.as<int64_t>(), h->stream));
+      HIP_TRY(h, hipMemcpyAsync(scores_out, h->rows_t.p, (size_t)N * P * 8,
+                                hipMemcpyDeviceToHost, h->stream));
+    }
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    if (bitmask_out && W * P > 0) {
+      if (mode == YODA_MODE_DISKIO) {  // Filter is a pass-through: every node feasible
+        for (uint64_t p = 0; p < P; ++p)
+          for (uint64_t w = 0; w < W; ++w) {
+            const uint32_t bits = (w + 1) * 32 <= N ? 0xffffffffu : ((1u << (N % 32)) - 1);
+            bitmask_out[p * W + w] = bits;
+          }
+      } else if ((rc = yoda_download_bitmask(h, bitmask_out, n_bitmask_words))) {
+        return rc;
+      }
+    }
+    return YODA_OK;
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
 }
 
 int yoda_eval(yoda_t* h, const yoda_pod_soa* pods, int mode, yoda_eval_out* out) {

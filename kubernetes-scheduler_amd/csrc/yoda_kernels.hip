@@ -209,13 +209,14 @@ __global__ __launch_bounds__(kBlock) void k_prep2(const uint64_t* __restrict__ m
 // ---------------------------------------------------------------------------------------
 // K2 (F64 path): CalculateBasicScore + Allocate + Actual in exact f64, running argmax with
 // lowest-index ties, tie count and min over the feasible nodes of the chunk.
-template <int K>
+// ROWS: also write every feasible pair's raw score to rows[n][p] (plugin row mode).
+template <int K, bool ROWS>
 __global__ __launch_bounds__(kBlock) void k2_score_fast(
     const unsigned char* __restrict__ nodes, uint32_t n_nodes, uint32_t chunk_nodes,
     const double* __restrict__ m_f, const double* __restrict__ c_f,
     const double* __restrict__ rcp, uint32_t n_pods, const uint32_t* __restrict__ bitmask,
     double* __restrict__ pbest, uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties,
-    double* __restrict__ plow) {
+    double* __restrict__ plow, int64_t* __restrict__ rows) {
   using R = Rec<Path::F64>;
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t chunk = blockIdx.y;
@@ -261,6 +262,7 @@ __global__ __launch_bounds__(kBlock) void k2_score_fast(
         basic += ((fr.v[j] >= m) & (ck.v[j] >= c)) ? s : 0.0;  // algorithm.go:271
       }
       const double raw = basic + stat;  // algorithm.go:96
+      if constexpr (ROWS) rows[(size_t)n * n_pods + p] = (int64_t)raw;
       if (raw > best) {
         best = raw;
         idx = n;
@@ -281,13 +283,14 @@ __global__ __launch_bounds__(kBlock) void k2_score_fast(
 
 // K2 (N32 path): same score; the four small-field quotients in f32 (exact under the N32
 // bounds), the two memory quotients in f64, the card score summed in u32 (< 2^27).
-template <int K>
+template <int K, bool ROWS>
 __global__ __launch_bounds__(kBlock) void k2_score_n32(
     const unsigned char* __restrict__ nodes, uint32_t n_nodes, uint32_t chunk_nodes,
     const uint32_t* __restrict__ m_32, const uint32_t* __restrict__ c_32,
     const double* __restrict__ rcp, const float* __restrict__ rcp32, uint32_t n_pods,
     const uint32_t* __restrict__ bitmask, double* __restrict__ pbest,
-    uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties, double* __restrict__ plow) {
+    uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties, double* __restrict__ plow,
+    int64_t* __restrict__ rows) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t chunk = blockIdx.y;
   const uint32_t n0 = chunk * chunk_nodes;
@@ -331,6 +334,7 @@ __global__ __launch_bounds__(kBlock) void k2_score_n32(
         basic += ((fr.v[j] >= m) & (ck.v[j] >= c)) ? s : 0u;  // algorithm.go:271
       }
       const double raw = (double)basic + stat;  // algorithm.go:96
+      if constexpr (ROWS) rows[(size_t)n * n_pods + p] = (int64_t)raw;
       if (raw > best) {
         best = raw;
         idx = n;
@@ -381,13 +385,13 @@ __device__ __forceinline__ int64_t raw_score_u64(const unsigned char* rec, uint6
   return raw > (uint64_t)kI64Max ? 0 : (int64_t)raw;  // filter.Uint64ToInt64 (filter.go:84-86)
 }
 
-template <int K>
+template <int K, bool ROWS>
 __global__ __launch_bounds__(kBlock) void k2_score_generic(
     const unsigned char* __restrict__ nodes, uint32_t n_nodes, uint32_t chunk_nodes,
     const uint64_t* __restrict__ m_u, const uint64_t* __restrict__ c_u,
     const uint64_t* __restrict__ maxima, uint32_t n_pods, const uint32_t* __restrict__ bitmask,
     int64_t* __restrict__ pbest, uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties,
-    int64_t* __restrict__ plow) {
+    int64_t* __restrict__ plow, int64_t* __restrict__ rows) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t chunk = blockIdx.y;
   const uint32_t n0 = chunk * chunk_nodes;
@@ -406,6 +410,7 @@ __global__ __launch_bounds__(kBlock) void k2_score_generic(
     if ((n & 31u) == 0u) word = live ? bitmask[(size_t)(n >> 5) * n_pods + p] : 0u;
     if ((word >> (n & 31u)) & 1u) {
       const int64_t s = raw_score_u64<K>(nodes + (size_t)n * node_stride(K), m, c, M);
+      if constexpr (ROWS) rows[(size_t)n * n_pods + p] = s;
       if (s > best) {
         best = s;
         idx = n;
@@ -427,6 +432,7 @@ __global__ __launch_bounds__(kBlock) void k2_score_generic(
 // ---------------------------------------------------------------------------------------
 // K2B: BalancedCpuDiskIOPriority (algorithm.go:99-119), every node feasible
 // (Yoda.Filter is a pass-through, scheduler.go:96-99).  No FMA contraction (Go on amd64).
+template <bool ROWS>
 __global__ __launch_bounds__(kBlock) void k2_diskio(const NodeRecB* __restrict__ nodes,
                                                     uint32_t n_nodes, uint32_t chunk_nodes,
                                                     const double* __restrict__ alpha_in,
@@ -434,7 +440,8 @@ __global__ __launch_bounds__(kBlock) void k2_diskio(const NodeRecB* __restrict__
                                                     uint32_t n_pods, double* __restrict__ pbest,
                                                     uint32_t* __restrict__ pidx,
                                                     uint32_t* __restrict__ pties,
-                                                    double* __restrict__ plow) {
+                                                    double* __restrict__ plow,
+                                                    int64_t* __restrict__ rows) {
 #pragma clang fp contract(off)
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t chunk = blockIdx.y;
@@ -453,6 +460,9 @@ __global__ __launch_bounds__(kBlock) void k2_diskio(const NodeRecB* __restrict__
     const double s = 10.0 - t;                // :111
     // uint64(Si) on amd64 then Uint64ToInt64: trunc for Si >= 1, else 0 (NaN, negatives)
     const double score = (s >= 1.0) ? __builtin_trunc(s) : 0.0;
+    if constexpr (ROWS) {
+      if (live) rows[(size_t)n * n_pods + p] = (int64_t)score;
+    }
     if (score > best) {
       best = score;
       idx = n;
@@ -736,7 +746,7 @@ int kernel_capacity(int K, Path path, int which, int mode_diskio) {
   const void* fn = nullptr;
 #define YODA_FN(expr) fn = reinterpret_cast<const void*>(expr)
   if (mode_diskio) {
-    YODA_FN(&k2_diskio);
+    YODA_FN(&k2_diskio<false>);
   } else if (which == 1) {
     switch (path) {
       case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k1_filter_maxima<KK, Path::N32>))); break;
@@ -745,9 +755,9 @@ int kernel_capacity(int K, Path path, int which, int mode_diskio) {
     }
   } else {
     switch (path) {
-      case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k2_score_n32<KK>))); break;
-      case Path::F64: YODA_K_SWITCH(K, YODA_FN((&k2_score_fast<KK>))); break;
-      case Path::U64: YODA_K_SWITCH(K, YODA_FN((&k2_score_generic<KK>))); break;
+      case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k2_score_n32<KK, false>))); break;
+      case Path::F64: YODA_K_SWITCH(K, YODA_FN((&k2_score_fast<KK, false>))); break;
+      case Path::U64: YODA_K_SWITCH(K, YODA_FN((&k2_score_generic<KK, false>))); break;
     }
   }
 #undef YODA_FN
@@ -768,38 +778,78 @@ hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, fl
   return hipGetLastError();
 }
 
-hipError_t launch_k2(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
-                     uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
-                     const double* rcp, const float* rcp32, uint32_t n_pods,
-                     const uint32_t* bitmask, const Partials& part, hipStream_t s) {
+template <bool ROWS>
+static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
+                              uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
+                              const uint64_t* maxima, const double* rcp, const float* rcp32,
+                              uint32_t n_pods, const uint32_t* bitmask, const Partials& part,
+                              int64_t* rows, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   switch (path) {
     case Path::N32:
-      YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_n32<KK>), grid, dim3(kBlock), 0, s, nodes,
-                                          n_nodes, chunk_nodes, pp.m_32, pp.c_32, rcp, rcp32,
-                                          n_pods, bitmask, part.best_f, part.idx, part.ties,
-                                          part.low_f));
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_n32<KK, ROWS>), grid, dim3(kBlock), 0, s,
+                                          nodes, n_nodes, chunk_nodes, pp.m_32, pp.c_32, rcp,
+                                          rcp32, n_pods, bitmask, part.best_f, part.idx,
+                                          part.ties, part.low_f, rows));
       break;
     case Path::F64:
-      YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_fast<KK>), grid, dim3(kBlock), 0, s, nodes,
-                                          n_nodes, chunk_nodes, pp.m_f, pp.c_f, rcp, n_pods,
-                                          bitmask, part.best_f, part.idx, part.ties, part.low_f));
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_fast<KK, ROWS>), grid, dim3(kBlock), 0, s,
+                                          nodes, n_nodes, chunk_nodes, pp.m_f, pp.c_f, rcp,
+                                          n_pods, bitmask, part.best_f, part.idx, part.ties,
+                                          part.low_f, rows));
       break;
     case Path::U64:
-      YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_generic<KK>), grid, dim3(kBlock), 0, s, nodes,
-                                          n_nodes, chunk_nodes, pp.m_u, pp.c_u, maxima, n_pods,
-                                          bitmask, part.best_i, part.idx, part.ties, part.low_i));
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_generic<KK, ROWS>), grid, dim3(kBlock), 0,
+                                          s, nodes, n_nodes, chunk_nodes, pp.m_u, pp.c_u, maxima,
+                                          n_pods, bitmask, part.best_i, part.idx, part.ties,
+                                          part.low_i, rows));
       break;
   }
   return hipGetLastError();
 }
 
+hipError_t launch_k2(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
+                     uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
+                     const double* rcp, const float* rcp32, uint32_t n_pods,
+                     const uint32_t* bitmask, const Partials& part, int64_t* rows,
+                     hipStream_t s) {
+  if (rows)
+    return launch_k2_t<true>(K, path, nodes, n_nodes, chunk_nodes, C, pp, maxima, rcp, rcp32,
+                             n_pods, bitmask, part, rows, s);
+  return launch_k2_t<false>(K, path, nodes, n_nodes, chunk_nodes, C, pp, maxima, rcp, rcp32,
+                            n_pods, bitmask, part, rows, s);
+}
+
 hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
                             uint32_t C, const PodParams& pp, uint32_t n_pods, const Partials& part,
-                            hipStream_t s) {
+                            int64_t* rows, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
-  hipLaunchKernelGGL(k2_diskio, grid, dim3(kBlock), 0, s, nodes, n_nodes, chunk_nodes, pp.alpha,
-                     pp.beta, n_pods, part.best_f, part.idx, part.ties, part.low_f);
+  if (rows)
+    hipLaunchKernelGGL(k2_diskio<true>, grid, dim3(kBlock), 0, s, nodes, n_nodes, chunk_nodes,
+                       pp.alpha, pp.beta, n_pods, part.best_f, part.idx, part.ties, part.low_f,
+                       rows);
+  else
+    hipLaunchKernelGGL(k2_diskio<false>, grid, dim3(kBlock), 0, s, nodes, n_nodes, chunk_nodes,
+                       pp.alpha, pp.beta, n_pods, part.best_f, part.idx, part.ties, part.low_f,
+                       rows);
+  return hipGetLastError();
+}
+
+// rows [N][P] (coalesced for the kernels) -> [P][N] (host API layout).
+__global__ __launch_bounds__(kBlock) void k_rows_transpose(const int64_t* __restrict__ in,
+                                                           uint32_t n_nodes, uint32_t n_pods,
+                                                           int64_t* __restrict__ out) {
+  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= (uint64_t)n_nodes * n_pods) return;
+  const uint32_t p = (uint32_t)(t / n_nodes), n = (uint32_t)(t % n_nodes);
+  out[t] = in[(size_t)n * n_pods + p];
+}
+
+hipError_t launch_rows_transpose(const int64_t* in, uint32_t n_nodes, uint32_t n_pods,
+                                 int64_t* out, hipStream_t s) {
+  const uint64_t total = (uint64_t)n_nodes * n_pods;
+  dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
+  hipLaunchKernelGGL(k_rows_transpose, grid, dim3(kBlock), 0, s, in, n_nodes, n_pods, out);
   return hipGetLastError();
 }
 

@@ -44,6 +44,8 @@ _SIGS = {
     "yoda_run": ([_vp, C.c_int, _u32], C.c_int),
     "yoda_download": ([_vp, C.POINTER(CEvalOut)], C.c_int),
     "yoda_download_bitmask": ([_vp, C.POINTER(C.c_uint32), C.c_uint64], C.c_int),
+    "yoda_score_rows": ([_vp, C.c_int, C.POINTER(C.c_uint32), C.c_uint64,
+                         C.POINTER(C.c_int64), C.c_uint64], C.c_int),
     "yoda_shard_phase1": ([_vp, C.c_int, _vp, _vp], C.c_int),
     "yoda_shard_phase2": ([_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "yoda_shard_prepare_merge": ([_vp, _vp, _vp, _vp, _vp], C.c_int),
@@ -151,6 +153,11 @@ class Yoda:
         return lib().yoda_uses_generic_path(self._h) == 1
 
     @property
+    def path_code(self) -> int:
+        """0 = N32, 1 = F64, 2 = U64 (include/yoda.h YODA_PATH_*)."""
+        return int(lib().yoda_record_path(self._h))
+
+    @property
     def path(self) -> str:
         return {0: "n32", 1: "f64", 2: "u64"}[lib().yoda_record_path(self._h)]
 
@@ -182,6 +189,19 @@ class Yoda:
             self._h, words.ctypes.data_as(C.POINTER(C.c_uint32)), words.size),
             "yoda_download_bitmask")
         return words
+
+    def score_rows(self, mode: int = 0):
+        """(feasible bool [P, N], raw Score int64 [P, N] with -1 where Filter fails) for the
+        uploaded pods — the plugin's per-cycle lookups."""
+        P, N = self.n_pods, self.n_nodes
+        w = (N + 31) // 32
+        words = np.zeros((P, w), np.uint32)
+        scores = np.zeros((P, N), np.int64)
+        self._check(lib().yoda_score_rows(
+            self._h, mode, words.ctypes.data_as(C.POINTER(C.c_uint32)), words.size,
+            scores.ctypes.data_as(C.POINTER(C.c_int64)), scores.size), "yoda_score_rows")
+        feas = np.unpackbits(words.view(np.uint8), axis=1, bitorder="little")[:, :N].astype(bool)
+        return feas, scores
 
     def eval(self, pods: PodSoA, mode: int = 0) -> EvalResult:
         self.upload_pods(pods)

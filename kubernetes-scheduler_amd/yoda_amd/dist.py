@@ -104,6 +104,20 @@ def merge_phase2(reduce: Reducer, bufs: List[ShardBuffers],
     reduce([b.lowest for b in bufs], "min")
 
 
+def agree_on_path(reduce: Reducer, handles, shards, offsets, device):
+    """Every shard must run the SAME record path: the exactness bounds of the fast paths
+    involve maxima contributed by other shards.  Take the widest path any
+    shard needs (N32 < F64 < U64) and re-upload the shards that chose a narrower one."""
+    codes = [torch.tensor([h.path_code], dtype=torch.int64, device=device) for h in handles]
+    reduce(codes, "max")
+    target = int(codes[0].item())
+    for h, nodes, off in zip(handles, shards, offsets):
+        if h.path_code != target:
+            h.upload_nodes(nodes, node_offset=off, force_generic=target == 2,
+                           force_f64=target == 1)
+    return target
+
+
 class ShardExchange:
     """Drives libyoda handles (one per shard) through the sharded entry points."""
 
@@ -117,12 +131,21 @@ class ShardExchange:
             h.set_stream(stream)
 
     @classmethod
-    def local(cls, handles, device):
-        return cls(handles, Reducer(local=True), device)
+    def local(cls, handles, device, shards=None, offsets=None):
+        """Several shards in one process (single-GPU testing).  Pass the node shards to
+        enforce a common record path."""
+        red = Reducer(local=True)
+        if shards is not None:
+            agree_on_path(red, handles, shards, offsets, device)
+        return cls(handles, red, device)
 
     @classmethod
-    def distributed(cls, handle, device, group=None):
-        return cls([handle], Reducer(group=group), device)
+    def distributed(cls, handle, device, shard=None, offset=0, group=None):
+        """One shard per rank over torch.distributed (RCCL)."""
+        red = Reducer(group=group)
+        if shard is not None:
+            agree_on_path(red, [handle], [shard], [offset], device)
+        return cls([handle], red, device)
 
     def _prepare(self, h, b: ShardBuffers):
         p = ShardBuffers.ptr

@@ -66,7 +66,7 @@ _HEX = re.compile(r"^0[xX]([0-9a-fA-F_]*)(?:\.([0-9a-fA-F_]*))?[pP]([+-]?[0-9_]+
 
 def _underscore_ok(s: str) -> bool:
     """strconv.underscoreOK: '_' only between digits (or after a base prefix)."""
-    if s[:1] in "+-":
+    if s and s[0] in "+-":
         s = s[1:]
     saw = "^"
     i = 0
@@ -118,13 +118,13 @@ def parse_float(s: str, bit_size: int = 64) -> Tuple[float, bool]:
     as a float64.  Syntax error -> (0, False); overflow -> (±Inf, False)."""
     t = s
     neg = False
-    if t[:1] in "+-":
+    if t and t[0] in "+-":
         neg = t[0] == "-"
         t = t[1:]
     low = t.lower()
     if low in ("inf", "infinity"):
         return (-math.inf if neg else math.inf), True
-    if low == "nan" and s[:1] not in "+-":
+    if low == "nan" and not (s and s[0] in "+-"):
         return math.nan, True
     q = None
     m = _HEX.match(t)

@@ -185,3 +185,27 @@ def scvs_from_soa(nodes: NodeSoA, prefix: str = "node-") -> List[Dict]:
                                "freeMemorySum": int(nodes.free_memory_sum[i]),
                                "totalMemorySum": int(nodes.total_memory_sum[i])}})
     return out
+
+
+def pods_to_dicts(pods: PodSoA, prefix: str = "pod-") -> List[Dict]:
+    """PodSoA -> k8s-style pod dicts that pack_pods maps back to the same SoA (labels as
+    decimal strings; rio written with repr so ParseFloat(., 32) returns it; rcpu as a
+    millicore request)."""
+    out = []
+    for i in range(pods.n_pods):
+        labels = {}
+        if pods.has_number[i]:
+            labels["scv/number"] = str(int(pods.number[i]))
+        if pods.has_memory[i]:
+            labels["scv/memory"] = str(int(pods.memory[i]))
+        if pods.has_clock[i]:
+            labels["scv/clock"] = str(int(pods.clock[i]))
+        if pods.priority[i]:
+            labels["scv/priority"] = str(int(pods.priority[i]))
+        rio = float(pods.rio[i])
+        ann = {"diskIO": repr(rio) if np.isfinite(rio) else ("+Inf" if rio > 0 else "-Inf")} \
+            if rio != 0 else {}
+        out.append({"metadata": {"name": f"{prefix}{i}", "labels": labels, "annotations": ann},
+                    "spec": {"containers": [{"name": "c", "resources": {"requests": {
+                        "cpu": f"{int(pods.rcpu[i])}m"}}}]}})
+    return out

@@ -1,0 +1,59 @@
+"""Committed golden fixtures (tests/golden/, made by make_golden.py from the oracle and the
+independent Python restatement): the oracle must reproduce them (CPU) and so must libyoda
+(GPU), on every record path."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from yoda_amd.soa import EvalResult, NodeSoA, PodSoA
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FIXTURES = sorted(glob.glob(os.path.join(HERE, "*.npz")))
+OUT = ["pick", "status", "n_feasible", "n_ties", "top_score", "maxima"]
+
+
+def load(path):
+    z = np.load(path, allow_pickle=False)
+    nodes = NodeSoA(**{k[5:]: z[k] for k in z.files if k.startswith("node_")})
+    pods = PodSoA(**{k[4:]: z[k] for k in z.files if k.startswith("pod_")})
+    return nodes, pods, z
+
+
+def check(res, z, mode):
+    ok = z[f"mode{mode}_status"] == 0
+    for f in OUT:
+        want, got = z[f"mode{mode}_{f}"], getattr(res, f)
+        if f in ("n_ties", "top_score"):
+            want, got = want[ok], got[ok]
+        if f == "maxima" and mode == 1:
+            continue
+        np.testing.assert_array_equal(got, want, err_msg=f)
+
+
+def test_fixtures_present():
+    assert len(FIXTURES) >= 6
+
+
+@pytest.mark.parametrize("path", FIXTURES, ids=os.path.basename)
+def test_oracle_reproduces_golden(path):
+    nodes, pods, z = load(path)
+    for mode in (0, 1):
+        check(oracle.schedule(nodes, pods, mode), z, mode)
+    for flags in (0, 1):
+        pick, _ = oracle.greedy(nodes, pods, 0, flags)
+        np.testing.assert_array_equal(pick, z[f"greedy{flags}_pick"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", FIXTURES, ids=os.path.basename)
+def test_gpu_reproduces_golden(path):
+    from yoda_amd.capi import Yoda
+    nodes, pods, z = load(path)
+    with Yoda(0) as y:
+        for rec in ("auto", "f64", "u64"):
+            y.upload_nodes(nodes, force_f64=rec == "f64", force_generic=rec == "u64")
+            for mode in (0, 1):
+                check(y.eval(pods, mode), z, mode)

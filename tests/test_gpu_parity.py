@@ -221,19 +221,44 @@ def test_sharded_merge_on_one_gpu(dev):
     want = oracle.schedule(nodes, pods, MODE_SCV, threads=8)
     for G in (2, 3):
         bounds = np.linspace(0, nodes.n_nodes, G + 1).astype(int)
-        handles = []
+        handles, shards = [], []
         for g in range(G):
             y = Yoda(0)
-            y.upload_nodes(nodes.slice(bounds[g], bounds[g + 1]), node_offset=int(bounds[g]))
+            shards.append(nodes.slice(bounds[g], bounds[g + 1]))
+            y.upload_nodes(shards[-1], node_offset=int(bounds[g]))
             y.upload_pods(pods)
             handles.append(y)
-        ex = ShardExchange.local(handles, torch.device("cuda:0"))
+        ex = ShardExchange.local(handles, torch.device("cuda:0"), shards,
+                                 [int(b) for b in bounds[:-1]])
         for mode in (MODE_SCV, MODE_DISKIO):
             res = ex.run(mode)
             w = want if mode == MODE_SCV else oracle.schedule(nodes, pods, mode, threads=8)
             assert_same(res, w, mode)
         for y in handles:
             y.close()
+
+
+def test_sharded_paths_agree(dev):
+    """One shard needs the F64 path (a wide field), the other would pick N32: both must
+    end on F64, and the merged result must equal the single-handle result."""
+    import torch
+    from yoda_amd.dist import ShardExchange
+    nodes, pods = synth.make_config(2, pods=300, nodes=2000)
+    nodes.card_bandwidth[1500, 0] = np.uint64(70000)   # > 55738: F64 on shard 1 only
+    want = oracle.schedule(nodes, pods, MODE_SCV, threads=8)
+    shards = [nodes.slice(0, 1000), nodes.slice(1000, 2000)]
+    handles = []
+    for i, sh in enumerate(shards):
+        y = Yoda(0)
+        y.upload_nodes(sh, node_offset=1000 * i)
+        y.upload_pods(pods)
+        handles.append(y)
+    assert [h.path for h in handles] == ["n32", "f64"]
+    ex = ShardExchange.local(handles, torch.device("cuda:0"), shards, [0, 1000])
+    assert [h.path for h in handles] == ["f64", "f64"]
+    assert_same(ex.run(MODE_SCV), want)
+    for y in handles:
+        y.close()
 
 
 def test_full_size_config3_sampled(dev):
@@ -252,3 +277,35 @@ def test_full_size_config3_sampled(dev):
     assert (got.pick[ok] < nodes.n_nodes).all()
     assert (got.n_ties[ok] >= 1).all() and (got.n_ties[ok] <= got.n_feasible[ok]).all()
     assert (got.n_feasible[got.status == 1] == 0).all()
+
+
+@pytest.mark.parametrize("mode", [MODE_SCV, MODE_DISKIO])
+@pytest.mark.parametrize("path", ["n32", "f64", "u64"])
+def test_score_rows_match_oracle(dev, mode, path):
+    """yoda_score_rows: the Filter bit and raw Score of every node (plugin row mode)."""
+    nodes, pods = synth.make_config(2, pods=24, nodes=900)
+    nodes.total_memory_sum[3] = 0
+    dev.upload_nodes(nodes, force_f64=path == "f64", force_generic=path == "u64")
+    dev.upload_pods(pods)
+    feas, rows = dev.score_rows(mode)
+    for p in range(pods.n_pods):
+        _, f, raw, _ = oracle.pod_detail(nodes, pods, p, mode)
+        np.testing.assert_array_equal(feas[p], f)
+        ok = f & (nodes.total_memory_sum != 0) if mode == MODE_SCV else f
+        np.testing.assert_array_equal(rows[p][ok], raw[ok])
+        assert (rows[p][~f] == -1).all()
+    want = oracle.schedule(nodes, pods, mode, threads=8)
+    assert_same(dev.download(), want, mode)
+
+
+def test_plugin_over_libyoda(dev):
+    from yoda_amd.pack import pods_to_dicts
+    from yoda_amd.plugin import YodaPlugin, schedule_one
+    nodes, pods = synth.make_config(2, pods=30, nodes=700)
+    names = [f"node-{i}" for i in range(nodes.n_nodes)]
+    dev.upload_nodes(nodes)
+    plugin = YodaPlugin(dev, names, nodes)
+    want = oracle.schedule(nodes, pods, MODE_SCV, threads=8)
+    for p, pod in enumerate(pods_to_dicts(pods)):
+        node, st = schedule_one(plugin, pod)
+        assert (node == names[want.pick[p]]) if want.status[p] == 0 else node is None
