@@ -57,6 +57,18 @@ hipError_t launch_reduce3(const Partials& part, uint32_t C, const uint32_t* flag
 hipError_t launch_bitmask_transpose(const uint32_t* in, uint32_t W, uint32_t n_pods,
                                     uint32_t* out, hipStream_t s);
 int kernel_capacity(int K, Path path, int which, int mode_diskio);
+hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
+                          uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
+                          const double* rcp, const float* rcp32, uint32_t n_pods,
+                          const uint32_t* bitmask, const Partials& part, double* tk_s,
+                          uint32_t* tk_i, hipStream_t s);
+hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t C,
+                             uint32_t n_pods, uint32_t node_offset, double* out_s,
+                             uint32_t* out_i, hipStream_t s);
+hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32_t* node,
+                             const uint64_t* value, const uint64_t* card_number, uint32_t count,
+                             hipStream_t s);
+int topk_k();
 }  // namespace yoda
 
 using namespace yoda;
@@ -112,7 +124,7 @@ struct yoda_handle {
   DevBuf nodes;     // fast or generic records
   DevBuf nodes_b;   // Mode B records
   std::vector<unsigned char> host_records;  // kept for alloc updates (greedy)
-  std::vector<uint64_t> h_total_sum, h_free_sum;
+  std::vector<uint64_t> h_total_sum, h_free_sum, h_alloc, h_card_number;
 
   // pods
   bool has_pods = false;
@@ -126,6 +138,9 @@ struct yoda_handle {
   // state
   DevBuf maxima, counts, rcp, rcp32, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
   DevBuf bitmask, bitmask_t, rows, rows_t;
+  // greedy
+  DevBuf tk_s_part, tk_i_part, tk_s, tk_i, upd_node, upd_val, upd_cn;
+  uint32_t greedy_windows = 0, greedy_fallbacks = 0;
   DevBuf p_max_u, p_cnt, p_best_f, p_best_i, p_idx, p_ties, p_low_f, p_low_i, p_err;
   uint32_t C1 = 1, chunk1 = 32;  // K1 node chunking
   uint32_t C2 = 1, chunk2 = 32;  // K2 / K3 node chunking
@@ -158,7 +173,8 @@ struct yoda_handle {
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
                      &n_flagged, &bitmask,   &bitmask_t,  &p_max_u,      &p_cnt,
-                     &rows,      &rows_t,
+                     &rows,      &rows_t,    &tk_s_part,  &tk_i_part,    &tk_s,
+                     &tk_i,      &upd_node,  &upd_val,    &upd_cn,
                      &p_best_f,  &p_best_i,  &p_idx,      &p_ties,       &p_low_f,
                      &p_low_i,   &p_err};
     for (DevBuf* b : all) b->release();
@@ -572,6 +588,9 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     h->host_records.swap(rec);
     h->h_total_sum.assign(nd->total_memory_sum, nd->total_memory_sum + N);
     h->h_free_sum.assign(nd->free_memory_sum, nd->free_memory_sum + N);
+    h->h_card_number.assign(nd->card_number, nd->card_number + N);
+    h->h_alloc.assign(N, 0);
+    if (nd->alloc_memory) h->h_alloc.assign(nd->alloc_memory, nd->alloc_memory + N);
     h->nodes_diskio = diskio;
     h->n_nodes = N;
     h->node_offset = node_offset;
@@ -954,12 +973,300 @@ int yoda_profile_read(yoda_t* h, double* k1_ms, double* k2_ms, uint32_t* n_launc
   return YODA_OK;
 }
 
+namespace {
+
+// Device-side node state for the greedy resolve: the static score (Allocate + Actual) and
+// CardNumber of the nodes picked so far, pushed in small batches (k_set_static).
+struct GreedyState {
+  yoda_t* h;
+  std::vector<uint64_t> alloc, card_number, stat;    // current, per node
+  std::vector<uint64_t> stat_w;                       // static at window start
+  std::vector<uint8_t> touched_w, dirty;
+  std::vector<uint32_t> touched_list, dirty_list;
+
+  uint64_t stat_bits(uint64_t v) const {  // header word: f64 bits on the fast paths
+    if (h->generic) return v;
+    const double d = (double)v;
+    uint64_t b;
+    std::memcpy(&b, &d, 8);
+    return b;
+  }
+  void touch(uint32_t n) {
+    if (!touched_w[n]) {
+      touched_w[n] = 1;
+      stat_w[n] = stat[n];
+      touched_list.push_back(n);
+    }
+    if (!dirty[n]) {
+      dirty[n] = 1;
+      dirty_list.push_back(n);
+    }
+  }
+  int push(std::vector<uint32_t>& list, std::vector<uint8_t>* marks) {
+    if (list.empty()) return YODA_OK;
+    std::vector<uint64_t> val(list.size()), cn(list.size());
+    for (size_t i = 0; i < list.size(); ++i) {
+      val[i] = stat_bits(stat[list[i]]);
+      cn[i] = card_number[list[i]];
+    }
+    const uint32_t cnt = (uint32_t)list.size();
+    HIP_TRY(h, h->upd_node.ensure(cnt * 4ull));
+    HIP_TRY(h, h->upd_val.ensure(cnt * 8ull));
+    HIP_TRY(h, h->upd_cn.ensure(cnt * 8ull));
+    HIP_TRY(h, hipMemcpyAsync(h->upd_node.p, list.data(), cnt * 4ull, hipMemcpyHostToDevice,
+                              h->stream));
+    HIP_TRY(h, hipMemcpyAsync(h->upd_val.p, val.data(), cnt * 8ull, hipMemcpyHostToDevice,
+                              h->stream));
+    HIP_TRY(h, hipMemcpyAsync(h->upd_cn.p, cn.data(), cnt * 8ull, hipMemcpyHostToDevice,
+                              h->stream));
+    const uint32_t stride = h->path == Path::N32 ? n32_stride(h->K) : node_stride(h->K);
+    HIP_TRY(h, launch_set_static(h->nodes.as<unsigned char>(), stride, h->upd_node.as<uint32_t>(),
+                                 h->upd_val.as<uint64_t>(), h->upd_cn.as<uint64_t>(), cnt,
+                                 h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));  // host vectors die at return
+    if (marks)
+      for (uint32_t n : list) (*marks)[n] = 0;
+    list.clear();
+    return YODA_OK;
+  }
+  int push_dirty() { return push(dirty_list, &dirty); }
+};
+
+// A pod SoA holding the pods `idx` of `src` (in that order).
+struct PodGather {
+  std::vector<uint8_t> hn, hm, hc;
+  std::vector<uint64_t> n, m, c;
+  std::vector<int64_t> prio, rcpu;
+  std::vector<double> rio;
+  yoda_pod_soa soa{};
+  void build(const yoda_pod_soa* src, const uint32_t* idx, uint32_t cnt) {
+    hn.resize(cnt), hm.resize(cnt), hc.resize(cnt), n.resize(cnt), m.resize(cnt), c.resize(cnt);
+    prio.assign(cnt, 0), rcpu.assign(cnt, 0), rio.assign(cnt, 0.0);
+    for (uint32_t i = 0; i < cnt; ++i) {
+      const uint32_t p = idx[i];
+      hn[i] = src->has_number[p], n[i] = src->number[p];
+      hm[i] = src->has_memory[p], m[i] = src->memory[p];
+      hc[i] = src->has_clock[p], c[i] = src->clock[p];
+      if (src->priority) prio[i] = src->priority[p];
+      if (src->rio) rio[i] = src->rio[p];
+      if (src->rcpu) rcpu[i] = src->rcpu[p];
+    }
+    soa.n_pods = cnt;
+    soa.has_number = hn.data(), soa.number = n.data();
+    soa.has_memory = hm.data(), soa.memory = m.data();
+    soa.has_clock = hc.data(), soa.clock = c.data();
+    soa.priority = prio.data();
+    soa.rio = src->rio ? rio.data() : nullptr;
+    soa.rcpu = src->rcpu ? rcpu.data() : nullptr;
+  }
+};
+
+// Exact evaluation of ONE pod against the current device state (pushes pending updates).
+int greedy_eval_one(GreedyState& g, const yoda_pod_soa* pods, uint32_t p, int mode,
+                    int32_t* pick_out) {
+  yoda_t* h = g.h;
+  int rc = g.push_dirty();
+  if (rc) return rc;
+  PodGather one;
+  one.build(pods, &p, 1);
+  if ((rc = yoda_upload_pods(h, &one.soa))) return rc;
+  if ((rc = yoda_run(h, mode, 0))) return rc;
+  HIP_TRY(h, hipMemcpyAsync(pick_out, h->pick.p, 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return YODA_OK;
+}
+
+}  // namespace
+
 int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, int32_t* pick) {
-  (void)pods;
-  (void)mode;
-  (void)flags;
-  (void)pick;
-  return fail(h, YODA_ERR_STATE, "yoda_greedy: not implemented yet");
+  if (!h) return YODA_ERR_INVALID_ARG;
+  if (!pods || !pick) return fail(h, YODA_ERR_INVALID_ARG, "NULL pods or pick");
+  if (!h->has_nodes) return fail(h, YODA_ERR_NO_NODES, "no node snapshot uploaded");
+  try {
+    HIP_TRY(h, hipSetDevice(h->device));
+    const uint32_t P = pods->n_pods, N = h->n_nodes;
+    h->greedy_windows = 0;
+    h->greedy_fallbacks = 0;
+    if (P == 0) return YODA_OK;
+    int rc;
+    // Queue order: sort.Less (sort.go:8-10) -- scv/priority descending, then input index.
+    std::vector<uint32_t> order(P);
+    for (uint32_t i = 0; i < P; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+      const int64_t pa = pods->priority ? pods->priority[a] : 0;
+      const int64_t pb = pods->priority ? pods->priority[b] : 0;
+      return pa > pb;
+    });
+    if (mode == YODA_MODE_DISKIO) {  // Mode B reads no assumed-pod state: independent cycles
+      PodGather all;
+      all.build(pods, order.data(), P);
+      if ((rc = yoda_upload_pods(h, &all.soa)) || (rc = yoda_run(h, mode, 0))) return rc;
+      std::vector<int32_t> pk(P);
+      HIP_TRY(h, hipMemcpy(pk.data(), h->pick.p, P * 4ull, hipMemcpyDeviceToHost));
+      for (uint32_t i = 0; i < P; ++i) pick[order[i]] = pk[i];
+      return YODA_OK;
+    }
+    GreedyState g;
+    g.h = h;
+    g.alloc = h->h_alloc;
+    g.card_number = h->h_card_number;
+    g.stat.resize(N);
+    g.stat_w.resize(N);
+    g.touched_w.assign(N, 0);
+    g.dirty.assign(N, 0);
+    for (uint32_t n = 0; n < N; ++n) {
+      bool z;
+      g.stat[n] = static_score(h->h_free_sum[n], h->h_total_sum[n], g.alloc[n], &z);
+    }
+    const std::vector<uint64_t> stat0 = g.stat;
+    std::vector<uint32_t> all_touched;
+    std::vector<uint8_t> ever(N, 0);
+    auto apply_pick = [&](uint32_t p, int32_t node) {
+      if (node < 0) return;
+      const uint32_t n = (uint32_t)node - h->node_offset;
+      if (pods->has_memory[p]) g.alloc[n] += pods->memory[p];  // uint64 wrap (algorithm.go:301)
+      if (flags & YODA_GREEDY_CARD_CAPACITY) {
+        const uint64_t num = pods->has_number[p] ? pods->number[p] : 1;
+        g.card_number[n] = g.card_number[n] >= num ? g.card_number[n] - num : 0;
+      }
+      bool z;
+      g.stat[n] = static_score(h->h_free_sum[n], h->h_total_sum[n], g.alloc[n], &z);
+      g.touch(n);
+      if (!ever[n]) {
+        ever[n] = 1;
+        all_touched.push_back(n);
+      }
+    };
+    const bool exact_seq = (flags & YODA_GREEDY_CARD_CAPACITY) || h->generic;
+    if (exact_seq) {
+      // Feasibility (CardNumber) or the U64 normalize check can change after every pick:
+      // evaluate each pod exactly against the current state.
+      for (uint32_t i = 0; i < P; ++i) {
+        const uint32_t p = order[i];
+        int32_t pk = -1;
+        if ((rc = greedy_eval_one(g, pods, p, mode, &pk))) return rc;
+        pick[p] = pk;
+        apply_pick(p, pk);
+        ++h->greedy_fallbacks;
+      }
+    } else {
+      // Windowed top-k + certified sequential resolve (greedy).  Within a
+      // window only the Allocate term of picked nodes changes, and it never increases
+      // (unless alloc wraps around 2^64: then the rest of the window is evaluated exactly).
+      const uint32_t KT = (uint32_t)topk_k();
+      const uint32_t W = std::min<uint32_t>(P, 1u << 16);
+      PodGather win;
+      std::vector<uint32_t> counts(2 * (size_t)W);
+      std::vector<double> ts((size_t)KT * W);
+      std::vector<uint32_t> ti((size_t)KT * W);
+      for (uint32_t ws = 0; ws < P; ws += W) {
+        const uint32_t wn = std::min(W, P - ws);
+        if ((rc = g.push_dirty())) return rc;
+        for (uint32_t n : g.touched_list) g.touched_w[n] = 0;
+        g.touched_list.clear();
+        win.build(pods, order.data() + ws, wn);
+        if ((rc = yoda_upload_pods(h, &win.soa))) return rc;
+        if ((rc = prepare_run(h, YODA_MODE_SCV))) return rc;
+        const size_t CPk = (size_t)h->C2 * KT * wn;
+        HIP_TRY(h, h->tk_s_part.ensure(CPk * 8));
+        HIP_TRY(h, h->tk_i_part.ensure(CPk * 4));
+        HIP_TRY(h, h->tk_s.ensure((size_t)KT * wn * 8));
+        HIP_TRY(h, h->tk_i.ensure((size_t)KT * wn * 4));
+        if (N > 0) {
+          if ((rc = phase1(h, YODA_MODE_SCV, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>())))
+            return rc;
+          HIP_TRY(h, launch_prep2(h->maxima.as<uint64_t>(), wn, h->rcp.as<double>(),
+                                  h->rcp32.as<float>(), h->stream));
+          HIP_TRY(h, launch_k2_topk(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk2,
+                                    h->C2, pod_params(h), h->rcp.as<double>(),
+                                    h->rcp32.as<float>(), wn, h->bitmask.as<uint32_t>(),
+                                    partials(h), h->tk_s_part.as<double>(),
+                                    h->tk_i_part.as<uint32_t>(), h->stream));
+          HIP_TRY(h, launch_topk_merge(h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),
+                                       h->C2, wn, h->node_offset, h->tk_s.as<double>(),
+                                       h->tk_i.as<uint32_t>(), h->stream));
+          HIP_TRY(h, hipMemcpyAsync(counts.data(), h->counts.p, 2ull * wn * 4,
+                                    hipMemcpyDeviceToHost, h->stream));
+          HIP_TRY(h, hipMemcpyAsync(ts.data(), h->tk_s.p, (size_t)KT * wn * 8,
+                                    hipMemcpyDeviceToHost, h->stream));
+          HIP_TRY(h, hipMemcpyAsync(ti.data(), h->tk_i.p, (size_t)KT * wn * 4,
+                                    hipMemcpyDeviceToHost, h->stream));
+          HIP_TRY(h, hipStreamSynchronize(h->stream));
+        } else {
+          std::fill(counts.begin(), counts.end(), 0u);
+        }
+        ++h->greedy_windows;
+        bool wrapped = false;
+        for (uint32_t i = 0; i < wn; ++i) {
+          const uint32_t p = order[ws + i];
+          const uint32_t nf = counts[i], nz = counts[(size_t)wn + i];
+          int32_t pk;
+          if (nf == 0) {
+            pk = YODA_PICK_NONE;
+          } else if (nf >= 2 && nz > 0) {
+            pk = YODA_PICK_ERROR;  // Score would divide by TotalMemorySum == 0
+          } else if (nf == 1) {
+            pk = (int32_t)ti[i];   // the only feasible node, returned without scoring
+          } else if (wrapped) {
+            if ((rc = greedy_eval_one(g, pods, p, YODA_MODE_SCV, &pk))) return rc;
+            ++h->greedy_fallbacks;
+          } else {
+            // current score of each candidate: window-start score - old static + new static
+            const uint32_t len = std::min<uint32_t>(nf, KT);
+            double bs = -1.0;
+            uint32_t bi = 0xffffffffu;
+            for (uint32_t k = 0; k < len; ++k) {
+              const uint32_t node = ti[(size_t)k * wn + i];
+              const uint32_t n = node - h->node_offset;
+              double cur = ts[(size_t)k * wn + i];
+              if (g.touched_w[n]) cur = cur - (double)g.stat_w[n] + (double)g.stat[n];
+              if (cur > bs || (cur == bs && node < bi)) {
+                bs = cur;
+                bi = node;
+              }
+            }
+            // every node outside the list scored <= T at window start (ties: higher index)
+            // and its score can only have dropped since
+            const double T = ts[(size_t)(len - 1) * wn + i];
+            const uint32_t tidx = ti[(size_t)(len - 1) * wn + i];
+            const bool certified = nf <= KT || bs > T || (bs == T && bi <= tidx);
+            if (certified) {
+              pk = (int32_t)bi;
+            } else {
+              if ((rc = greedy_eval_one(g, pods, p, YODA_MODE_SCV, &pk))) return rc;
+              ++h->greedy_fallbacks;
+            }
+          }
+          pick[p] = pk;
+          if (pk >= 0) {
+            const uint32_t n = (uint32_t)pk - h->node_offset;
+            const uint64_t before = g.alloc[n];
+            apply_pick(p, pk);
+            if (g.alloc[n] < before) wrapped = true;  // Allocate may grow: stop certifying
+          }
+        }
+      }
+    }
+    // Leave the uploaded snapshot unchanged: restore static score and CardNumber.
+    for (uint32_t n : all_touched) {
+      g.stat[n] = stat0[n];
+      g.card_number[n] = h->h_card_number[n];
+    }
+    if ((rc = g.push(all_touched, nullptr))) return rc;
+    h->ran = false;
+    return YODA_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(h, YODA_ERR_INVALID_ARG, "host allocation failed");
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
+int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  if (windows) *windows = h->greedy_windows;
+  if (fallbacks) *fallbacks = h->greedy_fallbacks;
+  return YODA_OK;
 }
 
 }  // extern "C"

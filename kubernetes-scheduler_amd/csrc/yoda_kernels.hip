@@ -207,150 +207,243 @@ __global__ __launch_bounds__(kBlock) void k_prep2(const uint64_t* __restrict__ m
 }
 
 // ---------------------------------------------------------------------------------------
-// K2 (F64 path): CalculateBasicScore + Allocate + Actual in exact f64, running argmax with
-// lowest-index ties, tie count and min over the feasible nodes of the chunk.
-// ROWS: also write every feasible pair's raw score to rows[n][p] (plugin row mode).
-template <int K, bool ROWS>
-__global__ __launch_bounds__(kBlock) void k2_score_fast(
-    const unsigned char* __restrict__ nodes, uint32_t n_nodes, uint32_t chunk_nodes,
-    const double* __restrict__ m_f, const double* __restrict__ c_f,
-    const double* __restrict__ rcp, uint32_t n_pods, const uint32_t* __restrict__ bitmask,
-    double* __restrict__ pbest, uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties,
-    double* __restrict__ plow, int64_t* __restrict__ rows) {
-  using R = Rec<Path::F64>;
-  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t chunk = blockIdx.y;
-  const uint32_t n0 = chunk * chunk_nodes;
-  const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
-  const bool live = p < n_pods;
-  double m = 0, c = 0, r_bw = 0, r_core = 0, r_pow = 0, r_free = 0, r_tot = 0;
-  if (live) {
-    m = m_f[p];
-    c = c_f[p];
-    r_bw = rcp[0 * (size_t)n_pods + p];
-    r_core = rcp[1 * (size_t)n_pods + p];
-    r_pow = rcp[2 * (size_t)n_pods + p];
-    r_free = rcp[3 * (size_t)n_pods + p];
-    r_tot = rcp[4 * (size_t)n_pods + p];
-  }
-  double best = -1.0, low = 1.0e300;
-  uint32_t idx = 0xffffffffu, ties = 0, word = 0;
-  for (uint32_t n = n0; n < n1; ++n) {
-    if ((n & 31u) == 0u) word = live ? bitmask[(size_t)(n >> 5) * n_pods + p] : 0u;
-    const bool feas = (word >> (n & 31u)) & 1u;
-    if (feas) {
-      const unsigned char* rec = nodes + (size_t)n * R::stride(K);
-      const double stat = reinterpret_cast<const NodeHdrF*>(rec)->static_score;
-      const Group<double, K> fr = load_group<double, K>(rec + R::off(kFree, K));
-      const Group<double, K> ck = load_group<double, K>(rec + R::off(kClock, K));
-      const Group<double, K> bw = load_group<double, K>(rec + R::off(kBandwidth, K));
-      const Group<double, K> co = load_group<double, K>(rec + R::off(kCore, K));
-      const Group<double, K> pw = load_group<double, K>(rec + R::off(kPower, K));
-      const Group<double, K> to = load_group<double, K>(rec + R::off(kTotal, K));
-      double basic = 0.0;
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        // CalculateCardScore (algorithm.go:280-291): each quotient truncates before its
-        // weight; clock is divided by MaxBandwidth (:283).  Every term is an exact integer
-        // < 2^52, so the sum is exact in any order and the weights fold into FMAs.
-        double s = __builtin_trunc(bw.v[j] * r_bw);
-        s += __builtin_trunc(ck.v[j] * r_bw);
-        s = __builtin_fma(__builtin_trunc(co.v[j] * r_core), 2.0, s);
-        s += __builtin_trunc(pw.v[j] * r_pow);
-        s = __builtin_fma(__builtin_trunc(fr.v[j] * r_free), 3.0, s);
-        s += __builtin_trunc(to.v[j] * r_tot);
-        basic += ((fr.v[j] >= m) & (ck.v[j] >= c)) ? s : 0.0;  // algorithm.go:271
-      }
-      const double raw = basic + stat;  // algorithm.go:96
-      if constexpr (ROWS) rows[(size_t)n * n_pods + p] = (int64_t)raw;
-      if (raw > best) {
-        best = raw;
-        idx = n;
-        ties = 1;
-      } else if (raw == best) {
-        ++ties;
-      }
-      low = fmin(low, raw);
-    }
-  }
-  if (!live) return;
-  const size_t o = (size_t)chunk * n_pods + p;
-  pbest[o] = best;
-  pidx[o] = idx;
-  pties[o] = ties;
-  plow[o] = low;
-}
+// K2 on the fast paths: CalculateBasicScore + Allocate + Actual (algorithm.go:96,264-310),
+// exact.  A Scorer holds one pod's thresholds and reciprocals in VGPRs and
+// scores one node record (read through the scalar path).
+struct ScoreArgs {
+  const double* m_f;
+  const double* c_f;
+  const uint32_t* m_32;
+  const uint32_t* c_32;
+  const double* rcp;    // [5][P] f64: bw, core, power, free, total
+  const float* rcp32;   // [3][P] f32: bw, core, power
+};
 
-// K2 (N32 path): same score; the four small-field quotients in f32 (exact under the N32
-// bounds), the two memory quotients in f64, the card score summed in u32 (< 2^27).
-template <int K, bool ROWS>
-__global__ __launch_bounds__(kBlock) void k2_score_n32(
-    const unsigned char* __restrict__ nodes, uint32_t n_nodes, uint32_t chunk_nodes,
-    const uint32_t* __restrict__ m_32, const uint32_t* __restrict__ c_32,
-    const double* __restrict__ rcp, const float* __restrict__ rcp32, uint32_t n_pods,
-    const uint32_t* __restrict__ bitmask, double* __restrict__ pbest,
-    uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties, double* __restrict__ plow,
-    int64_t* __restrict__ rows) {
-  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t chunk = blockIdx.y;
-  const uint32_t n0 = chunk * chunk_nodes;
-  const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
-  const bool live = p < n_pods;
+template <Path P>
+struct Scorer;
+
+// F64: every quotient in f64; each term is an exact integer < 2^52, so the sum is exact in
+// any order and the weights fold into FMAs.
+template <>
+struct Scorer<Path::F64> {
+  using R = Rec<Path::F64>;
+  double m = 0, c = 0, r_bw = 0, r_core = 0, r_pow = 0, r_free = 0, r_tot = 0;
+  __device__ void load(const ScoreArgs& a, uint32_t p, uint32_t n_pods) {
+    m = a.m_f[p];
+    c = a.c_f[p];
+    r_bw = a.rcp[0 * (size_t)n_pods + p];
+    r_core = a.rcp[1 * (size_t)n_pods + p];
+    r_pow = a.rcp[2 * (size_t)n_pods + p];
+    r_free = a.rcp[3 * (size_t)n_pods + p];
+    r_tot = a.rcp[4 * (size_t)n_pods + p];
+  }
+  template <int K>
+  __device__ __forceinline__ double raw(const unsigned char* rec) const {
+    const double stat = reinterpret_cast<const NodeHdrF*>(rec)->static_score;
+    const Group<double, K> fr = load_group<double, K>(rec + R::off(kFree, K));
+    const Group<double, K> ck = load_group<double, K>(rec + R::off(kClock, K));
+    const Group<double, K> bw = load_group<double, K>(rec + R::off(kBandwidth, K));
+    const Group<double, K> co = load_group<double, K>(rec + R::off(kCore, K));
+    const Group<double, K> pw = load_group<double, K>(rec + R::off(kPower, K));
+    const Group<double, K> to = load_group<double, K>(rec + R::off(kTotal, K));
+    double basic = 0.0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      // CalculateCardScore (algorithm.go:280-291): each quotient truncates before its
+      // weight; clock is divided by MaxBandwidth (:283).
+      double sc = __builtin_trunc(bw.v[j] * r_bw);
+      sc += __builtin_trunc(ck.v[j] * r_bw);
+      sc = __builtin_fma(__builtin_trunc(co.v[j] * r_core), 2.0, sc);
+      sc += __builtin_trunc(pw.v[j] * r_pow);
+      sc = __builtin_fma(__builtin_trunc(fr.v[j] * r_free), 3.0, sc);
+      sc += __builtin_trunc(to.v[j] * r_tot);
+      basic += ((fr.v[j] >= m) & (ck.v[j] >= c)) ? sc : 0.0;  // algorithm.go:271
+    }
+    return basic + stat;
+  }
+};
+
+// N32: the four small-field quotients in f32 (exact under the N32 bounds), the two memory
+// quotients in f64, the card score summed in u32 (< 2^27).
+template <>
+struct Scorer<Path::N32> {
   uint32_t m = 0, c = 0;
   float r_bw = 0, r_core = 0, r_pow = 0;
   double r_free = 0, r_tot = 0;
-  if (live) {
-    m = m_32[p];
-    c = c_32[p];
-    r_bw = rcp32[0 * (size_t)n_pods + p];
-    r_core = rcp32[1 * (size_t)n_pods + p];
-    r_pow = rcp32[2 * (size_t)n_pods + p];
-    r_free = rcp[3 * (size_t)n_pods + p];
-    r_tot = rcp[4 * (size_t)n_pods + p];
+  __device__ void load(const ScoreArgs& a, uint32_t p, uint32_t n_pods) {
+    m = a.m_32[p];
+    c = a.c_32[p];
+    r_bw = a.rcp32[0 * (size_t)n_pods + p];
+    r_core = a.rcp32[1 * (size_t)n_pods + p];
+    r_pow = a.rcp32[2 * (size_t)n_pods + p];
+    r_free = a.rcp[3 * (size_t)n_pods + p];
+    r_tot = a.rcp[4 * (size_t)n_pods + p];
   }
+  template <int K>
+  __device__ __forceinline__ double raw(const unsigned char* rec) const {
+    const double stat = reinterpret_cast<const NodeHdrF*>(rec)->static_score;
+    const Group<uint32_t, K> fr = load_group<uint32_t, K>(rec + n32_u32_off(kFree, K));
+    const Group<uint32_t, K> ck = load_group<uint32_t, K>(rec + n32_u32_off(kClock, K));
+    const Group<float, K> bwf = load_group<float, K>(rec + n32_f32_off(kF32Bandwidth, K));
+    const Group<float, K> ckf = load_group<float, K>(rec + n32_f32_off(kF32Clock, K));
+    const Group<float, K> cof = load_group<float, K>(rec + n32_f32_off(kF32Core, K));
+    const Group<float, K> pwf = load_group<float, K>(rec + n32_f32_off(kF32Power, K));
+    const Group<double, K> frd = load_group<double, K>(rec + n32_f64_off(kF64Free, K));
+    const Group<double, K> tod = load_group<double, K>(rec + n32_f64_off(kF64Total, K));
+    uint32_t basic = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      // CalculateCardScore (algorithm.go:280-291); clock / MaxBandwidth (:283)
+      uint32_t sc = (uint32_t)(bwf.v[j] * r_bw) + (uint32_t)(ckf.v[j] * r_bw) +
+                    (uint32_t)(pwf.v[j] * r_pow) + (uint32_t)(tod.v[j] * r_tot);
+      sc += 2u * (uint32_t)(cof.v[j] * r_core) + 3u * (uint32_t)(frd.v[j] * r_free);
+      basic += ((fr.v[j] >= m) & (ck.v[j] >= c)) ? sc : 0u;  // algorithm.go:271
+    }
+    return (double)basic + stat;  // algorithm.go:96
+  }
+};
+
+__device__ __forceinline__ uint32_t rec_stride(Path p, int K) {
+  return p == Path::N32 ? n32_stride(K) : node_stride(K);
+}
+
+// Output flavours of the fast K2: running argmax (OUT_ARGMAX), argmax + every feasible raw
+// score to rows[n][p] (OUT_ROWS, the plugin row mode), or the TOPK best (score, node) per pod
+// sorted by (score desc, node asc) into tk_s/tk_i [C][TOPK][P] (greedy candidates).
+enum K2Out { OUT_ARGMAX = 0, OUT_ROWS = 1, OUT_TOPK = 2 };
+constexpr int kTopK = 8;
+
+template <int K, Path PATH, int OUT>
+__global__ __launch_bounds__(kBlock) void k2_score(
+    const unsigned char* __restrict__ nodes, uint32_t n_nodes, uint32_t chunk_nodes,
+    ScoreArgs args, uint32_t n_pods, const uint32_t* __restrict__ bitmask,
+    double* __restrict__ pbest, uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties,
+    double* __restrict__ plow, int64_t* __restrict__ rows, double* __restrict__ tk_s,
+    uint32_t* __restrict__ tk_i) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t chunk = blockIdx.y;
+  const uint32_t n0 = chunk * chunk_nodes;
+  const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
+  const bool live = p < n_pods;
+  Scorer<PATH> sc;
+  if (live) sc.load(args, p, n_pods);
+  constexpr uint32_t stride = PATH == Path::N32 ? n32_stride(K) : node_stride(K);
   double best = -1.0, low = 1.0e300;
   uint32_t idx = 0xffffffffu, ties = 0, word = 0;
+  double ts[OUT == OUT_TOPK ? kTopK : 1];
+  uint32_t ti[OUT == OUT_TOPK ? kTopK : 1];
+  if constexpr (OUT == OUT_TOPK) {
+#pragma unroll
+    for (int k = 0; k < kTopK; ++k) {
+      ts[k] = -1.0;
+      ti[k] = 0xffffffffu;
+    }
+  }
   for (uint32_t n = n0; n < n1; ++n) {
     if ((n & 31u) == 0u) word = live ? bitmask[(size_t)(n >> 5) * n_pods + p] : 0u;
     const bool feas = (word >> (n & 31u)) & 1u;
     if (feas) {
-      const unsigned char* rec = nodes + (size_t)n * n32_stride(K);
-      const double stat = reinterpret_cast<const NodeHdrF*>(rec)->static_score;
-      const Group<uint32_t, K> fr = load_group<uint32_t, K>(rec + n32_u32_off(kFree, K));
-      const Group<uint32_t, K> ck = load_group<uint32_t, K>(rec + n32_u32_off(kClock, K));
-      const Group<float, K> bwf = load_group<float, K>(rec + n32_f32_off(kF32Bandwidth, K));
-      const Group<float, K> ckf = load_group<float, K>(rec + n32_f32_off(kF32Clock, K));
-      const Group<float, K> cof = load_group<float, K>(rec + n32_f32_off(kF32Core, K));
-      const Group<float, K> pwf = load_group<float, K>(rec + n32_f32_off(kF32Power, K));
-      const Group<double, K> frd = load_group<double, K>(rec + n32_f64_off(kF64Free, K));
-      const Group<double, K> tod = load_group<double, K>(rec + n32_f64_off(kF64Total, K));
-      uint32_t basic = 0;
+      const double raw = sc.template raw<K>(nodes + (size_t)n * stride);
+      if constexpr (OUT == OUT_ROWS) rows[(size_t)n * n_pods + p] = (int64_t)raw;
+      if constexpr (OUT == OUT_TOPK) {
+        // strict '>' keeps the earlier (lower) node first among equal scores
+        if (raw > ts[kTopK - 1]) {
+          double cs = raw;
+          uint32_t ci = n;
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
-        // CalculateCardScore (algorithm.go:280-291); clock / MaxBandwidth (:283)
-        uint32_t s = (uint32_t)(bwf.v[j] * r_bw) + (uint32_t)(ckf.v[j] * r_bw) +
-                     (uint32_t)(pwf.v[j] * r_pow) + (uint32_t)(tod.v[j] * r_tot);
-        s += 2u * (uint32_t)(cof.v[j] * r_core) + 3u * (uint32_t)(frd.v[j] * r_free);
-        basic += ((fr.v[j] >= m) & (ck.v[j] >= c)) ? s : 0u;  // algorithm.go:271
+          for (int k = 0; k < kTopK; ++k) {
+            const bool gt = cs > ts[k];
+            const double os = ts[k];
+            const uint32_t oi = ti[k];
+            ts[k] = gt ? cs : os;
+            ti[k] = gt ? ci : oi;
+            cs = gt ? os : cs;
+            ci = gt ? oi : ci;
+          }
+        }
+      } else {
+        if (raw > best) {
+          best = raw;
+          idx = n;
+          ties = 1;
+        } else if (raw == best) {
+          ++ties;
+        }
+        low = fmin(low, raw);
       }
-      const double raw = (double)basic + stat;  // algorithm.go:96
-      if constexpr (ROWS) rows[(size_t)n * n_pods + p] = (int64_t)raw;
-      if (raw > best) {
-        best = raw;
-        idx = n;
-        ties = 1;
-      } else if (raw == best) {
-        ++ties;
-      }
-      low = fmin(low, raw);
     }
   }
   if (!live) return;
-  const size_t o = (size_t)chunk * n_pods + p;
-  pbest[o] = best;
-  pidx[o] = idx;
-  pties[o] = ties;
-  plow[o] = low;
+  if constexpr (OUT == OUT_TOPK) {
+#pragma unroll
+    for (int k = 0; k < kTopK; ++k) {
+      const size_t o = ((size_t)chunk * kTopK + k) * n_pods + p;
+      tk_s[o] = ts[k];
+      tk_i[o] = ti[k];
+    }
+  } else {
+    const size_t o = (size_t)chunk * n_pods + p;
+    pbest[o] = best;
+    pidx[o] = idx;
+    pties[o] = ties;
+    plow[o] = low;
+  }
+}
+
+// Merge the per-chunk top-k lists of each pod (chunks in node order, so the strict '>'
+// insertion keeps lower node indices first among equal scores) -> [TOPK][P], global ids.
+__global__ __launch_bounds__(kBlock) void k_topk_merge(const double* __restrict__ tk_s,
+                                                       const uint32_t* __restrict__ tk_i,
+                                                       uint32_t C, uint32_t n_pods,
+                                                       uint32_t node_offset,
+                                                       double* __restrict__ out_s,
+                                                       uint32_t* __restrict__ out_i) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= n_pods) return;
+  double ts[kTopK];
+  uint32_t ti[kTopK];
+#pragma unroll
+  for (int k = 0; k < kTopK; ++k) {
+    ts[k] = -1.0;
+    ti[k] = 0xffffffffu;
+  }
+  for (uint32_t c = 0; c < C; ++c) {
+    for (int e = 0; e < kTopK; ++e) {
+      const size_t o = ((size_t)c * kTopK + e) * n_pods + p;
+      double cs = tk_s[o];
+      uint32_t ci = tk_i[o];
+      if (!(cs > ts[kTopK - 1])) break;  // lists are sorted: the rest cannot enter
+#pragma unroll
+      for (int k = 0; k < kTopK; ++k) {
+        const bool gt = cs > ts[k];
+        const double os = ts[k];
+        const uint32_t oi = ti[k];
+        ts[k] = gt ? cs : os;
+        ti[k] = gt ? ci : oi;
+        cs = gt ? os : cs;
+        ci = gt ? oi : ci;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kTopK; ++k) {
+    out_s[(size_t)k * n_pods + p] = ts[k];
+    out_i[(size_t)k * n_pods + p] = ti[k] == 0xffffffffu ? ti[k] : ti[k] + node_offset;
+  }
+}
+
+// Greedy: overwrite the static score (record header offset 0) of a few nodes.
+__global__ __launch_bounds__(kBlock) void k_set_static(unsigned char* __restrict__ nodes,
+                                                       uint32_t stride,
+                                                       const uint32_t* __restrict__ node,
+                                                       const uint64_t* __restrict__ value,
+                                                       const uint64_t* __restrict__ card_number,
+                                                       uint32_t count) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= count) return;
+  uint64_t* hdr = reinterpret_cast<uint64_t*>(nodes + (size_t)node[t] * stride);
+  hdr[0] = value[t];        // static_score bits (f64 on the fast paths, u64 on U64)
+  hdr[1] = card_number[t];  // CardNumber
 }
 
 // ---------------------------------------------------------------------------------------
@@ -755,8 +848,8 @@ int kernel_capacity(int K, Path path, int which, int mode_diskio) {
     }
   } else {
     switch (path) {
-      case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k2_score_n32<KK, false>))); break;
-      case Path::F64: YODA_K_SWITCH(K, YODA_FN((&k2_score_fast<KK, false>))); break;
+      case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k2_score<KK, Path::N32, OUT_ARGMAX>))); break;
+      case Path::F64: YODA_K_SWITCH(K, YODA_FN((&k2_score<KK, Path::F64, OUT_ARGMAX>))); break;
       case Path::U64: YODA_K_SWITCH(K, YODA_FN((&k2_score_generic<KK, false>))); break;
     }
   }
@@ -778,35 +871,65 @@ hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, fl
   return hipGetLastError();
 }
 
-template <bool ROWS>
+template <int OUT>
 static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                               uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                               const uint64_t* maxima, const double* rcp, const float* rcp32,
                               uint32_t n_pods, const uint32_t* bitmask, const Partials& part,
-                              int64_t* rows, hipStream_t s) {
+                              int64_t* rows, double* tk_s, uint32_t* tk_i, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
+  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
   switch (path) {
     case Path::N32:
-      YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_n32<KK, ROWS>), grid, dim3(kBlock), 0, s,
-                                          nodes, n_nodes, chunk_nodes, pp.m_32, pp.c_32, rcp,
-                                          rcp32, n_pods, bitmask, part.best_f, part.idx,
-                                          part.ties, part.low_f, rows));
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score<KK, Path::N32, OUT>), grid, dim3(kBlock), 0,
+                                          s, nodes, n_nodes, chunk_nodes, a, n_pods, bitmask,
+                                          part.best_f, part.idx, part.ties, part.low_f, rows,
+                                          tk_s, tk_i));
       break;
     case Path::F64:
-      YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_fast<KK, ROWS>), grid, dim3(kBlock), 0, s,
-                                          nodes, n_nodes, chunk_nodes, pp.m_f, pp.c_f, rcp,
-                                          n_pods, bitmask, part.best_f, part.idx, part.ties,
-                                          part.low_f, rows));
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score<KK, Path::F64, OUT>), grid, dim3(kBlock), 0,
+                                          s, nodes, n_nodes, chunk_nodes, a, n_pods, bitmask,
+                                          part.best_f, part.idx, part.ties, part.low_f, rows,
+                                          tk_s, tk_i));
       break;
     case Path::U64:
-      YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_generic<KK, ROWS>), grid, dim3(kBlock), 0,
-                                          s, nodes, n_nodes, chunk_nodes, pp.m_u, pp.c_u, maxima,
-                                          n_pods, bitmask, part.best_i, part.idx, part.ties,
-                                          part.low_i, rows));
+      if (OUT == OUT_TOPK) return hipErrorInvalidValue;
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_generic<KK, OUT == OUT_ROWS>), grid,
+                                          dim3(kBlock), 0, s, nodes, n_nodes, chunk_nodes,
+                                          pp.m_u, pp.c_u, maxima, n_pods, bitmask, part.best_i,
+                                          part.idx, part.ties, part.low_i, rows));
       break;
   }
   return hipGetLastError();
 }
+
+hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
+                          uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
+                          const double* rcp, const float* rcp32, uint32_t n_pods,
+                          const uint32_t* bitmask, const Partials& part, double* tk_s,
+                          uint32_t* tk_i, hipStream_t s) {
+  return launch_k2_t<OUT_TOPK>(K, path, nodes, n_nodes, chunk_nodes, C, pp, nullptr, rcp, rcp32,
+                               n_pods, bitmask, part, nullptr, tk_s, tk_i, s);
+}
+
+hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t C,
+                             uint32_t n_pods, uint32_t node_offset, double* out_s,
+                             uint32_t* out_i, hipStream_t s) {
+  hipLaunchKernelGGL(k_topk_merge, pod_grid(n_pods), dim3(kBlock), 0, s, tk_s, tk_i, C, n_pods,
+                     node_offset, out_s, out_i);
+  return hipGetLastError();
+}
+
+hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32_t* node,
+                             const uint64_t* value, const uint64_t* card_number, uint32_t count,
+                             hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_set_static, pod_grid(count), dim3(kBlock), 0, s, nodes, stride, node,
+                     value, card_number, count);
+  return hipGetLastError();
+}
+
+int topk_k() { return kTopK; }
 
 hipError_t launch_k2(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
@@ -814,10 +937,10 @@ hipError_t launch_k2(int K, Path path, const unsigned char* nodes, uint32_t n_no
                      const uint32_t* bitmask, const Partials& part, int64_t* rows,
                      hipStream_t s) {
   if (rows)
-    return launch_k2_t<true>(K, path, nodes, n_nodes, chunk_nodes, C, pp, maxima, rcp, rcp32,
-                             n_pods, bitmask, part, rows, s);
-  return launch_k2_t<false>(K, path, nodes, n_nodes, chunk_nodes, C, pp, maxima, rcp, rcp32,
-                            n_pods, bitmask, part, rows, s);
+    return launch_k2_t<OUT_ROWS>(K, path, nodes, n_nodes, chunk_nodes, C, pp, maxima, rcp,
+                                 rcp32, n_pods, bitmask, part, rows, nullptr, nullptr, s);
+  return launch_k2_t<OUT_ARGMAX>(K, path, nodes, n_nodes, chunk_nodes, C, pp, maxima, rcp,
+                                 rcp32, n_pods, bitmask, part, rows, nullptr, nullptr, s);
 }
 
 hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,

@@ -55,6 +55,7 @@ _SIGS = {
     "yoda_profile_read": ([_vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                            C.POINTER(C.c_uint32)], C.c_int),
     "yoda_greedy": ([_vp, C.POINTER(CPodSoA), C.c_int, _u32, C.POINTER(C.c_int32)], C.c_int),
+    "yoda_greedy_stats": ([_vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)], C.c_int),
 }
 
 
@@ -215,6 +216,12 @@ class Yoda:
         self._check(lib().yoda_greedy(self._h, C.byref(cp), mode, flags,
                                       pick.ctypes.data_as(C.POINTER(C.c_int32))), "yoda_greedy")
         return pick
+
+    def greedy_stats(self):
+        """(top-k windows, pods evaluated one by one) of the last greedy()."""
+        w, f = C.c_uint32(), C.c_uint32()
+        self._check(lib().yoda_greedy_stats(self._h, C.byref(w), C.byref(f)), "yoda_greedy_stats")
+        return w.value, f.value
 
     def profile(self, enable: bool = True):
         self._check(lib().yoda_profile(self._h, 1 if enable else 0), "yoda_profile")

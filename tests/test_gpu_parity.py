@@ -309,3 +309,31 @@ def test_plugin_over_libyoda(dev):
     for p, pod in enumerate(pods_to_dicts(pods)):
         node, st = schedule_one(plugin, pod)
         assert (node == names[want.pick[p]]) if want.status[p] == 0 else node is None
+
+
+@pytest.mark.parametrize("flags", [0, 1])
+@pytest.mark.parametrize("path", ["n32", "f64", "u64"])
+def test_greedy_matches_sequential_oracle(dev, flags, path):
+    """Batched greedy (config 5 semantics, scaled down) == the sequential oracle."""
+    nodes, pods = synth.make_config(5, pods=2500, nodes=600)
+    dev.upload_nodes(nodes, force_f64=path == "f64", force_generic=path == "u64")
+    got = dev.greedy(pods, MODE_SCV, flags)
+    want, _ = oracle.greedy(nodes, pods, MODE_SCV, flags)
+    np.testing.assert_array_equal(got, want)
+    windows, fallbacks = dev.greedy_stats()
+    if flags == 0 and path != "u64":
+        assert windows >= 1 and fallbacks < pods.n_pods
+    # the uploaded snapshot is unchanged afterwards
+    assert_same(dev.eval(pods, MODE_SCV), oracle.schedule(nodes, pods, MODE_SCV, threads=8))
+
+
+def test_greedy_small_windows_and_mode_b(dev):
+    nodes, pods = synth.make_config(5, pods=400, nodes=300)
+    pods.priority[:] = 0
+    dev.upload_nodes(nodes)
+    np.testing.assert_array_equal(dev.greedy(pods, MODE_DISKIO),
+                                  oracle.greedy(nodes, pods, MODE_DISKIO)[0])
+    # heavy contention: every pod wants the same few nodes
+    pods.memory[:] = 1
+    pods.has_memory[:] = 1
+    np.testing.assert_array_equal(dev.greedy(pods, MODE_SCV), oracle.greedy(nodes, pods)[0])
