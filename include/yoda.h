@@ -150,6 +150,7 @@ int yoda_synchronize(yoda_t* h);
  * (DESIGN.md §Exactness). */
 #define YODA_UPLOAD_FORCE_GENERIC 1u /* always the exact-u64 path                     */
 #define YODA_UPLOAD_FORCE_F64 2u     /* never the narrow path (tests)                 */
+#define YODA_UPLOAD_NO_UNIFORM 4u    /* disable the per-node GPU-model factoring (tests) */
 int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nodes, uint32_t node_offset,
                       uint32_t flags);
 /* 1 if the uploaded snapshot runs on the generic (u64) path, 0 on a fast path. */

@@ -538,6 +538,16 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
       hd.card_number = nd->card_number[i];
       hd.healthy_mask = hm;
       hd.zero_total = zt[i];
+      const uint32_t cnt = nd->card_count[i];
+      hd.real_mask = cnt >= 32 ? 0xffffffffu : ((1u << cnt) - 1u);
+      bool uni = cnt > 0;
+      for (uint32_t j = 1; j < cnt; ++j) {
+        const size_t a = (size_t)i * KS, b = a + j;
+        uni = uni && nd->card_clock[b] == nd->card_clock[a] &&
+              nd->card_bandwidth[b] == nd->card_bandwidth[a] &&
+              nd->card_core[b] == nd->card_core[a] && nd->card_power[b] == nd->card_power[a];
+      }
+      hd.flags = (uni && !(flags & YODA_UPLOAD_NO_UNIFORM)) ? kNodeUniform4 : 0u;
       if (path == Path::U64) {
         hd.static_score = stat[i];
       } else {
@@ -1124,6 +1134,7 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
     auto apply_pick = [&](uint32_t p, int32_t node) {
       if (node < 0) return;
       const uint32_t n = (uint32_t)node - h->node_offset;
+      g.touch(n);  // snapshots the window-start static before it changes
       if (pods->has_memory[p]) g.alloc[n] += pods->memory[p];  // uint64 wrap (algorithm.go:301)
       if (flags & YODA_GREEDY_CARD_CAPACITY) {
         const uint64_t num = pods->has_number[p] ? pods->number[p] : 1;
@@ -1131,7 +1142,6 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
       }
       bool z;
       g.stat[n] = static_score(h->h_free_sum[n], h->h_total_sum[n], g.alloc[n], &z);
-      g.touch(n);
       if (!ever[n]) {
         ever[n] = 1;
         all_touched.push_back(n);

@@ -112,16 +112,48 @@ __global__ __launch_bounds__(kBlock) void k1_filter_maxima(
     const NodeHdrG hd = *reinterpret_cast<const NodeHdrG*>(rec);
     const Group<T, K> fr = load_group<T, K>(rec + R::off(kFree, K));
     const Group<T, K> ck = load_group<T, K>(rec + R::off(kClock, K));
+    // one GPU model on the node (scalar flag, so the branch is wave-uniform)
+    bool uniform = false;
+    if constexpr (PATH == Path::N32) uniform = (hd.flags & kNodeUniform4) != 0u;
     uint32_t cm = 0, cc = 0;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       const uint32_t hj = (hd.healthy_mask >> j) & 1u;
       cm += (uint32_t)(fr.v[j] >= m) & hj;   // CardFitsMemory (filter.go:52-54)
-      cc += (uint32_t)(ck.v[j] == c) & hj;   // CardFitsClock  (filter.go:56-58)
+    }
+    if (uniform) {
+      // every real card has clock ck[0]: CardFitsClock counts all healthy cards or none
+      cc = (ck.v[0] == c) ? (uint32_t)__builtin_popcount(hd.healthy_mask) : 0u;
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        cc += (uint32_t)(ck.v[j] == c) & ((hd.healthy_mask >> j) & 1u);  // filter.go:56-58
     }
     const bool feas = (number <= hd.card_number) & (cm >= need_mem) & (cc >= need_clk);
     bits |= (uint32_t)feas << (n & 31u);
-    if (feas) {
+    if (feas && uniform) {
+      ++nf;
+      nz += hd.zero_total;
+      // qualifying cards (collection.go:46) = real cards with free >= m, if clock >= c
+      if (ck.v[0] >= c) {
+        const Group<T, K> to = load_group<T, K>(rec + R::off(kTotal, K));
+        uint32_t any = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const uint32_t q = ((hd.real_mask >> j) & 1u) & (uint32_t)(fr.v[j] >= m);
+          mx[kMaxFree] = fmax_t(mx[kMaxFree], q ? fr.v[j] : T(0));
+          mx[kMaxTotal] = fmax_t(mx[kMaxTotal], q ? to.v[j] : T(0));
+          any |= q;
+        }
+        if (any) {
+          const T* g = reinterpret_cast<const T*>(rec);
+          mx[kMaxBw] = fmax_t(mx[kMaxBw], g[R::off(kBandwidth, K) / sizeof(T)]);
+          mx[kMaxClock] = fmax_t(mx[kMaxClock], ck.v[0]);
+          mx[kMaxCore] = fmax_t(mx[kMaxCore], g[R::off(kCore, K) / sizeof(T)]);
+          mx[kMaxPower] = fmax_t(mx[kMaxPower], g[R::off(kPower, K) / sizeof(T)]);
+        }
+      }
+    } else if (feas) {
       ++nf;
       nz += hd.zero_total;
       const Group<T, K> bw = load_group<T, K>(rec + R::off(kBandwidth, K));
@@ -281,7 +313,32 @@ struct Scorer<Path::N32> {
   }
   template <int K>
   __device__ __forceinline__ double raw(const unsigned char* rec) const {
-    const double stat = reinterpret_cast<const NodeHdrF*>(rec)->static_score;
+    const NodeHdrF* hd = reinterpret_cast<const NodeHdrF*>(rec);
+    const double stat = hd->static_score;
+    if (hd->flags & kNodeUniform4) {
+      // One GPU model: the bandwidth, clock, core and power quotients are the same for every
+      // real card, so the card-score sum factors into  nq * shared + sum(3 q_free + q_tot)
+      // over the nq qualifying real cards — the same integers, added in another order.
+      const Group<uint32_t, K> fr = load_group<uint32_t, K>(rec + n32_u32_off(kFree, K));
+      const uint32_t ck0 = reinterpret_cast<const uint32_t*>(rec + n32_u32_off(kClock, K))[0];
+      const float* f32 = reinterpret_cast<const float*>(rec + n32_f32_off(0, K));
+      const Group<double, K> frd = load_group<double, K>(rec + n32_f64_off(kF64Free, K));
+      const Group<double, K> tod = load_group<double, K>(rec + n32_f64_off(kF64Total, K));
+      const uint32_t shared = (uint32_t)(f32[kF32Bandwidth * K] * r_bw) +
+                              (uint32_t)(f32[kF32Clock * K] * r_bw) +
+                              2u * (uint32_t)(f32[kF32Core * K] * r_core) +
+                              (uint32_t)(f32[kF32Power * K] * r_pow);
+      uint32_t nq = 0, mem = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const uint32_t q = ((hd->real_mask >> j) & 1u) & (uint32_t)(fr.v[j] >= m);
+        const uint32_t t = 3u * (uint32_t)(frd.v[j] * r_free) + (uint32_t)(tod.v[j] * r_tot);
+        mem += q ? t : 0u;
+        nq += q;
+      }
+      const uint32_t basic = (ck0 >= c) ? nq * shared + mem : 0u;  // algorithm.go:271
+      return (double)basic + stat;
+    }
     const Group<uint32_t, K> fr = load_group<uint32_t, K>(rec + n32_u32_off(kFree, K));
     const Group<uint32_t, K> ck = load_group<uint32_t, K>(rec + n32_u32_off(kClock, K));
     const Group<float, K> bwf = load_group<float, K>(rec + n32_f32_off(kF32Bandwidth, K));
@@ -352,7 +409,8 @@ __global__ __launch_bounds__(kBlock) void k2_score(
           uint32_t ci = n;
 #pragma unroll
           for (int k = 0; k < kTopK; ++k) {
-            const bool gt = cs > ts[k];
+            // (score desc, node asc): a carried entry that ties a slot must still shift
+            const bool gt = cs > ts[k] || (cs == ts[k] && ci < ti[k]);
             const double os = ts[k];
             const uint32_t oi = ti[k];
             ts[k] = gt ? cs : os;
@@ -412,10 +470,11 @@ __global__ __launch_bounds__(kBlock) void k_topk_merge(const double* __restrict_
       const size_t o = ((size_t)c * kTopK + e) * n_pods + p;
       double cs = tk_s[o];
       uint32_t ci = tk_i[o];
-      if (!(cs > ts[kTopK - 1])) break;  // lists are sorted: the rest cannot enter
+      // lists are sorted and later chunks hold higher node ids: the rest cannot enter
+      if (!(cs > ts[kTopK - 1])) break;
 #pragma unroll
       for (int k = 0; k < kTopK; ++k) {
-        const bool gt = cs > ts[k];
+        const bool gt = cs > ts[k] || (cs == ts[k] && ci < ti[k]);
         const double os = ts[k];
         const uint32_t oi = ti[k];
         ts[k] = gt ? cs : os;

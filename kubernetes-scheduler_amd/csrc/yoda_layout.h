@@ -34,8 +34,13 @@ struct alignas(16) NodeHdrF {
   uint64_t card_number;   // Status.CardNumber
   uint32_t healthy_mask;  // bit j: card j Healthy
   uint32_t zero_total;    // Status.TotalMemorySum == 0 (reference panics if scored)
-  uint32_t pad0, pad1;
+  uint32_t real_mask;     // bit j: j < len(CardList) (slots beyond are padding)
+  uint32_t flags;         // kNodeUniform4, ...
 };
+// Every real card of the node has the same clock, bandwidth, core and power (one GPU
+// model per node, the common case): K1 takes those maxima once per node and K2 computes
+// their quotients once per node (N32 path).
+constexpr uint32_t kNodeUniform4 = 1u;
 static_assert(sizeof(NodeHdrF) == 32, "NodeHdrF layout");
 
 // Generic (exact uint64) path: same shape with uint64 card fields.
@@ -44,7 +49,8 @@ struct alignas(16) NodeHdrG {
   uint64_t card_number;
   uint32_t healthy_mask;
   uint32_t zero_total;
-  uint32_t pad0, pad1;
+  uint32_t real_mask;
+  uint32_t flags;
 };
 static_assert(sizeof(NodeHdrG) == 32, "NodeHdrG layout");
 

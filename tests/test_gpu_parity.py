@@ -337,3 +337,25 @@ def test_greedy_small_windows_and_mode_b(dev):
     pods.memory[:] = 1
     pods.has_memory[:] = 1
     np.testing.assert_array_equal(dev.greedy(pods, MODE_SCV), oracle.greedy(nodes, pods)[0])
+
+
+def test_uniform_node_factoring(dev):
+    """Nodes with one GPU model take the factored K1/K2 branch; mixed nodes the per-card
+    one.  Both must equal the oracle, and equal each other with the factoring disabled."""
+    nodes, pods = synth.make_config(2, pods=400, nodes=3000)
+    rng = np.random.default_rng(12)
+    mixed = rng.random(nodes.n_nodes) < 0.5
+    k = nodes.card_clock.shape[1]
+    nodes.card_clock[mixed] = synth.CLOCKS[rng.integers(0, 3, size=(mixed.sum(), k))]
+    nodes.card_bandwidth[mixed[:, None] & (rng.random(nodes.card_bandwidth.shape) < 0.3)] = 1200
+    nodes = nodes.normalized()
+    want = oracle.schedule(nodes, pods, MODE_SCV, threads=8)
+    for no_uniform in (False, True):
+        dev.upload_nodes(nodes, no_uniform=no_uniform)
+        assert dev.path == "n32"
+        assert_same(dev.eval(pods, MODE_SCV), want)
+        dev.upload_pods(pods.slice(0, 16))
+        feas, rows = dev.score_rows(MODE_SCV)
+        for p in range(16):
+            _, f, raw, _ = oracle.pod_detail(nodes, pods, p)
+            np.testing.assert_array_equal(rows[p][f], raw[f])
