@@ -225,8 +225,11 @@ int yoda_profile_read(yoda_t* h, double* k1_ms, double* k2_ms, uint32_t* n_launc
 #define YODA_GREEDY_CARD_CAPACITY 1u
 int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, int32_t* pick);
 /* Work counters of the last yoda_greedy: GPU top-k windows, pods evaluated one by one
- * (uncertified candidates, or every pod on the exact sequential path). */
-int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks);
+ * (uncertified candidates, or every pod on the exact sequential path), and host wall time
+ * (ms) in times_ms[0..2] = {window candidate passes, sequential resolve, exact fallbacks}
+ * (times_ms may be NULL). */
+int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks,
+                      double* times_ms);
 
 #ifdef __cplusplus
 }

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -105,6 +106,33 @@ struct DevBuf {
   }
 };
 
+// Grow-only pinned host buffer (fast async H2D).
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= bytes) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    const size_t alloc = std::max<size_t>(n, 4096);
+    hipError_t e = hipHostMalloc(&p, alloc, hipHostMallocDefault);
+    if (e == hipSuccess) bytes = alloc;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+enum PodArray {
+  kPodMF, kPodCF, kPodMU, kPodCU, kPodNumber, kPodAlpha, kPodBeta,
+  kPodM32, kPodC32, kPodNeedMem, kPodNeedClk, kPodArrays
+};
+constexpr size_t kPodArrayBytes[kPodArrays] = {8, 8, 8, 8, 8, 8, 8, 4, 4, 4, 4};
+
 }  // namespace
 
 struct yoda_handle {
@@ -126,21 +154,25 @@ struct yoda_handle {
   std::vector<unsigned char> host_records;  // kept for alloc updates (greedy)
   std::vector<uint64_t> h_total_sum, h_free_sum, h_alloc, h_card_number;
 
-  // pods
+  // pods: one device blob of per-pod arrays (PodArray order), staged through pinned memory
   bool has_pods = false;
   uint32_t n_pods = 0;
-  std::vector<uint64_t> h_pod_mem;      // scv/memory (0 if absent) for greedy alloc
-  std::vector<uint8_t> h_pod_has_mem;
-  std::vector<uint64_t> h_pod_number;   // PodFitsNumber operand
-  DevBuf pod_m_f, pod_c_f, pod_m_u, pod_c_u, pod_m_32, pod_c_32, pod_number, pod_need_mem, pod_need_clk, pod_alpha,
-      pod_beta;
+  DevBuf pod_blob;
+  PinnedBuf pod_stage;
+  hipEvent_t stage_event = nullptr;
+  bool stage_pending = false;
+  size_t pod_off[kPodArrays] = {};
 
   // state
   DevBuf maxima, counts, rcp, rcp32, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
   DevBuf bitmask, bitmask_t, rows, rows_t;
   // greedy
   DevBuf tk_s_part, tk_i_part, tk_s, tk_i, upd_node, upd_val, upd_cn;
+  PinnedBuf upd_stage, pick_stage;
+  hipEvent_t upd_event = nullptr;
+  bool upd_pending = false;
   uint32_t greedy_windows = 0, greedy_fallbacks = 0;
+  double greedy_window_ms = 0, greedy_fallback_ms = 0, greedy_resolve_ms = 0;
   DevBuf p_max_u, p_cnt, p_best_f, p_best_i, p_idx, p_ties, p_low_f, p_low_i, p_err;
   uint32_t C1 = 1, chunk1 = 32;  // K1 node chunking
   uint32_t C2 = 1, chunk2 = 32;  // K2 / K3 node chunking
@@ -167,9 +199,7 @@ struct yoda_handle {
 
   ~yoda_handle() {
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&nodes,     &nodes_b,   &pod_m_f,    &pod_c_f,      &pod_m_u,
-                     &pod_c_u,   &pod_m_32,  &pod_c_32,   &pod_number,   &pod_need_mem,
-                     &pod_need_clk, &pod_alpha, &pod_beta, &maxima,      &counts,
+    DevBuf* all[] = {&nodes,     &nodes_b,   &pod_blob,   &maxima,       &counts,
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
                      &n_flagged, &bitmask,   &bitmask_t,  &p_max_u,      &p_cnt,
@@ -178,6 +208,11 @@ struct yoda_handle {
                      &p_best_f,  &p_best_i,  &p_idx,      &p_ties,       &p_low_f,
                      &p_low_i,   &p_err};
     for (DevBuf* b : all) b->release();
+    pod_stage.release();
+    upd_stage.release();
+    pick_stage.release();
+    if (stage_event) (void)hipEventDestroy(stage_event);
+    if (upd_event) (void)hipEventDestroy(upd_event);
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 };
@@ -272,18 +307,19 @@ int ensure_state(yoda_t* h, uint32_t P) {
 }
 
 PodParams pod_params(yoda_t* h) {
+  unsigned char* b = h->pod_blob.as<unsigned char>();
   PodParams pp;
-  pp.m_f = h->pod_m_f.as<double>();
-  pp.c_f = h->pod_c_f.as<double>();
-  pp.m_u = h->pod_m_u.as<uint64_t>();
-  pp.c_u = h->pod_c_u.as<uint64_t>();
-  pp.m_32 = h->pod_m_32.as<uint32_t>();
-  pp.c_32 = h->pod_c_32.as<uint32_t>();
-  pp.number = h->pod_number.as<uint64_t>();
-  pp.need_mem = h->pod_need_mem.as<uint32_t>();
-  pp.need_clk = h->pod_need_clk.as<uint32_t>();
-  pp.alpha = h->pod_alpha.as<double>();
-  pp.beta = h->pod_beta.as<double>();
+  pp.m_f = reinterpret_cast<double*>(b + h->pod_off[kPodMF]);
+  pp.c_f = reinterpret_cast<double*>(b + h->pod_off[kPodCF]);
+  pp.m_u = reinterpret_cast<uint64_t*>(b + h->pod_off[kPodMU]);
+  pp.c_u = reinterpret_cast<uint64_t*>(b + h->pod_off[kPodCU]);
+  pp.m_32 = reinterpret_cast<uint32_t*>(b + h->pod_off[kPodM32]);
+  pp.c_32 = reinterpret_cast<uint32_t*>(b + h->pod_off[kPodC32]);
+  pp.number = reinterpret_cast<uint64_t*>(b + h->pod_off[kPodNumber]);
+  pp.need_mem = reinterpret_cast<uint32_t*>(b + h->pod_off[kPodNeedMem]);
+  pp.need_clk = reinterpret_cast<uint32_t*>(b + h->pod_off[kPodNeedClk]);
+  pp.alpha = reinterpret_cast<double*>(b + h->pod_off[kPodAlpha]);
+  pp.beta = reinterpret_cast<double*>(b + h->pod_off[kPodBeta]);
   return pp;
 }
 
@@ -440,6 +476,11 @@ int yoda_create(int device, yoda_t** out) {
     return YODA_ERR_HIP;
   }
   h->stream = h->own_stream;
+  if (hipEventCreateWithFlags(&h->stage_event, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->upd_event, hipEventDisableTiming) != hipSuccess) {
+    delete h;
+    return YODA_ERR_HIP;
+  }
   *out = h;
   return YODA_OK;
 }
@@ -663,13 +704,28 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
                   !pd->has_clock || !pd->clock))
       return fail(h, YODA_ERR_INVALID_ARG, "a required pod array is NULL");
     HIP_TRY(h, hipSetDevice(h->device));
-    const uint64_t kClamp = 1ull << 53;  // > every fast-path card field (<= 2^44)
-    std::vector<double> mf(P), cf(P), al(P), be(P);
-    std::vector<uint64_t> mu(P), cu(P), num(P);
-    std::vector<uint32_t> nm(P), nc(P), m32(P), c32(P);
-    h->h_pod_mem.assign(P, 0);
-    h->h_pod_has_mem.assign(P, 0);
-    h->h_pod_number.assign(P, 1);
+    // One blob of per-pod arrays, staged in pinned memory and sent with ONE copy.
+    size_t off[kPodArrays], total = 0;
+    for (int a = 0; a < kPodArrays; ++a) {
+      off[a] = total;
+      total += ((size_t)std::max<uint32_t>(P, 1) * kPodArrayBytes[a] + 255) / 256 * 256;
+    }
+    if (h->stage_pending) HIP_TRY(h, hipEventSynchronize(h->stage_event));  // staging reuse
+    HIP_TRY(h, h->pod_stage.ensure(total));
+    HIP_TRY(h, h->pod_blob.ensure(total));
+    unsigned char* st = static_cast<unsigned char*>(h->pod_stage.p);
+    double* mf = reinterpret_cast<double*>(st + off[kPodMF]);
+    double* cf = reinterpret_cast<double*>(st + off[kPodCF]);
+    uint64_t* mu = reinterpret_cast<uint64_t*>(st + off[kPodMU]);
+    uint64_t* cu = reinterpret_cast<uint64_t*>(st + off[kPodCU]);
+    uint64_t* num = reinterpret_cast<uint64_t*>(st + off[kPodNumber]);
+    double* al = reinterpret_cast<double*>(st + off[kPodAlpha]);
+    double* be = reinterpret_cast<double*>(st + off[kPodBeta]);
+    uint32_t* m32 = reinterpret_cast<uint32_t*>(st + off[kPodM32]);
+    uint32_t* c32 = reinterpret_cast<uint32_t*>(st + off[kPodC32]);
+    uint32_t* nm = reinterpret_cast<uint32_t*>(st + off[kPodNeedMem]);
+    uint32_t* nc = reinterpret_cast<uint32_t*>(st + off[kPodNeedClk]);
+    const uint64_t kClamp = 1ull << 53;  // > every F64-path card field (<= 2^44)
     for (uint32_t p = 0; p < P; ++p) {
       const uint64_t number = pd->has_number[p] ? pd->number[p] : 1;  // filter.go:12-15
       const uint64_t m = pd->has_memory[p] ? pd->memory[p] : 0;       // filter.go:19,32
@@ -684,33 +740,17 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
       cf[p] = (double)std::min(c, kClamp);
       m32[p] = (uint32_t)std::min<uint64_t>(m, 0xffffffffull);  // > every N32 field
       c32[p] = (uint32_t)std::min<uint64_t>(c, 0xffffffffull);
-      h->h_pod_mem[p] = pd->memory[p];
-      h->h_pod_has_mem[p] = pd->has_memory[p];
-      h->h_pod_number[p] = number;
+      al[p] = be[p] = 0.0;
       if (pd->rio && pd->rcpu) {  // algorithm.go:105-106
         const double beta = 1.0 / (1.0 + (double)pd->rcpu[p] / pd->rio[p]);
         be[p] = beta;
         al[p] = 1 - beta;
       }
     }
-    auto up = [&](DevBuf& b, const void* src, size_t bytes) -> int {
-      HIP_TRY(h, b.ensure(bytes));
-      if (bytes) HIP_TRY(h, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, h->stream));
-      return YODA_OK;
-    };
-    int rc;
-    if ((rc = up(h->pod_m_f, mf.data(), P * 8ull)) ||
-        (rc = up(h->pod_c_f, cf.data(), P * 8ull)) ||
-        (rc = up(h->pod_m_u, mu.data(), P * 8ull)) ||
-        (rc = up(h->pod_c_u, cu.data(), P * 8ull)) ||
-        (rc = up(h->pod_m_32, m32.data(), P * 4ull)) ||
-        (rc = up(h->pod_c_32, c32.data(), P * 4ull)) ||
-        (rc = up(h->pod_number, num.data(), P * 8ull)) ||
-        (rc = up(h->pod_need_mem, nm.data(), P * 4ull)) ||
-        (rc = up(h->pod_need_clk, nc.data(), P * 4ull)) ||
-        (rc = up(h->pod_alpha, al.data(), P * 8ull)) || (rc = up(h->pod_beta, be.data(), P * 8ull)))
-      return rc;
-    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    HIP_TRY(h, hipMemcpyAsync(h->pod_blob.p, st, total, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(h, hipEventRecord(h->stage_event, h->stream));
+    h->stage_pending = true;
+    for (int a = 0; a < kPodArrays; ++a) h->pod_off[a] = off[a];
     h->n_pods = P;
     h->has_pods = true;
     h->ran = false;
@@ -1014,26 +1054,31 @@ struct GreedyState {
   }
   int push(std::vector<uint32_t>& list, std::vector<uint8_t>* marks) {
     if (list.empty()) return YODA_OK;
-    std::vector<uint64_t> val(list.size()), cn(list.size());
-    for (size_t i = 0; i < list.size(); ++i) {
+    // one pinned staging copy: [node u32 x cnt | pad | static u64 x cnt | CardNumber u64 x cnt]
+    const uint32_t cnt = (uint32_t)list.size();
+    const size_t o_val = ((size_t)cnt * 4 + 15) / 16 * 16, o_cn = o_val + (size_t)cnt * 8;
+    const size_t bytes = o_cn + (size_t)cnt * 8;
+    if (h->upd_pending) HIP_TRY(h, hipEventSynchronize(h->upd_event));
+    HIP_TRY(h, h->upd_stage.ensure(bytes));
+    HIP_TRY(h, h->upd_node.ensure(bytes));
+    unsigned char* st = static_cast<unsigned char*>(h->upd_stage.p);
+    uint32_t* nd = reinterpret_cast<uint32_t*>(st);
+    uint64_t* val = reinterpret_cast<uint64_t*>(st + o_val);
+    uint64_t* cn = reinterpret_cast<uint64_t*>(st + o_cn);
+    for (uint32_t i = 0; i < cnt; ++i) {
+      nd[i] = list[i];
       val[i] = stat_bits(stat[list[i]]);
       cn[i] = card_number[list[i]];
     }
-    const uint32_t cnt = (uint32_t)list.size();
-    HIP_TRY(h, h->upd_node.ensure(cnt * 4ull));
-    HIP_TRY(h, h->upd_val.ensure(cnt * 8ull));
-    HIP_TRY(h, h->upd_cn.ensure(cnt * 8ull));
-    HIP_TRY(h, hipMemcpyAsync(h->upd_node.p, list.data(), cnt * 4ull, hipMemcpyHostToDevice,
-                              h->stream));
-    HIP_TRY(h, hipMemcpyAsync(h->upd_val.p, val.data(), cnt * 8ull, hipMemcpyHostToDevice,
-                              h->stream));
-    HIP_TRY(h, hipMemcpyAsync(h->upd_cn.p, cn.data(), cnt * 8ull, hipMemcpyHostToDevice,
-                              h->stream));
+    HIP_TRY(h, hipMemcpyAsync(h->upd_node.p, st, bytes, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(h, hipEventRecord(h->upd_event, h->stream));
+    h->upd_pending = true;
+    unsigned char* d = h->upd_node.as<unsigned char>();
     const uint32_t stride = h->path == Path::N32 ? n32_stride(h->K) : node_stride(h->K);
-    HIP_TRY(h, launch_set_static(h->nodes.as<unsigned char>(), stride, h->upd_node.as<uint32_t>(),
-                                 h->upd_val.as<uint64_t>(), h->upd_cn.as<uint64_t>(), cnt,
-                                 h->stream));
-    HIP_TRY(h, hipStreamSynchronize(h->stream));  // host vectors die at return
+    HIP_TRY(h, launch_set_static(h->nodes.as<unsigned char>(), stride,
+                                 reinterpret_cast<const uint32_t*>(d),
+                                 reinterpret_cast<const uint64_t*>(d + o_val),
+                                 reinterpret_cast<const uint64_t*>(d + o_cn), cnt, h->stream));
     if (marks)
       for (uint32_t n : list) (*marks)[n] = 0;
     list.clear();
@@ -1071,6 +1116,8 @@ struct PodGather {
   }
 };
 
+constexpr uint32_t kGreedyWindow = 4096;
+
 // Exact evaluation of ONE pod against the current device state (pushes pending updates).
 int greedy_eval_one(GreedyState& g, const yoda_pod_soa* pods, uint32_t p, int mode,
                     int32_t* pick_out) {
@@ -1081,8 +1128,10 @@ int greedy_eval_one(GreedyState& g, const yoda_pod_soa* pods, uint32_t p, int mo
   one.build(pods, &p, 1);
   if ((rc = yoda_upload_pods(h, &one.soa))) return rc;
   if ((rc = yoda_run(h, mode, 0))) return rc;
-  HIP_TRY(h, hipMemcpyAsync(pick_out, h->pick.p, 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, h->pick_stage.ensure(16));
+  HIP_TRY(h, hipMemcpyAsync(h->pick_stage.p, h->pick.p, 4, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
+  *pick_out = *static_cast<int32_t*>(h->pick_stage.p);
   return YODA_OK;
 }
 
@@ -1097,6 +1146,11 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
     const uint32_t P = pods->n_pods, N = h->n_nodes;
     h->greedy_windows = 0;
     h->greedy_fallbacks = 0;
+    h->greedy_window_ms = h->greedy_fallback_ms = h->greedy_resolve_ms = 0;
+    using Clock = std::chrono::steady_clock;
+    auto ms_since = [](Clock::time_point t0) {
+      return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+    };
     if (P == 0) return YODA_OK;
     int rc;
     // Queue order: sort.Less (sort.go:8-10) -- scv/priority descending, then input index.
@@ -1164,13 +1218,16 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
       // window only the Allocate term of picked nodes changes, and it never increases
       // (unless alloc wraps around 2^64: then the rest of the window is evaluated exactly).
       const uint32_t KT = (uint32_t)topk_k();
-      const uint32_t W = std::min<uint32_t>(P, 1u << 16);
+      // Small windows: the GPU work is the same P x N in total, while fewer nodes are
+      // touched per window, so fewer candidate lists lose certification.
+      const uint32_t W = std::min<uint32_t>(P, kGreedyWindow);
       PodGather win;
       std::vector<uint32_t> counts(2 * (size_t)W);
       std::vector<double> ts((size_t)KT * W);
       std::vector<uint32_t> ti((size_t)KT * W);
       for (uint32_t ws = 0; ws < P; ws += W) {
         const uint32_t wn = std::min(W, P - ws);
+        const auto tw = Clock::now();
         if ((rc = g.push_dirty())) return rc;
         for (uint32_t n : g.touched_list) g.touched_w[n] = 0;
         g.touched_list.clear();
@@ -1206,6 +1263,9 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
           std::fill(counts.begin(), counts.end(), 0u);
         }
         ++h->greedy_windows;
+        h->greedy_window_ms += ms_since(tw);
+        const auto tr = Clock::now();
+        double fb_ms = 0;
         bool wrapped = false;
         for (uint32_t i = 0; i < wn; ++i) {
           const uint32_t p = order[ws + i];
@@ -1218,8 +1278,10 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
           } else if (nf == 1) {
             pk = (int32_t)ti[i];   // the only feasible node, returned without scoring
           } else if (wrapped) {
+            const auto tf = Clock::now();
             if ((rc = greedy_eval_one(g, pods, p, YODA_MODE_SCV, &pk))) return rc;
             ++h->greedy_fallbacks;
+            fb_ms += ms_since(tf);
           } else {
             // current score of each candidate: window-start score - old static + new static
             const uint32_t len = std::min<uint32_t>(nf, KT);
@@ -1243,8 +1305,10 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
             if (certified) {
               pk = (int32_t)bi;
             } else {
+              const auto tf = Clock::now();
               if ((rc = greedy_eval_one(g, pods, p, YODA_MODE_SCV, &pk))) return rc;
               ++h->greedy_fallbacks;
+              fb_ms += ms_since(tf);
             }
           }
           pick[p] = pk;
@@ -1255,6 +1319,8 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
             if (g.alloc[n] < before) wrapped = true;  // Allocate may grow: stop certifying
           }
         }
+        h->greedy_fallback_ms += fb_ms;
+        h->greedy_resolve_ms += ms_since(tr) - fb_ms;
       }
     }
     // Leave the uploaded snapshot unchanged: restore static score and CardNumber.
@@ -1263,6 +1329,7 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
       g.card_number[n] = h->h_card_number[n];
     }
     if ((rc = g.push(all_touched, nullptr))) return rc;
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
     h->ran = false;
     return YODA_OK;
   } catch (const std::bad_alloc&) {
@@ -1272,10 +1339,16 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
   }
 }
 
-int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks) {
+int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks,
+                      double* times_ms) {
   if (!h) return YODA_ERR_INVALID_ARG;
   if (windows) *windows = h->greedy_windows;
   if (fallbacks) *fallbacks = h->greedy_fallbacks;
+  if (times_ms) {
+    times_ms[0] = h->greedy_window_ms;
+    times_ms[1] = h->greedy_resolve_ms;
+    times_ms[2] = h->greedy_fallback_ms;
+  }
   return YODA_OK;
 }
 

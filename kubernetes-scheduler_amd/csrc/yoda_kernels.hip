@@ -204,6 +204,29 @@ __global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__
   }
 }
 
+// Wave-per-pod variant of k_reduce1 for many chunks (small pod batches, e.g. the greedy
+// single-pod fallback): the 64 lanes stride over the chunks, then a shuffle reduction.
+__global__ __launch_bounds__(kWave) void k_reduce1_wave(const uint64_t* __restrict__ pmax,
+                                                         const uint32_t* __restrict__ pcnt,
+                                                         uint32_t C, uint32_t n_pods,
+                                                         uint64_t* __restrict__ maxima,
+                                                         uint32_t* __restrict__ counts) {
+  const uint32_t p = blockIdx.x, lane = threadIdx.x;
+  for (int f = 0; f < 6; ++f) {
+    uint64_t mx = 1;
+    for (uint32_t c = lane; c < C; c += kWave)
+      mx = umax64(mx, pmax[((size_t)f * C + c) * n_pods + p]);
+    for (int o = kWave / 2; o > 0; o >>= 1) mx = umax64(mx, __shfl_xor(mx, o, kWave));
+    if (lane == 0) maxima[(size_t)f * n_pods + p] = mx;
+  }
+  for (int f = 0; f < 2; ++f) {
+    uint32_t sum = 0;
+    for (uint32_t c = lane; c < C; c += kWave) sum += pcnt[((size_t)f * C + c) * n_pods + p];
+    for (int o = kWave / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, kWave);
+    if (lane == 0) counts[(size_t)f * n_pods + p] = sum;
+  }
+}
+
 // RU(100 / M): the smallest double >= 100/M.  With every card field <= 2^44,
 // floor(x * RU(100/M)) == floor(100 x / M) exactly.
 __device__ __forceinline__ double ru_100_over(double M) {
@@ -491,6 +514,65 @@ __global__ __launch_bounds__(kBlock) void k_topk_merge(const double* __restrict_
   }
 }
 
+// Wave-per-pod top-k merge: each lane folds a strided subset of chunk lists into its own
+// top-k, then the 64 lists are folded pairwise through shuffles.  The (score desc, node asc)
+// comparison is a total order, so the result does not depend on the folding order.
+__device__ __forceinline__ void topk_insert(double (&ts)[kTopK], uint32_t (&ti)[kTopK],
+                                            double cs, uint32_t ci) {
+#pragma unroll
+  for (int k = 0; k < kTopK; ++k) {
+    const bool gt = cs > ts[k] || (cs == ts[k] && ci < ti[k]);
+    const double os = ts[k];
+    const uint32_t oi = ti[k];
+    ts[k] = gt ? cs : os;
+    ti[k] = gt ? ci : oi;
+    cs = gt ? os : cs;
+    ci = gt ? oi : ci;
+  }
+}
+
+__global__ __launch_bounds__(kWave) void k_topk_merge_wave(const double* __restrict__ tk_s,
+                                                            const uint32_t* __restrict__ tk_i,
+                                                            uint32_t C, uint32_t n_pods,
+                                                            uint32_t node_offset,
+                                                            double* __restrict__ out_s,
+                                                            uint32_t* __restrict__ out_i) {
+  const uint32_t p = blockIdx.x, lane = threadIdx.x;
+  double ts[kTopK];
+  uint32_t ti[kTopK];
+#pragma unroll
+  for (int k = 0; k < kTopK; ++k) {
+    ts[k] = -1.0;
+    ti[k] = 0xffffffffu;
+  }
+  for (uint32_t c = lane; c < C; c += kWave) {
+    for (int e = 0; e < kTopK; ++e) {
+      const size_t o = ((size_t)c * kTopK + e) * n_pods + p;
+      const double cs = tk_s[o];
+      const uint32_t ci = tk_i[o];
+      if (!(cs > ts[kTopK - 1] || (cs == ts[kTopK - 1] && ci < ti[kTopK - 1]))) break;
+      topk_insert(ts, ti, cs, ci);
+    }
+  }
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    double ps[kTopK];
+    uint32_t pi[kTopK];
+#pragma unroll
+    for (int k = 0; k < kTopK; ++k) {
+      ps[k] = __shfl_xor(ts[k], o, kWave);
+      pi[k] = __shfl_xor(ti[k], o, kWave);
+    }
+#pragma unroll
+    for (int k = 0; k < kTopK; ++k) topk_insert(ts, ti, ps[k], pi[k]);
+  }
+  if (lane != 0) return;
+#pragma unroll
+  for (int k = 0; k < kTopK; ++k) {
+    out_s[(size_t)k * n_pods + p] = ts[k];
+    out_i[(size_t)k * n_pods + p] = ti[k] == 0xffffffffu ? ti[k] : ti[k] + node_offset;
+  }
+}
+
 // Greedy: overwrite the static score (record header offset 0) of a few nodes.
 __global__ __launch_bounds__(kBlock) void k_set_static(unsigned char* __restrict__ nodes,
                                                        uint32_t stride,
@@ -671,6 +753,67 @@ __global__ __launch_bounds__(kBlock) void k_reduce2(const double* __restrict__ p
     }
     low = l < low ? l : low;
   }
+  best_out[p] = best;
+  idx_out[p] = idx == 0xffffffffu ? idx : idx + node_offset;
+  ties_out[p] = ties;
+  low_out[p] = low;
+}
+
+// Wave-per-pod variant of k_reduce2 (many chunks).  Each lane merges a strided subset of
+// chunks in increasing order; lanes then combine (best desc, idx asc), summing ties.
+__global__ __launch_bounds__(kWave) void k_reduce2_wave(const double* __restrict__ pbest_f,
+                                                         const int64_t* __restrict__ pbest_i,
+                                                         const uint32_t* __restrict__ pidx,
+                                                         const uint32_t* __restrict__ pties,
+                                                         const double* __restrict__ plow_f,
+                                                         const int64_t* __restrict__ plow_i,
+                                                         uint32_t C, uint32_t n_pods, int is_f64,
+                                                         uint32_t node_offset,
+                                                         int64_t* __restrict__ best_out,
+                                                         uint32_t* __restrict__ idx_out,
+                                                         uint32_t* __restrict__ ties_out,
+                                                         int64_t* __restrict__ low_out) {
+  const uint32_t p = blockIdx.x, lane = threadIdx.x;
+  int64_t best = -1, low = kI64Max;
+  uint32_t idx = 0xffffffffu, ties = 0;
+  for (uint32_t c = lane; c < C; c += kWave) {
+    const size_t o = (size_t)c * n_pods + p;
+    int64_t b, l;
+    if (is_f64) {
+      const double bf = pbest_f[o], lf = plow_f[o];
+      b = bf < 0.0 ? -1 : (int64_t)bf;
+      l = lf > 9.0e18 ? kI64Max : (int64_t)lf;
+    } else {
+      b = pbest_i[o];
+      l = plow_i[o];
+    }
+    if (b < 0) continue;
+    if (b > best) {
+      best = b;
+      idx = pidx[o];
+      ties = pties[o];
+    } else if (b == best) {
+      ties += pties[o];
+      idx = min(idx, pidx[o]);
+    }
+    low = l < low ? l : low;
+  }
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    const int64_t ob = __shfl_xor(best, o, kWave);
+    const uint32_t oi = __shfl_xor(idx, o, kWave);
+    const uint32_t ot = __shfl_xor(ties, o, kWave);
+    const int64_t ol = __shfl_xor(low, o, kWave);
+    if (ob > best) {
+      best = ob;
+      idx = oi;
+      ties = ot;
+    } else if (ob == best && ob >= 0) {
+      ties += ot;
+      idx = min(idx, oi);
+    }
+    low = ol < low ? ol : low;
+  }
+  if (lane != 0) return;
   best_out[p] = best;
   idx_out[p] = idx == 0xffffffffu ? idx : idx + node_offset;
   ties_out[p] = ties;
@@ -917,10 +1060,18 @@ int kernel_capacity(int K, Path path, int which, int mode_diskio) {
   return nb * cus;
 }
 
+// Chunk partials are merged one thread per pod (coalesced over pods) when there are few
+// chunks, one wave per pod (strided over chunks) when there are many.
+constexpr uint32_t kWaveReduceChunks = 48;
+
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uint64_t* maxima,
                           uint32_t* counts, hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce1, pod_grid(n_pods), dim3(kBlock), 0, s, part.max_u, part.cnt, C,
-                     n_pods, maxima, counts);
+  if (C > kWaveReduceChunks)
+    hipLaunchKernelGGL(k_reduce1_wave, dim3(n_pods), dim3(kWave), 0, s, part.max_u, part.cnt, C,
+                       n_pods, maxima, counts);
+  else
+    hipLaunchKernelGGL(k_reduce1, pod_grid(n_pods), dim3(kBlock), 0, s, part.max_u, part.cnt, C,
+                       n_pods, maxima, counts);
   return hipGetLastError();
 }
 
@@ -974,6 +1125,11 @@ hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t
 hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t C,
                              uint32_t n_pods, uint32_t node_offset, double* out_s,
                              uint32_t* out_i, hipStream_t s) {
+  if (C > 8) {
+    hipLaunchKernelGGL(k_topk_merge_wave, dim3(n_pods), dim3(kWave), 0, s, tk_s, tk_i, C, n_pods,
+                       node_offset, out_s, out_i);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_topk_merge, pod_grid(n_pods), dim3(kBlock), 0, s, tk_s, tk_i, C, n_pods,
                      node_offset, out_s, out_i);
   return hipGetLastError();
@@ -1038,6 +1194,12 @@ hipError_t launch_rows_transpose(const int64_t* in, uint32_t n_nodes, uint32_t n
 hipError_t launch_reduce2(const Partials& part, uint32_t C, uint32_t n_pods, bool is_f64,
                           uint32_t node_offset, int64_t* best, uint32_t* idx, uint32_t* ties,
                           int64_t* low, hipStream_t s) {
+  if (C > kWaveReduceChunks) {
+    hipLaunchKernelGGL(k_reduce2_wave, dim3(n_pods), dim3(kWave), 0, s, part.best_f, part.best_i,
+                       part.idx, part.ties, part.low_f, part.low_i, C, n_pods, is_f64 ? 1 : 0,
+                       node_offset, best, idx, ties, low);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_reduce2, pod_grid(n_pods), dim3(kBlock), 0, s, part.best_f, part.best_i,
                      part.idx, part.ties, part.low_f, part.low_i, C, n_pods, is_f64 ? 1 : 0,
                      node_offset, best, idx, ties, low);

@@ -55,7 +55,8 @@ _SIGS = {
     "yoda_profile_read": ([_vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                            C.POINTER(C.c_uint32)], C.c_int),
     "yoda_greedy": ([_vp, C.POINTER(CPodSoA), C.c_int, _u32, C.POINTER(C.c_int32)], C.c_int),
-    "yoda_greedy_stats": ([_vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)], C.c_int),
+    "yoda_greedy_stats": ([_vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                           C.POINTER(C.c_double)], C.c_int),
 }
 
 
@@ -217,10 +218,16 @@ class Yoda:
                                       pick.ctypes.data_as(C.POINTER(C.c_int32))), "yoda_greedy")
         return pick
 
-    def greedy_stats(self):
-        """(top-k windows, pods evaluated one by one) of the last greedy()."""
+    def greedy_stats(self, times: bool = False):
+        """(top-k windows, pods evaluated one by one[, {window, resolve, fallback} ms]) of
+        the last greedy()."""
         w, f = C.c_uint32(), C.c_uint32()
-        self._check(lib().yoda_greedy_stats(self._h, C.byref(w), C.byref(f)), "yoda_greedy_stats")
+        t = (C.c_double * 3)()
+        self._check(lib().yoda_greedy_stats(self._h, C.byref(w), C.byref(f), t),
+                    "yoda_greedy_stats")
+        if times:
+            return w.value, f.value, {"window_ms": t[0], "resolve_ms": t[1],
+                                      "fallback_ms": t[2]}
         return w.value, f.value
 
     def profile(self, enable: bool = True):
