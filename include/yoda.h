@@ -208,6 +208,13 @@ int yoda_shard_finalize(yoda_t* h, int mode, const uint32_t* d_counts, const int
  * the exact normalize (scheduler.go:176-179).  Returns the number of such pods in *n_pods. */
 int yoda_shard_overflow_count(yoda_t* h, uint32_t* n_pods);
 
+/* ---- batch ordering ---------------------------------------------------------------- */
+/* Mode A runs of more than 128 pods (yoda_run, yoda_score_rows, yoda_shard_phase1) sort the
+ * batch on the device by the Filter's inputs so that whole wavefronts skip infeasible nodes;
+ * every output is returned in the caller's pod order, so results never depend on it.
+ * enable = 0 turns the ordering off (default on).  Takes effect from the next run. */
+int yoda_set_pod_order(yoda_t* h, int enable);
+
 /* ---- kernel timing ----------------------------------------------------------------- */
 /* enable != 0: every subsequent K1 / K2 launch is bracketed by HIP events recorded on the
  * launch stream.  yoda_profile_read synchronizes, returns the summed K1 and K2 durations

@@ -35,6 +35,7 @@ hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t ch
                             uint32_t C, const PodParams& pp, uint32_t n_pods, const Partials& part,
                             int64_t* rows, hipStream_t s);
 hipError_t launch_rows_transpose(const int64_t* in, uint32_t n_nodes, uint32_t n_pods,
+                                 const uint32_t* perm,
                                  int64_t* out, hipStream_t s);
 hipError_t launch_reduce2(const Partials& part, uint32_t C, uint32_t n_pods, bool is_f64,
                           uint32_t node_offset, int64_t* best, uint32_t* idx, uint32_t* ties,
@@ -56,7 +57,7 @@ hipError_t launch_reduce3(const Partials& part, uint32_t C, const uint32_t* flag
                           const uint32_t* n_flagged, uint32_t max_flagged, uint32_t node_offset,
                           int32_t* pick, int32_t* status, uint32_t* ties, hipStream_t s);
 hipError_t launch_bitmask_transpose(const uint32_t* in, uint32_t W, uint32_t n_pods,
-                                    uint32_t* out, hipStream_t s);
+                                    const uint32_t* perm, uint32_t* out, hipStream_t s);
 int kernel_capacity(int K, Path path, int which, int mode_diskio);
 hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                           uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
@@ -70,6 +71,12 @@ hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32
                              const uint64_t* value, const uint64_t* card_number, uint32_t count,
                              hipStream_t s);
 int topk_k();
+size_t order_scratch_bytes(uint32_t n_pods);
+hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
+                             uint32_t n_pods, void* scratch, size_t scratch_bytes,
+                             uint32_t* perm, hipStream_t s);
+hipError_t launch_permute(const PermTable& t, const uint32_t* perm, uint32_t n_pods, bool scatter,
+                          hipStream_t s);
 }  // namespace yoda
 
 using namespace yoda;
@@ -162,6 +169,12 @@ struct yoda_handle {
   hipEvent_t stage_event = nullptr;
   bool stage_pending = false;
   size_t pod_off[kPodArrays] = {};
+  // batch ordering (yoda_order.hip): when `ordered`, the kernels of this run read the pods
+  // from pod_sorted (sorted position i = original pod perm[i]); bitmask/rows stay in sorted
+  // order and are un-permuted by their transposes, the per-pod outputs by finalize().
+  bool order_enabled = true;
+  bool ordered = false;
+  DevBuf pod_sorted, perm, order_scratch, unperm;
 
   // state
   DevBuf maxima, counts, rcp, rcp32, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
@@ -200,6 +213,7 @@ struct yoda_handle {
   ~yoda_handle() {
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     DevBuf* all[] = {&nodes,     &nodes_b,   &pod_blob,   &maxima,       &counts,
+                     &pod_sorted, &perm,     &order_scratch, &unperm,
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
                      &n_flagged, &bitmask,   &bitmask_t,  &p_max_u,      &p_cnt,
@@ -307,7 +321,7 @@ int ensure_state(yoda_t* h, uint32_t P) {
 }
 
 PodParams pod_params(yoda_t* h) {
-  unsigned char* b = h->pod_blob.as<unsigned char>();
+  unsigned char* b = (h->ordered ? h->pod_sorted : h->pod_blob).as<unsigned char>();
   PodParams pp;
   pp.m_f = reinterpret_cast<double*>(b + h->pod_off[kPodMF]);
   pp.c_f = reinterpret_cast<double*>(b + h->pod_off[kPodCF]);
@@ -346,6 +360,78 @@ int check_ready(yoda_t* h, int mode) {
   if (mode == YODA_MODE_DISKIO && !(h->nodes_diskio && h->pods_diskio))
     return fail(h, YODA_ERR_INVALID_ARG, "Mode B needs node cpu/disk_io and pod rio/rcpu");
   HIP_TRY(h, hipSetDevice(h->device));
+  return YODA_OK;
+}
+
+// Batches above this size are sorted (below it a batch fills at most one wave).
+constexpr uint32_t kOrderMinPods = 2 * kWave;
+
+// Sort the batch by its Filter inputs and gather the pod arrays (yoda_order.hip).  Runs on
+// the device inside every run, so its cost is part of the measured step.
+int order_pods(yoda_t* h, int mode) {
+  const uint32_t P = h->n_pods;
+  h->ordered = false;
+  if (!h->order_enabled || mode != YODA_MODE_SCV || P < kOrderMinPods || h->n_nodes == 0)
+    return YODA_OK;
+  const unsigned char* b = h->pod_blob.as<unsigned char>();
+  const size_t scratch = order_scratch_bytes(P);
+  HIP_TRY(h, h->order_scratch.ensure(scratch));
+  HIP_TRY(h, h->perm.ensure((size_t)P * 4));
+  HIP_TRY(h, h->pod_sorted.ensure(h->pod_blob.bytes));
+  HIP_TRY(h, launch_order_pods(reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodNumber]),
+                               reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodMU]),
+                               reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodCU]), P,
+                               h->order_scratch.p, h->order_scratch.bytes,
+                               h->perm.as<uint32_t>(), h->stream));
+  PermTable t{};
+  for (int a = 0; a < kPodArrays; ++a) {
+    t.src[t.n] = b + h->pod_off[a];
+    t.dst[t.n] = h->pod_sorted.as<unsigned char>() + h->pod_off[a];
+    t.bytes[t.n] = (uint32_t)kPodArrayBytes[a];
+    ++t.n;
+  }
+  HIP_TRY(h, launch_permute(t, h->perm.as<uint32_t>(), P, false, h->stream));
+  h->ordered = true;
+  return YODA_OK;
+}
+
+// Scatter the per-pod outputs of an ordered run back to the caller's pod order.
+int unpermute_outputs(yoda_t* h) {
+  const uint32_t P = h->n_pods;
+  if (!h->ordered || P == 0) return YODA_OK;
+  struct Arr {
+    DevBuf* buf;
+    size_t row;
+    uint32_t bytes;
+  };
+  const Arr arrs[] = {{&h->pick, 0, 4},   {&h->status, 0, 4}, {&h->ties_out, 0, 4},
+                      {&h->counts, 0, 4}, {&h->counts, 1, 4}, {&h->best, 0, 8},
+                      {&h->maxima, 0, 8}, {&h->maxima, 1, 8}, {&h->maxima, 2, 8},
+                      {&h->maxima, 3, 8}, {&h->maxima, 4, 8}, {&h->maxima, 5, 8}};
+  size_t total = 0;
+  for (const Arr& a : arrs) total += (size_t)P * a.bytes;
+  HIP_TRY(h, h->unperm.ensure(total));
+  PermTable t{};
+  size_t off = 0;
+  for (const Arr& a : arrs) {
+    t.src[t.n] = a.buf->as<unsigned char>() + a.row * P * a.bytes;
+    t.dst[t.n] = h->unperm.as<unsigned char>() + off;
+    t.bytes[t.n] = a.bytes;
+    ++t.n;
+    off += (size_t)P * a.bytes;
+  }
+  HIP_TRY(h, launch_permute(t, h->perm.as<uint32_t>(), P, true, h->stream));
+  // the rows of one buffer are contiguous in both places: one copy per buffer
+  off = 0;
+  for (size_t i = 0; i < sizeof(arrs) / sizeof(arrs[0]);) {
+    size_t j = i, bytes = 0;
+    while (j < sizeof(arrs) / sizeof(arrs[0]) && arrs[j].buf == arrs[i].buf)
+      bytes += (size_t)P * arrs[j++].bytes;
+    HIP_TRY(h, hipMemcpyAsync(arrs[i].buf->p, h->unperm.as<unsigned char>() + off, bytes,
+                              hipMemcpyDeviceToDevice, h->stream));
+    off += bytes;
+    i = j;
+  }
   return YODA_OK;
 }
 
@@ -449,7 +535,7 @@ int finalize(yoda_t* h, int mode, const uint32_t* counts, const int64_t* best,
                                 h->ties_out.as<uint32_t>(), h->stream));
     }
   }
-  return YODA_OK;
+  return unpermute_outputs(h);
 }
 
 bool is_pow2_le16(uint32_t k) { return k == 1 || k == 2 || k == 4 || k == 8 || k == 16; }
@@ -588,7 +674,13 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
               nd->card_bandwidth[b] == nd->card_bandwidth[a] &&
               nd->card_core[b] == nd->card_core[a] && nd->card_power[b] == nd->card_power[a];
       }
-      hd.flags = (uni && !(flags & YODA_UPLOAD_NO_UNIFORM)) ? kNodeUniform4 : 0u;
+      bool uni_total = uni;
+      for (uint32_t j = 1; j < cnt; ++j)
+        uni_total = uni_total && nd->card_total_memory[(size_t)i * KS + j] ==
+                                     nd->card_total_memory[(size_t)i * KS];
+      hd.flags = 0u;
+      if (uni && !(flags & YODA_UPLOAD_NO_UNIFORM))
+        hd.flags = kNodeUniform4 | (uni_total ? kNodeUniformTotal : 0u);
       if (path == Path::U64) {
         hd.static_score = stat[i];
       } else {
@@ -755,6 +847,7 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     h->has_pods = true;
     h->ran = false;
     h->phase1_done = false;
+    h->ordered = false;
     h->pods_diskio = pd->rio != nullptr && pd->rcpu != nullptr;
     return YODA_OK;
   } catch (const std::bad_alloc&) {
@@ -775,6 +868,7 @@ int yoda_run(yoda_t* h, int mode, uint32_t flags) {
   int rc = prepare_run(h, mode);
   if (rc) return rc;
   try {
+    if ((rc = order_pods(h, mode))) return rc;
     if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>()))) return rc;
     if ((rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->best.as<int64_t>(),
                      h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>())))
@@ -844,6 +938,7 @@ int yoda_download_bitmask(yoda_t* h, uint32_t* words, uint64_t n_words) {
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, h->bitmask_t.ensure(need * 4));
   HIP_TRY(h, launch_bitmask_transpose(h->bitmask.as<uint32_t>(), W, h->n_pods,
+                                      h->ordered ? h->perm.as<uint32_t>() : nullptr,
                                       h->bitmask_t.as<uint32_t>(), h->stream));
   HIP_TRY(h, hipMemcpyAsync(words, h->bitmask_t.p, need * 4, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
@@ -870,6 +965,7 @@ int yoda_score_rows(yoda_t* h, int mode, uint32_t* bitmask_out, uint64_t n_bitma
       HIP_TRY(h, hipMemsetAsync(h->rows.p, 0xff, (size_t)N * P * 8, h->stream));  // -1
       rows = h->rows.as<int64_t>();
     }
+    if ((rc = order_pods(h, mode))) return rc;
     if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>()))) return rc;
     if ((rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->best.as<int64_t>(),
                      h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(),
@@ -883,7 +979,8 @@ int yoda_score_rows(yoda_t* h, int mode, uint32_t* bitmask_out, uint64_t n_bitma
     h->ran_bitmask = mode == YODA_MODE_SCV;
     h->last_mode = mode;
     if (rows) {
-      HIP_TRY(h, launch_rows_transpose(rows, N, P, h->rows_t.as<int64_t>(), h->stream));
+      HIP_TRY(h, launch_rows_transpose(rows, N, P, h->ordered ? h->perm.as<uint32_t>() : nullptr,
+                                       h->rows_t.as<int64_t>(), h->stream));
       HIP_TRY(h, hipMemcpyAsync(scores_out, h->rows_t.p, (size_t)N * P * 8,
                                 hipMemcpyDeviceToHost, h->stream));
     }
@@ -918,6 +1015,7 @@ int yoda_shard_phase1(yoda_t* h, int mode, uint64_t* d_maxima, uint32_t* d_count
   if (rc) return rc;
   if (!d_maxima || !d_counts) return fail(h, YODA_ERR_INVALID_ARG, "NULL exchange buffer");
   try {
+    if ((rc = order_pods(h, mode))) return rc;
     if ((rc = phase1(h, mode, d_maxima, d_counts))) return rc;
     h->phase1_done = true;
     h->ran = false;
@@ -990,6 +1088,12 @@ int yoda_shard_overflow_count(yoda_t* h, uint32_t* n_pods) {
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, hipMemcpyAsync(n_pods, h->n_flagged.p, 4, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return YODA_OK;
+}
+
+int yoda_set_pod_order(yoda_t* h, int enable) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  h->order_enabled = enable != 0;
   return YODA_OK;
 }
 

@@ -136,17 +136,28 @@ __global__ __launch_bounds__(kBlock) void k1_filter_maxima(
       nz += hd.zero_total;
       // qualifying cards (collection.go:46) = real cards with free >= m, if clock >= c
       if (ck.v[0] >= c) {
-        const Group<T, K> to = load_group<T, K>(rec + R::off(kTotal, K));
         uint32_t any = 0;
+        if (hd.flags & kNodeUniformTotal) {
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-          const uint32_t q = ((hd.real_mask >> j) & 1u) & (uint32_t)(fr.v[j] >= m);
-          mx[kMaxFree] = fmax_t(mx[kMaxFree], q ? fr.v[j] : T(0));
-          mx[kMaxTotal] = fmax_t(mx[kMaxTotal], q ? to.v[j] : T(0));
-          any |= q;
+          for (int j = 0; j < K; ++j) {
+            const uint32_t q = ((hd.real_mask >> j) & 1u) & (uint32_t)(fr.v[j] >= m);
+            mx[kMaxFree] = fmax_t(mx[kMaxFree], q ? fr.v[j] : T(0));
+            any |= q;
+          }
+        } else {
+          const Group<T, K> to = load_group<T, K>(rec + R::off(kTotal, K));
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            const uint32_t q = ((hd.real_mask >> j) & 1u) & (uint32_t)(fr.v[j] >= m);
+            mx[kMaxFree] = fmax_t(mx[kMaxFree], q ? fr.v[j] : T(0));
+            mx[kMaxTotal] = fmax_t(mx[kMaxTotal], q ? to.v[j] : T(0));
+            any |= q;
+          }
         }
         if (any) {
           const T* g = reinterpret_cast<const T*>(rec);
+          if (hd.flags & kNodeUniformTotal)
+            mx[kMaxTotal] = fmax_t(mx[kMaxTotal], g[R::off(kTotal, K) / sizeof(T)]);
           mx[kMaxBw] = fmax_t(mx[kMaxBw], g[R::off(kBandwidth, K) / sizeof(T)]);
           mx[kMaxClock] = fmax_t(mx[kMaxClock], ck.v[0]);
           mx[kMaxCore] = fmax_t(mx[kMaxCore], g[R::off(kCore, K) / sizeof(T)]);
@@ -347,17 +358,27 @@ struct Scorer<Path::N32> {
       const float* f32 = reinterpret_cast<const float*>(rec + n32_f32_off(0, K));
       const Group<double, K> frd = load_group<double, K>(rec + n32_f64_off(kF64Free, K));
       const Group<double, K> tod = load_group<double, K>(rec + n32_f64_off(kF64Total, K));
-      const uint32_t shared = (uint32_t)(f32[kF32Bandwidth * K] * r_bw) +
-                              (uint32_t)(f32[kF32Clock * K] * r_bw) +
-                              2u * (uint32_t)(f32[kF32Core * K] * r_core) +
-                              (uint32_t)(f32[kF32Power * K] * r_pow);
+      uint32_t shared = (uint32_t)(f32[kF32Bandwidth * K] * r_bw) +
+                        (uint32_t)(f32[kF32Clock * K] * r_bw) +
+                        2u * (uint32_t)(f32[kF32Core * K] * r_core) +
+                        (uint32_t)(f32[kF32Power * K] * r_pow);
       uint32_t nq = 0, mem = 0;
+      if (hd->flags & kNodeUniformTotal) {
+        shared += (uint32_t)(tod.v[0] * r_tot);
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const uint32_t q = ((hd->real_mask >> j) & 1u) & (uint32_t)(fr.v[j] >= m);
-        const uint32_t t = 3u * (uint32_t)(frd.v[j] * r_free) + (uint32_t)(tod.v[j] * r_tot);
-        mem += q ? t : 0u;
-        nq += q;
+        for (int j = 0; j < K; ++j) {
+          const uint32_t q = ((hd->real_mask >> j) & 1u) & (uint32_t)(fr.v[j] >= m);
+          mem += q ? 3u * (uint32_t)(frd.v[j] * r_free) : 0u;
+          nq += q;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const uint32_t q = ((hd->real_mask >> j) & 1u) & (uint32_t)(fr.v[j] >= m);
+          const uint32_t t = 3u * (uint32_t)(frd.v[j] * r_free) + (uint32_t)(tod.v[j] * r_tot);
+          mem += q ? t : 0u;
+          nq += q;
+        }
       }
       const uint32_t basic = (ck0 >= c) ? nq * shared + mem : 0u;  // algorithm.go:271
       return (double)basic + stat;
@@ -983,11 +1004,14 @@ __global__ __launch_bounds__(kBlock) void k_reduce3(const int64_t* __restrict__ 
 // Bitmask [W][P] (device, coalesced for the kernels) -> [P][W] (host API layout).
 __global__ __launch_bounds__(kBlock) void k_bitmask_transpose(const uint32_t* __restrict__ in,
                                                               uint32_t W, uint32_t n_pods,
+                                                              const uint32_t* __restrict__ perm,
                                                               uint32_t* __restrict__ out) {
   const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (t >= (uint64_t)W * n_pods) return;
   const uint32_t p = (uint32_t)(t / W), w = (uint32_t)(t % W);
-  out[t] = in[(size_t)w * n_pods + p];
+  // row p of the output belongs to caller pod perm[p] when the run was ordered
+  const uint32_t q = perm ? perm[p] : p;
+  out[(size_t)q * W + w] = in[(size_t)w * n_pods + p];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1176,18 +1200,21 @@ hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t ch
 // rows [N][P] (coalesced for the kernels) -> [P][N] (host API layout).
 __global__ __launch_bounds__(kBlock) void k_rows_transpose(const int64_t* __restrict__ in,
                                                            uint32_t n_nodes, uint32_t n_pods,
+                                                           const uint32_t* __restrict__ perm,
                                                            int64_t* __restrict__ out) {
   const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (t >= (uint64_t)n_nodes * n_pods) return;
   const uint32_t p = (uint32_t)(t / n_nodes), n = (uint32_t)(t % n_nodes);
-  out[t] = in[(size_t)n * n_pods + p];
+  const uint32_t q = perm ? perm[p] : p;
+  out[(size_t)q * n_nodes + n] = in[(size_t)n * n_pods + p];
 }
 
 hipError_t launch_rows_transpose(const int64_t* in, uint32_t n_nodes, uint32_t n_pods,
-                                 int64_t* out, hipStream_t s) {
+                                 const uint32_t* perm, int64_t* out, hipStream_t s) {
   const uint64_t total = (uint64_t)n_nodes * n_pods;
   dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
-  hipLaunchKernelGGL(k_rows_transpose, grid, dim3(kBlock), 0, s, in, n_nodes, n_pods, out);
+  hipLaunchKernelGGL(k_rows_transpose, grid, dim3(kBlock), 0, s, in, n_nodes, n_pods, perm,
+                     out);
   return hipGetLastError();
 }
 
@@ -1252,10 +1279,10 @@ hipError_t launch_reduce3(const Partials& part, uint32_t C, const uint32_t* flag
 }
 
 hipError_t launch_bitmask_transpose(const uint32_t* in, uint32_t W, uint32_t n_pods,
-                                    uint32_t* out, hipStream_t s) {
+                                    const uint32_t* perm, uint32_t* out, hipStream_t s) {
   const uint64_t total = (uint64_t)W * n_pods;
   dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
-  hipLaunchKernelGGL(k_bitmask_transpose, grid, dim3(kBlock), 0, s, in, W, n_pods, out);
+  hipLaunchKernelGGL(k_bitmask_transpose, grid, dim3(kBlock), 0, s, in, W, n_pods, perm, out);
   return hipGetLastError();
 }
 

@@ -41,6 +41,9 @@ struct alignas(16) NodeHdrF {
 // model per node, the common case): K1 takes those maxima once per node and K2 computes
 // their quotients once per node (N32 path).
 constexpr uint32_t kNodeUniform4 = 1u;
+// ... and also the same TotalMemory on every real card: the total-memory maximum and
+// quotient are per node too.
+constexpr uint32_t kNodeUniformTotal = 2u;
 static_assert(sizeof(NodeHdrF) == 32, "NodeHdrF layout");
 
 // Generic (exact uint64) path: same shape with uint64 card fields.
@@ -128,6 +131,15 @@ struct Partials {
   double* low_f;       // [C][P]
   int64_t* low_i;      // [C][P]
   uint32_t* err;       // [C][P] exact normalize: score out of range seen
+};
+
+// Per-pod array table for the batch permutation (yoda_order.hip).
+constexpr int kPermArrays = 16;
+struct PermTable {
+  const void* src[kPermArrays];
+  void* dst[kPermArrays];
+  uint32_t bytes[kPermArrays];
+  uint32_t n;
 };
 
 }  // namespace yoda

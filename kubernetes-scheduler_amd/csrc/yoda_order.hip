@@ -1,0 +1,87 @@
+// yoda_order.hip — batch pod ordering for the independent-cycle paths.
+//
+// The pods of a batch are independent scheduling cycles (the reference runs one
+// scheduleOne per pod), so the kernels may visit them in any order.  K1 and K2 map lane =
+// pod and skip a node when no lane of the wave is feasible on it; a random batch keeps
+// every wave busy on every node.  Sorting the batch by the Filter's inputs (clock, number,
+// memory) groups pods that fail together, so whole waves skip: ~43% of (wave, node) pairs
+// stay busy on config 3 instead of 100%.  The permutation is
+// computed on the device inside every run (its cost is in the measured step), the pod
+// arrays are gathered into sorted order, and every per-pod output is scattered back before
+// it leaves the library — results do not depend on the order.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstdint>
+
+#include "yoda_layout.h"
+
+namespace yoda {
+
+// key = clock (24 bits, clamped) | number (8 bits) | memory (32 bits): ascending clock puts
+// the K1 `clock >= c` skips together too.  Any key is correct; this one is just fast.
+__global__ __launch_bounds__(kBlock) void k_order_keys(const uint64_t* __restrict__ number,
+                                                       const uint64_t* __restrict__ m_u,
+                                                       const uint64_t* __restrict__ c_u,
+                                                       uint32_t n_pods, uint64_t* __restrict__ keys,
+                                                       uint32_t* __restrict__ idx) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= n_pods) return;
+  const uint64_t c = c_u[p] < 0xffffffull ? c_u[p] : 0xffffffull;
+  const uint64_t n = number[p] < 0xffull ? number[p] : 0xffull;
+  const uint64_t m = m_u[p] < 0xffffffffull ? m_u[p] : 0xffffffffull;
+  keys[p] = (c << 40) | (n << 32) | m;
+  idx[p] = p;
+}
+
+// gather (dst[i] = src[perm[i]]) or scatter (dst[perm[i]] = src[i]) of up to kPermArrays
+// per-pod arrays of 4 or 8 bytes; grid.y = array.
+__global__ __launch_bounds__(kBlock) void k_permute(PermTable t, const uint32_t* __restrict__ perm,
+                                                    uint32_t n_pods, int scatter) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t a = blockIdx.y;
+  if (i >= n_pods || a >= t.n) return;
+  const uint32_t j = perm[i];
+  const uint32_t s = scatter ? i : j, d = scatter ? j : i;
+  if (t.bytes[a] == 8)
+    static_cast<uint64_t*>(t.dst[a])[d] = static_cast<const uint64_t*>(t.src[a])[s];
+  else
+    static_cast<uint32_t*>(t.dst[a])[d] = static_cast<const uint32_t*>(t.src[a])[s];
+}
+
+// Scratch for the sort: keys[2][P] u64, idx[2][P] u32, then hipcub's temp storage.
+size_t order_scratch_bytes(uint32_t n_pods) {
+  size_t temp = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const uint64_t*)nullptr,
+                                           (uint64_t*)nullptr, (const uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (int)n_pods);
+  return 16ull * n_pods + 8ull * n_pods + 256 + temp;
+}
+
+// perm[i] = the original index of the i-th pod in sorted order.
+hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
+                             uint32_t n_pods, void* scratch, size_t scratch_bytes,
+                             uint32_t* perm, hipStream_t s) {
+  unsigned char* b = static_cast<unsigned char*>(scratch);
+  uint64_t* keys_in = reinterpret_cast<uint64_t*>(b);
+  uint64_t* keys_out = keys_in + n_pods;
+  uint32_t* idx_in = reinterpret_cast<uint32_t*>(keys_out + n_pods);
+  unsigned char* temp = b + ((16ull * n_pods + 4ull * n_pods + 255) / 256 * 256);
+  size_t temp_bytes = scratch_bytes - (size_t)(temp - b);
+  hipLaunchKernelGGL(k_order_keys, dim3((n_pods + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                     number, m_u, c_u, n_pods, keys_in, idx_in);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, perm,
+                                            (int)n_pods, 0, 64, s);
+}
+
+hipError_t launch_permute(const PermTable& t, const uint32_t* perm, uint32_t n_pods, bool scatter,
+                          hipStream_t s) {
+  if (t.n == 0 || n_pods == 0) return hipSuccess;
+  dim3 grid((n_pods + kBlock - 1) / kBlock, t.n);
+  hipLaunchKernelGGL(k_permute, grid, dim3(kBlock), 0, s, t, perm, n_pods, scatter ? 1 : 0);
+  return hipGetLastError();
+}
+
+}  // namespace yoda

@@ -52,6 +52,7 @@ _SIGS = {
     "yoda_shard_finalize": ([_vp, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "yoda_shard_overflow_count": ([_vp, C.POINTER(C.c_uint32)], C.c_int),
     "yoda_profile": ([_vp, C.c_int], C.c_int),
+    "yoda_set_pod_order": ([_vp, C.c_int], C.c_int),
     "yoda_profile_read": ([_vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                            C.POINTER(C.c_uint32)], C.c_int),
     "yoda_greedy": ([_vp, C.POINTER(CPodSoA), C.c_int, _u32, C.POINTER(C.c_int32)], C.c_int),
@@ -229,6 +230,11 @@ class Yoda:
             return w.value, f.value, {"window_ms": t[0], "resolve_ms": t[1],
                                       "fallback_ms": t[2]}
         return w.value, f.value
+
+    def set_pod_order(self, enable: bool = True):
+        """Sort Mode-A batches on the device before K1/K2 (default on); results are returned
+        in the caller's pod order either way."""
+        self._check(lib().yoda_set_pod_order(self._h, 1 if enable else 0), "yoda_set_pod_order")
 
     def profile(self, enable: bool = True):
         self._check(lib().yoda_profile(self._h, 1 if enable else 0), "yoda_profile")

@@ -202,6 +202,38 @@ def test_bitmask_matches_oracle(dev):
         np.testing.assert_array_equal(bits[p], feas)
 
 
+@pytest.mark.parametrize("path", ["n32", "f64", "u64"])
+def test_pod_order_is_invisible(dev, path):
+    """The device-side batch sort (yoda_order.hip) changes only the visiting order: picks,
+    statuses, ties, top scores, maxima, feasible counts, the bitmask and the score rows must
+    be identical with it on and off, and equal to the oracle."""
+    nodes, pods = synth.make_config(2, pods=700, nodes=2500)
+    kw = {"n32": {}, "f64": {"force_f64": True}, "u64": {"force_generic": True}}[path]
+    want = oracle.schedule(nodes, pods, MODE_SCV, threads=8)
+    outs = []
+    for order in (True, False):
+        dev.set_pod_order(order)
+        dev.upload_nodes(nodes, **kw)
+        got = dev.eval(pods, MODE_SCV)
+        assert_same(got, want)
+        dev.upload_pods(pods)
+        dev.run(MODE_SCV, bitmask=True)
+        words = dev.download_bitmask()
+        dev.upload_pods(pods.slice(0, 200))
+        feas, rows = dev.score_rows(MODE_SCV)
+        outs.append((got, words, feas, rows))
+    dev.set_pod_order(True)
+    (a, wa, fa, ra), (b, wb, fb, rb) = outs
+    for f in ("pick", "status", "n_ties", "top_score", "maxima", "n_feasible"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+    np.testing.assert_array_equal(wa, wb)
+    np.testing.assert_array_equal(fa, fb)
+    np.testing.assert_array_equal(ra, rb)
+    for p in (0, 77, 199):
+        _, f, raw, _ = oracle.pod_detail(nodes, pods, p)
+        np.testing.assert_array_equal(ra[p][f], raw[f])
+
+
 def test_mode_b_kats(dev):
     from test_oracle import KAT2
     pod = po.Pod(rio=10.0, rcpu=100)
@@ -348,11 +380,14 @@ def test_uniform_node_factoring(dev):
     k = nodes.card_clock.shape[1]
     nodes.card_clock[mixed] = synth.CLOCKS[rng.integers(0, 3, size=(mixed.sum(), k))]
     nodes.card_bandwidth[mixed[:, None] & (rng.random(nodes.card_bandwidth.shape) < 0.3)] = 1200
+    # one model but mixed TotalMemory: the uniform branch without the per-node total
+    mixed_total = ~mixed & (rng.random(nodes.n_nodes) < 0.4)
+    nodes.card_total_memory[mixed_total, 0] += 4096
     nodes = nodes.normalized()
     want = oracle.schedule(nodes, pods, MODE_SCV, threads=8)
-    for no_uniform in (False, True):
-        dev.upload_nodes(nodes, no_uniform=no_uniform)
-        assert dev.path == "n32"
+    for no_uniform, force_f64 in ((False, False), (True, False), (False, True)):
+        dev.upload_nodes(nodes, no_uniform=no_uniform, force_f64=force_f64)
+        assert dev.path == ("f64" if force_f64 else "n32")
         assert_same(dev.eval(pods, MODE_SCV), want)
         dev.upload_pods(pods.slice(0, 16))
         feas, rows = dev.score_rows(MODE_SCV)
