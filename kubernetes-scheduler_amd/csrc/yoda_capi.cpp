@@ -19,9 +19,10 @@
 
 namespace yoda {
 // launchers (yoda_kernels.hip)
-hipError_t launch_k1(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
-                     uint32_t chunk_nodes, uint32_t C, const PodParams& pp, uint32_t n_pods,
-                     const Partials& part, uint32_t* bitmask, hipStream_t s);
+hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigned char* sum,
+                     uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
+                     uint32_t n_pods, const Partials& part, uint64_t* bm, uint32_t bm_stride,
+                     hipStream_t s);
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uint64_t* maxima,
                           uint32_t* counts, hipStream_t s);
 hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
@@ -29,8 +30,8 @@ hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, fl
 hipError_t launch_k2(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
                      const double* rcp, const float* rcp32, uint32_t n_pods,
-                     const uint32_t* bitmask, const Partials& part, int64_t* rows,
-                     hipStream_t s);
+                     const uint64_t* bm, uint32_t bm_stride, const Partials& part,
+                     int64_t* rows, hipStream_t s);
 hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
                             uint32_t C, const PodParams& pp, uint32_t n_pods, const Partials& part,
                             int64_t* rows, hipStream_t s);
@@ -50,26 +51,28 @@ hipError_t launch_finalize(const uint32_t* counts, const int64_t* best, const ui
                            uint32_t* flagged, uint32_t* n_flagged, hipStream_t s);
 hipError_t launch_k3(int K, const unsigned char* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
                      uint32_t C, const PodParams& pp, const uint64_t* maxima, uint32_t n_pods,
-                     const uint32_t* bitmask, const uint32_t* flagged, const uint32_t* n_flagged,
+                     const uint64_t* bm, uint32_t bm_stride, const uint32_t* flagged,
+                     const uint32_t* n_flagged,
                      const int64_t* best, const int64_t* low, const Partials& part,
                      uint32_t max_flagged, hipStream_t s);
 hipError_t launch_reduce3(const Partials& part, uint32_t C, const uint32_t* flagged,
                           const uint32_t* n_flagged, uint32_t max_flagged, uint32_t node_offset,
                           int32_t* pick, int32_t* status, uint32_t* ties, hipStream_t s);
-hipError_t launch_bitmask_transpose(const uint32_t* in, uint32_t W, uint32_t n_pods,
-                                    const uint32_t* perm, uint32_t* out, hipStream_t s);
+hipError_t launch_bitmask_transpose(const uint64_t* bm, uint32_t bm_stride, uint32_t n_nodes,
+                                    uint32_t W, uint32_t n_pods, const uint32_t* perm,
+                                    uint32_t* out, hipStream_t s);
 int kernel_capacity(int K, Path path, int which, int mode_diskio);
 hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                           uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                           const double* rcp, const float* rcp32, uint32_t n_pods,
-                          const uint32_t* bitmask, const Partials& part, double* tk_s,
-                          uint32_t* tk_i, hipStream_t s);
+                          const uint64_t* bm, uint32_t bm_stride, const Partials& part,
+                          double* tk_s, uint32_t* tk_i, hipStream_t s);
 hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t C,
                              uint32_t n_pods, uint32_t node_offset, double* out_s,
                              uint32_t* out_i, hipStream_t s);
 hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32_t* node,
                              const uint64_t* value, const uint64_t* card_number, uint32_t count,
-                             hipStream_t s);
+                             unsigned char* sum, uint32_t sum_stride, hipStream_t s);
 int topk_k();
 size_t order_scratch_bytes(uint32_t n_pods);
 hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
@@ -158,6 +161,8 @@ struct yoda_handle {
   uint32_t n_nodes = 0, node_offset = 0;
   DevBuf nodes;     // fast or generic records
   DevBuf nodes_b;   // Mode B records
+  DevBuf k1sum;     // K1 node summaries (N32 path, yoda_layout.h K1SumWord)
+  bool has_k1sum = false;
   std::vector<unsigned char> host_records;  // kept for alloc updates (greedy)
   std::vector<uint64_t> h_total_sum, h_free_sum, h_alloc, h_card_number;
 
@@ -212,7 +217,7 @@ struct yoda_handle {
 
   ~yoda_handle() {
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&nodes,     &nodes_b,   &pod_blob,   &maxima,       &counts,
+    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &pod_blob,   &maxima,       &counts,
                      &pod_sorted, &perm,     &order_scratch, &unperm,
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
@@ -291,7 +296,6 @@ void plan_chunks(yoda_t* h, int mode, uint32_t n_pods, uint32_t n_nodes) {
 
 int ensure_state(yoda_t* h, uint32_t P) {
   const size_t CP = (size_t)std::max(h->C1, h->C2) * P;
-  const size_t W = (h->n_nodes + 31) / 32;
   HIP_TRY(h, h->maxima.ensure(6 * (size_t)P * 8));
   HIP_TRY(h, h->counts.ensure(2 * (size_t)P * 4));
   HIP_TRY(h, h->rcp.ensure(5 * (size_t)P * 8));
@@ -305,7 +309,8 @@ int ensure_state(yoda_t* h, uint32_t P) {
   HIP_TRY(h, h->ties_out.ensure((size_t)P * 4));
   HIP_TRY(h, h->flagged.ensure((size_t)P * 4));
   HIP_TRY(h, h->n_flagged.ensure(16));
-  HIP_TRY(h, h->bitmask.ensure(W * P * 4));
+  // [wave][node] u64 masks (yoda_layout.h), +8 words: K2 reads masks in groups of 8
+  HIP_TRY(h, h->bitmask.ensure(((size_t)(P + 63) / 64 * bm_row(h->n_nodes) + 8) * 8));
   HIP_TRY(h, h->p_max_u.ensure(6 * CP * 8));
   if (h->generic) {
     HIP_TRY(h, h->p_best_i.ensure(CP * 8));
@@ -455,8 +460,10 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts) {
   hipEvent_t e0 = h->profiling ? h->next_event() : nullptr;
   hipEvent_t e1 = h->profiling ? h->next_event() : nullptr;
   if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
-  HIP_TRY(h, launch_k1(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes, h->chunk1,
-                       h->C1, pod_params(h), P, part, h->bitmask.as<uint32_t>(), h->stream));
+  HIP_TRY(h, launch_k1(h->K, h->path, h->nodes.as<unsigned char>(),
+                       h->has_k1sum ? h->k1sum.as<unsigned char>() : nullptr, h->n_nodes,
+                       h->chunk1, h->C1, pod_params(h), P, part, h->bitmask.as<uint64_t>(),
+                       bm_row(h->n_nodes), h->stream));
   if (e1) {
     HIP_TRY(h, hipEventRecord(e1, h->stream));
     h->ev_k1.emplace_back(e0, e1);
@@ -493,8 +500,8 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, int64_t* best, uint32_t*
   } else {
     HIP_TRY(h, launch_k2(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes,
                          h->chunk2, h->C2, pod_params(h), maxima, h->rcp.as<double>(),
-                         h->rcp32.as<float>(), P, h->bitmask.as<uint32_t>(), part, rows,
-                         h->stream));
+                         h->rcp32.as<float>(), P, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
+                         part, rows, h->stream));
     is_f64 = !h->generic;
   }
   if (e1) {
@@ -527,7 +534,8 @@ int finalize(yoda_t* h, int mode, const uint32_t* counts, const int64_t* best,
                     "on the sharded path yet; evaluate on a single handle");
       Partials part = partials(h);
       HIP_TRY(h, launch_k3(h->K, h->nodes.as<unsigned char>(), h->n_nodes, h->chunk2, h->C2,
-                           pod_params(h), h->maxima.as<uint64_t>(), P, h->bitmask.as<uint32_t>(),
+                           pod_params(h), h->maxima.as<uint64_t>(), P, h->bitmask.as<uint64_t>(),
+                           bm_row(h->n_nodes),
                            h->flagged.as<uint32_t>(), h->n_flagged.as<uint32_t>(), best, low,
                            part, nfl, h->stream));
       HIP_TRY(h, launch_reduce3(part, h->C2, h->flagged.as<uint32_t>(), h->n_flagged.as<uint32_t>(),
@@ -656,6 +664,10 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     // Build records.
     const size_t stride = path == Path::N32 ? n32_stride(K) : node_stride(K);
     std::vector<unsigned char> rec((size_t)std::max<uint32_t>(N, 1) * stride, 0);
+    // K1 node summaries (N32 path): the facts the block-classified K1 reads per node
+    const bool want_sum = path == Path::N32;
+    const size_t sstride = k1sum_stride(K);
+    std::vector<uint32_t> sum(want_sum ? (size_t)std::max<uint32_t>(N, 1) * sstride / 4 : 0, 0);
     for (uint32_t i = 0; i < N; ++i) {
       unsigned char* r = rec.data() + (size_t)i * stride;
       uint32_t hm = 0;
@@ -688,6 +700,32 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
         std::memcpy(&hd.static_score, &sd, 8);
       }
       std::memcpy(r, &hd, sizeof(hd));
+      if (want_sum) {
+        uint32_t* s = sum.data() + (size_t)i * sstride / 4;
+        const size_t a = (size_t)i * KS;
+        s[kSumCnLo] = (uint32_t)hd.card_number;
+        s[kSumCnHi] = (uint32_t)(hd.card_number >> 32);
+        s[kSumMeta] = ((hd.flags & kNodeUniform4) ? kSumUni4 : 0u) |
+                      ((hd.flags & kNodeUniformTotal) ? kSumUniTotal : 0u) |
+                      (zt[i] ? kSumZeroTotal : 0u) | ((uint32_t)__builtin_popcount(hm) << 8);
+        if (cnt > 0) {  // the model values of card 0 (all cards under kSumUni4)
+          s[kSumClock] = (uint32_t)nd->card_clock[a];
+          s[kSumTotal] = (uint32_t)nd->card_total_memory[a];
+          s[kSumBw] = (uint32_t)nd->card_bandwidth[a];
+          s[kSumCore] = (uint32_t)nd->card_core[a];
+          s[kSumPower] = (uint32_t)nd->card_power[a];
+        }
+        uint32_t mrf1 = 0, nhf = 0;
+        uint32_t hfs[YODA_MAX_CARDS];
+        for (uint32_t j = 0; j < cnt; ++j) {  // N32: free <= 0xFFFFFFFE, so free + 1 fits
+          const uint32_t f1 = (uint32_t)nd->card_free_memory[a + j] + 1u;
+          mrf1 = std::max(mrf1, f1);
+          if (nd->card_healthy[a + j]) hfs[nhf++] = f1;
+        }
+        std::sort(hfs, hfs + nhf, [](uint32_t x, uint32_t y) { return x > y; });
+        s[kSumMrf1] = mrf1;
+        for (uint32_t j = 0; j < nhf; ++j) s[kSumHfs + j] = hfs[j];
+      }
       for (uint32_t j = 0; j < nd->card_count[i]; ++j) {
         const size_t k = (size_t)i * KS + j;
         const uint64_t v[6] = {nd->card_free_memory[k], nd->card_clock[k],
@@ -716,6 +754,11 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     HIP_TRY(h, h->nodes.ensure(rec.size()));
     HIP_TRY(h, hipMemcpyAsync(h->nodes.p, rec.data(), rec.size(), hipMemcpyHostToDevice,
                               h->stream));
+    if (want_sum) {
+      HIP_TRY(h, h->k1sum.ensure(sum.size() * 4));
+      HIP_TRY(h, hipMemcpyAsync(h->k1sum.p, sum.data(), sum.size() * 4, hipMemcpyHostToDevice,
+                                h->stream));
+    }
     const bool diskio = nd->cpu && nd->disk_io;
     if (diskio && N > 0) {
       std::vector<NodeRecB> rb(N);
@@ -740,6 +783,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     if (h->K != K || h->path != path) std::memset(h->cap, 0, sizeof(h->cap));
     h->K = K;
     h->path = path;
+    h->has_k1sum = want_sum && !(flags & YODA_UPLOAD_PER_NODE_K1);
     h->generic = path == Path::U64;
     h->has_nodes = true;
     h->ran = false;
@@ -937,7 +981,8 @@ int yoda_download_bitmask(yoda_t* h, uint32_t* words, uint64_t n_words) {
   if (need == 0) return YODA_OK;
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, h->bitmask_t.ensure(need * 4));
-  HIP_TRY(h, launch_bitmask_transpose(h->bitmask.as<uint32_t>(), W, h->n_pods,
+  HIP_TRY(h, launch_bitmask_transpose(h->bitmask.as<uint64_t>(), bm_row(h->n_nodes), h->n_nodes,
+                                      W, h->n_pods,
                                       h->ordered ? h->perm.as<uint32_t>() : nullptr,
                                       h->bitmask_t.as<uint32_t>(), h->stream));
   HIP_TRY(h, hipMemcpyAsync(words, h->bitmask_t.p, need * 4, hipMemcpyDeviceToHost, h->stream));
@@ -1182,7 +1227,9 @@ struct GreedyState {
     HIP_TRY(h, launch_set_static(h->nodes.as<unsigned char>(), stride,
                                  reinterpret_cast<const uint32_t*>(d),
                                  reinterpret_cast<const uint64_t*>(d + o_val),
-                                 reinterpret_cast<const uint64_t*>(d + o_cn), cnt, h->stream));
+                                 reinterpret_cast<const uint64_t*>(d + o_cn), cnt,
+                                 h->has_k1sum ? h->k1sum.as<unsigned char>() : nullptr,
+                                 k1sum_stride(h->K), h->stream));
     if (marks)
       for (uint32_t n : list) (*marks)[n] = 0;
     list.clear();
@@ -1350,7 +1397,8 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
                                   h->rcp32.as<float>(), h->stream));
           HIP_TRY(h, launch_k2_topk(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk2,
                                     h->C2, pod_params(h), h->rcp.as<double>(),
-                                    h->rcp32.as<float>(), wn, h->bitmask.as<uint32_t>(),
+                                    h->rcp32.as<float>(), wn, h->bitmask.as<uint64_t>(),
+                                    bm_row(N),
                                     partials(h), h->tk_s_part.as<double>(),
                                     h->tk_i_part.as<uint32_t>(), h->stream));
           HIP_TRY(h, launch_topk_merge(h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),

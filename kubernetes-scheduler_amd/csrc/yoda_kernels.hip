@@ -74,16 +74,143 @@ __device__ __forceinline__ uint64_t fmax_t(uint64_t a, uint64_t b) { return umax
 
 // ---------------------------------------------------------------------------------------
 // K1: Filter (PodFitsNumber ∧ PodFitsMemory ∧ PodFitsClock, collection.go:41-44) and the
-// PreScore maxima (CollectMaxValues).  Writes the feasibility bitmask [W][P] and per-chunk
-// partials.  Branch-free in the card loop: a short-circuit `healthy && free >= m` would
+// PreScore maxima (CollectMaxValues).  k1_node evaluates ONE node record for every pod lane
+// of the wave: it returns the lane's feasibility and folds the node into the lane's maxima
+// and counts.  Branch-free in the card loop: a short-circuit `healthy && free >= m` would
 // make every field load conditional and serialise one scalar-load round trip per card.
+template <int K, Path PATH>
+__device__ __forceinline__ bool k1_node(const unsigned char* rec, typename Rec<PATH>::T m,
+                                        typename Rec<PATH>::T c, uint64_t number,
+                                        uint32_t need_mem, uint32_t need_clk,
+                                        typename Rec<PATH>::T (&mx)[6], uint32_t& nf,
+                                        uint32_t& nz) {
+  using R = Rec<PATH>;
+  using T = typename R::T;
+  const NodeHdrG hd = *reinterpret_cast<const NodeHdrG*>(rec);
+  const Group<T, K> fr = load_group<T, K>(rec + R::off(kFree, K));
+  const Group<T, K> ck = load_group<T, K>(rec + R::off(kClock, K));
+  // one GPU model on the node (scalar flag, so the branch is wave-uniform)
+  bool uniform = false;
+  if constexpr (PATH == Path::N32) uniform = (hd.flags & kNodeUniform4) != 0u;
+  uint32_t cm = 0, cc = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint32_t hj = (hd.healthy_mask >> j) & 1u;
+    cm += (uint32_t)(fr.v[j] >= m) & hj;   // CardFitsMemory (filter.go:52-54)
+  }
+  if (uniform) {
+    // every real card has clock ck[0]: CardFitsClock counts all healthy cards or none
+    cc = (ck.v[0] == c) ? (uint32_t)__builtin_popcount(hd.healthy_mask) : 0u;
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      cc += (uint32_t)(ck.v[j] == c) & ((hd.healthy_mask >> j) & 1u);  // filter.go:56-58
+  }
+  const bool feas = (number <= hd.card_number) & (cm >= need_mem) & (cc >= need_clk);
+  if (feas && uniform) {
+    ++nf;
+    nz += hd.zero_total;
+    // qualifying cards (collection.go:46) = real cards with free >= m, if clock >= c
+    if (ck.v[0] >= c) {
+      uint32_t any = 0;
+      if (hd.flags & kNodeUniformTotal) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const uint32_t q = ((hd.real_mask >> j) & 1u) & (uint32_t)(fr.v[j] >= m);
+          mx[kMaxFree] = fmax_t(mx[kMaxFree], q ? fr.v[j] : T(0));
+          any |= q;
+        }
+      } else {
+        const Group<T, K> to = load_group<T, K>(rec + R::off(kTotal, K));
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const uint32_t q = ((hd.real_mask >> j) & 1u) & (uint32_t)(fr.v[j] >= m);
+          mx[kMaxFree] = fmax_t(mx[kMaxFree], q ? fr.v[j] : T(0));
+          mx[kMaxTotal] = fmax_t(mx[kMaxTotal], q ? to.v[j] : T(0));
+          any |= q;
+        }
+      }
+      if (any) {
+        const T* g = reinterpret_cast<const T*>(rec);
+        if (hd.flags & kNodeUniformTotal)
+          mx[kMaxTotal] = fmax_t(mx[kMaxTotal], g[R::off(kTotal, K) / sizeof(T)]);
+        mx[kMaxBw] = fmax_t(mx[kMaxBw], g[R::off(kBandwidth, K) / sizeof(T)]);
+        mx[kMaxClock] = fmax_t(mx[kMaxClock], ck.v[0]);
+        mx[kMaxCore] = fmax_t(mx[kMaxCore], g[R::off(kCore, K) / sizeof(T)]);
+        mx[kMaxPower] = fmax_t(mx[kMaxPower], g[R::off(kPower, K) / sizeof(T)]);
+      }
+    }
+  } else if (feas) {
+    ++nf;
+    nz += hd.zero_total;
+    const Group<T, K> bw = load_group<T, K>(rec + R::off(kBandwidth, K));
+    const Group<T, K> co = load_group<T, K>(rec + R::off(kCore, K));
+    const Group<T, K> pw = load_group<T, K>(rec + R::off(kPower, K));
+    const Group<T, K> to = load_group<T, K>(rec + R::off(kTotal, K));
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if ((fr.v[j] >= m) & (ck.v[j] >= c)) {  // collection.go:46: no health check, >= clock
+        mx[kMaxBw] = fmax_t(mx[kMaxBw], bw.v[j]);
+        mx[kMaxClock] = fmax_t(mx[kMaxClock], ck.v[j]);
+        mx[kMaxCore] = fmax_t(mx[kMaxCore], co.v[j]);
+        mx[kMaxFree] = fmax_t(mx[kMaxFree], fr.v[j]);
+        mx[kMaxPower] = fmax_t(mx[kMaxPower], pw.v[j]);
+        mx[kMaxTotal] = fmax_t(mx[kMaxTotal], to.v[j]);
+      }
+    }
+  }
+  return feas;
+}
+
+__device__ __forceinline__ uint64_t ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & (kWave - 1); }
+__device__ __forceinline__ uint32_t uniform_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+  return (uint64_t)uniform_u32((uint32_t)v) | ((uint64_t)uniform_u32((uint32_t)(v >> 32)) << 32);
+}
+// Wave-wide reductions (every lane gets the result; once per workgroup chunk, not hot).
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, kWave));
+  return uniform_u32(v);
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) { return ~wave_max_u32(~v); }
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    const uint64_t u = (uint64_t)__shfl_xor((unsigned long long)v, o, kWave);
+    v = v > u ? v : u;
+  }
+  return uniform_u64(v);
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) { return ~wave_max_u64(~v); }
+
+// Lane j of (lo, hi) := the 64-bit wave mask b (j wave-uniform).
+__device__ __forceinline__ void set_lane(uint32_t& lo, uint32_t& hi, uint64_t b, uint32_t j) {
+  const bool me = lane_id() == j;
+  lo = me ? (uint32_t)b : lo;
+  hi = me ? (uint32_t)(b >> 32) : hi;
+}
+
+// Stores of the per-(wave, node) feasibility masks: lane j of (lo, hi) holds node nb + j.
+__device__ __forceinline__ void bm_store(uint64_t* __restrict__ bm_row_w, uint32_t nb,
+                                         uint32_t n_end, uint32_t lo, uint32_t hi) {
+  const uint32_t n = nb + lane_id();
+  if (n < n_end) bm_row_w[n] = ((uint64_t)hi << 32) | lo;
+}
+
+// K1, per-node sweep (F64 / U64 record paths): every wave evaluates every node of its chunk
+// with k1_node; the wave's feasibility ballot of node n goes to lane n % 64 of (lo, hi) and
+// 64 nodes' masks are stored with one coalesced store.
 template <int K, Path PATH>
 __global__ __launch_bounds__(kBlock) void k1_filter_maxima(
     const unsigned char* __restrict__ nodes, uint32_t n_nodes, uint32_t chunk_nodes,
     const typename Rec<PATH>::T* __restrict__ m_in, const typename Rec<PATH>::T* __restrict__ c_in,
     const uint64_t* __restrict__ number_in, const uint32_t* __restrict__ need_mem_in,
     const uint32_t* __restrict__ need_clk_in, uint32_t n_pods, uint64_t* __restrict__ pmax,
-    uint32_t* __restrict__ pcnt, uint32_t* __restrict__ bitmask) {
+    uint32_t* __restrict__ pcnt, uint64_t* __restrict__ bm, uint32_t bm_stride) {
   using R = Rec<PATH>;
   using T = typename R::T;
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
@@ -91,9 +218,11 @@ __global__ __launch_bounds__(kBlock) void k1_filter_maxima(
   const uint32_t n0 = chunk * chunk_nodes;
   const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
   const bool live = p < n_pods;
+  if (ballot(live) == 0) return;  // a wave past the batch: no bitmask row, no partials
+  uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
 
   T m = 0, c = 0;
-  uint64_t number = ~0ull;  // padding lanes never fit
+  uint64_t number = ~0ull;
   uint32_t need_mem = 0, need_clk = 0;
   if (live) {
     m = m_in[p];
@@ -105,94 +234,172 @@ __global__ __launch_bounds__(kBlock) void k1_filter_maxima(
   T mx[6];
 #pragma unroll
   for (int f = 0; f < 6; ++f) mx[f] = T(1);  // floor 1 (collection.go:31-38)
-  uint32_t nf = 0, nz = 0, bits = 0;
-
+  uint32_t nf = 0, nz = 0, lo = 0, hi = 0;
   for (uint32_t n = n0; n < n1; ++n) {
-    const unsigned char* rec = nodes + (size_t)n * R::stride(K);
-    const NodeHdrG hd = *reinterpret_cast<const NodeHdrG*>(rec);
-    const Group<T, K> fr = load_group<T, K>(rec + R::off(kFree, K));
-    const Group<T, K> ck = load_group<T, K>(rec + R::off(kClock, K));
-    // one GPU model on the node (scalar flag, so the branch is wave-uniform)
-    bool uniform = false;
-    if constexpr (PATH == Path::N32) uniform = (hd.flags & kNodeUniform4) != 0u;
-    uint32_t cm = 0, cc = 0;
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const uint32_t hj = (hd.healthy_mask >> j) & 1u;
-      cm += (uint32_t)(fr.v[j] >= m) & hj;   // CardFitsMemory (filter.go:52-54)
-    }
-    if (uniform) {
-      // every real card has clock ck[0]: CardFitsClock counts all healthy cards or none
-      cc = (ck.v[0] == c) ? (uint32_t)__builtin_popcount(hd.healthy_mask) : 0u;
-    } else {
-#pragma unroll
-      for (int j = 0; j < K; ++j)
-        cc += (uint32_t)(ck.v[j] == c) & ((hd.healthy_mask >> j) & 1u);  // filter.go:56-58
-    }
-    const bool feas = (number <= hd.card_number) & (cm >= need_mem) & (cc >= need_clk);
-    bits |= (uint32_t)feas << (n & 31u);
-    if (feas && uniform) {
-      ++nf;
-      nz += hd.zero_total;
-      // qualifying cards (collection.go:46) = real cards with free >= m, if clock >= c
-      if (ck.v[0] >= c) {
-        uint32_t any = 0;
-        if (hd.flags & kNodeUniformTotal) {
-#pragma unroll
-          for (int j = 0; j < K; ++j) {
-            const uint32_t q = ((hd.real_mask >> j) & 1u) & (uint32_t)(fr.v[j] >= m);
-            mx[kMaxFree] = fmax_t(mx[kMaxFree], q ? fr.v[j] : T(0));
-            any |= q;
-          }
-        } else {
-          const Group<T, K> to = load_group<T, K>(rec + R::off(kTotal, K));
-#pragma unroll
-          for (int j = 0; j < K; ++j) {
-            const uint32_t q = ((hd.real_mask >> j) & 1u) & (uint32_t)(fr.v[j] >= m);
-            mx[kMaxFree] = fmax_t(mx[kMaxFree], q ? fr.v[j] : T(0));
-            mx[kMaxTotal] = fmax_t(mx[kMaxTotal], q ? to.v[j] : T(0));
-            any |= q;
-          }
-        }
-        if (any) {
-          const T* g = reinterpret_cast<const T*>(rec);
-          if (hd.flags & kNodeUniformTotal)
-            mx[kMaxTotal] = fmax_t(mx[kMaxTotal], g[R::off(kTotal, K) / sizeof(T)]);
-          mx[kMaxBw] = fmax_t(mx[kMaxBw], g[R::off(kBandwidth, K) / sizeof(T)]);
-          mx[kMaxClock] = fmax_t(mx[kMaxClock], ck.v[0]);
-          mx[kMaxCore] = fmax_t(mx[kMaxCore], g[R::off(kCore, K) / sizeof(T)]);
-          mx[kMaxPower] = fmax_t(mx[kMaxPower], g[R::off(kPower, K) / sizeof(T)]);
-        }
-      }
-    } else if (feas) {
-      ++nf;
-      nz += hd.zero_total;
-      const Group<T, K> bw = load_group<T, K>(rec + R::off(kBandwidth, K));
-      const Group<T, K> co = load_group<T, K>(rec + R::off(kCore, K));
-      const Group<T, K> pw = load_group<T, K>(rec + R::off(kPower, K));
-      const Group<T, K> to = load_group<T, K>(rec + R::off(kTotal, K));
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        if ((fr.v[j] >= m) & (ck.v[j] >= c)) {  // collection.go:46: no health check, >= clock
-          mx[kMaxBw] = fmax_t(mx[kMaxBw], bw.v[j]);
-          mx[kMaxClock] = fmax_t(mx[kMaxClock], ck.v[j]);
-          mx[kMaxCore] = fmax_t(mx[kMaxCore], co.v[j]);
-          mx[kMaxFree] = fmax_t(mx[kMaxFree], fr.v[j]);
-          mx[kMaxPower] = fmax_t(mx[kMaxPower], pw.v[j]);
-          mx[kMaxTotal] = fmax_t(mx[kMaxTotal], to.v[j]);
-        }
-      }
-    }
-    if ((n & 31u) == 31u || n + 1 == n1) {
-      if (live) bitmask[(size_t)(n >> 5) * n_pods + p] = bits;
-      bits = 0;
-    }
+    const bool f = k1_node<K, PATH>(nodes + (size_t)n * R::stride(K), m, c, number, need_mem,
+                                    need_clk, mx, nf, nz) && live;
+    const uint64_t b = ballot(f);
+    const int j = (int)(n & 63u);
+    set_lane(lo, hi, b, (uint32_t)j);
+    if (j == 63 || n + 1 == n1) bm_store(bmw, n & ~63u, n1, lo, hi);
   }
   if (!live) return;
 #pragma unroll
   for (int f = 0; f < 6; ++f) pmax[((size_t)f * C + chunk) * n_pods + p] = (uint64_t)mx[f];
   pcnt[((size_t)0 * C + chunk) * n_pods + p] = nf;
   pcnt[((size_t)1 * C + chunk) * n_pods + p] = nz;
+}
+
+// K1, block-classified sweep (N32 path).  The batch is sorted by the Filter's inputs
+// (yoda_order.hip), so the 64 pods of a wave usually share their clock / number labels and
+// span a narrow memory range.  The wave first reduces its pods' thresholds to bounds
+// (max/min of number, scv/memory, scv/clock, card counts needed), then walks its chunk in
+// blocks of 64 nodes with LANE = NODE, reading the node summaries (K1Sum) coalesced, and
+// classifies every node for the whole wave:
+//   NONE  the bounds prove every pod of the wave infeasible (e.g. CardNumber < min number,
+//         or the need_min-th largest healthy free < min memory);
+//   ALL   the bounds prove every pod feasible AND the node's maxima contribution is the same
+//         for every pod (one GPU model, uniform TotalMemory or no qualifying card);
+//   PART  anything else: the node is evaluated exactly for every pod lane with k1_node.
+// NONE and ALL are exact statements about every (pod, node) pair of the block, not
+// approximations: ALL nodes fold their contribution into node-lane maxima that are reduced
+// across the wave once per chunk, and both write their 64-bit masks with one store.
+template <int K>
+__global__ __launch_bounds__(kBlock) void k1_block_n32(
+    const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum,
+    uint32_t n_nodes, uint32_t chunk_nodes, const uint32_t* __restrict__ m_in,
+    const uint32_t* __restrict__ c_in, const uint64_t* __restrict__ number_in,
+    const uint32_t* __restrict__ need_mem_in, const uint32_t* __restrict__ need_clk_in,
+    uint32_t n_pods, uint64_t* __restrict__ pmax, uint32_t* __restrict__ pcnt,
+    uint64_t* __restrict__ bm, uint32_t bm_stride) {
+  constexpr uint32_t SS = k1sum_stride(K);
+  constexpr uint32_t NS = n32_stride(K);
+  const uint32_t lane = lane_id();
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t chunk = blockIdx.y, C = gridDim.y;
+  const uint32_t n0 = chunk * chunk_nodes;
+  const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
+  const bool live = p < n_pods;
+  const uint64_t live_mask = ballot(live);
+  if (live_mask == 0) return;  // a wave past the batch: no bitmask row, no partials
+  uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
+
+  uint32_t m = 0, c = 0, need_mem = 0, need_clk = 0;
+  uint64_t number = ~0ull;
+  if (live) {
+    m = m_in[p];
+    c = c_in[p];
+    number = number_in[p];
+    need_mem = need_mem_in[p];
+    need_clk = need_clk_in[p];
+  }
+  // ---- wave bounds (pm: pods with the scv/memory label, pc: with scv/clock) ----
+  const bool pm = live && need_mem > 0, pc = live && need_clk > 0;
+  const uint64_t pm_mask = ballot(pm), pc_mask = ballot(pc);
+  const bool any_pm = pm_mask != 0, all_pm = pm_mask == live_mask;
+  const bool any_pc = pc_mask != 0, all_pc = pc_mask == live_mask;
+  const uint64_t num_max = wave_max_u64(live ? number : 0ull);
+  const uint64_t num_min = wave_min_u64(live ? number : ~0ull);
+  const uint32_t nm_max = wave_max_u32(pm ? need_mem : 0u);
+  const uint32_t nm_min = wave_min_u32(pm ? need_mem : ~0u);
+  const uint32_t mpm_max = wave_max_u32(pm ? m : 0u);
+  const uint32_t mpm_min = wave_min_u32(pm ? m : ~0u);
+  const uint32_t nc_max = wave_max_u32(pc ? need_clk : 0u);
+  const uint32_t nc_min = wave_min_u32(pc ? need_clk : ~0u);
+  const uint32_t cpc_max = wave_max_u32(pc ? c : 0u);
+  const uint32_t cpc_min = wave_min_u32(pc ? c : ~0u);
+  const uint32_t m_max = wave_max_u32(live ? m : 0u), m_min = wave_min_u32(live ? m : ~0u);
+  const uint32_t c_max = wave_max_u32(live ? c : 0u), c_min = wave_min_u32(live ? c : ~0u);
+  const bool c_uni = cpc_min == cpc_max;
+  // hfs slot of the (1-based) need; a need beyond the K slots has no such card (hfs = 0)
+  const bool hfs_all_ok = nm_max <= (uint32_t)K, hfs_none_ok = nm_min <= (uint32_t)K;
+  const uint32_t hfs_all = kSumHfs + (any_pm && hfs_all_ok ? nm_max - 1u : 0u);
+  const uint32_t hfs_none = kSumHfs + (hfs_none_ok ? nm_min - 1u : 0u);
+
+  uint32_t mx[6];
+#pragma unroll
+  for (int f = 0; f < 6; ++f) mx[f] = 1u;  // floor 1 (collection.go:31-38)
+  uint32_t nf = 0, nz = 0;
+  // node-lane maxima of the ALL nodes (their contribution is the same for every pod lane)
+  uint32_t a_bw = 0, a_ck = 0, a_core = 0, a_free = 0, a_pw = 0, a_tot = 0;
+  uint32_t nf_all = 0, nz_all = 0;
+
+  for (uint32_t nb = n0; nb < n1; nb += kWave) {
+    const uint32_t n = nb + lane;
+    const bool valid = n < n1;
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(sum + (size_t)(valid ? n : nb) * SS);
+    const uint4 w0 = *reinterpret_cast<const uint4*>(s);
+    const uint4 w1 = *reinterpret_cast<const uint4*>(s + 4);
+    const uint32_t pw = s[kSumPower];
+    const uint32_t t_all = s[hfs_all], t_none = s[hfs_none];
+    const uint64_t cn = (uint64_t)w0.x | ((uint64_t)w0.y << 32);
+    const uint32_t ck = w0.z, meta = w0.w, mrf1 = w1.x, tot = w1.y, bw = w1.z, core = w1.w;
+    const bool uni4 = (meta & kSumUni4) != 0u, unit = (meta & kSumUniTotal) != 0u;
+    const uint32_t nh = (meta >> 8) & 0xffu;
+    // PodFitsNumber / PodFitsMemory / PodFitsClock for every pod of the wave at once
+    const bool mem_all = !any_pm || (hfs_all_ok && t_all > mpm_max);
+    const bool mem_none = all_pm && (!hfs_none_ok || t_none <= mpm_min);
+    const bool clk_all = !any_pc || (c_uni && uni4 && ck == cpc_max && nh >= nc_max);
+    const bool clk_none = all_pc && c_uni && uni4 && (ck != cpc_max || nh < nc_min);
+    const bool feas_all = (num_max <= cn) && mem_all && clk_all;
+    const bool feas_none = (num_min > cn) || mem_none || clk_none;
+    // CollectMaxValues card predicate (collection.go:46) on a one-model node:
+    // some card qualifies  <=>  clock >= c  and  max free >= m
+    const bool qual_all = ck >= c_max && mrf1 > m_max;
+    const bool qual_none = ck < c_min || mrf1 <= m_min;
+    const bool is_none = valid && feas_none;
+    const bool is_all =
+        valid && !feas_none && feas_all && uni4 && (qual_none || (qual_all && unit));
+    const uint64_t all_b = ballot(is_all);
+    uint64_t part_b = ballot(valid) & ~all_b & ~ballot(is_none);
+    nf_all += (uint32_t)__builtin_popcountll(all_b);
+    nz_all += (uint32_t)__builtin_popcountll(ballot(is_all && (meta & kSumZeroTotal)));
+    if (is_all && qual_all) {
+      a_bw = max(a_bw, bw);
+      a_ck = max(a_ck, ck);
+      a_core = max(a_core, core);
+      a_free = max(a_free, mrf1 - 1u);
+      a_pw = max(a_pw, pw);
+      a_tot = max(a_tot, tot);
+    }
+    uint32_t lo = is_all ? (uint32_t)live_mask : 0u;
+    uint32_t hi = is_all ? (uint32_t)(live_mask >> 32) : 0u;
+    while (part_b) {  // wave-uniform loop over the nodes the bounds could not decide
+      const int j = __builtin_ctzll(part_b);
+      part_b &= part_b - 1;
+      const bool f = k1_node<K, Path::N32>(nodes + (size_t)(nb + (uint32_t)j) * NS, m, c, number,
+                                           need_mem, need_clk, mx, nf, nz) && live;
+      const uint64_t b = ballot(f);
+      set_lane(lo, hi, b, (uint32_t)j);
+    }
+    bm_store(bmw, nb, n1, lo, hi);
+  }
+  // fold the ALL nodes into every pod lane
+  a_bw = wave_max_u32(a_bw);
+  a_ck = wave_max_u32(a_ck);
+  a_core = wave_max_u32(a_core);
+  a_free = wave_max_u32(a_free);
+  a_pw = wave_max_u32(a_pw);
+  a_tot = wave_max_u32(a_tot);
+  if (!live) return;
+  mx[kMaxBw] = max(mx[kMaxBw], a_bw);
+  mx[kMaxClock] = max(mx[kMaxClock], a_ck);
+  mx[kMaxCore] = max(mx[kMaxCore], a_core);
+  mx[kMaxFree] = max(mx[kMaxFree], a_free);
+  mx[kMaxPower] = max(mx[kMaxPower], a_pw);
+  mx[kMaxTotal] = max(mx[kMaxTotal], a_tot);
+  nf += nf_all;
+  nz += nz_all;
+#pragma unroll
+  for (int f = 0; f < 6; ++f) pmax[((size_t)f * C + chunk) * n_pods + p] = (uint64_t)mx[f];
+  pcnt[((size_t)0 * C + chunk) * n_pods + p] = nf;
+  pcnt[((size_t)1 * C + chunk) * n_pods + p] = nz;
+}
+
+// feasibility of (pod p, node n) in the [wave][node] bitmask
+__device__ __forceinline__ bool bm_bit(const uint64_t* __restrict__ bm, uint32_t bm_stride,
+                                       uint32_t p, uint32_t n) {
+  return (bm[(size_t)(p >> 6) * bm_stride + n] >> (p & 63u)) & 1ull;
 }
 
 // Per-pod merge of K1 chunk partials -> maxima [6][P] and counts [2][P].
@@ -417,7 +624,7 @@ constexpr int kTopK = 8;
 template <int K, Path PATH, int OUT>
 __global__ __launch_bounds__(kBlock) void k2_score(
     const unsigned char* __restrict__ nodes, uint32_t n_nodes, uint32_t chunk_nodes,
-    ScoreArgs args, uint32_t n_pods, const uint32_t* __restrict__ bitmask,
+    ScoreArgs args, uint32_t n_pods, const uint64_t* __restrict__ bm, uint32_t bm_stride,
     double* __restrict__ pbest, uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties,
     double* __restrict__ plow, int64_t* __restrict__ rows, double* __restrict__ tk_s,
     uint32_t* __restrict__ tk_i) {
@@ -426,11 +633,14 @@ __global__ __launch_bounds__(kBlock) void k2_score(
   const uint32_t n0 = chunk * chunk_nodes;
   const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
   const bool live = p < n_pods;
+  if (ballot(live) == 0) return;  // a wave past the batch
+  const uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
+  const uint32_t lane = lane_id();
   Scorer<PATH> sc;
   if (live) sc.load(args, p, n_pods);
   constexpr uint32_t stride = PATH == Path::N32 ? n32_stride(K) : node_stride(K);
   double best = -1.0, low = 1.0e300;
-  uint32_t idx = 0xffffffffu, ties = 0, word = 0;
+  uint32_t idx = 0xffffffffu, ties = 0;
   double ts[OUT == OUT_TOPK ? kTopK : 1];
   uint32_t ti[OUT == OUT_TOPK ? kTopK : 1];
   if constexpr (OUT == OUT_TOPK) {
@@ -440,10 +650,18 @@ __global__ __launch_bounds__(kBlock) void k2_score(
       ti[k] = 0xffffffffu;
     }
   }
-  for (uint32_t n = n0; n < n1; ++n) {
-    if ((n & 31u) == 0u) word = live ? bitmask[(size_t)(n >> 5) * n_pods + p] : 0u;
-    const bool feas = (word >> (n & 31u)) & 1u;
-    if (feas) {
+  // The wave's feasibility masks of 8 nodes come in with one scalar load; a node no pod of
+  // the wave can use costs a scalar compare, a group of 8 such nodes one more.
+  for (uint32_t g = n0; g < n1; g += 8) {
+    const Group<uint64_t, 8> mk = load_group<uint64_t, 8>(
+        reinterpret_cast<const unsigned char*>(bmw + g));
+    if ((mk.v[0] | mk.v[1] | mk.v[2] | mk.v[3] | mk.v[4] | mk.v[5] | mk.v[6] | mk.v[7]) == 0)
+      continue;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+    const uint32_t n = g + (uint32_t)j;
+    if (mk.v[j] == 0 || n >= n1) continue;
+    if ((mk.v[j] >> lane) & 1ull) {
       const double raw = sc.template raw<K>(nodes + (size_t)n * stride);
       if constexpr (OUT == OUT_ROWS) rows[(size_t)n * n_pods + p] = (int64_t)raw;
       if constexpr (OUT == OUT_TOPK) {
@@ -473,6 +691,7 @@ __global__ __launch_bounds__(kBlock) void k2_score(
         }
         low = fmin(low, raw);
       }
+    }
     }
   }
   if (!live) return;
@@ -600,12 +819,19 @@ __global__ __launch_bounds__(kBlock) void k_set_static(unsigned char* __restrict
                                                        const uint32_t* __restrict__ node,
                                                        const uint64_t* __restrict__ value,
                                                        const uint64_t* __restrict__ card_number,
-                                                       uint32_t count) {
+                                                       uint32_t count,
+                                                       unsigned char* __restrict__ sum,
+                                                       uint32_t sum_stride) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= count) return;
   uint64_t* hdr = reinterpret_cast<uint64_t*>(nodes + (size_t)node[t] * stride);
   hdr[0] = value[t];        // static_score bits (f64 on the fast paths, u64 on U64)
   hdr[1] = card_number[t];  // CardNumber
+  if (sum) {                // the K1 summary's copy of CardNumber (words cn_lo, cn_hi)
+    uint32_t* s = reinterpret_cast<uint32_t*>(sum + (size_t)node[t] * sum_stride);
+    s[kSumCnLo] = (uint32_t)card_number[t];
+    s[kSumCnHi] = (uint32_t)(card_number[t] >> 32);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -644,9 +870,9 @@ template <int K, bool ROWS>
 __global__ __launch_bounds__(kBlock) void k2_score_generic(
     const unsigned char* __restrict__ nodes, uint32_t n_nodes, uint32_t chunk_nodes,
     const uint64_t* __restrict__ m_u, const uint64_t* __restrict__ c_u,
-    const uint64_t* __restrict__ maxima, uint32_t n_pods, const uint32_t* __restrict__ bitmask,
-    int64_t* __restrict__ pbest, uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties,
-    int64_t* __restrict__ plow, int64_t* __restrict__ rows) {
+    const uint64_t* __restrict__ maxima, uint32_t n_pods, const uint64_t* __restrict__ bm,
+    uint32_t bm_stride, int64_t* __restrict__ pbest, uint32_t* __restrict__ pidx,
+    uint32_t* __restrict__ pties, int64_t* __restrict__ plow, int64_t* __restrict__ rows) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t chunk = blockIdx.y;
   const uint32_t n0 = chunk * chunk_nodes;
@@ -660,10 +886,14 @@ __global__ __launch_bounds__(kBlock) void k2_score_generic(
     for (int f = 0; f < 6; ++f) M[f] = maxima[(size_t)f * n_pods + p];
   }
   int64_t best = -1, low = kI64Max;
-  uint32_t idx = 0xffffffffu, ties = 0, word = 0;
+  uint32_t idx = 0xffffffffu, ties = 0;
+  if (ballot(live) == 0) return;
+  const uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
+  const uint32_t lane = lane_id();
   for (uint32_t n = n0; n < n1; ++n) {
-    if ((n & 31u) == 0u) word = live ? bitmask[(size_t)(n >> 5) * n_pods + p] : 0u;
-    if ((word >> (n & 31u)) & 1u) {
+    const uint64_t mask = bmw[n];
+    if (mask == 0) continue;
+    if ((mask >> lane) & 1ull) {
       const int64_t s = raw_score_u64<K>(nodes + (size_t)n * node_stride(K), m, c, M);
       if constexpr (ROWS) rows[(size_t)n * n_pods + p] = s;
       if (s > best) {
@@ -920,8 +1150,9 @@ template <int K>
 __global__ __launch_bounds__(kBlock) void k3_exact_normalize(
     const unsigned char* __restrict__ nodes, uint32_t n_nodes, uint32_t chunk_nodes,
     const uint64_t* __restrict__ m_u, const uint64_t* __restrict__ c_u,
-    const uint64_t* __restrict__ maxima, uint32_t n_pods, const uint32_t* __restrict__ bitmask,
-    const uint32_t* __restrict__ flagged, const uint32_t* __restrict__ n_flagged_p,
+    const uint64_t* __restrict__ maxima, uint32_t n_pods, const uint64_t* __restrict__ bm,
+    uint32_t bm_stride, const uint32_t* __restrict__ flagged,
+    const uint32_t* __restrict__ n_flagged_p,
     const int64_t* __restrict__ best_in, const int64_t* __restrict__ low_in,
     int64_t* __restrict__ pbest, uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties,
     uint32_t* __restrict__ perr, uint32_t max_flagged) {
@@ -942,8 +1173,7 @@ __global__ __launch_bounds__(kBlock) void k3_exact_normalize(
   int64_t best = -1;
   uint32_t idx = 0xffffffffu, ties = 0, err = 0;
   for (uint32_t n = n0; n < n1; ++n) {
-    const uint32_t word = bitmask[(size_t)(n >> 5) * n_pods + p];
-    if (!((word >> (n & 31u)) & 1u)) continue;
+    if (!bm_bit(bm, bm_stride, p, n)) continue;
     const int64_t s = raw_score_u64<K>(nodes + (size_t)n * node_stride(K), m, c, M);
     const int64_t norm = (int64_t)((uint64_t)(s - l) * 100u) / d;  // scheduler.go:178
     if (norm < 0 || norm > 100) err = 1;                            // RunScorePlugins check
@@ -1001,9 +1231,12 @@ __global__ __launch_bounds__(kBlock) void k_reduce3(const int64_t* __restrict__ 
   }
 }
 
-// Bitmask [W][P] (device, coalesced for the kernels) -> [P][W] (host API layout).
-__global__ __launch_bounds__(kBlock) void k_bitmask_transpose(const uint32_t* __restrict__ in,
-                                                              uint32_t W, uint32_t n_pods,
+// Bitmask [wave][node] u64 (device, yoda_layout.h) -> [P][W] u32 words (host API layout:
+// word w of pod q, bit b = node 32 w + b).
+__global__ __launch_bounds__(kBlock) void k_bitmask_transpose(const uint64_t* __restrict__ bm,
+                                                              uint32_t bm_stride,
+                                                              uint32_t n_nodes, uint32_t W,
+                                                              uint32_t n_pods,
                                                               const uint32_t* __restrict__ perm,
                                                               uint32_t* __restrict__ out) {
   const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1011,7 +1244,10 @@ __global__ __launch_bounds__(kBlock) void k_bitmask_transpose(const uint32_t* __
   const uint32_t p = (uint32_t)(t / W), w = (uint32_t)(t % W);
   // row p of the output belongs to caller pod perm[p] when the run was ordered
   const uint32_t q = perm ? perm[p] : p;
-  out[(size_t)q * W + w] = in[(size_t)w * n_pods + p];
+  uint32_t bits = 0;
+  for (uint32_t b = 0; b < 32u && 32u * w + b < n_nodes; ++b)
+    bits |= (uint32_t)bm_bit(bm, bm_stride, p, 32u * w + b) << b;
+  out[(size_t)q * W + w] = bits;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1028,28 +1264,36 @@ __global__ __launch_bounds__(kBlock) void k_bitmask_transpose(const uint32_t* __
 
 static inline dim3 pod_grid(uint32_t n) { return dim3((n + kBlock - 1) / kBlock); }
 
-hipError_t launch_k1(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
-                     uint32_t chunk_nodes, uint32_t C, const PodParams& pp, uint32_t n_pods,
-                     const Partials& part, uint32_t* bitmask, hipStream_t s) {
+hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigned char* sum,
+                     uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
+                     uint32_t n_pods, const Partials& part, uint64_t* bm, uint32_t bm_stride,
+                     hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   switch (path) {
     case Path::N32:
-      YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_filter_maxima<KK, Path::N32>), grid, dim3(kBlock), 0,
-                                          s, nodes, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
-                                          pp.number, pp.need_mem, pp.need_clk, n_pods, part.max_u,
-                                          part.cnt, bitmask));
+      if (sum) {
+        YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK>), grid, dim3(kBlock), 0, s, nodes,
+                                            sum, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
+                                            pp.number, pp.need_mem, pp.need_clk, n_pods,
+                                            part.max_u, part.cnt, bm, bm_stride));
+      } else {
+        YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_filter_maxima<KK, Path::N32>), grid, dim3(kBlock),
+                                            0, s, nodes, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
+                                            pp.number, pp.need_mem, pp.need_clk, n_pods,
+                                            part.max_u, part.cnt, bm, bm_stride));
+      }
       break;
     case Path::F64:
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_filter_maxima<KK, Path::F64>), grid, dim3(kBlock), 0,
                                           s, nodes, n_nodes, chunk_nodes, pp.m_f, pp.c_f,
                                           pp.number, pp.need_mem, pp.need_clk, n_pods, part.max_u,
-                                          part.cnt, bitmask));
+                                          part.cnt, bm, bm_stride));
       break;
     case Path::U64:
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_filter_maxima<KK, Path::U64>), grid, dim3(kBlock), 0,
                                           s, nodes, n_nodes, chunk_nodes, pp.m_u, pp.c_u,
                                           pp.number, pp.need_mem, pp.need_clk, n_pods, part.max_u,
-                                          part.cnt, bitmask));
+                                          part.cnt, bm, bm_stride));
       break;
   }
   return hipGetLastError();
@@ -1068,7 +1312,7 @@ int kernel_capacity(int K, Path path, int which, int mode_diskio) {
     YODA_FN(&k2_diskio<false>);
   } else if (which == 1) {
     switch (path) {
-      case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k1_filter_maxima<KK, Path::N32>))); break;
+      case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k1_block_n32<KK>))); break;
       case Path::F64: YODA_K_SWITCH(K, YODA_FN((&k1_filter_maxima<KK, Path::F64>))); break;
       case Path::U64: YODA_K_SWITCH(K, YODA_FN((&k1_filter_maxima<KK, Path::U64>))); break;
     }
@@ -1109,20 +1353,20 @@ template <int OUT>
 static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                               uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                               const uint64_t* maxima, const double* rcp, const float* rcp32,
-                              uint32_t n_pods, const uint32_t* bitmask, const Partials& part,
+                              uint32_t n_pods, const uint64_t* bm, uint32_t bm_stride, const Partials& part,
                               int64_t* rows, double* tk_s, uint32_t* tk_i, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
   switch (path) {
     case Path::N32:
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score<KK, Path::N32, OUT>), grid, dim3(kBlock), 0,
-                                          s, nodes, n_nodes, chunk_nodes, a, n_pods, bitmask,
+                                          s, nodes, n_nodes, chunk_nodes, a, n_pods, bm, bm_stride,
                                           part.best_f, part.idx, part.ties, part.low_f, rows,
                                           tk_s, tk_i));
       break;
     case Path::F64:
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score<KK, Path::F64, OUT>), grid, dim3(kBlock), 0,
-                                          s, nodes, n_nodes, chunk_nodes, a, n_pods, bitmask,
+                                          s, nodes, n_nodes, chunk_nodes, a, n_pods, bm, bm_stride,
                                           part.best_f, part.idx, part.ties, part.low_f, rows,
                                           tk_s, tk_i));
       break;
@@ -1130,7 +1374,7 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes, uint
       if (OUT == OUT_TOPK) return hipErrorInvalidValue;
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score_generic<KK, OUT == OUT_ROWS>), grid,
                                           dim3(kBlock), 0, s, nodes, n_nodes, chunk_nodes,
-                                          pp.m_u, pp.c_u, maxima, n_pods, bitmask, part.best_i,
+                                          pp.m_u, pp.c_u, maxima, n_pods, bm, bm_stride, part.best_i,
                                           part.idx, part.ties, part.low_i, rows));
       break;
   }
@@ -1140,10 +1384,10 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes, uint
 hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                           uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                           const double* rcp, const float* rcp32, uint32_t n_pods,
-                          const uint32_t* bitmask, const Partials& part, double* tk_s,
+                          const uint64_t* bm, uint32_t bm_stride, const Partials& part, double* tk_s,
                           uint32_t* tk_i, hipStream_t s) {
   return launch_k2_t<OUT_TOPK>(K, path, nodes, n_nodes, chunk_nodes, C, pp, nullptr, rcp, rcp32,
-                               n_pods, bitmask, part, nullptr, tk_s, tk_i, s);
+                               n_pods, bm, bm_stride, part, nullptr, tk_s, tk_i, s);
 }
 
 hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t C,
@@ -1161,10 +1405,10 @@ hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t 
 
 hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32_t* node,
                              const uint64_t* value, const uint64_t* card_number, uint32_t count,
-                             hipStream_t s) {
+                             unsigned char* sum, uint32_t sum_stride, hipStream_t s) {
   if (count == 0) return hipSuccess;
   hipLaunchKernelGGL(k_set_static, pod_grid(count), dim3(kBlock), 0, s, nodes, stride, node,
-                     value, card_number, count);
+                     value, card_number, count, sum, sum_stride);
   return hipGetLastError();
 }
 
@@ -1173,13 +1417,13 @@ int topk_k() { return kTopK; }
 hipError_t launch_k2(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
                      const double* rcp, const float* rcp32, uint32_t n_pods,
-                     const uint32_t* bitmask, const Partials& part, int64_t* rows,
+                     const uint64_t* bm, uint32_t bm_stride, const Partials& part, int64_t* rows,
                      hipStream_t s) {
   if (rows)
     return launch_k2_t<OUT_ROWS>(K, path, nodes, n_nodes, chunk_nodes, C, pp, maxima, rcp,
-                                 rcp32, n_pods, bitmask, part, rows, nullptr, nullptr, s);
+                                 rcp32, n_pods, bm, bm_stride, part, rows, nullptr, nullptr, s);
   return launch_k2_t<OUT_ARGMAX>(K, path, nodes, n_nodes, chunk_nodes, C, pp, maxima, rcp,
-                                 rcp32, n_pods, bitmask, part, rows, nullptr, nullptr, s);
+                                 rcp32, n_pods, bm, bm_stride, part, rows, nullptr, nullptr, s);
 }
 
 hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
@@ -1258,13 +1502,13 @@ hipError_t launch_finalize(const uint32_t* counts, const int64_t* best, const ui
 
 hipError_t launch_k3(int K, const unsigned char* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
                      uint32_t C, const PodParams& pp, const uint64_t* maxima, uint32_t n_pods,
-                     const uint32_t* bitmask, const uint32_t* flagged, const uint32_t* n_flagged,
+                     const uint64_t* bm, uint32_t bm_stride, const uint32_t* flagged, const uint32_t* n_flagged,
                      const int64_t* best, const int64_t* low, const Partials& part,
                      uint32_t max_flagged, hipStream_t s) {
   dim3 grid((max_flagged + kBlock - 1) / kBlock, C);
   YODA_K_SWITCH(K, hipLaunchKernelGGL((k3_exact_normalize<KK>), grid, dim3(kBlock), 0, s, nodes,
                                       n_nodes, chunk_nodes, pp.m_u, pp.c_u, maxima, n_pods,
-                                      bitmask, flagged, n_flagged, best, low, part.best_i,
+                                      bm, bm_stride, flagged, n_flagged, best, low, part.best_i,
                                       part.idx, part.ties, part.err, max_flagged));
   return hipGetLastError();
 }
@@ -1278,11 +1522,13 @@ hipError_t launch_reduce3(const Partials& part, uint32_t C, const uint32_t* flag
   return hipGetLastError();
 }
 
-hipError_t launch_bitmask_transpose(const uint32_t* in, uint32_t W, uint32_t n_pods,
-                                    const uint32_t* perm, uint32_t* out, hipStream_t s) {
+hipError_t launch_bitmask_transpose(const uint64_t* bm, uint32_t bm_stride, uint32_t n_nodes,
+                                    uint32_t W, uint32_t n_pods, const uint32_t* perm,
+                                    uint32_t* out, hipStream_t s) {
   const uint64_t total = (uint64_t)W * n_pods;
   dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
-  hipLaunchKernelGGL(k_bitmask_transpose, grid, dim3(kBlock), 0, s, in, W, n_pods, perm, out);
+  hipLaunchKernelGGL(k_bitmask_transpose, grid, dim3(kBlock), 0, s, bm, bm_stride, n_nodes, W,
+                     n_pods, perm, out);
   return hipGetLastError();
 }
 

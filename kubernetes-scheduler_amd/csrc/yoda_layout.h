@@ -12,7 +12,7 @@ namespace yoda {
 
 constexpr int kBlock = 256;             // threads per workgroup = 4 waves = 256 pods
 constexpr int kWave = 64;
-constexpr uint32_t kChunkAlign = 32;    // node-chunk granularity (one bitmask word)
+constexpr uint32_t kChunkAlign = 64;    // node-chunk granularity (one K1 node block)
 
 // Three exact record formats, chosen per snapshot by the host:
 //   N32  every card field <= 0xFFFFFFFE and bandwidth/clock/core/power <= 55738
@@ -78,6 +78,31 @@ enum N32F64 { kF64Free = 0, kF64Total = 1 };
 __host__ __device__ constexpr uint32_t n32_f64_off(int g, int k) {
   return 32u + 40u * (uint32_t)k + 8u * (uint32_t)(g * k);
 }
+
+// K1 node summary (N32 path): the Filter / PreScore facts of one node in a few u32 words,
+// read by the block-classified K1 with lane = node (k1_block_n32).  One record per node,
+// k1sum_stride(K) bytes, words:
+//   cn_lo, cn_hi      Status.CardNumber
+//   clock             the clock of every real card (valid when kSumUni4)
+//   meta              kSumUni4 | kSumUniTotal | kSumZeroTotal | (healthy count << 8)
+//   mrf1              1 + max FreeMemory over the real cards (0: empty CardList)
+//   total, bw, core, power   the per-node values (valid under kSumUni4 / kSumUniTotal)
+//   hfs[K]            1 + FreeMemory of the HEALTHY cards, sorted descending, 0-padded:
+//                     #healthy cards with free >= m  >= need  <=>  hfs[need-1] > m
+enum K1SumWord {
+  kSumCnLo = 0, kSumCnHi = 1, kSumClock = 2, kSumMeta = 3, kSumMrf1 = 4, kSumTotal = 5,
+  kSumBw = 6, kSumCore = 7, kSumPower = 8, kSumHfs = 12
+};
+constexpr uint32_t kSumUni4 = 1u, kSumUniTotal = 2u, kSumZeroTotal = 4u;
+__host__ __device__ constexpr uint32_t k1sum_stride(int k) {
+  return (48u + 4u * (uint32_t)k + 15u) & ~15u;
+}
+
+// Feasibility bitmask: one u64 per (pod wave, node), bit l = pod 64 w + l (in the order the
+// kernels see the pods) feasible on node n, at bm[w * bm_stride + n]; bm_stride = N rounded
+// up to 64.  K1 writes it coalesced (lane = node); K2 reads one wave's mask per node through
+// the scalar path and skips the node when it is 0.
+__host__ __device__ constexpr uint32_t bm_row(uint32_t n_nodes) { return (n_nodes + 63u) & ~63u; }
 
 // Mode B node record: V = Cpu/100, U = DiskIO/50 (algorithm.go:71,73).
 struct alignas(16) NodeRecB {

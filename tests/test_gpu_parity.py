@@ -125,11 +125,68 @@ def test_randomized_edges(dev, seed):
     pods.number[rng.random(400) < 0.05] = 0
     pods.memory[rng.random(400) < 0.05] = np.uint64((1 << 64) - 5)
     pods.clock[rng.random(400) < 0.05] = np.uint64(1 << 60)
-    for path in ("n32", "f64", "u64"):
-        got, want = run_both(dev, nodes, pods, force_generic=path == "u64",
-                             force_f64=path == "f64")
-        assert dev.path == path
-        assert_same(got, want)
+    for path in ("n32", "n32-per-node", "f64", "u64"):
+        dev.upload_nodes(nodes, force_generic=path == "u64", force_f64=path == "f64",
+                         per_node_k1=path == "n32-per-node")
+        assert dev.path == path.split("-")[0]
+        assert_same(dev.eval(pods, MODE_SCV), oracle.schedule(nodes, pods, MODE_SCV, threads=8))
+
+
+def _boundary_cluster(rng, n, k, pods):
+    """Nodes whose card fields sit exactly on the pods' thresholds (free == m, free == m - 1,
+    clock == c), mixed one-model / mixed-model nodes, empty and short CardLists, CardNumber
+    edge values: the cases where K1's wave bounds must not decide a node wrongly."""
+    nodes = synth.make_nodes(n, int(rng.integers(1 << 30)), cards=k)
+    mem = pods.memory[pods.has_memory == 1]
+    pick = rng.integers(0, max(len(mem), 1), size=nodes.card_free_memory.shape)
+    on = rng.random(nodes.card_free_memory.shape) < 0.3
+    if len(mem):
+        edge = mem[pick].astype(np.int64) - rng.integers(0, 2, size=pick.shape)
+        edge = np.clip(edge, 0, None).astype(np.uint64)
+        nodes.card_free_memory[on] = np.minimum(edge[on], nodes.card_total_memory[on])
+    mixed = rng.random(n) < 0.25
+    nodes.card_clock[mixed] = synth.CLOCKS[rng.integers(0, 3, size=(int(mixed.sum()), k))]
+    nodes.card_healthy[rng.random(nodes.card_healthy.shape) < 0.2] = 0
+    cn = nodes.card_number
+    cn[rng.random(n) < 0.05] = np.uint64((1 << 64) - 1)
+    cn[rng.random(n) < 0.05] = np.uint64((1 << 32) + 3)
+    cn[rng.random(n) < 0.05] = 0
+    nodes.card_count[rng.random(n) < 0.1] = rng.integers(0, k + 1)
+    return nodes.normalized()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_k1_block_classification(dev, seed):
+    """The block-classified K1 (N32) against the per-node K1 and the oracle, on sorted and
+    unsorted batches (waves of similar or of unrelated pods), including the bitmask."""
+    rng = np.random.default_rng(7000 + seed)
+    pods = synth.make_pods(900, int(rng.integers(1 << 30)))
+    pods.number[rng.random(900) < 0.05] = np.uint64((1 << 32) + 1)
+    pods.number[rng.random(900) < 0.05] = np.uint64((1 << 64) - 1)
+    pods.number[rng.random(900) < 0.05] = 0
+    pods.number[rng.random(900) < 0.05] = 17
+    pods.memory[rng.random(900) < 0.05] = 0
+    pods = pods.normalized()
+    nodes = _boundary_cluster(rng, 2200, 8, pods)
+    want = oracle.schedule(nodes, pods, MODE_SCV, threads=8)
+    words = {}
+    for order in (True, False):
+        dev.set_pod_order(order)
+        for per_node in (False, True):
+            dev.upload_nodes(nodes, per_node_k1=per_node)
+            assert dev.path == "n32"
+            assert_same(dev.eval(pods, MODE_SCV), want)
+            dev.upload_pods(pods)
+            dev.run(MODE_SCV, bitmask=True)
+            words[(order, per_node)] = dev.download_bitmask()
+    dev.set_pod_order(True)
+    ref = words[(False, True)]
+    for w in words.values():
+        np.testing.assert_array_equal(w, ref)
+    bits = np.unpackbits(ref.view(np.uint8), bitorder="little", axis=1)[:, :nodes.n_nodes]
+    for p in range(0, 900, 97):
+        _, feas, _, _ = oracle.pod_detail(nodes, pods, p)
+        np.testing.assert_array_equal(bits[p].astype(bool), feas)
 
 
 def test_tie_heavy(dev):
@@ -385,8 +442,9 @@ def test_uniform_node_factoring(dev):
     nodes.card_total_memory[mixed_total, 0] += 4096
     nodes = nodes.normalized()
     want = oracle.schedule(nodes, pods, MODE_SCV, threads=8)
-    for no_uniform, force_f64 in ((False, False), (True, False), (False, True)):
-        dev.upload_nodes(nodes, no_uniform=no_uniform, force_f64=force_f64)
+    for no_uniform, force_f64, per_node in ((False, False, False), (True, False, False),
+                                            (False, True, False), (False, False, True)):
+        dev.upload_nodes(nodes, no_uniform=no_uniform, force_f64=force_f64, per_node_k1=per_node)
         assert dev.path == ("f64" if force_f64 else "n32")
         assert_same(dev.eval(pods, MODE_SCV), want)
         dev.upload_pods(pods.slice(0, 16))
