@@ -153,6 +153,8 @@ int yoda_synchronize(yoda_t* h);
 #define YODA_UPLOAD_NO_UNIFORM 4u    /* disable the per-node GPU-model factoring (tests) */
 #define YODA_UPLOAD_PER_NODE_K1 8u   /* N32: per-node K1 sweep instead of the block-
                                         classified one (tests, A/B measurements)      */
+#define YODA_UPLOAD_PER_NODE_K2 16u  /* N32: per-pod K2 scoring instead of the block-
+                                        classified one (tests, A/B measurements)      */
 int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nodes, uint32_t node_offset,
                       uint32_t flags);
 /* 1 if the uploaded snapshot runs on the generic (u64) path, 0 on a fast path. */

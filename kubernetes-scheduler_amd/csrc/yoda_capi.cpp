@@ -27,7 +27,8 @@ hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uin
                           uint32_t* counts, hipStream_t s);
 hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
                         hipStream_t s);
-hipError_t launch_k2(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
+hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigned char* sum2,
+                     uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
                      const double* rcp, const float* rcp32, uint32_t n_pods,
                      const uint64_t* bm, uint32_t bm_stride, const Partials& part,
@@ -72,7 +73,8 @@ hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t 
                              uint32_t* out_i, hipStream_t s);
 hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32_t* node,
                              const uint64_t* value, const uint64_t* card_number, uint32_t count,
-                             unsigned char* sum, uint32_t sum_stride, hipStream_t s);
+                             unsigned char* sum, uint32_t sum_stride, unsigned char* sum2,
+                             uint32_t sum2_stride, hipStream_t s);
 int topk_k();
 size_t order_scratch_bytes(uint32_t n_pods);
 hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
@@ -162,8 +164,10 @@ struct yoda_handle {
   DevBuf nodes;     // fast or generic records
   DevBuf nodes_b;   // Mode B records
   DevBuf k1sum;     // K1 node summaries (N32 path, yoda_layout.h K1SumWord)
-  bool has_k1sum = false;
+  DevBuf k2sum;     // K2 node summaries (N32 path, yoda_layout.h K2SumWord)
+  bool has_k1sum = false, has_k2sum = false;
   std::vector<unsigned char> host_records;  // kept for alloc updates (greedy)
+  std::vector<uint32_t> host_k2sum;         // idem (its static score words)
   std::vector<uint64_t> h_total_sum, h_free_sum, h_alloc, h_card_number;
 
   // pods: one device blob of per-pod arrays (PodArray order), staged through pinned memory
@@ -217,7 +221,7 @@ struct yoda_handle {
 
   ~yoda_handle() {
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &pod_blob,   &maxima,       &counts,
+    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &pod_blob,   &maxima,       &counts,
                      &pod_sorted, &perm,     &order_scratch, &unperm,
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
@@ -498,7 +502,8 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, int64_t* best, uint32_t*
     HIP_TRY(h, launch_k2_diskio(h->nodes_b.as<NodeRecB>(), h->n_nodes, h->chunk2, h->C2,
                                 pod_params(h), P, part, rows, h->stream));
   } else {
-    HIP_TRY(h, launch_k2(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes,
+    HIP_TRY(h, launch_k2(h->K, h->path, h->nodes.as<unsigned char>(),
+                         h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr, h->n_nodes,
                          h->chunk2, h->C2, pod_params(h), maxima, h->rcp.as<double>(),
                          h->rcp32.as<float>(), P, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
                          part, rows, h->stream));
@@ -668,6 +673,8 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     const bool want_sum = path == Path::N32;
     const size_t sstride = k1sum_stride(K);
     std::vector<uint32_t> sum(want_sum ? (size_t)std::max<uint32_t>(N, 1) * sstride / 4 : 0, 0);
+    const size_t s2stride = k2sum_stride(K);
+    std::vector<uint32_t> sum2(want_sum ? (size_t)std::max<uint32_t>(N, 1) * s2stride / 4 : 0, 0);
     for (uint32_t i = 0; i < N; ++i) {
       unsigned char* r = rec.data() + (size_t)i * stride;
       uint32_t hm = 0;
@@ -725,6 +732,23 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
         std::sort(hfs, hfs + nhf, [](uint32_t x, uint32_t y) { return x > y; });
         s[kSumMrf1] = mrf1;
         for (uint32_t j = 0; j < nhf; ++j) s[kSumHfs + j] = hfs[j];
+        // K2 summary: real cards in descending free order (stable: ties keep card order)
+        uint32_t* s2 = sum2.data() + (size_t)i * s2stride / 4;
+        std::memcpy(s2 + kS2Static, &hd.static_score, 8);  // f64 bits (set above)
+        s2[kS2Clock] = s[kSumClock];
+        s2[kS2Meta] = ((hd.flags & kNodeUniform4) ? kSumUni4 : 0u) | (cnt << 8);
+        s2[kS2Bw] = s[kSumBw];
+        s2[kS2Core] = s[kSumCore];
+        s2[kS2Power] = s[kSumPower];
+        uint32_t ord[YODA_MAX_CARDS];
+        for (uint32_t j = 0; j < cnt; ++j) ord[j] = j;
+        std::stable_sort(ord, ord + cnt, [&](uint32_t x, uint32_t y) {
+          return nd->card_free_memory[a + x] > nd->card_free_memory[a + y];
+        });
+        for (uint32_t j = 0; j < cnt; ++j) {
+          s2[kS2Fs + j] = (uint32_t)nd->card_free_memory[a + ord[j]];
+          s2[kS2Fs + K + j] = (uint32_t)nd->card_total_memory[a + ord[j]];
+        }
       }
       for (uint32_t j = 0; j < nd->card_count[i]; ++j) {
         const size_t k = (size_t)i * KS + j;
@@ -758,6 +782,9 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
       HIP_TRY(h, h->k1sum.ensure(sum.size() * 4));
       HIP_TRY(h, hipMemcpyAsync(h->k1sum.p, sum.data(), sum.size() * 4, hipMemcpyHostToDevice,
                                 h->stream));
+      HIP_TRY(h, h->k2sum.ensure(sum2.size() * 4));
+      HIP_TRY(h, hipMemcpyAsync(h->k2sum.p, sum2.data(), sum2.size() * 4, hipMemcpyHostToDevice,
+                                h->stream));
     }
     const bool diskio = nd->cpu && nd->disk_io;
     if (diskio && N > 0) {
@@ -772,6 +799,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     }
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     h->host_records.swap(rec);
+    h->host_k2sum.swap(sum2);
     h->h_total_sum.assign(nd->total_memory_sum, nd->total_memory_sum + N);
     h->h_free_sum.assign(nd->free_memory_sum, nd->free_memory_sum + N);
     h->h_card_number.assign(nd->card_number, nd->card_number + N);
@@ -784,6 +812,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     h->K = K;
     h->path = path;
     h->has_k1sum = want_sum && !(flags & YODA_UPLOAD_PER_NODE_K1);
+    h->has_k2sum = want_sum && !(flags & YODA_UPLOAD_PER_NODE_K2);
     h->generic = path == Path::U64;
     h->has_nodes = true;
     h->ran = false;
@@ -818,12 +847,20 @@ int yoda_update_alloc(yoda_t* h, const uint64_t* alloc) {
       } else {
         reinterpret_cast<NodeHdrF*>(r)->static_score = (double)s;
         max_static = std::max(max_static, s);
+        if (h->has_k2sum) {
+          const double sd = (double)s;
+          std::memcpy(h->host_k2sum.data() + (size_t)i * k2sum_stride(h->K) / 4 + kS2Static, &sd,
+                      8);
+        }
       }
     }
     if (!h->generic && max_static >= (1ull << 51))
       return fail(h, YODA_ERR_RANGE, "static score leaves the fast path; re-upload the nodes");
     HIP_TRY(h, hipMemcpyAsync(h->nodes.p, h->host_records.data(), h->host_records.size(),
                               hipMemcpyHostToDevice, h->stream));
+    if (h->has_k2sum)
+      HIP_TRY(h, hipMemcpyAsync(h->k2sum.p, h->host_k2sum.data(), h->host_k2sum.size() * 4,
+                                hipMemcpyHostToDevice, h->stream));
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     return YODA_OK;
   } catch (...) {
@@ -1229,7 +1266,9 @@ struct GreedyState {
                                  reinterpret_cast<const uint64_t*>(d + o_val),
                                  reinterpret_cast<const uint64_t*>(d + o_cn), cnt,
                                  h->has_k1sum ? h->k1sum.as<unsigned char>() : nullptr,
-                                 k1sum_stride(h->K), h->stream));
+                                 k1sum_stride(h->K),
+                                 h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr,
+                                 k2sum_stride(h->K), h->stream));
     if (marks)
       for (uint32_t n : list) (*marks)[n] = 0;
     list.clear();

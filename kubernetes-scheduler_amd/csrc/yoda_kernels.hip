@@ -711,6 +711,185 @@ __global__ __launch_bounds__(kBlock) void k2_score(
   }
 }
 
+// K2, block-classified (N32 path, argmax output).  After K1 the pods of a wave usually share
+// their PreScore maxima (same feasible set), so the reciprocals RU(100/M) are the same on
+// every lane ("uniform maxima", checked once per wave).  The wave then walks its chunk in
+// blocks of 64 nodes with LANE = NODE and, for every one-model node, computes with those
+// uniform reciprocals the node's shared quotient sum and the prefix sums of its free-sorted
+// card terms (3 q_free + q_total) into LDS.  A node is
+//   U     if every pod of the wave is feasible on it and has the same qualifying cards
+//         (no real card's free memory between the wave's min and max scv/memory, clock not
+//         between its min and max scv/clock): its score is one number for the whole wave,
+//         folded into node-lane argmax/ties/min state that is reduced once per chunk;
+//   FAST  a one-model node that is not U: each pod lane counts its qualifying cards nq and
+//         reads  nq * shared + prefix[nq]  from LDS (the same integers as Scorer<N32>);
+//   EXACT anything else (mixed-model node, or non-uniform maxima): Scorer<N32>::raw.
+// Every term is an exact integer < 2^52 in each form, so all three give the same raw score.
+template <int K>
+__global__ __launch_bounds__(kBlock) void k2_block_n32(
+    const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum2,
+    uint32_t n_nodes, uint32_t chunk_nodes, ScoreArgs args, uint32_t n_pods,
+    const uint64_t* __restrict__ bm, uint32_t bm_stride, double* __restrict__ pbest,
+    uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties, double* __restrict__ plow) {
+  constexpr uint32_t S2 = k2sum_stride(K), NS = n32_stride(K);
+  constexpr uint32_t PSW = K + 2;  // LDS words per node: prefix[0..K], shared
+  __shared__ uint32_t lds_all[kBlock / kWave][kWave * PSW];
+  const uint32_t lane = lane_id();
+  uint32_t* lds = lds_all[threadIdx.x >> 6];
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t chunk = blockIdx.y;
+  const uint32_t n0 = chunk * chunk_nodes;
+  const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
+  const bool live = p < n_pods;
+  const uint64_t live_mask = ballot(live);
+  if (live_mask == 0) return;  // a wave past the batch
+  const uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
+  Scorer<Path::N32> sc;
+  if (live) sc.load(args, p, n_pods);
+  // live lanes are a prefix of the wave: lane 0 is live
+  const float u_bw = __int_as_float((int)uniform_u32((uint32_t)__float_as_int(sc.r_bw)));
+  const float u_core = __int_as_float((int)uniform_u32((uint32_t)__float_as_int(sc.r_core)));
+  const float u_pow = __int_as_float((int)uniform_u32((uint32_t)__float_as_int(sc.r_pow)));
+  const double u_free =
+      __longlong_as_double((long long)uniform_u64((uint64_t)__double_as_longlong(sc.r_free)));
+  const double u_tot =
+      __longlong_as_double((long long)uniform_u64((uint64_t)__double_as_longlong(sc.r_tot)));
+  const bool same = sc.r_bw == u_bw && sc.r_core == u_core && sc.r_pow == u_pow &&
+                    sc.r_free == u_free && sc.r_tot == u_tot;
+  const bool uni_max = ballot(!live || same) == ~0ull;
+  const uint32_t m_max = wave_max_u32(live ? sc.m : 0u), m_min = wave_min_u32(live ? sc.m : ~0u);
+  const uint32_t c_max = wave_max_u32(live ? sc.c : 0u), c_min = wave_min_u32(live ? sc.c : ~0u);
+
+  double best = -1.0, low = 1.0e300;        // pod lane
+  uint32_t idx = 0xffffffffu, ties = 0;
+  double ubest = -1.0, ulow = 1.0e300;      // node lane (U nodes)
+  uint32_t uidx = 0xffffffffu, uties = 0;
+  for (uint32_t nb = n0; nb < n1; nb += kWave) {
+    const uint32_t n = nb + lane;
+    const bool valid = n < n1;
+    const uint64_t mask = valid ? bmw[n] : 0ull;
+    const uint64_t feas_b = ballot(mask != 0ull);
+    if (feas_b == 0) continue;  // no pod of the wave can use any node of the block
+    uint64_t fast_b = 0, u_b = 0;
+    if (uni_max) {
+      const uint32_t* s = reinterpret_cast<const uint32_t*>(sum2 + (size_t)(valid ? n : nb) * S2);
+      const uint4 h0 = *reinterpret_cast<const uint4*>(s);
+      const uint4 h1 = *reinterpret_cast<const uint4*>(s + 4);
+      const double stat = __longlong_as_double((long long)((uint64_t)h0.x | ((uint64_t)h0.y << 32)));
+      const uint32_t ck = h0.z, meta = h0.w, bw = h1.x, core = h1.y, pw = h1.z;
+      const uint32_t cnt = (meta >> 8) & 0xffu;
+      const bool fast = mask != 0ull && (meta & kSumUni4) != 0u;
+      fast_b = ballot(fast);
+      // CalculateCardScore terms (algorithm.go:280-291) with the wave's reciprocals
+      const uint32_t shared = (uint32_t)((float)bw * u_bw) + (uint32_t)((float)ck * u_bw) +
+                              2u * (uint32_t)((float)core * u_core) +
+                              (uint32_t)((float)pw * u_pow);
+      const Group<uint32_t, K> fs = load_group<uint32_t, K>(
+          reinterpret_cast<const unsigned char*>(s + kS2Fs));
+      const Group<uint32_t, K> ts = load_group<uint32_t, K>(
+          reinterpret_cast<const unsigned char*>(s + kS2Fs + K));
+      uint32_t nq_lo = 0, nq_hi = 0;  // qualifying cards for the largest / smallest m
+#pragma unroll
+      for (int t = 0; t < K; ++t) {
+        nq_lo += (uint32_t)(fs.v[t] >= m_max);
+        nq_hi += (uint32_t)(fs.v[t] >= m_min);
+      }
+      nq_lo = min(nq_lo, cnt);
+      nq_hi = min(nq_hi, cnt);
+      uint32_t acc = 0, sel = 0;  // prefix sums of (3 q_free + q_total) in free order
+      lds[lane * PSW + 0] = 0u;
+#pragma unroll
+      for (int t = 0; t < K; ++t) {
+        acc += 3u * (uint32_t)((double)fs.v[t] * u_free) + (uint32_t)((double)ts.v[t] * u_tot);
+        lds[lane * PSW + t + 1] = acc;
+        sel = (uint32_t)(t + 1) == nq_lo ? acc : sel;
+      }
+      lds[lane * PSW + K + 1] = shared;
+      const bool q_all = ck >= c_max, q_none = ck < c_min;
+      const bool is_u = fast && mask == live_mask && nq_lo == nq_hi && (q_all || q_none);
+      u_b = ballot(is_u);
+      if (is_u) {
+        const uint32_t basic = q_all ? nq_lo * shared + sel : 0u;  // algorithm.go:271
+        const double raw = (double)basic + stat;                   // algorithm.go:96
+        if (raw > ubest) {
+          ubest = raw;
+          uidx = n;
+          uties = 1;
+        } else if (raw == ubest) {
+          ++uties;
+        }
+        ulow = fmin(ulow, raw);
+      }
+    }
+    uint64_t part_b = feas_b & ~u_b;
+    while (part_b) {  // wave-uniform loop over the remaining feasible nodes
+      const int j = __builtin_ctzll(part_b);
+      part_b &= part_b - 1;
+      const uint32_t nn = nb + (uint32_t)j;
+      const uint64_t mj = ((uint64_t)uniform_u32(__shfl((uint32_t)(mask >> 32), j, kWave)) << 32) |
+                          uniform_u32(__shfl((uint32_t)mask, j, kWave));
+      double raw;
+      if ((fast_b >> j) & 1ull) {
+        const uint32_t* s = reinterpret_cast<const uint32_t*>(sum2 + (size_t)nn * S2);
+        const Group<uint32_t, K> fs = load_group<uint32_t, K>(
+            reinterpret_cast<const unsigned char*>(s + kS2Fs));
+        const uint32_t cnt = (s[kS2Meta] >> 8) & 0xffu;
+        uint32_t nq = 0;
+#pragma unroll
+        for (int t = 0; t < K; ++t) nq += (uint32_t)(fs.v[t] >= sc.m);
+        nq = min(nq, cnt);
+        const uint32_t basic =
+            s[kS2Clock] >= sc.c ? nq * lds[(uint32_t)j * PSW + K + 1] + lds[(uint32_t)j * PSW + nq]
+                                : 0u;
+        raw = (double)basic +
+              __longlong_as_double((long long)((uint64_t)s[0] | ((uint64_t)s[1] << 32)));
+      } else {
+        raw = sc.template raw<K>(nodes + (size_t)nn * NS);
+      }
+      if ((mj >> lane) & 1ull) {
+        if (raw > best) {
+          best = raw;
+          idx = nn;
+          ties = 1;
+        } else if (raw == best) {
+          ++ties;
+        }
+        low = fmin(low, raw);
+      }
+    }
+  }
+  // merge the U nodes (the same for every pod lane) into each pod lane
+  double wb = ubest;
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) wb = fmax(wb, __shfl_xor(wb, o, kWave));
+  const bool top = ubest == wb && uties > 0;
+  uint32_t wi = top ? uidx : 0xffffffffu, wt = top ? uties : 0u;
+  double wl = ulow;
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    wi = min(wi, (uint32_t)__shfl_xor((int)wi, o, kWave));
+    wt += (uint32_t)__shfl_xor((int)wt, o, kWave);
+    wl = fmin(wl, __shfl_xor(wl, o, kWave));
+  }
+  if (!live) return;
+  if (wt > 0) {
+    if (wb > best) {
+      best = wb;
+      idx = wi;
+      ties = wt;
+    } else if (wb == best) {
+      idx = min(idx, wi);
+      ties += wt;
+    }
+    low = fmin(low, wl);
+  }
+  const size_t o = (size_t)chunk * n_pods + p;
+  pbest[o] = best;
+  pidx[o] = idx;
+  pties[o] = ties;
+  plow[o] = low;
+}
+
 // Merge the per-chunk top-k lists of each pod (chunks in node order, so the strict '>'
 // insertion keeps lower node indices first among equal scores) -> [TOPK][P], global ids.
 __global__ __launch_bounds__(kBlock) void k_topk_merge(const double* __restrict__ tk_s,
@@ -821,7 +1000,9 @@ __global__ __launch_bounds__(kBlock) void k_set_static(unsigned char* __restrict
                                                        const uint64_t* __restrict__ card_number,
                                                        uint32_t count,
                                                        unsigned char* __restrict__ sum,
-                                                       uint32_t sum_stride) {
+                                                       uint32_t sum_stride,
+                                                       unsigned char* __restrict__ sum2,
+                                                       uint32_t sum2_stride) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= count) return;
   uint64_t* hdr = reinterpret_cast<uint64_t*>(nodes + (size_t)node[t] * stride);
@@ -831,6 +1012,11 @@ __global__ __launch_bounds__(kBlock) void k_set_static(unsigned char* __restrict
     uint32_t* s = reinterpret_cast<uint32_t*>(sum + (size_t)node[t] * sum_stride);
     s[kSumCnLo] = (uint32_t)card_number[t];
     s[kSumCnHi] = (uint32_t)(card_number[t] >> 32);
+  }
+  if (sum2) {  // the K2 summary's copy of the static score (words 0-1)
+    uint32_t* s = reinterpret_cast<uint32_t*>(sum2 + (size_t)node[t] * sum2_stride);
+    s[kS2Static] = (uint32_t)value[t];
+    s[kS2Static + 1] = (uint32_t)(value[t] >> 32);
   }
 }
 
@@ -1318,7 +1504,7 @@ int kernel_capacity(int K, Path path, int which, int mode_diskio) {
     }
   } else {
     switch (path) {
-      case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k2_score<KK, Path::N32, OUT_ARGMAX>))); break;
+      case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k2_block_n32<KK>))); break;
       case Path::F64: YODA_K_SWITCH(K, YODA_FN((&k2_score<KK, Path::F64, OUT_ARGMAX>))); break;
       case Path::U64: YODA_K_SWITCH(K, YODA_FN((&k2_score_generic<KK, false>))); break;
     }
@@ -1350,7 +1536,8 @@ hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, fl
 }
 
 template <int OUT>
-static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
+static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
+                              const unsigned char* sum2, uint32_t n_nodes,
                               uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                               const uint64_t* maxima, const double* rcp, const float* rcp32,
                               uint32_t n_pods, const uint64_t* bm, uint32_t bm_stride, const Partials& part,
@@ -1359,6 +1546,12 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes, uint
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
   switch (path) {
     case Path::N32:
+      if (OUT == OUT_ARGMAX && sum2) {
+        YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK>), grid, dim3(kBlock), 0, s, nodes,
+                                            sum2, n_nodes, chunk_nodes, a, n_pods, bm, bm_stride,
+                                            part.best_f, part.idx, part.ties, part.low_f));
+        break;
+      }
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score<KK, Path::N32, OUT>), grid, dim3(kBlock), 0,
                                           s, nodes, n_nodes, chunk_nodes, a, n_pods, bm, bm_stride,
                                           part.best_f, part.idx, part.ties, part.low_f, rows,
@@ -1386,7 +1579,8 @@ hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t
                           const double* rcp, const float* rcp32, uint32_t n_pods,
                           const uint64_t* bm, uint32_t bm_stride, const Partials& part, double* tk_s,
                           uint32_t* tk_i, hipStream_t s) {
-  return launch_k2_t<OUT_TOPK>(K, path, nodes, n_nodes, chunk_nodes, C, pp, nullptr, rcp, rcp32,
+  return launch_k2_t<OUT_TOPK>(K, path, nodes, nullptr, n_nodes, chunk_nodes, C, pp, nullptr, rcp,
+                               rcp32,
                                n_pods, bm, bm_stride, part, nullptr, tk_s, tk_i, s);
 }
 
@@ -1405,24 +1599,26 @@ hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t 
 
 hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32_t* node,
                              const uint64_t* value, const uint64_t* card_number, uint32_t count,
-                             unsigned char* sum, uint32_t sum_stride, hipStream_t s) {
+                             unsigned char* sum, uint32_t sum_stride, unsigned char* sum2,
+                             uint32_t sum2_stride, hipStream_t s) {
   if (count == 0) return hipSuccess;
   hipLaunchKernelGGL(k_set_static, pod_grid(count), dim3(kBlock), 0, s, nodes, stride, node,
-                     value, card_number, count, sum, sum_stride);
+                     value, card_number, count, sum, sum_stride, sum2, sum2_stride);
   return hipGetLastError();
 }
 
 int topk_k() { return kTopK; }
 
-hipError_t launch_k2(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
+hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigned char* sum2,
+                     uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
                      const double* rcp, const float* rcp32, uint32_t n_pods,
                      const uint64_t* bm, uint32_t bm_stride, const Partials& part, int64_t* rows,
                      hipStream_t s) {
   if (rows)
-    return launch_k2_t<OUT_ROWS>(K, path, nodes, n_nodes, chunk_nodes, C, pp, maxima, rcp,
+    return launch_k2_t<OUT_ROWS>(K, path, nodes, nullptr, n_nodes, chunk_nodes, C, pp, maxima, rcp,
                                  rcp32, n_pods, bm, bm_stride, part, rows, nullptr, nullptr, s);
-  return launch_k2_t<OUT_ARGMAX>(K, path, nodes, n_nodes, chunk_nodes, C, pp, maxima, rcp,
+  return launch_k2_t<OUT_ARGMAX>(K, path, nodes, sum2, n_nodes, chunk_nodes, C, pp, maxima, rcp,
                                  rcp32, n_pods, bm, bm_stride, part, rows, nullptr, nullptr, s);
 }
 

@@ -98,6 +98,18 @@ __host__ __device__ constexpr uint32_t k1sum_stride(int k) {
   return (48u + 4u * (uint32_t)k + 15u) & ~15u;
 }
 
+// K2 node summary (N32 path), read by the block K2 (k2_block_n32) with lane = node and, for
+// single nodes, through the scalar path.  k2sum_stride(K) bytes, u32 words:
+//   static (f64, words 0-1)   CalculateAllocateScore + CalculateActualScore
+//   clock, meta, bw, core, power   meta = kSumUni4 | (len(CardList) << 8)
+//   fs[K]   FreeMemory of the REAL cards, sorted descending (0-padded)
+//   ts[K]   TotalMemory of the same cards, in the same order
+// The qualifying cards of a one-model node (algorithm.go:271) are then a prefix of that
+// order: nq(m) = #{fs >= m} (capped at len(CardList)).
+enum K2SumWord { kS2Static = 0, kS2Clock = 2, kS2Meta = 3, kS2Bw = 4, kS2Core = 5, kS2Power = 6,
+                 kS2Fs = 8 };
+__host__ __device__ constexpr uint32_t k2sum_stride(int k) { return 32u + 8u * (uint32_t)k; }
+
 // Feasibility bitmask: one u64 per (pod wave, node), bit l = pod 64 w + l (in the order the
 // kernels see the pods) feasible on node n, at bm[w * bm_stride + n]; bm_stride = N rounded
 // up to 64.  K1 writes it coalesced (lane = node); K2 reads one wave's mask per node through

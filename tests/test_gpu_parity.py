@@ -127,7 +127,7 @@ def test_randomized_edges(dev, seed):
     pods.clock[rng.random(400) < 0.05] = np.uint64(1 << 60)
     for path in ("n32", "n32-per-node", "f64", "u64"):
         dev.upload_nodes(nodes, force_generic=path == "u64", force_f64=path == "f64",
-                         per_node_k1=path == "n32-per-node")
+                         per_node_k1=path == "n32-per-node", per_node_k2=path == "n32-per-node")
         assert dev.path == path.split("-")[0]
         assert_same(dev.eval(pods, MODE_SCV), oracle.schedule(nodes, pods, MODE_SCV, threads=8))
 
@@ -173,7 +173,7 @@ def test_k1_block_classification(dev, seed):
     for order in (True, False):
         dev.set_pod_order(order)
         for per_node in (False, True):
-            dev.upload_nodes(nodes, per_node_k1=per_node)
+            dev.upload_nodes(nodes, per_node_k1=per_node, per_node_k2=per_node)
             assert dev.path == "n32"
             assert_same(dev.eval(pods, MODE_SCV), want)
             dev.upload_pods(pods)
@@ -444,7 +444,8 @@ def test_uniform_node_factoring(dev):
     want = oracle.schedule(nodes, pods, MODE_SCV, threads=8)
     for no_uniform, force_f64, per_node in ((False, False, False), (True, False, False),
                                             (False, True, False), (False, False, True)):
-        dev.upload_nodes(nodes, no_uniform=no_uniform, force_f64=force_f64, per_node_k1=per_node)
+        dev.upload_nodes(nodes, no_uniform=no_uniform, force_f64=force_f64, per_node_k1=per_node,
+                         per_node_k2=per_node)
         assert dev.path == ("f64" if force_f64 else "n32")
         assert_same(dev.eval(pods, MODE_SCV), want)
         dev.upload_pods(pods.slice(0, 16))
@@ -452,3 +453,35 @@ def test_uniform_node_factoring(dev):
         for p in range(16):
             _, f, raw, _ = oracle.pod_detail(nodes, pods, p)
             np.testing.assert_array_equal(rows[p][f], raw[f])
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_k2_block_scoring(dev, seed):
+    """The block-classified K2 (N32: node-lane scores for U nodes, LDS prefix sums for FAST
+    nodes) against the per-pod K2 and the oracle: waves of near-identical pods (sorted, many
+    U nodes), waves of unrelated pods (unsorted, non-uniform maxima), free memory on the
+    pods' thresholds (qualifying sets that differ inside a wave), mixed-model nodes."""
+    rng = np.random.default_rng(8100 + seed)
+    pods = synth.make_pods(1100, int(rng.integers(1 << 30)))
+    # clusters of identical requests: whole waves with one qualifying set
+    same = rng.random(1100) < 0.4
+    pods.memory[same] = rng.choice(np.array([0, 1000, 16000, 40000], dtype=np.uint64),
+                                   size=int(same.sum()))
+    pods = pods.normalized()
+    nodes = _boundary_cluster(rng, 2600, 8, pods)
+    # keep alloc varied: many distinct static scores, and ties through equal records
+    dup = rng.random(nodes.n_nodes) < 0.1
+    src = rng.integers(0, nodes.n_nodes, size=int(dup.sum()))
+    for f in ("card_free_memory", "card_total_memory", "card_clock", "card_bandwidth",
+              "card_core", "card_power", "card_healthy"):
+        getattr(nodes, f)[dup] = getattr(nodes, f)[src]
+    for f in ("card_number", "card_count", "free_memory_sum", "total_memory_sum", "alloc_memory"):
+        getattr(nodes, f)[dup] = getattr(nodes, f)[src]
+    nodes = nodes.normalized()
+    want = oracle.schedule(nodes, pods, MODE_SCV, threads=8)
+    for order in (True, False):
+        dev.set_pod_order(order)
+        for k1, k2 in ((False, False), (True, False), (False, True)):
+            dev.upload_nodes(nodes, per_node_k1=k1, per_node_k2=k2)
+            assert_same(dev.eval(pods, MODE_SCV), want)
+    dev.set_pod_order(True)
