@@ -1356,7 +1356,9 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
       all.build(pods, order.data(), P);
       if ((rc = yoda_upload_pods(h, &all.soa)) || (rc = yoda_run(h, mode, 0))) return rc;
       std::vector<int32_t> pk(P);
-      HIP_TRY(h, hipMemcpy(pk.data(), h->pick.p, P * 4ull, hipMemcpyDeviceToHost));
+      // the handle's stream may be non-blocking: copy and wait on it, not on the null stream
+      HIP_TRY(h, hipMemcpyAsync(pk.data(), h->pick.p, P * 4ull, hipMemcpyDeviceToHost, h->stream));
+      HIP_TRY(h, hipStreamSynchronize(h->stream));
       for (uint32_t i = 0; i < P; ++i) pick[order[i]] = pk[i];
       return YODA_OK;
     }

@@ -274,6 +274,9 @@ __global__ __launch_bounds__(kBlock) void k1_block_n32(
     uint64_t* __restrict__ bm, uint32_t bm_stride) {
   constexpr uint32_t SS = k1sum_stride(K);
   constexpr uint32_t NS = n32_stride(K);
+  constexpr uint32_t HW = K + 1;  // LDS words per node: hfs[0..K-1], 0
+  __shared__ uint32_t lds_all[kBlock / kWave][kWave * HW];
+  uint32_t* lds = lds_all[threadIdx.x >> 6];
   const uint32_t lane = lane_id();
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t chunk = blockIdx.y, C = gridDim.y;
@@ -332,6 +335,13 @@ __global__ __launch_bounds__(kBlock) void k1_block_n32(
     const uint4 w1 = *reinterpret_cast<const uint4*>(s + 4);
     const uint32_t pw = s[kSumPower];
     const uint32_t t_all = s[hfs_all], t_none = s[hfs_none];
+    {  // the node's healthy frees for the per-pod pass: lds[node][need - 1] (slot K: 0)
+      const Group<uint32_t, K> hf =
+          load_group<uint32_t, K>(reinterpret_cast<const unsigned char*>(s + kSumHfs));
+#pragma unroll
+      for (int t = 0; t < K; ++t) lds[lane * HW + t] = hf.v[t];
+      lds[lane * HW + K] = 0u;
+    }
     const uint64_t cn = (uint64_t)w0.x | ((uint64_t)w0.y << 32);
     const uint32_t ck = w0.z, meta = w0.w, mrf1 = w1.x, tot = w1.y, bw = w1.z, core = w1.w;
     const bool uni4 = (meta & kSumUni4) != 0u, unit = (meta & kSumUniTotal) != 0u;
@@ -367,8 +377,36 @@ __global__ __launch_bounds__(kBlock) void k1_block_n32(
     while (part_b) {  // wave-uniform loop over the nodes the bounds could not decide
       const int j = __builtin_ctzll(part_b);
       part_b &= part_b - 1;
-      const bool f = k1_node<K, Path::N32>(nodes + (size_t)(nb + (uint32_t)j) * NS, m, c, number,
-                                           need_mem, need_clk, mx, nf, nz) && live;
+      const uint32_t mj = (uint32_t)__builtin_amdgcn_readlane((int)meta, j);
+      bool f;
+      if ((mj & (kSumUni4 | kSumUniTotal)) == (kSumUni4 | kSumUniTotal)) {
+        // one-model node: the same predicates from the node lane's summary (no memory
+        // round trip): CardFitsMemory count >= need  <=>  hfs[need-1] > m
+        const uint64_t cnj =
+            (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)w0.x, j) |
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)w0.y, j) << 32);
+        const uint32_t ckj = (uint32_t)__builtin_amdgcn_readlane((int)ck, j);
+        const uint32_t mrfj = (uint32_t)__builtin_amdgcn_readlane((int)mrf1, j);
+        const uint32_t hk = need_mem == 0u ? (uint32_t)K : min(need_mem, (uint32_t)K + 1u) - 1u;
+        const uint32_t th = lds[(uint32_t)j * HW + hk];
+        f = live && number <= cnj && (need_mem == 0u || th > m) &&
+            (need_clk == 0u || (ckj == c && ((mj >> 8) & 0xffu) >= need_clk));
+        if (f) {
+          ++nf;
+          nz += (mj & kSumZeroTotal) ? 1u : 0u;
+          if (ckj >= c && mrfj > m) {  // collection.go:46, one-model node
+            mx[kMaxBw] = max(mx[kMaxBw], (uint32_t)__builtin_amdgcn_readlane((int)bw, j));
+            mx[kMaxClock] = max(mx[kMaxClock], ckj);
+            mx[kMaxCore] = max(mx[kMaxCore], (uint32_t)__builtin_amdgcn_readlane((int)core, j));
+            mx[kMaxFree] = max(mx[kMaxFree], mrfj - 1u);
+            mx[kMaxPower] = max(mx[kMaxPower], (uint32_t)__builtin_amdgcn_readlane((int)pw, j));
+            mx[kMaxTotal] = max(mx[kMaxTotal], (uint32_t)__builtin_amdgcn_readlane((int)tot, j));
+          }
+        }
+      } else {
+        f = k1_node<K, Path::N32>(nodes + (size_t)(nb + (uint32_t)j) * NS, m, c, number,
+                                  need_mem, need_clk, mx, nf, nz) && live;
+      }
       const uint64_t b = ballot(f);
       set_lane(lo, hi, b, (uint32_t)j);
     }
@@ -771,9 +809,12 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
     const uint64_t feas_b = ballot(mask != 0ull);
     if (feas_b == 0) continue;  // no pod of the wave can use any node of the block
     uint64_t fast_b = 0, u_b = 0;
+    // node-lane summary, kept for the per-pod pass (read back with v_readlane)
+    uint4 h0 = make_uint4(0u, 0u, 0u, 0u);
+    Group<uint32_t, K> fs;
     if (uni_max) {
       const uint32_t* s = reinterpret_cast<const uint32_t*>(sum2 + (size_t)(valid ? n : nb) * S2);
-      const uint4 h0 = *reinterpret_cast<const uint4*>(s);
+      h0 = *reinterpret_cast<const uint4*>(s);
       const uint4 h1 = *reinterpret_cast<const uint4*>(s + 4);
       const double stat = __longlong_as_double((long long)((uint64_t)h0.x | ((uint64_t)h0.y << 32)));
       const uint32_t ck = h0.z, meta = h0.w, bw = h1.x, core = h1.y, pw = h1.z;
@@ -784,8 +825,7 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
       const uint32_t shared = (uint32_t)((float)bw * u_bw) + (uint32_t)((float)ck * u_bw) +
                               2u * (uint32_t)((float)core * u_core) +
                               (uint32_t)((float)pw * u_pow);
-      const Group<uint32_t, K> fs = load_group<uint32_t, K>(
-          reinterpret_cast<const unsigned char*>(s + kS2Fs));
+      fs = load_group<uint32_t, K>(reinterpret_cast<const unsigned char*>(s + kS2Fs));
       const Group<uint32_t, K> ts = load_group<uint32_t, K>(
           reinterpret_cast<const unsigned char*>(s + kS2Fs + K));
       uint32_t nq_lo = 0, nq_hi = 0;  // qualifying cards for the largest / smallest m
@@ -830,19 +870,20 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
                           uniform_u32(__shfl((uint32_t)mask, j, kWave));
       double raw;
       if ((fast_b >> j) & 1ull) {
-        const uint32_t* s = reinterpret_cast<const uint32_t*>(sum2 + (size_t)nn * S2);
-        const Group<uint32_t, K> fs = load_group<uint32_t, K>(
-            reinterpret_cast<const unsigned char*>(s + kS2Fs));
-        const uint32_t cnt = (s[kS2Meta] >> 8) & 0xffu;
+        // one-model node: nq qualifying cards (a prefix of the free order), then
+        // nq * shared + prefix[nq] from LDS -- the node's facts come from its lane
+        const uint32_t cnt = ((uint32_t)__builtin_amdgcn_readlane((int)h0.w, j) >> 8) & 0xffu;
         uint32_t nq = 0;
 #pragma unroll
-        for (int t = 0; t < K; ++t) nq += (uint32_t)(fs.v[t] >= sc.m);
+        for (int t = 0; t < K; ++t)
+          nq += (uint32_t)((uint32_t)__builtin_amdgcn_readlane((int)fs.v[t], j) >= sc.m);
         nq = min(nq, cnt);
+        const uint32_t ckj = (uint32_t)__builtin_amdgcn_readlane((int)h0.z, j);
         const uint32_t basic =
-            s[kS2Clock] >= sc.c ? nq * lds[(uint32_t)j * PSW + K + 1] + lds[(uint32_t)j * PSW + nq]
-                                : 0u;
-        raw = (double)basic +
-              __longlong_as_double((long long)((uint64_t)s[0] | ((uint64_t)s[1] << 32)));
+            ckj >= sc.c ? nq * lds[(uint32_t)j * PSW + K + 1] + lds[(uint32_t)j * PSW + nq] : 0u;
+        const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h0.x, j) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h0.y, j) << 32);
+        raw = (double)basic + __longlong_as_double((long long)sb);
       } else {
         raw = sc.template raw<K>(nodes + (size_t)nn * NS);
       }
