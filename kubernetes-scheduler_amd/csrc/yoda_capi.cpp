@@ -281,10 +281,14 @@ void plan_chunks_for(uint32_t cap, uint32_t n_pods, uint32_t n_nodes, uint32_t* 
   if (cap == 0) cap = 2048;
   uint32_t C = std::max<uint32_t>(1, (uint32_t)((6ull * cap) / pod_blocks));
   C = std::min(C, max_chunks);
+  // a multiple of 8 chunks lets the kernels give each XCD whole chunks (tile() in
+  // yoda_kernels.hip); trailing chunks may then be empty (they write identity partials)
+  const bool xcd = C >= 8;
+  if (xcd) C = (C + 7) / 8 * 8;
   uint32_t chunk = (n_nodes + C - 1) / C;
   chunk = std::max<uint32_t>(kChunkAlign, (chunk + kChunkAlign - 1) / kChunkAlign * kChunkAlign);
   *chunk_out = chunk;
-  *C_out = std::max<uint32_t>(1, (n_nodes + chunk - 1) / chunk);
+  *C_out = xcd ? C : std::max<uint32_t>(1, (n_nodes + chunk - 1) / chunk);
 }
 
 int capacity(yoda_t* h, int which, int mode) {

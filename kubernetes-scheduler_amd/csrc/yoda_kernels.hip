@@ -170,6 +170,22 @@ __device__ __forceinline__ uint32_t uniform_u32(uint32_t v) {
 __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
   return (uint64_t)uniform_u32((uint32_t)v) | ((uint64_t)uniform_u32((uint32_t)(v >> 32)) << 32);
 }
+// Workgroup -> (pod block, node chunk), XCD-aware.  The grid is (pod blocks, chunks);
+// workgroups are dealt round-robin over the 8 XCDs in linear order, so with C a multiple of
+// 8 the linear id is remapped to give each XCD whole chunks (chunk % 8 == its slot), visited
+// one chunk at a time across all pod blocks: the chunk's node records and summaries stay in
+// that XCD's L2 while every pod block reads them.  Placement only affects speed.
+struct Tile {
+  uint32_t pb, chunk;
+};
+__device__ __forceinline__ Tile tile() {
+  const uint32_t PB = gridDim.x, C = gridDim.y;
+  if ((C & 7u) != 0u) return {blockIdx.x, blockIdx.y};
+  const uint32_t L = blockIdx.x + blockIdx.y * PB;
+  const uint32_t i = L >> 3;
+  return {i % PB, (i / PB) * 8u + (L & 7u)};
+}
+
 // Wave-wide reductions (every lane gets the result; once per workgroup chunk, not hot).
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
@@ -213,8 +229,9 @@ __global__ __launch_bounds__(kBlock) void k1_filter_maxima(
     uint32_t* __restrict__ pcnt, uint64_t* __restrict__ bm, uint32_t bm_stride) {
   using R = Rec<PATH>;
   using T = typename R::T;
-  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t chunk = blockIdx.y, C = gridDim.y;
+  const Tile tl = tile();
+  const uint32_t p = tl.pb * kBlock + threadIdx.x;
+  const uint32_t chunk = tl.chunk, C = gridDim.y;
   const uint32_t n0 = chunk * chunk_nodes;
   const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
   const bool live = p < n_pods;
@@ -278,8 +295,9 @@ __global__ __launch_bounds__(kBlock) void k1_block_n32(
   __shared__ uint32_t lds_all[kBlock / kWave][kWave * HW];
   uint32_t* lds = lds_all[threadIdx.x >> 6];
   const uint32_t lane = lane_id();
-  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t chunk = blockIdx.y, C = gridDim.y;
+  const Tile tl = tile();
+  const uint32_t p = tl.pb * kBlock + threadIdx.x;
+  const uint32_t chunk = tl.chunk, C = gridDim.y;
   const uint32_t n0 = chunk * chunk_nodes;
   const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
   const bool live = p < n_pods;
@@ -666,8 +684,9 @@ __global__ __launch_bounds__(kBlock) void k2_score(
     double* __restrict__ pbest, uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties,
     double* __restrict__ plow, int64_t* __restrict__ rows, double* __restrict__ tk_s,
     uint32_t* __restrict__ tk_i) {
-  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t chunk = blockIdx.y;
+  const Tile tl = tile();
+  const uint32_t p = tl.pb * kBlock + threadIdx.x;
+  const uint32_t chunk = tl.chunk;
   const uint32_t n0 = chunk * chunk_nodes;
   const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
   const bool live = p < n_pods;
@@ -774,8 +793,9 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
   __shared__ uint32_t lds_all[kBlock / kWave][kWave * PSW];
   const uint32_t lane = lane_id();
   uint32_t* lds = lds_all[threadIdx.x >> 6];
-  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t chunk = blockIdx.y;
+  const Tile tl = tile();
+  const uint32_t p = tl.pb * kBlock + threadIdx.x;
+  const uint32_t chunk = tl.chunk;
   const uint32_t n0 = chunk * chunk_nodes;
   const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
   const bool live = p < n_pods;
@@ -806,16 +826,21 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
     const uint32_t n = nb + lane;
     const bool valid = n < n1;
     const uint64_t mask = valid ? bmw[n] : 0ull;
+    // node-lane summary, kept for the per-pod pass (read back with v_readlane); issued
+    // together with the mask load so the block pays one memory latency, not two
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(sum2 + (size_t)(valid ? n : nb) * S2);
+    uint4 h0 = make_uint4(0u, 0u, 0u, 0u), h1 = h0;
+    Group<uint32_t, K> fs, ts;
+    if (uni_max) {
+      h0 = *reinterpret_cast<const uint4*>(s);
+      h1 = *reinterpret_cast<const uint4*>(s + 4);
+      fs = load_group<uint32_t, K>(reinterpret_cast<const unsigned char*>(s + kS2Fs));
+      ts = load_group<uint32_t, K>(reinterpret_cast<const unsigned char*>(s + kS2Fs + K));
+    }
     const uint64_t feas_b = ballot(mask != 0ull);
     if (feas_b == 0) continue;  // no pod of the wave can use any node of the block
     uint64_t fast_b = 0, u_b = 0;
-    // node-lane summary, kept for the per-pod pass (read back with v_readlane)
-    uint4 h0 = make_uint4(0u, 0u, 0u, 0u);
-    Group<uint32_t, K> fs;
     if (uni_max) {
-      const uint32_t* s = reinterpret_cast<const uint32_t*>(sum2 + (size_t)(valid ? n : nb) * S2);
-      h0 = *reinterpret_cast<const uint4*>(s);
-      const uint4 h1 = *reinterpret_cast<const uint4*>(s + 4);
       const double stat = __longlong_as_double((long long)((uint64_t)h0.x | ((uint64_t)h0.y << 32)));
       const uint32_t ck = h0.z, meta = h0.w, bw = h1.x, core = h1.y, pw = h1.z;
       const uint32_t cnt = (meta >> 8) & 0xffu;
@@ -825,9 +850,6 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
       const uint32_t shared = (uint32_t)((float)bw * u_bw) + (uint32_t)((float)ck * u_bw) +
                               2u * (uint32_t)((float)core * u_core) +
                               (uint32_t)((float)pw * u_pow);
-      fs = load_group<uint32_t, K>(reinterpret_cast<const unsigned char*>(s + kS2Fs));
-      const Group<uint32_t, K> ts = load_group<uint32_t, K>(
-          reinterpret_cast<const unsigned char*>(s + kS2Fs + K));
       uint32_t nq_lo = 0, nq_hi = 0;  // qualifying cards for the largest / smallest m
 #pragma unroll
       for (int t = 0; t < K; ++t) {
@@ -1100,8 +1122,9 @@ __global__ __launch_bounds__(kBlock) void k2_score_generic(
     const uint64_t* __restrict__ maxima, uint32_t n_pods, const uint64_t* __restrict__ bm,
     uint32_t bm_stride, int64_t* __restrict__ pbest, uint32_t* __restrict__ pidx,
     uint32_t* __restrict__ pties, int64_t* __restrict__ plow, int64_t* __restrict__ rows) {
-  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t chunk = blockIdx.y;
+  const Tile tl = tile();
+  const uint32_t p = tl.pb * kBlock + threadIdx.x;
+  const uint32_t chunk = tl.chunk;
   const uint32_t n0 = chunk * chunk_nodes;
   const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
   const bool live = p < n_pods;
@@ -1155,8 +1178,9 @@ __global__ __launch_bounds__(kBlock) void k2_diskio(const NodeRecB* __restrict__
                                                     double* __restrict__ plow,
                                                     int64_t* __restrict__ rows) {
 #pragma clang fp contract(off)
-  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t chunk = blockIdx.y;
+  const Tile tl = tile();
+  const uint32_t p = tl.pb * kBlock + threadIdx.x;
+  const uint32_t chunk = tl.chunk;
   const uint32_t n0 = chunk * chunk_nodes;
   const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
   const bool live = p < n_pods;

@@ -72,6 +72,38 @@ def main():
         k1["part"] += int((~feas_none & ~is_all).sum())
     tot = sum(k1.values())
     print("K1 (wave, node) pairs:", {k: f"{v / tot:.4f}" for k, v in k1.items()})
+    # K2: needs every pod's feasibility and maxima (the C oracle, sorted order)
+    import oracle
+    res = oracle.schedule(nodes, pods.take(order), 0, threads=8)
+    mx = res.maxima  # [P][6] in collection.go order: bw, clock, core, free, power, total
+    key_m = mx[:, [0, 2, 3, 4, 5]]
+    k2 = {"skip": 0, "u": 0, "fast": 0, "exact": 0}
+    uni_waves = 0
+    for w0 in range(0, P, 64):
+        sl = slice(w0, min(w0 + 64, P))
+        mm, cc = m[sl], c[sl]
+        nu, nm, nc = number[sl], need_m[sl], need_c[sl]
+        hidx = np.clip(nm, 1, K + 1) - 1
+        feas = ((nu[:, None] <= cn[None, :])
+                & ((nm[:, None] == 0) | (hfs[:, hidx].T > mm[:, None]))
+                & ((nc[:, None] == 0) | ((ck[None, :] == cc[:, None]) & (nh[None, :] >= nc[:, None]))))
+        anyf = feas.any(axis=0)
+        allf = feas.all(axis=0)
+        uni = (key_m[sl] == key_m[sl][0]).all()
+        uni_waves += uni
+        k2["skip"] += int((~anyf).sum())
+        if not uni:
+            k2["exact"] += int(anyf.sum())
+            continue
+        nq_lo = (fs >= mm.max()).sum(axis=1)
+        nq_hi = (fs >= mm.min()).sum(axis=1)
+        qall, qnone = ck >= cc.max(), ck < cc.min()
+        u = allf & (nq_lo == nq_hi) & (qall | qnone)
+        k2["u"] += int(u.sum())
+        k2["fast"] += int((anyf & ~u).sum())
+    tot = sum(k2.values())
+    print("K2 (wave, node) pairs:", {k: f"{v / tot:.4f}" for k, v in k2.items()},
+          f"uniform-maxima waves {uni_waves}/{(P + 63) // 64}")
 
 
 if __name__ == "__main__":

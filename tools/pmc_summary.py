@@ -11,10 +11,11 @@ from collections import defaultdict
 
 def short(name: str) -> str:
     n = name.split("(")[0]
-    for k in ("k1_filter_maxima", "k2_score", "k2_diskio", "k_reduce1", "k_reduce2",
-              "k_prep2", "k_finalize", "k3_exact_normalize"):
+    for k in ("k1_block_n32", "k2_block_n32", "k1_filter_maxima", "k2_score", "k2_diskio",
+              "k_reduce1", "k_reduce2", "k_prep2", "k_finalize", "k3_exact_normalize",
+              "k_order_keys", "k_permute"):
         if k in n:
-            return k + (n[n.index("<"):] if "<" in n else "")
+            return k
     return n
 
 
