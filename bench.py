@@ -124,6 +124,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true",
+                    help="N>1: rank 0 re-evaluates the batch on one unsharded handle and "
+                         "asserts identical picks / statuses / ties (rehearsal)")
     ap.add_argument("--workload", choices=["eval", "greedy"], default="eval",
                     help="eval: the headline batch (config 3); greedy: config 5 sequential assume")
     args = ap.parse_args()
@@ -136,18 +139,25 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    device = torch.device("cuda", local_rank)
+    # Rehearsal knobs (one-GPU boxes): YODA_BENCH_SAME_DEVICE=1 puts every rank on cuda:0,
+    # YODA_DIST_BACKEND=gloo exchanges over gloo.  The driver's runs use neither (RCCL).
+    dev_index = 0 if os.environ.get("YODA_BENCH_SAME_DEVICE") == "1" else local_rank
+    device = torch.device("cuda", dev_index)
     torch.cuda.set_device(device)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        backend = os.environ.get("YODA_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     nodes, pods = synth.make_config(args.config, pods=args.pods, nodes=args.nodes)
     P, N = pods.n_pods, nodes.n_nodes
     from yoda_amd.dist import ShardExchange, shard_bounds
     b = shard_bounds(N, world)
     lo, hi = int(b[rank]), int(b[rank + 1])
-    y = Yoda(local_rank)
+    y = Yoda(dev_index)
     shard = nodes.slice(lo, hi)
     y.upload_nodes(shard, node_offset=lo)
     y.upload_pods(pods)
@@ -240,6 +250,15 @@ def main():
         "e2e_ms": e2e_ms,
         "status_counts": {str(s): int((res.status == s).sum()) for s in np.unique(res.status)},
     }
+    if world > 1 and args.check and rank == 0:
+        full = Yoda(dev_index)
+        full.upload_nodes(nodes)
+        ref = full.eval(pods, mode)
+        full.close()
+        for f in ("pick", "status", "n_ties", "n_feasible"):
+            if not np.array_equal(getattr(res, f), getattr(ref, f)):
+                raise SystemExit(f"--check: sharded {f} differs from the unsharded handle")
+        out["check"] = "sharded picks/statuses/ties/feasible == unsharded"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(nodes, pods, mode, args.cpu_seconds,
                                            args.cpu_threads, res)
