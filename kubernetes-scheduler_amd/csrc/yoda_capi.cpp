@@ -23,8 +23,8 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                      uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                      uint32_t n_pods, const Partials& part, uint64_t* bm, uint32_t bm_stride,
                      hipStream_t s);
-hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uint64_t* maxima,
-                          uint32_t* counts, hipStream_t s);
+hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool narrow,
+                          uint64_t* maxima, uint32_t* counts, hipStream_t s);
 hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
                         hipStream_t s);
 hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigned char* sum2,
@@ -476,7 +476,8 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts) {
     HIP_TRY(h, hipEventRecord(e1, h->stream));
     h->ev_k1.emplace_back(e0, e1);
   }
-  HIP_TRY(h, launch_reduce1(part, h->C1, P, maxima, counts, h->stream));
+  // the block-classified K1 (N32) writes u32 maxima partials
+  HIP_TRY(h, launch_reduce1(part, h->C1, P, h->has_k1sum, maxima, counts, h->stream));
   return YODA_OK;
 }
 

@@ -446,8 +446,9 @@ __global__ __launch_bounds__(kBlock) void k1_block_n32(
   mx[kMaxTotal] = max(mx[kMaxTotal], a_tot);
   nf += nf_all;
   nz += nz_all;
+  uint32_t* pmax32 = reinterpret_cast<uint32_t*>(pmax);  // N32: u32 partials (k_reduce1<true>)
 #pragma unroll
-  for (int f = 0; f < 6; ++f) pmax[((size_t)f * C + chunk) * n_pods + p] = (uint64_t)mx[f];
+  for (int f = 0; f < 6; ++f) pmax32[((size_t)f * C + chunk) * n_pods + p] = mx[f];
   pcnt[((size_t)0 * C + chunk) * n_pods + p] = nf;
   pcnt[((size_t)1 * C + chunk) * n_pods + p] = nz;
 }
@@ -458,28 +459,44 @@ __device__ __forceinline__ bool bm_bit(const uint64_t* __restrict__ bm, uint32_t
   return (bm[(size_t)(p >> 6) * bm_stride + n] >> (p & 63u)) & 1ull;
 }
 
-// Per-pod merge of K1 chunk partials -> maxima [6][P] and counts [2][P].
+// Per-pod merge of K1 chunk partials -> maxima [6][P] and counts [2][P].  One thread per
+// (pod, field) (grid.y = the 6 maxima + 2 counts), chunk loads unrolled so each thread keeps
+// several in flight.  NARROW: u32 maxima partials (the N32 K1).
+template <bool NARROW>
 __global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__ pmax,
                                                     const uint32_t* __restrict__ pcnt, uint32_t C,
                                                     uint32_t n_pods,
                                                     uint64_t* __restrict__ maxima,
                                                     uint32_t* __restrict__ counts) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t f = blockIdx.y;
   if (p >= n_pods) return;
-  for (int f = 0; f < 6; ++f) {
+  if (f < 6) {
     uint64_t mx = 1;
-    for (uint32_t c = 0; c < C; ++c) mx = umax64(mx, pmax[((size_t)f * C + c) * n_pods + p]);
+    if constexpr (NARROW) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(pmax) + (size_t)f * C * n_pods + p;
+      uint32_t m32 = 1;
+#pragma unroll 8
+      for (uint32_t c = 0; c < C; ++c) m32 = max(m32, src[(size_t)c * n_pods]);
+      mx = m32;
+    } else {
+      const uint64_t* src = pmax + (size_t)f * C * n_pods + p;
+#pragma unroll 8
+      for (uint32_t c = 0; c < C; ++c) mx = umax64(mx, src[(size_t)c * n_pods]);
+    }
     maxima[(size_t)f * n_pods + p] = mx;
-  }
-  for (int f = 0; f < 2; ++f) {
+  } else {
+    const uint32_t* src = pcnt + (size_t)(f - 6) * C * n_pods + p;
     uint32_t s = 0;
-    for (uint32_t c = 0; c < C; ++c) s += pcnt[((size_t)f * C + c) * n_pods + p];
-    counts[(size_t)f * n_pods + p] = s;
+#pragma unroll 8
+    for (uint32_t c = 0; c < C; ++c) s += src[(size_t)c * n_pods];
+    counts[(size_t)(f - 6) * n_pods + p] = s;
   }
 }
 
 // Wave-per-pod variant of k_reduce1 for many chunks (small pod batches, e.g. the greedy
 // single-pod fallback): the 64 lanes stride over the chunks, then a shuffle reduction.
+template <bool NARROW>
 __global__ __launch_bounds__(kWave) void k_reduce1_wave(const uint64_t* __restrict__ pmax,
                                                          const uint32_t* __restrict__ pcnt,
                                                          uint32_t C, uint32_t n_pods,
@@ -488,8 +505,10 @@ __global__ __launch_bounds__(kWave) void k_reduce1_wave(const uint64_t* __restri
   const uint32_t p = blockIdx.x, lane = threadIdx.x;
   for (int f = 0; f < 6; ++f) {
     uint64_t mx = 1;
-    for (uint32_t c = lane; c < C; c += kWave)
-      mx = umax64(mx, pmax[((size_t)f * C + c) * n_pods + p]);
+    for (uint32_t c = lane; c < C; c += kWave) {
+      const size_t o = ((size_t)f * C + c) * n_pods + p;
+      mx = umax64(mx, NARROW ? (uint64_t)reinterpret_cast<const uint32_t*>(pmax)[o] : pmax[o]);
+    }
     for (int o = kWave / 2; o > 0; o >>= 1) mx = umax64(mx, __shfl_xor(mx, o, kWave));
     if (lane == 0) maxima[(size_t)f * n_pods + p] = mx;
   }
@@ -888,8 +907,9 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
       const int j = __builtin_ctzll(part_b);
       part_b &= part_b - 1;
       const uint32_t nn = nb + (uint32_t)j;
-      const uint64_t mj = ((uint64_t)uniform_u32(__shfl((uint32_t)(mask >> 32), j, kWave)) << 32) |
-                          uniform_u32(__shfl((uint32_t)mask, j, kWave));
+      const uint64_t mj =
+          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mask >> 32), j) << 32) |
+          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mask, j);
       double raw;
       if ((fast_b >> j) & 1ull) {
         // one-model node: nq qualifying cards (a prefix of the free order), then
@@ -1583,14 +1603,24 @@ int kernel_capacity(int K, Path path, int which, int mode_diskio) {
 // chunks, one wave per pod (strided over chunks) when there are many.
 constexpr uint32_t kWaveReduceChunks = 48;
 
-hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uint64_t* maxima,
-                          uint32_t* counts, hipStream_t s) {
-  if (C > kWaveReduceChunks)
-    hipLaunchKernelGGL(k_reduce1_wave, dim3(n_pods), dim3(kWave), 0, s, part.max_u, part.cnt, C,
-                       n_pods, maxima, counts);
-  else
-    hipLaunchKernelGGL(k_reduce1, pod_grid(n_pods), dim3(kBlock), 0, s, part.max_u, part.cnt, C,
-                       n_pods, maxima, counts);
+hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool narrow,
+                          uint64_t* maxima, uint32_t* counts, hipStream_t s) {
+  if (C > kWaveReduceChunks) {
+    if (narrow)
+      hipLaunchKernelGGL(k_reduce1_wave<true>, dim3(n_pods), dim3(kWave), 0, s, part.max_u,
+                         part.cnt, C, n_pods, maxima, counts);
+    else
+      hipLaunchKernelGGL(k_reduce1_wave<false>, dim3(n_pods), dim3(kWave), 0, s, part.max_u,
+                         part.cnt, C, n_pods, maxima, counts);
+  } else {
+    const dim3 grid((n_pods + kBlock - 1) / kBlock, 8);
+    if (narrow)
+      hipLaunchKernelGGL(k_reduce1<true>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
+                         n_pods, maxima, counts);
+    else
+      hipLaunchKernelGGL(k_reduce1<false>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
+                         n_pods, maxima, counts);
+  }
   return hipGetLastError();
 }
 
