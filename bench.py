@@ -42,6 +42,33 @@ def bytes_per_pair(k: int, mode: int) -> int:
     return 16 if mode == MODE_DISKIO else 32 * k + 40
 
 
+def kernel_names(path: str, mode: int):
+    """(K1, K2) kernel names of a record path, as rocprofv3 / tools/pmc_summary.py name them."""
+    if mode == MODE_DISKIO:
+        return "k_fill_diskio_state", "k2_diskio"
+    return {"n32": ("k1_block_n32", "k2_block_n32"),
+            "f64": ("k1_filter_maxima", "k2_score"),
+            "u64": ("k1_filter_maxima", "k2_score_generic")}[path]
+
+
+def committed_pmc(kernel: str, P: int, N: int, world: int) -> dict:
+    """PMC-derived per-launch figures of `kernel` from the committed rocprofv3 summary of
+    this same workload (profiles/pmc_latest.json, written by tools/profile.sh +
+    tools/pmc_summary.py: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, in bytes).  Only
+    used when it was taken on the same P x N at one GPU; {} otherwise."""
+    path = os.path.join(REPO, "profiles", "pmc_latest.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return {}
+    meta = d.get("_workload", {})
+    if (meta.get("pods"), meta.get("nodes"), world) != (P, N, 1):
+        return {}
+    out = dict(d.get(kernel, {}))
+    out["_source"] = "profiles/pmc_latest.json (" + meta.get("profile", "?") + ")"
+    return out
+
+
 def cpu_baseline(nodes, pods, mode, target_s: float, threads: int, gpu_res):
     """Time the C oracle (scalar, reference-shaped) on a bounded pod sample; also checks the
     sample's picks against the GPU's (the oracle is the checker here)."""
@@ -209,16 +236,11 @@ def main():
     # dominant kernel of this rank: K2 (score) unless K1 takes longer
     k1_avg = k1_ms / max(launches, 1)
     k2_avg = k2_ms / max(launches, 1)
-    dom, dom_ms = ("k2_score", k2_avg) if k2_avg >= k1_avg else ("k1_filter_maxima", k1_avg)
+    names = kernel_names(y.path, mode)
+    dom, dom_ms = (names[1], k2_avg) if k2_avg >= k1_avg else (names[0], k1_avg)
     algo_bytes = P * n_local * bytes_per_pair(k_slots, mode)
     achieved = algo_bytes / (dom_ms / 1e3) / 1e9 if dom_ms > 0 else 0.0
-    traffic = None
-    pmc = os.path.join(REPO, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    pmc = committed_pmc(dom, P, N, world)
 
     out = {
         "metric": "pod-node pair evals/sec (filter+score+select) at 100k×100k; bit-exact picks",
@@ -243,10 +265,21 @@ def main():
                    "parallelism": f"node-shard x{world}" + (" (RCCL all-reduce merge)"
                                                             if world > 1 else "")},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": pmc.get("hbm_bytes_per_launch"),
                      "avg_launch_ms": dom_ms, "k1_avg_ms": k1_avg, "k2_avg_ms": k2_avg,
                      "bytes_per_pair": bytes_per_pair(k_slots, mode),
-                     "pairs_per_launch": P * n_local},
+                     "pairs_per_launch": P * n_local,
+                     # achieved > peak: a node record is consulted once per 64-pod wave,
+                     # not once per pair; the binding limits are these:
+                     "traffic_gbs": (pmc["hbm_bytes_per_launch"] / (dom_ms / 1e3) / 1e9
+                                     if pmc.get("hbm_bytes_per_launch") and dom_ms > 0
+                                     else None),
+                     "issue": {k: pmc[k] for k in ("valu_issue_util", "salu_issue_util",
+                                                   "wave_frac_waitcnt",
+                                                   "wave_frac_issue_stall",
+                                                   "wave_frac_issuing") if k in pmc},
+                     "pmc_source": pmc.get("_source")},
         "e2e_ms": e2e_ms,
         "status_counts": {str(s): int((res.status == s).sum()) for s in np.unique(res.status)},
     }

@@ -11,7 +11,8 @@ from collections import defaultdict
 
 def short(name: str) -> str:
     n = name.split("(")[0]
-    for k in ("k1_block_n32", "k2_block_n32", "k1_filter_maxima", "k2_score", "k2_diskio",
+    for k in ("k1_block_n32", "k2_block_n32", "k1_filter_maxima", "k2_score_generic",
+              "k2_score", "k2_diskio",
               "k_reduce1", "k_reduce2", "k_prep2", "k_finalize", "k3_exact_normalize",
               "k_order_keys", "k_permute"):
         if k in n:
@@ -26,6 +27,14 @@ def main(out):
         for r in csv.DictReader(open(path)):
             res[short(r["Name"])]["avg_ns"] = float(r["AverageNs"])
             res[short(r["Name"])]["calls"] = int(r["Calls"])
+    # per-dispatch durations of the trace pass: the median drops a cold first launch
+    for path in glob.glob(os.path.join(out, "trace", "**", "*kernel_trace.csv"), recursive=True):
+        durs = defaultdict(list)
+        for r in csv.DictReader(open(path)):
+            durs[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        for k, v in durs.items():
+            v.sort()
+            res[k]["median_ns"] = float(v[len(v) // 2])
     for path in glob.glob(os.path.join(out, "*", "**", "*counter_collection.csv"), recursive=True):
         acc = defaultdict(lambda: defaultdict(list))
         for r in csv.DictReader(open(path)):
@@ -44,6 +53,29 @@ def main(out):
             d["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             d["hbm_bytes_per_launch"] = d["hbm_read_bytes_corrected_x2"] + d["hbm_write_bytes"]
+        if d.get("GRBM_GUI_ACTIVE"):
+            # GRBM_GUI_ACTIVE sums the 8 XCDs (MI355X_MICROARCH.md, DVFS item): kernel cycles
+            cyc = d["GRBM_GUI_ACTIVE"] / 8.0
+            d["kernel_cycles"] = cyc
+            if "SQ_INSTS_VALU" in d:  # a wave64 VALU op occupies a SIMD-32 for 2 cycles
+                d["valu_issue_util"] = d["SQ_INSTS_VALU"] * 2.0 / (1024 * cyc)
+            if "SQ_INSTS_SALU" in d:  # one scalar unit per CU
+                d["salu_issue_util"] = d["SQ_INSTS_SALU"] / (256 * cyc)
+        if d.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in d:
+            w = d["SQ_WAVE_CYCLES"]
+            d["wave_frac_waitcnt"] = d["SQ_WAIT_ANY"] / w         # parked on memory / LDS
+            d["wave_frac_issue_stall"] = d.get("SQ_WAIT_INST_ANY", 0.0) / w
+            d["wave_frac_issuing"] = d.get("SQ_ACTIVE_INST_ANY", 0.0) / w
+    # the workload the profiled bench ran (its JSON line in the trace pass's log)
+    try:
+        for line in open(os.path.join(out, "trace.log")):
+            if line.startswith("{"):
+                cfg = json.loads(line)["config"]
+                res["_workload"] = {"pods": cfg["pods"], "nodes": cfg["nodes"],
+                                    "path": cfg.get("path"),
+                                    "profile": os.path.basename(os.path.normpath(out))}
+    except (OSError, ValueError, KeyError):
+        pass
     json.dump(res, sys.stdout, indent=1, sort_keys=True)
 
 
