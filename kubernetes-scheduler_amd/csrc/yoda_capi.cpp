@@ -22,13 +22,13 @@ namespace yoda {
 hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigned char* sum,
                      uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                      uint32_t n_pods, const Partials& part, uint64_t* bm, uint32_t bm_stride,
-                     hipStream_t s);
+                     uint64_t* blk, uint32_t blk_stride, hipStream_t s);
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool narrow,
                           uint64_t* maxima, uint32_t* counts, hipStream_t s);
 hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
                         hipStream_t s);
 hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigned char* sum2,
-                     uint32_t n_nodes,
+                     const uint64_t* blk, uint32_t blk_stride, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
                      const double* rcp, const float* rcp32, uint32_t n_pods,
                      const uint64_t* bm, uint32_t bm_stride, const Partials& part,
@@ -188,6 +188,8 @@ struct yoda_handle {
   // state
   DevBuf maxima, counts, rcp, rcp32, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
   DevBuf bitmask, bitmask_t, rows, rows_t;
+  DevBuf blk;               // [wave][node block / 64] u64: blocks with a feasible pod (K1 -> K2)
+  bool blk_valid = false;   // the last K1 wrote blk (block-classified K1 on this batch)
   // greedy
   DevBuf tk_s_part, tk_i_part, tk_s, tk_i, upd_node, upd_val, upd_cn;
   PinnedBuf upd_stage, pick_stage;
@@ -225,7 +227,7 @@ struct yoda_handle {
                      &pod_sorted, &perm,     &order_scratch, &unperm,
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
-                     &n_flagged, &bitmask,   &bitmask_t,  &p_max_u,      &p_cnt,
+                     &n_flagged, &bitmask,   &bitmask_t,  &blk,  &p_max_u,      &p_cnt,
                      &rows,      &rows_t,    &tk_s_part,  &tk_i_part,    &tk_s,
                      &tk_i,      &upd_node,  &upd_val,    &upd_cn,
                      &p_best_f,  &p_best_i,  &p_idx,      &p_ties,       &p_low_f,
@@ -319,6 +321,7 @@ int ensure_state(yoda_t* h, uint32_t P) {
   HIP_TRY(h, h->n_flagged.ensure(16));
   // [wave][node] u64 masks (yoda_layout.h), +8 words: K2 reads masks in groups of 8
   HIP_TRY(h, h->bitmask.ensure(((size_t)(P + 63) / 64 * bm_row(h->n_nodes) + 8) * 8));
+  HIP_TRY(h, h->blk.ensure((size_t)(P + 63) / 64 * blk_row(h->n_nodes) * 8));
   HIP_TRY(h, h->p_max_u.ensure(6 * CP * 8));
   if (h->generic) {
     HIP_TRY(h, h->p_best_i.ensure(CP * 8));
@@ -468,10 +471,15 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts) {
   hipEvent_t e0 = h->profiling ? h->next_event() : nullptr;
   hipEvent_t e1 = h->profiling ? h->next_event() : nullptr;
   if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
+  h->blk_valid = h->has_k1sum;
+  if (h->blk_valid)
+    HIP_TRY(h, hipMemsetAsync(h->blk.p, 0, (size_t)(P + 63) / 64 * blk_row(h->n_nodes) * 8,
+                              h->stream));
   HIP_TRY(h, launch_k1(h->K, h->path, h->nodes.as<unsigned char>(),
                        h->has_k1sum ? h->k1sum.as<unsigned char>() : nullptr, h->n_nodes,
                        h->chunk1, h->C1, pod_params(h), P, part, h->bitmask.as<uint64_t>(),
-                       bm_row(h->n_nodes), h->stream));
+                       bm_row(h->n_nodes), h->blk.as<uint64_t>(), blk_row(h->n_nodes),
+                       h->stream));
   if (e1) {
     HIP_TRY(h, hipEventRecord(e1, h->stream));
     h->ev_k1.emplace_back(e0, e1);
@@ -508,7 +516,9 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, int64_t* best, uint32_t*
                                 pod_params(h), P, part, rows, h->stream));
   } else {
     HIP_TRY(h, launch_k2(h->K, h->path, h->nodes.as<unsigned char>(),
-                         h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr, h->n_nodes,
+                         h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr,
+                         h->blk_valid ? h->blk.as<uint64_t>() : nullptr, blk_row(h->n_nodes),
+                         h->n_nodes,
                          h->chunk2, h->C2, pod_params(h), maxima, h->rcp.as<double>(),
                          h->rcp32.as<float>(), P, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
                          part, rows, h->stream));

@@ -15,6 +15,7 @@
 //   K3  k3_exact_normalize scheduler.go:176-179 with int64 wrap (generic path only)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include "yoda_layout.h"
 
@@ -288,7 +289,8 @@ __global__ __launch_bounds__(kBlock) void k1_block_n32(
     const uint32_t* __restrict__ c_in, const uint64_t* __restrict__ number_in,
     const uint32_t* __restrict__ need_mem_in, const uint32_t* __restrict__ need_clk_in,
     uint32_t n_pods, uint64_t* __restrict__ pmax, uint32_t* __restrict__ pcnt,
-    uint64_t* __restrict__ bm, uint32_t bm_stride) {
+    uint64_t* __restrict__ bm, uint32_t bm_stride, uint64_t* __restrict__ blk,
+    uint32_t blk_stride) {
   constexpr uint32_t SS = k1sum_stride(K);
   constexpr uint32_t NS = n32_stride(K);
   constexpr uint32_t HW = K + 1;  // LDS words per node: hfs[0..K-1], 0
@@ -344,6 +346,15 @@ __global__ __launch_bounds__(kBlock) void k1_block_n32(
   // node-lane maxima of the ALL nodes (their contribution is the same for every pod lane)
   uint32_t a_bw = 0, a_ck = 0, a_core = 0, a_free = 0, a_pw = 0, a_tot = 0;
   uint32_t nf_all = 0, nz_all = 0;
+  // blocks with a feasible pod of this wave, for K2 (bit b of word b/64; flushed with an
+  // atomic OR when the word changes -- neighbouring chunks may share a word)
+  uint64_t* blkw = blk + (size_t)uniform_u32(p >> 6) * blk_stride;
+  uint32_t blk_wi = (n0 >> 6) >> 6;
+  uint64_t blk_bits = 0;
+  auto blk_flush = [&]() {
+    if (blk_bits != 0 && lane == 0)
+      atomicOr(reinterpret_cast<unsigned long long*>(blkw + blk_wi), (unsigned long long)blk_bits);
+  };
 
   for (uint32_t nb = n0; nb < n1; nb += kWave) {
     const uint32_t n = nb + lane;
@@ -429,7 +440,17 @@ __global__ __launch_bounds__(kBlock) void k1_block_n32(
       set_lane(lo, hi, b, (uint32_t)j);
     }
     bm_store(bmw, nb, n1, lo, hi);
+    if (ballot(valid && (lo | hi) != 0u) != 0) {
+      const uint32_t bi = nb >> 6;
+      if ((bi >> 6) != blk_wi) {
+        blk_flush();
+        blk_wi = bi >> 6;
+        blk_bits = 0;
+      }
+      blk_bits |= 1ull << (bi & 63u);
+    }
   }
+  blk_flush();
   // fold the ALL nodes into every pod lane
   a_bw = wave_max_u32(a_bw);
   a_ck = wave_max_u32(a_ck);
@@ -805,7 +826,8 @@ template <int K>
 __global__ __launch_bounds__(kBlock) void k2_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum2,
     uint32_t n_nodes, uint32_t chunk_nodes, ScoreArgs args, uint32_t n_pods,
-    const uint64_t* __restrict__ bm, uint32_t bm_stride, double* __restrict__ pbest,
+    const uint64_t* __restrict__ bm, uint32_t bm_stride, const uint64_t* __restrict__ blk,
+    uint32_t blk_stride, double* __restrict__ pbest,
     uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties, double* __restrict__ plow) {
   constexpr uint32_t S2 = k2sum_stride(K), NS = n32_stride(K);
   constexpr uint32_t PSW = K + 2;  // LDS words per node: prefix[0..K], shared
@@ -841,23 +863,21 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
   uint32_t idx = 0xffffffffu, ties = 0;
   double ubest = -1.0, ulow = 1.0e300;      // node lane (U nodes)
   uint32_t uidx = 0xffffffffu, uties = 0;
-  for (uint32_t nb = n0; nb < n1; nb += kWave) {
+  // One block: the wave's mask of node nb + lane and its summary (kept for the per-pod pass,
+  // read back with v_readlane), loaded together: one memory latency per block.
+  auto block = [&](uint32_t nb) {
     const uint32_t n = nb + lane;
     const bool valid = n < n1;
     const uint64_t mask = valid ? bmw[n] : 0ull;
-    // node-lane summary, kept for the per-pod pass (read back with v_readlane); issued
-    // together with the mask load so the block pays one memory latency, not two
     const uint32_t* s = reinterpret_cast<const uint32_t*>(sum2 + (size_t)(valid ? n : nb) * S2);
-    uint4 h0 = make_uint4(0u, 0u, 0u, 0u), h1 = h0;
-    Group<uint32_t, K> fs, ts;
-    if (uni_max) {
-      h0 = *reinterpret_cast<const uint4*>(s);
-      h1 = *reinterpret_cast<const uint4*>(s + 4);
-      fs = load_group<uint32_t, K>(reinterpret_cast<const unsigned char*>(s + kS2Fs));
-      ts = load_group<uint32_t, K>(reinterpret_cast<const unsigned char*>(s + kS2Fs + K));
-    }
+    const uint4 h0 = *reinterpret_cast<const uint4*>(s);
+    const uint4 h1 = *reinterpret_cast<const uint4*>(s + 4);
+    const Group<uint32_t, K> fs =
+        load_group<uint32_t, K>(reinterpret_cast<const unsigned char*>(s + kS2Fs));
+    const Group<uint32_t, K> ts =
+        load_group<uint32_t, K>(reinterpret_cast<const unsigned char*>(s + kS2Fs + K));
     const uint64_t feas_b = ballot(mask != 0ull);
-    if (feas_b == 0) continue;  // no pod of the wave can use any node of the block
+    if (feas_b == 0) return;  // no pod of the wave can use any node of the block
     uint64_t fast_b = 0, u_b = 0;
     if (uni_max) {
       const double stat = __longlong_as_double((long long)((uint64_t)h0.x | ((uint64_t)h0.y << 32)));
@@ -902,6 +922,9 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
         ulow = fmin(ulow, raw);
       }
     }
+    // waves whose pods do not share their maxima: one-model nodes are still scored from the
+    // node lane's summary, each pod lane with its own reciprocals (no record round trip)
+    const uint64_t own_b = uni_max ? 0ull : ballot(mask != 0ull && (h0.w & kSumUni4) != 0u);
     uint64_t part_b = feas_b & ~u_b;
     while (part_b) {  // wave-uniform loop over the remaining feasible nodes
       const int j = __builtin_ctzll(part_b);
@@ -926,6 +949,31 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
         const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h0.x, j) |
                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h0.y, j) << 32);
         raw = (double)basic + __longlong_as_double((long long)sb);
+      } else if ((own_b >> j) & 1ull) {
+        // Scorer<N32>'s one-model branch on the node lane's data: shared quotients in f32,
+        // memory quotients in f64, over the qualifying prefix of the free order
+        const uint32_t cnt = ((uint32_t)__builtin_amdgcn_readlane((int)h0.w, j) >> 8) & 0xffu;
+        const uint32_t ckj = (uint32_t)__builtin_amdgcn_readlane((int)h0.z, j);
+        const uint32_t shared =
+            (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.x, j) * sc.r_bw) +
+            (uint32_t)((float)ckj * sc.r_bw) +
+            2u * (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.y, j) * sc.r_core) +
+            (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.z, j) * sc.r_pow);
+        uint32_t nq = 0, mem = 0;
+#pragma unroll
+        for (int t = 0; t < K; ++t) {
+          const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)fs.v[t], j);
+          const uint32_t to = (uint32_t)__builtin_amdgcn_readlane((int)ts.v[t], j);
+          const bool q = f >= sc.m && (uint32_t)t < cnt;
+          const uint32_t term = 3u * (uint32_t)((double)f * sc.r_free) +
+                                (uint32_t)((double)to * sc.r_tot);
+          nq += q ? 1u : 0u;
+          mem += q ? term : 0u;
+        }
+        const uint32_t basic = ckj >= sc.c ? nq * shared + mem : 0u;  // algorithm.go:271
+        const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h0.x, j) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h0.y, j) << 32);
+        raw = (double)basic + __longlong_as_double((long long)sb);
       } else {
         raw = sc.template raw<K>(nodes + (size_t)nn * NS);
       }
@@ -940,6 +988,24 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
         low = fmin(low, raw);
       }
     }
+  };
+  if (blk) {
+    // only the blocks K1 found a feasible pod of this wave in (bit b of word b/64)
+    const uint64_t* bw = blk + (size_t)uniform_u32(p >> 6) * blk_stride;
+    const uint32_t b0 = n0 >> 6, b1 = (n1 + 63) >> 6;
+    for (uint32_t wi = b0 >> 6; b0 < b1 && wi <= (b1 - 1) >> 6; ++wi) {
+      uint64_t bits = bw[wi];
+      const uint32_t base = wi << 6;
+      if (b0 > base) bits &= ~0ull << (b0 - base);
+      if (b1 < base + 64) bits &= (1ull << (b1 - base)) - 1ull;
+      while (bits) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(bits);
+        bits &= bits - 1;
+        block((base + j) << 6);
+      }
+    }
+  } else {
+    for (uint32_t nb = n0; nb < n1; nb += kWave) block(nb);
   }
   // merge the U nodes (the same for every pod lane) into each pod lane
   double wb = ubest;
@@ -1535,10 +1601,11 @@ __global__ __launch_bounds__(kBlock) void k_bitmask_transpose(const uint64_t* __
 
 static inline dim3 pod_grid(uint32_t n) { return dim3((n + kBlock - 1) / kBlock); }
 
+
 hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigned char* sum,
                      uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                      uint32_t n_pods, const Partials& part, uint64_t* bm, uint32_t bm_stride,
-                     hipStream_t s) {
+                     uint64_t* blk, uint32_t blk_stride, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   switch (path) {
     case Path::N32:
@@ -1546,7 +1613,8 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
         YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK>), grid, dim3(kBlock), 0, s, nodes,
                                             sum, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
                                             pp.number, pp.need_mem, pp.need_clk, n_pods,
-                                            part.max_u, part.cnt, bm, bm_stride));
+                                            part.max_u, part.cnt, bm, bm_stride, blk,
+                                            blk_stride));
       } else {
         YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_filter_maxima<KK, Path::N32>), grid, dim3(kBlock),
                                             0, s, nodes, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
@@ -1589,7 +1657,9 @@ int kernel_capacity(int K, Path path, int which, int mode_diskio) {
     }
   } else {
     switch (path) {
-      case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k2_block_n32<KK>))); break;
+      case Path::N32:
+        YODA_K_SWITCH(K, YODA_FN((&k2_block_n32<KK>)));
+        break;
       case Path::F64: YODA_K_SWITCH(K, YODA_FN((&k2_score<KK, Path::F64, OUT_ARGMAX>))); break;
       case Path::U64: YODA_K_SWITCH(K, YODA_FN((&k2_score_generic<KK, false>))); break;
     }
@@ -1632,7 +1702,8 @@ hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, fl
 
 template <int OUT>
 static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
-                              const unsigned char* sum2, uint32_t n_nodes,
+                              const unsigned char* sum2, const uint64_t* blk, uint32_t blk_stride,
+                              uint32_t n_nodes,
                               uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                               const uint64_t* maxima, const double* rcp, const float* rcp32,
                               uint32_t n_pods, const uint64_t* bm, uint32_t bm_stride, const Partials& part,
@@ -1644,7 +1715,8 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
       if (OUT == OUT_ARGMAX && sum2) {
         YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK>), grid, dim3(kBlock), 0, s, nodes,
                                             sum2, n_nodes, chunk_nodes, a, n_pods, bm, bm_stride,
-                                            part.best_f, part.idx, part.ties, part.low_f));
+                                            blk, blk_stride, part.best_f, part.idx, part.ties,
+                                            part.low_f));
         break;
       }
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score<KK, Path::N32, OUT>), grid, dim3(kBlock), 0,
@@ -1674,7 +1746,7 @@ hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t
                           const double* rcp, const float* rcp32, uint32_t n_pods,
                           const uint64_t* bm, uint32_t bm_stride, const Partials& part, double* tk_s,
                           uint32_t* tk_i, hipStream_t s) {
-  return launch_k2_t<OUT_TOPK>(K, path, nodes, nullptr, n_nodes, chunk_nodes, C, pp, nullptr, rcp,
+  return launch_k2_t<OUT_TOPK>(K, path, nodes, nullptr, nullptr, 0, n_nodes, chunk_nodes, C, pp, nullptr, rcp,
                                rcp32,
                                n_pods, bm, bm_stride, part, nullptr, tk_s, tk_i, s);
 }
@@ -1705,15 +1777,15 @@ hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32
 int topk_k() { return kTopK; }
 
 hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigned char* sum2,
-                     uint32_t n_nodes,
+                     const uint64_t* blk, uint32_t blk_stride, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
                      const double* rcp, const float* rcp32, uint32_t n_pods,
                      const uint64_t* bm, uint32_t bm_stride, const Partials& part, int64_t* rows,
                      hipStream_t s) {
   if (rows)
-    return launch_k2_t<OUT_ROWS>(K, path, nodes, nullptr, n_nodes, chunk_nodes, C, pp, maxima, rcp,
+    return launch_k2_t<OUT_ROWS>(K, path, nodes, nullptr, nullptr, 0, n_nodes, chunk_nodes, C, pp, maxima, rcp,
                                  rcp32, n_pods, bm, bm_stride, part, rows, nullptr, nullptr, s);
-  return launch_k2_t<OUT_ARGMAX>(K, path, nodes, sum2, n_nodes, chunk_nodes, C, pp, maxima, rcp,
+  return launch_k2_t<OUT_ARGMAX>(K, path, nodes, sum2, blk, blk_stride, n_nodes, chunk_nodes, C, pp, maxima, rcp,
                                  rcp32, n_pods, bm, bm_stride, part, rows, nullptr, nullptr, s);
 }
 

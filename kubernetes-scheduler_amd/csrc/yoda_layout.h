@@ -115,6 +115,12 @@ __host__ __device__ constexpr uint32_t k2sum_stride(int k) { return 32u + 8u * (
 // up to 64.  K1 writes it coalesced (lane = node); K2 reads one wave's mask per node through
 // the scalar path and skips the node when it is 0.
 __host__ __device__ constexpr uint32_t bm_row(uint32_t n_nodes) { return (n_nodes + 63u) & ~63u; }
+// Non-empty node blocks: u64 blk[wave][w], bit b % 64 of word b / 64 set when node block b
+// (nodes 64 b .. 64 b + 63) has a feasible pod of the wave.  Written by the block K1, read by
+// the block K2 to visit only those blocks.
+__host__ __device__ constexpr uint32_t blk_row(uint32_t n_nodes) {
+  return ((n_nodes + 63u) / 64u + 63u) / 64u;
+}
 
 // Mode B node record: V = Cpu/100, U = DiskIO/50 (algorithm.go:71,73).
 struct alignas(16) NodeRecB {
