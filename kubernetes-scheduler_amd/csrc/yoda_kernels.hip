@@ -831,7 +831,8 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
     uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties, double* __restrict__ plow) {
   constexpr uint32_t S2 = k2sum_stride(K), NS = n32_stride(K);
   constexpr uint32_t PSW = K + 2;  // LDS words per node: prefix[0..K], shared
-  __shared__ uint32_t lds_all[kBlock / kWave][kWave * PSW];
+  constexpr uint32_t TAB = kWave * PSW;  // one table: 64 nodes
+  __shared__ uint32_t lds_all[kBlock / kWave][2 * TAB];
   const uint32_t lane = lane_id();
   uint32_t* lds = lds_all[threadIdx.x >> 6];
   const Tile tl = tile();
@@ -855,7 +856,25 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
       __longlong_as_double((long long)uniform_u64((uint64_t)__double_as_longlong(sc.r_tot)));
   const bool same = sc.r_bw == u_bw && sc.r_core == u_core && sc.r_pow == u_pow &&
                     sc.r_free == u_free && sc.r_tot == u_tot;
-  const bool uni_max = ballot(!live || same) == ~0ull;
+  const uint64_t same_b = ballot(!live || same);
+  const bool uni_max = same_b == ~0ull;
+  // Otherwise a second reciprocal set (the first lane that differs from lane 0): lanes of
+  // either set read prefix tables from LDS, the rest (grp 2) compute with their own.
+  const int l1 = uni_max ? 0 : __builtin_ctzll(~same_b);
+  auto rl_f = [&](float x) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l1));
+  };
+  auto rl_d = [&](double x) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    return __longlong_as_double((long long)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
+        (int)(uint32_t)b, l1) | ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
+        (int)(uint32_t)(b >> 32), l1) << 32)));
+  };
+  const float v_bw = rl_f(sc.r_bw), v_core = rl_f(sc.r_core), v_pow = rl_f(sc.r_pow);
+  const double v_free = rl_d(sc.r_free), v_tot = rl_d(sc.r_tot);
+  const bool same1 = sc.r_bw == v_bw && sc.r_core == v_core && sc.r_pow == v_pow &&
+                     sc.r_free == v_free && sc.r_tot == v_tot;
+  const uint32_t grp = same ? 0u : (same1 ? 1u : 2u);
   const uint32_t m_max = wave_max_u32(live ? sc.m : 0u), m_min = wave_min_u32(live ? sc.m : ~0u);
   const uint32_t c_max = wave_max_u32(live ? sc.c : 0u), c_min = wave_min_u32(live ? sc.c : ~0u);
 
@@ -878,13 +897,33 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
         load_group<uint32_t, K>(reinterpret_cast<const unsigned char*>(s + kS2Fs + K));
     const uint64_t feas_b = ballot(mask != 0ull);
     if (feas_b == 0) return;  // no pod of the wave can use any node of the block
-    uint64_t fast_b = 0, u_b = 0;
-    if (uni_max) {
+    uint64_t fast_b = ballot(mask != 0ull && (h0.w & kSumUni4) != 0u), u_b = 0;
+    if (!uni_max) {
+      // prefix tables for both reciprocal sets (no U nodes: scores differ across the wave)
+      const uint32_t ck = h0.z, bw = h1.x, core = h1.y, pw = h1.z;
+      uint32_t a0 = 0, a1 = 0;
+      lds[lane * PSW + 0] = 0u;
+      lds[TAB + lane * PSW + 0] = 0u;
+#pragma unroll
+      for (int t = 0; t < K; ++t) {
+        const double f = (double)fs.v[t], to = (double)ts.v[t];
+        a0 += 3u * (uint32_t)(f * u_free) + (uint32_t)(to * u_tot);
+        a1 += 3u * (uint32_t)(f * v_free) + (uint32_t)(to * v_tot);
+        lds[lane * PSW + t + 1] = a0;
+        lds[TAB + lane * PSW + t + 1] = a1;
+      }
+      lds[lane * PSW + K + 1] = (uint32_t)((float)bw * u_bw) + (uint32_t)((float)ck * u_bw) +
+                                2u * (uint32_t)((float)core * u_core) +
+                                (uint32_t)((float)pw * u_pow);
+      lds[TAB + lane * PSW + K + 1] = (uint32_t)((float)bw * v_bw) +
+                                      (uint32_t)((float)ck * v_bw) +
+                                      2u * (uint32_t)((float)core * v_core) +
+                                      (uint32_t)((float)pw * v_pow);
+    } else {
       const double stat = __longlong_as_double((long long)((uint64_t)h0.x | ((uint64_t)h0.y << 32)));
       const uint32_t ck = h0.z, meta = h0.w, bw = h1.x, core = h1.y, pw = h1.z;
       const uint32_t cnt = (meta >> 8) & 0xffu;
       const bool fast = mask != 0ull && (meta & kSumUni4) != 0u;
-      fast_b = ballot(fast);
       // CalculateCardScore terms (algorithm.go:280-291) with the wave's reciprocals
       const uint32_t shared = (uint32_t)((float)bw * u_bw) + (uint32_t)((float)ck * u_bw) +
                               2u * (uint32_t)((float)core * u_core) +
@@ -922,9 +961,6 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
         ulow = fmin(ulow, raw);
       }
     }
-    // waves whose pods do not share their maxima: one-model nodes are still scored from the
-    // node lane's summary, each pod lane with its own reciprocals (no record round trip)
-    const uint64_t own_b = uni_max ? 0ull : ballot(mask != 0ull && (h0.w & kSumUni4) != 0u);
     uint64_t part_b = feas_b & ~u_b;
     while (part_b) {  // wave-uniform loop over the remaining feasible nodes
       const int j = __builtin_ctzll(part_b);
@@ -944,35 +980,31 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
           nq += (uint32_t)((uint32_t)__builtin_amdgcn_readlane((int)fs.v[t], j) >= sc.m);
         nq = min(nq, cnt);
         const uint32_t ckj = (uint32_t)__builtin_amdgcn_readlane((int)h0.z, j);
-        const uint32_t basic =
-            ckj >= sc.c ? nq * lds[(uint32_t)j * PSW + K + 1] + lds[(uint32_t)j * PSW + nq] : 0u;
         const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h0.x, j) |
                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h0.y, j) << 32);
-        raw = (double)basic + __longlong_as_double((long long)sb);
-      } else if ((own_b >> j) & 1ull) {
-        // Scorer<N32>'s one-model branch on the node lane's data: shared quotients in f32,
-        // memory quotients in f64, over the qualifying prefix of the free order
-        const uint32_t cnt = ((uint32_t)__builtin_amdgcn_readlane((int)h0.w, j) >> 8) & 0xffu;
-        const uint32_t ckj = (uint32_t)__builtin_amdgcn_readlane((int)h0.z, j);
-        const uint32_t shared =
+        uint32_t basic;
+        if (grp < 2u) {
+          const uint32_t* tab = lds + grp * TAB + (uint32_t)j * PSW;
+          basic = ckj >= sc.c ? nq * tab[K + 1] + tab[nq] : 0u;
+        } else {
+          // a pod outside both sets: Scorer<N32>'s one-model branch on the node lane's data,
+          // with its own reciprocals (shared quotients f32, memory quotients f64)
+          const uint32_t shared =
             (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.x, j) * sc.r_bw) +
             (uint32_t)((float)ckj * sc.r_bw) +
             2u * (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.y, j) * sc.r_core) +
             (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.z, j) * sc.r_pow);
-        uint32_t nq = 0, mem = 0;
+          uint32_t mem = 0;
 #pragma unroll
-        for (int t = 0; t < K; ++t) {
-          const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)fs.v[t], j);
-          const uint32_t to = (uint32_t)__builtin_amdgcn_readlane((int)ts.v[t], j);
-          const bool q = f >= sc.m && (uint32_t)t < cnt;
-          const uint32_t term = 3u * (uint32_t)((double)f * sc.r_free) +
-                                (uint32_t)((double)to * sc.r_tot);
-          nq += q ? 1u : 0u;
-          mem += q ? term : 0u;
+          for (int t = 0; t < K; ++t) {
+            const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)fs.v[t], j);
+            const uint32_t to = (uint32_t)__builtin_amdgcn_readlane((int)ts.v[t], j);
+            const uint32_t term = 3u * (uint32_t)((double)f * sc.r_free) +
+                                  (uint32_t)((double)to * sc.r_tot);
+            mem += (uint32_t)t < nq ? term : 0u;  // the qualifying cards are a prefix
+          }
+          basic = ckj >= sc.c ? nq * shared + mem : 0u;  // algorithm.go:271
         }
-        const uint32_t basic = ckj >= sc.c ? nq * shared + mem : 0u;  // algorithm.go:271
-        const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h0.x, j) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h0.y, j) << 32);
         raw = (double)basic + __longlong_as_double((long long)sb);
       } else {
         raw = sc.template raw<K>(nodes + (size_t)nn * NS);
