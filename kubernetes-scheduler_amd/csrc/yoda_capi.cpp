@@ -793,7 +793,16 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     HIP_TRY(h, h->nodes.ensure(rec.size()));
     HIP_TRY(h, hipMemcpyAsync(h->nodes.p, rec.data(), rec.size(), hipMemcpyHostToDevice,
                               h->stream));
-    if (want_sum) {
+    if (want_sum) {  // node-major as built -> 64-node tiles (sum_index, yoda_layout.h)
+      auto tiles = [N](const std::vector<uint32_t>& v, uint32_t stride) {
+        std::vector<uint32_t> t(sum_words(std::max<uint32_t>(N, 1), stride), 0u);
+        const uint32_t W = stride / 4u;
+        for (uint32_t i = 0; i < N; ++i)
+          for (uint32_t w = 0; w < W; ++w) t[sum_index(i, w, stride)] = v[(size_t)i * W + w];
+        return t;
+      };
+      sum = tiles(sum, (uint32_t)sstride);
+      sum2 = tiles(sum2, (uint32_t)s2stride);
       HIP_TRY(h, h->k1sum.ensure(sum.size() * 4));
       HIP_TRY(h, hipMemcpyAsync(h->k1sum.p, sum.data(), sum.size() * 4, hipMemcpyHostToDevice,
                                 h->stream));
@@ -864,8 +873,10 @@ int yoda_update_alloc(yoda_t* h, const uint64_t* alloc) {
         max_static = std::max(max_static, s);
         if (h->has_k2sum) {
           const double sd = (double)s;
-          std::memcpy(h->host_k2sum.data() + (size_t)i * k2sum_stride(h->K) / 4 + kS2Static, &sd,
-                      8);
+          uint64_t sb;
+          std::memcpy(&sb, &sd, 8);
+          h->host_k2sum[sum_index(i, kS2Static, k2sum_stride(h->K))] = (uint32_t)sb;
+          h->host_k2sum[sum_index(i, kS2Static + 1, k2sum_stride(h->K))] = (uint32_t)(sb >> 32);
         }
       }
     }

@@ -163,6 +163,44 @@ __device__ __forceinline__ bool k1_node(const unsigned char* rec, typename Rec<P
   return feas;
 }
 
+// k1_node for the block-classified N32 K1's undecided MIXED-model nodes (one-model nodes are
+// decided from the node summary there): the same predicates and maxima, but the maxima
+// fields are read one card at a time, so the rare path holds ~2K + 6 SGPRs instead of 6K
+// and does not push the whole kernel into SGPR spills.
+template <int K>
+__device__ __forceinline__ bool k1_node_lean(const unsigned char* rec, uint32_t m, uint32_t c,
+                                             uint64_t number, uint32_t need_mem,
+                                             uint32_t need_clk, uint32_t (&mx)[6], uint32_t& nf,
+                                             uint32_t& nz) {
+  const NodeHdrG hd = *reinterpret_cast<const NodeHdrG*>(rec);
+  const uint32_t* g = reinterpret_cast<const uint32_t*>(rec + n32_u32_off(0, K));
+  uint32_t cm = 0, cc = 0;
+#pragma unroll 1
+  for (int j = 0; j < K; ++j) {
+    const uint32_t hj = (hd.healthy_mask >> j) & 1u, fj = g[kFree * K + j], cj = g[kClock * K + j];
+    cm += (uint32_t)(fj >= m) & hj;   // CardFitsMemory (filter.go:52-54)
+    cc += (uint32_t)(cj == c) & hj;   // CardFitsClock (filter.go:56-58)
+  }
+  const bool feas = (number <= hd.card_number) & (cm >= need_mem) & (cc >= need_clk);
+  if (feas) {
+    ++nf;
+    nz += hd.zero_total;
+#pragma unroll 1
+    for (int j = 0; j < K; ++j) {
+      const uint32_t fj = g[kFree * K + j], cj = g[kClock * K + j];
+      if ((fj >= m) & (cj >= c)) {  // collection.go:46: no health check, >= clock
+        mx[kMaxBw] = max(mx[kMaxBw], g[kBandwidth * K + j]);
+        mx[kMaxClock] = max(mx[kMaxClock], cj);
+        mx[kMaxCore] = max(mx[kMaxCore], g[kCore * K + j]);
+        mx[kMaxFree] = max(mx[kMaxFree], fj);
+        mx[kMaxPower] = max(mx[kMaxPower], g[kPower * K + j]);
+        mx[kMaxTotal] = max(mx[kMaxTotal], g[kTotal * K + j]);
+      }
+    }
+  }
+  return feas;
+}
+
 __device__ __forceinline__ uint64_t ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & (kWave - 1); }
 __device__ __forceinline__ uint32_t uniform_u32(uint32_t v) {
@@ -203,6 +241,24 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
   return uniform_u64(v);
 }
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) { return ~wave_max_u64(~v); }
+// The same reductions left in VGPRs (every lane holds the result; the compiler does not know
+// it is uniform): for wave bounds that are only VALU operands, so that a kernel with many of
+// them does not run out of SGPRs (spills, lower occupancy).
+__device__ __forceinline__ uint32_t wave_max_u32v(uint32_t v) {
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, kWave));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_min_u32v(uint32_t v) { return ~wave_max_u32v(~v); }
+__device__ __forceinline__ uint64_t wave_max_u64v(uint64_t v) {
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    const uint64_t u = (uint64_t)__shfl_xor((unsigned long long)v, o, kWave);
+    v = v > u ? v : u;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_min_u64v(uint64_t v) { return ~wave_max_u64v(~v); }
 
 // Lane j of (lo, hi) := the 64-bit wave mask b (j wave-uniform).
 __device__ __forceinline__ void set_lane(uint32_t& lo, uint32_t& hi, uint64_t b, uint32_t j) {
@@ -283,7 +339,7 @@ __global__ __launch_bounds__(kBlock) void k1_filter_maxima(
 // approximations: ALL nodes fold their contribution into node-lane maxima that are reduced
 // across the wave once per chunk, and both write their 64-bit masks with one store.
 template <int K>
-__global__ __launch_bounds__(kBlock) void k1_block_n32(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 ? 6 : 8))) void k1_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum,
     uint32_t n_nodes, uint32_t chunk_nodes, const uint32_t* __restrict__ m_in,
     const uint32_t* __restrict__ c_in, const uint64_t* __restrict__ number_in,
@@ -338,6 +394,10 @@ __global__ __launch_bounds__(kBlock) void k1_block_n32(
   const bool hfs_all_ok = nm_max <= (uint32_t)K, hfs_none_ok = nm_min <= (uint32_t)K;
   const uint32_t hfs_all = kSumHfs + (any_pm && hfs_all_ok ? nm_max - 1u : 0u);
   const uint32_t hfs_none = kSumHfs + (hfs_none_ok ? nm_min - 1u : 0u);
+  // Every pod of the wave needs the same number of memory-fitting cards (or none has the
+  // scv/memory label): the per-pod pass reads that card's threshold hfs[need-1] from the
+  // node lane (t_all) instead of an LDS row of all K, and the rows are not staged at all.
+  const bool need_uni = uniform_u32(!any_pm || (all_pm && nm_min == nm_max)) != 0u;
 
   uint32_t mx[6];
 #pragma unroll
@@ -359,16 +419,17 @@ __global__ __launch_bounds__(kBlock) void k1_block_n32(
   for (uint32_t nb = n0; nb < n1; nb += kWave) {
     const uint32_t n = nb + lane;
     const bool valid = n < n1;
-    const uint32_t* s = reinterpret_cast<const uint32_t*>(sum + (size_t)(valid ? n : nb) * SS);
-    const uint4 w0 = *reinterpret_cast<const uint4*>(s);
-    const uint4 w1 = *reinterpret_cast<const uint4*>(s + 4);
-    const uint32_t pw = s[kSumPower];
-    const uint32_t t_all = s[hfs_all], t_none = s[hfs_none];
-    {  // the node's healthy frees for the per-pod pass: lds[node][need - 1] (slot K: 0)
-      const Group<uint32_t, K> hf =
-          load_group<uint32_t, K>(reinterpret_cast<const unsigned char*>(s + kSumHfs));
+    // this block's tile of summaries (nb is a multiple of 64): word w at s[64 w]
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(sum) + sum_index(nb, 0, SS) + lane;
+    const uint4 w0 = make_uint4(s[64 * kSumCnLo], s[64 * kSumCnHi], s[64 * kSumClock],
+                                s[64 * kSumMeta]);
+    const uint4 w1 = make_uint4(s[64 * kSumMrf1], s[64 * kSumTotal], s[64 * kSumBw],
+                                s[64 * kSumCore]);
+    const uint32_t pw = s[64 * kSumPower];
+    const uint32_t t_all = s[64 * hfs_all], t_none = s[64 * hfs_none];
+    if (!need_uni) {  // the node's healthy frees for the per-pod pass: lds[node][need - 1] (slot K: 0)
 #pragma unroll
-      for (int t = 0; t < K; ++t) lds[lane * HW + t] = hf.v[t];
+      for (int t = 0; t < K; ++t) lds[lane * HW + t] = s[64 * (kSumHfs + t)];
       lds[lane * HW + K] = 0u;
     }
     const uint64_t cn = (uint64_t)w0.x | ((uint64_t)w0.y << 32);
@@ -416,8 +477,14 @@ __global__ __launch_bounds__(kBlock) void k1_block_n32(
             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)w0.y, j) << 32);
         const uint32_t ckj = (uint32_t)__builtin_amdgcn_readlane((int)ck, j);
         const uint32_t mrfj = (uint32_t)__builtin_amdgcn_readlane((int)mrf1, j);
-        const uint32_t hk = need_mem == 0u ? (uint32_t)K : min(need_mem, (uint32_t)K + 1u) - 1u;
-        const uint32_t th = lds[(uint32_t)j * HW + hk];
+        uint32_t th;
+        if (need_uni) {  // hfs[need-1] of node j from its lane (a need beyond K: no such card)
+          const uint32_t tj = (uint32_t)__builtin_amdgcn_readlane((int)t_all, j);
+          th = hfs_all_ok ? tj : 0u;
+        } else {
+          const uint32_t hk = need_mem == 0u ? (uint32_t)K : min(need_mem, (uint32_t)K + 1u) - 1u;
+          th = lds[(uint32_t)j * HW + hk];
+        }
         f = live && number <= cnj && (need_mem == 0u || th > m) &&
             (need_clk == 0u || (ckj == c && ((mj >> 8) & 0xffu) >= need_clk));
         if (f) {
@@ -433,8 +500,8 @@ __global__ __launch_bounds__(kBlock) void k1_block_n32(
           }
         }
       } else {
-        f = k1_node<K, Path::N32>(nodes + (size_t)(nb + (uint32_t)j) * NS, m, c, number,
-                                  need_mem, need_clk, mx, nf, nz) && live;
+        f = k1_node_lean<K>(nodes + (size_t)(nb + (uint32_t)j) * NS, m, c, number, need_mem,
+                            need_clk, mx, nf, nz) && live;
       }
       const uint64_t b = ballot(f);
       set_lane(lo, hi, b, (uint32_t)j);
@@ -888,13 +955,17 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
     const uint32_t n = nb + lane;
     const bool valid = n < n1;
     const uint64_t mask = valid ? bmw[n] : 0ull;
-    const uint32_t* s = reinterpret_cast<const uint32_t*>(sum2 + (size_t)(valid ? n : nb) * S2);
-    const uint4 h0 = *reinterpret_cast<const uint4*>(s);
-    const uint4 h1 = *reinterpret_cast<const uint4*>(s + 4);
-    const Group<uint32_t, K> fs =
-        load_group<uint32_t, K>(reinterpret_cast<const unsigned char*>(s + kS2Fs));
-    const Group<uint32_t, K> ts =
-        load_group<uint32_t, K>(reinterpret_cast<const unsigned char*>(s + kS2Fs + K));
+    // this block's tile of summaries (nb is a multiple of 64): word w at s[64 w]
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(sum2) + sum_index(nb, 0, S2) + lane;
+    const uint4 h0 = make_uint4(s[64 * kS2Static], s[64 * (kS2Static + 1)], s[64 * kS2Clock],
+                                s[64 * kS2Meta]);
+    const uint4 h1 = make_uint4(s[64 * kS2Bw], s[64 * kS2Core], s[64 * kS2Power], 0u);
+    Group<uint32_t, K> fs, ts;
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      fs.v[t] = s[64 * (kS2Fs + t)];
+      ts.v[t] = s[64 * (kS2Fs + K + t)];
+    }
     const uint64_t feas_b = ballot(mask != 0ull);
     if (feas_b == 0) return;  // no pod of the wave can use any node of the block
     uint64_t fast_b = ballot(mask != 0ull && (h0.w & kSumUni4) != 0u), u_b = 0;
@@ -1190,14 +1261,14 @@ __global__ __launch_bounds__(kBlock) void k_set_static(unsigned char* __restrict
   hdr[0] = value[t];        // static_score bits (f64 on the fast paths, u64 on U64)
   hdr[1] = card_number[t];  // CardNumber
   if (sum) {                // the K1 summary's copy of CardNumber (words cn_lo, cn_hi)
-    uint32_t* s = reinterpret_cast<uint32_t*>(sum + (size_t)node[t] * sum_stride);
-    s[kSumCnLo] = (uint32_t)card_number[t];
-    s[kSumCnHi] = (uint32_t)(card_number[t] >> 32);
+    uint32_t* s = reinterpret_cast<uint32_t*>(sum);
+    s[sum_index(node[t], kSumCnLo, sum_stride)] = (uint32_t)card_number[t];
+    s[sum_index(node[t], kSumCnHi, sum_stride)] = (uint32_t)(card_number[t] >> 32);
   }
   if (sum2) {  // the K2 summary's copy of the static score (words 0-1)
-    uint32_t* s = reinterpret_cast<uint32_t*>(sum2 + (size_t)node[t] * sum2_stride);
-    s[kS2Static] = (uint32_t)value[t];
-    s[kS2Static + 1] = (uint32_t)(value[t] >> 32);
+    uint32_t* s = reinterpret_cast<uint32_t*>(sum2);
+    s[sum_index(node[t], kS2Static, sum2_stride)] = (uint32_t)value[t];
+    s[sum_index(node[t], kS2Static + 1, sum2_stride)] = (uint32_t)(value[t] >> 32);
   }
 }
 

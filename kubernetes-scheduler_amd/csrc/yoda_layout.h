@@ -110,6 +110,18 @@ enum K2SumWord { kS2Static = 0, kS2Clock = 2, kS2Meta = 3, kS2Bw = 4, kS2Core = 
                  kS2Fs = 8 };
 __host__ __device__ constexpr uint32_t k2sum_stride(int k) { return 32u + 8u * (uint32_t)k; }
 
+// Both summaries are stored in tiles of 64 nodes, word-major inside a tile (AoSoA): word w
+// of node n is u32 number sum_index(n, w, stride).  The block kernels read them with
+// lane = node, so loading one word for 64 nodes is one contiguous 256-B access (2 cache
+// lines) instead of 64 strided ones (a 16-B load over an 80-B stride touches 40 lines).
+// The last tile is padded to 64 nodes (zeros; the kernels mask those lanes).
+__host__ __device__ constexpr size_t sum_index(uint32_t n, uint32_t w, uint32_t stride) {
+  return ((size_t)(n >> 6) * (stride / 4u) + w) * 64u + (n & 63u);
+}
+__host__ __device__ constexpr size_t sum_words(uint32_t n_nodes, uint32_t stride) {
+  return (size_t)((n_nodes + 63u) >> 6) * 64u * (stride / 4u);
+}
+
 // Feasibility bitmask: one u64 per (pod wave, node), bit l = pod 64 w + l (in the order the
 // kernels see the pods) feasible on node n, at bm[w * bm_stride + n]; bm_stride = N rounded
 // up to 64.  K1 writes it coalesced (lane = node); K2 reads one wave's mask per node through

@@ -15,7 +15,8 @@ import numpy as np
 from .soa import CEvalOut, CNodeSoA, CPodSoA, EvalResult, NodeSoA, PodSoA
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libyoda.so")
+# YODA_LIB_PATH: another build of libyoda for interleaved A/B timing (tools/ab_lib.sh)
+LIB_PATH = os.environ.get("YODA_LIB_PATH") or os.path.join(_HERE, "libyoda.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "yoda.h")
 
 ERRORS = {
