@@ -76,6 +76,12 @@ hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32
                              unsigned char* sum, uint32_t sum_stride, unsigned char* sum2,
                              uint32_t sum2_stride, hipStream_t s);
 int topk_k();
+uint32_t greedy_one_blocks();
+hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
+                             const PodParams& pp, const double* rcp, const float* rcp32,
+                             uint32_t n_pods, uint32_t s, const uint64_t* bm, uint32_t bm_stride,
+                             double* part_s, uint32_t* part_i, uint32_t* done, uint32_t* out,
+                             hipStream_t st);
 size_t order_scratch_bytes(uint32_t n_pods);
 hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
                              uint32_t n_pods, void* scratch, size_t scratch_bytes,
@@ -192,6 +198,7 @@ struct yoda_handle {
   bool blk_valid = false;   // the last K1 wrote blk (block-classified K1 on this batch)
   // greedy
   DevBuf tk_s_part, tk_i_part, tk_s, tk_i, upd_node, upd_val, upd_cn;
+  DevBuf g1_part, g1_done;  // k_greedy_one partials + block counter (zeroed once)
   PinnedBuf upd_stage, pick_stage;
   hipEvent_t upd_event = nullptr;
   bool upd_pending = false;
@@ -229,7 +236,7 @@ struct yoda_handle {
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
                      &n_flagged, &bitmask,   &bitmask_t,  &blk,  &p_max_u,      &p_cnt,
                      &rows,      &rows_t,    &tk_s_part,  &tk_i_part,    &tk_s,
-                     &tk_i,      &upd_node,  &upd_val,    &upd_cn,
+                     &tk_i,      &upd_node,  &upd_val,    &upd_cn,    &g1_part,   &g1_done,
                      &p_best_f,  &p_best_i,  &p_idx,      &p_ties,       &p_low_f,
                      &p_low_i,   &p_err};
     for (DevBuf* b : all) b->release();
@@ -1351,6 +1358,35 @@ int greedy_eval_one(GreedyState& g, const yoda_pod_soa* pods, uint32_t p, int mo
   return YODA_OK;
 }
 
+// Exact evaluation of the window pod at sorted position s against the current node state,
+// reusing the window's feasibility bits and maxima (only static scores change inside a
+// window, and push_dirty makes them current): one launch + an 4-byte copy.
+int greedy_eval_fast(GreedyState& g, uint32_t s, int32_t* pick_out) {
+  yoda_t* h = g.h;
+  int rc = g.push_dirty();
+  if (rc) return rc;
+  const uint32_t nb = greedy_one_blocks();
+  if (h->g1_done.bytes == 0) {
+    HIP_TRY(h, h->g1_done.ensure(16));
+    HIP_TRY(h, hipMemsetAsync(h->g1_done.p, 0, 16, h->stream));
+  }
+  HIP_TRY(h, h->g1_part.ensure((size_t)nb * 12 + 16));
+  double* ps = h->g1_part.as<double>();
+  uint32_t* pi = reinterpret_cast<uint32_t*>(ps + nb);
+  uint32_t* done = h->g1_done.as<uint32_t>();
+  HIP_TRY(h, launch_greedy_one(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes,
+                               pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(),
+                               h->n_pods, s, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes), ps,
+                               pi, done, done + 1, h->stream));
+  HIP_TRY(h, h->pick_stage.ensure(16));
+  HIP_TRY(h, hipMemcpyAsync(h->pick_stage.p, done + 1, 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  const uint32_t n = *static_cast<uint32_t*>(h->pick_stage.p);
+  if (n == 0xffffffffu) return fail(h, YODA_ERR_INVALID_ARG, "greedy: no feasible node found");
+  *pick_out = (int32_t)(n + h->node_offset);
+  return YODA_OK;
+}
+
 }  // namespace
 
 int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, int32_t* pick) {
@@ -1443,6 +1479,7 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
       std::vector<uint32_t> counts(2 * (size_t)W);
       std::vector<double> ts((size_t)KT * W);
       std::vector<uint32_t> ti((size_t)KT * W);
+      std::vector<uint32_t> perm(W), pos(W);
       for (uint32_t ws = 0; ws < P; ws += W) {
         const uint32_t wn = std::min(W, P - ws);
         const auto tw = Clock::now();
@@ -1452,6 +1489,9 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
         win.build(pods, order.data() + ws, wn);
         if ((rc = yoda_upload_pods(h, &win.soa))) return rc;
         if ((rc = prepare_run(h, YODA_MODE_SCV))) return rc;
+        // sort the window like any batch (whole waves skip nodes); outputs stay in sorted
+        // order and are read through pos[i] = sorted position of window pod i
+        if ((rc = order_pods(h, YODA_MODE_SCV))) return rc;
         const size_t CPk = (size_t)h->C2 * KT * wn;
         HIP_TRY(h, h->tk_s_part.ensure(CPk * 8));
         HIP_TRY(h, h->tk_i_part.ensure(CPk * 4));
@@ -1477,10 +1517,16 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
                                     hipMemcpyDeviceToHost, h->stream));
           HIP_TRY(h, hipMemcpyAsync(ti.data(), h->tk_i.p, (size_t)KT * wn * 4,
                                     hipMemcpyDeviceToHost, h->stream));
+          if (h->ordered)
+            HIP_TRY(h, hipMemcpyAsync(perm.data(), h->perm.p, (size_t)wn * 4,
+                                      hipMemcpyDeviceToHost, h->stream));
           HIP_TRY(h, hipStreamSynchronize(h->stream));
         } else {
           std::fill(counts.begin(), counts.end(), 0u);
         }
+        for (uint32_t i = 0; i < wn; ++i) pos[i] = i;
+        if (h->ordered)
+          for (uint32_t q = 0; q < wn; ++q) pos[perm[q]] = q;
         ++h->greedy_windows;
         h->greedy_window_ms += ms_since(tw);
         const auto tr = Clock::now();
@@ -1488,17 +1534,18 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
         bool wrapped = false;
         for (uint32_t i = 0; i < wn; ++i) {
           const uint32_t p = order[ws + i];
-          const uint32_t nf = counts[i], nz = counts[(size_t)wn + i];
+          const uint32_t q = pos[i];  // sorted position: the device outputs' index
+          const uint32_t nf = counts[q], nz = counts[(size_t)wn + q];
           int32_t pk;
           if (nf == 0) {
             pk = YODA_PICK_NONE;
           } else if (nf >= 2 && nz > 0) {
             pk = YODA_PICK_ERROR;  // Score would divide by TotalMemorySum == 0
           } else if (nf == 1) {
-            pk = (int32_t)ti[i];   // the only feasible node, returned without scoring
+            pk = (int32_t)ti[q];   // the only feasible node, returned without scoring
           } else if (wrapped) {
             const auto tf = Clock::now();
-            if ((rc = greedy_eval_one(g, pods, p, YODA_MODE_SCV, &pk))) return rc;
+            if ((rc = greedy_eval_fast(g, q, &pk))) return rc;
             ++h->greedy_fallbacks;
             fb_ms += ms_since(tf);
           } else {
@@ -1507,9 +1554,9 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
             double bs = -1.0;
             uint32_t bi = 0xffffffffu;
             for (uint32_t k = 0; k < len; ++k) {
-              const uint32_t node = ti[(size_t)k * wn + i];
+              const uint32_t node = ti[(size_t)k * wn + q];
               const uint32_t n = node - h->node_offset;
-              double cur = ts[(size_t)k * wn + i];
+              double cur = ts[(size_t)k * wn + q];
               if (g.touched_w[n]) cur = cur - (double)g.stat_w[n] + (double)g.stat[n];
               if (cur > bs || (cur == bs && node < bi)) {
                 bs = cur;
@@ -1518,14 +1565,14 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
             }
             // every node outside the list scored <= T at window start (ties: higher index)
             // and its score can only have dropped since
-            const double T = ts[(size_t)(len - 1) * wn + i];
-            const uint32_t tidx = ti[(size_t)(len - 1) * wn + i];
+            const double T = ts[(size_t)(len - 1) * wn + q];
+            const uint32_t tidx = ti[(size_t)(len - 1) * wn + q];
             const bool certified = nf <= KT || bs > T || (bs == T && bi <= tidx);
             if (certified) {
               pk = (int32_t)bi;
             } else {
               const auto tf = Clock::now();
-              if ((rc = greedy_eval_one(g, pods, p, YODA_MODE_SCV, &pk))) return rc;
+              if ((rc = greedy_eval_fast(g, q, &pk))) return rc;
               ++h->greedy_fallbacks;
               fb_ms += ms_since(tf);
             }

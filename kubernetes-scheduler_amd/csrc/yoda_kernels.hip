@@ -15,6 +15,7 @@
 //   K3  k3_exact_normalize scheduler.go:176-179 with int64 wrap (generic path only)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <algorithm>
 #include <cstdlib>
 
 #include "yoda_layout.h"
@@ -1272,6 +1273,82 @@ __global__ __launch_bounds__(kBlock) void k_set_static(unsigned char* __restrict
   }
 }
 
+// Greedy fallback: ONE pod of the current window (sorted position `s`) scored exactly against
+// the CURRENT node state, lane = node.  In the reference-faithful greedy only the nodes'
+// static scores (Allocate) change inside a window: the pod's feasibility bits (bm, written by
+// the window's K1) and its PreScore maxima / reciprocals stay valid, and k_set_static keeps
+// the records' static scores current.  Result: argmax raw score, lowest node index among
+// equal scores (the same pick as a full evaluation).  One launch: every block
+// writes its (best, index) partial and the last block to finish merges them (the counter is
+// reset for the next call).
+template <int K, Path PATH>
+__global__ __launch_bounds__(kBlock) void k_greedy_one(
+    const unsigned char* __restrict__ nodes, uint32_t n_nodes, ScoreArgs args, uint32_t n_pods,
+    uint32_t s, const uint64_t* __restrict__ bm, uint32_t bm_stride, double* __restrict__ part_s,
+    uint32_t* __restrict__ part_i, uint32_t* __restrict__ done, uint32_t* __restrict__ out) {
+  constexpr uint32_t stride = PATH == Path::N32 ? n32_stride(K) : node_stride(K);
+  __shared__ double red_s[kBlock / kWave];
+  __shared__ uint32_t red_i[kBlock / kWave];
+  __shared__ bool last;
+  Scorer<PATH> sc;
+  sc.load(args, s, n_pods);  // the same pod on every lane
+  const uint64_t* row = bm + (size_t)(s >> 6) * bm_stride;
+  const uint32_t bit = s & 63u;
+  double best = -1.0;
+  uint32_t idx = 0xffffffffu;
+  for (uint32_t n = blockIdx.x * kBlock + threadIdx.x; n < n_nodes; n += gridDim.x * kBlock) {
+    if ((row[n] >> bit) & 1ull) {
+      const double raw = sc.template raw<K>(nodes + (size_t)n * stride);
+      if (raw > best) {  // n grows along the thread's sweep: the first maximum is the lowest
+        best = raw;
+        idx = n;
+      }
+    }
+  }
+  auto merge = [](double& b, uint32_t& i, double ob, uint32_t oi) {
+    if (ob > b || (ob == b && oi < i)) {
+      b = ob;
+      i = oi;
+    }
+  };
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1)
+    merge(best, idx, __shfl_xor(best, o, kWave), (uint32_t)__shfl_xor((int)idx, o, kWave));
+  const uint32_t w = threadIdx.x >> 6;
+  if (lane_id() == 0) {
+    red_s[w] = best;
+    red_i[w] = idx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t k = 1; k < kBlock / kWave; ++k) merge(best, idx, red_s[k], red_i[k]);
+    part_s[blockIdx.x] = best;
+    part_i[blockIdx.x] = idx;
+    __threadfence();
+    last = atomicAdd(done, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  best = -1.0;
+  idx = 0xffffffffu;
+  for (uint32_t b = threadIdx.x; b < gridDim.x; b += kBlock)
+    merge(best, idx, static_cast<volatile double*>(part_s)[b], static_cast<volatile uint32_t*>(part_i)[b]);
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1)
+    merge(best, idx, __shfl_xor(best, o, kWave), (uint32_t)__shfl_xor((int)idx, o, kWave));
+  if (lane_id() == 0) {
+    red_s[w] = best;
+    red_i[w] = idx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t k = 1; k < kBlock / kWave; ++k) merge(best, idx, red_s[k], red_i[k]);
+    out[0] = idx;
+    *done = 0u;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Generic (exact uint64, Go wrap-around) card score — algorithm.go:280-291.
 __device__ __forceinline__ uint64_t card_score_u64(uint64_t bw, uint64_t ck, uint64_t core,
@@ -1878,6 +1955,35 @@ hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32
 }
 
 int topk_k() { return kTopK; }
+
+// Partials of k_greedy_one: at most this many blocks (grid-stride over the nodes).
+constexpr uint32_t kGreedyOneBlocks = 512;
+uint32_t greedy_one_blocks() { return kGreedyOneBlocks; }
+
+hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
+                             const PodParams& pp, const double* rcp, const float* rcp32,
+                             uint32_t n_pods, uint32_t s, const uint64_t* bm, uint32_t bm_stride,
+                             double* part_s, uint32_t* part_i, uint32_t* done, uint32_t* out,
+                             hipStream_t st) {
+  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
+  const dim3 grid(std::max<uint32_t>(1, std::min<uint32_t>(kGreedyOneBlocks,
+                                                           (n_nodes + kBlock - 1) / kBlock)));
+  switch (path) {
+    case Path::N32:
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k_greedy_one<KK, Path::N32>), grid, dim3(kBlock), 0,
+                                          st, nodes, n_nodes, a, n_pods, s, bm, bm_stride, part_s,
+                                          part_i, done, out));
+      break;
+    case Path::F64:
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k_greedy_one<KK, Path::F64>), grid, dim3(kBlock), 0,
+                                          st, nodes, n_nodes, a, n_pods, s, bm, bm_stride, part_s,
+                                          part_i, done, out));
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
 
 hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigned char* sum2,
                      const uint64_t* blk, uint32_t blk_stride, uint32_t n_nodes,

@@ -416,6 +416,19 @@ def test_greedy_matches_sequential_oracle(dev, flags, path):
     assert_same(dev.eval(pods, MODE_SCV), oracle.schedule(nodes, pods, MODE_SCV, threads=8))
 
 
+@pytest.mark.parametrize("path", ["n32", "f64"])
+def test_greedy_several_sorted_windows(dev, path):
+    """Several 4096-pod windows (each sorted on the device, outputs read through the
+    permutation) with exact single-pod fallbacks (k_greedy_one) == the sequential oracle."""
+    nodes, pods = synth.make_config(5, pods=9000, nodes=300)
+    dev.upload_nodes(nodes, force_f64=path == "f64")
+    got = dev.greedy(pods, MODE_SCV, 0)
+    want, _ = oracle.greedy(nodes, pods, MODE_SCV, 0)
+    np.testing.assert_array_equal(got, want)
+    windows, fallbacks = dev.greedy_stats()
+    assert windows == 3 and 0 < fallbacks < pods.n_pods
+
+
 def test_greedy_small_windows_and_mode_b(dev):
     nodes, pods = synth.make_config(5, pods=400, nodes=300)
     pods.priority[:] = 0
