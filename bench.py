@@ -125,7 +125,11 @@ def bench_greedy(args):
         # the sequential oracle on a prefix of the queue (greedy is order-dependent, so a
         # prefix in queue order is an exact sub-problem)
         order = oracle.queue_order(pods)
-        n = int(args.cpu_seconds * 2)  # ~0.5 s per pod at 100k nodes
+        probe = min(pods.n_pods, 16)
+        t0 = time.perf_counter()
+        oracle.greedy(nodes, pods.take(order[:probe]), MODE_SCV, flags)
+        per_pod = max((time.perf_counter() - t0) / probe, 1e-9)
+        n = int(max(probe, min(pods.n_pods, args.cpu_seconds / per_pod)))
         prefix = pods.take(order[:n])
         t0 = time.perf_counter()
         want, _ = oracle.greedy(nodes, prefix, MODE_SCV, flags)
