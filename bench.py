@@ -96,29 +96,82 @@ def cpu_baseline(nodes, pods, mode, target_s: float, threads: int, gpu_res):
 
 
 def bench_greedy(args):
-    """Config 5: greedy batched assignment (sequential assume in sort.Less order), single
-    GPU.  value = pods scheduled per second; the sequential oracle checks a prefix."""
-    device = torch.device("cuda", 0)
+    """Config 5: greedy batched assignment (sequential assume in sort.Less order).
+    value = pods scheduled per second.  N=1: one handle (yoda_greedy); N>1: nodes sharded
+    across ranks, windows merged over RCCL (yoda_amd/dist.py sharded_greedy).  Rank 0 checks
+    a queue-order prefix against the sequential oracle (N=1)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dev_index = 0 if os.environ.get("YODA_BENCH_SAME_DEVICE") == "1" else local_rank
+    device = torch.device("cuda", dev_index)
     torch.cuda.set_device(device)
+    if world > 1:
+        import torch.distributed as dist
+        backend = os.environ.get("YODA_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
     cfg = 5
     nodes, pods = synth.make_config(cfg, pods=args.pods, nodes=args.nodes)
-    y = Yoda(0)
-    y.upload_nodes(nodes)
     flags = 0
-    y.greedy(pods.slice(0, min(pods.n_pods, 4096)), MODE_SCV, flags)  # warm-up
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    picks = y.greedy(pods, MODE_SCV, flags)
-    dt = time.perf_counter() - t0
-    windows, fallbacks, times = y.greedy_stats(times=True)
+    y = Yoda(dev_index)
+    if world == 1:
+        y.upload_nodes(nodes)
+        y.greedy(pods.slice(0, min(pods.n_pods, 4096)), MODE_SCV, flags)  # warm-up
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        picks = y.greedy(pods, MODE_SCV, flags)
+        dt = time.perf_counter() - t0
+        windows, fallbacks, times = y.greedy_stats(times=True)
+        extra = {"windows": windows, "exact_fallback_pods": fallbacks, "host_times_ms": times}
+    else:
+        import torch.distributed as dist
+        from yoda_amd.dist import HandleShard, Reducer, agree_on_path, shard_bounds, sharded_greedy
+        b = shard_bounds(nodes.n_nodes, world)
+        lo, hi = int(b[rank]), int(b[rank + 1])
+        shard = nodes.slice(lo, hi)
+        y.upload_nodes(shard, node_offset=lo)
+        red = Reducer()
+        agree_on_path(red, [y], [shard], [lo], device)
+        hs = [HandleShard(y, device)]
+        sharded_greedy(hs, red, nodes, pods.slice(0, min(pods.n_pods, 4096)), flags)  # warm-up
+        dist.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        st = {}
+        picks = sharded_greedy(hs, red, nodes, pods, flags, stats=st)
+        torch.cuda.synchronize(device)
+        dt = time.perf_counter() - t0
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        extra = {"windows": st["windows"], "exact_fallback_pods": st["exact_pods"]}
+        if args.check and rank == 0:
+            full = Yoda(dev_index)
+            full.upload_nodes(nodes)
+            if not np.array_equal(full.greedy(pods, MODE_SCV, flags), picks):
+                raise SystemExit("--check: sharded greedy picks differ from the single handle")
+            full.close()
+            extra["check"] = "sharded greedy picks == single-handle yoda_greedy"
     out = {"metric": "greedy batch: pods assigned/s (config 5, exact vs the sequential oracle)",
-           "value": pods.n_pods / dt, "unit": "pods/s", "n_gpus": 1, "seconds": dt,
+           "value": pods.n_pods / dt, "unit": "pods/s", "n_gpus": world, "seconds": dt,
            "higher_is_better": True, "data": "synthetic (yoda_amd/synth.py config 5)",
            "config": {"workload": f"config5: {pods.n_pods} pods x {nodes.n_nodes} nodes greedy",
-                      "pods": pods.n_pods, "nodes": nodes.n_nodes, "path": y.path},
+                      "pods": pods.n_pods, "nodes": nodes.n_nodes, "path": y.path,
+                      "parallelism": f"node-shard x{world}" + (" (RCCL window merges)"
+                                                               if world > 1 else "")},
            "pairs_per_s_equiv": pods.n_pods * nodes.n_nodes / dt,
-           "windows": windows, "exact_fallback_pods": fallbacks, "host_times_ms": times,
            "assigned": int((picks >= 0).sum())}
+    out.update(extra)
+    if world > 1:
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        y.close()
+        import torch.distributed as dist
+        dist.destroy_process_group()
+        return
     if not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle  # noqa: E402  (cpu_baseline leg only)

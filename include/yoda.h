@@ -242,6 +242,61 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
 int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks,
                       double* times_ms);
 
+/* ---- sharded greedy batch (node shards on several GPUs) ------------------------------
+ * yoda_greedy's windowed algorithm split at its exchange points, so each rank's handle holds
+ * a node shard (reference semantics as yoda_greedy: sort.go:8-10 order, the scheduler-cache
+ * assume of algorithm.go:299-303).  Per window of W pods, on every rank:
+ *   yoda_upload_pods(window) ; yoda_shard_phase1 ; all-reduce maxima MAX, counts SUM ;
+ *   yoda_shard_topk -> the shard's best yoda_topk_k() (score, global node) per pod, sorted by
+ *     score desc / node asc, -1.0 / 0xFFFFFFFF padding, plus the reduced counts, all in the
+ *     window's pod order ;
+ *   merge the shards' lists (keep the first yoda_topk_k() of their union in that order) ;
+ *   yoda_gs_begin_window ; loop { yoda_gs_resolve -> next ; if next == W break ;
+ *     push yoda_gs_take_dirty to every shard (yoda_set_node_state) ;
+ *     yoda_shard_best_one(next) on every shard ; pick = max score, lowest node ;
+ *     yoda_gs_assign(ws + next, pick) } ; push yoda_gs_take_dirty.
+ * Fast record paths (N32 / F64) and flags == 0 only: with YODA_GREEDY_CARD_CAPACITY or the
+ * U64 path, evaluate each pod exactly with the sharded yoda_shard_* sequence instead and
+ * feed the pick to yoda_gs_assign. */
+int yoda_topk_k(void);
+/* Set the allocated memory (and CardNumber) of the listed nodes (GLOBAL ids; ids outside
+ * this handle's shard are ignored) and refresh their static score on the device. */
+int yoda_set_node_state(yoda_t* h, uint32_t count, const uint32_t* nodes, const uint64_t* alloc,
+                        const uint64_t* card_number);
+/* After yoda_shard_phase1 and the caller's reduction of its buffers (d_maxima, d_counts as
+ * there).  Host outputs: counts [2][P] (n_feasible, n_zero_total), top_score [k][P] (f64,
+ * exact integers), top_node [k][P]. */
+int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_counts,
+                    uint32_t* counts, double* top_score, uint32_t* top_node);
+/* Exact best node of pod `pod` (index in the batch of the last yoda_shard_topk) over this
+ * shard against the CURRENT node state: *node = global id or -1 (no feasible node here),
+ * *score = its raw score (lowest node among equal scores). */
+int yoda_shard_best_one(yoda_t* h, uint32_t pod, double* score, int32_t* node);
+
+/* Host-side sequential resolve over the GLOBAL node set (no GPU); identical on every rank. */
+typedef struct yoda_greedy_session yoda_gs_t;
+/* nodes: the full snapshot (card_number, free/total memory sums, alloc_memory (may be NULL)
+ * are read); pods: the whole batch (number/memory/priority are read). */
+int yoda_gs_create(const yoda_node_soa* nodes, const yoda_pod_soa* pods, uint32_t flags,
+                   yoda_gs_t** out);
+int yoda_gs_destroy(yoda_gs_t* g);
+/* order[q] = input index of the pod at queue position q (sort.go:8-10). */
+int yoda_gs_queue_order(const yoda_gs_t* g, uint32_t* order);
+/* Window = queue positions [ws, ws + wn); arrays in window order as yoda_shard_topk's. */
+int yoda_gs_begin_window(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
+                         const uint32_t* counts, const double* top_score,
+                         const uint32_t* top_node);
+int yoda_gs_resolve(yoda_gs_t* g, uint32_t* next);
+int yoda_gs_assign(yoda_gs_t* g, uint32_t queue_pos, int32_t pick);
+/* Nodes whose state changed since the last call (at most cap), with their current state. */
+int yoda_gs_take_dirty(yoda_gs_t* g, uint32_t cap, uint32_t* nodes, uint64_t* alloc,
+                       uint64_t* card_number, uint32_t* count);
+/* Every node the session ever changed, with its ORIGINAL state (to restore the shards). */
+int yoda_gs_touched_original(const yoda_gs_t* g, uint32_t cap, uint32_t* nodes, uint64_t* alloc,
+                             uint64_t* card_number, uint32_t* count);
+/* pick [P] in input order; pods certified from candidate lists; pods assigned by the caller. */
+int yoda_gs_picks(const yoda_gs_t* g, int32_t* pick, uint32_t* resolved, uint32_t* assigned);
+
 #ifdef __cplusplus
 }
 #endif

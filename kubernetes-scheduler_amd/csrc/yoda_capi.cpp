@@ -202,6 +202,8 @@ struct yoda_handle {
   PinnedBuf upd_stage, pick_stage;
   hipEvent_t upd_event = nullptr;
   bool upd_pending = false;
+  std::vector<uint32_t> h_pos;  // yoda_shard_topk: caller pod index -> sorted position
+  bool topk_ready = false;      // the bitmask / reciprocals of that batch are still valid
   uint32_t greedy_windows = 0, greedy_fallbacks = 0;
   double greedy_window_ms = 0, greedy_fallback_ms = 0, greedy_resolve_ms = 0;
   DevBuf p_max_u, p_cnt, p_best_f, p_best_i, p_idx, p_ties, p_low_f, p_low_i, p_err;
@@ -642,6 +644,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
   try {
     if (!nd) return fail(h, YODA_ERR_INVALID_ARG, "nodes is NULL");
     const uint32_t N = nd->n_nodes, KS = nd->max_cards;
+    h->topk_ready = false;
     if (KS < 1 || KS > YODA_MAX_CARDS)
       return fail(h, YODA_ERR_INVALID_ARG, "max_cards must be in 1..16");
     if (N > 0 && (!nd->card_number || !nd->card_count || !nd->free_memory_sum ||
@@ -909,6 +912,7 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     if (P > 0 && (!pd->has_number || !pd->number || !pd->has_memory || !pd->memory ||
                   !pd->has_clock || !pd->clock))
       return fail(h, YODA_ERR_INVALID_ARG, "a required pod array is NULL");
+    h->topk_ready = false;
     HIP_TRY(h, hipSetDevice(h->device));
     // One blob of per-pod arrays, staged in pinned memory and sent with ONE copy.
     size_t off[kPodArrays], total = 0;
@@ -974,6 +978,7 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
 static int prepare_run(yoda_t* h, int mode) {
   int rc = check_ready(h, mode);
   if (rc) return rc;
+  h->topk_ready = false;  // this run overwrites the bitmask and reciprocals
   plan_chunks(h, mode, h->n_pods, h->n_nodes);
   return ensure_state(h, std::max<uint32_t>(h->n_pods, 1));
 }
@@ -1615,6 +1620,431 @@ int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks,
     times_ms[1] = h->greedy_resolve_ms;
     times_ms[2] = h->greedy_fallback_ms;
   }
+  return YODA_OK;
+}
+
+// ---- sharded greedy (config 5 across GPUs) ---------------------------------------------
+// Each rank's handle holds a node shard.  Per window: yoda_shard_phase1 (+ MAX/SUM
+// all-reduce) -> yoda_shard_topk (local top-k with the global maxima) -> the caller merges
+// the shards' lists -> the host session resolves the window in queue order; pods it cannot
+// certify are scored exactly on every shard (yoda_shard_best_one) and merged by the caller.
+// Between steps the caller pushes the nodes the session changed (yoda_gs_take_dirty ->
+// yoda_set_node_state on every shard).
+
+int yoda_topk_k(void) { return topk_k(); }
+
+namespace {
+
+// Overwrite the static score (and CardNumber) of a few local nodes on the device.
+int push_node_state(yoda_t* h, const std::vector<uint32_t>& loc, const std::vector<uint64_t>& val,
+                    const std::vector<uint64_t>& cn) {
+  const uint32_t cnt = (uint32_t)loc.size();
+  if (cnt == 0) return YODA_OK;
+  const size_t o_val = ((size_t)cnt * 4 + 15) / 16 * 16, o_cn = o_val + (size_t)cnt * 8;
+  const size_t bytes = o_cn + (size_t)cnt * 8;
+  if (h->upd_pending) HIP_TRY(h, hipEventSynchronize(h->upd_event));
+  HIP_TRY(h, h->upd_stage.ensure(bytes));
+  HIP_TRY(h, h->upd_node.ensure(bytes));
+  unsigned char* st = static_cast<unsigned char*>(h->upd_stage.p);
+  std::memcpy(st, loc.data(), (size_t)cnt * 4);
+  std::memcpy(st + o_val, val.data(), (size_t)cnt * 8);
+  std::memcpy(st + o_cn, cn.data(), (size_t)cnt * 8);
+  HIP_TRY(h, hipMemcpyAsync(h->upd_node.p, st, bytes, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(h, hipEventRecord(h->upd_event, h->stream));
+  h->upd_pending = true;
+  unsigned char* d = h->upd_node.as<unsigned char>();
+  const uint32_t stride = h->path == Path::N32 ? n32_stride(h->K) : node_stride(h->K);
+  HIP_TRY(h, launch_set_static(h->nodes.as<unsigned char>(), stride,
+                               reinterpret_cast<const uint32_t*>(d),
+                               reinterpret_cast<const uint64_t*>(d + o_val),
+                               reinterpret_cast<const uint64_t*>(d + o_cn), cnt,
+                               h->has_k1sum ? h->k1sum.as<unsigned char>() : nullptr,
+                               k1sum_stride(h->K),
+                               h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr,
+                               k2sum_stride(h->K), h->stream));
+  return YODA_OK;
+}
+
+}  // namespace
+
+int yoda_set_node_state(yoda_t* h, uint32_t count, const uint32_t* nodes, const uint64_t* alloc,
+                        const uint64_t* card_number) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  if (!h->has_nodes) return fail(h, YODA_ERR_NO_NODES, "no node snapshot uploaded");
+  if (count && (!nodes || !alloc || !card_number))
+    return fail(h, YODA_ERR_INVALID_ARG, "NULL node state array");
+  try {
+    HIP_TRY(h, hipSetDevice(h->device));
+    std::vector<uint32_t> loc;
+    std::vector<uint64_t> stat, val, cn;
+    for (uint32_t t = 0; t < count; ++t) {
+      if (nodes[t] < h->node_offset || nodes[t] - h->node_offset >= h->n_nodes) continue;
+      const uint32_t i = nodes[t] - h->node_offset;
+      bool z = false;
+      const uint64_t s = static_score(h->h_free_sum[i], h->h_total_sum[i], alloc[t], &z);
+      if (!h->generic && s >= (1ull << 51))
+        return fail(h, YODA_ERR_RANGE, "static score leaves the fast path; re-upload the nodes");
+      loc.push_back(i);
+      stat.push_back(s);
+      cn.push_back(card_number[t]);
+      uint64_t bits = s;
+      if (!h->generic) {
+        const double d = (double)s;
+        std::memcpy(&bits, &d, 8);
+      }
+      val.push_back(bits);
+    }
+    // keep the host copies current (yoda_update_alloc / yoda_greedy start from them)
+    const size_t stride = h->path == Path::N32 ? n32_stride(h->K) : node_stride(h->K);
+    for (size_t t = 0, ti = 0; t < count; ++t) {
+      if (nodes[t] < h->node_offset || nodes[t] - h->node_offset >= h->n_nodes) continue;
+      const uint32_t i = loc[ti];
+      h->h_alloc[i] = alloc[t];
+      h->h_card_number[i] = cn[ti];
+      unsigned char* r = h->host_records.data() + (size_t)i * stride;
+      std::memcpy(r, &val[ti], 8);       // header word 0: static score
+      std::memcpy(r + 8, &cn[ti], 8);    // header word 1: CardNumber
+      if (h->has_k2sum) {
+        h->host_k2sum[sum_index(i, kS2Static, k2sum_stride(h->K))] = (uint32_t)val[ti];
+        h->host_k2sum[sum_index(i, kS2Static + 1, k2sum_stride(h->K))] = (uint32_t)(val[ti] >> 32);
+      }
+      ++ti;
+    }
+    return push_node_state(h, loc, val, cn);
+  } catch (const std::bad_alloc&) {
+    return fail(h, YODA_ERR_INVALID_ARG, "host allocation failed");
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
+int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_counts,
+                    uint32_t* counts, double* top_score, uint32_t* top_node) {
+  int rc = check_ready(h, YODA_MODE_SCV);
+  if (rc) return rc;
+  if (!h->phase1_done) return fail(h, YODA_ERR_STATE, "yoda_shard_topk before yoda_shard_phase1");
+  if (h->generic)
+    return fail(h, YODA_ERR_STATE, "top-k lists need a fast record path (N32 or F64)");
+  if (!d_maxima || !d_counts || !counts || !top_score || !top_node)
+    return fail(h, YODA_ERR_INVALID_ARG, "NULL buffer");
+  try {
+    const uint32_t P = h->n_pods, N = h->n_nodes, KT = (uint32_t)topk_k();
+    h->h_pos.resize(P);
+    for (uint32_t i = 0; i < P; ++i) h->h_pos[i] = i;
+    h->topk_ready = false;
+    if (P == 0) return YODA_OK;
+    std::vector<uint32_t> cnt(2 * (size_t)P), ti((size_t)KT * P, 0xffffffffu), perm(P);
+    std::vector<double> ts((size_t)KT * P, -1.0);
+    HIP_TRY(h, hipMemcpyAsync(h->maxima.p, d_maxima, 6ull * P * 8, hipMemcpyDeviceToDevice,
+                              h->stream));
+    HIP_TRY(h, hipMemcpyAsync(cnt.data(), d_counts, 2ull * P * 4, hipMemcpyDeviceToHost,
+                              h->stream));
+    if (N > 0) {
+      const size_t CPk = (size_t)h->C2 * KT * P;
+      HIP_TRY(h, h->tk_s_part.ensure(CPk * 8));
+      HIP_TRY(h, h->tk_i_part.ensure(CPk * 4));
+      HIP_TRY(h, h->tk_s.ensure((size_t)KT * P * 8));
+      HIP_TRY(h, h->tk_i.ensure((size_t)KT * P * 4));
+      HIP_TRY(h, launch_prep2(h->maxima.as<uint64_t>(), P, h->rcp.as<double>(),
+                              h->rcp32.as<float>(), h->stream));
+      HIP_TRY(h, launch_k2_topk(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk2, h->C2,
+                                pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(), P,
+                                h->bitmask.as<uint64_t>(), bm_row(N), partials(h),
+                                h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),
+                                h->stream));
+      HIP_TRY(h, launch_topk_merge(h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(), h->C2,
+                                   P, h->node_offset, h->tk_s.as<double>(),
+                                   h->tk_i.as<uint32_t>(), h->stream));
+      HIP_TRY(h, hipMemcpyAsync(ts.data(), h->tk_s.p, (size_t)KT * P * 8, hipMemcpyDeviceToHost,
+                                h->stream));
+      HIP_TRY(h, hipMemcpyAsync(ti.data(), h->tk_i.p, (size_t)KT * P * 4, hipMemcpyDeviceToHost,
+                                h->stream));
+    }
+    if (h->ordered)
+      HIP_TRY(h, hipMemcpyAsync(perm.data(), h->perm.p, (size_t)P * 4, hipMemcpyDeviceToHost,
+                                h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    if (h->ordered)
+      for (uint32_t q = 0; q < P; ++q) h->h_pos[perm[q]] = q;  // perm[q]: pod at sorted q
+    for (uint32_t i = 0; i < P; ++i) {
+      const uint32_t q = h->h_pos[i];
+      counts[i] = cnt[q];
+      counts[(size_t)P + i] = cnt[(size_t)P + q];
+      for (uint32_t k = 0; k < KT; ++k) {
+        top_score[(size_t)k * P + i] = ts[(size_t)k * P + q];
+        top_node[(size_t)k * P + i] = ti[(size_t)k * P + q];
+      }
+    }
+    h->topk_ready = true;
+    return YODA_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(h, YODA_ERR_INVALID_ARG, "host allocation failed");
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
+int yoda_shard_best_one(yoda_t* h, uint32_t pod, double* score, int32_t* node) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  if (!score || !node) return fail(h, YODA_ERR_INVALID_ARG, "NULL output");
+  if (!h->topk_ready) return fail(h, YODA_ERR_STATE, "yoda_shard_best_one before yoda_shard_topk");
+  if (pod >= h->n_pods) return fail(h, YODA_ERR_INVALID_ARG, "pod index out of range");
+  *score = -1.0;
+  *node = -1;
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (h->n_nodes == 0) return YODA_OK;
+  const uint32_t s = h->h_pos[pod];
+  const uint32_t nb = greedy_one_blocks();
+  if (h->g1_done.bytes == 0) {
+    HIP_TRY(h, h->g1_done.ensure(16));
+    HIP_TRY(h, hipMemsetAsync(h->g1_done.p, 0, 16, h->stream));
+  }
+  HIP_TRY(h, h->g1_part.ensure((size_t)nb * 12 + 16));
+  double* ps = h->g1_part.as<double>();
+  uint32_t* pi = reinterpret_cast<uint32_t*>(ps + nb);
+  uint32_t* done = h->g1_done.as<uint32_t>();
+  HIP_TRY(h, launch_greedy_one(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes,
+                               pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(),
+                               h->n_pods, s, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes), ps,
+                               pi, done, done + 1, h->stream));
+  HIP_TRY(h, h->pick_stage.ensure(16));
+  HIP_TRY(h, hipMemcpyAsync(h->pick_stage.p, done, 16, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  const unsigned char* st = static_cast<const unsigned char*>(h->pick_stage.p);
+  uint32_t n;
+  double b;
+  std::memcpy(&n, st + 4, 4);
+  std::memcpy(&b, st + 8, 8);
+  if (n != 0xffffffffu) {
+    *node = (int32_t)(n + h->node_offset);
+    *score = b;
+  }
+  return YODA_OK;
+}
+
+}  // extern "C"
+
+// ---- host-side greedy session ---------------------------------------------------------
+// The sequential part of the greedy batch (yoda_greedy's resolve), over the GLOBAL node set,
+// fed with merged candidate lists.  Pure host code: identical on every rank.
+struct yoda_greedy_session {
+  uint32_t N = 0, P = 0, flags = 0;
+  std::vector<uint64_t> free_sum, total_sum, alloc, card_number, alloc0, cn0, stat, stat_w;
+  std::vector<uint8_t> has_memory, has_number, touched_w, dirty, ever;
+  std::vector<uint64_t> memory, number;
+  std::vector<uint32_t> order, touched_list, dirty_list, ever_list;
+  std::vector<int32_t> pick;
+  // current window (queue positions [ws, ws + wn)), inputs in window order
+  uint32_t ws = 0, wn = 0, k = 0, next = 0, resolved = 0, assigned = 0;
+  bool in_window = false, wrapped = false;
+  std::vector<uint32_t> counts, ti;
+  std::vector<double> ts;
+
+  void apply(uint32_t p, int32_t node) {
+    if (node < 0) return;
+    const uint32_t n = (uint32_t)node;
+    if (!touched_w[n]) {
+      touched_w[n] = 1;
+      stat_w[n] = stat[n];
+      touched_list.push_back(n);
+    }
+    if (!dirty[n]) {
+      dirty[n] = 1;
+      dirty_list.push_back(n);
+    }
+    if (!ever[n]) {
+      ever[n] = 1;
+      ever_list.push_back(n);
+    }
+    const uint64_t before = alloc[n];
+    if (has_memory[p]) alloc[n] += memory[p];  // uint64 wrap (algorithm.go:301)
+    if (alloc[n] < before) wrapped = true;     // Allocate may grow: stop certifying
+    if (flags & YODA_GREEDY_CARD_CAPACITY) {
+      const uint64_t num = has_number[p] ? number[p] : 1;
+      card_number[n] = card_number[n] >= num ? card_number[n] - num : 0;
+    }
+    bool z;
+    stat[n] = static_score(free_sum[n], total_sum[n], alloc[n], &z);
+  }
+};
+
+extern "C" {
+
+int yoda_gs_create(const yoda_node_soa* nodes, const yoda_pod_soa* pods, uint32_t flags,
+                   yoda_gs_t** out) {
+  if (!out || !nodes || !pods) return YODA_ERR_INVALID_ARG;
+  *out = nullptr;
+  const uint32_t N = nodes->n_nodes, P = pods->n_pods;
+  if (N && (!nodes->free_memory_sum || !nodes->total_memory_sum || !nodes->card_number))
+    return YODA_ERR_INVALID_ARG;
+  if (P && (!pods->has_memory || !pods->memory || !pods->has_number || !pods->number))
+    return YODA_ERR_INVALID_ARG;
+  if (N >= 0x7fffffffu) return YODA_ERR_RANGE;
+  try {
+    yoda_gs_t* g = new yoda_gs_t();
+    g->N = N, g->P = P, g->flags = flags;
+    g->free_sum.assign(nodes->free_memory_sum, nodes->free_memory_sum + N);
+    g->total_sum.assign(nodes->total_memory_sum, nodes->total_memory_sum + N);
+    g->card_number.assign(nodes->card_number, nodes->card_number + N);
+    if (nodes->alloc_memory)
+      g->alloc.assign(nodes->alloc_memory, nodes->alloc_memory + N);
+    else
+      g->alloc.assign(N, 0);
+    g->alloc0 = g->alloc;
+    g->cn0 = g->card_number;
+    g->stat.resize(N);
+    g->stat_w.resize(N);
+    for (uint32_t n = 0; n < N; ++n) {
+      bool z;
+      g->stat[n] = static_score(g->free_sum[n], g->total_sum[n], g->alloc[n], &z);
+    }
+    g->touched_w.assign(N, 0);
+    g->dirty.assign(N, 0);
+    g->ever.assign(N, 0);
+    g->has_memory.assign(pods->has_memory, pods->has_memory + P);
+    g->memory.assign(pods->memory, pods->memory + P);
+    g->has_number.assign(pods->has_number, pods->has_number + P);
+    g->number.assign(pods->number, pods->number + P);
+    g->pick.assign(P, YODA_PICK_NONE);
+    // queue order: sort.Less (sort.go:8-10), scv/priority descending, then input index
+    g->order.resize(P);
+    for (uint32_t i = 0; i < P; ++i) g->order[i] = i;
+    const int64_t* pr = pods->priority;
+    std::stable_sort(g->order.begin(), g->order.end(), [pr](uint32_t a, uint32_t b) {
+      return (pr ? pr[a] : 0) > (pr ? pr[b] : 0);
+    });
+    *out = g;
+    return YODA_OK;
+  } catch (...) {
+    return YODA_ERR_INVALID_ARG;
+  }
+}
+
+int yoda_gs_destroy(yoda_gs_t* g) {
+  if (!g) return YODA_ERR_INVALID_ARG;
+  delete g;
+  return YODA_OK;
+}
+
+int yoda_gs_queue_order(const yoda_gs_t* g, uint32_t* order) {
+  if (!g || (!order && g->P)) return YODA_ERR_INVALID_ARG;
+  std::copy(g->order.begin(), g->order.end(), order);
+  return YODA_OK;
+}
+
+int yoda_gs_begin_window(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
+                         const uint32_t* counts, const double* top_score,
+                         const uint32_t* top_node) {
+  if (!g || ws > g->P || wn > g->P - ws || k == 0 || !counts || !top_score || !top_node)
+    return YODA_ERR_INVALID_ARG;
+  for (uint32_t i = 0; i < (uint32_t)k * wn; ++i)
+    if (top_node[i] != 0xffffffffu && top_node[i] >= g->N) return YODA_ERR_RANGE;
+  try {
+    for (uint32_t n : g->touched_list) g->touched_w[n] = 0;
+    g->touched_list.clear();
+    g->ws = ws, g->wn = wn, g->k = k, g->next = 0;
+    g->in_window = true;
+    g->wrapped = false;
+    g->counts.assign(counts, counts + 2 * (size_t)wn);
+    g->ts.assign(top_score, top_score + (size_t)k * wn);
+    g->ti.assign(top_node, top_node + (size_t)k * wn);
+    return YODA_OK;
+  } catch (...) {
+    return YODA_ERR_INVALID_ARG;
+  }
+}
+
+// Resolve the window in queue order until a pod cannot be certified from its candidate list
+// (greedy): *next = its window index, or wn when the window is done.
+int yoda_gs_resolve(yoda_gs_t* g, uint32_t* next) {
+  if (!g || !next || !g->in_window) return YODA_ERR_INVALID_ARG;
+  const uint32_t wn = g->wn, KT = g->k;
+  while (g->next < wn) {
+    const uint32_t i = g->next;
+    const uint32_t p = g->order[g->ws + i];
+    const uint32_t nf = g->counts[i], nz = g->counts[(size_t)wn + i];
+    int32_t pk;
+    if (nf == 0) {
+      pk = YODA_PICK_NONE;
+    } else if (nf >= 2 && nz > 0) {
+      pk = YODA_PICK_ERROR;  // Score would divide by TotalMemorySum == 0
+    } else if (nf == 1) {
+      pk = (int32_t)g->ti[i];  // the only feasible node, returned without scoring
+    } else if (g->wrapped) {
+      break;
+    } else {
+      const uint32_t len = std::min<uint32_t>(nf, KT);
+      double bs = -1.0;
+      uint32_t bi = 0xffffffffu;
+      for (uint32_t k = 0; k < len; ++k) {
+        const uint32_t n = g->ti[(size_t)k * wn + i];
+        double cur = g->ts[(size_t)k * wn + i];
+        if (g->touched_w[n]) cur = cur - (double)g->stat_w[n] + (double)g->stat[n];
+        if (cur > bs || (cur == bs && n < bi)) {
+          bs = cur;
+          bi = n;
+        }
+      }
+      const double T = g->ts[(size_t)(len - 1) * wn + i];
+      const uint32_t tidx = g->ti[(size_t)(len - 1) * wn + i];
+      if (!(nf <= KT || bs > T || (bs == T && bi <= tidx))) break;
+      pk = (int32_t)bi;
+    }
+    g->pick[p] = pk;
+    g->apply(p, pk);
+    ++g->next;
+    ++g->resolved;
+  }
+  *next = g->next;
+  return YODA_OK;
+}
+
+int yoda_gs_assign(yoda_gs_t* g, uint32_t queue_pos, int32_t pick) {
+  if (!g || queue_pos >= g->P) return YODA_ERR_INVALID_ARG;
+  if (pick >= 0 && (uint32_t)pick >= g->N) return YODA_ERR_RANGE;
+  const uint32_t p = g->order[queue_pos];
+  g->pick[p] = pick;
+  g->apply(p, pick);
+  ++g->assigned;
+  if (g->in_window && queue_pos == g->ws + g->next) ++g->next;
+  return YODA_OK;
+}
+
+int yoda_gs_take_dirty(yoda_gs_t* g, uint32_t cap, uint32_t* nodes, uint64_t* alloc,
+                       uint64_t* card_number, uint32_t* count) {
+  if (!g || !count || (cap && (!nodes || !alloc || !card_number))) return YODA_ERR_INVALID_ARG;
+  const uint32_t n = std::min<uint32_t>(cap, (uint32_t)g->dirty_list.size());
+  for (uint32_t t = 0; t < n; ++t) {
+    const uint32_t v = g->dirty_list[t];
+    nodes[t] = v;
+    alloc[t] = g->alloc[v];
+    card_number[t] = g->card_number[v];
+    g->dirty[v] = 0;
+  }
+  g->dirty_list.erase(g->dirty_list.begin(), g->dirty_list.begin() + n);
+  *count = n;
+  return YODA_OK;
+}
+
+int yoda_gs_touched_original(const yoda_gs_t* g, uint32_t cap, uint32_t* nodes, uint64_t* alloc,
+                             uint64_t* card_number, uint32_t* count) {
+  if (!g || !count || (cap && (!nodes || !alloc || !card_number))) return YODA_ERR_INVALID_ARG;
+  const uint32_t n = std::min<uint32_t>(cap, (uint32_t)g->ever_list.size());
+  for (uint32_t t = 0; t < n; ++t) {
+    const uint32_t v = g->ever_list[t];
+    nodes[t] = v;
+    alloc[t] = g->alloc0[v];
+    card_number[t] = g->cn0[v];
+  }
+  *count = n;
+  return YODA_OK;
+}
+
+int yoda_gs_picks(const yoda_gs_t* g, int32_t* pick, uint32_t* resolved, uint32_t* assigned) {
+  if (!g) return YODA_ERR_INVALID_ARG;
+  if (pick) std::copy(g->pick.begin(), g->pick.end(), pick);
+  if (resolved) *resolved = g->resolved;
+  if (assigned) *assigned = g->assigned;
   return YODA_OK;
 }
 

@@ -1278,7 +1278,8 @@ __global__ __launch_bounds__(kBlock) void k_set_static(unsigned char* __restrict
 // static scores (Allocate) change inside a window: the pod's feasibility bits (bm, written by
 // the window's K1) and its PreScore maxima / reciprocals stay valid, and k_set_static keeps
 // the records' static scores current.  Result: argmax raw score, lowest node index among
-// equal scores (the same pick as a full evaluation).  One launch: every block
+// equal scores (the same pick as a full evaluation); out[0] = node (local),
+// out[1..2] = its raw score as f64 (-1: no feasible node).  One launch: every block
 // writes its (best, index) partial and the last block to finish merges them (the counter is
 // reset for the next call).
 template <int K, Path PATH>
@@ -1345,6 +1346,7 @@ __global__ __launch_bounds__(kBlock) void k_greedy_one(
   if (threadIdx.x == 0) {
     for (uint32_t k = 1; k < kBlock / kWave; ++k) merge(best, idx, red_s[k], red_i[k]);
     out[0] = idx;
+    *reinterpret_cast<double*>(out + 1) = best;  // 8-byte aligned: out = done + 1 (sharded merge)
     *done = 0u;
   }
 }

@@ -59,6 +59,19 @@ _SIGS = {
     "yoda_greedy": ([_vp, C.POINTER(CPodSoA), C.c_int, _u32, C.POINTER(C.c_int32)], C.c_int),
     "yoda_greedy_stats": ([_vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                            C.POINTER(C.c_double)], C.c_int),
+    "yoda_topk_k": ([], C.c_int),
+    "yoda_set_node_state": ([_vp, _u32, _vp, _vp, _vp], C.c_int),
+    "yoda_shard_topk": ([_vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "yoda_shard_best_one": ([_vp, _u32, C.POINTER(C.c_double), C.POINTER(C.c_int32)], C.c_int),
+    "yoda_gs_create": ([C.POINTER(CNodeSoA), C.POINTER(CPodSoA), _u32, C.POINTER(_vp)], C.c_int),
+    "yoda_gs_destroy": ([_vp], C.c_int),
+    "yoda_gs_queue_order": ([_vp, _vp], C.c_int),
+    "yoda_gs_begin_window": ([_vp, _u32, _u32, _u32, _vp, _vp, _vp], C.c_int),
+    "yoda_gs_resolve": ([_vp, C.POINTER(C.c_uint32)], C.c_int),
+    "yoda_gs_assign": ([_vp, _u32, C.c_int32], C.c_int),
+    "yoda_gs_take_dirty": ([_vp, _u32, _vp, _vp, _vp, C.POINTER(C.c_uint32)], C.c_int),
+    "yoda_gs_touched_original": ([_vp, _u32, _vp, _vp, _vp, C.POINTER(C.c_uint32)], C.c_int),
+    "yoda_gs_picks": ([_vp, _vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)], C.c_int),
 }
 
 
@@ -264,10 +277,122 @@ class Yoda:
                                                    _vp(d_best_local), _vp(d_idx), _vp(d_ties)),
                     "yoda_shard_prepare_merge")
 
+    def set_node_state(self, nodes: np.ndarray, alloc: np.ndarray, card_number: np.ndarray):
+        """Allocated memory / CardNumber of the listed GLOBAL node ids (others ignored)."""
+        n = np.ascontiguousarray(nodes, np.uint32)
+        a = np.ascontiguousarray(alloc, np.uint64)
+        c = np.ascontiguousarray(card_number, np.uint64)
+        self._check(lib().yoda_set_node_state(self._h, n.size, _np_ptr(n), _np_ptr(a),
+                                              _np_ptr(c)), "yoda_set_node_state")
+
+    def shard_topk(self, d_maxima: int, d_counts: int):
+        """(counts [2, P], top_score [k, P], top_node [k, P]) of the uploaded batch."""
+        P, k = self.n_pods, topk_k()
+        counts = np.zeros((2, max(P, 1)), np.uint32)
+        ts = np.zeros((k, max(P, 1)), np.float64)
+        ti = np.zeros((k, max(P, 1)), np.uint32)
+        self._check(lib().yoda_shard_topk(self._h, _vp(d_maxima), _vp(d_counts), _np_ptr(counts),
+                                          _np_ptr(ts), _np_ptr(ti)), "yoda_shard_topk")
+        return counts[:, :P], ts[:, :P], ti[:, :P]
+
+    def shard_best_one(self, pod: int):
+        """(raw score, global node or -1) of batch pod `pod` over this shard, current state."""
+        s, n = C.c_double(), C.c_int32()
+        self._check(lib().yoda_shard_best_one(self._h, pod, C.byref(s), C.byref(n)),
+                    "yoda_shard_best_one")
+        return s.value, n.value
+
     def shard_finalize(self, mode, d_counts, d_best, d_idx, d_ties, d_lowest):
         self._check(lib().yoda_shard_finalize(self._h, mode, _vp(d_counts), _vp(d_best),
                                               _vp(d_idx), _vp(d_ties), _vp(d_lowest)),
                     "yoda_shard_finalize")
+
+
+def topk_k() -> int:
+    """Candidates per pod in the greedy top-k lists (yoda_topk_k)."""
+    return int(lib().yoda_topk_k())
+
+
+def _np_ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+class GreedySession:
+    """Host-side sequential resolve of the sharded greedy batch (yoda_gs_*, include/yoda.h):
+    pure host code over the GLOBAL node set, identical on every rank."""
+
+    def __init__(self, nodes: NodeSoA, pods: PodSoA, flags: int = 0):
+        self._nodes = nodes.normalized()
+        self._pods = pods.normalized()
+        cn, cp = self._nodes.c(), self._pods.c()
+        self._g = _vp()
+        rc = lib().yoda_gs_create(C.byref(cn), C.byref(cp), flags, C.byref(self._g))
+        if rc != 0:
+            raise YodaError(f"yoda_gs_create: {ERRORS.get(rc, rc)}")
+        self.n_nodes, self.n_pods = self._nodes.n_nodes, self._pods.n_pods
+        self._buf_n = np.zeros(max(self.n_nodes, 1), np.uint32)
+        self._buf_a = np.zeros(max(self.n_nodes, 1), np.uint64)
+        self._buf_c = np.zeros(max(self.n_nodes, 1), np.uint64)
+
+    @staticmethod
+    def _check(rc: int, what: str):
+        if rc != 0:
+            raise YodaError(f"{what}: {ERRORS.get(rc, rc)}")
+
+    def close(self):
+        if self._g:
+            lib().yoda_gs_destroy(self._g)
+            self._g = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def queue_order(self) -> np.ndarray:
+        order = np.zeros(max(self.n_pods, 1), np.uint32)
+        self._check(lib().yoda_gs_queue_order(self._g, _np_ptr(order)), "yoda_gs_queue_order")
+        return order[:self.n_pods]
+
+    def begin_window(self, ws: int, k: int, counts, top_score, top_node):
+        c = np.ascontiguousarray(counts, np.uint32)
+        s = np.ascontiguousarray(top_score, np.float64)
+        i = np.ascontiguousarray(top_node, np.uint32)
+        wn = c.size // 2
+        self._check(lib().yoda_gs_begin_window(self._g, ws, wn, k, _np_ptr(c), _np_ptr(s),
+                                               _np_ptr(i)), "yoda_gs_begin_window")
+
+    def resolve(self) -> int:
+        nxt = C.c_uint32()
+        self._check(lib().yoda_gs_resolve(self._g, C.byref(nxt)), "yoda_gs_resolve")
+        return nxt.value
+
+    def assign(self, queue_pos: int, pick: int):
+        self._check(lib().yoda_gs_assign(self._g, queue_pos, pick), "yoda_gs_assign")
+
+    def _nodes_call(self, fn, what):
+        cnt = C.c_uint32()
+        self._check(fn(self._g, self._buf_n.size, _np_ptr(self._buf_n), _np_ptr(self._buf_a),
+                       _np_ptr(self._buf_c), C.byref(cnt)), what)
+        n = cnt.value
+        return self._buf_n[:n].copy(), self._buf_a[:n].copy(), self._buf_c[:n].copy()
+
+    def take_dirty(self):
+        """(nodes, alloc, card_number) changed since the last call."""
+        return self._nodes_call(lib().yoda_gs_take_dirty, "yoda_gs_take_dirty")
+
+    def touched_original(self):
+        """(nodes, alloc, card_number) of every node ever changed, original values."""
+        return self._nodes_call(lib().yoda_gs_touched_original, "yoda_gs_touched_original")
+
+    def picks(self):
+        """(pick [P] in input order, pods certified from lists, pods assigned by the caller)."""
+        pick = np.zeros(max(self.n_pods, 1), np.int32)
+        r, a = C.c_uint32(), C.c_uint32()
+        self._check(lib().yoda_gs_picks(self._g, _np_ptr(pick), C.byref(r), C.byref(a)),
+                    "yoda_gs_picks")
+        return pick[:self.n_pods], r.value, a.value
 
 
 def header_symbols(path: str = HEADER_PATH):

@@ -76,6 +76,20 @@ class Reducer:
         for t in ts:
             dist.all_reduce(t, op=rop, group=self.group)
 
+    def gather(self, arrays: Sequence[np.ndarray]) -> List[np.ndarray]:
+        """All-gather of one float64 array per local shard -> every shard's array (rank order).
+        Local mode: the arrays themselves.  RCCL needs device tensors, gloo host tensors."""
+        if self.local:
+            return [np.asarray(a, np.float64) for a in arrays]
+        import torch.distributed as dist
+        backend = dist.get_backend(self.group)
+        dev = (torch.device("cuda", torch.cuda.current_device()) if backend == "nccl"
+               else torch.device("cpu"))
+        t = torch.from_numpy(np.ascontiguousarray(arrays[0], np.float64)).to(dev)
+        out = [torch.empty_like(t) for _ in range(dist.get_world_size(self.group))]
+        dist.all_gather(out, t, group=self.group)
+        return [o.cpu().numpy() for o in out]
+
 
 def merge_phase1(reduce: Reducer, bufs: List[ShardBuffers]):
     """Global maxima (MAX, unsigned) and feasible / zero-total counts (SUM)."""
@@ -174,3 +188,122 @@ class ShardExchange:
 def shard_bounds(n_nodes: int, world: int) -> np.ndarray:
     """Contiguous node blocks, one per rank."""
     return np.linspace(0, n_nodes, world + 1).astype(np.int64)
+
+
+# ---- sharded greedy batch (config 5 across GPUs) ------------------------------------------
+GREEDY_CARD_CAPACITY = 1  # include/yoda.h YODA_GREEDY_CARD_CAPACITY
+
+
+class HandleShard:
+    """A libyoda handle (one node shard) as seen by sharded_greedy."""
+
+    def __init__(self, handle, device):
+        self.h = handle
+        self.device = device
+        self.bufs = None
+        if device.type == "cuda":
+            handle.set_stream(torch.cuda.current_stream(device).cuda_stream)
+
+    @property
+    def generic(self) -> bool:
+        return self.h.generic
+
+    def upload_pods(self, pods):
+        self.h.upload_pods(pods)
+
+    def phase1(self) -> ShardBuffers:
+        from .soa import MODE_SCV
+        if self.bufs is None or self.bufs.n_pods != self.h.n_pods:
+            self.bufs = ShardBuffers(self.h.n_pods, self.device)
+        self.h.shard_phase1(MODE_SCV, self.bufs.maxima.data_ptr(), self.bufs.counts.data_ptr())
+        return self.bufs
+
+    def topk(self):
+        return self.h.shard_topk(self.bufs.maxima.data_ptr(), self.bufs.counts.data_ptr())
+
+    def best_one(self, i: int):
+        return self.h.shard_best_one(i)
+
+    def set_node_state(self, nodes, alloc, card_number):
+        self.h.set_node_state(nodes, alloc, card_number)
+
+
+def merge_topk(ts_list: Sequence[np.ndarray], ti_list: Sequence[np.ndarray], k: int):
+    """The first k of the union of the shards' candidate lists ([k, P] each), in the lists'
+    order (score desc, node asc; padding -1.0 / 0xFFFFFFFF sorts last).  The global top-k is
+    contained in the union of the shards' top-k, so this is exact."""
+    S = np.concatenate([np.asarray(t, np.float64) for t in ts_list], axis=0)
+    I = np.concatenate([np.asarray(t).astype(np.uint64) for t in ti_list], axis=0)
+    o = np.lexsort((I, -S), axis=0)[:k]
+    return (np.take_along_axis(S, o, axis=0),
+            np.take_along_axis(I, o, axis=0).astype(np.uint32))
+
+
+def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window: int = 4096,
+                   stats: dict | None = None) -> np.ndarray:
+    """Greedy batch assignment (yoda_greedy's semantics: sort.go:8-10 queue order, each pick
+    adding the pod's scv/memory to the node, algorithm.go:299-303) over node shards.
+
+    Per window: K1 on every shard, maxima MAX / counts SUM all-reduced, per-shard top-k lists
+    all-gathered and merged, then the host session (identical on every rank) resolves the
+    window in queue order; a pod it cannot certify is scored exactly on every shard against
+    the current node state and the (score, node) candidates are all-gathered.  With
+    YODA_GREEDY_CARD_CAPACITY feasibility changes after every pick, so windows hold one pod.
+    `shards`: this process's shards (HandleShard); `nodes`: the FULL snapshot.  The shards'
+    node state is restored at the end."""
+    from .capi import GreedySession, topk_k
+    if any(s.generic for s in shards):
+        raise ValueError("sharded greedy needs a fast record path (N32/F64); the U64 path is "
+                         "served by the single-handle yoda_greedy")
+    k = topk_k()
+    gs = GreedySession(nodes, pods, flags)
+    order = gs.queue_order()
+    P = pods.n_pods
+    W = 1 if flags & GREEDY_CARD_CAPACITY else max(1, int(window))
+
+    def push():
+        n, a, c = gs.take_dirty()
+        if n.size:
+            for s in shards:
+                s.set_node_state(n, a, c)
+
+    windows = exact = 0
+    try:
+        for ws in range(0, P, W):
+            wn = min(W, P - ws)
+            push()
+            win = pods.take(order[ws:ws + wn])
+            for s in shards:
+                s.upload_pods(win)
+            merge_phase1(reduce, [s.phase1() for s in shards])
+            lists = [s.topk() for s in shards]
+            g = reduce.gather([np.stack([ts, ti.astype(np.float64)]) for _, ts, ti in lists])
+            ts, ti = merge_topk([x[0] for x in g], [x[1].astype(np.uint64) for x in g], k)
+            gs.begin_window(ws, k, lists[0][0], ts, ti)
+            while True:
+                i = gs.resolve()
+                if i >= wn:
+                    break
+                push()
+                cands = reduce.gather([np.array(s.best_one(i), np.float64) for s in shards])
+                bs, bn = -1.0, -1
+                for sc, nd in cands:
+                    nd = int(nd)
+                    if nd >= 0 and (sc > bs or (sc == bs and nd < bn)):
+                        bs, bn = float(sc), nd
+                if bn < 0:
+                    raise RuntimeError(f"greedy: no feasible node for window pod {i}")
+                gs.assign(ws + i, bn)
+                exact += 1
+            windows += 1
+        push()
+    finally:
+        n, a, c = gs.touched_original()
+        if n.size:
+            for s in shards:
+                s.set_node_state(n, a, c)
+    pick, resolved, assigned = gs.picks()
+    if stats is not None:
+        stats.update(windows=windows, exact_pods=exact, certified_pods=resolved)
+    gs.close()
+    return pick

@@ -1,0 +1,157 @@
+"""Sharded greedy batch (config 5 across GPUs) on CPU: the real driver (yoda_amd/dist.py
+sharded_greedy) and the real host session (libyoda yoda_gs_*, pure host code), with each
+shard's device work (K1 counts/maxima, top-k lists, exact single-pod best) computed by the
+oracle for that shard's nodes.  The picks must equal the sequential oracle's
+(oracle_greedy: sort.go:8-10 order, algorithm.go:299-303 assume), including the
+YODA_GREEDY_CARD_CAPACITY extension.  World 1 (three shards in one process) and world 2 over
+gloo."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from yoda_amd import synth
+from yoda_amd.capi import topk_k
+from yoda_amd.dist import Reducer, ShardBuffers, shard_bounds, sharded_greedy
+from yoda_amd.soa import MODE_SCV
+
+P, N = 60, 40
+
+
+def _cluster(contended=False, seed=5):
+    nodes = synth.make_nodes(N, seed=seed)
+    pods = synth.make_pods(P, seed=seed + 1, priorities=True)
+    if not contended:
+        nodes.total_memory_sum[3] = 0  # a zero-total node: the Error status
+        return nodes.normalized(), pods.normalized()
+    # identical nodes and pods: every candidate list is a tie, each pick drops its node below
+    # the list's threshold, and after k picks the resolve must fall back to exact scoring
+    for f in ("card_number", "card_count", "free_memory_sum", "total_memory_sum",
+              "alloc_memory"):
+        getattr(nodes, f)[:] = getattr(nodes, f)[0]
+    for f in ("card_free_memory", "card_total_memory", "card_clock", "card_bandwidth",
+              "card_core", "card_power", "card_healthy"):
+        getattr(nodes, f)[:] = getattr(nodes, f)[0]
+    pods.has_number[:], pods.number[:] = 1, 1
+    pods.has_memory[:], pods.memory[:] = 1, 2000
+    pods.has_clock[:] = 0
+    return nodes.normalized(), pods.normalized()
+
+
+class OracleShard:
+    """Nodes [lo, hi) of a mutable copy of the snapshot; device work done by the oracle."""
+    generic = False
+
+    def __init__(self, nodes, lo, hi):
+        self.nodes = nodes.slice(0, nodes.n_nodes)  # a copy
+        self.nodes.alloc_memory = np.array(nodes.alloc_memory, np.uint64)
+        self.nodes.card_number = np.array(nodes.card_number, np.uint64)
+        self.lo, self.hi = lo, hi
+        self.bufs = None
+
+    def upload_pods(self, pods):
+        self.pods = pods
+
+    def _detail(self, p):
+        _, feas, raw, _ = oracle.pod_detail(self.nodes, self.pods, p)
+        f = np.nonzero(feas[self.lo:self.hi])[0] + self.lo
+        return f, raw
+
+    def phase1(self):
+        n = self.pods.n_pods
+        res = oracle.schedule(self.nodes.slice(self.lo, self.hi), self.pods, MODE_SCV)
+        self.bufs = ShardBuffers(n, torch.device("cpu"))
+        self.bufs.maxima.copy_(torch.from_numpy(res.maxima.T.copy().reshape(-1).view(np.int64)))
+        nz = [int((self.nodes.total_memory_sum[self._detail(p)[0]] == 0).sum()) for p in range(n)]
+        self.bufs.counts.copy_(torch.tensor(list(res.n_feasible.astype(np.int64)) + nz,
+                                            dtype=torch.int32))
+        return self.bufs
+
+    def topk(self):
+        k, n = topk_k(), self.pods.n_pods
+        ts = np.full((k, n), -1.0)
+        ti = np.full((k, n), 0xFFFFFFFF, np.uint32)
+        for p in range(n):
+            f, raw = self._detail(p)
+            sc = np.where(self.nodes.total_memory_sum[f] == 0, 0, raw[f])
+            o = np.lexsort((f, -sc))[:k]
+            ts[:len(o), p], ti[:len(o), p] = sc[o], f[o]
+        counts = self.bufs.counts.numpy().view(np.uint32).reshape(2, n).copy()
+        return counts, ts, ti
+
+    def best_one(self, i):
+        f, raw = self._detail(i)
+        if f.size == 0:
+            return -1.0, -1
+        b = raw[f].max()
+        return float(b), int(f[raw[f] == b][0])
+
+    def set_node_state(self, nodes, alloc, card_number):
+        self.nodes.alloc_memory[nodes] = alloc
+        self.nodes.card_number[nodes] = card_number
+
+
+def _want(nodes, pods, flags):
+    pick, _ = oracle.greedy(nodes, pods, MODE_SCV, flags)
+    return pick
+
+
+@pytest.mark.parametrize("contended", [False, True])
+@pytest.mark.parametrize("flags,window", [(0, 7), (0, 4096), (1, 4096)])
+def test_sharded_greedy_local(flags, window, contended):
+    nodes, pods = _cluster(contended)
+    b = shard_bounds(N, 3)
+    shards = [OracleShard(nodes, int(b[r]), int(b[r + 1])) for r in range(3)]
+    stats = {}
+    got = sharded_greedy(shards, Reducer(local=True), nodes, pods, flags, window, stats)
+    np.testing.assert_array_equal(got, _want(nodes, pods, flags))
+    if contended and flags == 0 and window == 4096:
+        assert stats["exact_pods"] > 0  # the fallback path ran
+    for s in shards:  # node state restored
+        np.testing.assert_array_equal(s.nodes.alloc_memory, nodes.alloc_memory)
+        np.testing.assert_array_equal(s.nodes.card_number, nodes.card_number)
+
+
+def _worker(rank, world, port, flags, contended, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        nodes, pods = _cluster(contended)
+        b = shard_bounds(N, world)
+        shard = OracleShard(nodes, int(b[rank]), int(b[rank + 1]))
+        q.put((rank, sharded_greedy([shard], Reducer(), nodes, pods, flags, 16)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("flags,contended", [(0, False), (0, True), (1, False)])
+def test_sharded_greedy_gloo(flags, contended):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, flags, contended, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nodes, pods = _cluster(contended)
+    want = _want(nodes, pods, flags)
+    for rank, got in outs:
+        np.testing.assert_array_equal(got, want, err_msg=f"rank {rank}")
