@@ -5,8 +5,10 @@ Metric (BASELINE.json): pod-node pair evals/sec (filter+score+select) at 100k x 
 bit-exact picks.  One step = feasibility + PreScore maxima + score + NormalizeScore/select of
 ALL P pods over ALL N nodes (percentageOfNodesToScore 100), node snapshot and pods already
 resident in HBM, picks left in device memory.  Workload: BASELINE config 3 (100k pods x 100k
-nodes, K=8, seed 7; synthetic data), nodes sharded across ranks for --gpus N (strong
-scaling: total work fixed), merged by RCCL all-reduces (yoda_amd/dist.py).
+nodes, K=8, seed 7; synthetic data).  --gpus N (strong scaling: total work fixed): by
+default the nodes are sharded across ranks and the per-pod results merged with RCCL
+all-reduces (yoda_amd/dist.py); --shard pods gives each rank a pod slice and the whole node
+snapshot instead, with no collective (dist.pod_partition).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -211,6 +213,11 @@ def main():
     ap.add_argument("--check", action="store_true",
                     help="N>1: rank 0 re-evaluates the batch on one unsharded handle and "
                          "asserts identical picks / statuses / ties (rehearsal)")
+    ap.add_argument("--shard", choices=["nodes", "pods"], default="nodes",
+                    help="--gpus N > 1: nodes = node blocks merged by RCCL all-reduces "
+                         "(yoda_amd/dist.py); pods = each rank evaluates a pod slice against "
+                         "the whole node snapshot, no collective (dist.pod_partition; slower "
+                         "per rank on one MI355X, profiles/r01/current/shard_timing.txt)")
     ap.add_argument("--workload", choices=["eval", "greedy"], default="eval",
                     help="eval: the headline batch (config 3); greedy: config 5 sequential assume")
     args = ap.parse_args()
@@ -238,18 +245,29 @@ def main():
 
     nodes, pods = synth.make_config(args.config, pods=args.pods, nodes=args.nodes)
     P, N = pods.n_pods, nodes.n_nodes
-    from yoda_amd.dist import ShardExchange, shard_bounds
-    b = shard_bounds(N, world)
-    lo, hi = int(b[rank]), int(b[rank + 1])
+    from yoda_amd.dist import ShardExchange, pod_partition, shard_bounds
+    pod_shard = world > 1 and args.shard == "pods"
     y = Yoda(dev_index)
-    shard = nodes.slice(lo, hi)
-    y.upload_nodes(shard, node_offset=lo)
-    y.upload_pods(pods)
+    if pod_shard:
+        # rank r: pods part[r] x ALL nodes; nothing to exchange (dist.pod_partition)
+        my_pods_idx = pod_partition(pods, world)[rank]
+        my_pods = pods.take(my_pods_idx)
+        lo, hi = 0, N
+        shard = nodes
+        y.upload_nodes(nodes)
+        y.upload_pods(my_pods)
+    else:
+        my_pods = pods
+        b = shard_bounds(N, world)
+        lo, hi = int(b[rank]), int(b[rank + 1])
+        shard = nodes.slice(lo, hi)
+        y.upload_nodes(shard, node_offset=lo)
+        y.upload_pods(pods)
     y.set_stream(torch.cuda.current_stream(device).cuda_stream)
     k_slots = int(nodes.card_count.max()) if N else 1
     k_slots = 1 << max(0, (k_slots - 1).bit_length())
 
-    if world > 1:
+    if world > 1 and not pod_shard:
         ex = ShardExchange.distributed(y, device, shard=shard, offset=lo)
         step = lambda: ex.step(mode)  # noqa: E731
     else:
@@ -295,7 +313,8 @@ def main():
     k2_avg = k2_ms / max(launches, 1)
     names = kernel_names(y.path, mode)
     dom, dom_ms = (names[1], k2_avg) if k2_avg >= k1_avg else (names[0], k1_avg)
-    algo_bytes = P * n_local * bytes_per_pair(k_slots, mode)
+    p_local = my_pods.n_pods
+    algo_bytes = p_local * n_local * bytes_per_pair(k_slots, mode)
     achieved = algo_bytes / (dom_ms / 1e3) / 1e9 if dom_ms > 0 else 0.0
     pmc = committed_pmc(dom, P, N, world)
 
@@ -319,14 +338,16 @@ def main():
                                f", K={k_slots} card slots",
                    "pods": P, "nodes": N, "mode": args.mode,
                    "path": y.path,
-                   "parallelism": f"node-shard x{world}" + (" (RCCL all-reduce merge)"
-                                                            if world > 1 else "")},
+                   "parallelism": (f"pod-shard x{world} (whole node snapshot per GPU, "
+                                   "no collective)" if pod_shard else
+                                   f"node-shard x{world}" + (" (RCCL all-reduce merge)"
+                                                            if world > 1 else ""))},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": pmc.get("hbm_bytes_per_launch"),
                      "avg_launch_ms": dom_ms, "k1_avg_ms": k1_avg, "k2_avg_ms": k2_avg,
                      "bytes_per_pair": bytes_per_pair(k_slots, mode),
-                     "pairs_per_launch": P * n_local,
+                     "pairs_per_launch": p_local * n_local,
                      # achieved > peak: a node record is consulted once per 64-pod wave,
                      # not once per pair; the binding limits are these:
                      "traffic_gbs": (pmc["hbm_bytes_per_launch"] / (dom_ms / 1e3) / 1e9
@@ -345,10 +366,12 @@ def main():
         full.upload_nodes(nodes)
         ref = full.eval(pods, mode)
         full.close()
+        sel = my_pods_idx if pod_shard else slice(None)
         for f in ("pick", "status", "n_ties", "n_feasible"):
-            if not np.array_equal(getattr(res, f), getattr(ref, f)):
+            if not np.array_equal(getattr(res, f), getattr(ref, f)[sel]):
                 raise SystemExit(f"--check: sharded {f} differs from the unsharded handle")
-        out["check"] = "sharded picks/statuses/ties/feasible == unsharded"
+        out["check"] = ("rank 0's pod shard" if pod_shard else "merged") + \
+            " picks/statuses/ties/feasible == unsharded"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(nodes, pods, mode, args.cpu_seconds,
                                            args.cpu_threads, res)

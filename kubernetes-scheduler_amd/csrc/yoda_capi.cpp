@@ -9,6 +9,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -285,13 +286,25 @@ uint64_t static_score(uint64_t free_sum, uint64_t total_sum, uint64_t alloc, boo
 // to ~6 full "rounds" of the kernel's resident capacity (occupancy API), so the last round is
 // nearly full (efficiency >= 1 - pod_blocks / (6 cap)) and chunks stay small enough to
 // balance data-dependent work (K2 skips infeasible nodes).
+// Tuning knobs for A/B runs (tools/ab.sh): YODA_CHUNK_ROUNDS (default 6) and
+// YODA_MIN_CHUNK_NODES (default 0 = no floor; a floor keeps the per-(wave, chunk) set-up of
+// the block-classified kernels amortised when few pod blocks would otherwise mean many
+// small chunks, e.g. one rank's pod shard).  Read once per process.
+static uint32_t env_u32(const char* name, uint32_t dflt) {
+  const char* s = std::getenv(name);
+  return (s && *s) ? (uint32_t)std::strtoul(s, nullptr, 10) : dflt;
+}
+
 void plan_chunks_for(uint32_t cap, uint32_t n_pods, uint32_t n_nodes, uint32_t* C_out,
                      uint32_t* chunk_out) {
+  static const uint32_t rounds = std::max<uint32_t>(1, env_u32("YODA_CHUNK_ROUNDS", 6));
+  static const uint32_t min_chunk = env_u32("YODA_MIN_CHUNK_NODES", 0);
   const uint32_t pod_blocks = std::max<uint32_t>(1, (n_pods + kBlock - 1) / kBlock);
   const uint32_t max_chunks = std::max<uint32_t>(1, (n_nodes + kChunkAlign - 1) / kChunkAlign);
   if (cap == 0) cap = 2048;
-  uint32_t C = std::max<uint32_t>(1, (uint32_t)((6ull * cap) / pod_blocks));
+  uint32_t C = std::max<uint32_t>(1, (uint32_t)(((uint64_t)rounds * cap) / pod_blocks));
   C = std::min(C, max_chunks);
+  if (min_chunk) C = std::min(C, std::max<uint32_t>(1, (n_nodes + min_chunk - 1) / min_chunk));
   // a multiple of 8 chunks lets the kernels give each XCD whole chunks (tile() in
   // yoda_kernels.hip); trailing chunks may then be empty (they write identity partials)
   const bool xcd = C >= 8;

@@ -6,13 +6,21 @@ Per batch:
      CollectMaxValues is a reduction over ALL nodes (collection.go:30-55), so the maxima
      must be global before any score is final.
   2. K2 on the shard with the global maxima -> per-pod (best raw score MAX, then the lowest
-     node index among shards reaching it MIN, tie counts SUM, lowest raw score MIN).
+     node index among shards reaching it and the lowest raw score in ONE MIN, tie counts
+     SUM).
 Collectives are torch.distributed all-reduces on device tensors (backend "nccl" = RCCL over
 xGMI on MI355X; "gloo" in the CPU tests).  libyoda launches on torch's current stream so
 the collectives are ordered after the kernels without host synchronisation.
 
 uint64/uint32 buffers are reduced through their signed views with the sign bit flipped,
 which maps unsigned order onto signed order (MAX/MIN stay exact for all 64-bit values).
+
+An evaluation batch can instead be POD-sharded (`pod_partition`): every rank holds the whole
+node snapshot (100k nodes are ~70 MB of 288 GB) and a slice of the pods, and no collective
+is needed at all (bench.py --shard pods).  Node sharding stays the default: its per-rank
+kernels are faster on one MI355X at 2-8 ranks (each rank's K1/K2 keep all 100k pods' wave
+classes; profiles/r01/current/shard_timing.txt), and it is the path for node sets split
+across GPUs and for the greedy batch (whose picks change node state).
 """
 from __future__ import annotations
 
@@ -40,7 +48,12 @@ class ShardBuffers:
         self.best_g = torch.empty(P, dtype=torch.int64, device=device)
         self.idx = torch.empty(P, dtype=torch.int32, device=device)         # u32
         self.ties = torch.empty(P, dtype=torch.int32, device=device)        # u32
-        self.lowest = torch.empty(P, dtype=torch.int64, device=device)
+        # [lowest i64 | idx widened to i64]: both merge by MIN, so one all-reduce serves both
+        self.mins = torch.empty(2 * P, dtype=torch.int64, device=device)
+        self.lowest = self.mins[:P]
+        # maxima need the sign flip only when a field can exceed 2^63 (U64 path); the fast
+        # record paths bound every field by 2^44
+        self.unsigned_maxima = True
 
     @staticmethod
     def ptr(t: torch.Tensor) -> int:
@@ -93,11 +106,14 @@ class Reducer:
 
 def merge_phase1(reduce: Reducer, bufs: List[ShardBuffers]):
     """Global maxima (MAX, unsigned) and feasible / zero-total counts (SUM)."""
-    for b in bufs:
-        _flip(b.maxima, I64_SIGN)
+    flip = any(b.unsigned_maxima for b in bufs)
+    if flip:
+        for b in bufs:
+            _flip(b.maxima, I64_SIGN)
     reduce([b.maxima for b in bufs], "max")
-    for b in bufs:
-        _flip(b.maxima, I64_SIGN)
+    if flip:
+        for b in bufs:
+            _flip(b.maxima, I64_SIGN)
     reduce([b.counts for b in bufs], "sum")
 
 
@@ -110,12 +126,12 @@ def merge_phase2(reduce: Reducer, bufs: List[ShardBuffers],
     reduce([b.best_g for b in bufs], "max")
     for b in bufs:
         prepare(b)
-        _flip(b.idx, I32_SIGN)
-    reduce([b.idx for b in bufs], "min")
+        hi = b.mins[b.lowest.numel():]
+        hi.copy_(b.idx).bitwise_and_(0xFFFFFFFF)  # u32 order as non-negative i64
+    reduce([b.mins for b in bufs], "min")         # lowest and idx together
     for b in bufs:
-        _flip(b.idx, I32_SIGN)
+        b.idx.copy_(b.mins[b.lowest.numel():])    # back to the u32 bit pattern
     reduce([b.ties for b in bufs], "sum")
-    reduce([b.lowest for b in bufs], "min")
 
 
 def agree_on_path(reduce: Reducer, handles, shards, offsets, device):
@@ -135,11 +151,14 @@ def agree_on_path(reduce: Reducer, handles, shards, offsets, device):
 class ShardExchange:
     """Drives libyoda handles (one per shard) through the sharded entry points."""
 
-    def __init__(self, handles, reducer: Reducer, device):
+    def __init__(self, handles, reducer: Reducer, device, path_code=None):
         self.handles = list(handles)
         self.reduce = reducer
         self.device = device
         self.bufs = [ShardBuffers(h.n_pods, device) for h in self.handles]
+        if path_code is not None and path_code != 2:  # agreed fast path: maxima < 2^63
+            for b in self.bufs:
+                b.unsigned_maxima = False
         stream = torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0
         for h in self.handles:
             h.set_stream(stream)
@@ -149,17 +168,19 @@ class ShardExchange:
         """Several shards in one process (single-GPU testing).  Pass the node shards to
         enforce a common record path."""
         red = Reducer(local=True)
+        path = None
         if shards is not None:
-            agree_on_path(red, handles, shards, offsets, device)
-        return cls(handles, red, device)
+            path = agree_on_path(red, handles, shards, offsets, device)
+        return cls(handles, red, device, path)
 
     @classmethod
     def distributed(cls, handle, device, shard=None, offset=0, group=None):
         """One shard per rank over torch.distributed (RCCL)."""
         red = Reducer(group=group)
+        path = None
         if shard is not None:
-            agree_on_path(red, [handle], [shard], [offset], device)
-        return cls([handle], red, device)
+            path = agree_on_path(red, [handle], [shard], [offset], device)
+        return cls([handle], red, device, path)
 
     def _prepare(self, h, b: ShardBuffers):
         p = ShardBuffers.ptr
@@ -188,6 +209,45 @@ class ShardExchange:
 def shard_bounds(n_nodes: int, world: int) -> np.ndarray:
     """Contiguous node blocks, one per rank."""
     return np.linspace(0, n_nodes, world + 1).astype(np.int64)
+
+
+POD_BLOCK = 256  # pods per K1/K2 workgroup (4 waves of 64), yoda_kernels.hip
+
+
+def pod_partition(pods, world: int, by_key: bool = True,
+                  block: int = POD_BLOCK, snake: bool = False) -> List[np.ndarray]:
+    """Pod sharding of an evaluation batch: rank r evaluates pods part[r] (input indices)
+    against the WHOLE node snapshot.  Every pod's Filter / PreScore maxima / Score / select
+    reads only the node snapshot (collection.go:30-55, algorithm.go:96, scheduler.go:158-183;
+    the batch has no assume between its pods), so the ranks exchange nothing: the union of
+    their results is the unsharded result.  Any partition is exact.
+
+    by_key (default): sort the batch by the request key (scv/clock, scv/number, scv/memory —
+    the device sort's key, yoda_order.hip), cut it into blocks of `block` pods and deal the
+    blocks round-robin.  Each block is a workgroup's worth of near-identical requests, as in
+    one global sort, so the block classes of K1/K2 work as well per rank as on
+    one GPU; dealing them cyclically gives every rank the same mix of cheap and expensive
+    requests (contiguous key ranges are 2x out of balance at 8 ranks: a low scv/clock
+    request is feasible on many more nodes).  Part sizes differ by at most `block`.
+    by_key=False: contiguous slices of the input order (sizes differ by at most 1)."""
+    P = pods.n_pods
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    if not by_key or not P:
+        return [np.ascontiguousarray(x)
+                for x in np.array_split(np.arange(P, dtype=np.int64), world)]
+    c = np.where(pods.has_clock != 0, pods.clock, 0).astype(np.uint64)
+    n = np.where(pods.has_number != 0, pods.number, 0).astype(np.uint64)
+    m = np.where(pods.has_memory != 0, pods.memory, 0).astype(np.uint64)
+    order = np.lexsort((np.arange(P), m, n, c)).astype(np.int64)
+    blocks = [order[i:i + block] for i in range(0, P, block)]
+    owner = np.arange(len(blocks)) % world
+    if snake:  # boustrophedon deal: 0..W-1, W-1..0, ...
+        rev = (np.arange(len(blocks)) // world) % 2 == 1
+        owner = np.where(rev, world - 1 - owner, owner)
+    mine = [[b for b, o in zip(blocks, owner) if o == r] for r in range(world)]
+    return [np.ascontiguousarray(np.concatenate(x) if x else np.zeros(0, np.int64))
+            for x in mine]
 
 
 # ---- sharded greedy batch (config 5 across GPUs) ------------------------------------------

@@ -131,3 +131,33 @@ def test_gloo_shard_merge(world):
 
 
 PORTS = {2: _free_port(), 3: _free_port()}
+
+
+@pytest.mark.parametrize("by_key", [True, False])
+def test_pod_partition_covers_batch(by_key):
+    """dist.pod_partition (bench.py's default --gpus N sharding): disjoint, balanced, covers
+    every pod, deterministic; and evaluating each part separately against the whole node
+    snapshot gives the unsharded result (the oracle is the checker; pods exchange nothing)."""
+    from yoda_amd.dist import pod_partition
+    nodes, pods = synth.make_config(2, pods=301, nodes=400)
+    want = oracle.schedule(nodes, pods, MODE_SCV, threads=4)
+    for world in (1, 2, 3, 8):
+        parts = pod_partition(pods, world, by_key=by_key, block=16)
+        assert len(parts) == world
+        sizes = [len(p) for p in parts]
+        assert max(sizes) - min(sizes) <= (16 if by_key else 1)
+        allp = np.concatenate(parts)
+        assert np.array_equal(np.sort(allp), np.arange(pods.n_pods))
+        if by_key:  # whole key-sorted blocks, dealt round-robin
+            key = np.lexsort((np.arange(pods.n_pods), pods.memory * pods.has_memory,
+                              pods.number * pods.has_number, pods.clock * pods.has_clock))
+            assert np.array_equal(parts[0][:16], key[:16])
+            if world > 1:
+                assert np.array_equal(parts[1][:16], key[16:32])
+        again = pod_partition(pods, world, by_key=by_key, block=16)
+        assert all(np.array_equal(a, b) for a, b in zip(parts, again))
+        for idx in parts[:2]:
+            got = oracle.schedule(nodes, pods.take(idx), MODE_SCV, threads=4)
+            for f in ("pick", "status", "n_feasible", "n_ties", "top_score"):
+                assert np.array_equal(getattr(got, f), getattr(want, f)[idx]), f
+    assert [len(p) for p in pod_partition(pods.slice(0, 0), 3)] == [0, 0, 0]

@@ -327,6 +327,30 @@ def test_sharded_merge_on_one_gpu(dev):
             y.close()
 
 
+@pytest.mark.parametrize("by_key", [True, False])
+def test_pod_sharded_on_one_gpu(dev, by_key):
+    """Pod sharding (bench.py --gpus N default): G handles, each with the WHOLE node snapshot
+    and the pods of dist.pod_partition; the union of their results is the oracle's, with
+    nothing exchanged.  More than 128 pods per shard so the device pod sort runs per shard."""
+    from yoda_amd.dist import pod_partition
+    nodes, pods = synth.make_config(2, pods=1500, nodes=3000)
+    for mode in (MODE_SCV, MODE_DISKIO):
+        want = oracle.schedule(nodes, pods, mode, threads=8)
+        for G in (1, 2, 3, 8):
+            parts = pod_partition(pods, G, by_key=by_key)
+            dev.upload_nodes(nodes)
+            for idx in parts:
+                got = dev.eval(pods.take(idx), mode)
+                for f in ("status", "pick", "n_feasible"):
+                    np.testing.assert_array_equal(getattr(got, f), getattr(want, f)[idx],
+                                                  err_msg=f"{f} G={G}")
+                ok = want.status[idx] == 0
+                np.testing.assert_array_equal(got.n_ties[ok], want.n_ties[idx][ok])
+                np.testing.assert_array_equal(got.top_score[ok], want.top_score[idx][ok])
+                if mode == MODE_SCV:
+                    np.testing.assert_array_equal(got.maxima, want.maxima[idx])
+
+
 def test_sharded_paths_agree(dev):
     """One shard needs the F64 path (a wide field), the other would pick N32: both must
     end on F64, and the merged result must equal the single-handle result."""
