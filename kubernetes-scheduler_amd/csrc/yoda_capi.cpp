@@ -190,10 +190,12 @@ struct yoda_handle {
   // order and are un-permuted by their transposes, the per-pod outputs by finalize().
   bool order_enabled = true;
   bool ordered = false;
-  DevBuf pod_sorted, perm, order_scratch, unperm;
+  DevBuf pod_sorted, perm, order_scratch;
 
   // state
   DevBuf maxima, counts, rcp, rcp32, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
+  // scatter targets of unpermute_outputs, swapped with the buffers above after each scatter
+  DevBuf pick_alt, status_alt, ties_out_alt, counts_alt, best_alt, maxima_alt;
   DevBuf bitmask, bitmask_t, rows, rows_t;
   DevBuf blk;               // [wave][node block / 64] u64: blocks with a feasible pod (K1 -> K2)
   bool blk_valid = false;   // the last K1 wrote blk (block-classified K1 on this batch)
@@ -234,14 +236,15 @@ struct yoda_handle {
   ~yoda_handle() {
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &pod_blob,   &maxima,       &counts,
-                     &pod_sorted, &perm,     &order_scratch, &unperm,
+                     &pod_sorted, &perm,     &order_scratch,
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
                      &n_flagged, &bitmask,   &bitmask_t,  &blk,  &p_max_u,      &p_cnt,
                      &rows,      &rows_t,    &tk_s_part,  &tk_i_part,    &tk_s,
                      &tk_i,      &upd_node,  &upd_val,    &upd_cn,    &g1_part,   &g1_done,
                      &p_best_f,  &p_best_i,  &p_idx,      &p_ties,       &p_low_f,
-                     &p_low_i,   &p_err};
+                     &p_low_i,   &p_err,     &pick_alt,   &status_alt,   &ties_out_alt,
+                     &counts_alt, &best_alt, &maxima_alt};
     for (DevBuf* b : all) b->release();
     pod_stage.release();
     upd_stage.release();
@@ -437,39 +440,29 @@ int order_pods(yoda_t* h, int mode) {
 int unpermute_outputs(yoda_t* h) {
   const uint32_t P = h->n_pods;
   if (!h->ordered || P == 0) return YODA_OK;
+  // Scatter every row into a second buffer of the same shape, then swap the two: no copy
+  // back (the swapped-out buffers become the next scatter's targets).
   struct Arr {
     DevBuf* buf;
-    size_t row;
+    DevBuf* alt;
+    uint32_t rows;
     uint32_t bytes;
   };
-  const Arr arrs[] = {{&h->pick, 0, 4},   {&h->status, 0, 4}, {&h->ties_out, 0, 4},
-                      {&h->counts, 0, 4}, {&h->counts, 1, 4}, {&h->best, 0, 8},
-                      {&h->maxima, 0, 8}, {&h->maxima, 1, 8}, {&h->maxima, 2, 8},
-                      {&h->maxima, 3, 8}, {&h->maxima, 4, 8}, {&h->maxima, 5, 8}};
-  size_t total = 0;
-  for (const Arr& a : arrs) total += (size_t)P * a.bytes;
-  HIP_TRY(h, h->unperm.ensure(total));
+  const Arr arrs[] = {{&h->pick, &h->pick_alt, 1, 4},         {&h->status, &h->status_alt, 1, 4},
+                      {&h->ties_out, &h->ties_out_alt, 1, 4}, {&h->counts, &h->counts_alt, 2, 4},
+                      {&h->best, &h->best_alt, 1, 8},         {&h->maxima, &h->maxima_alt, 6, 8}};
   PermTable t{};
-  size_t off = 0;
   for (const Arr& a : arrs) {
-    t.src[t.n] = a.buf->as<unsigned char>() + a.row * P * a.bytes;
-    t.dst[t.n] = h->unperm.as<unsigned char>() + off;
-    t.bytes[t.n] = a.bytes;
-    ++t.n;
-    off += (size_t)P * a.bytes;
+    HIP_TRY(h, a.alt->ensure((size_t)a.rows * P * a.bytes));
+    for (uint32_t r = 0; r < a.rows; ++r) {
+      t.src[t.n] = a.buf->as<unsigned char>() + (size_t)r * P * a.bytes;
+      t.dst[t.n] = a.alt->as<unsigned char>() + (size_t)r * P * a.bytes;
+      t.bytes[t.n] = a.bytes;
+      ++t.n;
+    }
   }
   HIP_TRY(h, launch_permute(t, h->perm.as<uint32_t>(), P, true, h->stream));
-  // the rows of one buffer are contiguous in both places: one copy per buffer
-  off = 0;
-  for (size_t i = 0; i < sizeof(arrs) / sizeof(arrs[0]);) {
-    size_t j = i, bytes = 0;
-    while (j < sizeof(arrs) / sizeof(arrs[0]) && arrs[j].buf == arrs[i].buf)
-      bytes += (size_t)P * arrs[j++].bytes;
-    HIP_TRY(h, hipMemcpyAsync(arrs[i].buf->p, h->unperm.as<unsigned char>() + off, bytes,
-                              hipMemcpyDeviceToDevice, h->stream));
-    off += bytes;
-    i = j;
-  }
+  for (const Arr& a : arrs) std::swap(*a.buf, *a.alt);
   return YODA_OK;
 }
 
