@@ -85,8 +85,8 @@ hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes, uint3
                              hipStream_t st);
 size_t order_scratch_bytes(uint32_t n_pods);
 hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
-                             uint32_t n_pods, void* scratch, size_t scratch_bytes,
-                             uint32_t* perm, hipStream_t s);
+                             uint32_t n_pods, const uint32_t key_bits[3], void* scratch,
+                             size_t scratch_bytes, uint32_t* perm, hipStream_t s);
 hipError_t launch_permute(const PermTable& t, const uint32_t* perm, uint32_t n_pods, bool scatter,
                           hipStream_t s);
 }  // namespace yoda
@@ -191,6 +191,7 @@ struct yoda_handle {
   bool order_enabled = true;
   bool ordered = false;
   DevBuf pod_sorted, perm, order_scratch;
+  uint32_t key_bits[3] = {24, 8, 32};  // widths of the batch's sort-key fields (c, n, m)
 
   // state
   DevBuf maxima, counts, rcp, rcp32, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
@@ -422,6 +423,7 @@ int order_pods(yoda_t* h, int mode) {
   HIP_TRY(h, launch_order_pods(reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodNumber]),
                                reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodMU]),
                                reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodCU]), P,
+                               h->key_bits,
                                h->order_scratch.p, h->order_scratch.bytes,
                                h->perm.as<uint32_t>(), h->stream));
   PermTable t{};
@@ -942,6 +944,7 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     uint32_t* nm = reinterpret_cast<uint32_t*>(st + off[kPodNeedMem]);
     uint32_t* nc = reinterpret_cast<uint32_t*>(st + off[kPodNeedClk]);
     const uint64_t kClamp = 1ull << 53;  // > every F64-path card field (<= 2^44)
+    uint64_t key_or[3] = {0, 0, 0};       // OR of the sort key's clamped fields (c, n, m)
     for (uint32_t p = 0; p < P; ++p) {
       const uint64_t number = pd->has_number[p] ? pd->number[p] : 1;  // filter.go:12-15
       const uint64_t m = pd->has_memory[p] ? pd->memory[p] : 0;       // filter.go:19,32
@@ -956,6 +959,9 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
       cf[p] = (double)std::min(c, kClamp);
       m32[p] = (uint32_t)std::min<uint64_t>(m, 0xffffffffull);  // > every N32 field
       c32[p] = (uint32_t)std::min<uint64_t>(c, 0xffffffffull);
+      key_or[0] |= std::min<uint64_t>(c, 0xffffffull);  // the clamps of k_order_keys
+      key_or[1] |= std::min<uint64_t>(number, 0xffull);
+      key_or[2] |= std::min<uint64_t>(m, 0xffffffffull);
       al[p] = be[p] = 0.0;
       if (pd->rio && pd->rcpu) {  // algorithm.go:105-106
         const double beta = 1.0 / (1.0 + (double)pd->rcpu[p] / pd->rio[p]);
@@ -967,6 +973,11 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     HIP_TRY(h, hipEventRecord(h->stage_event, h->stream));
     h->stage_pending = true;
     for (int a = 0; a < kPodArrays; ++a) h->pod_off[a] = off[a];
+    for (int f = 0; f < 3; ++f) {
+      uint32_t bits = 0;
+      while (bits < 64 && (key_or[f] >> bits)) ++bits;
+      h->key_bits[f] = bits;
+    }
     h->n_pods = P;
     h->has_pods = true;
     h->ran = false;

@@ -18,19 +18,23 @@
 
 namespace yoda {
 
-// key = clock (24 bits, clamped) | number (8 bits) | memory (32 bits): ascending clock puts
-// the K1 `clock >= c` skips together too.  Any key is correct; this one is just fast.
+// key = clock (clamped to 24 bits) | number (8 bits) | memory (32 bits), lexicographic:
+// ascending clock puts the K1 `clock >= c` skips together too.  Any key is correct; this one
+// is just fast.  The fields are packed at the widths the batch actually uses (host: the OR
+// of each clamped field at upload), so the radix sort runs over bn + bm + bc bits only —
+// same order as the full-width key, fewer passes.
 __global__ __launch_bounds__(kBlock) void k_order_keys(const uint64_t* __restrict__ number,
                                                        const uint64_t* __restrict__ m_u,
                                                        const uint64_t* __restrict__ c_u,
-                                                       uint32_t n_pods, uint64_t* __restrict__ keys,
+                                                       uint32_t n_pods, uint32_t n_shift,
+                                                       uint32_t c_shift, uint64_t* __restrict__ keys,
                                                        uint32_t* __restrict__ idx) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (p >= n_pods) return;
   const uint64_t c = c_u[p] < 0xffffffull ? c_u[p] : 0xffffffull;
   const uint64_t n = number[p] < 0xffull ? number[p] : 0xffull;
   const uint64_t m = m_u[p] < 0xffffffffull ? m_u[p] : 0xffffffffull;
-  keys[p] = (c << 40) | (n << 32) | m;
+  keys[p] = (c << c_shift) | (n << n_shift) | m;
   idx[p] = p;
 }
 
@@ -60,8 +64,14 @@ size_t order_scratch_bytes(uint32_t n_pods) {
 
 // perm[i] = the original index of the i-th pod in sorted order.
 hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
-                             uint32_t n_pods, void* scratch, size_t scratch_bytes,
-                             uint32_t* perm, hipStream_t s) {
+                             uint32_t n_pods, const uint32_t key_bits[3], void* scratch,
+                             size_t scratch_bytes, uint32_t* perm, hipStream_t s) {
+  // key_bits = widths of (c, n, m); each <= its clamp (24, 8, 32), so the total is <= 64
+  const uint32_t bc = key_bits[0] < 24 ? key_bits[0] : 24;
+  const uint32_t bn = key_bits[1] < 8 ? key_bits[1] : 8;
+  const uint32_t bm = key_bits[2] < 32 ? key_bits[2] : 32;
+  const uint32_t n_shift = bm, c_shift = bm + bn;
+  const int end_bit = (int)(bc + bn + bm) > 0 ? (int)(bc + bn + bm) : 1;
   unsigned char* b = static_cast<unsigned char*>(scratch);
   uint64_t* keys_in = reinterpret_cast<uint64_t*>(b);
   uint64_t* keys_out = keys_in + n_pods;
@@ -69,11 +79,11 @@ hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const 
   unsigned char* temp = b + ((16ull * n_pods + 4ull * n_pods + 255) / 256 * 256);
   size_t temp_bytes = scratch_bytes - (size_t)(temp - b);
   hipLaunchKernelGGL(k_order_keys, dim3((n_pods + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                     number, m_u, c_u, n_pods, keys_in, idx_in);
+                     number, m_u, c_u, n_pods, n_shift, c_shift, keys_in, idx_in);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, perm,
-                                            (int)n_pods, 0, 64, s);
+                                            (int)n_pods, 0, end_bit, s);
 }
 
 hipError_t launch_permute(const PermTable& t, const uint32_t* perm, uint32_t n_pods, bool scatter,
