@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--kinds", default="key256,key64,contig")
     ap.add_argument("--reverse", action="store_true", help="time the ranks last to first")
+    ap.add_argument("--all-ranks", action="store_true", help="node shards: time every rank")
     args = ap.parse_args()
     nodes, pods = synth.make_config(3)
     P, N = pods.n_pods, nodes.n_nodes
@@ -70,7 +71,7 @@ def main():
             b = shard_bounds(N, W)
             y.upload_pods(pods)
             per_rank = []
-            for r in (0, W - 1):
+            for r in ((list(range(W))[::-1] if args.reverse else list(range(W))) if args.all_ranks else (0, W - 1)):
                 y.upload_nodes(nodes.slice(int(b[r]), int(b[r + 1])), node_offset=int(b[r]))
                 y.run(MODE_SCV)
                 torch.cuda.synchronize(dev)
@@ -79,7 +80,8 @@ def main():
                     y.run(MODE_SCV)
                 torch.cuda.synchronize(dev)
                 per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
-            print(f"W={W} nodes  ms/step ranks 0, W-1 (kernels only, no merge): "
+            print(f"W={W} nodes  ms/step ranks {'all' if args.all_ranks else '0, W-1'} "
+                  f"(kernels only, no merge): "
                   f"{' '.join(f'{t:.3f}' for t in per_rank)}", flush=True)
             y.upload_nodes(nodes)
     y.close()
