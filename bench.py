@@ -218,6 +218,9 @@ def main():
                          "(yoda_amd/dist.py); pods = each rank evaluates a pod slice against "
                          "the whole node snapshot, no collective (dist.pod_partition; slower "
                          "per rank on one MI355X, profiles/r01/current/shard_timing.txt)")
+    ap.add_argument("--no-balance", action="store_true",
+                    help="--shard nodes: keep equal node blocks (default: re-cut them once "
+                         "after warm-up so every rank's measured K1 + K2 time is equal)")
     ap.add_argument("--workload", choices=["eval", "greedy"], default="eval",
                     help="eval: the headline batch (config 3); greedy: config 5 sequential assume")
     args = ap.parse_args()
@@ -282,6 +285,33 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
+    if world > 1 and not pod_shard and not args.no_balance:
+        # Setup, before the timed region: re-cut the node blocks so every rank's K1 + K2
+        # time is equal (the cost per node is data-dependent), then re-upload.
+        import torch.distributed as dist
+        from yoda_amd.dist import balanced_bounds
+        for _ in range(2):
+            y.profile(True)
+            for _ in range(3):
+                step()
+            barrier()
+            y.profile(False)
+            k1, k2, nl = y.profile_read()
+            cost = torch.tensor([(k1 + k2) / max(nl, 1)], dtype=torch.float64, device=device)
+            costs = [torch.zeros_like(cost) for _ in range(world)]
+            dist.all_gather(costs, cost)
+            nb = balanced_bounds(b, [float(t.item()) for t in costs])
+            if np.array_equal(nb, b) or np.abs(nb - b).max() < 64:
+                break
+            b = nb
+            lo, hi = int(b[rank]), int(b[rank + 1])
+            shard = nodes.slice(lo, hi)
+            y.upload_nodes(shard, node_offset=lo)
+            ex = ShardExchange.distributed(y, device, shard=shard, offset=lo)
+            step = lambda: ex.step(mode)  # noqa: E731
+            for _ in range(max(args.warmup, 1)):
+                step()
+            barrier()
     y.profile(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -341,7 +371,9 @@ def main():
                    "parallelism": (f"pod-shard x{world} (whole node snapshot per GPU, "
                                    "no collective)" if pod_shard else
                                    f"node-shard x{world}" + (" (RCCL all-reduce merge)"
-                                                            if world > 1 else ""))},
+                                                            if world > 1 else "")),
+                   "node_bounds": [int(v) for v in b] if world > 1 and not pod_shard
+                   else None},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": pmc.get("hbm_bytes_per_launch"),

@@ -214,6 +214,27 @@ def shard_bounds(n_nodes: int, world: int) -> np.ndarray:
 POD_BLOCK = 256  # pods per K1/K2 workgroup (4 waves of 64), yoda_kernels.hip
 
 
+def balanced_bounds(bounds, costs) -> np.ndarray:
+    """New contiguous node bounds with equal estimated cost per rank: the cost of each old
+    shard (e.g. its measured K1 + K2 time) is spread evenly over its nodes, and the new bounds
+    are the equal-cost quantiles of that piecewise-linear cumulative cost.  Every shard keeps
+    at least one node (when there are as many nodes as ranks).  Any contiguous split is exact;
+    this one only evens out the ranks' step times."""
+    b = np.asarray(bounds, np.float64)
+    c = np.maximum(np.asarray(costs, np.float64), 0.0)
+    W = len(c)
+    n = int(b[-1])
+    if W <= 1 or c.sum() <= 0 or n < W:
+        return np.asarray(bounds, np.int64)
+    cum = np.concatenate([[0.0], np.cumsum(c)])
+    targets = cum[-1] * np.arange(1, W) / W
+    new = np.interp(targets, cum, b)
+    out = np.concatenate([[0], np.rint(new), [n]]).astype(np.int64)
+    for k in range(1, W):  # strictly increasing, room for the later shards
+        out[k] = min(max(out[k], out[k - 1] + 1), n - (W - k))
+    return out
+
+
 def pod_partition(pods, world: int, by_key: bool = True,
                   block: int = POD_BLOCK, snake: bool = False) -> List[np.ndarray]:
     """Pod sharding of an evaluation batch: rank r evaluates pods part[r] (input indices)

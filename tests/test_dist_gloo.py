@@ -161,3 +161,23 @@ def test_pod_partition_covers_batch(by_key):
             for f in ("pick", "status", "n_feasible", "n_ties", "top_score"):
                 assert np.array_equal(getattr(got, f), getattr(want, f)[idx]), f
     assert [len(p) for p in pod_partition(pods.slice(0, 0), 3)] == [0, 0, 0]
+
+
+def test_balanced_bounds():
+    """dist.balanced_bounds (bench.py re-cuts node blocks by measured K1 + K2 time)."""
+    from yoda_amd.dist import balanced_bounds
+    b = shard_bounds(100_000, 8)
+    assert np.array_equal(balanced_bounds(b, [1.0] * 8), b)  # already even
+    costs = [0.86] + [0.71] * 7
+    nb = balanced_bounds(b, costs)
+    assert nb[0] == 0 and nb[-1] == 100_000 and np.all(np.diff(nb) > 0)
+    assert nb[1] < b[1]  # the expensive first shard shrinks
+    # estimated cost per new shard (cost spread evenly within each old shard) is equal
+    dens = np.repeat(np.array(costs) / np.diff(b), np.diff(b))
+    per = [dens[nb[k]:nb[k + 1]].sum() for k in range(8)]
+    assert max(per) - min(per) < 1e-3 * sum(per)
+    # degenerate inputs: zero costs, one rank, as many nodes as ranks
+    assert np.array_equal(balanced_bounds(b, [0.0] * 8), b)
+    assert np.array_equal(balanced_bounds([0, 10], [3.0]), [0, 10])
+    tight = balanced_bounds([0, 1, 2, 3], [100.0, 0.0, 0.0])
+    assert np.array_equal(tight, [0, 1, 2, 3])

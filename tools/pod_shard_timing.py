@@ -80,6 +80,22 @@ def main():
                     y.run(MODE_SCV)
                 torch.cuda.synchronize(dev)
                 per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
+            if args.all_ranks and not args.reverse:
+                from yoda_amd.dist import balanced_bounds
+                nb = balanced_bounds(b, per_rank)
+                bal = []
+                for r in range(W):
+                    y.upload_nodes(nodes.slice(int(nb[r]), int(nb[r + 1])),
+                                   node_offset=int(nb[r]))
+                    y.run(MODE_SCV)
+                    torch.cuda.synchronize(dev)
+                    t0 = time.perf_counter()
+                    for _ in range(args.steps):
+                        y.run(MODE_SCV)
+                    torch.cuda.synchronize(dev)
+                    bal.append((time.perf_counter() - t0) / args.steps * 1e3)
+                print(f"W={W} nodes  balanced bounds {list(map(int, nb))}: "
+                      f"{' '.join(f'{t:.3f}' for t in bal)}  max {max(bal):.3f}", flush=True)
             print(f"W={W} nodes  ms/step ranks {'all' if args.all_ranks else '0, W-1'} "
                   f"(kernels only, no merge): "
                   f"{' '.join(f'{t:.3f}' for t in per_rank)}", flush=True)
