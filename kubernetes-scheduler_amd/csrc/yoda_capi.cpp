@@ -1362,6 +1362,15 @@ struct PodGather {
 };
 
 constexpr uint32_t kGreedyWindow = 4096;
+// A/B knob: YODA_GREEDY_WINDOW overrides the window size (pods per GPU window).
+uint32_t greedy_window() {
+  static const uint32_t w = [] {
+    const char* s = std::getenv("YODA_GREEDY_WINDOW");
+    const unsigned long v = (s && *s) ? std::strtoul(s, nullptr, 10) : 0;
+    return v >= 64 && v <= (1u << 20) ? (uint32_t)v : kGreedyWindow;
+  }();
+  return w;
+}
 
 // Exact evaluation of ONE pod against the current device state (pushes pending updates).
 int greedy_eval_one(GreedyState& g, const yoda_pod_soa* pods, uint32_t p, int mode,
@@ -1496,7 +1505,7 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
       const uint32_t KT = (uint32_t)topk_k();
       // Small windows: the GPU work is the same P x N in total, while fewer nodes are
       // touched per window, so fewer candidate lists lose certification.
-      const uint32_t W = std::min<uint32_t>(P, kGreedyWindow);
+      const uint32_t W = std::min<uint32_t>(P, greedy_window());
       PodGather win;
       std::vector<uint32_t> counts(2 * (size_t)W);
       std::vector<double> ts((size_t)KT * W);
