@@ -38,6 +38,23 @@ __global__ __launch_bounds__(kBlock) void k_order_keys(const uint64_t* __restric
   idx[p] = p;
 }
 
+// The same key when it fits 32 bits (the usual case: clock < 2^11, number < 2^4, memory in
+// MiB < 2^17): half the bytes per radix pass.
+__global__ __launch_bounds__(kBlock) void k_order_keys32(const uint64_t* __restrict__ number,
+                                                         const uint64_t* __restrict__ m_u,
+                                                         const uint64_t* __restrict__ c_u,
+                                                         uint32_t n_pods, uint32_t n_shift,
+                                                         uint32_t c_shift, uint32_t* __restrict__ keys,
+                                                         uint32_t* __restrict__ idx) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= n_pods) return;
+  const uint64_t c = c_u[p] < 0xffffffull ? c_u[p] : 0xffffffull;
+  const uint64_t n = number[p] < 0xffull ? number[p] : 0xffull;
+  const uint64_t m = m_u[p] < 0xffffffffull ? m_u[p] : 0xffffffffull;
+  keys[p] = (uint32_t)((c << c_shift) | (n << n_shift) | m);
+  idx[p] = p;
+}
+
 // gather (dst[i] = src[perm[i]]) or scatter (dst[perm[i]] = src[i]) of up to kPermArrays
 // per-pod arrays of 4 or 8 bytes; grid.y = array.
 __global__ __launch_bounds__(kBlock) void k_permute(PermTable t, const uint32_t* __restrict__ perm,
@@ -55,11 +72,14 @@ __global__ __launch_bounds__(kBlock) void k_permute(PermTable t, const uint32_t*
 
 // Scratch for the sort: keys[2][P] u64, idx[2][P] u32, then hipcub's temp storage.
 size_t order_scratch_bytes(uint32_t n_pods) {
-  size_t temp = 0;
+  size_t temp = 0, temp32 = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const uint64_t*)nullptr,
                                            (uint64_t*)nullptr, (const uint32_t*)nullptr,
                                            (uint32_t*)nullptr, (int)n_pods);
-  return 16ull * n_pods + 8ull * n_pods + 256 + temp;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, temp32, (const uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (const uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (int)n_pods);
+  return 16ull * n_pods + 8ull * n_pods + 256 + (temp > temp32 ? temp : temp32);
 }
 
 // perm[i] = the original index of the i-th pod in sorted order.
@@ -78,6 +98,16 @@ hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const 
   uint32_t* idx_in = reinterpret_cast<uint32_t*>(keys_out + n_pods);
   unsigned char* temp = b + ((16ull * n_pods + 4ull * n_pods + 255) / 256 * 256);
   size_t temp_bytes = scratch_bytes - (size_t)(temp - b);
+  if (end_bit <= 32) {
+    uint32_t* k32_in = reinterpret_cast<uint32_t*>(keys_in);
+    uint32_t* k32_out = reinterpret_cast<uint32_t*>(keys_out);
+    hipLaunchKernelGGL(k_order_keys32, dim3((n_pods + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                       number, m_u, c_u, n_pods, n_shift, c_shift, k32_in, idx_in);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k32_in, k32_out, idx_in, perm,
+                                              (int)n_pods, 0, end_bit, s);
+  }
   hipLaunchKernelGGL(k_order_keys, dim3((n_pods + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
                      number, m_u, c_u, n_pods, n_shift, c_shift, keys_in, idx_in);
   hipError_t e = hipGetLastError();
