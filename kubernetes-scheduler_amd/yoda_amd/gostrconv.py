@@ -26,7 +26,10 @@ I64_MIN = -(1 << 63)
 
 def atoi(s: str) -> Tuple[int, bool]:
     """strconv.Atoi on a 64-bit platform: (value, ok).  On a syntax error the value is 0;
-    on a range error it is clamped to MaxInt64 / MinInt64 (ParseInt's behaviour)."""
+    on a range error it is clamped to MaxInt64 / MinInt64 (ParseInt's behaviour).
+
+    The range is decided from the digit count before any int() conversion: a label of
+    thousands of digits must clamp like Go does, not hit CPython's int-string limit."""
     if 0 < len(s) < 19:  # fast path: no underscores, plain decimal
         body = s[1:] if s[0] in "+-" else s
         if not body or any(not ("0" <= ch <= "9") for ch in body):
@@ -40,7 +43,9 @@ def atoi(s: str) -> Tuple[int, bool]:
     body = s[1:] if s[0] in "+-" else s
     if not body or any(not ("0" <= ch <= "9") for ch in body):
         return 0, False
-    n = int(body)
+    digits = body.lstrip("0")
+    # 2^63 has 19 digits: anything longer is out of range whatever the digits are
+    n = int(digits) if 0 < len(digits) <= 19 else (0 if not digits else 1 << 64)
     if not neg and n > I64_MAX:
         return I64_MAX, False
     if neg and n > (1 << 63):
@@ -113,9 +118,55 @@ def _round_to_bits(q: Fraction, mant_bits: int, emin: int, emax: int) -> float:
     return float(Fraction(n) * scale)
 
 
+# Decimal digits that decide a correctly rounded binary64 (767 suffice; Go's decimal
+# fallback keeps 800): longer mantissas are cut there with a sticky digit.
+_MAX_SIG_DIGITS = 800
+
+
+def _digits_to_int(d: str, base: int = 10) -> int:
+    """int(d, base) without CPython's limit on decimal string length (chunked)."""
+    if base != 10 or len(d) <= 4000:
+        return int(d, base) if d else 0
+    n = 0
+    for i in range(0, len(d), 4000):
+        c = d[i:i + 4000]
+        n = n * 10 ** len(c) + int(c)
+    return n
+
+
+def _exponent(e: str) -> int:
+    """Decimal exponent text -> int, saturated (Go saturates the exponent at 10000 too)."""
+    e = e.replace("_", "")
+    sign = -1 if e.startswith("-") else 1
+    body = e.lstrip("+-").lstrip("0") or "0"
+    return sign * (int(body) if len(body) <= 9 else 10 ** 9)
+
+
+def _dec_fraction(ip: str, fp: str, ex: int, bit_size: int):
+    """Exact (or sticky-truncated) rational value of ip.fp e ex, or 'inf' / 'zero' when the
+    decimal exponent alone decides overflow / underflow (no huge powers are built)."""
+    digits = (ip + fp).lstrip("0")
+    if not digits:
+        return Fraction(0)
+    # value = 0.digits * 10^(e10)
+    e10 = len(ip + fp) - len(fp) + ex - ((len(ip + fp)) - len(digits))
+    hi = 40 if bit_size == 32 else 310    # 0.d * 10^40 > MaxFloat32, 10^310 > MaxFloat64
+    lo = -50 if bit_size == 32 else -330  # below half the smallest subnormal
+    if e10 > hi:
+        return "inf"
+    if e10 < lo:
+        return "zero"
+    if len(digits) > _MAX_SIG_DIGITS:
+        sticky = digits[_MAX_SIG_DIGITS:].strip("0") != ""
+        digits = digits[:_MAX_SIG_DIGITS] + ("1" if sticky else "")
+    return Fraction(_digits_to_int(digits)) * Fraction(10) ** (e10 - len(digits))
+
+
 def parse_float(s: str, bit_size: int = 64) -> Tuple[float, bool]:
     """strconv.ParseFloat(s, bitSize): (value, ok).  bitSize 32 returns the nearest float32
-    as a float64.  Syntax error -> (0, False); overflow -> (±Inf, False)."""
+    as a float64.  Syntax error -> (0, False); overflow -> (±Inf, False); underflow -> ±0.
+    The cost is bounded by the string length: huge exponents are decided before any big
+    power is built (a '1e999999999' annotation must not stall the packer)."""
     t = s
     neg = False
     if t and t[0] in "+-":
@@ -130,10 +181,19 @@ def parse_float(s: str, bit_size: int = 64) -> Tuple[float, bool]:
     m = _HEX.match(t)
     if m and ("_" not in t or _underscore_ok(s)):
         ip, fp, ex = (m.group(1) or "").replace("_", ""), (m.group(2) or "").replace("_", ""), \
-            m.group(3).replace("_", "")
+            _exponent(m.group(3))
         if ip or fp:
-            q = Fraction(int(ip + fp, 16) if (ip + fp) else 0) * Fraction(2) ** int(ex) \
-                / Fraction(16) ** len(fp)
+            mant = _digits_to_int(ip + fp, 16)
+            if mant == 0:
+                q = Fraction(0)
+            else:
+                e2 = ex - 4 * len(fp) + mant.bit_length()  # value in [2^(e2-1), 2^e2)
+                if e2 > 1100:
+                    q = "inf"
+                elif e2 < -1200:
+                    q = "zero"
+                else:
+                    q = Fraction(mant) * Fraction(2) ** (ex - 4 * len(fp))
     else:
         m = _DEC.match(t)
         if m and (m.group(1) or m.group(2)):
@@ -143,11 +203,15 @@ def parse_float(s: str, bit_size: int = 64) -> Tuple[float, bool]:
             fp = (m.group(2) or "").replace("_", "")
             if m.group(3) is not None and not m.group(3).replace("_", "").lstrip("+-"):
                 return 0.0, False
-            ex = int(m.group(3).replace("_", "")) if m.group(3) else 0
+            ex = _exponent(m.group(3)) if m.group(3) else 0
             if ip or fp:
-                q = Fraction(int(ip + fp) if (ip + fp) else 0) * Fraction(10) ** (ex - len(fp))
+                q = _dec_fraction(ip, fp, ex, bit_size)
     if q is None:
         return 0.0, False
+    if q == "inf":
+        return (-math.inf if neg else math.inf), False
+    if q == "zero":
+        return (-0.0 if neg else 0.0), True
     if bit_size == 32:
         v = _round_to_bits(q, 24, -126, 127)
     else:

@@ -61,6 +61,44 @@ def test_parse_float32(s, want, ok):
     assert got_ok == ok and v == want
 
 
+@pytest.mark.parametrize("s,want,ok", [
+    ("1e999999999", math.inf, False), ("-1e999999999", -math.inf, False),
+    ("1e-999999999", 0.0, True), ("0e999999999", 0.0, True), ("0x1p999999999", math.inf, False),
+    ("1" * 5000, math.inf, False), ("1" * 5000 + "e-4990", 1111111111.1111112, True),
+    ("0." + "0" * 5000 + "25e5001", 2.5, True), ("1e" + "9" * 5000, math.inf, False)])
+def test_parse_float_bounded(s, want, ok):
+    """Huge exponents and long mantissas are decided from the digit counts (Go returns
+    ±Inf / range error or 0 at once); the packer must neither stall nor raise on them."""
+    import time
+    t0 = time.perf_counter()
+    v, got_ok = g.parse_float(s, 64)
+    assert (v, got_ok) == (want, ok)
+    assert g.parse_float(s, 32)[1] == ok
+    assert time.perf_counter() - t0 < 1.0
+
+
+@pytest.mark.parametrize("digits", [20, 5000])
+def test_long_integer_labels_clamp(digits):
+    """A 20- or 5000-digit scv/* label is a range error in Go's Atoi: StrToUint64 gives 0,
+    GetPodPriority the clamped MaxInt64 / MinInt64 (no CPython int-string limit error)."""
+    assert g.str_to_uint("9" * digits) == 0
+    assert g.pod_priority("9" * digits) == (1 << 63) - 1
+    assert g.pod_priority("-" + "9" * digits) == -(1 << 63)
+    assert g.atoi("0" * digits + "42") == (42, True)
+    pod = {"metadata": {"labels": {"scv/memory": "7" * digits, "scv/priority": "8" * digits},
+                        "annotations": {"diskIO": "1e" + "9" * digits}}}
+    p = pack_pods([pod])
+    assert (p.has_memory[0], p.memory[0], p.priority[0]) == (1, 0, (1 << 63) - 1)
+    assert p.rio[0] == math.inf
+
+
+def test_parse_float_matches_correct_rounding():
+    rng = np.random.default_rng(3)
+    for _ in range(3000):
+        s = f"{int(rng.integers(1, 10 ** 17))}e{int(rng.integers(-340, 312))}"
+        assert g.parse_float(s, 64)[0] == float(s), s
+
+
 def test_parse_float32_rounds_once():
     # correctly rounded to float32 directly from the decimal (no double rounding)
     rng = np.random.default_rng(0)
