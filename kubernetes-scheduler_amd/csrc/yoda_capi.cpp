@@ -23,7 +23,8 @@ namespace yoda {
 hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigned char* sum,
                      uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                      uint32_t n_pods, const Partials& part, uint64_t* bm, uint32_t bm_stride,
-                     uint64_t* blk, uint32_t blk_stride, hipStream_t s);
+                     BlockMask* bs, uint32_t bs_stride, uint64_t* blk, uint32_t blk_stride,
+                     hipStream_t s);
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool narrow,
                           uint64_t* maxima, uint32_t* counts, hipStream_t s);
 hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
@@ -32,8 +33,8 @@ hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigne
                      const uint64_t* blk, uint32_t blk_stride, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
                      const double* rcp, const float* rcp32, uint32_t n_pods,
-                     const uint64_t* bm, uint32_t bm_stride, const Partials& part,
-                     int64_t* rows, hipStream_t s);
+                     const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
+                     uint32_t bs_stride, const Partials& part, int64_t* rows, hipStream_t s);
 hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
                             uint32_t C, const PodParams& pp, uint32_t n_pods, const Partials& part,
                             int64_t* rows, hipStream_t s);
@@ -60,14 +61,16 @@ hipError_t launch_k3(int K, const unsigned char* nodes, uint32_t n_nodes, uint32
 hipError_t launch_reduce3(const Partials& part, uint32_t C, const uint32_t* flagged,
                           const uint32_t* n_flagged, uint32_t max_flagged, uint32_t node_offset,
                           int32_t* pick, int32_t* status, uint32_t* ties, hipStream_t s);
-hipError_t launch_bitmask_transpose(const uint64_t* bm, uint32_t bm_stride, uint32_t n_nodes,
+hipError_t launch_bitmask_transpose(const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
+                                    uint32_t bs_stride, uint32_t n_nodes,
                                     uint32_t W, uint32_t n_pods, const uint32_t* perm,
                                     uint32_t* out, hipStream_t s);
 int kernel_capacity(int K, Path path, int which, int mode_diskio);
 hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                           uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                           const double* rcp, const float* rcp32, uint32_t n_pods,
-                          const uint64_t* bm, uint32_t bm_stride, const Partials& part,
+                          const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
+                          uint32_t bs_stride, const Partials& part,
                           double* tk_s, uint32_t* tk_i, hipStream_t s);
 hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t C,
                              uint32_t n_pods, uint32_t node_offset, double* out_s,
@@ -81,6 +84,7 @@ uint32_t greedy_one_blocks();
 hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                              const PodParams& pp, const double* rcp, const float* rcp32,
                              uint32_t n_pods, uint32_t s, const uint64_t* bm, uint32_t bm_stride,
+                             const BlockMask* bs, uint32_t bs_stride,
                              double* part_s, uint32_t* part_i, uint32_t* done, uint32_t* out,
                              hipStream_t st);
 size_t order_scratch_bytes(uint32_t n_pods);
@@ -200,6 +204,9 @@ struct yoda_handle {
   DevBuf bitmask, bitmask_t, rows, rows_t;
   DevBuf blk;               // [wave][node block / 64] u64: blocks with a feasible pod (K1 -> K2)
   bool blk_valid = false;   // the last K1 wrote blk (block-classified K1 on this batch)
+  DevBuf bsum;              // [wave][node block] BlockMask: the block K1's sparse masks
+  bool bm_sparse = false;   // the last K1 wrote the sparse form (bsum + partial masks only)
+  const BlockMask* bs_ptr() const { return bm_sparse ? bsum.as<BlockMask>() : nullptr; }
   // greedy
   DevBuf tk_s_part, tk_i_part, tk_s, tk_i, upd_node, upd_val, upd_cn;
   DevBuf g1_part, g1_done;  // k_greedy_one partials + block counter (zeroed once)
@@ -240,7 +247,7 @@ struct yoda_handle {
                      &pod_sorted, &perm,     &order_scratch,
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
-                     &n_flagged, &bitmask,   &bitmask_t,  &blk,  &p_max_u,      &p_cnt,
+                     &n_flagged, &bitmask,   &bitmask_t,  &blk,  &bsum, &p_max_u,      &p_cnt,
                      &rows,      &rows_t,    &tk_s_part,  &tk_i_part,    &tk_s,
                      &tk_i,      &upd_node,  &upd_val,    &upd_cn,    &g1_part,   &g1_done,
                      &p_best_f,  &p_best_i,  &p_idx,      &p_ties,       &p_low_f,
@@ -348,6 +355,7 @@ int ensure_state(yoda_t* h, uint32_t P) {
   // [wave][node] u64 masks (yoda_layout.h), +8 words: K2 reads masks in groups of 8
   HIP_TRY(h, h->bitmask.ensure(((size_t)(P + 63) / 64 * bm_row(h->n_nodes) + 8) * 8));
   HIP_TRY(h, h->blk.ensure((size_t)(P + 63) / 64 * blk_row(h->n_nodes) * 8));
+  HIP_TRY(h, h->bsum.ensure((size_t)(P + 63) / 64 * bs_row(h->n_nodes) * sizeof(BlockMask)));
   HIP_TRY(h, h->p_max_u.ensure(6 * CP * 8));
   if (h->generic) {
     HIP_TRY(h, h->p_best_i.ensure(CP * 8));
@@ -489,14 +497,15 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts) {
   hipEvent_t e1 = h->profiling ? h->next_event() : nullptr;
   if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
   h->blk_valid = h->has_k1sum;
+  h->bm_sparse = h->has_k1sum;  // the block K1 writes the sparse form
   if (h->blk_valid)
     HIP_TRY(h, hipMemsetAsync(h->blk.p, 0, (size_t)(P + 63) / 64 * blk_row(h->n_nodes) * 8,
                               h->stream));
   HIP_TRY(h, launch_k1(h->K, h->path, h->nodes.as<unsigned char>(),
                        h->has_k1sum ? h->k1sum.as<unsigned char>() : nullptr, h->n_nodes,
                        h->chunk1, h->C1, pod_params(h), P, part, h->bitmask.as<uint64_t>(),
-                       bm_row(h->n_nodes), h->blk.as<uint64_t>(), blk_row(h->n_nodes),
-                       h->stream));
+                       bm_row(h->n_nodes), h->bsum.as<BlockMask>(), bs_row(h->n_nodes),
+                       h->blk.as<uint64_t>(), blk_row(h->n_nodes), h->stream));
   if (e1) {
     HIP_TRY(h, hipEventRecord(e1, h->stream));
     h->ev_k1.emplace_back(e0, e1);
@@ -538,7 +547,7 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, int64_t* best, uint32_t*
                          h->n_nodes,
                          h->chunk2, h->C2, pod_params(h), maxima, h->rcp.as<double>(),
                          h->rcp32.as<float>(), P, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
-                         part, rows, h->stream));
+                         h->bs_ptr(), bs_row(h->n_nodes), part, rows, h->stream));
     is_f64 = !h->generic;
   }
   if (e1) {
@@ -1073,7 +1082,8 @@ int yoda_download_bitmask(yoda_t* h, uint32_t* words, uint64_t n_words) {
   if (need == 0) return YODA_OK;
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, h->bitmask_t.ensure(need * 4));
-  HIP_TRY(h, launch_bitmask_transpose(h->bitmask.as<uint64_t>(), bm_row(h->n_nodes), h->n_nodes,
+  HIP_TRY(h, launch_bitmask_transpose(h->bitmask.as<uint64_t>(), bm_row(h->n_nodes), h->bs_ptr(),
+                                      bs_row(h->n_nodes), h->n_nodes,
                                       W, h->n_pods,
                                       h->ordered ? h->perm.as<uint32_t>() : nullptr,
                                       h->bitmask_t.as<uint32_t>(), h->stream));
@@ -1407,8 +1417,8 @@ int greedy_eval_fast(GreedyState& g, uint32_t s, int32_t* pick_out) {
   uint32_t* done = h->g1_done.as<uint32_t>();
   HIP_TRY(h, launch_greedy_one(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes,
                                pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(),
-                               h->n_pods, s, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes), ps,
-                               pi, done, done + 1, h->stream));
+                               h->n_pods, s, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
+                               h->bs_ptr(), bs_row(h->n_nodes), ps, pi, done, done + 1, h->stream));
   HIP_TRY(h, h->pick_stage.ensure(16));
   HIP_TRY(h, hipMemcpyAsync(h->pick_stage.p, done + 1, 4, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
@@ -1536,7 +1546,7 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
           HIP_TRY(h, launch_k2_topk(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk2,
                                     h->C2, pod_params(h), h->rcp.as<double>(),
                                     h->rcp32.as<float>(), wn, h->bitmask.as<uint64_t>(),
-                                    bm_row(N),
+                                    bm_row(N), h->bs_ptr(), bs_row(N),
                                     partials(h), h->tk_s_part.as<double>(),
                                     h->tk_i_part.as<uint32_t>(), h->stream));
           HIP_TRY(h, launch_topk_merge(h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),
@@ -1775,8 +1785,8 @@ int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_count
                               h->rcp32.as<float>(), h->stream));
       HIP_TRY(h, launch_k2_topk(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk2, h->C2,
                                 pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(), P,
-                                h->bitmask.as<uint64_t>(), bm_row(N), partials(h),
-                                h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),
+                                h->bitmask.as<uint64_t>(), bm_row(N), h->bs_ptr(), bs_row(N),
+                                partials(h), h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),
                                 h->stream));
       HIP_TRY(h, launch_topk_merge(h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(), h->C2,
                                    P, h->node_offset, h->tk_s.as<double>(),
@@ -1831,8 +1841,8 @@ int yoda_shard_best_one(yoda_t* h, uint32_t pod, double* score, int32_t* node) {
   uint32_t* done = h->g1_done.as<uint32_t>();
   HIP_TRY(h, launch_greedy_one(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes,
                                pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(),
-                               h->n_pods, s, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes), ps,
-                               pi, done, done + 1, h->stream));
+                               h->n_pods, s, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
+                               h->bs_ptr(), bs_row(h->n_nodes), ps, pi, done, done + 1, h->stream));
   HIP_TRY(h, h->pick_stage.ensure(16));
   HIP_TRY(h, hipMemcpyAsync(h->pick_stage.p, done, 16, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(h, hipStreamSynchronize(h->stream));

@@ -346,8 +346,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
     const uint32_t* __restrict__ c_in, const uint64_t* __restrict__ number_in,
     const uint32_t* __restrict__ need_mem_in, const uint32_t* __restrict__ need_clk_in,
     uint32_t n_pods, uint64_t* __restrict__ pmax, uint32_t* __restrict__ pcnt,
-    uint64_t* __restrict__ bm, uint32_t bm_stride, uint64_t* __restrict__ blk,
-    uint32_t blk_stride) {
+    uint64_t* __restrict__ bm, uint32_t bm_stride, BlockMask* __restrict__ bs,
+    uint32_t bs_stride, uint64_t* __restrict__ blk, uint32_t blk_stride) {
   constexpr uint32_t SS = k1sum_stride(K);
   constexpr uint32_t NS = n32_stride(K);
   constexpr uint32_t HW = K + 1;  // LDS words per node: hfs[0..K-1], 0
@@ -363,6 +363,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
   const uint64_t live_mask = ballot(live);
   if (live_mask == 0) return;  // a wave past the batch: no bitmask row, no partials
   uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
+  BlockMask* bsw = bs + (size_t)uniform_u32(p >> 6) * bs_stride;
 
   uint32_t m = 0, c = 0, need_mem = 0, need_clk = 0;
   uint64_t number = ~0ull;
@@ -507,8 +508,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
       const uint64_t b = ballot(f);
       set_lane(lo, hi, b, (uint32_t)j);
     }
-    bm_store(bmw, nb, n1, lo, hi);
-    if (ballot(valid && (lo | hi) != 0u) != 0) {
+    // sparse masks: the block's (nz, full) words always, a node's own mask only when it is
+    // neither empty nor the wave's live mask (the ALL / NONE nodes cost no mask traffic)
+    const uint64_t mine = ((uint64_t)hi << 32) | lo;
+    const bool nzl = valid && mine != 0ull, fulll = nzl && mine == live_mask;
+    const uint64_t nz_b = ballot(nzl), full_b = ballot(fulll);
+    if (nzl && !fulll) bmw[nb + lane] = mine;
+    if (lane == 0) bsw[nb >> 6] = BlockMask{nz_b, full_b};
+    if (nz_b != 0) {
       const uint32_t bi = nb >> 6;
       if ((bi >> 6) != blk_wi) {
         blk_flush();
@@ -546,6 +553,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
 __device__ __forceinline__ bool bm_bit(const uint64_t* __restrict__ bm, uint32_t bm_stride,
                                        uint32_t p, uint32_t n) {
   return (bm[(size_t)(p >> 6) * bm_stride + n] >> (p & 63u)) & 1ull;
+}
+
+// Live pods of wave w of a batch of n_pods (bit l: pod 64 w + l < n_pods).
+__device__ __forceinline__ uint64_t wave_live(uint32_t w, uint32_t n_pods) {
+  const uint32_t rem = n_pods - min(n_pods, 64u * w);
+  return rem >= 64u ? ~0ull : ((1ull << rem) - 1ull);
+}
+
+// Where a kernel reads the feasibility masks: dense [wave][node] (bs == nullptr; the per-node
+// K1s) or the block K1's sparse form (yoda_layout.h BlockMask).
+struct MaskSrc {
+  const uint64_t* bm;
+  const BlockMask* bs;
+  uint32_t bm_stride, bs_stride;
+};
+
+// Mask of (wave w, node n) for a thread that reads single masks (not the hot kernels).
+__device__ __forceinline__ uint64_t mask_at(const MaskSrc& m, uint32_t w, uint32_t n,
+                                            uint32_t n_pods) {
+  if (!m.bs) return m.bm[(size_t)w * m.bm_stride + n];
+  const BlockMask b = m.bs[(size_t)w * m.bs_stride + (n >> 6)];
+  const uint32_t j = n & 63u;
+  if ((b.full >> j) & 1ull) return wave_live(w, n_pods);
+  if ((b.nz >> j) & 1ull) return m.bm[(size_t)w * m.bm_stride + n];
+  return 0ull;
 }
 
 // Per-pod merge of K1 chunk partials -> maxima [6][P] and counts [2][P].  One thread per
@@ -788,7 +820,7 @@ constexpr int kTopK = 8;
 template <int K, Path PATH, int OUT>
 __global__ __launch_bounds__(kBlock) void k2_score(
     const unsigned char* __restrict__ nodes, uint32_t n_nodes, uint32_t chunk_nodes,
-    ScoreArgs args, uint32_t n_pods, const uint64_t* __restrict__ bm, uint32_t bm_stride,
+    ScoreArgs args, uint32_t n_pods, const MaskSrc ms,
     double* __restrict__ pbest, uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties,
     double* __restrict__ plow, int64_t* __restrict__ rows, double* __restrict__ tk_s,
     uint32_t* __restrict__ tk_i) {
@@ -798,8 +830,10 @@ __global__ __launch_bounds__(kBlock) void k2_score(
   const uint32_t n0 = chunk * chunk_nodes;
   const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
   const bool live = p < n_pods;
-  if (ballot(live) == 0) return;  // a wave past the batch
-  const uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
+  const uint64_t live_mask = ballot(live);
+  if (live_mask == 0) return;  // a wave past the batch
+  const uint32_t w = uniform_u32(p >> 6);
+  const uint64_t* bmw = ms.bm + (size_t)w * ms.bm_stride;
   const uint32_t lane = lane_id();
   Scorer<PATH> sc;
   if (live) sc.load(args, p, n_pods);
@@ -815,48 +849,67 @@ __global__ __launch_bounds__(kBlock) void k2_score(
       ti[k] = 0xffffffffu;
     }
   }
-  // The wave's feasibility masks of 8 nodes come in with one scalar load; a node no pod of
-  // the wave can use costs a scalar compare, a group of 8 such nodes one more.
-  for (uint32_t g = n0; g < n1; g += 8) {
-    const Group<uint64_t, 8> mk = load_group<uint64_t, 8>(
-        reinterpret_cast<const unsigned char*>(bmw + g));
-    if ((mk.v[0] | mk.v[1] | mk.v[2] | mk.v[3] | mk.v[4] | mk.v[5] | mk.v[6] | mk.v[7]) == 0)
-      continue;
+  // score node n for this lane's pod (the caller checked the lane's feasibility bit)
+  auto visit = [&](uint32_t n) {
+    const double raw = sc.template raw<K>(nodes + (size_t)n * stride);
+    if constexpr (OUT == OUT_ROWS) rows[(size_t)n * n_pods + p] = (int64_t)raw;
+    if constexpr (OUT == OUT_TOPK) {
+      // strict '>' keeps the earlier (lower) node first among equal scores
+      if (raw > ts[kTopK - 1]) {
+        double cs = raw;
+        uint32_t ci = n;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-    const uint32_t n = g + (uint32_t)j;
-    if (mk.v[j] == 0 || n >= n1) continue;
-    if ((mk.v[j] >> lane) & 1ull) {
-      const double raw = sc.template raw<K>(nodes + (size_t)n * stride);
-      if constexpr (OUT == OUT_ROWS) rows[(size_t)n * n_pods + p] = (int64_t)raw;
-      if constexpr (OUT == OUT_TOPK) {
-        // strict '>' keeps the earlier (lower) node first among equal scores
-        if (raw > ts[kTopK - 1]) {
-          double cs = raw;
-          uint32_t ci = n;
-#pragma unroll
-          for (int k = 0; k < kTopK; ++k) {
-            // (score desc, node asc): a carried entry that ties a slot must still shift
-            const bool gt = cs > ts[k] || (cs == ts[k] && ci < ti[k]);
-            const double os = ts[k];
-            const uint32_t oi = ti[k];
-            ts[k] = gt ? cs : os;
-            ti[k] = gt ? ci : oi;
-            cs = gt ? os : cs;
-            ci = gt ? oi : ci;
-          }
+        for (int k = 0; k < kTopK; ++k) {
+          // (score desc, node asc): a carried entry that ties a slot must still shift
+          const bool gt = cs > ts[k] || (cs == ts[k] && ci < ti[k]);
+          const double os = ts[k];
+          const uint32_t oi = ti[k];
+          ts[k] = gt ? cs : os;
+          ti[k] = gt ? ci : oi;
+          cs = gt ? os : cs;
+          ci = gt ? oi : ci;
         }
-      } else {
-        if (raw > best) {
-          best = raw;
-          idx = n;
-          ties = 1;
-        } else if (raw == best) {
-          ++ties;
-        }
-        low = fmin(low, raw);
+      }
+    } else {
+      if (raw > best) {
+        best = raw;
+        idx = n;
+        ties = 1;
+      } else if (raw == best) {
+        ++ties;
+      }
+      low = fmin(low, raw);
+    }
+  };
+  if (ms.bs) {
+    // sparse masks: one (nz, full) pair per 64 nodes through the scalar path; a partial
+    // node's own mask is one more scalar load
+    const BlockMask* bsw = ms.bs + (size_t)w * ms.bs_stride;
+    for (uint32_t nb = n0; nb < n1; nb += kWave) {
+      const BlockMask bk = bsw[nb >> 6];
+      uint64_t bits = bk.nz;
+      while (bits) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(bits);
+        bits &= bits - 1;
+        const uint32_t n = nb + j;
+        const uint64_t mj = ((bk.full >> j) & 1ull) ? live_mask : bmw[n];
+        if ((mj >> lane) & 1ull) visit(n);
       }
     }
+  } else {
+    // The wave's feasibility masks of 8 nodes come in with one scalar load; a node no pod of
+    // the wave can use costs a scalar compare, a group of 8 such nodes one more.
+    for (uint32_t g = n0; g < n1; g += 8) {
+      const Group<uint64_t, 8> mk = load_group<uint64_t, 8>(
+          reinterpret_cast<const unsigned char*>(bmw + g));
+      if ((mk.v[0] | mk.v[1] | mk.v[2] | mk.v[3] | mk.v[4] | mk.v[5] | mk.v[6] | mk.v[7]) == 0)
+        continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t n = g + (uint32_t)j;
+        if (mk.v[j] == 0 || n >= n1) continue;
+        if ((mk.v[j] >> lane) & 1ull) visit(n);
+      }
     }
   }
   if (!live) return;
@@ -894,7 +947,8 @@ template <int K>
 __global__ __launch_bounds__(kBlock) void k2_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum2,
     uint32_t n_nodes, uint32_t chunk_nodes, ScoreArgs args, uint32_t n_pods,
-    const uint64_t* __restrict__ bm, uint32_t bm_stride, const uint64_t* __restrict__ blk,
+    const uint64_t* __restrict__ bm, uint32_t bm_stride, const BlockMask* __restrict__ bs,
+    uint32_t bs_stride, const uint64_t* __restrict__ blk,
     uint32_t blk_stride, double* __restrict__ pbest,
     uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties, double* __restrict__ plow) {
   constexpr uint32_t S2 = k2sum_stride(K), NS = n32_stride(K);
@@ -912,6 +966,7 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
   const uint64_t live_mask = ballot(live);
   if (live_mask == 0) return;  // a wave past the batch
   const uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
+  const BlockMask* bsw = bs ? bs + (size_t)uniform_u32(p >> 6) * bs_stride : nullptr;
   Scorer<Path::N32> sc;
   if (live) sc.load(args, p, n_pods);
   // live lanes are a prefix of the wave: lane 0 is live
@@ -955,7 +1010,18 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
   auto block = [&](uint32_t nb) {
     const uint32_t n = nb + lane;
     const bool valid = n < n1;
-    const uint64_t mask = valid ? bmw[n] : 0ull;
+    // the wave's mask of node n: from the block's (nz, full) words, and a load of its own
+    // only for a partial node (sparse form); or the dense [wave][node] array
+    uint64_t mask, feas_b;
+    if (bsw) {
+      const BlockMask bk = bsw[nb >> 6];
+      mask = ((bk.full >> lane) & 1ull) ? live_mask : 0ull;
+      if (((bk.nz & ~bk.full) >> lane) & 1ull) mask = bmw[n];
+      feas_b = bk.nz;
+    } else {
+      mask = valid ? bmw[n] : 0ull;
+      feas_b = ballot(mask != 0ull);
+    }
     // this block's tile of summaries (nb is a multiple of 64): word w at s[64 w]
     const uint32_t* s = reinterpret_cast<const uint32_t*>(sum2) + sum_index(nb, 0, S2) + lane;
     const uint4 h0 = make_uint4(s[64 * kS2Static], s[64 * (kS2Static + 1)], s[64 * kS2Clock],
@@ -967,7 +1033,6 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
       fs.v[t] = s[64 * (kS2Fs + t)];
       ts.v[t] = s[64 * (kS2Fs + K + t)];
     }
-    const uint64_t feas_b = ballot(mask != 0ull);
     if (feas_b == 0) return;  // no pod of the wave can use any node of the block
     uint64_t fast_b = ballot(mask != 0ull && (h0.w & kSumUni4) != 0u), u_b = 0;
     if (!uni_max) {
@@ -1285,7 +1350,7 @@ __global__ __launch_bounds__(kBlock) void k_set_static(unsigned char* __restrict
 template <int K, Path PATH>
 __global__ __launch_bounds__(kBlock) void k_greedy_one(
     const unsigned char* __restrict__ nodes, uint32_t n_nodes, ScoreArgs args, uint32_t n_pods,
-    uint32_t s, const uint64_t* __restrict__ bm, uint32_t bm_stride, double* __restrict__ part_s,
+    uint32_t s, const MaskSrc ms, double* __restrict__ part_s,
     uint32_t* __restrict__ part_i, uint32_t* __restrict__ done, uint32_t* __restrict__ out) {
   constexpr uint32_t stride = PATH == Path::N32 ? n32_stride(K) : node_stride(K);
   __shared__ double red_s[kBlock / kWave];
@@ -1293,12 +1358,11 @@ __global__ __launch_bounds__(kBlock) void k_greedy_one(
   __shared__ bool last;
   Scorer<PATH> sc;
   sc.load(args, s, n_pods);  // the same pod on every lane
-  const uint64_t* row = bm + (size_t)(s >> 6) * bm_stride;
   const uint32_t bit = s & 63u;
   double best = -1.0;
   uint32_t idx = 0xffffffffu;
   for (uint32_t n = blockIdx.x * kBlock + threadIdx.x; n < n_nodes; n += gridDim.x * kBlock) {
-    if ((row[n] >> bit) & 1ull) {
+    if ((mask_at(ms, s >> 6, n, n_pods) >> bit) & 1ull) {
       const double raw = sc.template raw<K>(nodes + (size_t)n * stride);
       if (raw > best) {  // n grows along the thread's sweep: the first maximum is the lowest
         best = raw;
@@ -1752,8 +1816,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce3(const int64_t* __restrict__ 
 
 // Bitmask [wave][node] u64 (device, yoda_layout.h) -> [P][W] u32 words (host API layout:
 // word w of pod q, bit b = node 32 w + b).
-__global__ __launch_bounds__(kBlock) void k_bitmask_transpose(const uint64_t* __restrict__ bm,
-                                                              uint32_t bm_stride,
+__global__ __launch_bounds__(kBlock) void k_bitmask_transpose(const MaskSrc ms,
                                                               uint32_t n_nodes, uint32_t W,
                                                               uint32_t n_pods,
                                                               const uint32_t* __restrict__ perm,
@@ -1765,7 +1828,7 @@ __global__ __launch_bounds__(kBlock) void k_bitmask_transpose(const uint64_t* __
   const uint32_t q = perm ? perm[p] : p;
   uint32_t bits = 0;
   for (uint32_t b = 0; b < 32u && 32u * w + b < n_nodes; ++b)
-    bits |= (uint32_t)bm_bit(bm, bm_stride, p, 32u * w + b) << b;
+    bits |= (uint32_t)((mask_at(ms, p >> 6, 32u * w + b, n_pods) >> (p & 63u)) & 1ull) << b;
   out[(size_t)q * W + w] = bits;
 }
 
@@ -1787,7 +1850,8 @@ static inline dim3 pod_grid(uint32_t n) { return dim3((n + kBlock - 1) / kBlock)
 hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigned char* sum,
                      uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                      uint32_t n_pods, const Partials& part, uint64_t* bm, uint32_t bm_stride,
-                     uint64_t* blk, uint32_t blk_stride, hipStream_t s) {
+                     BlockMask* bs, uint32_t bs_stride, uint64_t* blk, uint32_t blk_stride,
+                     hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   switch (path) {
     case Path::N32:
@@ -1795,8 +1859,8 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
         YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK>), grid, dim3(kBlock), 0, s, nodes,
                                             sum, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
                                             pp.number, pp.need_mem, pp.need_clk, n_pods,
-                                            part.max_u, part.cnt, bm, bm_stride, blk,
-                                            blk_stride));
+                                            part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,
+                                            blk, blk_stride));
       } else {
         YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_filter_maxima<KK, Path::N32>), grid, dim3(kBlock),
                                             0, s, nodes, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
@@ -1888,27 +1952,29 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
                               uint32_t n_nodes,
                               uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                               const uint64_t* maxima, const double* rcp, const float* rcp32,
-                              uint32_t n_pods, const uint64_t* bm, uint32_t bm_stride, const Partials& part,
+                              uint32_t n_pods, const uint64_t* bm, uint32_t bm_stride,
+                              const BlockMask* bs, uint32_t bs_stride, const Partials& part,
                               int64_t* rows, double* tk_s, uint32_t* tk_i, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
+  const MaskSrc ms{bm, bs, bm_stride, bs_stride};
   switch (path) {
     case Path::N32:
       if (OUT == OUT_ARGMAX && sum2) {
         YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK>), grid, dim3(kBlock), 0, s, nodes,
                                             sum2, n_nodes, chunk_nodes, a, n_pods, bm, bm_stride,
-                                            blk, blk_stride, part.best_f, part.idx, part.ties,
+                                            bs, bs_stride, blk, blk_stride, part.best_f, part.idx, part.ties,
                                             part.low_f));
         break;
       }
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score<KK, Path::N32, OUT>), grid, dim3(kBlock), 0,
-                                          s, nodes, n_nodes, chunk_nodes, a, n_pods, bm, bm_stride,
+                                          s, nodes, n_nodes, chunk_nodes, a, n_pods, ms,
                                           part.best_f, part.idx, part.ties, part.low_f, rows,
                                           tk_s, tk_i));
       break;
     case Path::F64:
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score<KK, Path::F64, OUT>), grid, dim3(kBlock), 0,
-                                          s, nodes, n_nodes, chunk_nodes, a, n_pods, bm, bm_stride,
+                                          s, nodes, n_nodes, chunk_nodes, a, n_pods, ms,
                                           part.best_f, part.idx, part.ties, part.low_f, rows,
                                           tk_s, tk_i));
       break;
@@ -1926,11 +1992,12 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
 hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                           uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                           const double* rcp, const float* rcp32, uint32_t n_pods,
-                          const uint64_t* bm, uint32_t bm_stride, const Partials& part, double* tk_s,
+                          const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
+                          uint32_t bs_stride, const Partials& part, double* tk_s,
                           uint32_t* tk_i, hipStream_t s) {
   return launch_k2_t<OUT_TOPK>(K, path, nodes, nullptr, nullptr, 0, n_nodes, chunk_nodes, C, pp, nullptr, rcp,
                                rcp32,
-                               n_pods, bm, bm_stride, part, nullptr, tk_s, tk_i, s);
+                               n_pods, bm, bm_stride, bs, bs_stride, part, nullptr, tk_s, tk_i, s);
 }
 
 hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t C,
@@ -1965,20 +2032,21 @@ uint32_t greedy_one_blocks() { return kGreedyOneBlocks; }
 hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                              const PodParams& pp, const double* rcp, const float* rcp32,
                              uint32_t n_pods, uint32_t s, const uint64_t* bm, uint32_t bm_stride,
-                             double* part_s, uint32_t* part_i, uint32_t* done, uint32_t* out,
+                             const BlockMask* bs, uint32_t bs_stride, double* part_s, uint32_t* part_i, uint32_t* done, uint32_t* out,
                              hipStream_t st) {
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
+  const MaskSrc ms{bm, bs, bm_stride, bs_stride};
   const dim3 grid(std::max<uint32_t>(1, std::min<uint32_t>(kGreedyOneBlocks,
                                                            (n_nodes + kBlock - 1) / kBlock)));
   switch (path) {
     case Path::N32:
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k_greedy_one<KK, Path::N32>), grid, dim3(kBlock), 0,
-                                          st, nodes, n_nodes, a, n_pods, s, bm, bm_stride, part_s,
+                                          st, nodes, n_nodes, a, n_pods, s, ms, part_s,
                                           part_i, done, out));
       break;
     case Path::F64:
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k_greedy_one<KK, Path::F64>), grid, dim3(kBlock), 0,
-                                          st, nodes, n_nodes, a, n_pods, s, bm, bm_stride, part_s,
+                                          st, nodes, n_nodes, a, n_pods, s, ms, part_s,
                                           part_i, done, out));
       break;
     default:
@@ -1991,13 +2059,15 @@ hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigne
                      const uint64_t* blk, uint32_t blk_stride, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
                      const double* rcp, const float* rcp32, uint32_t n_pods,
-                     const uint64_t* bm, uint32_t bm_stride, const Partials& part, int64_t* rows,
-                     hipStream_t s) {
+                     const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
+                     uint32_t bs_stride, const Partials& part, int64_t* rows, hipStream_t s) {
   if (rows)
     return launch_k2_t<OUT_ROWS>(K, path, nodes, nullptr, nullptr, 0, n_nodes, chunk_nodes, C, pp, maxima, rcp,
-                                 rcp32, n_pods, bm, bm_stride, part, rows, nullptr, nullptr, s);
+                                 rcp32, n_pods, bm, bm_stride, bs, bs_stride, part, rows, nullptr,
+                                 nullptr, s);
   return launch_k2_t<OUT_ARGMAX>(K, path, nodes, sum2, blk, blk_stride, n_nodes, chunk_nodes, C, pp, maxima, rcp,
-                                 rcp32, n_pods, bm, bm_stride, part, rows, nullptr, nullptr, s);
+                                 rcp32, n_pods, bm, bm_stride, bs, bs_stride, part, rows, nullptr,
+                                 nullptr, s);
 }
 
 hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
@@ -2096,12 +2166,14 @@ hipError_t launch_reduce3(const Partials& part, uint32_t C, const uint32_t* flag
   return hipGetLastError();
 }
 
-hipError_t launch_bitmask_transpose(const uint64_t* bm, uint32_t bm_stride, uint32_t n_nodes,
+hipError_t launch_bitmask_transpose(const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
+                                    uint32_t bs_stride, uint32_t n_nodes,
                                     uint32_t W, uint32_t n_pods, const uint32_t* perm,
                                     uint32_t* out, hipStream_t s) {
   const uint64_t total = (uint64_t)W * n_pods;
   dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
-  hipLaunchKernelGGL(k_bitmask_transpose, grid, dim3(kBlock), 0, s, bm, bm_stride, n_nodes, W,
+  const MaskSrc ms{bm, bs, bm_stride, bs_stride};
+  hipLaunchKernelGGL(k_bitmask_transpose, grid, dim3(kBlock), 0, s, ms, n_nodes, W,
                      n_pods, perm, out);
   return hipGetLastError();
 }

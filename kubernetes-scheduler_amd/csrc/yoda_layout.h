@@ -127,6 +127,17 @@ __host__ __device__ constexpr size_t sum_words(uint32_t n_nodes, uint32_t stride
 // up to 64.  K1 writes it coalesced (lane = node); K2 reads one wave's mask per node through
 // the scalar path and skips the node when it is 0.
 __host__ __device__ constexpr uint32_t bm_row(uint32_t n_nodes) { return (n_nodes + 63u) & ~63u; }
+// Sparse form written by the block-classified K1 (N32 path), so the [wave][node] array is
+// not streamed through HBM in full: per (pod wave, 64-node block) one BlockMask,
+//   nz   bit j: node 64 b + j has a feasible pod of the wave,
+//   full bit j: every live pod of the wave is feasible on it (mask == the wave's live mask),
+// at bs[w * bs_row(N) + b], written for every block of the wave's chunks; bm[w][n] is then
+// written (and read) only for the PARTIAL nodes, nz & ~full.  Mask of (w, n):
+//   full ? live(w) : nz ? bm[w][n] : 0.
+struct alignas(16) BlockMask {
+  uint64_t nz, full;
+};
+__host__ __device__ constexpr uint32_t bs_row(uint32_t n_nodes) { return (n_nodes + 63u) / 64u; }
 // Non-empty node blocks: u64 blk[wave][w], bit b % 64 of word b / 64 set when node block b
 // (nodes 64 b .. 64 b + 63) has a feasible pod of the wave.  Written by the block K1, read by
 // the block K2 to visit only those blocks.
