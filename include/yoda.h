@@ -231,12 +231,14 @@ int yoda_profile_read(yoda_t* h, double* k1_ms, double* k2_ms, uint32_t* n_launc
  * descending, then input index), each pick feeding the next cycle through the node's
  * Allocate score (alloc_memory += scv/memory, algorithm.go:299-303; the scheduler-cache
  * "assume" of SURVEY §3.4).  YODA_GREEDY_CARD_CAPACITY additionally decrements the picked
- * node's CardNumber by the pod's number (saturating at 0): a build-defined extension.
- * The uploaded snapshot is left unchanged. */
+ * node's CardNumber by the pod's number (saturating at 0): a build-defined extension,
+ * batched as well (a window restarts at the first pod the capacity certificate cannot
+ * clear).  The uploaded snapshot is left unchanged. */
 #define YODA_GREEDY_CARD_CAPACITY 1u
 int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, int32_t* pick);
 /* Work counters of the last yoda_greedy: GPU top-k windows, pods evaluated one by one
- * (uncertified candidates, or every pod on the exact sequential path), and host wall time
+ * (uncertified candidates, or every pod on the exact sequential path; with
+ * YODA_GREEDY_CARD_CAPACITY: windows restarted at an uncertified pod), and host wall time
  * (ms) in times_ms[0..2] = {window candidate passes, sequential resolve, exact fallbacks}
  * (times_ms may be NULL). */
 int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks,
@@ -273,6 +275,22 @@ int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_count
  * *score = its raw score (lowest node among equal scores). */
 int yoda_shard_best_one(yoda_t* h, uint32_t pod, double* score, int32_t* node);
 
+/* YODA_GREEDY_CARD_CAPACITY across shards (fast record paths).  Per window, instead of
+ * yoda_shard_phase1: yoda_shard_phase1_witness also writes d_wit [2][6][P] u32 -- per PreScore
+ * maxima field the shard's witness count (nodes whose qualifying cards reach the shard's
+ * maximum) and its lowest witness (GLOBAL id).  Exchange: keep a copy of the local d_maxima,
+ * all-reduce d_maxima MAX and d_counts SUM, yoda_shard_witness_prepare(global, local, d_wit)
+ * (clears the fields where this shard does not reach the global maximum), then SUM-reduce
+ * d_wit[0, 6P) and MIN-reduce (unsigned) d_wit[6P, 12P).  yoda_shard_topk as usual; then
+ * yoda_shard_witness_download gives maxima [6][P] and wit [12][P] in the caller's pod order
+ * for yoda_gs_set_witness.  A pod the session cannot certify starts the next window. */
+int yoda_shard_phase1_witness(yoda_t* h, uint64_t* d_maxima, uint32_t* d_counts,
+                              uint32_t* d_wit);
+int yoda_shard_witness_prepare(yoda_t* h, const uint64_t* d_maxima_global,
+                               const uint64_t* d_maxima_local, uint32_t* d_wit);
+int yoda_shard_witness_download(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_wit,
+                                uint64_t* maxima, uint32_t* wit);
+
 /* Host-side sequential resolve over the GLOBAL node set (no GPU); identical on every rank. */
 typedef struct yoda_greedy_session yoda_gs_t;
 /* nodes: the full snapshot (card_number, free/total memory sums, alloc_memory (may be NULL)
@@ -286,6 +304,18 @@ int yoda_gs_queue_order(const yoda_gs_t* g, uint32_t* order);
 int yoda_gs_begin_window(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
                          const uint32_t* counts, const double* top_score,
                          const uint32_t* top_node);
+/* YODA_GREEDY_CARD_CAPACITY sessions: the window's PreScore maxima [6][wn] with their
+ * witnesses -- per field the number of window-start feasible nodes whose qualifying cards
+ * reach the maximum, and the lowest such node (GLOBAL id, 0xFFFFFFFF if none) -- window
+ * order as yoda_gs_begin_window's arrays; call after it.  Without them a capacity session
+ * certifies a pod only while no node it could use has lost cards in the window. */
+int yoda_gs_set_witness(yoda_gs_t* g, const uint64_t* maxima, const uint32_t* wit_count,
+                        const uint32_t* wit_node);
+/* Resolve the window in queue order; *next = the first window pod it cannot certify (wn when
+ * the window is done).  flags == 0: the caller scores that pod exactly against the current
+ * state (yoda_shard_best_one) and feeds it to yoda_gs_assign.  YODA_GREEDY_CARD_CAPACITY:
+ * the caller starts the next window at that pod instead (the certificate of DESIGN.md §5
+ * also tracks CardNumber decrements: feasibility and, through the witnesses, the maxima). */
 int yoda_gs_resolve(yoda_gs_t* g, uint32_t* next);
 int yoda_gs_assign(yoda_gs_t* g, uint32_t queue_pos, int32_t pick);
 /* Nodes whose state changed since the last call (at most cap), with their current state. */

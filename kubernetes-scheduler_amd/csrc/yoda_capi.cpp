@@ -87,6 +87,15 @@ hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes, uint3
                              const BlockMask* bs, uint32_t bs_stride,
                              double* part_s, uint32_t* part_i, uint32_t* done, uint32_t* out,
                              hipStream_t st);
+hipError_t launch_k1_witness(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
+                             uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
+                             uint32_t n_pods, uint64_t* pmax, uint32_t* pwit, uint32_t* pcnt,
+                             uint64_t* bm, uint32_t bm_stride, hipStream_t s);
+hipError_t launch_reduce_wit(const uint64_t* pmax, const uint32_t* pwit, const uint32_t* pcnt,
+                             uint32_t C, uint32_t n_pods, uint32_t node_offset, uint64_t* maxima,
+                             uint32_t* counts, uint32_t* wcount, uint32_t* wnode, hipStream_t s);
+hipError_t launch_wit_prepare(const uint64_t* gmax, const uint64_t* lmax, uint32_t n_pods,
+                              uint32_t* wit, hipStream_t s);
 size_t order_scratch_bytes(uint32_t n_pods);
 hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
                              uint32_t n_pods, const uint32_t key_bits[3], void* scratch,
@@ -210,7 +219,9 @@ struct yoda_handle {
   // greedy
   DevBuf tk_s_part, tk_i_part, tk_s, tk_i, upd_node, upd_val, upd_cn;
   DevBuf g1_part, g1_done;  // k_greedy_one partials + block counter (zeroed once)
-  PinnedBuf upd_stage, pick_stage;
+  DevBuf p_wit, wit;        // capacity greedy: witness partials [2][6][C][P], merged [2][6][P]
+  PinnedBuf upd_stage, pick_stage, win_stage;
+  uint32_t greedy_restarts = 0;
   hipEvent_t upd_event = nullptr;
   bool upd_pending = false;
   std::vector<uint32_t> h_pos;  // yoda_shard_topk: caller pod index -> sorted position
@@ -252,11 +263,13 @@ struct yoda_handle {
                      &tk_i,      &upd_node,  &upd_val,    &upd_cn,    &g1_part,   &g1_done,
                      &p_best_f,  &p_best_i,  &p_idx,      &p_ties,       &p_low_f,
                      &p_low_i,   &p_err,     &pick_alt,   &status_alt,   &ties_out_alt,
+                     &p_wit,     &wit,
                      &counts_alt, &best_alt, &maxima_alt};
     for (DevBuf* b : all) b->release();
     pod_stage.release();
     upd_stage.release();
     pick_stage.release();
+    win_stage.release();
     if (stage_event) (void)hipEventDestroy(stage_event);
     if (upd_event) (void)hipEventDestroy(upd_event);
     if (own_stream) (void)hipStreamDestroy(own_stream);
@@ -512,6 +525,35 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts) {
   }
   // the block-classified K1 (N32) writes u32 maxima partials
   HIP_TRY(h, launch_reduce1(part, h->C1, P, h->has_k1sum, maxima, counts, h->stream));
+  return YODA_OK;
+}
+
+// Phase 1 of a capacity-decrement greedy window: Filter + PreScore maxima with their
+// witnesses (k1_witness), dense masks.  Outputs maxima [6][P], counts [2][P] and
+// wit [2][6][P] (witness count, lowest witness node + node_offset), in the run's pod order.
+int phase1_witness(yoda_t* h, uint64_t* maxima, uint32_t* counts, uint32_t* wit,
+                   uint32_t node_offset) {
+  const uint32_t P = h->n_pods, N = h->n_nodes;
+  if (P == 0) return YODA_OK;
+  h->bm_sparse = false;
+  h->blk_valid = false;
+  if (N == 0) {
+    HIP_TRY(h, hipMemsetAsync(counts, 0, 2 * (size_t)P * 4, h->stream));
+    HIP_TRY(h, hipMemsetAsync(wit, 0, 6 * (size_t)P * 4, h->stream));
+    HIP_TRY(h, hipMemsetAsync(wit + 6 * (size_t)P, 0xff, 6 * (size_t)P * 4, h->stream));
+    std::vector<uint64_t> ones(6 * (size_t)P, 1);
+    HIP_TRY(h, hipMemcpyAsync(maxima, ones.data(), ones.size() * 8, hipMemcpyHostToDevice,
+                              h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    return YODA_OK;
+  }
+  HIP_TRY(h, h->p_wit.ensure(12 * (size_t)h->C1 * P * 4));
+  Partials part = partials(h);
+  HIP_TRY(h, launch_k1_witness(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk1, h->C1,
+                               pod_params(h), P, part.max_u, h->p_wit.as<uint32_t>(), part.cnt,
+                               h->bitmask.as<uint64_t>(), bm_row(N), h->stream));
+  HIP_TRY(h, launch_reduce_wit(part.max_u, h->p_wit.as<uint32_t>(), part.cnt, h->C1, P,
+                               node_offset, maxima, counts, wit, wit + 6 * (size_t)P, h->stream));
   return YODA_OK;
 }
 
@@ -1430,6 +1472,10 @@ int greedy_eval_fast(GreedyState& g, uint32_t s, int32_t* pick_out) {
 
 }  // namespace
 
+}  // extern "C"
+static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick);
+extern "C" {
+
 int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, int32_t* pick) {
   if (!h) return YODA_ERR_INVALID_ARG;
   if (!pods || !pick) return fail(h, YODA_ERR_INVALID_ARG, "NULL pods or pick");
@@ -1439,6 +1485,7 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
     const uint32_t P = pods->n_pods, N = h->n_nodes;
     h->greedy_windows = 0;
     h->greedy_fallbacks = 0;
+    h->greedy_restarts = 0;
     h->greedy_window_ms = h->greedy_fallback_ms = h->greedy_resolve_ms = 0;
     using Clock = std::chrono::steady_clock;
     auto ms_since = [](Clock::time_point t0) {
@@ -1465,6 +1512,7 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
       for (uint32_t i = 0; i < P; ++i) pick[order[i]] = pk[i];
       return YODA_OK;
     }
+    if ((flags & YODA_GREEDY_CARD_CAPACITY) && !h->generic) return greedy_capacity(h, pods, pick);
     GreedyState g;
     g.h = h;
     g.alloc = h->h_alloc;
@@ -1820,6 +1868,61 @@ int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_count
   }
 }
 
+int yoda_shard_phase1_witness(yoda_t* h, uint64_t* d_maxima, uint32_t* d_counts,
+                              uint32_t* d_wit) {
+  int rc = prepare_run(h, YODA_MODE_SCV);
+  if (rc) return rc;
+  if (h->generic)
+    return fail(h, YODA_ERR_STATE, "witness phase 1 needs a fast record path (N32 or F64)");
+  if (!d_maxima || !d_counts || !d_wit) return fail(h, YODA_ERR_INVALID_ARG, "NULL buffer");
+  try {
+    if ((rc = order_pods(h, YODA_MODE_SCV))) return rc;
+    if ((rc = phase1_witness(h, d_maxima, d_counts, d_wit, h->node_offset))) return rc;
+    h->phase1_done = true;
+    h->ran = false;
+    return YODA_OK;
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
+int yoda_shard_witness_prepare(yoda_t* h, const uint64_t* d_maxima_global,
+                               const uint64_t* d_maxima_local, uint32_t* d_wit) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  if (!d_maxima_global || !d_maxima_local || !d_wit)
+    return fail(h, YODA_ERR_INVALID_ARG, "NULL buffer");
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, launch_wit_prepare(d_maxima_global, d_maxima_local, h->n_pods, d_wit, h->stream));
+  return YODA_OK;
+}
+
+int yoda_shard_witness_download(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_wit,
+                                uint64_t* maxima, uint32_t* wit) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  if (!d_maxima || !d_wit || !maxima || !wit) return fail(h, YODA_ERR_INVALID_ARG, "NULL buffer");
+  if (!h->topk_ready)
+    return fail(h, YODA_ERR_STATE, "yoda_shard_witness_download before yoda_shard_topk");
+  try {
+    const uint32_t P = h->n_pods;
+    if (P == 0) return YODA_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    std::vector<uint64_t> mx(6 * (size_t)P);
+    std::vector<uint32_t> wt(12 * (size_t)P);
+    HIP_TRY(h, hipMemcpyAsync(mx.data(), d_maxima, mx.size() * 8, hipMemcpyDeviceToHost,
+                              h->stream));
+    HIP_TRY(h, hipMemcpyAsync(wt.data(), d_wit, wt.size() * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    for (uint32_t i = 0; i < P; ++i) {
+      const uint32_t q = h->h_pos[i];
+      for (int f = 0; f < 6; ++f) maxima[(size_t)f * P + i] = mx[(size_t)f * P + q];
+      for (int f = 0; f < 12; ++f) wit[(size_t)f * P + i] = wt[(size_t)f * P + q];
+    }
+    return YODA_OK;
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
 int yoda_shard_best_one(yoda_t* h, uint32_t pod, double* score, int32_t* node) {
   if (!h) return YODA_ERR_INVALID_ARG;
   if (!score || !node) return fail(h, YODA_ERR_INVALID_ARG, "NULL output");
@@ -1864,8 +1967,10 @@ int yoda_shard_best_one(yoda_t* h, uint32_t pod, double* score, int32_t* node) {
 // The sequential part of the greedy batch (yoda_greedy's resolve), over the GLOBAL node set,
 // fed with merged candidate lists.  Pure host code: identical on every rank.
 struct yoda_greedy_session {
+  static constexpr uint32_t kCrossQ = 64;  // capacity mode: per-q removal counts up to here
   uint32_t N = 0, P = 0, flags = 0;
   std::vector<uint64_t> free_sum, total_sum, alloc, card_number, alloc0, cn0, stat, stat_w;
+  std::vector<uint64_t> cn_w;  // CardNumber of a window-touched node at the window start
   std::vector<uint8_t> has_memory, has_number, touched_w, dirty, ever;
   std::vector<uint64_t> memory, number;
   std::vector<uint32_t> order, touched_list, dirty_list, ever_list;
@@ -1875,6 +1980,14 @@ struct yoda_greedy_session {
   bool in_window = false, wrapped = false;
   std::vector<uint32_t> counts, ti;
   std::vector<double> ts;
+  // YODA_GREEDY_CARD_CAPACITY (greedy): cross[q] = window-touched nodes whose
+  // CardNumber has dropped from >= q (window start) to < q, i.e. nodes a pod needing q cards
+  // has lost since its candidate list was made; and the window's PreScore maxima with their
+  // witnesses ([6][wn] each, window order), when the caller supplied them.
+  uint32_t cross[kCrossQ + 1] = {};
+  bool has_wit = false;
+  std::vector<uint64_t> wmax;
+  std::vector<uint32_t> wcnt, wnode;
 
   void apply(uint32_t p, int32_t node) {
     if (node < 0) return;
@@ -1882,6 +1995,7 @@ struct yoda_greedy_session {
     if (!touched_w[n]) {
       touched_w[n] = 1;
       stat_w[n] = stat[n];
+      cn_w[n] = card_number[n];
       touched_list.push_back(n);
     }
     if (!dirty[n]) {
@@ -1897,12 +2011,107 @@ struct yoda_greedy_session {
     if (alloc[n] < before) wrapped = true;     // Allocate may grow: stop certifying
     if (flags & YODA_GREEDY_CARD_CAPACITY) {
       const uint64_t num = has_number[p] ? number[p] : 1;
-      card_number[n] = card_number[n] >= num ? card_number[n] - num : 0;
+      const uint64_t a = card_number[n], b = a >= num ? a - num : 0;
+      card_number[n] = b;
+      // pods needing q in (b, a] cards have just lost this node
+      for (uint64_t q = b + 1; q <= std::min<uint64_t>(a, kCrossQ); ++q) ++cross[q];
     }
     bool z;
     stat[n] = static_score(free_sum[n], total_sum[n], alloc[n], &z);
   }
+  // PodFitsNumber operand of pod p (filter.go:11-16): the label, or 1 (CardNumber > 0)
+  uint64_t need_cards(uint32_t p) const { return has_number[p] ? number[p] : 1; }
+  // node n was feasible for a pod needing q cards at the window start and is not any more
+  bool removed(uint32_t n, uint64_t q) const {
+    return touched_w[n] && card_number[n] < q && cn_w[n] >= q;
+  }
+  // how many nodes a pod needing q cards has lost in this window (an upper bound on its
+  // feasible nodes lost: a touched node may never have passed its other predicates)
+  uint64_t lost(uint64_t q) const {
+    if (q <= kCrossQ) return cross[q];
+    uint64_t r = 0;
+    for (uint32_t n : touched_list) r += removed(n, q) ? 1 : 0;
+    return r;
+  }
+  // CollectMaxValues over the remaining feasible nodes still gives window pod i's maxima:
+  // every field keeps a witness (more witnesses than lost nodes, or its only witness kept);
+  // a maximum of 1 is the floor and cannot drop (collection.go:31-38)
+  bool maxima_kept(uint32_t i, uint64_t q, uint64_t lost_q) const {
+    if (lost_q == 0) return true;
+    if (!has_wit) return false;
+    for (int f = 0; f < 6; ++f) {
+      const size_t o = (size_t)f * wn + i;
+      if (wmax[o] <= 1 || wcnt[o] > lost_q) continue;
+      if (wcnt[o] == 1 && wnode[o] < N && !removed(wnode[o], q)) continue;
+      return false;
+    }
+    return true;
+  }
+  // Capacity-mode resolve of window pod i (input pod p): true with *pk when certified.
+  bool resolve_capacity(uint32_t i, uint32_t p, int32_t* pk) const;
 };
+
+bool yoda_greedy_session::resolve_capacity(uint32_t i, uint32_t p, int32_t* pk) const {
+  const uint32_t KT = k;
+  const uint32_t nf0 = counts[i], nz0 = counts[(size_t)wn + i];
+  if (nf0 == 0) {  // feasibility only shrinks: still no node
+    *pk = YODA_PICK_NONE;
+    return true;
+  }
+  if (wrapped) return false;
+  const uint64_t q = need_cards(p);
+  const uint32_t len = std::min<uint32_t>(nf0, KT);
+  const bool whole = nf0 <= KT;  // the list holds every feasible node of the window start
+  const uint64_t lq = lost(q);
+  uint32_t alive = 0, first = 0xffffffffu, alive_zero = 0;
+  double bs = -1.0;
+  uint32_t bi = 0xffffffffu;
+  for (uint32_t kk = 0; kk < len; ++kk) {
+    const uint32_t n = ti[(size_t)kk * wn + i];
+    if (n >= N || removed(n, q)) continue;
+    ++alive;
+    if (first == 0xffffffffu) first = n;
+    alive_zero += total_sum[n] == 0 ? 1u : 0u;
+    double cur = ts[(size_t)kk * wn + i];
+    if (touched_w[n]) cur = cur - (double)stat_w[n] + (double)stat[n];
+    if (cur > bs || (cur == bs && n < bi)) {
+      bs = cur;
+      bi = n;
+    }
+  }
+  if (whole) {
+    if (alive == 0) {
+      *pk = YODA_PICK_NONE;
+      return true;
+    }
+    if (alive == 1) {  // k8s returns the only feasible node without scoring
+      *pk = (int32_t)first;
+      return true;
+    }
+    if (alive_zero > 0) {  // Score would divide by TotalMemorySum == 0
+      *pk = YODA_PICK_ERROR;
+      return true;
+    }
+  } else {
+    if (nf0 < 2 + lq) return false;  // might be down to 0 or 1 feasible nodes
+    if (nz0 > 0) {
+      if (lq > 0) return false;       // a zero-total node may be among the lost ones
+      *pk = YODA_PICK_ERROR;
+      return true;
+    }
+  }
+  if (!maxima_kept(i, q, lq)) return false;  // scores of unlisted nodes may have moved
+  if (bi == 0xffffffffu) return false;       // every listed node lost
+  if (!whole) {
+    // every unlisted node scored <= T at the window start (ties: higher index) and has
+    // only lost Allocate since, or feasibility
+    const double T = ts[(size_t)(len - 1) * wn + i];
+    const uint32_t tidx = ti[(size_t)(len - 1) * wn + i];
+    if (!(bs > T || (bs == T && bi <= tidx))) return false;
+  }
+  *pk = (int32_t)bi;
+  return true;
+}
 
 extern "C" {
 
@@ -1930,6 +2139,7 @@ int yoda_gs_create(const yoda_node_soa* nodes, const yoda_pod_soa* pods, uint32_
     g->cn0 = g->card_number;
     g->stat.resize(N);
     g->stat_w.resize(N);
+    g->cn_w.resize(N);
     for (uint32_t n = 0; n < N; ++n) {
       bool z;
       g->stat[n] = static_score(g->free_sum[n], g->total_sum[n], g->alloc[n], &z);
@@ -1981,9 +2191,27 @@ int yoda_gs_begin_window(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
     g->ws = ws, g->wn = wn, g->k = k, g->next = 0;
     g->in_window = true;
     g->wrapped = false;
+    std::fill(std::begin(g->cross), std::end(g->cross), 0u);
+    g->has_wit = false;
     g->counts.assign(counts, counts + 2 * (size_t)wn);
     g->ts.assign(top_score, top_score + (size_t)k * wn);
     g->ti.assign(top_node, top_node + (size_t)k * wn);
+    return YODA_OK;
+  } catch (...) {
+    return YODA_ERR_INVALID_ARG;
+  }
+}
+
+int yoda_gs_set_witness(yoda_gs_t* g, const uint64_t* maxima, const uint32_t* wit_count,
+                        const uint32_t* wit_node) {
+  if (!g || !g->in_window || (g->wn && (!maxima || !wit_count || !wit_node)))
+    return YODA_ERR_INVALID_ARG;
+  try {
+    const size_t n = 6 * (size_t)g->wn;
+    g->wmax.assign(maxima, maxima + n);
+    g->wcnt.assign(wit_count, wit_count + n);
+    g->wnode.assign(wit_node, wit_node + n);
+    g->has_wit = true;
     return YODA_OK;
   } catch (...) {
     return YODA_ERR_INVALID_ARG;
@@ -1995,12 +2223,15 @@ int yoda_gs_begin_window(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
 int yoda_gs_resolve(yoda_gs_t* g, uint32_t* next) {
   if (!g || !next || !g->in_window) return YODA_ERR_INVALID_ARG;
   const uint32_t wn = g->wn, KT = g->k;
+  const bool capacity = (g->flags & YODA_GREEDY_CARD_CAPACITY) != 0;
   while (g->next < wn) {
     const uint32_t i = g->next;
     const uint32_t p = g->order[g->ws + i];
     const uint32_t nf = g->counts[i], nz = g->counts[(size_t)wn + i];
     int32_t pk;
-    if (nf == 0) {
+    if (capacity) {
+      if (!g->resolve_capacity(i, p, &pk)) break;
+    } else if (nf == 0) {
       pk = YODA_PICK_NONE;
     } else if (nf >= 2 && nz > 0) {
       pk = YODA_PICK_ERROR;  // Score would divide by TotalMemorySum == 0
@@ -2085,3 +2316,167 @@ int yoda_gs_picks(const yoda_gs_t* g, int32_t* pick, uint32_t* resolved, uint32_
 }
 
 }  // extern "C"
+
+// ---- capacity-decrement greedy on one handle -------------------------------------------
+// YODA_GREEDY_CARD_CAPACITY on a fast record path (greedy): windows of pods
+// are evaluated on the device against the state at the window start (k1_witness + top-k
+// K2), then the host session resolves them in queue order with the capacity certificate
+// (yoda_greedy_session::resolve_capacity).  A pod it cannot certify starts the next window,
+// so it is evaluated against the current state; the window size adapts to how far the last
+// window got.  Node ids inside are local; picks are returned global.
+static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
+  using Clock = std::chrono::steady_clock;
+  auto ms_since = [](Clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+  };
+  const uint32_t P = pods->n_pods, N = h->n_nodes, KT = (uint32_t)topk_k();
+  yoda_node_soa nv{};
+  nv.n_nodes = N;
+  nv.max_cards = 1;
+  nv.card_number = h->h_card_number.data();
+  nv.free_memory_sum = h->h_free_sum.data();
+  nv.total_memory_sum = h->h_total_sum.data();
+  nv.alloc_memory = h->h_alloc.data();
+  yoda_gs_t* g = nullptr;
+  int rc = yoda_gs_create(&nv, pods, YODA_GREEDY_CARD_CAPACITY, &g);
+  if (rc) return fail(h, rc, "greedy: session setup failed");
+  struct Guard {
+    yoda_gs_t* g;
+    ~Guard() { yoda_gs_destroy(g); }
+  } guard{g};
+  const uint32_t Wmax = greedy_window();
+  uint32_t W = Wmax;
+  std::vector<uint32_t> ids, cnt_w, ti_w, wc_w, pos;
+  std::vector<uint64_t> al, cn, mx_w;
+  std::vector<double> ts_w;
+  auto push = [&]() -> int {  // nodes the session changed -> the device
+    const uint32_t d = (uint32_t)g->dirty_list.size();
+    if (d == 0) return YODA_OK;
+    ids.resize(d), al.resize(d), cn.resize(d);
+    uint32_t got = 0;
+    int r = yoda_gs_take_dirty(g, d, ids.data(), al.data(), cn.data(), &got);
+    if (r) return fail(h, r, "greedy: take_dirty");
+    for (uint32_t t = 0; t < got; ++t) ids[t] += h->node_offset;
+    return yoda_set_node_state(h, got, ids.data(), al.data(), cn.data());
+  };
+  PodGather win;
+  uint32_t ws = 0;
+  while (ws < P) {
+    const auto tw = Clock::now();
+    if ((rc = push())) return rc;
+    const uint32_t wn = std::min(W, P - ws);
+    win.build(pods, g->order.data() + ws, wn);
+    if ((rc = yoda_upload_pods(h, &win.soa))) return rc;
+    if ((rc = prepare_run(h, YODA_MODE_SCV))) return rc;
+    if ((rc = order_pods(h, YODA_MODE_SCV))) return rc;
+    HIP_TRY(h, h->wit.ensure(12 * (size_t)wn * 4));
+    HIP_TRY(h, h->tk_s_part.ensure((size_t)h->C2 * KT * wn * 8));
+    HIP_TRY(h, h->tk_i_part.ensure((size_t)h->C2 * KT * wn * 4));
+    HIP_TRY(h, h->tk_s.ensure((size_t)KT * wn * 8));
+    HIP_TRY(h, h->tk_i.ensure((size_t)KT * wn * 4));
+    if ((rc = phase1_witness(h, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(),
+                             h->wit.as<uint32_t>(), 0)))
+      return rc;
+    // pinned staging of the window's outputs (sorted order): counts | maxima | wit |
+    // top scores | top nodes | perm
+    const size_t o_cnt = 0, o_mx = o_cnt + 8 * (size_t)wn, o_wit = o_mx + 48 * (size_t)wn,
+                 o_ts = o_wit + 48 * (size_t)wn, o_ti = o_ts + 8 * (size_t)KT * wn,
+                 o_perm = o_ti + 4 * (size_t)KT * wn, total = o_perm + 4 * (size_t)wn;
+    HIP_TRY(h, h->win_stage.ensure(total));
+    unsigned char* st = static_cast<unsigned char*>(h->win_stage.p);
+    if (N > 0) {
+      HIP_TRY(h, launch_prep2(h->maxima.as<uint64_t>(), wn, h->rcp.as<double>(),
+                              h->rcp32.as<float>(), h->stream));
+      HIP_TRY(h, launch_k2_topk(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk2, h->C2,
+                                pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(), wn,
+                                h->bitmask.as<uint64_t>(), bm_row(N), nullptr, 0, partials(h),
+                                h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),
+                                h->stream));
+      HIP_TRY(h, launch_topk_merge(h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(), h->C2,
+                                   wn, 0, h->tk_s.as<double>(), h->tk_i.as<uint32_t>(), h->stream));
+      HIP_TRY(h, hipMemcpyAsync(st + o_ts, h->tk_s.p, 8 * (size_t)KT * wn, hipMemcpyDeviceToHost,
+                                h->stream));
+      HIP_TRY(h, hipMemcpyAsync(st + o_ti, h->tk_i.p, 4 * (size_t)KT * wn, hipMemcpyDeviceToHost,
+                                h->stream));
+    } else {
+      for (size_t t = 0; t < (size_t)KT * wn; ++t) {
+        reinterpret_cast<double*>(st + o_ts)[t] = -1.0;
+        reinterpret_cast<uint32_t*>(st + o_ti)[t] = 0xffffffffu;
+      }
+    }
+    HIP_TRY(h, hipMemcpyAsync(st + o_cnt, h->counts.p, 8 * (size_t)wn, hipMemcpyDeviceToHost,
+                              h->stream));
+    HIP_TRY(h, hipMemcpyAsync(st + o_mx, h->maxima.p, 48 * (size_t)wn, hipMemcpyDeviceToHost,
+                              h->stream));
+    HIP_TRY(h, hipMemcpyAsync(st + o_wit, h->wit.p, 48 * (size_t)wn, hipMemcpyDeviceToHost,
+                              h->stream));
+    if (h->ordered)
+      HIP_TRY(h, hipMemcpyAsync(st + o_perm, h->perm.p, 4 * (size_t)wn, hipMemcpyDeviceToHost,
+                                h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    // sorted position -> window order
+    pos.resize(wn);
+    for (uint32_t i = 0; i < wn; ++i) pos[i] = i;
+    if (h->ordered) {
+      const uint32_t* perm = reinterpret_cast<const uint32_t*>(st + o_perm);
+      for (uint32_t q = 0; q < wn; ++q) pos[perm[q]] = q;
+    }
+    cnt_w.resize(2 * (size_t)wn), mx_w.resize(6 * (size_t)wn), wc_w.resize(12 * (size_t)wn);
+    ts_w.resize((size_t)KT * wn), ti_w.resize((size_t)KT * wn);
+    const uint32_t* cnt_s = reinterpret_cast<const uint32_t*>(st + o_cnt);
+    const uint64_t* mx_s = reinterpret_cast<const uint64_t*>(st + o_mx);
+    const uint32_t* wit_s = reinterpret_cast<const uint32_t*>(st + o_wit);
+    const double* ts_s = reinterpret_cast<const double*>(st + o_ts);
+    const uint32_t* ti_s = reinterpret_cast<const uint32_t*>(st + o_ti);
+    for (uint32_t i = 0; i < wn; ++i) {
+      const uint32_t q = pos[i];
+      cnt_w[i] = cnt_s[q];
+      cnt_w[(size_t)wn + i] = cnt_s[(size_t)wn + q];
+      for (int f = 0; f < 6; ++f) {
+        mx_w[(size_t)f * wn + i] = mx_s[(size_t)f * wn + q];
+        wc_w[(size_t)f * wn + i] = wit_s[(size_t)f * wn + q];
+        wc_w[(size_t)(6 + f) * wn + i] = wit_s[(size_t)(6 + f) * wn + q];
+      }
+      for (uint32_t kk = 0; kk < KT; ++kk) {
+        ts_w[(size_t)kk * wn + i] = ts_s[(size_t)kk * wn + q];
+        ti_w[(size_t)kk * wn + i] = ti_s[(size_t)kk * wn + q];
+      }
+    }
+    ++h->greedy_windows;
+    h->greedy_window_ms += ms_since(tw);
+    const auto tr = Clock::now();
+    if ((rc = yoda_gs_begin_window(g, ws, wn, KT, cnt_w.data(), ts_w.data(), ti_w.data())) ||
+        (rc = yoda_gs_set_witness(g, mx_w.data(), wc_w.data(), wc_w.data() + 6 * (size_t)wn)))
+      return fail(h, rc, "greedy: session window");
+    uint32_t next = 0;
+    if ((rc = yoda_gs_resolve(g, &next))) return fail(h, rc, "greedy: resolve");
+    h->greedy_resolve_ms += ms_since(tr);
+    if (next < wn) {
+      // pod ws + next could not be certified: it opens the next window (evaluated against the
+      // current state, so it is always resolved there); size it after this one's progress
+      ++h->greedy_restarts;
+      ++h->greedy_fallbacks;
+      uint32_t w2 = 64;
+      while (w2 < 2 * next && w2 < Wmax) w2 <<= 1;
+      W = std::min(w2, Wmax);
+      ws += next;
+    } else {
+      ws += wn;
+      W = std::min(2 * W, Wmax);
+    }
+  }
+  if ((rc = yoda_gs_picks(g, pick, nullptr, nullptr))) return fail(h, rc, "greedy: picks");
+  for (uint32_t p = 0; p < P; ++p)
+    if (pick[p] >= 0) pick[p] += (int32_t)h->node_offset;
+  // leave the uploaded snapshot as it was
+  const uint32_t ne = (uint32_t)g->ever_list.size();
+  ids.resize(ne), al.resize(ne), cn.resize(ne);
+  uint32_t got = 0;
+  if ((rc = yoda_gs_touched_original(g, ne, ids.data(), al.data(), cn.data(), &got)))
+    return fail(h, rc, "greedy: restore");
+  for (uint32_t t = 0; t < got; ++t) ids[t] += h->node_offset;
+  if ((rc = yoda_set_node_state(h, got, ids.data(), al.data(), cn.data()))) return rc;
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  h->ran = false;
+  return YODA_OK;
+}

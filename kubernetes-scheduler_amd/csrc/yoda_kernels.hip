@@ -325,6 +325,165 @@ __global__ __launch_bounds__(kBlock) void k1_filter_maxima(
   pcnt[((size_t)1 * C + chunk) * n_pods + p] = nz;
 }
 
+// K1 for the capacity-decrement greedy windows (YODA_GREEDY_CARD_CAPACITY, fast record
+// paths): the per-node sweep of k1_filter_maxima, plus, per PreScore maxima field, the number
+// of feasible nodes whose qualifying cards reach the pod's maximum and the lowest such node
+// ("witnesses").  A pick only lowers CardNumber, so later pods of the window lose feasible
+// nodes, never gain any; a maximum of CollectMaxValues (collection.go:30-76) can only move
+// when every one of its witnesses is lost -- the host resolve checks that instead of
+// re-evaluating the pod (greedy).  Dense masks, chunk partials
+// pmax [6][C][P], pwit [2][6][C][P] (count, lowest local node), pcnt [2][C][P].
+template <int K, Path PATH>
+__global__ __launch_bounds__(kBlock) void k1_witness(
+    const unsigned char* __restrict__ nodes, uint32_t n_nodes, uint32_t chunk_nodes,
+    const typename Rec<PATH>::T* __restrict__ m_in, const typename Rec<PATH>::T* __restrict__ c_in,
+    const uint64_t* __restrict__ number_in, const uint32_t* __restrict__ need_mem_in,
+    const uint32_t* __restrict__ need_clk_in, uint32_t n_pods, uint64_t* __restrict__ pmax,
+    uint32_t* __restrict__ pwit, uint32_t* __restrict__ pcnt, uint64_t* __restrict__ bm,
+    uint32_t bm_stride) {
+  using R = Rec<PATH>;
+  using T = typename R::T;
+  const Tile tl = tile();
+  const uint32_t p = tl.pb * kBlock + threadIdx.x;
+  const uint32_t chunk = tl.chunk, C = gridDim.y;
+  const uint32_t n0 = chunk * chunk_nodes;
+  const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
+  const bool live = p < n_pods;
+  if (ballot(live) == 0) return;
+  uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
+  T m = 0, c = 0;
+  uint64_t number = ~0ull;
+  uint32_t need_mem = 0, need_clk = 0;
+  if (live) {
+    m = m_in[p];
+    c = c_in[p];
+    number = number_in[p];
+    need_mem = need_mem_in[p];
+    need_clk = need_clk_in[p];
+  }
+  T mx[6];
+  uint32_t wc[6], wn[6];
+#pragma unroll
+  for (int f = 0; f < 6; ++f) {
+    mx[f] = T(1);  // floor 1 (collection.go:31-38)
+    wc[f] = 0u;
+    wn[f] = 0xffffffffu;
+  }
+  uint32_t nf = 0, nz = 0, lo = 0, hi = 0;
+  for (uint32_t n = n0; n < n1; ++n) {
+    const unsigned char* rec = nodes + (size_t)n * R::stride(K);
+    const NodeHdrG hd = *reinterpret_cast<const NodeHdrG*>(rec);
+    const Group<T, K> fr = load_group<T, K>(rec + R::off(kFree, K));
+    const Group<T, K> ck = load_group<T, K>(rec + R::off(kClock, K));
+    uint32_t cm = 0, cc = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint32_t hj = (hd.healthy_mask >> j) & 1u;
+      cm += (uint32_t)(fr.v[j] >= m) & hj;  // CardFitsMemory (filter.go:52-54)
+      cc += (uint32_t)(ck.v[j] == c) & hj;  // CardFitsClock (filter.go:56-58)
+    }
+    const bool feas =
+        live && (number <= hd.card_number) & (cm >= need_mem) & (cc >= need_clk);
+    if (feas) {
+      ++nf;
+      nz += hd.zero_total;
+      const Group<T, K> bw = load_group<T, K>(rec + R::off(kBandwidth, K));
+      const Group<T, K> co = load_group<T, K>(rec + R::off(kCore, K));
+      const Group<T, K> pw = load_group<T, K>(rec + R::off(kPower, K));
+      const Group<T, K> to = load_group<T, K>(rec + R::off(kTotal, K));
+      // this node's contribution: the max of each field over its qualifying cards
+      T v[6] = {T(0), T(0), T(0), T(0), T(0), T(0)};
+      uint32_t any = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const bool q = (fr.v[j] >= m) & (ck.v[j] >= c);  // collection.go:46
+        any |= (uint32_t)q;
+        v[kMaxBw] = (q && bw.v[j] > v[kMaxBw]) ? bw.v[j] : v[kMaxBw];
+        v[kMaxClock] = (q && ck.v[j] > v[kMaxClock]) ? ck.v[j] : v[kMaxClock];
+        v[kMaxCore] = (q && co.v[j] > v[kMaxCore]) ? co.v[j] : v[kMaxCore];
+        v[kMaxFree] = (q && fr.v[j] > v[kMaxFree]) ? fr.v[j] : v[kMaxFree];
+        v[kMaxPower] = (q && pw.v[j] > v[kMaxPower]) ? pw.v[j] : v[kMaxPower];
+        v[kMaxTotal] = (q && to.v[j] > v[kMaxTotal]) ? to.v[j] : v[kMaxTotal];
+      }
+      if (any) {
+#pragma unroll
+        for (int f = 0; f < 6; ++f) {
+          if (v[f] > mx[f]) {  // nodes in increasing order: the first witness is the lowest
+            mx[f] = v[f];
+            wc[f] = 1u;
+            wn[f] = n;
+          } else if (v[f] == mx[f]) {
+            ++wc[f];
+          }
+        }
+      }
+    }
+    const uint64_t b = ballot(feas);
+    const int j = (int)(n & 63u);
+    set_lane(lo, hi, b, (uint32_t)j);
+    if (j == 63 || n + 1 == n1) bm_store(bmw, n & ~63u, n1, lo, hi);
+  }
+  if (!live) return;
+#pragma unroll
+  for (int f = 0; f < 6; ++f) {
+    const size_t o = ((size_t)f * C + chunk) * n_pods + p;
+    pmax[o] = (uint64_t)mx[f];
+    pwit[o] = wc[f];
+    pwit[(size_t)6 * C * n_pods + o] = wn[f];
+  }
+  pcnt[((size_t)0 * C + chunk) * n_pods + p] = nf;
+  pcnt[((size_t)1 * C + chunk) * n_pods + p] = nz;
+}
+
+// Merge of k1_witness partials, one wave per pod: maxima [6][P], counts [2][P], and per field
+// the witness count (summed over the chunks reaching the maximum) and the lowest witness
+// (global id; 0xFFFFFFFF when no node reaches it, i.e. the floor of 1).
+__global__ __launch_bounds__(kWave) void k_reduce_wit(const uint64_t* __restrict__ pmax,
+                                                       const uint32_t* __restrict__ pwit,
+                                                       const uint32_t* __restrict__ pcnt,
+                                                       uint32_t C, uint32_t n_pods,
+                                                       uint32_t node_offset,
+                                                       uint64_t* __restrict__ maxima,
+                                                       uint32_t* __restrict__ counts,
+                                                       uint32_t* __restrict__ wcount,
+                                                       uint32_t* __restrict__ wnode) {
+  const uint32_t p = blockIdx.x, lane = threadIdx.x;
+  for (int f = 0; f < 6; ++f) {
+    uint64_t mx = 1;
+    uint32_t wc = 0, wn = 0xffffffffu;
+    auto merge = [&](uint64_t m2, uint32_t c2, uint32_t n2) {
+      if (m2 > mx) {
+        mx = m2;
+        wc = c2;
+        wn = n2;
+      } else if (m2 == mx) {
+        wc += c2;
+        wn = min(wn, n2);
+      }
+    };
+    for (uint32_t c = lane; c < C; c += kWave) {
+      const size_t o = ((size_t)f * C + c) * n_pods + p;
+      merge(pmax[o], pwit[o], pwit[(size_t)6 * C * n_pods + o]);
+    }
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      const uint64_t m2 = __shfl_xor(mx, o, kWave);
+      const uint32_t c2 = __shfl_xor(wc, o, kWave), n2 = __shfl_xor(wn, o, kWave);
+      merge(m2, c2, n2);
+    }
+    if (lane == 0) {
+      maxima[(size_t)f * n_pods + p] = mx;
+      wcount[(size_t)f * n_pods + p] = wc;
+      wnode[(size_t)f * n_pods + p] = wn == 0xffffffffu ? wn : wn + node_offset;
+    }
+  }
+  for (int f = 0; f < 2; ++f) {
+    uint32_t sum = 0;
+    for (uint32_t c = lane; c < C; c += kWave) sum += pcnt[((size_t)f * C + c) * n_pods + p];
+    for (int o = kWave / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, kWave);
+    if (lane == 0) counts[(size_t)f * n_pods + p] = sum;
+  }
+}
+
 // K1, block-classified sweep (N32 path).  The batch is sorted by the Filter's inputs
 // (yoda_order.hip), so the 64 pods of a wave usually share their clock / number labels and
 // span a narrow memory range.  The wave first reduces its pods' thresholds to bounds
@@ -2175,6 +2334,61 @@ hipError_t launch_bitmask_transpose(const uint64_t* bm, uint32_t bm_stride, cons
   const MaskSrc ms{bm, bs, bm_stride, bs_stride};
   hipLaunchKernelGGL(k_bitmask_transpose, grid, dim3(kBlock), 0, s, ms, n_nodes, W,
                      n_pods, perm, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_k1_witness(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
+                             uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
+                             uint32_t n_pods, uint64_t* pmax, uint32_t* pwit, uint32_t* pcnt,
+                             uint64_t* bm, uint32_t bm_stride, hipStream_t s) {
+  dim3 grid((n_pods + kBlock - 1) / kBlock, C);
+  switch (path) {
+    case Path::N32:
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_witness<KK, Path::N32>), grid, dim3(kBlock), 0, s,
+                                          nodes, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
+                                          pp.number, pp.need_mem, pp.need_clk, n_pods, pmax, pwit,
+                                          pcnt, bm, bm_stride));
+      break;
+    case Path::F64:
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_witness<KK, Path::F64>), grid, dim3(kBlock), 0, s,
+                                          nodes, n_nodes, chunk_nodes, pp.m_f, pp.c_f, pp.number,
+                                          pp.need_mem, pp.need_clk, n_pods, pmax, pwit, pcnt, bm,
+                                          bm_stride));
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce_wit(const uint64_t* pmax, const uint32_t* pwit, const uint32_t* pcnt,
+                             uint32_t C, uint32_t n_pods, uint32_t node_offset, uint64_t* maxima,
+                             uint32_t* counts, uint32_t* wcount, uint32_t* wnode, hipStream_t s) {
+  if (n_pods == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_reduce_wit, dim3(n_pods), dim3(kWave), 0, s, pmax, pwit, pcnt, C, n_pods,
+                     node_offset, maxima, counts, wcount, wnode);
+  return hipGetLastError();
+}
+
+// Sharded capacity greedy: after the MAX all-reduce of the maxima, a shard whose own maximum
+// of a field is below the global one has no witness of it: zero its count and clear its node
+// (then the caller SUM-reduces the counts and MIN-reduces the nodes).
+__global__ __launch_bounds__(kBlock) void k_wit_prepare(const uint64_t* __restrict__ gmax,
+                                                        const uint64_t* __restrict__ lmax,
+                                                        uint32_t n, uint32_t* __restrict__ wit) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  if (lmax[i] != gmax[i]) {
+    wit[i] = 0u;
+    wit[n + i] = 0xffffffffu;
+  }
+}
+
+hipError_t launch_wit_prepare(const uint64_t* gmax, const uint64_t* lmax, uint32_t n_pods,
+                              uint32_t* wit, hipStream_t s) {
+  const uint32_t n = 6u * n_pods;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_wit_prepare, pod_grid(n), dim3(kBlock), 0, s, gmax, lmax, n, wit);
   return hipGetLastError();
 }
 

@@ -63,10 +63,14 @@ _SIGS = {
     "yoda_set_node_state": ([_vp, _u32, _vp, _vp, _vp], C.c_int),
     "yoda_shard_topk": ([_vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "yoda_shard_best_one": ([_vp, _u32, C.POINTER(C.c_double), C.POINTER(C.c_int32)], C.c_int),
+    "yoda_shard_phase1_witness": ([_vp, _vp, _vp, _vp], C.c_int),
+    "yoda_shard_witness_prepare": ([_vp, _vp, _vp, _vp], C.c_int),
+    "yoda_shard_witness_download": ([_vp, _vp, _vp, _vp, _vp], C.c_int),
     "yoda_gs_create": ([C.POINTER(CNodeSoA), C.POINTER(CPodSoA), _u32, C.POINTER(_vp)], C.c_int),
     "yoda_gs_destroy": ([_vp], C.c_int),
     "yoda_gs_queue_order": ([_vp, _vp], C.c_int),
     "yoda_gs_begin_window": ([_vp, _u32, _u32, _u32, _vp, _vp, _vp], C.c_int),
+    "yoda_gs_set_witness": ([_vp, _vp, _vp, _vp], C.c_int),
     "yoda_gs_resolve": ([_vp, C.POINTER(C.c_uint32)], C.c_int),
     "yoda_gs_assign": ([_vp, _u32, C.c_int32], C.c_int),
     "yoda_gs_take_dirty": ([_vp, _u32, _vp, _vp, _vp, C.POINTER(C.c_uint32)], C.c_int),
@@ -295,6 +299,26 @@ class Yoda:
                                           _np_ptr(ts), _np_ptr(ti)), "yoda_shard_topk")
         return counts[:, :P], ts[:, :P], ti[:, :P]
 
+    def shard_phase1_witness(self, d_maxima: int, d_counts: int, d_wit: int):
+        """Capacity greedy: phase 1 with the maxima witnesses (yoda_shard_phase1_witness)."""
+        self._check(lib().yoda_shard_phase1_witness(self._h, _vp(d_maxima), _vp(d_counts),
+                                                    _vp(d_wit)), "yoda_shard_phase1_witness")
+
+    def shard_witness_prepare(self, d_maxima_global: int, d_maxima_local: int, d_wit: int):
+        self._check(lib().yoda_shard_witness_prepare(self._h, _vp(d_maxima_global),
+                                                     _vp(d_maxima_local), _vp(d_wit)),
+                    "yoda_shard_witness_prepare")
+
+    def shard_witness_download(self, d_maxima: int, d_wit: int):
+        """(maxima [6, P] u64, wit [12, P] u32: counts then lowest nodes), caller's order."""
+        P = self.n_pods
+        mx = np.zeros((6, max(P, 1)), np.uint64)
+        wt = np.zeros((12, max(P, 1)), np.uint32)
+        self._check(lib().yoda_shard_witness_download(self._h, _vp(d_maxima), _vp(d_wit),
+                                                      _np_ptr(mx), _np_ptr(wt)),
+                    "yoda_shard_witness_download")
+        return mx[:, :P], wt[:, :P]
+
     def shard_best_one(self, pod: int):
         """(raw score, global node or -1) of batch pod `pod` over this shard, current state."""
         s, n = C.c_double(), C.c_int32()
@@ -362,6 +386,15 @@ class GreedySession:
         wn = c.size // 2
         self._check(lib().yoda_gs_begin_window(self._g, ws, wn, k, _np_ptr(c), _np_ptr(s),
                                                _np_ptr(i)), "yoda_gs_begin_window")
+
+    def set_witness(self, maxima, wit_count, wit_node):
+        """Capacity sessions: the window's maxima [6][wn] and witnesses (yoda_gs_set_witness)."""
+        self._keep_w = (np.ascontiguousarray(maxima, np.uint64),
+                        np.ascontiguousarray(wit_count, np.uint32),
+                        np.ascontiguousarray(wit_node, np.uint32))
+        m, c, n = self._keep_w
+        self._check(lib().yoda_gs_set_witness(self._g, _np_ptr(m), _np_ptr(c), _np_ptr(n)),
+                    "yoda_gs_set_witness")
 
     def resolve(self) -> int:
         nxt = C.c_uint32()

@@ -55,6 +55,16 @@ class ShardBuffers:
         # record paths bound every field by 2^44
         self.unsigned_maxima = True
 
+    def ensure_witness(self):
+        """Capacity greedy: witness buffers, [2][6][P] u32 (counts | lowest nodes), the local
+        maxima kept across the MAX all-reduce, and the nodes widened for the unsigned MIN."""
+        if getattr(self, "wit", None) is None:
+            P = max(self.n_pods, 1)
+            dev = self.maxima.device
+            self.wit = torch.empty(12 * P, dtype=torch.int32, device=dev)
+            self.maxima_local = torch.empty(6 * P, dtype=torch.int64, device=dev)
+            self.wit_node64 = torch.empty(6 * P, dtype=torch.int64, device=dev)
+
     @staticmethod
     def ptr(t: torch.Tensor) -> int:
         return t.data_ptr()
@@ -132,6 +142,24 @@ def merge_phase2(reduce: Reducer, bufs: List[ShardBuffers],
     for b in bufs:
         b.idx.copy_(b.mins[b.lowest.numel():])    # back to the u32 bit pattern
     reduce([b.ties for b in bufs], "sum")
+
+
+def merge_witness(reduce: Reducer, bufs: List[ShardBuffers], prepare: Callable):
+    """Capacity greedy phase 1: global maxima (MAX) and counts (SUM) as merge_phase1, then the
+    witnesses: a shard below a field's global maximum clears its witness of it (prepare),
+    the counts are SUM-reduced and the lowest nodes MIN-reduced (unsigned)."""
+    for b in bufs:
+        b.maxima_local.copy_(b.maxima)
+    merge_phase1(reduce, bufs)
+    for b in bufs:
+        prepare(b)
+    n = 6 * max(bufs[0].n_pods, 1)
+    reduce([b.wit[:n] for b in bufs], "sum")
+    for b in bufs:
+        b.wit_node64.copy_(b.wit[n:]).bitwise_and_(0xFFFFFFFF)  # u32 order as non-negative i64
+    reduce([b.wit_node64 for b in bufs], "min")
+    for b in bufs:
+        b.wit[n:].copy_(b.wit_node64)
 
 
 def agree_on_path(reduce: Reducer, handles, shards, offsets, device):
@@ -299,6 +327,23 @@ class HandleShard:
         self.h.shard_phase1(MODE_SCV, self.bufs.maxima.data_ptr(), self.bufs.counts.data_ptr())
         return self.bufs
 
+    def phase1_witness(self) -> ShardBuffers:
+        """Capacity windows: phase 1 with the maxima witnesses (yoda_shard_phase1_witness)."""
+        if self.bufs is None or self.bufs.n_pods != self.h.n_pods:
+            self.bufs = ShardBuffers(self.h.n_pods, self.device)
+        b = self.bufs
+        b.ensure_witness()
+        self.h.shard_phase1_witness(b.maxima.data_ptr(), b.counts.data_ptr(), b.wit.data_ptr())
+        return b
+
+    def witness_prepare(self, b: ShardBuffers):
+        self.h.shard_witness_prepare(b.maxima.data_ptr(), b.maxima_local.data_ptr(),
+                                     b.wit.data_ptr())
+
+    def witness(self):
+        """(maxima [6, P], wit [12, P]) after the merge and topk(), caller's pod order."""
+        return self.h.shard_witness_download(self.bufs.maxima.data_ptr(), self.bufs.wit.data_ptr())
+
     def topk(self):
         return self.h.shard_topk(self.bufs.maxima.data_ptr(), self.bufs.counts.data_ptr())
 
@@ -329,7 +374,9 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
     all-gathered and merged, then the host session (identical on every rank) resolves the
     window in queue order; a pod it cannot certify is scored exactly on every shard against
     the current node state and the (score, node) candidates are all-gathered.  With
-    YODA_GREEDY_CARD_CAPACITY feasibility changes after every pick, so windows hold one pod.
+    YODA_GREEDY_CARD_CAPACITY phase 1 also merges the maxima witnesses, the session applies
+    the capacity certificate, and a pod it cannot certify opens the next window (sized after
+    how far the last one got), as the single-handle yoda_greedy does.
     `shards`: this process's shards (HandleShard); `nodes`: the FULL snapshot.  The shards'
     node state is restored at the end."""
     from .capi import GreedySession, topk_k
@@ -340,7 +387,8 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
     gs = GreedySession(nodes, pods, flags)
     order = gs.queue_order()
     P = pods.n_pods
-    W = 1 if flags & GREEDY_CARD_CAPACITY else max(1, int(window))
+    W = max(1, int(window))
+    capacity = bool(flags & GREEDY_CARD_CAPACITY)
 
     def push():
         n, a, c = gs.take_dirty()
@@ -348,9 +396,35 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
             for s in shards:
                 s.set_node_state(n, a, c)
 
-    windows = exact = 0
+    windows = exact = restarts = 0
     try:
-        for ws in range(0, P, W):
+        if capacity:
+            ws, Wc = 0, W
+            while ws < P:
+                wn = min(Wc, P - ws)
+                push()
+                win = pods.take(order[ws:ws + wn])
+                for s in shards:
+                    s.upload_pods(win)
+                bufs = [s.phase1_witness() for s in shards]
+                sb = dict(zip(map(id, bufs), shards))
+                merge_witness(reduce, bufs, lambda b: sb[id(b)].witness_prepare(b))
+                lists = [s.topk() for s in shards]
+                g = reduce.gather([np.stack([ts, ti.astype(np.float64)]) for _, ts, ti in lists])
+                ts, ti = merge_topk([x[0] for x in g], [x[1].astype(np.uint64) for x in g], k)
+                mx, wit = shards[0].witness()
+                gs.begin_window(ws, k, lists[0][0], ts, ti)
+                gs.set_witness(mx, wit[:6], wit[6:])
+                nxt = gs.resolve()
+                windows += 1
+                if nxt < wn:  # the uncertified pod opens the next window
+                    restarts += 1
+                    ws += nxt
+                    Wc = min(W, max(64, 1 << int(2 * max(nxt, 1) - 1).bit_length()))
+                else:
+                    ws += wn
+                    Wc = min(W, 2 * Wc)
+        for ws in (range(0, P, W) if not capacity else ()):
             wn = min(W, P - ws)
             push()
             win = pods.take(order[ws:ws + wn])
@@ -385,6 +459,7 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
                 s.set_node_state(n, a, c)
     pick, resolved, assigned = gs.picks()
     if stats is not None:
-        stats.update(windows=windows, exact_pods=exact, certified_pods=resolved)
+        stats.update(windows=windows, exact_pods=exact, certified_pods=resolved,
+                     restarts=restarts)
     gs.close()
     return pick

@@ -465,6 +465,39 @@ def test_greedy_small_windows_and_mode_b(dev):
     np.testing.assert_array_equal(dev.greedy(pods, MODE_SCV), oracle.greedy(nodes, pods)[0])
 
 
+@pytest.mark.parametrize("path", ["n32", "f64"])
+@pytest.mark.parametrize("shape", ["config5", "contended", "zero_total", "wrap"])
+def test_greedy_card_capacity_batched(dev, path, shape):
+    """YODA_GREEDY_CARD_CAPACITY, batched (windows restart at the first pod the capacity
+    certificate cannot clear) == the sequential oracle, on inputs that stress each branch:
+    nodes running out of cards (lists exhausted, maxima witnesses lost), identical nodes
+    (every list a tie), zero-total nodes (Error status changing with feasibility), and an
+    allocated-memory sum wrapping past 2^64."""
+    nodes, pods = synth.make_config(5, pods=6000, nodes=500)
+    if shape == "contended":
+        for f in ("card_number", "card_count", "free_memory_sum", "total_memory_sum",
+                  "alloc_memory", "card_free_memory", "card_total_memory", "card_clock",
+                  "card_bandwidth", "card_core", "card_power", "card_healthy"):
+            getattr(nodes, f)[:] = getattr(nodes, f)[0]
+        pods.has_memory[:] = 1
+        pods.memory[:] = 100
+    elif shape == "zero_total":
+        nodes.total_memory_sum[::7] = 0
+    elif shape == "wrap":
+        pods.has_memory[:5] = 1
+        pods.memory[:5] = np.uint64((1 << 64) - 3)
+        pods.priority[:5] = 100
+    nodes, pods = nodes.normalized(), pods.normalized()
+    dev.upload_nodes(nodes, force_f64=path == "f64")
+    got = dev.greedy(pods, MODE_SCV, 1)
+    want, _ = oracle.greedy(nodes, pods, MODE_SCV, 1)
+    np.testing.assert_array_equal(got, want)
+    windows, restarts = dev.greedy_stats()
+    assert windows >= 2 and restarts < pods.n_pods
+    assert_same(dev.eval(pods.slice(0, 300), MODE_SCV),
+                oracle.schedule(nodes, pods.slice(0, 300), MODE_SCV, threads=8))
+
+
 def test_uniform_node_factoring(dev):
     """Nodes with one GPU model take the factored K1/K2 branch; mixed nodes the per-card
     one.  Both must equal the oracle, and equal each other with the factoring disabled."""

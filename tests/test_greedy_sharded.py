@@ -84,6 +84,48 @@ class OracleShard:
         counts = self.bufs.counts.numpy().view(np.uint32).reshape(2, n).copy()
         return counts, ts, ti
 
+    def phase1_witness(self):
+        """Phase 1 plus, per maxima field, the shard's witnesses: feasible nodes whose
+        qualifying cards (collection.go:46) reach the shard's maximum, and the lowest one."""
+        b = self.phase1()
+        b.ensure_witness()
+        n, nd = self.pods.n_pods, self.nodes
+        mx = b.maxima.numpy().view(np.uint64).reshape(6, n)
+        wc = np.zeros((6, n), np.uint32)
+        wn = np.full((6, n), 0xFFFFFFFF, np.uint32)
+        K = nd.card_free_memory.shape[1]
+        for p in range(n):
+            f, _ = self._detail(p)
+            if f.size == 0:
+                continue
+            m = int(self.pods.memory[p]) if self.pods.has_memory[p] else 0
+            c = int(self.pods.clock[p]) if self.pods.has_clock[p] else 0
+            real = np.arange(K)[None, :] < nd.card_count[f][:, None]
+            q = real & (nd.card_free_memory[f] >= m) & (nd.card_clock[f] >= c)
+            anyq = q.any(axis=1)
+            fields = (nd.card_bandwidth, nd.card_clock, nd.card_core, nd.card_free_memory,
+                      nd.card_power, nd.card_total_memory)  # MaxValue order
+            for fi, arr in enumerate(fields):
+                contrib = np.where(q, arr[f], 0).max(axis=1)
+                hit = anyq & (contrib == mx[fi, p])
+                wc[fi, p] = hit.sum()
+                if hit.any():
+                    wn[fi, p] = f[hit].min()
+        b.wit.copy_(torch.from_numpy(np.concatenate([wc, wn]).reshape(-1).view(np.int32)))
+        return b
+
+    def witness_prepare(self, b):
+        n = self.pods.n_pods
+        off = (b.maxima_local != b.maxima).numpy()
+        w = b.wit.numpy()
+        w[:6 * n][off] = 0
+        w[6 * n:][off] = -1
+
+    def witness(self):
+        n = self.pods.n_pods
+        return (self.bufs.maxima.numpy().view(np.uint64).reshape(6, n).copy(),
+                self.bufs.wit.numpy().view(np.uint32).reshape(12, n).copy())
+
     def best_one(self, i):
         f, raw = self._detail(i)
         if f.size == 0:
@@ -102,7 +144,7 @@ def _want(nodes, pods, flags):
 
 
 @pytest.mark.parametrize("contended", [False, True])
-@pytest.mark.parametrize("flags,window", [(0, 7), (0, 4096), (1, 4096)])
+@pytest.mark.parametrize("flags,window", [(0, 7), (0, 4096), (1, 4096), (1, 5)])
 def test_sharded_greedy_local(flags, window, contended):
     nodes, pods = _cluster(contended)
     b = shard_bounds(N, 3)
@@ -112,6 +154,8 @@ def test_sharded_greedy_local(flags, window, contended):
     np.testing.assert_array_equal(got, _want(nodes, pods, flags))
     if contended and flags == 0 and window == 4096:
         assert stats["exact_pods"] > 0  # the fallback path ran
+    if contended and flags == 1 and window == 4096:
+        assert stats["restarts"] > 0    # the capacity certificate failed and windows restarted
     for s in shards:  # node state restored
         np.testing.assert_array_equal(s.nodes.alloc_memory, nodes.alloc_memory)
         np.testing.assert_array_equal(s.nodes.card_number, nodes.card_number)
@@ -137,7 +181,7 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("flags,contended", [(0, False), (0, True), (1, False)])
+@pytest.mark.parametrize("flags,contended", [(0, False), (0, True), (1, False), (1, True)])
 def test_sharded_greedy_gloo(flags, contended):
     world = 2
     ctx = mp.get_context("spawn")
