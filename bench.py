@@ -39,9 +39,45 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
 def bytes_per_pair(k: int, mode: int) -> int:
-    """SURVEY.md §8d / BASELINE.md: one consult of the compact node record,
-    B_node = 32*K + 40 B (Mode B: 16 B)."""
+    """SURVEY.md §8d / BASELINE.md: one consult of the compact node record per pair,
+    B_node = 32*K + 40 B (Mode B: 16 B).  Kept for reference only: the kernels consult a
+    node's facts once per 64-pod wave (and decide most pairs for a whole wave), so this
+    per-pair model overstates the bytes ~100x and is not the roofline."""
     return 16 if mode == MODE_DISKIO else 32 * k + 40
+
+
+def k2_unique_bytes(P: int, N: int, k: int, path: str, mode: int) -> int:
+    """Algorithmic bytes of ONE K2 launch: every byte it must read or write
+    at least once -- per node its K2 summary (32 + 8K B) and its record (N32: 32 + 56K B,
+    F64/U64: 32 + 48K B), per pod its thresholds and reciprocals (36 B) and its argmax
+    outputs (best, index, ties, lowest: 24 B).  The feasibility relation between K1 and K2
+    is an intermediate (sparse form in HBM, visible in the counter traffic)."""
+    if mode == MODE_DISKIO:
+        return N * 16 + P * (16 + 24)
+    rec = 32 + (56 if path == "n32" else 48) * k
+    summ = (32 + 8 * k) if path == "n32" else 0
+    return N * (rec + summ) + P * (36 + 24)
+
+
+def step_unique_bytes(P: int, N: int, k: int, path: str, mode: int) -> int:
+    """Algorithmic bytes of one whole step: node records + both summaries (K1: 48 + 4K B,
+    K2: 32 + 8K B), the pod blob (68 B) and the per-pod outputs (pick, status, ties,
+    n_feasible, n_zero_total, best, 6 maxima: 76 B)."""
+    if mode == MODE_DISKIO:
+        return N * 16 + P * (68 + 76)
+    rec = 32 + (56 if path == "n32" else 48) * k
+    summ = ((48 + 4 * k + 15) // 16 * 16 + 32 + 8 * k) if path == "n32" else 0
+    return N * (rec + summ) + P * (68 + 76)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def kernel_names(path: str, mode: int):
@@ -51,6 +87,27 @@ def kernel_names(path: str, mode: int):
     return {"n32": ("k1_block_n32", "k2_block_n32"),
             "f64": ("k1_filter_maxima", "k2_score"),
             "u64": ("k1_filter_maxima", "k2_score_generic")}[path]
+
+
+def committed_step_traffic(P: int, N: int, world: int):
+    """Counter HBM bytes of one whole step (every kernel, FETCH_SIZE x2 + WRITE_SIZE, per
+    launch x launches per step) from the committed summary, or None."""
+    path = os.path.join(REPO, "profiles", "pmc_latest.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    meta = d.get("_workload", {})
+    if (meta.get("pods"), meta.get("nodes"), world) != (P, N, 1):
+        return None
+    steps = d.get("k2_block_n32", {}).get("calls")
+    if not steps:
+        return None
+    tot = 0.0
+    for k, v in d.items():
+        if isinstance(v, dict) and "hbm_bytes_per_launch" in v and v.get("calls"):
+            tot += v["hbm_bytes_per_launch"] * v["calls"] / steps
+    return tot
 
 
 def committed_pmc(kernel: str, P: int, N: int, world: int) -> dict:
@@ -69,6 +126,21 @@ def committed_pmc(kernel: str, P: int, N: int, world: int) -> dict:
     out = dict(d.get(kernel, {}))
     out["_source"] = "profiles/pmc_latest.json (" + meta.get("profile", "?") + ")"
     return out
+
+
+def cpu_baselines(nodes, pods, mode, target_s: float, threads: int, gpu_res):
+    """The C oracle at T=1 and T=`threads` (the box's CPU share and k8s' 16-goroutine
+    parallelizer); T=nproc is reported, not run (nproc counts the whole machine, beyond this
+    box's share).  The headline entry is the T=`threads` one."""
+    one = cpu_baseline(nodes, pods, mode, target_s / 2, 1, gpu_res)
+    many = cpu_baseline(nodes, pods, mode, target_s / 2, threads, gpu_res)
+    many["by_threads"] = {"1": {k: one[k] for k in ("value", "sample", "sample_picks_match_gpu")},
+                          str(threads): {k: many[k] for k in ("value", "sample")}}
+    many["cpu_model"] = cpu_model()
+    many["nproc"] = os.cpu_count()
+    many["nproc_note"] = (f"T=nproc ({os.cpu_count()}) not run: the GPU box's CPU share is "
+                          f"{threads} threads (OMP_NUM_THREADS), nproc counts the whole machine")
+    return many
 
 
 def cpu_baseline(nodes, pods, mode, target_s: float, threads: int, gpu_res):
@@ -99,9 +171,12 @@ def cpu_baseline(nodes, pods, mode, target_s: float, threads: int, gpu_res):
 
 def bench_greedy(args):
     """Config 5: greedy batched assignment (sequential assume in sort.Less order).
-    value = pods scheduled per second.  N=1: one handle (yoda_greedy); N>1: nodes sharded
-    across ranks, windows merged over RCCL (yoda_amd/dist.py sharded_greedy).  Rank 0 checks
-    a queue-order prefix against the sequential oracle (N=1)."""
+    value = pods scheduled per second, reference-faithful mode (flags 0: allocated memory
+    feeds Allocate, algorithm.go:299-303); `capacity` = the same batch with the CardNumber
+    decrement (YODA_GREEDY_CARD_CAPACITY, the build-defined extension BASELINE config 5 names).
+    N=1: one handle (yoda_greedy); N>1: nodes sharded across ranks, windows merged over RCCL
+    (yoda_amd/dist.py sharded_greedy).  Rank 0 checks a queue-order prefix against the
+    sequential oracle (N=1), for both modes."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -117,17 +192,21 @@ def bench_greedy(args):
             dist.init_process_group(backend)
     cfg = 5
     nodes, pods = synth.make_config(cfg, pods=args.pods, nodes=args.nodes)
-    flags = 0
     y = Yoda(dev_index)
+    runs = {}
     if world == 1:
         y.upload_nodes(nodes)
-        y.greedy(pods.slice(0, min(pods.n_pods, 4096)), MODE_SCV, flags)  # warm-up
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        picks = y.greedy(pods, MODE_SCV, flags)
-        dt = time.perf_counter() - t0
-        windows, fallbacks, times = y.greedy_stats(times=True)
-        extra = {"windows": windows, "exact_fallback_pods": fallbacks, "host_times_ms": times}
+        for flags in (0, 1):
+            y.greedy(pods.slice(0, min(pods.n_pods, 4096)), MODE_SCV, flags)  # warm-up
+            torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            picks = y.greedy(pods, MODE_SCV, flags)
+            dt = time.perf_counter() - t0
+            windows, fallbacks, times = y.greedy_stats(times=True)
+            runs[flags] = {"seconds": dt, "picks": picks, "windows": windows,
+                           "exact_fallback_pods": fallbacks, "host_times_ms": times}
+            if flags:
+                runs[flags]["window_restarts"] = y.greedy_restarts()
     else:
         import torch.distributed as dist
         from yoda_amd.dist import HandleShard, Reducer, agree_on_path, shard_bounds, sharded_greedy
@@ -138,35 +217,44 @@ def bench_greedy(args):
         red = Reducer()
         agree_on_path(red, [y], [shard], [lo], device)
         hs = [HandleShard(y, device)]
-        sharded_greedy(hs, red, nodes, pods.slice(0, min(pods.n_pods, 4096)), flags)  # warm-up
-        dist.barrier()
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        st = {}
-        picks = sharded_greedy(hs, red, nodes, pods, flags, stats=st)
-        torch.cuda.synchronize(device)
-        dt = time.perf_counter() - t0
-        t = torch.tensor([dt], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        extra = {"windows": st["windows"], "exact_fallback_pods": st["exact_pods"]}
-        if args.check and rank == 0:
-            full = Yoda(dev_index)
-            full.upload_nodes(nodes)
-            if not np.array_equal(full.greedy(pods, MODE_SCV, flags), picks):
-                raise SystemExit("--check: sharded greedy picks differ from the single handle")
-            full.close()
-            extra["check"] = "sharded greedy picks == single-handle yoda_greedy"
+        for flags in (0, 1):
+            sharded_greedy(hs, red, nodes, pods.slice(0, min(pods.n_pods, 4096)), flags)  # warm-up
+            dist.barrier()
+            torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            st = {}
+            picks = sharded_greedy(hs, red, nodes, pods, flags, stats=st)
+            torch.cuda.synchronize(device)
+            dt = time.perf_counter() - t0
+            t = torch.tensor([dt], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            runs[flags] = {"seconds": float(t.item()), "picks": picks, "windows": st["windows"],
+                           ("exact_fallback_pods" if flags == 0 else "window_restarts"):
+                           st["exact_pods"] if flags == 0 else st["restarts"]}
+            if args.check and rank == 0:
+                full = Yoda(dev_index)
+                full.upload_nodes(nodes)
+                if not np.array_equal(full.greedy(pods, MODE_SCV, flags), picks):
+                    raise SystemExit(f"--check: sharded greedy picks (flags {flags}) differ "
+                                     "from the single handle")
+                full.close()
+                runs[flags]["check"] = "sharded greedy picks == single-handle yoda_greedy"
+    r0, r1 = runs[0], runs[1]
     out = {"metric": "greedy batch: pods assigned/s (config 5, exact vs the sequential oracle)",
-           "value": pods.n_pods / dt, "unit": "pods/s", "n_gpus": world, "seconds": dt,
-           "higher_is_better": True, "data": "synthetic (yoda_amd/synth.py config 5)",
+           "value": pods.n_pods / r0["seconds"], "unit": "pods/s", "n_gpus": world,
+           "seconds": r0["seconds"], "higher_is_better": True,
+           "data": "synthetic (yoda_amd/synth.py config 5)",
            "config": {"workload": f"config5: {pods.n_pods} pods x {nodes.n_nodes} nodes greedy",
                       "pods": pods.n_pods, "nodes": nodes.n_nodes, "path": y.path,
                       "parallelism": f"node-shard x{world}" + (" (RCCL window merges)"
                                                                if world > 1 else "")},
-           "pairs_per_s_equiv": pods.n_pods * nodes.n_nodes / dt,
-           "assigned": int((picks >= 0).sum())}
-    out.update(extra)
+           "pairs_per_s_equiv": pods.n_pods * nodes.n_nodes / r0["seconds"],
+           "assigned": int((r0["picks"] >= 0).sum())}
+    out.update({k: v for k, v in r0.items() if k not in ("seconds", "picks")})
+    out["capacity"] = {"flags": "YODA_GREEDY_CARD_CAPACITY", "value": pods.n_pods / r1["seconds"],
+                       "unit": "pods/s", "seconds": r1["seconds"],
+                       "assigned": int((r1["picks"] >= 0).sum())}
+    out["capacity"].update({k: v for k, v in r1.items() if k not in ("seconds", "picks")})
     if world > 1:
         if rank == 0:
             print(json.dumps(out), flush=True)
@@ -180,22 +268,88 @@ def bench_greedy(args):
         # the sequential oracle on a prefix of the queue (greedy is order-dependent, so a
         # prefix in queue order is an exact sub-problem)
         order = oracle.queue_order(pods)
-        probe = min(pods.n_pods, 16)
-        t0 = time.perf_counter()
-        oracle.greedy(nodes, pods.take(order[:probe]), MODE_SCV, flags)
-        per_pod = max((time.perf_counter() - t0) / probe, 1e-9)
-        n = int(max(probe, min(pods.n_pods, args.cpu_seconds / per_pod)))
-        prefix = pods.take(order[:n])
-        t0 = time.perf_counter()
-        want, _ = oracle.greedy(nodes, prefix, MODE_SCV, flags)
-        cdt = time.perf_counter() - t0
-        got = y.greedy(prefix, MODE_SCV, flags)
-        out["cpu_baseline"] = {"value": n / cdt, "unit": "pods/s", "cores": 1, "kind": "port",
-                               "sample": f"first {n} pods in queue order, sequential oracle "
-                                         f"(yoda_oracle.c oracle_greedy), {cdt:.1f} s",
-                               "sample_picks_match_gpu": bool(np.array_equal(got, want))}
+        for flags, dst in ((0, out), (1, out["capacity"])):
+            probe = min(pods.n_pods, 16)
+            t0 = time.perf_counter()
+            oracle.greedy(nodes, pods.take(order[:probe]), MODE_SCV, flags)
+            per_pod = max((time.perf_counter() - t0) / probe, 1e-9)
+            n = int(max(probe, min(pods.n_pods, args.cpu_seconds / 2 / per_pod)))
+            prefix = pods.take(order[:n])
+            t0 = time.perf_counter()
+            want, _ = oracle.greedy(nodes, prefix, MODE_SCV, flags)
+            cdt = time.perf_counter() - t0
+            got = y.greedy(prefix, MODE_SCV, flags)
+            dst["cpu_baseline"] = {"value": n / cdt, "unit": "pods/s", "cores": 1, "kind": "port",
+                                   "sample": f"first {n} pods in queue order, sequential oracle "
+                                             f"(yoda_oracle.c oracle_greedy, flags {flags}), "
+                                             f"{cdt:.1f} s",
+                                   "sample_picks_match_gpu": bool(np.array_equal(got, want))}
     print(json.dumps(out), flush=True)
     y.close()
+
+
+def _timed_steps(step, barrier, n: int) -> float:
+    step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        step()
+    barrier()
+    return (time.perf_counter() - t0) / n * 1e3
+
+
+def disclosure(y, nodes, pods, step, barrier, args) -> dict:
+    """What the headline depends on, measured after the timed region on
+    the same GPU: the block kernels' work classes for this batch (device counters), the step
+    time of the per-pair kernels on the same workload, of a variant whose nodes mix GPU models
+    (half the nodes, so the one-model shortcuts apply less), and of the F64 record path
+    (memory fields in bytes instead of MiB)."""
+    out = {}
+    y.class_stats(True)
+    step()
+    barrier()
+    y.class_stats(False)
+    out["classes"] = y.class_stats()
+    P, N = pods.n_pods, nodes.n_nodes
+    variants = {}
+    rng = np.random.default_rng(12)
+    copy = lambda soa: type(soa)(**{f: np.array(getattr(soa, f))  # noqa: E731
+                                    for f in soa.__dataclass_fields__})
+    mixed = copy(nodes)
+    pick = rng.random(N) < 0.5
+    k = mixed.card_clock.shape[1]
+    models = rng.integers(0, 3, size=(int(pick.sum()), k))
+    real = np.arange(k)[None, :] < mixed.card_count[pick][:, None]
+    for arr, table in ((mixed.card_clock, synth.CLOCKS), (mixed.card_bandwidth, synth.BANDWIDTHS),
+                       (mixed.card_core, synth.CORES), (mixed.card_power, synth.POWERS)):
+        arr[pick] = np.where(real, table[models], 0)
+    mib = 1 << 20
+    f64n = copy(nodes)
+    for f in ("card_free_memory", "card_total_memory", "free_memory_sum", "total_memory_sum",
+              "alloc_memory"):
+        setattr(f64n, f, getattr(f64n, f) * np.uint64(mib))
+    f64p = copy(pods)
+    f64p.memory = f64p.memory * np.uint64(mib)
+    cases = (("per_pair_kernels", nodes, pods, dict(per_node_k1=True, per_node_k2=True)),
+             ("mixed_model_nodes_50pct", mixed.normalized(), pods, {}),
+             ("f64_path_memory_in_bytes", f64n.normalized(), f64p.normalized(), {}))
+    dev_index = torch.cuda.current_device()
+    for name, nd, pd, kw in cases:
+        z = Yoda(dev_index)
+        z.upload_nodes(nd, **kw)
+        z.upload_pods(pd)
+        z.set_stream(torch.cuda.current_stream().cuda_stream)
+        ms = _timed_steps(lambda: z.run(MODE_SCV), barrier, 3)
+        variants[name] = {"ms_per_step": ms, "pairs_per_s": P * N / (ms / 1e3), "path": z.path}
+        if name == "mixed_model_nodes_50pct":
+            z.class_stats(True)
+            z.run(MODE_SCV)
+            barrier()
+            z.class_stats(False)
+            variants[name]["classes"] = z.class_stats()
+        z.close()
+    out["variants"] = variants
+    return out
 
 
 def main():
@@ -210,6 +364,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the disclosure runs (work classes, per-pair path, mixed-model "
+                         "and F64 variants) after the timed region")
     ap.add_argument("--check", action="store_true",
                     help="N>1: rank 0 re-evaluates the batch on one unsharded handle and "
                          "asserts identical picks / statuses / ties (rehearsal)")
@@ -344,9 +501,12 @@ def main():
     names = kernel_names(y.path, mode)
     dom, dom_ms = (names[1], k2_avg) if k2_avg >= k1_avg else (names[0], k1_avg)
     p_local = my_pods.n_pods
-    algo_bytes = p_local * n_local * bytes_per_pair(k_slots, mode)
-    achieved = algo_bytes / (dom_ms / 1e3) / 1e9 if dom_ms > 0 else 0.0
-    pmc = committed_pmc(dom, P, N, world)
+    algo_bytes = k2_unique_bytes(p_local, n_local, k_slots, y.path, mode)
+    achieved = algo_bytes / (k2_avg / 1e3) / 1e9 if k2_avg > 0 else 0.0
+    pmc = committed_pmc(names[1], P, N, world)
+    pmc1 = committed_pmc(names[0], P, N, world)
+    step_traffic = committed_step_traffic(P, N, world)
+    step_bytes = step_unique_bytes(p_local, n_local, k_slots, y.path, mode)
 
     out = {
         "metric": "pod-node pair evals/sec (filter+score+select) at 100k×100k; bit-exact picks",
@@ -374,21 +534,35 @@ def main():
                                                             if world > 1 else "")),
                    "node_bounds": [int(v) for v in b] if world > 1 and not pod_shard
                    else None},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+        # dominant kernel K2: its algorithmic (unique) bytes per launch / its HIP-event launch
+        # time, against HBM peak; `traffic` = its measured HBM bytes per launch (PMC).  The
+        # kernels are bound by issue/latency, not bandwidth: the three fractions below say so.
+        "roofline": {"bound": "hbm", "kernel": names[1], "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": pmc.get("hbm_bytes_per_launch"),
-                     "avg_launch_ms": dom_ms, "k1_avg_ms": k1_avg, "k2_avg_ms": k2_avg,
-                     "bytes_per_pair": bytes_per_pair(k_slots, mode),
-                     "pairs_per_launch": p_local * n_local,
-                     # achieved > peak: a node record is consulted once per 64-pod wave,
-                     # not once per pair; the binding limits are these:
-                     "traffic_gbs": (pmc["hbm_bytes_per_launch"] / (dom_ms / 1e3) / 1e9
-                                     if pmc.get("hbm_bytes_per_launch") and dom_ms > 0
-                                     else None),
+                     "algo_bytes_per_launch": algo_bytes,
+                     "avg_launch_ms": k2_avg, "k1_avg_ms": k1_avg, "k2_avg_ms": k2_avg,
+                     "dominant_by_time": dom,
+                     "fractions": {
+                         # counter HBM bytes of K2 per launch / launch time / peak
+                         "counter_hbm": (pmc["hbm_bytes_per_launch"] / (k2_avg / 1e3) / 1e9
+                                         / HBM_PEAK_GBS
+                                         if pmc.get("hbm_bytes_per_launch") and k2_avg > 0
+                                         else None),
+                         # the whole step's algorithmic bytes / step time / peak
+                         "unique_bytes_step": step_bytes / (ms_per_step / 1e3) / 1e9
+                         / HBM_PEAK_GBS,
+                         # VALU issue utilisation of K2 and K1 (PMC)
+                         "valu_issue_k2": pmc.get("valu_issue_util"),
+                         "valu_issue_k1": pmc1.get("valu_issue_util")},
+                     "step_traffic_bytes": step_traffic,
+                     "step_unique_bytes": step_bytes,
+                     "k1_traffic": pmc1.get("hbm_bytes_per_launch"),
                      "issue": {k: pmc[k] for k in ("valu_issue_util", "salu_issue_util",
                                                    "wave_frac_waitcnt",
                                                    "wave_frac_issue_stall",
                                                    "wave_frac_issuing") if k in pmc},
+                     "per_pair_model_bytes": bytes_per_pair(k_slots, mode),
                      "pmc_source": pmc.get("_source")},
         "e2e_ms": e2e_ms,
         "status_counts": {str(s): int((res.status == s).sum()) for s in np.unique(res.status)},
@@ -404,9 +578,11 @@ def main():
                 raise SystemExit(f"--check: sharded {f} differs from the unsharded handle")
         out["check"] = ("rank 0's pod shard" if pod_shard else "merged") + \
             " picks/statuses/ties/feasible == unsharded"
+    if rank == 0 and world == 1 and not args.no_extras and mode == MODE_SCV:
+        out["extra"] = disclosure(y, nodes, pods, step, barrier, args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(nodes, pods, mode, args.cpu_seconds,
-                                           args.cpu_threads, res)
+        out["cpu_baseline"] = cpu_baselines(nodes, pods, mode, args.cpu_seconds,
+                                            args.cpu_threads, res)
     if rank == 0:
         print(json.dumps(out), flush=True)
     y.close()

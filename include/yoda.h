@@ -226,6 +226,14 @@ int yoda_set_pod_order(yoda_t* h, int enable);
 int yoda_profile(yoda_t* h, int enable);
 int yoda_profile_read(yoda_t* h, double* k1_ms, double* k2_ms, uint32_t* n_launches);
 
+/* ---- work classes ------------------------------------------------------------------ */
+/* Device counters of how the block-classified kernels (N32 path) split the
+ * (pod wave, node) pairs of the runs made while enabled (one atomic per wave and chunk).
+ * read: out[10] = {K1 ALL, K1 NONE, K1 PART, K2 U, K2 FAST, K2 EXACT, K2 skipped,
+ * K2 (wave, chunk)s with uniform maxima, K2 (wave, chunk)s, (wave, node) pairs}; resets them. */
+int yoda_class_stats_enable(yoda_t* h, int enable);
+int yoda_class_stats_read(yoda_t* h, uint64_t* out);
+
 /* ---- greedy batch ------------------------------------------------------------------- */
 /* Schedule the pods one after another in queue order (sort.go:8-10: scv/priority
  * descending, then input index), each pick feeding the next cycle through the node's
@@ -237,12 +245,15 @@ int yoda_profile_read(yoda_t* h, double* k1_ms, double* k2_ms, uint32_t* n_launc
 #define YODA_GREEDY_CARD_CAPACITY 1u
 int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, int32_t* pick);
 /* Work counters of the last yoda_greedy: GPU top-k windows, pods evaluated one by one
- * (uncertified candidates, or every pod on the exact sequential path; with
- * YODA_GREEDY_CARD_CAPACITY: windows restarted at an uncertified pod), and host wall time
+ * (uncertified candidates, or every pod on the exact sequential path), and host wall time
  * (ms) in times_ms[0..2] = {window candidate passes, sequential resolve, exact fallbacks}
  * (times_ms may be NULL). */
 int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks,
                       double* times_ms);
+/* YODA_GREEDY_CARD_CAPACITY: windows of the last yoda_greedy that ended early at a pod the
+ * capacity certificate could not clear (that pod then opened the next window); isolated
+ * uncertified pods are scheduled one by one instead (counted as fallbacks). */
+int yoda_greedy_restarts(const yoda_t* h, uint32_t* restarts);
 
 /* ---- sharded greedy batch (node shards on several GPUs) ------------------------------
  * yoda_greedy's windowed algorithm split at its exchange points, so each rank's handle holds

@@ -24,7 +24,7 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                      uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                      uint32_t n_pods, const Partials& part, uint64_t* bm, uint32_t bm_stride,
                      BlockMask* bs, uint32_t bs_stride, uint64_t* blk, uint32_t blk_stride,
-                     hipStream_t s);
+                     unsigned long long* stats, hipStream_t s);
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool narrow,
                           uint64_t* maxima, uint32_t* counts, hipStream_t s);
 hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
@@ -34,7 +34,8 @@ hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigne
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
                      const double* rcp, const float* rcp32, uint32_t n_pods,
                      const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
-                     uint32_t bs_stride, const Partials& part, int64_t* rows, hipStream_t s);
+                     uint32_t bs_stride, const Partials& part, int64_t* rows,
+                     unsigned long long* stats, hipStream_t s);
 hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
                             uint32_t C, const PodParams& pp, uint32_t n_pods, const Partials& part,
                             int64_t* rows, hipStream_t s);
@@ -96,6 +97,10 @@ hipError_t launch_reduce_wit(const uint64_t* pmax, const uint32_t* pwit, const u
                              uint32_t* counts, uint32_t* wcount, uint32_t* wnode, hipStream_t s);
 hipError_t launch_wit_prepare(const uint64_t* gmax, const uint64_t* lmax, uint32_t n_pods,
                               uint32_t* wit, hipStream_t s);
+uint32_t one_blocks();
+hipError_t launch_one(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
+                      const OnePod& pod, uint64_t* feas, void* part, uint32_t* done,
+                      OneOut* out, hipStream_t s);
 size_t order_scratch_bytes(uint32_t n_pods);
 hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
                              uint32_t n_pods, const uint32_t key_bits[3], void* scratch,
@@ -220,6 +225,7 @@ struct yoda_handle {
   DevBuf tk_s_part, tk_i_part, tk_s, tk_i, upd_node, upd_val, upd_cn;
   DevBuf g1_part, g1_done;  // k_greedy_one partials + block counter (zeroed once)
   DevBuf p_wit, wit;        // capacity greedy: witness partials [2][6][C][P], merged [2][6][P]
+  DevBuf one_feas, one_part, one_done, one_out;  // k_one_*: a pod against the current state
   PinnedBuf upd_stage, pick_stage, win_stage;
   uint32_t greedy_restarts = 0;
   hipEvent_t upd_event = nullptr;
@@ -237,6 +243,13 @@ struct yoda_handle {
   bool ran_bitmask = false;
   bool phase1_done = false;
 
+  // class counters of the block kernels (yoda_class_stats_*): device [8] u64 + host totals
+  bool class_stats = false;
+  DevBuf stats_dev;
+  uint64_t stats_pairs1 = 0, stats_pairs2 = 0;
+  unsigned long long* stats_ptr() const {
+    return class_stats ? stats_dev.as<unsigned long long>() : nullptr;
+  }
   // profiling: event pairs around K1 / K2
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
@@ -263,7 +276,8 @@ struct yoda_handle {
                      &tk_i,      &upd_node,  &upd_val,    &upd_cn,    &g1_part,   &g1_done,
                      &p_best_f,  &p_best_i,  &p_idx,      &p_ties,       &p_low_f,
                      &p_low_i,   &p_err,     &pick_alt,   &status_alt,   &ties_out_alt,
-                     &p_wit,     &wit,
+                     &p_wit,     &wit,       &stats_dev, &one_feas,  &one_part,  &one_done,
+                     &one_out,
                      &counts_alt, &best_alt, &maxima_alt};
     for (DevBuf* b : all) b->release();
     pod_stage.release();
@@ -518,7 +532,8 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts) {
                        h->has_k1sum ? h->k1sum.as<unsigned char>() : nullptr, h->n_nodes,
                        h->chunk1, h->C1, pod_params(h), P, part, h->bitmask.as<uint64_t>(),
                        bm_row(h->n_nodes), h->bsum.as<BlockMask>(), bs_row(h->n_nodes),
-                       h->blk.as<uint64_t>(), blk_row(h->n_nodes), h->stream));
+                       h->blk.as<uint64_t>(), blk_row(h->n_nodes), h->stats_ptr(), h->stream));
+  if (h->class_stats && h->has_k1sum) h->stats_pairs1 += (uint64_t)(P + 63) / 64 * h->n_nodes;
   if (e1) {
     HIP_TRY(h, hipEventRecord(e1, h->stream));
     h->ev_k1.emplace_back(e0, e1);
@@ -589,7 +604,10 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, int64_t* best, uint32_t*
                          h->n_nodes,
                          h->chunk2, h->C2, pod_params(h), maxima, h->rcp.as<double>(),
                          h->rcp32.as<float>(), P, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
-                         h->bs_ptr(), bs_row(h->n_nodes), part, rows, h->stream));
+                         h->bs_ptr(), bs_row(h->n_nodes), part, rows, h->stats_ptr(),
+                         h->stream));
+    if (h->class_stats && h->has_k2sum && !rows)
+      h->stats_pairs2 += (uint64_t)(P + 63) / 64 * h->n_nodes;
     is_f64 = !h->generic;
   }
   if (e1) {
@@ -1286,6 +1304,41 @@ int yoda_set_pod_order(yoda_t* h, int enable) {
   return YODA_OK;
 }
 
+int yoda_class_stats_enable(yoda_t* h, int enable) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (enable && !h->class_stats) {
+    HIP_TRY(h, h->stats_dev.ensure(8 * 8));
+    HIP_TRY(h, hipMemsetAsync(h->stats_dev.p, 0, 8 * 8, h->stream));
+    h->stats_pairs1 = h->stats_pairs2 = 0;
+  }
+  h->class_stats = enable != 0;
+  return YODA_OK;
+}
+
+int yoda_class_stats_read(yoda_t* h, uint64_t* out) {
+  if (!h || !out) return YODA_ERR_INVALID_ARG;
+  for (int i = 0; i < 10; ++i) out[i] = 0;
+  if (!h->stats_dev.p) return YODA_OK;
+  HIP_TRY(h, hipSetDevice(h->device));
+  uint64_t d[8] = {};
+  HIP_TRY(h, hipMemcpyAsync(d, h->stats_dev.p, 8 * 8, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  out[0] = d[0];                                                   // K1 ALL
+  out[1] = d[1];                                                   // K1 NONE
+  out[2] = h->stats_pairs1 - std::min(h->stats_pairs1, d[0] + d[1]);  // K1 PART
+  out[3] = d[2];                                                   // K2 U
+  out[4] = d[3];                                                   // K2 FAST
+  out[5] = d[4];                                                   // K2 EXACT
+  out[6] = h->stats_pairs2 - std::min(h->stats_pairs2, d[2] + d[3] + d[4]);  // K2 skipped
+  out[7] = d[5];                                                   // K2 (wave, chunk)s, uniform
+  out[8] = d[6];                                                   // K2 (wave, chunk)s
+  out[9] = h->stats_pairs1;
+  HIP_TRY(h, hipMemsetAsync(h->stats_dev.p, 0, 8 * 8, h->stream));
+  h->stats_pairs1 = h->stats_pairs2 = 0;
+  return YODA_OK;
+}
+
 int yoda_profile(yoda_t* h, int enable) {
   if (!h) return YODA_ERR_INVALID_ARG;
   h->profiling = enable != 0;
@@ -1694,6 +1747,12 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
   }
 }
 
+int yoda_greedy_restarts(const yoda_t* h, uint32_t* restarts) {
+  if (!h || !restarts) return YODA_ERR_INVALID_ARG;
+  *restarts = h->greedy_restarts;
+  return YODA_OK;
+}
+
 int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks,
                       double* times_ms) {
   if (!h) return YODA_ERR_INVALID_ARG;
@@ -1971,8 +2030,13 @@ struct yoda_greedy_session {
   uint32_t N = 0, P = 0, flags = 0;
   std::vector<uint64_t> free_sum, total_sum, alloc, card_number, alloc0, cn0, stat, stat_w;
   std::vector<uint64_t> cn_w;  // CardNumber of a window-touched node at the window start
-  std::vector<uint8_t> has_memory, has_number, touched_w, dirty, ever;
-  std::vector<uint64_t> memory, number;
+  std::vector<uint8_t> has_memory, has_number, has_clock, touched_w, dirty, ever;
+  std::vector<uint64_t> memory, number, clock;
+  // capacity mode: the nodes' cards (when the snapshot passed them), [N][K] in CardField
+  // order, to tell which lost nodes were witnesses of a pod's maxima
+  uint32_t K = 0;
+  std::vector<uint64_t> cards;  // [N][6][K]
+  std::vector<uint32_t> hmask, rmask;  // healthy / real card bits per node
   std::vector<uint32_t> order, touched_list, dirty_list, ever_list;
   std::vector<int32_t> pick;
   // current window (queue positions [ws, ws + wn)), inputs in window order
@@ -1985,6 +2049,7 @@ struct yoda_greedy_session {
   // has lost since its candidate list was made; and the window's PreScore maxima with their
   // witnesses ([6][wn] each, window order), when the caller supplied them.
   uint32_t cross[kCrossQ + 1] = {};
+  std::vector<uint32_t> cross_list[kCrossQ + 1];  // the nodes counted in cross[q]
   bool has_wit = false;
   std::vector<uint64_t> wmax;
   std::vector<uint32_t> wcnt, wnode;
@@ -2014,7 +2079,10 @@ struct yoda_greedy_session {
       const uint64_t a = card_number[n], b = a >= num ? a - num : 0;
       card_number[n] = b;
       // pods needing q in (b, a] cards have just lost this node
-      for (uint64_t q = b + 1; q <= std::min<uint64_t>(a, kCrossQ); ++q) ++cross[q];
+      for (uint64_t q = b + 1; q <= std::min<uint64_t>(a, kCrossQ); ++q) {
+        ++cross[q];
+        cross_list[q].push_back(n);
+      }
     }
     bool z;
     stat[n] = static_score(free_sum[n], total_sum[n], alloc[n], &z);
@@ -2033,32 +2101,102 @@ struct yoda_greedy_session {
     for (uint32_t n : touched_list) r += removed(n, q) ? 1 : 0;
     return r;
   }
+  // Node n passed pod p's Filter at the window start (it needs q cards; PodFitsNumber held
+  // then, n being a lost node): PodFitsMemory / PodFitsClock (filter.go:18-50) on its cards.
+  bool fit_ws(uint32_t n, uint32_t p, uint64_t q) const {
+    const uint64_t* c = cards.data() + (size_t)n * 6 * K;
+    uint64_t cm = 0, cc = 0;
+    for (uint32_t j = 0; j < K; ++j) {
+      if (!((hmask[n] >> j) & 1u)) continue;
+      cm += c[0 * K + j] >= memory[p];  // kFree
+      cc += c[1 * K + j] == clock[p];   // kClock
+    }
+    return (!has_memory[p] || cm >= q) && (!has_clock[p] || cc >= q);
+  }
+  // Node n's contribution to pod p's maxima (ProcessMaxValueWithCard over the cards with
+  // FreeMemory >= m and Clock >= c, collection.go:46-76), MaxValue field order.
+  bool contrib(uint32_t n, uint32_t p, uint64_t v[6]) const {
+    const uint64_t* c = cards.data() + (size_t)n * 6 * K;
+    const uint64_t m = has_memory[p] ? memory[p] : 0, ck = has_clock[p] ? clock[p] : 0;
+    bool any = false;
+    for (int f = 0; f < 6; ++f) v[f] = 0;
+    for (uint32_t j = 0; j < K; ++j) {
+      if (!((rmask[n] >> j) & 1u) || c[0 * K + j] < m || c[1 * K + j] < ck) continue;
+      any = true;
+      // CardField (free, clock, total, bw, core, power) -> MaxValue (bw, clock, core, free,
+      // power, total)
+      v[0] = std::max(v[0], c[3 * K + j]);
+      v[1] = std::max(v[1], c[1 * K + j]);
+      v[2] = std::max(v[2], c[4 * K + j]);
+      v[3] = std::max(v[3], c[0 * K + j]);
+      v[4] = std::max(v[4], c[5 * K + j]);
+      v[5] = std::max(v[5], c[2 * K + j]);
+    }
+    return any;
+  }
+  // The nodes pod p (needing q cards, window pod i) has lost in this window, examined with
+  // the cards at hand: how many had passed its Filter at the window start (lf), how many of
+  // those had TotalMemorySum == 0 (lz), and how many were witnesses of each of its maxima
+  // (lw).  False (nothing computed) without the cards or when too many nodes were lost.
+  static constexpr uint64_t kExactLost = 512;
+  bool scan_lost(uint32_t i, uint32_t p, uint64_t q, uint64_t lq, uint64_t* lf, uint64_t* lz,
+                 uint64_t lw[6]) const {
+    *lf = *lz = 0;
+    for (int f = 0; f < 6; ++f) lw[f] = 0;
+    if (lq == 0) return true;
+    if (cards.empty() || lq > kExactLost) return false;
+    auto visit = [&](uint32_t x) {
+      if (!fit_ws(x, p, q)) return;
+      ++*lf;
+      *lz += total_sum[x] == 0 ? 1 : 0;
+      uint64_t v[6];
+      if (has_wit && contrib(x, p, v))
+        for (int f = 0; f < 6; ++f) lw[f] += v[f] == wmax[(size_t)f * wn + i] ? 1 : 0;
+    };
+    if (q <= kCrossQ) {
+      for (uint32_t x : cross_list[q]) visit(x);
+    } else {
+      for (uint32_t x : touched_list)
+        if (removed(x, q)) visit(x);
+    }
+    return true;
+  }
   // CollectMaxValues over the remaining feasible nodes still gives window pod i's maxima:
-  // every field keeps a witness (more witnesses than lost nodes, or its only witness kept);
-  // a maximum of 1 is the floor and cannot drop (collection.go:31-38)
-  bool maxima_kept(uint32_t i, uint64_t q, uint64_t lost_q) const {
-    if (lost_q == 0) return true;
+  // every field keeps a witness.  A maximum of 1 is the floor and cannot drop
+  // (collection.go:31-38).  Exact: a field keeps its maximum iff fewer of its witnesses were
+  // lost than it had (lw from scan_lost).  Bounds only: more witnesses than lost nodes, or a
+  // single witness that is not lost.
+  bool maxima_kept(uint32_t i, uint64_t q, uint64_t lq, bool exact, const uint64_t lw[6]) const {
+    if (lq == 0) return true;
     if (!has_wit) return false;
     for (int f = 0; f < 6; ++f) {
       const size_t o = (size_t)f * wn + i;
-      if (wmax[o] <= 1 || wcnt[o] > lost_q) continue;
-      if (wcnt[o] == 1 && wnode[o] < N && !removed(wnode[o], q)) continue;
+      if (wmax[o] <= 1) continue;
+      if (exact) {
+        if (wcnt[o] > lw[f]) continue;
+      } else {
+        if (wcnt[o] > lq) continue;
+        if (wcnt[o] == 1 && wnode[o] < N && !removed(wnode[o], q)) continue;
+      }
       return false;
     }
     return true;
   }
   // Capacity-mode resolve of window pod i (input pod p): true with *pk when certified.
-  bool resolve_capacity(uint32_t i, uint32_t p, int32_t* pk) const;
+  bool resolve_capacity(uint32_t i, uint32_t p, int32_t* pk);
+  // why capacity certificates failed: wrap, few feasible left, zero-total, maxima, list
+  // exhausted, below the threshold
+  uint64_t why[6] = {};
 };
 
-bool yoda_greedy_session::resolve_capacity(uint32_t i, uint32_t p, int32_t* pk) const {
+bool yoda_greedy_session::resolve_capacity(uint32_t i, uint32_t p, int32_t* pk) {
   const uint32_t KT = k;
   const uint32_t nf0 = counts[i], nz0 = counts[(size_t)wn + i];
   if (nf0 == 0) {  // feasibility only shrinks: still no node
     *pk = YODA_PICK_NONE;
     return true;
   }
-  if (wrapped) return false;
+  if (wrapped) return ++why[0], false;
   const uint64_t q = need_cards(p);
   const uint32_t len = std::min<uint32_t>(nf0, KT);
   const bool whole = nf0 <= KT;  // the list holds every feasible node of the window start
@@ -2079,6 +2217,8 @@ bool yoda_greedy_session::resolve_capacity(uint32_t i, uint32_t p, int32_t* pk) 
       bi = n;
     }
   }
+  uint64_t lf, lz, lw[6];
+  const bool exact = scan_lost(i, p, q, lq, &lf, &lz, lw);
   if (whole) {
     if (alive == 0) {
       *pk = YODA_PICK_NONE;
@@ -2092,22 +2232,38 @@ bool yoda_greedy_session::resolve_capacity(uint32_t i, uint32_t p, int32_t* pk) 
       *pk = YODA_PICK_ERROR;
       return true;
     }
+  } else if (exact) {
+    // the feasible set is the window start's minus the lost nodes that were in it
+    const uint64_t nf = nf0 - std::min<uint64_t>(nf0, lf);
+    if (nf == 0) {
+      *pk = YODA_PICK_NONE;
+      return true;
+    }
+    if (nf == 1) {  // the only feasible node: listed and alive, or somewhere unlisted
+      if (alive != 1) return ++why[1], false;
+      *pk = (int32_t)first;
+      return true;
+    }
+    if (nz0 > lz) {  // a feasible zero-total node remains
+      *pk = YODA_PICK_ERROR;
+      return true;
+    }
   } else {
-    if (nf0 < 2 + lq) return false;  // might be down to 0 or 1 feasible nodes
+    if (nf0 < 2 + lq) return ++why[1], false;  // might be down to 0 or 1 feasible nodes
     if (nz0 > 0) {
-      if (lq > 0) return false;       // a zero-total node may be among the lost ones
+      if (lq > 0) return ++why[2], false;      // a zero-total node may be among the lost ones
       *pk = YODA_PICK_ERROR;
       return true;
     }
   }
-  if (!maxima_kept(i, q, lq)) return false;  // scores of unlisted nodes may have moved
-  if (bi == 0xffffffffu) return false;       // every listed node lost
+  if (!maxima_kept(i, q, lq, exact, lw)) return ++why[3], false;  // unlisted scores may move
+  if (bi == 0xffffffffu) return ++why[4], false;       // every listed node lost
   if (!whole) {
     // every unlisted node scored <= T at the window start (ties: higher index) and has
     // only lost Allocate since, or feasibility
     const double T = ts[(size_t)(len - 1) * wn + i];
     const uint32_t tidx = ti[(size_t)(len - 1) * wn + i];
-    if (!(bs > T || (bs == T && bi <= tidx))) return false;
+    if (!(bs > T || (bs == T && bi <= tidx))) return ++why[5], false;
   }
   *pk = (int32_t)bi;
   return true;
@@ -2151,6 +2307,36 @@ int yoda_gs_create(const yoda_node_soa* nodes, const yoda_pod_soa* pods, uint32_
     g->memory.assign(pods->memory, pods->memory + P);
     g->has_number.assign(pods->has_number, pods->has_number + P);
     g->number.assign(pods->number, pods->number + P);
+    if (pods->has_clock && pods->clock) {
+      g->has_clock.assign(pods->has_clock, pods->has_clock + P);
+      g->clock.assign(pods->clock, pods->clock + P);
+    } else {
+      g->has_clock.assign(P, 0);
+      g->clock.assign(P, 0);
+    }
+    // capacity mode: keep the cards for the exact witness accounting (optional)
+    if ((flags & YODA_GREEDY_CARD_CAPACITY) && N && nodes->max_cards >= 1 &&
+        nodes->max_cards <= YODA_MAX_CARDS && nodes->card_count && nodes->card_free_memory &&
+        nodes->card_total_memory && nodes->card_clock && nodes->card_bandwidth &&
+        nodes->card_core && nodes->card_power && nodes->card_healthy) {
+      const uint32_t K = nodes->max_cards;
+      g->K = K;
+      g->cards.assign((size_t)N * 6 * K, 0);
+      g->hmask.assign(N, 0);
+      g->rmask.assign(N, 0);
+      const uint64_t* src[6] = {nodes->card_free_memory, nodes->card_clock,
+                                nodes->card_total_memory, nodes->card_bandwidth,
+                                nodes->card_core, nodes->card_power};  // CardField order
+      for (uint32_t n = 0; n < N; ++n) {
+        const uint32_t cnt = std::min<uint32_t>(nodes->card_count[n], K);
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const size_t k = (size_t)n * K + j;
+          for (int f = 0; f < 6; ++f) g->cards[((size_t)n * 6 + f) * K + j] = src[f][k];
+          g->rmask[n] |= 1u << j;
+          if (nodes->card_healthy[k]) g->hmask[n] |= 1u << j;
+        }
+      }
+    }
     g->pick.assign(P, YODA_PICK_NONE);
     // queue order: sort.Less (sort.go:8-10), scv/priority descending, then input index
     g->order.resize(P);
@@ -2192,6 +2378,7 @@ int yoda_gs_begin_window(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
     g->in_window = true;
     g->wrapped = false;
     std::fill(std::begin(g->cross), std::end(g->cross), 0u);
+    for (auto& l : g->cross_list) l.clear();
     g->has_wit = false;
     g->counts.assign(counts, counts + 2 * (size_t)wn);
     g->ts.assign(top_score, top_score + (size_t)k * wn);
@@ -2317,6 +2504,51 @@ int yoda_gs_picks(const yoda_gs_t* g, int32_t* pick, uint32_t* resolved, uint32_
 
 }  // extern "C"
 
+// Pod p of `pods` scheduled exactly against the CURRENT device node state (k_one_*: Filter,
+// CollectMaxValues, Score, then k8s' outcome rules as k_finalize applies them).  Local pick.
+static int greedy_eval_exact(yoda_t* h, const yoda_pod_soa* pods, uint32_t p, int32_t* pick) {
+  const uint32_t N = h->n_nodes;
+  *pick = YODA_PICK_NONE;
+  if (N == 0) return YODA_OK;
+  OnePod op{};
+  const uint64_t number = pods->has_number[p] ? pods->number[p] : 1;  // filter.go:12-15
+  const uint32_t need = number > 0xffffffffull ? 0xffffffffu : (uint32_t)number;
+  const uint64_t m = pods->has_memory[p] ? pods->memory[p] : 0;
+  const uint64_t c = pods->has_clock[p] ? pods->clock[p] : 0;
+  op.number = number;
+  op.need_mem = pods->has_memory[p] ? need : 0;
+  op.need_clk = pods->has_clock[p] ? need : 0;
+  op.m32 = (uint32_t)std::min<uint64_t>(m, 0xffffffffull);
+  op.c32 = (uint32_t)std::min<uint64_t>(c, 0xffffffffull);
+  op.mf = (double)std::min<uint64_t>(m, 1ull << 53);
+  op.cf = (double)std::min<uint64_t>(c, 1ull << 53);
+  HIP_TRY(h, h->one_feas.ensure(((size_t)N + 63) / 64 * 8 + 64));
+  HIP_TRY(h, h->one_part.ensure((size_t)one_blocks() * 9 * 8));
+  HIP_TRY(h, h->one_out.ensure(sizeof(OneOut)));
+  if (h->one_done.bytes == 0) {
+    HIP_TRY(h, h->one_done.ensure(16));
+    HIP_TRY(h, hipMemsetAsync(h->one_done.p, 0, 16, h->stream));
+  }
+  HIP_TRY(h, launch_one(h->K, h->path, h->nodes.as<unsigned char>(), N, op,
+                        h->one_feas.as<uint64_t>(), h->one_part.p, h->one_done.as<uint32_t>(),
+                        h->one_out.as<OneOut>(), h->stream));
+  HIP_TRY(h, h->pick_stage.ensure(sizeof(OneOut)));
+  HIP_TRY(h, hipMemcpyAsync(h->pick_stage.p, h->one_out.p, sizeof(OneOut), hipMemcpyDeviceToHost,
+                            h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
+  OneOut o;
+  std::memcpy(&o, h->pick_stage.p, sizeof(o));
+  if (o.nf == 0)
+    *pick = YODA_PICK_NONE;
+  else if (o.nf == 1)  // k8s: the only feasible node is returned without scoring
+    *pick = (int32_t)o.first;
+  else if (o.nz > 0)   // Score would divide by TotalMemorySum == 0
+    *pick = YODA_PICK_ERROR;
+  else
+    *pick = (int32_t)o.idx;
+  return YODA_OK;
+}
+
 // ---- capacity-decrement greedy on one handle -------------------------------------------
 // YODA_GREEDY_CARD_CAPACITY on a fast record path (greedy): windows of pods
 // are evaluated on the device against the state at the window start (k1_witness + top-k
@@ -2337,6 +2569,36 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
   nv.free_memory_sum = h->h_free_sum.data();
   nv.total_memory_sum = h->h_total_sum.data();
   nv.alloc_memory = h->h_alloc.data();
+  // the cards, decoded from the host copy of the records, for the session's exact witness
+  // accounting (CardField order: free, clock, total, bandwidth, core, power)
+  const uint32_t K = (uint32_t)h->K;
+  const size_t stride = h->path == Path::N32 ? n32_stride(h->K) : node_stride(h->K);
+  std::vector<uint32_t> ccount(N);
+  std::vector<uint64_t> fld[6];
+  std::vector<uint8_t> healthy((size_t)N * K);
+  for (auto& v : fld) v.resize((size_t)N * K);
+  for (uint32_t n = 0; n < N; ++n) {
+    const unsigned char* r = h->host_records.data() + (size_t)n * stride;
+    const NodeHdrG* hd = reinterpret_cast<const NodeHdrG*>(r);
+    ccount[n] = (uint32_t)__builtin_popcount(hd->real_mask);
+    for (uint32_t j = 0; j < K; ++j) {
+      healthy[(size_t)n * K + j] = (hd->healthy_mask >> j) & 1u;
+      for (int f = 0; f < 6; ++f)
+        fld[f][(size_t)n * K + j] =
+            h->path == Path::N32
+                ? reinterpret_cast<const uint32_t*>(r + n32_u32_off(f, h->K))[j]
+                : (uint64_t) reinterpret_cast<const double*>(r + 32 + 8 * (size_t)f * K)[j];
+    }
+  }
+  nv.max_cards = K;
+  nv.card_count = ccount.data();
+  nv.card_free_memory = fld[kFree].data();
+  nv.card_clock = fld[kClock].data();
+  nv.card_total_memory = fld[kTotal].data();
+  nv.card_bandwidth = fld[kBandwidth].data();
+  nv.card_core = fld[kCore].data();
+  nv.card_power = fld[kPower].data();
+  nv.card_healthy = healthy.data();
   yoda_gs_t* g = nullptr;
   int rc = yoda_gs_create(&nv, pods, YODA_GREEDY_CARD_CAPACITY, &g);
   if (rc) return fail(h, rc, "greedy: session setup failed");
@@ -2448,14 +2710,29 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
     if ((rc = yoda_gs_begin_window(g, ws, wn, KT, cnt_w.data(), ts_w.data(), ti_w.data())) ||
         (rc = yoda_gs_set_witness(g, mx_w.data(), wc_w.data(), wc_w.data() + 6 * (size_t)wn)))
       return fail(h, rc, "greedy: session window");
-    uint32_t next = 0;
-    if ((rc = yoda_gs_resolve(g, &next))) return fail(h, rc, "greedy: resolve");
-    h->greedy_resolve_ms += ms_since(tr);
+    // resolve; an uncertified pod is scheduled exactly against the current state (k_one_*)
+    // while such pods stay rare in the window, else it opens the next window
+    uint32_t next = 0, fails = 0;
+    double fb_ms = 0;
+    for (;;) {
+      if ((rc = yoda_gs_resolve(g, &next))) return fail(h, rc, "greedy: resolve");
+      // YODA_GREEDY_FAIL_DIV (A/B knob): one exact evaluation allowed per that many resolved pods
+      static const uint32_t rate = env_u32("YODA_GREEDY_FAIL_DIV", 0);
+      if (next >= wn || ++fails > (rate ? next / rate : 0)) break;
+      const auto tf = Clock::now();
+      if ((rc = push())) return rc;
+      int32_t pk = YODA_PICK_NONE;
+      if ((rc = greedy_eval_exact(h, pods, g->order[ws + next], &pk))) return rc;
+      if ((rc = yoda_gs_assign(g, ws + next, pk))) return fail(h, rc, "greedy: assign");
+      ++h->greedy_fallbacks;
+      fb_ms += ms_since(tf);
+    }
+    h->greedy_fallback_ms += fb_ms;
+    h->greedy_resolve_ms += ms_since(tr) - fb_ms;
     if (next < wn) {
       // pod ws + next could not be certified: it opens the next window (evaluated against the
       // current state, so it is always resolved there); size it after this one's progress
       ++h->greedy_restarts;
-      ++h->greedy_fallbacks;
       uint32_t w2 = 64;
       while (w2 < 2 * next && w2 < Wmax) w2 <<= 1;
       W = std::min(w2, Wmax);
@@ -2466,6 +2743,14 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
     }
   }
   if ((rc = yoda_gs_picks(g, pick, nullptr, nullptr))) return fail(h, rc, "greedy: picks");
+  if (std::getenv("YODA_GREEDY_DEBUG"))
+    std::fprintf(stderr,
+                 "greedy capacity: windows %u restarts %u; failed certificates: wrap %llu, "
+                 "few-left %llu, zero-total %llu, maxima %llu, list-lost %llu, threshold %llu\n",
+                 h->greedy_windows, h->greedy_restarts, (unsigned long long)g->why[0],
+                 (unsigned long long)g->why[1], (unsigned long long)g->why[2],
+                 (unsigned long long)g->why[3], (unsigned long long)g->why[4],
+                 (unsigned long long)g->why[5]);
   for (uint32_t p = 0; p < P; ++p)
     if (pick[p] >= 0) pick[p] += (int32_t)h->node_offset;
   // leave the uploaded snapshot as it was

@@ -498,7 +498,7 @@ __global__ __launch_bounds__(kWave) void k_reduce_wit(const uint64_t* __restrict
 // NONE and ALL are exact statements about every (pod, node) pair of the block, not
 // approximations: ALL nodes fold their contribution into node-lane maxima that are reduced
 // across the wave once per chunk, and both write their 64-bit masks with one store.
-template <int K>
+template <int K, bool STATS>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 ? 6 : 8))) void k1_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum,
     uint32_t n_nodes, uint32_t chunk_nodes, const uint32_t* __restrict__ m_in,
@@ -506,7 +506,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
     const uint32_t* __restrict__ need_mem_in, const uint32_t* __restrict__ need_clk_in,
     uint32_t n_pods, uint64_t* __restrict__ pmax, uint32_t* __restrict__ pcnt,
     uint64_t* __restrict__ bm, uint32_t bm_stride, BlockMask* __restrict__ bs,
-    uint32_t bs_stride, uint64_t* __restrict__ blk, uint32_t blk_stride) {
+    uint32_t bs_stride, uint64_t* __restrict__ blk, uint32_t blk_stride,
+    unsigned long long* __restrict__ stats) {
   constexpr uint32_t SS = k1sum_stride(K);
   constexpr uint32_t NS = n32_stride(K);
   constexpr uint32_t HW = K + 1;  // LDS words per node: hfs[0..K-1], 0
@@ -611,8 +612,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
     const bool is_none = valid && feas_none;
     const bool is_all =
         valid && !feas_none && feas_all && uni4 && (qual_none || (qual_all && unit));
-    const uint64_t all_b = ballot(is_all);
-    uint64_t part_b = ballot(valid) & ~all_b & ~ballot(is_none);
+    const uint64_t all_b = ballot(is_all), none_b = ballot(is_none);
+    uint64_t part_b = ballot(valid) & ~all_b & ~none_b;
+    if (STATS && lane == 0) {  // class counts of (wave, node) pairs: ALL, NONE (PART = rest)
+      atomicAdd(stats + 0, (unsigned long long)__builtin_popcountll(all_b));
+      atomicAdd(stats + 1, (unsigned long long)__builtin_popcountll(none_b));
+    }
     nf_all += (uint32_t)__builtin_popcountll(all_b);
     nz_all += (uint32_t)__builtin_popcountll(ballot(is_all && (meta & kSumZeroTotal)));
     if (is_all && qual_all) {
@@ -974,7 +979,7 @@ __device__ __forceinline__ uint32_t rec_stride(Path p, int K) {
 // score to rows[n][p] (OUT_ROWS, the plugin row mode), or the TOPK best (score, node) per pod
 // sorted by (score desc, node asc) into tk_s/tk_i [C][TOPK][P] (greedy candidates).
 enum K2Out { OUT_ARGMAX = 0, OUT_ROWS = 1, OUT_TOPK = 2 };
-constexpr int kTopK = 8;
+constexpr int kTopK = 16;
 
 template <int K, Path PATH, int OUT>
 __global__ __launch_bounds__(kBlock) void k2_score(
@@ -1102,14 +1107,15 @@ __global__ __launch_bounds__(kBlock) void k2_score(
 //         reads  nq * shared + prefix[nq]  from LDS (the same integers as Scorer<N32>);
 //   EXACT anything else (mixed-model node, or non-uniform maxima): Scorer<N32>::raw.
 // Every term is an exact integer < 2^52 in each form, so all three give the same raw score.
-template <int K>
+template <int K, bool STATS>
 __global__ __launch_bounds__(kBlock) void k2_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum2,
     uint32_t n_nodes, uint32_t chunk_nodes, ScoreArgs args, uint32_t n_pods,
     const uint64_t* __restrict__ bm, uint32_t bm_stride, const BlockMask* __restrict__ bs,
     uint32_t bs_stride, const uint64_t* __restrict__ blk,
     uint32_t blk_stride, double* __restrict__ pbest,
-    uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties, double* __restrict__ plow) {
+    uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties, double* __restrict__ plow,
+    unsigned long long* __restrict__ stats) {
   constexpr uint32_t S2 = k2sum_stride(K), NS = n32_stride(K);
   constexpr uint32_t PSW = K + 2;  // LDS words per node: prefix[0..K], shared
   constexpr uint32_t TAB = kWave * PSW;  // one table: 64 nodes
@@ -1258,6 +1264,11 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
       }
     }
     uint64_t part_b = feas_b & ~u_b;
+    if (STATS && lane == 0) {  // (wave, node) pairs: U, FAST, EXACT (skipped = the rest)
+      atomicAdd(stats + 2, (unsigned long long)__builtin_popcountll(u_b));
+      atomicAdd(stats + 3, (unsigned long long)__builtin_popcountll(part_b & fast_b));
+      atomicAdd(stats + 4, (unsigned long long)__builtin_popcountll(part_b & ~fast_b));
+    }
     while (part_b) {  // wave-uniform loop over the remaining feasible nodes
       const int j = __builtin_ctzll(part_b);
       part_b &= part_b - 1;
@@ -1334,6 +1345,10 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
     }
   } else {
     for (uint32_t nb = n0; nb < n1; nb += kWave) block(nb);
+  }
+  if (STATS && lane == 0) {  // (wave, chunk)s with uniform maxima / all
+    atomicAdd(stats + 5, uni_max ? 1ull : 0ull);
+    atomicAdd(stats + 6, 1ull);
   }
   // merge the U nodes (the same for every pod lane) into each pod lane
   double wb = ubest;
@@ -1572,6 +1587,274 @@ __global__ __launch_bounds__(kBlock) void k_greedy_one(
     *reinterpret_cast<double*>(out + 1) = best;  // 8-byte aligned: out = done + 1 (sharded merge)
     *done = 0u;
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// One pod against the CURRENT node state, lane = node (the capacity greedy's exact fallback:
+// CardNumber may have dropped since the window's K1, so its bitmask and maxima are stale).
+// k_one_filter: Filter + CollectMaxValues for the pod over every node (feasibility bits
+// feas[n / 64], maxima, counts) and, in the last block to finish, the reciprocals of the
+// maxima.  k_one_score: Score of the feasible nodes with them, argmax / ties / lowest.  Both
+// reduce in the last block (a counter reset for the next call), so a pod costs two
+// launches and one small copy.
+template <int K, Path PATH>
+__global__ __launch_bounds__(kBlock) void k_one_filter(const unsigned char* __restrict__ nodes,
+                                                       uint32_t n_nodes, OnePod pod,
+                                                       uint64_t* __restrict__ feas,
+                                                       uint64_t* __restrict__ part,
+                                                       uint32_t* __restrict__ done,
+                                                       OneOut* __restrict__ out) {
+  using R = Rec<PATH>;
+  using T = typename R::T;
+  __shared__ uint64_t red[kBlock / kWave][9];
+  __shared__ bool last;
+  T m, c;
+  if constexpr (PATH == Path::N32) {
+    m = pod.m32;
+    c = pod.c32;
+  } else {
+    m = pod.mf;
+    c = pod.cf;
+  }
+  uint64_t mx[6] = {1, 1, 1, 1, 1, 1};  // floor 1 (collection.go:31-38)
+  uint32_t nf = 0, nz = 0, first = 0xffffffffu;
+  const uint32_t stride_n = gridDim.x * kBlock;
+  // every wave covers 64 consecutive nodes per step, so its ballot is one feasibility word
+  for (uint32_t nb = blockIdx.x * kBlock; nb < n_nodes; nb += stride_n) {
+    const uint32_t n = nb + threadIdx.x;
+    bool f = false;
+    if (n < n_nodes) {
+      const unsigned char* rec = nodes + (size_t)n * R::stride(K);
+      const NodeHdrG hd = *reinterpret_cast<const NodeHdrG*>(rec);
+      const Group<T, K> fr = load_group<T, K>(rec + R::off(kFree, K));
+      const Group<T, K> ck = load_group<T, K>(rec + R::off(kClock, K));
+      uint32_t cm = 0, cc = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const uint32_t hj = (hd.healthy_mask >> j) & 1u;
+        cm += (uint32_t)(fr.v[j] >= m) & hj;  // CardFitsMemory (filter.go:52-54)
+        cc += (uint32_t)(ck.v[j] == c) & hj;  // CardFitsClock (filter.go:56-58)
+      }
+      f = (pod.number <= hd.card_number) & (cm >= pod.need_mem) & (cc >= pod.need_clk);
+      if (f) {
+        ++nf;
+        nz += hd.zero_total;
+        first = min(first, n);
+        const Group<T, K> bw = load_group<T, K>(rec + R::off(kBandwidth, K));
+        const Group<T, K> co = load_group<T, K>(rec + R::off(kCore, K));
+        const Group<T, K> pw = load_group<T, K>(rec + R::off(kPower, K));
+        const Group<T, K> to = load_group<T, K>(rec + R::off(kTotal, K));
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          if ((fr.v[j] >= m) & (ck.v[j] >= c)) {  // collection.go:46
+            mx[kMaxBw] = umax64(mx[kMaxBw], (uint64_t)bw.v[j]);
+            mx[kMaxClock] = umax64(mx[kMaxClock], (uint64_t)ck.v[j]);
+            mx[kMaxCore] = umax64(mx[kMaxCore], (uint64_t)co.v[j]);
+            mx[kMaxFree] = umax64(mx[kMaxFree], (uint64_t)fr.v[j]);
+            mx[kMaxPower] = umax64(mx[kMaxPower], (uint64_t)pw.v[j]);
+            mx[kMaxTotal] = umax64(mx[kMaxTotal], (uint64_t)to.v[j]);
+          }
+        }
+      }
+    }
+    const uint64_t b = ballot(f);
+    if (lane_id() == 0 && nb + (threadIdx.x & ~63u) < n_nodes) feas[(nb + threadIdx.x) >> 6] = b;
+  }
+  // block reduce: waves through shuffles, then LDS
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+#pragma unroll
+    for (int f = 0; f < 6; ++f) mx[f] = umax64(mx[f], __shfl_xor(mx[f], o, kWave));
+    nf += __shfl_xor(nf, o, kWave);
+    nz += __shfl_xor(nz, o, kWave);
+    first = min(first, (uint32_t)__shfl_xor((int)first, o, kWave));
+  }
+  const uint32_t w = threadIdx.x >> 6;
+  if (lane_id() == 0) {
+    for (int f = 0; f < 6; ++f) red[w][f] = mx[f];
+    red[w][6] = nf;
+    red[w][7] = nz;
+    red[w][8] = first;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t k = 1; k < kBlock / kWave; ++k) {
+      for (int f = 0; f < 6; ++f) red[0][f] = umax64(red[0][f], red[k][f]);
+      red[0][6] += red[k][6];
+      red[0][7] += red[k][7];
+      red[0][8] = red[0][8] < red[k][8] ? red[0][8] : red[k][8];
+    }
+    for (int f = 0; f < 9; ++f) part[(size_t)blockIdx.x * 9 + f] = red[0][f];
+    __threadfence();
+    last = atomicAdd(done, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  // the last block merges every block's partial: threads stride over them, then as above
+  for (int f = 0; f < 6; ++f) mx[f] = 1;
+  nf = nz = 0;
+  first = 0xffffffffu;
+  const volatile uint64_t* vp = part;
+  for (uint32_t b = threadIdx.x; b < gridDim.x; b += kBlock) {
+    for (int f = 0; f < 6; ++f) mx[f] = umax64(mx[f], vp[(size_t)b * 9 + f]);
+    nf += (uint32_t)vp[(size_t)b * 9 + 6];
+    nz += (uint32_t)vp[(size_t)b * 9 + 7];
+    first = min(first, (uint32_t)vp[(size_t)b * 9 + 8]);
+  }
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+#pragma unroll
+    for (int f = 0; f < 6; ++f) mx[f] = umax64(mx[f], __shfl_xor(mx[f], o, kWave));
+    nf += __shfl_xor(nf, o, kWave);
+    nz += __shfl_xor(nz, o, kWave);
+    first = min(first, (uint32_t)__shfl_xor((int)first, o, kWave));
+  }
+  __syncthreads();
+  if (lane_id() == 0) {
+    for (int f = 0; f < 6; ++f) red[w][f] = mx[f];
+    red[w][6] = nf;
+    red[w][7] = nz;
+    red[w][8] = first;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  uint64_t acc[9];
+  for (int f = 0; f < 9; ++f) acc[f] = red[0][f];
+  for (uint32_t k = 1; k < kBlock / kWave; ++k) {
+    for (int f = 0; f < 6; ++f) acc[f] = umax64(acc[f], red[k][f]);
+    acc[6] += red[k][6];
+    acc[7] += red[k][7];
+    acc[8] = acc[8] < red[k][8] ? acc[8] : red[k][8];
+  }
+  for (int f = 0; f < 6; ++f) out->maxima[f] = acc[f];
+  out->nf = (uint32_t)acc[6];
+  out->nz = (uint32_t)acc[7];
+  out->first = (uint32_t)acc[8];
+  const int src[5] = {kMaxBw, kMaxCore, kMaxPower, kMaxFree, kMaxTotal};
+  for (int k = 0; k < 5; ++k) {
+    const double M = (double)acc[src[k]];
+    out->rcp[k] = ru_100_over(M);
+    if (k < 3) out->rcp32[k] = ru32_100_over(M);
+  }
+  *done = 0u;
+}
+
+template <int K, Path PATH>
+__global__ __launch_bounds__(kBlock) void k_one_score(const unsigned char* __restrict__ nodes,
+                                                      uint32_t n_nodes, OnePod pod,
+                                                      const uint64_t* __restrict__ feas,
+                                                      double* __restrict__ part,
+                                                      uint32_t* __restrict__ done,
+                                                      OneOut* __restrict__ out) {
+  __shared__ double red_d[kBlock / kWave][2];
+  __shared__ uint32_t red_u[kBlock / kWave][2];
+  __shared__ bool last;
+  Scorer<PATH> sc;
+  if constexpr (PATH == Path::N32) {
+    sc.m = pod.m32;
+    sc.c = pod.c32;
+    sc.r_bw = out->rcp32[0];
+    sc.r_core = out->rcp32[1];
+    sc.r_pow = out->rcp32[2];
+  } else {
+    sc.m = pod.mf;
+    sc.c = pod.cf;
+    sc.r_bw = out->rcp[0];
+    sc.r_core = out->rcp[1];
+    sc.r_pow = out->rcp[2];
+  }
+  sc.r_free = out->rcp[3];
+  sc.r_tot = out->rcp[4];
+  constexpr uint32_t stride = PATH == Path::N32 ? n32_stride(K) : node_stride(K);
+  double best = -1.0, low = 1.0e300;
+  uint32_t idx = 0xffffffffu, ties = 0;
+  for (uint32_t n = blockIdx.x * kBlock + threadIdx.x; n < n_nodes; n += gridDim.x * kBlock) {
+    if ((feas[n >> 6] >> (n & 63u)) & 1ull) {
+      const double raw = sc.template raw<K>(nodes + (size_t)n * stride);
+      if (raw > best) {  // n grows along the thread's sweep: the first maximum is the lowest
+        best = raw;
+        idx = n;
+        ties = 1;
+      } else if (raw == best) {
+        ++ties;
+      }
+      low = fmin(low, raw);
+    }
+  }
+  auto merge = [](double& b, uint32_t& i, uint32_t& t, double ob, uint32_t oi, uint32_t ot) {
+    if (ob > b) {
+      b = ob;
+      i = oi;
+      t = ot;
+    } else if (ob == b && ot) {
+      i = min(i, oi);
+      t += ot;
+    }
+  };
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    merge(best, idx, ties, __shfl_xor(best, o, kWave), (uint32_t)__shfl_xor((int)idx, o, kWave),
+          (uint32_t)__shfl_xor((int)ties, o, kWave));
+    low = fmin(low, __shfl_xor(low, o, kWave));
+  }
+  const uint32_t w = threadIdx.x >> 6;
+  if (lane_id() == 0) {
+    red_d[w][0] = best;
+    red_d[w][1] = low;
+    red_u[w][0] = idx;
+    red_u[w][1] = ties;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t k = 1; k < kBlock / kWave; ++k) {
+      merge(best, idx, ties, red_d[k][0], red_u[k][0], red_u[k][1]);
+      low = fmin(low, red_d[k][1]);
+    }
+    part[(size_t)blockIdx.x * 4 + 0] = best;
+    part[(size_t)blockIdx.x * 4 + 1] = low;
+    part[(size_t)blockIdx.x * 4 + 2] = (double)idx;
+    part[(size_t)blockIdx.x * 4 + 3] = (double)ties;
+    __threadfence();
+    last = atomicAdd(done, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  best = -1.0;
+  low = 1.0e300;
+  idx = 0xffffffffu;
+  ties = 0;
+  const volatile double* vp = part;
+  for (uint32_t b = threadIdx.x; b < gridDim.x; b += kBlock) {  // blocks in node order
+    merge(best, idx, ties, vp[(size_t)b * 4], (uint32_t)vp[(size_t)b * 4 + 2],
+          (uint32_t)vp[(size_t)b * 4 + 3]);
+    low = fmin(low, vp[(size_t)b * 4 + 1]);
+  }
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    merge(best, idx, ties, __shfl_xor(best, o, kWave), (uint32_t)__shfl_xor((int)idx, o, kWave),
+          (uint32_t)__shfl_xor((int)ties, o, kWave));
+    low = fmin(low, __shfl_xor(low, o, kWave));
+  }
+  __syncthreads();
+  if (lane_id() == 0) {
+    red_d[w][0] = best;
+    red_d[w][1] = low;
+    red_u[w][0] = idx;
+    red_u[w][1] = ties;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  for (uint32_t k = 1; k < kBlock / kWave; ++k) {
+    merge(best, idx, ties, red_d[k][0], red_u[k][0], red_u[k][1]);
+    low = fmin(low, red_d[k][1]);
+  }
+  out->best = best;
+  out->low = low;
+  out->idx = idx;
+  out->ties = ties;
+  *done = 0u;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2010,16 +2293,23 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                      uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                      uint32_t n_pods, const Partials& part, uint64_t* bm, uint32_t bm_stride,
                      BlockMask* bs, uint32_t bs_stride, uint64_t* blk, uint32_t blk_stride,
-                     hipStream_t s) {
+                     unsigned long long* stats, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   switch (path) {
     case Path::N32:
       if (sum) {
-        YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK>), grid, dim3(kBlock), 0, s, nodes,
-                                            sum, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
-                                            pp.number, pp.need_mem, pp.need_clk, n_pods,
-                                            part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,
-                                            blk, blk_stride));
+        if (stats)
+          YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK, true>), grid, dim3(kBlock), 0, s,
+                                              nodes, sum, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
+                                              pp.number, pp.need_mem, pp.need_clk, n_pods,
+                                              part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,
+                                              blk, blk_stride, stats))
+        else
+          YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK, false>), grid, dim3(kBlock), 0, s,
+                                              nodes, sum, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
+                                              pp.number, pp.need_mem, pp.need_clk, n_pods,
+                                              part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,
+                                              blk, blk_stride, stats));
       } else {
         YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_filter_maxima<KK, Path::N32>), grid, dim3(kBlock),
                                             0, s, nodes, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
@@ -2056,14 +2346,14 @@ int kernel_capacity(int K, Path path, int which, int mode_diskio) {
     YODA_FN(&k2_diskio<false>);
   } else if (which == 1) {
     switch (path) {
-      case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k1_block_n32<KK>))); break;
+      case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k1_block_n32<KK, false>))); break;
       case Path::F64: YODA_K_SWITCH(K, YODA_FN((&k1_filter_maxima<KK, Path::F64>))); break;
       case Path::U64: YODA_K_SWITCH(K, YODA_FN((&k1_filter_maxima<KK, Path::U64>))); break;
     }
   } else {
     switch (path) {
       case Path::N32:
-        YODA_K_SWITCH(K, YODA_FN((&k2_block_n32<KK>)));
+        YODA_K_SWITCH(K, YODA_FN((&k2_block_n32<KK, false>)));
         break;
       case Path::F64: YODA_K_SWITCH(K, YODA_FN((&k2_score<KK, Path::F64, OUT_ARGMAX>))); break;
       case Path::U64: YODA_K_SWITCH(K, YODA_FN((&k2_score_generic<KK, false>))); break;
@@ -2113,17 +2403,24 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
                               const uint64_t* maxima, const double* rcp, const float* rcp32,
                               uint32_t n_pods, const uint64_t* bm, uint32_t bm_stride,
                               const BlockMask* bs, uint32_t bs_stride, const Partials& part,
-                              int64_t* rows, double* tk_s, uint32_t* tk_i, hipStream_t s) {
+                              int64_t* rows, double* tk_s, uint32_t* tk_i,
+                              unsigned long long* stats, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
   const MaskSrc ms{bm, bs, bm_stride, bs_stride};
   switch (path) {
     case Path::N32:
       if (OUT == OUT_ARGMAX && sum2) {
-        YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK>), grid, dim3(kBlock), 0, s, nodes,
-                                            sum2, n_nodes, chunk_nodes, a, n_pods, bm, bm_stride,
-                                            bs, bs_stride, blk, blk_stride, part.best_f, part.idx, part.ties,
-                                            part.low_f));
+        if (stats)
+          YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, true>), grid, dim3(kBlock), 0, s,
+                                              nodes, sum2, n_nodes, chunk_nodes, a, n_pods, bm,
+                                              bm_stride, bs, bs_stride, blk, blk_stride,
+                                              part.best_f, part.idx, part.ties, part.low_f, stats))
+        else
+          YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false>), grid, dim3(kBlock), 0, s,
+                                              nodes, sum2, n_nodes, chunk_nodes, a, n_pods, bm,
+                                              bm_stride, bs, bs_stride, blk, blk_stride,
+                                              part.best_f, part.idx, part.ties, part.low_f, stats));
         break;
       }
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score<KK, Path::N32, OUT>), grid, dim3(kBlock), 0,
@@ -2156,7 +2453,8 @@ hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t
                           uint32_t* tk_i, hipStream_t s) {
   return launch_k2_t<OUT_TOPK>(K, path, nodes, nullptr, nullptr, 0, n_nodes, chunk_nodes, C, pp, nullptr, rcp,
                                rcp32,
-                               n_pods, bm, bm_stride, bs, bs_stride, part, nullptr, tk_s, tk_i, s);
+                               n_pods, bm, bm_stride, bs, bs_stride, part, nullptr, tk_s, tk_i,
+                               nullptr, s);
 }
 
 hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t C,
@@ -2219,14 +2517,15 @@ hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigne
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
                      const double* rcp, const float* rcp32, uint32_t n_pods,
                      const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
-                     uint32_t bs_stride, const Partials& part, int64_t* rows, hipStream_t s) {
+                     uint32_t bs_stride, const Partials& part, int64_t* rows,
+                     unsigned long long* stats, hipStream_t s) {
   if (rows)
     return launch_k2_t<OUT_ROWS>(K, path, nodes, nullptr, nullptr, 0, n_nodes, chunk_nodes, C, pp, maxima, rcp,
                                  rcp32, n_pods, bm, bm_stride, bs, bs_stride, part, rows, nullptr,
-                                 nullptr, s);
+                                 nullptr, stats, s);
   return launch_k2_t<OUT_ARGMAX>(K, path, nodes, sum2, blk, blk_stride, n_nodes, chunk_nodes, C, pp, maxima, rcp,
                                  rcp32, n_pods, bm, bm_stride, bs, bs_stride, part, rows, nullptr,
-                                 nullptr, s);
+                                 nullptr, stats, s);
 }
 
 hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
@@ -2389,6 +2688,36 @@ hipError_t launch_wit_prepare(const uint64_t* gmax, const uint64_t* lmax, uint32
   const uint32_t n = 6u * n_pods;
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_wit_prepare, pod_grid(n), dim3(kBlock), 0, s, gmax, lmax, n, wit);
+  return hipGetLastError();
+}
+
+// Blocks of the k_one_* launches (grid-stride over the nodes).
+constexpr uint32_t kOneBlocks = 512;
+uint32_t one_blocks() { return kOneBlocks; }
+
+hipError_t launch_one(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
+                      const OnePod& pod, uint64_t* feas, void* part, uint32_t* done,
+                      OneOut* out, hipStream_t s) {
+  const dim3 grid(std::max<uint32_t>(1, std::min<uint32_t>(kOneBlocks,
+                                                           (n_nodes + kBlock - 1) / kBlock)));
+  uint64_t* p1 = static_cast<uint64_t*>(part);
+  double* p2 = static_cast<double*>(part);
+  switch (path) {
+    case Path::N32:
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k_one_filter<KK, Path::N32>), grid, dim3(kBlock), 0, s,
+                                          nodes, n_nodes, pod, feas, p1, done, out);
+                    hipLaunchKernelGGL((k_one_score<KK, Path::N32>), grid, dim3(kBlock), 0, s,
+                                       nodes, n_nodes, pod, feas, p2, done + 1, out));
+      break;
+    case Path::F64:
+      YODA_K_SWITCH(K, hipLaunchKernelGGL((k_one_filter<KK, Path::F64>), grid, dim3(kBlock), 0, s,
+                                          nodes, n_nodes, pod, feas, p1, done, out);
+                    hipLaunchKernelGGL((k_one_score<KK, Path::F64>), grid, dim3(kBlock), 0, s,
+                                       nodes, n_nodes, pod, feas, p2, done + 1, out));
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

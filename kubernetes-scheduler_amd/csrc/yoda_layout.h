@@ -150,6 +150,24 @@ struct alignas(16) NodeRecB {
   double v, u;
 };
 
+// One pod evaluated alone against the CURRENT node state (greedy fallbacks), lane = node:
+// its Filter / card-predicate operands, passed by value (yoda_kernels.hip k_one_*).
+struct OnePod {
+  uint64_t number;            // PodFitsNumber operand: label value or 1
+  uint32_t need_mem, need_clk;  // healthy cards required (0: label absent)
+  uint32_t m32, c32;          // N32 thresholds (clamped to 0xFFFFFFFF)
+  double mf, cf;              // F64 thresholds (clamped to 2^53)
+};
+// Results of the two k_one_* launches (device, then copied to the host in one piece).
+struct alignas(16) OneOut {
+  uint64_t maxima[6];         // PreScore maxima, MaxValue order (floor 1)
+  uint32_t nf, nz, first, pad;  // feasible nodes, of them TotalMemorySum == 0, lowest one
+  double rcp[5];              // RU(100/M): bw, core, power, free, total
+  float rcp32[3], pad2;       // RU32(100/M): bw, core, power
+  double best, low;           // highest / lowest raw score over the feasible nodes
+  uint32_t idx, ties;         // lowest node reaching best, nodes reaching it
+};
+
 // Per-pod device parameters (struct of arrays, length P each).
 struct PodParams {
   // Filter / card predicate thresholds

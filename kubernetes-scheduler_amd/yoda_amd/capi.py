@@ -66,6 +66,9 @@ _SIGS = {
     "yoda_shard_phase1_witness": ([_vp, _vp, _vp, _vp], C.c_int),
     "yoda_shard_witness_prepare": ([_vp, _vp, _vp, _vp], C.c_int),
     "yoda_shard_witness_download": ([_vp, _vp, _vp, _vp, _vp], C.c_int),
+    "yoda_class_stats_enable": ([_vp, C.c_int], C.c_int),
+    "yoda_class_stats_read": ([_vp, _vp], C.c_int),
+    "yoda_greedy_restarts": ([_vp, C.POINTER(C.c_uint32)], C.c_int),
     "yoda_gs_create": ([C.POINTER(CNodeSoA), C.POINTER(CPodSoA), _u32, C.POINTER(_vp)], C.c_int),
     "yoda_gs_destroy": ([_vp], C.c_int),
     "yoda_gs_queue_order": ([_vp, _vp], C.c_int),
@@ -251,10 +254,33 @@ class Yoda:
                                       "fallback_ms": t[2]}
         return w.value, f.value
 
+    def greedy_restarts(self) -> int:
+        """Capacity greedy: windows that ended early at an uncertified pod."""
+        r = C.c_uint32()
+        self._check(lib().yoda_greedy_restarts(self._h, C.byref(r)), "yoda_greedy_restarts")
+        return r.value
+
     def set_pod_order(self, enable: bool = True):
         """Sort Mode-A batches on the device before K1/K2 (default on); results are returned
         in the caller's pod order either way."""
         self._check(lib().yoda_set_pod_order(self._h, 1 if enable else 0), "yoda_set_pod_order")
+
+    def class_stats(self, enable: bool | None = None):
+        """Block-kernel work classes (yoda_class_stats_*).  enable=True/False switches the
+        counters; enable=None reads (and resets) them as a dict of pair fractions."""
+        if enable is not None:
+            self._check(lib().yoda_class_stats_enable(self._h, 1 if enable else 0),
+                        "yoda_class_stats_enable")
+            return None
+        out = np.zeros(10, np.uint64)
+        self._check(lib().yoda_class_stats_read(self._h, _np_ptr(out)), "yoda_class_stats_read")
+        v = [int(x) for x in out]
+        pairs = max(v[9], 1)
+        return {"k1": {"all": v[0] / pairs, "none": v[1] / pairs, "part": v[2] / pairs},
+                "k2": {"skipped": v[6] / pairs, "u": v[3] / pairs, "fast": v[4] / pairs,
+                       "exact": v[5] / pairs},
+                "k2_uniform_maxima_wave_chunks": v[7] / max(v[8], 1),
+                "wave_node_pairs": v[9]}
 
     def profile(self, enable: bool = True):
         self._check(lib().yoda_profile(self._h, 1 if enable else 0), "yoda_profile")
