@@ -298,6 +298,40 @@ def _timed_steps(step, barrier, n: int) -> float:
     return (time.perf_counter() - t0) / n * 1e3
 
 
+def row_latency(dev_index: int, node_counts=(5000, 100000), cycles: int = 60) -> dict:
+    """Plugin row mode: one scheduling cycle's PreFilter through the
+    Python plugin mirror (yoda_amd/plugin.py) = pack the pod (Go label semantics), upload it,
+    yoda_score_rows (Filter bits + raw Score of every node) and copy the row back; and the
+    bare C-ABI part of it (upload_pods + score_rows).  P = 1, config-3 nodes."""
+    from yoda_amd.pack import pods_to_dicts
+    from yoda_amd.plugin import CycleState, YodaPlugin
+    out = {}
+    for n in node_counts:
+        nodes, pods = synth.make_config(3, pods=cycles, nodes=n)
+        z = Yoda(dev_index)
+        z.upload_nodes(nodes)
+        plugin = YodaPlugin(z, [f"node-{i}" for i in range(n)], nodes)
+        dicts = pods_to_dicts(pods)
+        for d in dicts[:3]:
+            plugin.pre_filter(CycleState(), d)
+        t_plugin, t_abi = [], []
+        for p, d in enumerate(dicts):
+            t0 = time.perf_counter()
+            plugin.pre_filter(CycleState(), d)
+            t_plugin.append((time.perf_counter() - t0) * 1e3)
+            one = pods.slice(p, p + 1)
+            t0 = time.perf_counter()
+            z.upload_pods(one)
+            z.score_rows(MODE_SCV)
+            t_abi.append((time.perf_counter() - t0) * 1e3)
+        z.close()
+        q = lambda v, x: float(np.percentile(v, x))  # noqa: E731
+        out[str(n)] = {"prefilter_ms_p50": q(t_plugin, 50), "prefilter_ms_p99": q(t_plugin, 99),
+                       "capi_ms_p50": q(t_abi, 50), "capi_ms_p99": q(t_abi, 99),
+                       "cycles": cycles}
+    return out
+
+
 def disclosure(y, nodes, pods, step, barrier, args) -> dict:
     """What the headline depends on, measured after the timed region on
     the same GPU: the block kernels' work classes for this batch (device counters), the step
@@ -349,6 +383,7 @@ def disclosure(y, nodes, pods, step, barrier, args) -> dict:
             variants[name]["classes"] = z.class_stats()
         z.close()
     out["variants"] = variants
+    out["plugin_row_latency"] = row_latency(dev_index)
     return out
 
 
@@ -378,11 +413,18 @@ def main():
     ap.add_argument("--no-balance", action="store_true",
                     help="--shard nodes: keep equal node blocks (default: re-cut them once "
                          "after warm-up so every rank's measured K1 + K2 time is equal)")
-    ap.add_argument("--workload", choices=["eval", "greedy"], default="eval",
-                    help="eval: the headline batch (config 3); greedy: config 5 sequential assume")
+    ap.add_argument("--workload", choices=["eval", "greedy", "row"], default="eval",
+                    help="eval: the headline batch (config 3); greedy: config 5 sequential "
+                         "assume; row: the plugin's per-cycle row latency (P = 1)")
     args = ap.parse_args()
     if args.workload == "greedy":
         return bench_greedy(args)
+    if args.workload == "row":
+        torch.cuda.set_device(0)
+        print(json.dumps({"metric": "plugin PreFilter latency (one pod vs every node)",
+                          "unit": "ms", "higher_is_better": False,
+                          "row_latency": row_latency(0)}), flush=True)
+        return
     mode = MODE_SCV if args.mode == "scv" else MODE_DISKIO
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -193,6 +193,13 @@ int yoda_download_bitmask(yoda_t* h, uint32_t* words, uint64_t n_words);
  * Also leaves the picks for yoda_download.  Either output may be NULL. */
 int yoda_score_rows(yoda_t* h, int mode, uint32_t* bitmask, uint64_t n_bitmask_words,
                     int64_t* scores, uint64_t n_scores);
+/* yoda_score_rows plus the normalized scores, computed on the device: norm [P][N] int64 =
+ * Yoda.NormalizeScore (scheduler.go:158-183) over each pod's feasible nodes -- highest =
+ * max(0, max raw), lowest = min raw, lowest-- when equal, (raw - lowest) * 100 /
+ * (highest - lowest) in Go's int64 arithmetic -- and -1 where Filter fails.  k8s then adds
+ * the plugin weight and validates [0, 100] (RunScorePlugins). */
+int yoda_score_rows_norm(yoda_t* h, int mode, uint32_t* bitmask, uint64_t n_bitmask_words,
+                         int64_t* scores, uint64_t n_scores, int64_t* norm, uint64_t n_norm);
 
 /* Sharded evaluation.  Each rank holds a node shard; between phases the caller reduces
  * the exchange buffers across ranks (RCCL all-reduce) with the op named per buffer.

@@ -101,6 +101,9 @@ uint32_t one_blocks();
 hipError_t launch_one(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                       const OnePod& pod, uint64_t* feas, void* part, uint32_t* done,
                       OneOut* out, hipStream_t s);
+hipError_t launch_norm_rows(const int64_t* rows, uint32_t n_nodes, uint32_t n_pods,
+                            const int64_t* best, const int64_t* lowest, int64_t* norm,
+                            hipStream_t s);
 size_t order_scratch_bytes(uint32_t n_pods);
 hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
                              uint32_t n_pods, const uint32_t key_bits[3], void* scratch,
@@ -215,7 +218,7 @@ struct yoda_handle {
   DevBuf maxima, counts, rcp, rcp32, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
   // scatter targets of unpermute_outputs, swapped with the buffers above after each scatter
   DevBuf pick_alt, status_alt, ties_out_alt, counts_alt, best_alt, maxima_alt;
-  DevBuf bitmask, bitmask_t, rows, rows_t;
+  DevBuf bitmask, bitmask_t, rows, rows_t, norm;
   DevBuf blk;               // [wave][node block / 64] u64: blocks with a feasible pod (K1 -> K2)
   bool blk_valid = false;   // the last K1 wrote blk (block-classified K1 on this batch)
   DevBuf bsum;              // [wave][node block] BlockMask: the block K1's sparse masks
@@ -272,7 +275,7 @@ struct yoda_handle {
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
                      &n_flagged, &bitmask,   &bitmask_t,  &blk,  &bsum, &p_max_u,      &p_cnt,
-                     &rows,      &rows_t,    &tk_s_part,  &tk_i_part,    &tk_s,
+                     &rows,      &rows_t,    &norm,      &tk_s_part,  &tk_i_part,    &tk_s,
                      &tk_i,      &upd_node,  &upd_val,    &upd_cn,    &g1_part,   &g1_done,
                      &p_best_f,  &p_best_i,  &p_idx,      &p_ties,       &p_low_f,
                      &p_low_i,   &p_err,     &pick_alt,   &status_alt,   &ties_out_alt,
@@ -1154,6 +1157,13 @@ int yoda_download_bitmask(yoda_t* h, uint32_t* words, uint64_t n_words) {
 
 int yoda_score_rows(yoda_t* h, int mode, uint32_t* bitmask_out, uint64_t n_bitmask_words,
                     int64_t* scores_out, uint64_t n_scores) {
+  return yoda_score_rows_norm(h, mode, bitmask_out, n_bitmask_words, scores_out, n_scores,
+                              nullptr, 0);
+}
+
+int yoda_score_rows_norm(yoda_t* h, int mode, uint32_t* bitmask_out, uint64_t n_bitmask_words,
+                         int64_t* scores_out, uint64_t n_scores, int64_t* norm_out,
+                         uint64_t n_norm) {
   int rc = prepare_run(h, mode);
   if (rc) return rc;
   try {
@@ -1163,10 +1173,12 @@ int yoda_score_rows(yoda_t* h, int mode, uint32_t* bitmask_out, uint64_t n_bitma
       return fail(h, YODA_ERR_INVALID_ARG, "bitmask buffer too small");
     if (scores_out && n_scores < (uint64_t)N * P)
       return fail(h, YODA_ERR_INVALID_ARG, "scores buffer too small");
+    if (norm_out && n_norm < (uint64_t)N * P)
+      return fail(h, YODA_ERR_INVALID_ARG, "norm buffer too small");
     if ((uint64_t)N * P > (1ull << 31))
       return fail(h, YODA_ERR_RANGE, "yoda_score_rows is for small pod batches (P*N <= 2^31)");
     int64_t* rows = nullptr;
-    if (scores_out && (uint64_t)N * P > 0) {
+    if ((scores_out || norm_out) && (uint64_t)N * P > 0) {
       HIP_TRY(h, h->rows.ensure((size_t)N * P * 8));
       HIP_TRY(h, h->rows_t.ensure((size_t)N * P * 8));
       HIP_TRY(h, hipMemsetAsync(h->rows.p, 0xff, (size_t)N * P * 8, h->stream));  // -1
@@ -1178,6 +1190,11 @@ int yoda_score_rows(yoda_t* h, int mode, uint32_t* bitmask_out, uint64_t n_bitma
                      h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(),
                      rows)))
       return rc;
+    if (norm_out && rows) {  // before finalize: best / lowest still in the rows' pod order
+      HIP_TRY(h, h->norm.ensure((size_t)N * P * 8));
+      HIP_TRY(h, launch_norm_rows(rows, N, P, h->best.as<int64_t>(), h->lowest.as<int64_t>(),
+                                  h->norm.as<int64_t>(), h->stream));
+    }
     if ((rc = finalize(h, mode, h->counts.as<uint32_t>(), h->best.as<int64_t>(),
                        h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(),
                        false)))
@@ -1185,11 +1202,19 @@ int yoda_score_rows(yoda_t* h, int mode, uint32_t* bitmask_out, uint64_t n_bitma
     h->ran = true;
     h->ran_bitmask = mode == YODA_MODE_SCV;
     h->last_mode = mode;
-    if (rows) {
+    if (rows && scores_out) {
       HIP_TRY(h, launch_rows_transpose(rows, N, P, h->ordered ? h->perm.as<uint32_t>() : nullptr,
                                        h->rows_t.as<int64_t>(), h->stream));
       HIP_TRY(h, hipMemcpyAsync(scores_out, h->rows_t.p, (size_t)N * P * 8,
                                 hipMemcpyDeviceToHost, h->stream));
+      if (norm_out) HIP_TRY(h, hipStreamSynchronize(h->stream));  // rows_t is reused below
+    }
+    if (rows && norm_out) {
+      HIP_TRY(h, launch_rows_transpose(h->norm.as<int64_t>(), N, P,
+                                       h->ordered ? h->perm.as<uint32_t>() : nullptr,
+                                       h->rows_t.as<int64_t>(), h->stream));
+      HIP_TRY(h, hipMemcpyAsync(norm_out, h->rows_t.p, (size_t)N * P * 8, hipMemcpyDeviceToHost,
+                                h->stream));
     }
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     if (bitmask_out && W * P > 0) {

@@ -2721,4 +2721,39 @@ hipError_t launch_one(int K, Path path, const unsigned char* nodes, uint32_t n_n
   return hipGetLastError();
 }
 
+// NormalizeScore (scheduler.go:158-183) of the plugin row mode, on the device: for every
+// (node, pod) of rows [N][P] (the raw Score, -1 where Filter failed), over the pod's feasible
+// nodes: highest = max(0, max raw) (init 0, :162), lowest = min raw (init the first score,
+// :163), lowest-- when equal (:173-175), norm = (raw - lowest) * 100 / (highest - lowest) in
+// Go's int64 arithmetic (wrapping multiply, truncating divide, :178).  best / lowest come
+// from the row-mode K2's reduction (same pod order as rows).  -1 where Filter failed.
+__global__ __launch_bounds__(kBlock) void k_norm_rows(const int64_t* __restrict__ rows,
+                                                      uint32_t n_nodes, uint32_t n_pods,
+                                                      const int64_t* __restrict__ best,
+                                                      const int64_t* __restrict__ lowest,
+                                                      int64_t* __restrict__ norm) {
+  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= (uint64_t)n_nodes * n_pods) return;
+  const uint32_t p = (uint32_t)(t % n_pods);
+  const int64_t s = rows[t];
+  if (s < 0) {
+    norm[t] = -1;
+    return;
+  }
+  const int64_t h = best[p] > 0 ? best[p] : 0;
+  int64_t l = lowest[p];
+  if (h == l) --l;
+  norm[t] = (int64_t)((uint64_t)(s - l) * 100u) / (h - l);
+}
+
+hipError_t launch_norm_rows(const int64_t* rows, uint32_t n_nodes, uint32_t n_pods,
+                            const int64_t* best, const int64_t* lowest, int64_t* norm,
+                            hipStream_t s) {
+  const uint64_t total = (uint64_t)n_nodes * n_pods;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_norm_rows, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     s, rows, n_nodes, n_pods, best, lowest, norm);
+  return hipGetLastError();
+}
+
 }  // namespace yoda

@@ -2,6 +2,12 @@
 // plugin (github.com/Mr-LvGJ/Yoda-Scheduler/pkg/yoda).  It is the Go half of the drop-in
 // boundary documented in INTEGRATION.md.
 //
+// cgo pointer rules: libyoda's SoA structs (yoda_node_soa, yoda_pod_soa, yoda_eval_out) hold
+// pointers, so every array they point at lives in C memory (cArrays below), never in the Go
+// heap; a Go pointer is passed to C only directly as an argument, to memory that holds no
+// pointers (output slices of plain numbers).  Runs clean under GODEBUG=cgocheck=1
+// (yodagpu_test.go).
+//
 // NOT COMPILED IN THIS REPOSITORY'S CI: the build image has no Go toolchain.  The C-ABI it
 // calls is exercised from C (tools/capi_example.c) and Python ctypes (yoda_amd/capi.py).
 package yodagpu
@@ -18,6 +24,7 @@ import (
 	"errors"
 	"fmt"
 	"runtime"
+	"strconv"
 	"unsafe"
 
 	scv "github.com/NJUPT-ISL/SCV/api/v1"
@@ -35,12 +42,80 @@ const (
 	ModeDiskIO Mode = C.YODA_MODE_DISKIO
 )
 
+// Status codes of a pod's outcome (include/yoda.h YODA_STATUS_*).
+const (
+	StatusOK            = C.YODA_STATUS_OK
+	StatusUnschedulable = C.YODA_STATUS_UNSCHEDULABLE
+	StatusDivZero       = C.YODA_STATUS_DIV_ZERO
+	StatusScoreRange    = C.YODA_STATUS_SCORE_RANGE
+)
+
+// cArray is a grow-only block of C memory.
+type cArray struct {
+	p unsafe.Pointer
+	n uintptr
+}
+
+func (a *cArray) ensure(bytes uintptr) unsafe.Pointer {
+	if bytes == 0 {
+		bytes = 8
+	}
+	if bytes > a.n {
+		C.free(a.p)
+		a.p = C.calloc(1, C.size_t(bytes))
+		if a.p == nil {
+			panic("yodagpu: out of C memory")
+		}
+		a.n = bytes
+	}
+	return a.p
+}
+
+func (a *cArray) free() {
+	C.free(a.p)
+	a.p, a.n = nil, 0
+}
+
+// Go views of C memory (Go 1.15-compatible: no unsafe.Slice).
+func u64s(a *cArray, n int) []uint64 {
+	return (*[1 << 30]uint64)(a.ensure(uintptr(n) * 8))[:n:n]
+}
+func u32s(a *cArray, n int) []uint32 {
+	return (*[1 << 30]uint32)(a.ensure(uintptr(n) * 4))[:n:n]
+}
+func i64s(a *cArray, n int) []int64 {
+	return (*[1 << 30]int64)(a.ensure(uintptr(n) * 8))[:n:n]
+}
+func i32s(a *cArray, n int) []int32 {
+	return (*[1 << 30]int32)(a.ensure(uintptr(n) * 4))[:n:n]
+}
+func u8s(a *cArray, n int) []uint8 {
+	return (*[1 << 31]uint8)(a.ensure(uintptr(n)))[:n:n]
+}
+func f64s(a *cArray, n int) []float64 {
+	return (*[1 << 30]float64)(a.ensure(uintptr(n) * 8))[:n:n]
+}
+
+// nodeArrays / podArrays: the SoA inputs, in C memory, reused across calls.
+type nodeArrays struct {
+	cardNumber, freeSum, totalSum, alloc, free, total, clock, bw, core, power cArray
+	cardCount, healthy, cpu, disk                                            cArray
+}
+
+type podArrays struct {
+	hasNumber, hasMemory, hasClock, number, memory, clock, priority, rio, rcpu cArray
+	pick, status                                                               cArray
+}
+
 // Handle owns one libyoda handle (one GPU, one node snapshot).  Not safe for concurrent
 // use: the framework calls PreFilter once per pod cycle, cycles are serial.
 type Handle struct {
-	h     *C.yoda_t
-	nodes []string
-	index map[string]int
+	h         *C.yoda_t
+	nodes     []string
+	index     map[string]int
+	zeroTotal []bool // Status.TotalMemorySum == 0 (the reference divides by it when scoring)
+	na        nodeArrays
+	pa        podArrays
 }
 
 func check(h *C.yoda_t, rc C.int, what string) error {
@@ -65,45 +140,19 @@ func New(device int) (*Handle, error) {
 	return g, nil
 }
 
-// Close releases the device memory.
+// Close releases the device memory and the C-side arrays.
 func (g *Handle) Close() {
 	if g.h != nil {
 		C.yoda_destroy(g.h)
 		g.h = nil
 	}
-}
-
-// cArray pins a Go slice for the duration of a call (cgo pointer rules: the C side keeps
-// no reference after returning).
-func u64p(s []uint64) *C.uint64_t {
-	if len(s) == 0 {
-		return nil
+	for _, a := range []*cArray{&g.na.cardNumber, &g.na.freeSum, &g.na.totalSum, &g.na.alloc,
+		&g.na.free, &g.na.total, &g.na.clock, &g.na.bw, &g.na.core, &g.na.power,
+		&g.na.cardCount, &g.na.healthy, &g.na.cpu, &g.na.disk, &g.pa.hasNumber, &g.pa.hasMemory,
+		&g.pa.hasClock, &g.pa.number, &g.pa.memory, &g.pa.clock, &g.pa.priority, &g.pa.rio,
+		&g.pa.rcpu, &g.pa.pick, &g.pa.status} {
+		a.free()
 	}
-	return (*C.uint64_t)(unsafe.Pointer(&s[0]))
-}
-func u32p(s []uint32) *C.uint32_t {
-	if len(s) == 0 {
-		return nil
-	}
-	return (*C.uint32_t)(unsafe.Pointer(&s[0]))
-}
-func u8p(s []uint8) *C.uint8_t {
-	if len(s) == 0 {
-		return nil
-	}
-	return (*C.uint8_t)(unsafe.Pointer(&s[0]))
-}
-func f64p(s []float64) *C.double {
-	if len(s) == 0 {
-		return nil
-	}
-	return (*C.double)(unsafe.Pointer(&s[0]))
-}
-func i64p(s []int64) *C.int64_t {
-	if len(s) == 0 {
-		return nil
-	}
-	return (*C.int64_t)(unsafe.Pointer(&s[0]))
 }
 
 // UploadNodes packs the SCV records (one per node, in the order of `names`) into the
@@ -113,6 +162,12 @@ func i64p(s []int64) *C.int64_t {
 func (g *Handle) UploadNodes(names []string, scvs []*scv.Scv, allocMemory []uint64,
 	cpu, diskIO []float64) error {
 	n := len(scvs)
+	if len(names) != n || (allocMemory != nil && len(allocMemory) != n) {
+		return errors.New("yodagpu: names/allocMemory do not match the SCV list")
+	}
+	if (cpu == nil) != (diskIO == nil) || (cpu != nil && (len(cpu) != n || len(diskIO) != n)) {
+		return errors.New("yodagpu: cpu/diskIO must both be nil or both have one value per node")
+	}
 	k := 1
 	for _, s := range scvs {
 		if len(s.Status.CardList) > k {
@@ -120,24 +175,29 @@ func (g *Handle) UploadNodes(names []string, scvs []*scv.Scv, allocMemory []uint
 		}
 	}
 	if k > C.YODA_MAX_CARDS {
-		return errors.New("more than YODA_MAX_CARDS cards on a node")
+		return errors.New("yodagpu: more than YODA_MAX_CARDS cards on a node")
 	}
-	cardNumber := make([]uint64, n)
-	cardCount := make([]uint32, n)
-	freeSum := make([]uint64, n)
-	totalSum := make([]uint64, n)
-	free := make([]uint64, n*k)
-	total := make([]uint64, n*k)
-	clock := make([]uint64, n*k)
-	bw := make([]uint64, n*k)
-	core := make([]uint64, n*k)
-	power := make([]uint64, n*k)
-	healthy := make([]uint8, n*k)
+	a := &g.na
+	cardNumber, cardCount := u64s(&a.cardNumber, n), u32s(&a.cardCount, n)
+	freeSum, totalSum, alloc := u64s(&a.freeSum, n), u64s(&a.totalSum, n), u64s(&a.alloc, n)
+	free, total, clock := u64s(&a.free, n*k), u64s(&a.total, n*k), u64s(&a.clock, n*k)
+	bw, core, power := u64s(&a.bw, n*k), u64s(&a.core, n*k), u64s(&a.power, n*k)
+	healthy := u8s(&a.healthy, n*k)
+	zero := make([]bool, n)
 	for i, s := range scvs {
 		cardNumber[i] = uint64(s.Status.CardNumber)
 		cardCount[i] = uint32(len(s.Status.CardList))
 		freeSum[i] = s.Status.FreeMemorySum
 		totalSum[i] = s.Status.TotalMemorySum
+		zero[i] = s.Status.TotalMemorySum == 0
+		alloc[i] = 0
+		if allocMemory != nil {
+			alloc[i] = allocMemory[i]
+		}
+		for j := 0; j < k; j++ {
+			o := i*k + j
+			free[o], total[o], clock[o], bw[o], core[o], power[o], healthy[o] = 0, 0, 0, 0, 0, 0, 0
+		}
 		for j, c := range s.Status.CardList {
 			o := i*k + j
 			free[o], total[o] = c.FreeMemory, c.TotalMemory
@@ -150,18 +210,28 @@ func (g *Handle) UploadNodes(names []string, scvs []*scv.Scv, allocMemory []uint
 	}
 	soa := C.yoda_node_soa{
 		n_nodes: C.uint32_t(n), max_cards: C.uint32_t(k),
-		card_number: u64p(cardNumber), card_count: u32p(cardCount),
-		free_memory_sum: u64p(freeSum), total_memory_sum: u64p(totalSum),
-		alloc_memory:     u64p(allocMemory),
-		card_free_memory: u64p(free), card_total_memory: u64p(total),
-		card_clock: u64p(clock), card_bandwidth: u64p(bw), card_core: u64p(core),
-		card_power: u64p(power), card_healthy: u8p(healthy),
-		cpu: f64p(cpu), disk_io: f64p(diskIO),
+		card_number:      (*C.uint64_t)(a.cardNumber.p),
+		card_count:       (*C.uint32_t)(a.cardCount.p),
+		free_memory_sum:  (*C.uint64_t)(a.freeSum.p),
+		total_memory_sum: (*C.uint64_t)(a.totalSum.p),
+		alloc_memory:     (*C.uint64_t)(a.alloc.p),
+		card_free_memory: (*C.uint64_t)(a.free.p), card_total_memory: (*C.uint64_t)(a.total.p),
+		card_clock: (*C.uint64_t)(a.clock.p), card_bandwidth: (*C.uint64_t)(a.bw.p),
+		card_core: (*C.uint64_t)(a.core.p), card_power: (*C.uint64_t)(a.power.p),
+		card_healthy: (*C.uint8_t)(a.healthy.p),
 	}
+	if cpu != nil {
+		copy(f64s(&a.cpu, n), cpu)
+		copy(f64s(&a.disk, n), diskIO)
+		soa.cpu = (*C.double)(a.cpu.p)
+		soa.disk_io = (*C.double)(a.disk.p)
+	}
+	// &soa is a Go pointer to memory holding only C pointers: allowed
 	if err := check(g.h, C.yoda_upload_nodes(g.h, &soa, 0, 0), "yoda_upload_nodes"); err != nil {
 		return err
 	}
 	g.nodes = names
+	g.zeroTotal = zero
 	g.index = make(map[string]int, len(names))
 	for i, name := range names {
 		g.index[name] = i
@@ -169,18 +239,32 @@ func (g *Handle) UploadNodes(names []string, scvs []*scv.Scv, allocMemory []uint
 	return nil
 }
 
-// PackPods parses the scv/* labels and the diskIO annotation with the reference's own
-// helpers (filter.go:60-74, sort.go:12-18, algorithm.go:103-104) into yoda_pod_soa arrays.
-type PodBatch struct {
-	hasNumber, hasMemory, hasClock []uint8
-	number, memory, clock          []uint64
-	priority, rcpu                 []int64
-	rio                            []float64
+// SetNodeState updates the allocated scv/memory (and CardNumber) of a few nodes on the
+// device without re-uploading the snapshot (yoda_set_node_state): the scheduler's assumes
+// and binds between two cycles.  idx are snapshot positions.
+func (g *Handle) SetNodeState(idx []uint32, alloc, cardNumber []uint64) error {
+	if len(idx) != len(alloc) || len(idx) != len(cardNumber) {
+		return errors.New("yodagpu: SetNodeState arrays differ in length")
+	}
+	if len(idx) == 0 {
+		return nil
+	}
+	// plain-number Go slices passed directly as arguments: allowed by the cgo rules
+	rc := C.yoda_set_node_state(g.h, C.uint32_t(len(idx)), (*C.uint32_t)(unsafe.Pointer(&idx[0])),
+		(*C.uint64_t)(unsafe.Pointer(&alloc[0])), (*C.uint64_t)(unsafe.Pointer(&cardNumber[0])))
+	return check(g.h, rc, "yoda_set_node_state")
 }
 
-func PackPods(pods []*v1.Pod) *PodBatch {
-	b := &PodBatch{}
-	for _, p := range pods {
+// packPods parses the scv/* labels and the diskIO annotation with the reference's own
+// helpers (filter.go:60-74, sort.go:12-18, algorithm.go:103-104) into the C-side
+// yoda_pod_soa arrays.
+func (g *Handle) packPods(pods []*v1.Pod) C.yoda_pod_soa {
+	n := len(pods)
+	a := &g.pa
+	hasNumber, hasMemory, hasClock := u8s(&a.hasNumber, n), u8s(&a.hasMemory, n), u8s(&a.hasClock, n)
+	number, memory, clock := u64s(&a.number, n), u64s(&a.memory, n), u64s(&a.clock, n)
+	priority, rcpu, rio := i64s(&a.priority, n), i64s(&a.rcpu, n), f64s(&a.rio, n)
+	for i, p := range pods {
 		l := p.GetLabels()
 		has := func(key string) (uint8, uint64) {
 			if v, ok := l[key]; ok {
@@ -188,32 +272,24 @@ func PackPods(pods []*v1.Pod) *PodBatch {
 			}
 			return 0, 0
 		}
-		hn, n := has("scv/number")
-		hm, m := has("scv/memory")
-		hc, c := has("scv/clock")
-		b.hasNumber, b.number = append(b.hasNumber, hn), append(b.number, n)
-		b.hasMemory, b.memory = append(b.hasMemory, hm), append(b.memory, m)
-		b.hasClock, b.clock = append(b.hasClock, hc), append(b.clock, c)
-		prio := int64(0)
+		hasNumber[i], number[i] = has("scv/number")
+		hasMemory[i], memory[i] = has("scv/memory")
+		hasClock[i], clock[i] = has("scv/clock")
+		priority[i] = 0
 		if v, ok := l["scv/priority"]; ok {
-			pr, _ := strconvAtoi(v)
-			prio = int64(pr)
+			pr, _ := strconv.Atoi(v) // sort.go:14-15 keeps Atoi's value on error
+			priority[i] = int64(pr)
 		}
-		b.priority = append(b.priority, prio)
-		rio, _ := strconvParseFloat32(p.Annotations["diskIO"])
-		b.rio = append(b.rio, rio)
-		b.rcpu = append(b.rcpu, score.CalculatePodResourceRequest(p, v1.ResourceCPU, true))
+		rio[i], _ = strconv.ParseFloat(p.Annotations["diskIO"], 32) // algorithm.go:103
+		rcpu[i] = score.CalculatePodResourceRequest(p, v1.ResourceCPU, true)
 	}
-	return b
-}
-
-func (b *PodBatch) soa() C.yoda_pod_soa {
 	return C.yoda_pod_soa{
-		n_pods:     C.uint32_t(len(b.number)),
-		has_number: u8p(b.hasNumber), number: u64p(b.number),
-		has_memory: u8p(b.hasMemory), memory: u64p(b.memory),
-		has_clock: u8p(b.hasClock), clock: u64p(b.clock),
-		priority: i64p(b.priority), rio: f64p(b.rio), rcpu: i64p(b.rcpu),
+		n_pods:     C.uint32_t(n),
+		has_number: (*C.uint8_t)(a.hasNumber.p), number: (*C.uint64_t)(a.number.p),
+		has_memory: (*C.uint8_t)(a.hasMemory.p), memory: (*C.uint64_t)(a.memory.p),
+		has_clock: (*C.uint8_t)(a.hasClock.p), clock: (*C.uint64_t)(a.clock.p),
+		priority: (*C.int64_t)(a.priority.p), rio: (*C.double)(a.rio.p),
+		rcpu: (*C.int64_t)(a.rcpu.p),
 	}
 }
 
@@ -226,41 +302,44 @@ type Row struct {
 // ScoreRow evaluates ONE pod against every node: the plugin's PreFilter calls it once per
 // scheduling cycle, so Filter and Score become lookups.
 func (g *Handle) ScoreRow(pod *v1.Pod, mode Mode) (*Row, error) {
-	b := PackPods([]*v1.Pod{pod})
-	s := b.soa()
+	s := g.packPods([]*v1.Pod{pod})
 	if err := check(g.h, C.yoda_upload_pods(g.h, &s), "yoda_upload_pods"); err != nil {
 		return nil, err
 	}
 	n := len(g.nodes)
-	row := &Row{Feasible: make([]uint32, (n+31)/32), Score: make([]int64, n)}
-	rc := C.yoda_score_rows(g.h, C.int(mode), u32p(row.Feasible), C.uint64_t(len(row.Feasible)),
-		i64p(row.Score), C.uint64_t(n))
+	row := &Row{Feasible: make([]uint32, (n+31)/32+1), Score: make([]int64, n+1)}
+	rc := C.yoda_score_rows(g.h, C.int(mode), (*C.uint32_t)(unsafe.Pointer(&row.Feasible[0])),
+		C.uint64_t((n+31)/32), (*C.int64_t)(unsafe.Pointer(&row.Score[0])), C.uint64_t(n))
 	if err := check(g.h, rc, "yoda_score_rows"); err != nil {
 		return nil, err
 	}
+	row.Feasible, row.Score = row.Feasible[:(n+31)/32], row.Score[:n]
 	return row, nil
 }
 
 // Batch schedules many pods independently against the snapshot (configs 2-4).  Picks are
 // node indices, -1 unschedulable, -2 error (see statuses).
 func (g *Handle) Batch(pods []*v1.Pod, mode Mode) (picks []int32, statuses []int32, err error) {
-	b := PackPods(pods)
-	s := b.soa()
-	picks = make([]int32, len(pods))
-	statuses = make([]int32, len(pods))
-	out := C.yoda_eval_out{
-		pick:   (*C.int32_t)(unsafe.Pointer(&picks[0])),
-		status: (*C.int32_t)(unsafe.Pointer(&statuses[0])),
+	if len(pods) == 0 {
+		return nil, nil, nil
 	}
-	err = check(g.h, C.yoda_eval(g.h, &s, C.int(mode), &out), "yoda_eval")
-	return
+	s := g.packPods(pods)
+	n := len(pods)
+	pk, st := i32s(&g.pa.pick, n), i32s(&g.pa.status, n)
+	out := C.yoda_eval_out{pick: (*C.int32_t)(g.pa.pick.p), status: (*C.int32_t)(g.pa.status.p)}
+	if err = check(g.h, C.yoda_eval(g.h, &s, C.int(mode), &out), "yoda_eval"); err != nil {
+		return nil, nil, err
+	}
+	return append([]int32(nil), pk...), append([]int32(nil), st...), nil
 }
 
 // Greedy schedules the pods one after another in sort.Less order, each pick updating the
-// node's Allocate score (config 5).
+// node's Allocate score (config 5); cardCapacity also decrements CardNumber.
 func (g *Handle) Greedy(pods []*v1.Pod, mode Mode, cardCapacity bool) ([]int32, error) {
-	b := PackPods(pods)
-	s := b.soa()
+	if len(pods) == 0 {
+		return nil, nil
+	}
+	s := g.packPods(pods)
 	picks := make([]int32, len(pods))
 	flags := C.uint32_t(0)
 	if cardCapacity {
@@ -275,3 +354,10 @@ func (g *Handle) NodeIndex(name string) (int, bool) {
 	i, ok := g.index[name]
 	return i, ok
 }
+
+// ZeroTotal reports whether node i has TotalMemorySum == 0: scoring it divides by zero in
+// the reference (algorithm.go:294,309), a framework Error here.
+func (g *Handle) ZeroTotal(i int) bool { return i >= 0 && i < len(g.zeroTotal) && g.zeroTotal[i] }
+
+// Nodes is the snapshot's node order.
+func (g *Handle) Nodes() []string { return g.nodes }

@@ -45,6 +45,8 @@ _SIGS = {
     "yoda_run": ([_vp, C.c_int, _u32], C.c_int),
     "yoda_download": ([_vp, C.POINTER(CEvalOut)], C.c_int),
     "yoda_download_bitmask": ([_vp, C.POINTER(C.c_uint32), C.c_uint64], C.c_int),
+    "yoda_score_rows_norm": ([_vp, C.c_int, _vp, C.c_uint64, _vp, C.c_uint64, _vp, C.c_uint64],
+                             C.c_int),
     "yoda_score_rows": ([_vp, C.c_int, C.POINTER(C.c_uint32), C.c_uint64,
                          C.POINTER(C.c_int64), C.c_uint64], C.c_int),
     "yoda_shard_phase1": ([_vp, C.c_int, _vp, _vp], C.c_int),
@@ -216,18 +218,25 @@ class Yoda:
             "yoda_download_bitmask")
         return words
 
-    def score_rows(self, mode: int = 0):
+    def score_rows(self, mode: int = 0, norm: bool = False):
         """(feasible bool [P, N], raw Score int64 [P, N] with -1 where Filter fails) for the
-        uploaded pods — the plugin's per-cycle lookups."""
+        uploaded pods — the plugin's per-cycle lookups; norm=True adds the device
+        NormalizeScore [P, N] (yoda_score_rows_norm, -1 where Filter fails)."""
         P, N = self.n_pods, self.n_nodes
         w = (N + 31) // 32
         words = np.zeros((P, w), np.uint32)
         scores = np.zeros((P, N), np.int64)
-        self._check(lib().yoda_score_rows(
-            self._h, mode, words.ctypes.data_as(C.POINTER(C.c_uint32)), words.size,
-            scores.ctypes.data_as(C.POINTER(C.c_int64)), scores.size), "yoda_score_rows")
+        if norm:
+            nrm = np.zeros((P, N), np.int64)
+            self._check(lib().yoda_score_rows_norm(
+                self._h, mode, _np_ptr(words), words.size, _np_ptr(scores), scores.size,
+                _np_ptr(nrm), nrm.size), "yoda_score_rows_norm")
+        else:
+            self._check(lib().yoda_score_rows(
+                self._h, mode, words.ctypes.data_as(C.POINTER(C.c_uint32)), words.size,
+                scores.ctypes.data_as(C.POINTER(C.c_int64)), scores.size), "yoda_score_rows")
         feas = np.unpackbits(words.view(np.uint8), axis=1, bitorder="little")[:, :N].astype(bool)
-        return feas, scores
+        return (feas, scores, nrm) if norm else (feas, scores)
 
     def eval(self, pods: PodSoA, mode: int = 0) -> EvalResult:
         self.upload_pods(pods)

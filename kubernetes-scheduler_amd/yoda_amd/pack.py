@@ -9,10 +9,13 @@ files instead of live Prometheus / API-server reads:
                lowerCamelCase as kubebuilder emits them): status.cardNumber, cardList[{health,
                freeMemory, totalMemory, clock, bandwidth, core, power}], freeMemorySum,
                totalMemorySum
-  advisor      advisor.Result.Info (advisor.go:22-32): {node name: {Cpu, Memory, DiskIO, ...}}
+  advisor      advisor.Result.Info (advisor.go:22-32): {node name: {Cpu, Memory, DiskIO, ...}},
+               built from the five Prometheus query responses by pack_advisor
+               (advisor.go:149-265)
 """
 from __future__ import annotations
 
+import json
 import math
 import re
 from fractions import Fraction
@@ -109,6 +112,114 @@ def pack_pods(pods: Sequence[Mapping]) -> PodSoA:
         out["rio"][i] = parse_float(str(ann.get("diskIO", "")), 32)[0]
         out["rcpu"][i] = pod_cpu_request(pod)
     return PodSoA(**out).normalized()
+
+
+# ---- advisor: Prometheus query responses -> advisor.Result.Info ---------------------------
+def _ci_get(obj, key):
+    """encoding/json field matching: the exact key first, then a case-insensitive one."""
+    if not isinstance(obj, dict):
+        return None
+    if key in obj:
+        return obj[key]
+    low = key.lower()
+    for k, v in obj.items():
+        if isinstance(k, str) and k.lower() == low:
+            return v
+    return None
+
+
+def prometheus_results(body) -> list:
+    """getCpu / getMemory / ... (advisor.go:63-147): `_ = json.Unmarshal(body, &res)` then
+    res.Data.Result.  The unmarshal error is ignored: an invalid body gives no results; a
+    body (str/bytes) or an already-decoded dict is accepted."""
+    if isinstance(body, (bytes, bytearray)):
+        body = body.decode("utf-8", "replace")
+    if isinstance(body, str):
+        try:
+            body = json.loads(body)
+        except ValueError:
+            return []
+    res = _ci_get(_ci_get(body, "Data"), "Result")
+    return res if isinstance(res, list) else []
+
+
+def _metric(r, field: str) -> str:
+    v = _ci_get(_ci_get(r, "Metric"), field)
+    return v if isinstance(v, str) else ""
+
+
+def _value(r) -> float:
+    """strconv.ParseFloat(Value[1].(string), 64); the type assertion panics in Go when the
+    sample is not a string (TypeError here), ParseFloat errors are returned (ValueError)."""
+    val = _ci_get(r, "Value")
+    if not isinstance(val, list) or len(val) < 2:
+        raise IndexError("Value[1]: index out of range")      # a Go panic
+    if not isinstance(val[1], str):
+        raise TypeError("interface conversion: Value[1] is not string")  # a Go panic
+    v, ok = parse_float(val[1], 64)
+    if not ok:
+        raise ValueError(f'strconv.ParseFloat: parsing "{val[1]}"')
+    return v
+
+
+def pack_advisor(cpu, memory, disk_io, net_up=None, net_down=None):
+    """advisor.Result.Init (advisor.go:149-265) restated over the bodies of its five
+    Prometheus queries (cpuQueryL, memoryQueryL, diskIOQueryL, networkIOUpQueryL,
+    networkIODownQueryL, advisor.go:16-20), so a snapshot can be a set of files.  A body of
+    None stands for a failed HTTP query.  Returns (info, err): info maps node name ->
+    {"Cpu", "Memory", "DiskIO", "NetworkIOUp", "NetworkIODown"}, err is the error Init would
+    return (info is then what it had built so far), or None.  The rules Init applies:
+      - names are strings.Trim(kubernetes_io_hostname, " ") (:157);
+      - the CPU query creates the entries; a duplicate CPU name keeps the first (:159-161);
+      - memory rows only update existing names, with no instance fallback (:186-191);
+      - disk and network rows fall back to the instance label when the hostname is empty
+        (:200-202, :225-227, :248-250) and only update existing names (later rows win);
+      - a ParseFloat error in the CPU/memory/disk rows returns it (:163-165, :183, :205);
+        the network queries end Init silently, with no error, on a failed query or a bad
+        value (:217-219, :230-232, :239-241, :253-255)."""
+    info = {}
+    if cpu is None:
+        return info, "cpu query failed"
+    for r in prometheus_results(cpu):
+        name = _metric(r, "kubernetes_io_hostname").strip(" ")
+        if name in info:
+            continue  # "Error! cpu info no exist!": the first entry stays
+        try:
+            v = _value(r)
+        except ValueError as e:
+            return info, str(e)
+        info[name] = {"Cpu": v, "Memory": 0.0, "DiskIO": 0.0, "NetworkIOUp": 0.0,
+                      "NetworkIODown": 0.0}
+    if memory is None:
+        return info, "memory query failed"
+    for r in prometheus_results(memory):
+        name = _metric(r, "kubernetes_io_hostname").strip(" ")
+        if name in info:
+            try:
+                info[name]["Memory"] = _value(r)
+            except ValueError as e:
+                return info, str(e)
+    if disk_io is None:
+        return info, "diskIO query failed"
+    for r in prometheus_results(disk_io):
+        name = _metric(r, "kubernetes_io_hostname").strip(" ") or _metric(r, "instance").strip(" ")
+        if name in info:
+            try:
+                info[name]["DiskIO"] = _value(r)
+            except ValueError as e:
+                return info, str(e)
+    for body, key in ((net_up, "NetworkIOUp"), (net_down, "NetworkIODown")):
+        if body is None:
+            return info, None
+        for r in prometheus_results(body):
+            name = (_metric(r, "kubernetes_io_hostname").strip(" ")
+                    or _metric(r, "instance").strip(" "))
+            if name in info:
+                try:
+                    info[name][key] = _value(r)
+                except ValueError:
+                    return info, None
+    return info, None
 
 
 # ---- nodes ---------------------------------------------------------------------------------

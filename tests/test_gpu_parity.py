@@ -411,6 +411,33 @@ def test_score_rows_match_oracle(dev, mode, path):
     assert_same(dev.download(), want, mode)
 
 
+@pytest.mark.parametrize("mode", [MODE_SCV, MODE_DISKIO])
+@pytest.mark.parametrize("path", ["n32", "f64", "u64"])
+def test_normalized_rows_match_oracle(dev, mode, path):
+    """yoda_score_rows_norm: the device NormalizeScore (scheduler.go:158-183) of every node
+    equals the oracle's (oracle_pod_detail norm), -1 where Filter fails.  Includes a pod with
+    a single feasible node (highest == lowest: lowest--), one with none, and zero-total
+    nodes (their raw score has no Allocate/Actual term in both)."""
+    nodes, pods = synth.make_config(2, pods=40, nodes=900)
+    nodes.total_memory_sum[3] = 0
+    nodes.card_number[5] = 16                       # the only node with 16 cards
+    pods.has_number[0], pods.number[0] = 1, 16
+    pods.has_memory[0] = pods.has_clock[0] = 0
+    pods.has_number[1], pods.number[1] = 1, 17      # no feasible node
+    nodes, pods = nodes.normalized(), pods.normalized()
+    dev.upload_nodes(nodes, force_f64=path == "f64", force_generic=path == "u64")
+    dev.upload_pods(pods)
+    feas, rows, norm = dev.score_rows(mode, norm=True)
+    for p in range(pods.n_pods):
+        _, f, raw, nrm = oracle.pod_detail(nodes, pods, p, mode)
+        np.testing.assert_array_equal(feas[p], f)
+        np.testing.assert_array_equal(norm[p], nrm, err_msg=f"pod {p}")
+        np.testing.assert_array_equal(rows[p][f], raw[f], err_msg=f"pod {p}")
+    if mode == MODE_SCV:
+        assert feas[0].sum() == 1 and norm[0][5] == 100 and feas[1].sum() == 0
+    assert ((norm[feas] >= 0) & (norm[feas] <= 100)).all()
+
+
 def test_plugin_over_libyoda(dev):
     from yoda_amd.pack import pods_to_dicts
     from yoda_amd.plugin import YodaPlugin, schedule_one

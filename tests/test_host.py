@@ -1,6 +1,7 @@
 """Host side (CPU): Go strconv semantics, k8s quantities, the SCV / pod / advisor packers
 and the plugin mirror (yoda_amd/plugin.py) driven by an oracle-backed row backend."""
 import math
+import os
 import random
 
 import numpy as np
@@ -236,3 +237,66 @@ def test_less_and_status():
     lo = {"metadata": {"labels": {}}}
     assert YodaPlugin.less(hi, lo) and not YodaPlugin.less(lo, hi)
     assert Status().is_success()
+
+
+# ---- advisor ingestion (advisor.go:149-265) ---------------------------------------------
+ADV = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "advisor")
+
+
+def _adv(name):
+    return open(os.path.join(ADV, name + ".json")).read()
+
+
+def test_pack_advisor_fixtures():
+    """The five query responses -> Result.Info, against the hand-derived expectation:
+    trimmed hostnames, first CPU entry wins, instance fallback for disk/network only, orphan
+    rows dropped, later disk rows win, a bad network value ends Init without an error."""
+    import json
+    from yoda_amd.pack import pack_advisor
+    info, err = pack_advisor(_adv("cpu"), _adv("memory"), _adv("diskio"), _adv("net_up"),
+                             _adv("net_down"))
+    want = json.load(open(os.path.join(ADV, "expected.json")))
+    assert err is None and info == want["info"]
+
+
+def test_pack_advisor_errors():
+    from yoda_amd.pack import pack_advisor
+    body = lambda rows: {"data": {"result": [{"metric": {"kubernetes_io_hostname": n},  # noqa: E731
+                                              "value": [0, v]} for n, v in rows]}}
+    info, err = pack_advisor(None, "{}", "{}")
+    assert info == {} and err                                   # failed CPU query
+    info, err = pack_advisor(body([("a", "1"), ("b", "x")]), "{}", "{}")
+    assert list(info) == ["a"] and "ParseFloat" in err          # partial result + the error
+    info, err = pack_advisor(body([("a", "1")]), body([("a", "1e999")]), "{}")
+    assert err and info["a"]["Memory"] == 0.0                   # range error is an error too
+    info, err = pack_advisor("not json", "{}", "{}")
+    assert info == {} and err is None                           # Unmarshal error ignored
+    info, err = pack_advisor(body([("a", "2")]), "{}", "{}", None)
+    assert err is None and info["a"]["Cpu"] == 2.0              # failed network query: no error
+    with pytest.raises(TypeError):                              # Value[1].(string) panics
+        pack_advisor({"data": {"result": [{"metric": {"kubernetes_io_hostname": "a"},
+                                           "value": [0, 1.5]}]}}, "{}", "{}")
+    # encoding/json matches keys case-insensitively
+    info, _ = pack_advisor({"Data": {"Result": [{"Metric": {"KUBERNETES_IO_HOSTNAME": "a"},
+                                                 "Value": [0, "3"]}]}}, "{}", "{}")
+    assert info["a"]["Cpu"] == 3.0
+
+
+def test_advisor_feeds_mode_b():
+    """Advisor metrics -> pack_scvs -> Mode B (BalancedCpuDiskIOPriority, algorithm.go:99-119)
+    for example/test-pod.yaml (Rcpu 100, Rio 10): scores 5, 9, 0, 2 (SURVEY §8c KAT 2 form)."""
+    from yoda_amd.pack import pack_advisor
+    info, err = pack_advisor(_adv("cpu"), _adv("memory"), _adv("diskio"), _adv("net_up"),
+                             _adv("net_down"))
+    nodes = synth.make_nodes(4, seed=3)
+    scvs = scvs_from_soa(nodes)
+    for s, name in zip(scvs, ["node-a", "node-b", "node-c", "node-d"]):
+        s["metadata"]["name"] = name
+    soa = pack_scvs(scvs, advisor=info)
+    np.testing.assert_array_equal(soa.cpu, [50.0, 5.25, 120.0, 0.0])
+    np.testing.assert_array_equal(soa.disk_io, [12.5, 0.5, 0.0, 400.0])
+    pods = pack_pods([TEST_POD])
+    for n, want in enumerate([5, 9, 0, 2]):
+        _, _, raw, _ = oracle.pod_detail(soa, pods, 0, MODE_DISKIO)
+        assert raw[n] == want, (n, raw)
+    assert oracle.schedule(soa, pods, MODE_DISKIO).pick[0] == 1
