@@ -5,10 +5,14 @@ files instead of live Prometheus / API-server reads:
 
   pod          k8s core/v1 Pod: metadata.labels scv/number|memory|clock|priority,
                metadata.annotations diskIO, spec.containers/initContainers/overhead cpu
-  scv          NJUPT-ISL/SCV api/v1 Scv (go.mod:6, not vendored — JSON field names assumed
-               lowerCamelCase as kubebuilder emits them): status.cardNumber, cardList[{health,
-               freeMemory, totalMemory, clock, bandwidth, core, power}], freeMemorySum,
-               totalMemorySum
+  scv          NJUPT-ISL/SCV api/v1 Scv (go.mod:6, not vendored).  The Go field names are
+               pinned by the reference's use (Status.CardNumber, CardList[].{Health,
+               FreeMemory, TotalMemory, Clock, Bandwidth, Core, Power}, FreeMemorySum,
+               TotalMemorySum: filter.go:13-57, collection.go:45-75, algorithm.go:294-309);
+               their JSON tags are not in the container, so keys are matched as Go's
+               encoding/json matches them: exact first, then case-insensitively -- the
+               kubebuilder lowerCamelCase tags (cardList, freeMemory, ...) and the field names
+               both decode
   advisor      advisor.Result.Info (advisor.go:22-32): {node name: {Cpu, Memory, DiskIO, ...}},
                built from the five Prometheus query responses by pack_advisor
                (advisor.go:149-265)
@@ -243,7 +247,8 @@ def pack_scvs(scvs: Sequence[Mapping], bound_pods: Iterable[Mapping] = (),
     node name -> advisor.NodeInfo fields {"Cpu", "DiskIO", ...}; a node missing from it
     makes the reference panic (algorithm.go:70,73), so it is an error here."""
     names = [(s.get("metadata", {}) or {}).get("name", str(i)) for i, s in enumerate(scvs)]
-    cards = [((s.get("status", {}) or {}).get("cardList") or []) for s in scvs]
+    status = [(_ci_get(s, "status") or {}) for s in scvs]
+    cards = [(_ci_get(st, "cardList") or []) for st in status]
     k = max_cards or max([len(c) for c in cards] + [1])
     if k > MAX_CARDS or any(len(c) > k for c in cards):
         raise ValueError(f"more than {min(k, MAX_CARDS)} cards on a node")
@@ -251,16 +256,17 @@ def pack_scvs(scvs: Sequence[Mapping], bound_pods: Iterable[Mapping] = (),
     z = lambda dt: np.zeros((N, k), dt)  # noqa: E731
     f, t, ck, bw, co, pw, h = (z(np.uint64), z(np.uint64), z(np.uint64), z(np.uint64),
                                z(np.uint64), z(np.uint64), z(np.uint8))
+    num = lambda obj, key: int(_ci_get(obj, key) or 0)  # noqa: E731
     for i, cl in enumerate(cards):
         for j, c in enumerate(cl):
-            f[i, j] = int(c.get("freeMemory", 0))
-            t[i, j] = int(c.get("totalMemory", 0))
-            ck[i, j] = int(c.get("clock", 0))
-            bw[i, j] = int(c.get("bandwidth", 0))
-            co[i, j] = int(c.get("core", 0))
-            pw[i, j] = int(c.get("power", 0))
-            h[i, j] = c.get("health") == "Healthy"   # filter.go:53,57
-    st = [(s.get("status", {}) or {}) for s in scvs]
+            f[i, j] = num(c, "freeMemory")
+            t[i, j] = num(c, "totalMemory")
+            ck[i, j] = num(c, "clock")
+            bw[i, j] = num(c, "bandwidth")
+            co[i, j] = num(c, "core")
+            pw[i, j] = num(c, "power")
+            h[i, j] = _ci_get(c, "health") == "Healthy"   # filter.go:53,57
+    st = status
     cpu = np.zeros(N)
     disk = np.zeros(N)
     if advisor is not None:
@@ -270,10 +276,10 @@ def pack_scvs(scvs: Sequence[Mapping], bound_pods: Iterable[Mapping] = (),
             cpu[i] = float(advisor[n].get("Cpu", 0.0))
             disk[i] = float(advisor[n].get("DiskIO", 0.0))
     return NodeSoA(
-        card_number=np.array([int(x.get("cardNumber", 0)) for x in st], np.uint64),
+        card_number=np.array([num(x, "cardNumber") for x in st], np.uint64),
         card_count=np.array([len(c) for c in cards], np.uint32),
-        free_memory_sum=np.array([int(x.get("freeMemorySum", 0)) for x in st], np.uint64),
-        total_memory_sum=np.array([int(x.get("totalMemorySum", 0)) for x in st], np.uint64),
+        free_memory_sum=np.array([num(x, "freeMemorySum") for x in st], np.uint64),
+        total_memory_sum=np.array([num(x, "totalMemorySum") for x in st], np.uint64),
         alloc_memory=node_alloc_memory(names, bound_pods),
         card_free_memory=f, card_total_memory=t, card_clock=ck, card_bandwidth=bw,
         card_core=co, card_power=pw, card_healthy=h, cpu=cpu, disk_io=disk).normalized()

@@ -300,3 +300,19 @@ def test_advisor_feeds_mode_b():
         _, _, raw, _ = oracle.pod_detail(soa, pods, 0, MODE_DISKIO)
         assert raw[n] == want, (n, raw)
     assert oracle.schedule(soa, pods, MODE_DISKIO).pick[0] == 1
+
+
+def test_pack_scvs_go_json_key_matching():
+    """SCV keys decode as encoding/json would: lowerCamelCase tags and Go field names alike."""
+    camel = {"metadata": {"name": "n0"}, "status": {"cardNumber": 2, "freeMemorySum": 7,
+             "totalMemorySum": 9, "cardList": [{"health": "Healthy", "freeMemory": 3,
+                                                "totalMemory": 4, "clock": 1500, "bandwidth": 900,
+                                                "core": 80, "power": 300}]}}
+    pascal = {"metadata": {"name": "n1"}, "Status": {"CardNumber": 2, "FreeMemorySum": 7,
+              "TotalMemorySum": 9, "CardList": [{"Health": "Healthy", "FreeMemory": 3,
+                                                 "TotalMemory": 4, "Clock": 1500,
+                                                 "Bandwidth": 900, "Core": 80, "Power": 300}]}}
+    a, b = pack_scvs([camel]), pack_scvs([pascal])
+    for f in a.__dataclass_fields__:
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+    assert a.card_healthy[0, 0] == 1 and a.card_clock[0, 0] == 1500 and a.card_number[0] == 2
