@@ -410,6 +410,10 @@ def main():
                          "(yoda_amd/dist.py); pods = each rank evaluates a pod slice against "
                          "the whole node snapshot, no collective (dist.pod_partition; slower "
                          "per rank on one MI355X, profiles/r01/current/shard_timing.txt)")
+    ap.add_argument("--exchange", choices=["torch", "libyoda"], default="torch",
+                    help="--shard nodes: torch = RCCL all-reduces through torch.distributed "
+                         "(yoda_amd/dist.py ShardExchange, 5 collectives per step); libyoda = "
+                         "libyoda's own RCCL exchanges (yoda_comm_run, 2 collectives per step)")
     ap.add_argument("--no-balance", action="store_true",
                     help="--shard nodes: keep equal node blocks (default: re-cut them once "
                          "after warm-up so every rank's measured K1 + K2 time is equal)")
@@ -469,8 +473,14 @@ def main():
     k_slots = int(nodes.card_count.max()) if N else 1
     k_slots = 1 << max(0, (k_slots - 1).bit_length())
 
+    def make_exchange():
+        if args.exchange == "libyoda":
+            from yoda_amd.dist import LibExchange
+            return LibExchange(y, device, shard=shard, offset=lo)
+        return ShardExchange.distributed(y, device, shard=shard, offset=lo)
+
     if world > 1 and not pod_shard:
-        ex = ShardExchange.distributed(y, device, shard=shard, offset=lo)
+        ex = make_exchange()
         step = lambda: ex.step(mode)  # noqa: E731
     else:
         step = lambda: y.run(mode)  # noqa: E731
@@ -506,7 +516,7 @@ def main():
             lo, hi = int(b[rank]), int(b[rank + 1])
             shard = nodes.slice(lo, hi)
             y.upload_nodes(shard, node_offset=lo)
-            ex = ShardExchange.distributed(y, device, shard=shard, offset=lo)
+            ex = make_exchange()
             step = lambda: ex.step(mode)  # noqa: E731
             for _ in range(max(args.warmup, 1)):
                 step()
@@ -572,8 +582,10 @@ def main():
                    "path": y.path,
                    "parallelism": (f"pod-shard x{world} (whole node snapshot per GPU, "
                                    "no collective)" if pod_shard else
-                                   f"node-shard x{world}" + (" (RCCL all-reduce merge)"
-                                                            if world > 1 else "")),
+                                   f"node-shard x{world}" + (
+                                       (" (RCCL inside libyoda: all-reduce + all-gather)"
+                                        if args.exchange == "libyoda" else
+                                        " (RCCL all-reduce merge)") if world > 1 else "")),
                    "node_bounds": [int(v) for v in b] if world > 1 and not pod_shard
                    else None},
         # dominant kernel K2: its algorithmic (unique) bytes per launch / its HIP-event launch

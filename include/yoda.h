@@ -219,6 +219,23 @@ int yoda_shard_finalize(yoda_t* h, int mode, const uint32_t* d_counts, const int
  * the exact normalize (scheduler.go:176-179).  Returns the number of such pods in *n_pods. */
 int yoda_shard_overflow_count(yoda_t* h, uint32_t* n_pods);
 
+/* ---- multi-GPU without a host framework: RCCL inside libyoda ------------------------
+ * For callers that have no torch.distributed (the Go plugin through cgo, C).  One handle per
+ * GPU holds a node shard (yoda_upload_nodes with its node_offset) and the same pod batch.
+ * Rank 0 calls yoda_comm_unique_id and hands the id to the other ranks out of band (a file,
+ * the k8s API, MPI ...); every rank then calls yoda_comm_init (collective).  yoda_comm_run is
+ * one whole sharded step on the handle's stream -- phase 1, ONE all-reduce(MAX) of the maxima
+ * with the per-rank count slots, phase 2, ONE all-gather of the per-shard (best, index, ties,
+ * lowest) records, the merge, finalize -- and leaves the picks for yoda_download, like
+ * yoda_run.  librccl.so.1 is opened at the first call (not a link dependency).
+ * yoda_comm_run_local runs the same step for `world` shard handles of ONE process on one
+ * device, with device copies as the transport (tests, single-process use). */
+#define YODA_COMM_ID_BYTES 128
+int yoda_comm_unique_id(uint8_t* id);
+int yoda_comm_init(yoda_t* h, const uint8_t* id, int rank, int world);
+int yoda_comm_run(yoda_t* h, int mode);
+int yoda_comm_run_local(yoda_t* const* handles, int world, int mode);
+
 /* ---- batch ordering ---------------------------------------------------------------- */
 /* Mode A runs of more than 128 pods (yoda_run, yoda_score_rows, yoda_shard_phase1) sort the
  * batch on the device by the Filter's inputs so that whole wavefronts skip infeasible nodes;

@@ -3,7 +3,9 @@
 // Packs the node snapshot and pod requests into the device layout of yoda_layout.h, picks
 // the exact-f64 fast path or the exact-u64 generic path, and sequences the kernels of
 // yoda_kernels.hip on the handle's stream.  No exception crosses the C boundary.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: librccl is opened at yoda_comm_init (dlopen)
 
 #include <algorithm>
 #include <chrono>
@@ -72,15 +74,16 @@ hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t
                           const double* rcp, const float* rcp32, uint32_t n_pods,
                           const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
                           uint32_t bs_stride, const Partials& part,
-                          double* tk_s, uint32_t* tk_i, hipStream_t s);
+                          double* tk_s, uint32_t* tk_i, int tk, hipStream_t s);
 hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t C,
                              uint32_t n_pods, uint32_t node_offset, double* out_s,
-                             uint32_t* out_i, hipStream_t s);
+                             uint32_t* out_i, int tk, hipStream_t s);
 hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32_t* node,
                              const uint64_t* value, const uint64_t* card_number, uint32_t count,
                              unsigned char* sum, uint32_t sum_stride, unsigned char* sum2,
                              uint32_t sum2_stride, hipStream_t s);
 int topk_k();
+int topk_k_capacity();
 uint32_t greedy_one_blocks();
 hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                              const PodParams& pp, const double* rcp, const float* rcp32,
@@ -103,6 +106,16 @@ hipError_t launch_one(int K, Path path, const unsigned char* nodes, uint32_t n_n
                       OneOut* out, hipStream_t s);
 hipError_t launch_norm_rows(const int64_t* rows, uint32_t n_nodes, uint32_t n_pods,
                             const int64_t* best, const int64_t* lowest, int64_t* norm,
+                            hipStream_t s);
+hipError_t launch_slot_counts(const uint32_t* counts, uint32_t n_pods, uint32_t rank,
+                              uint32_t world, uint64_t* slots, hipStream_t s);
+hipError_t launch_unslot_counts(const uint64_t* slots, uint32_t n_pods, uint32_t world,
+                                uint32_t* counts, hipStream_t s);
+hipError_t launch_pack_rec(const int64_t* best, const uint32_t* idx, const uint32_t* ties,
+                           const int64_t* low, uint32_t n_pods, ShardRec* rec, hipStream_t s);
+hipError_t launch_merge_rec(const ShardRec* all, uint32_t n_pods, uint32_t world, int64_t* best,
+                            uint32_t* idx, uint32_t* ties, int64_t* low, hipStream_t s);
+hipError_t launch_max_multi(const PtrList& src, uint32_t k, uint64_t n, uint64_t* dst,
                             hipStream_t s);
 size_t order_scratch_bytes(uint32_t n_pods);
 hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
@@ -166,6 +179,49 @@ struct PinnedBuf {
     bytes = 0;
   }
 };
+
+// RCCL entry points, resolved at the first yoda_comm_* call: libyoda itself does not link
+// RCCL (a process that already loaded one -- e.g. PyTorch's, same SONAME -- shares it).
+struct RcclApi {
+  bool tried = false, ok = false;
+  std::string err;
+  ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                             hipStream_t) = nullptr;
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t,
+                             hipStream_t) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
+  bool load() {
+    if (tried) return ok;
+    tried = true;
+    void* so = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!so) so = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!so) {
+      err = std::string("librccl.so.1 not found: ") + dlerror();
+      return false;
+    }
+    auto sym = [&](const char* name) {
+      void* f = dlsym(so, name);
+      if (!f) err = std::string("librccl: missing ") + name;
+      return f;
+    };
+    get_unique_id = reinterpret_cast<decltype(get_unique_id)>(sym("ncclGetUniqueId"));
+    comm_init_rank = reinterpret_cast<decltype(comm_init_rank)>(sym("ncclCommInitRank"));
+    all_reduce = reinterpret_cast<decltype(all_reduce)>(sym("ncclAllReduce"));
+    all_gather = reinterpret_cast<decltype(all_gather)>(sym("ncclAllGather"));
+    comm_destroy = reinterpret_cast<decltype(comm_destroy)>(sym("ncclCommDestroy"));
+    error_string = reinterpret_cast<decltype(error_string)>(sym("ncclGetErrorString"));
+    ok = get_unique_id && comm_init_rank && all_reduce && all_gather && comm_destroy &&
+         error_string;
+    return ok;
+  }
+};
+RcclApi& rccl() {
+  static RcclApi a;
+  return a;
+}
 
 enum PodArray {
   kPodMF, kPodCF, kPodMU, kPodCU, kPodNumber, kPodAlpha, kPodBeta,
@@ -253,6 +309,10 @@ struct yoda_handle {
   unsigned long long* stats_ptr() const {
     return class_stats ? stats_dev.as<unsigned long long>() : nullptr;
   }
+  // yoda_comm_*: this rank's RCCL communicator and the two exchange buffers of a step
+  ncclComm_t comm = nullptr;
+  int comm_rank = 0, comm_world = 1;
+  DevBuf ex1, rec, rec_all;  // [maxima 6P | count slots world x P] u64; ShardRec [P], [world][P]
   // profiling: event pairs around K1 / K2
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
@@ -269,6 +329,7 @@ struct yoda_handle {
   }
 
   ~yoda_handle() {
+    if (comm && rccl().ok) (void)rccl().comm_destroy(comm);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &pod_blob,   &maxima,       &counts,
                      &pod_sorted, &perm,     &order_scratch,
@@ -280,6 +341,7 @@ struct yoda_handle {
                      &p_best_f,  &p_best_i,  &p_idx,      &p_ties,       &p_low_f,
                      &p_low_i,   &p_err,     &pick_alt,   &status_alt,   &ties_out_alt,
                      &p_wit,     &wit,       &stats_dev, &one_feas,  &one_part,  &one_done,
+                     &ex1,       &rec,       &rec_all,
                      &one_out,
                      &counts_alt, &best_alt, &maxima_alt};
     for (DevBuf* b : all) b->release();
@@ -1674,10 +1736,10 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
                                     h->rcp32.as<float>(), wn, h->bitmask.as<uint64_t>(),
                                     bm_row(N), h->bs_ptr(), bs_row(N),
                                     partials(h), h->tk_s_part.as<double>(),
-                                    h->tk_i_part.as<uint32_t>(), h->stream));
+                                    h->tk_i_part.as<uint32_t>(), (int)KT, h->stream));
           HIP_TRY(h, launch_topk_merge(h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),
                                        h->C2, wn, h->node_offset, h->tk_s.as<double>(),
-                                       h->tk_i.as<uint32_t>(), h->stream));
+                                       h->tk_i.as<uint32_t>(), (int)KT, h->stream));
           HIP_TRY(h, hipMemcpyAsync(counts.data(), h->counts.p, 2ull * wn * 4,
                                     hipMemcpyDeviceToHost, h->stream));
           HIP_TRY(h, hipMemcpyAsync(ts.data(), h->tk_s.p, (size_t)KT * wn * 8,
@@ -1919,10 +1981,10 @@ int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_count
                                 pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(), P,
                                 h->bitmask.as<uint64_t>(), bm_row(N), h->bs_ptr(), bs_row(N),
                                 partials(h), h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),
-                                h->stream));
+                                (int)KT, h->stream));
       HIP_TRY(h, launch_topk_merge(h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(), h->C2,
                                    P, h->node_offset, h->tk_s.as<double>(),
-                                   h->tk_i.as<uint32_t>(), h->stream));
+                                   h->tk_i.as<uint32_t>(), (int)KT, h->stream));
       HIP_TRY(h, hipMemcpyAsync(ts.data(), h->tk_s.p, (size_t)KT * P * 8, hipMemcpyDeviceToHost,
                                 h->stream));
       HIP_TRY(h, hipMemcpyAsync(ti.data(), h->tk_i.p, (size_t)KT * P * 4, hipMemcpyDeviceToHost,
@@ -2586,7 +2648,7 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
   auto ms_since = [](Clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
   };
-  const uint32_t P = pods->n_pods, N = h->n_nodes, KT = (uint32_t)topk_k();
+  const uint32_t P = pods->n_pods, N = h->n_nodes, KT = (uint32_t)topk_k_capacity();
   yoda_node_soa nv{};
   nv.n_nodes = N;
   nv.max_cards = 1;
@@ -2677,10 +2739,11 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
       HIP_TRY(h, launch_k2_topk(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk2, h->C2,
                                 pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(), wn,
                                 h->bitmask.as<uint64_t>(), bm_row(N), nullptr, 0, partials(h),
-                                h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),
+                                h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(), (int)KT,
                                 h->stream));
       HIP_TRY(h, launch_topk_merge(h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(), h->C2,
-                                   wn, 0, h->tk_s.as<double>(), h->tk_i.as<uint32_t>(), h->stream));
+                                   wn, 0, h->tk_s.as<double>(), h->tk_i.as<uint32_t>(), (int)KT,
+                                   h->stream));
       HIP_TRY(h, hipMemcpyAsync(st + o_ts, h->tk_s.p, 8 * (size_t)KT * wn, hipMemcpyDeviceToHost,
                                 h->stream));
       HIP_TRY(h, hipMemcpyAsync(st + o_ti, h->tk_i.p, 4 * (size_t)KT * wn, hipMemcpyDeviceToHost,
@@ -2790,3 +2853,163 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
   h->ran = false;
   return YODA_OK;
 }
+
+// ---- multi-GPU step inside libyoda (RCCL, no torch) ---------------------------------------
+// One node shard per handle; a step is the sharded evaluation of yoda_shard_* with the
+// exchanges done here, two collectives per step:
+//   1. all-reduce(MAX, u64) over [maxima 6P | count slots world x P] -- the maxima of
+//      CollectMaxValues are a reduction over all nodes; the counts ride along as one slot per
+//      rank (an all-gather inside the MAX), summed after;
+//   2. all-gather of each shard's ShardRec [P] (best, lowest index reaching it, ties, lowest),
+//      folded per pod by k_merge_rec.
+// `hs` are the shards this process drives: one handle with an RCCL communicator
+// (yoda_comm_run), or every shard of the batch on one device with device copies as the
+// transport (yoda_comm_run_local, for tests and single-process use).
+static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local) {
+  yoda_t* h0 = hs[0];
+  const uint32_t P = h0->n_pods;
+  for (int i = 0; i < n; ++i) {
+    yoda_t* h = hs[i];
+    if (h->n_pods != P) return fail(h0, YODA_ERR_INVALID_ARG, "shards hold different batches");
+    int rc = prepare_run(h, mode);
+    if (rc) return rc;
+    if ((rc = order_pods(h, mode))) return rc;
+    HIP_TRY(h, h->ex1.ensure((6 + (size_t)world) * std::max<uint32_t>(P, 1) * 8));
+    HIP_TRY(h, h->rec.ensure((size_t)std::max<uint32_t>(P, 1) * sizeof(ShardRec)));
+    HIP_TRY(h, h->rec_all.ensure((size_t)world * std::max<uint32_t>(P, 1) * sizeof(ShardRec)));
+    if (P == 0) continue;
+    uint64_t* ex = h->ex1.as<uint64_t>();
+    if ((rc = phase1(h, mode, ex, h->counts.as<uint32_t>()))) return rc;
+    HIP_TRY(h, launch_slot_counts(h->counts.as<uint32_t>(), P, local ? (uint32_t)i
+                                                                      : (uint32_t)h->comm_rank,
+                                  (uint32_t)world, ex + 6 * (size_t)P, h->stream));
+  }
+  if (P == 0) {
+    for (int i = 0; i < n; ++i) hs[i]->ran = true;
+    return YODA_OK;
+  }
+  const size_t n1 = (6 + (size_t)world) * P;
+  if (local) {  // exchange 1: elementwise MAX over the shards, back to each
+    PtrList l{};
+    for (int i = 0; i < n; ++i) l.p[i] = hs[i]->ex1.p;
+    HIP_TRY(h0, launch_max_multi(l, (uint32_t)n, n1, h0->ex1.as<uint64_t>(), h0->stream));
+    for (int i = 1; i < n; ++i)
+      HIP_TRY(h0, hipMemcpyAsync(hs[i]->ex1.p, h0->ex1.p, n1 * 8, hipMemcpyDeviceToDevice,
+                                 h0->stream));
+  } else {
+    const ncclResult_t r = rccl().all_reduce(h0->ex1.p, h0->ex1.p, n1, ncclUint64, ncclMax,
+                                             h0->comm, h0->stream);
+    if (r != ncclSuccess)
+      return fail(h0, YODA_ERR_HIP, std::string("ncclAllReduce: ") + rccl().error_string(r));
+  }
+  for (int i = 0; i < n; ++i) {
+    yoda_t* h = hs[i];
+    uint64_t* ex = h->ex1.as<uint64_t>();
+    HIP_TRY(h, launch_unslot_counts(ex + 6 * (size_t)P, P, (uint32_t)world,
+                                    h->counts.as<uint32_t>(), h->stream));
+    HIP_TRY(h, hipMemcpyAsync(h->maxima.p, ex, 6 * (size_t)P * 8, hipMemcpyDeviceToDevice,
+                              h->stream));
+    int rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->best.as<int64_t>(),
+                    h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>());
+    if (rc) return rc;
+    HIP_TRY(h, launch_pack_rec(h->best.as<int64_t>(), h->idx.as<uint32_t>(),
+                               h->ties.as<uint32_t>(), h->lowest.as<int64_t>(), P,
+                               h->rec.as<ShardRec>(), h->stream));
+  }
+  const size_t rb = (size_t)P * sizeof(ShardRec);
+  if (local) {  // exchange 2: every shard's records to every shard
+    for (int r = 0; r < n; ++r)
+      for (int i = 0; i < n; ++i)
+        HIP_TRY(h0, hipMemcpyAsync(hs[i]->rec_all.as<unsigned char>() + r * rb, hs[r]->rec.p, rb,
+                                   hipMemcpyDeviceToDevice, h0->stream));
+  } else {
+    const ncclResult_t r = rccl().all_gather(h0->rec.p, h0->rec_all.p, rb / 8, ncclUint64,
+                                             h0->comm, h0->stream);
+    if (r != ncclSuccess)
+      return fail(h0, YODA_ERR_HIP, std::string("ncclAllGather: ") + rccl().error_string(r));
+  }
+  for (int i = 0; i < n; ++i) {
+    yoda_t* h = hs[i];
+    HIP_TRY(h, launch_merge_rec(h->rec_all.as<ShardRec>(), P, (uint32_t)world,
+                                h->best.as<int64_t>(), h->idx.as<uint32_t>(),
+                                h->ties.as<uint32_t>(), h->lowest.as<int64_t>(), h->stream));
+    int rc = finalize(h, mode, h->counts.as<uint32_t>(), h->best.as<int64_t>(),
+                      h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(),
+                      true);
+    if (rc) return rc;
+    h->ran = true;
+    h->ran_bitmask = false;
+    h->last_mode = mode;
+  }
+  return YODA_OK;
+}
+
+extern "C" {
+
+int yoda_comm_unique_id(uint8_t* id) {
+  if (!id) return YODA_ERR_INVALID_ARG;
+  if (!rccl().load()) return YODA_ERR_HIP;
+  ncclUniqueId u;
+  if (rccl().get_unique_id(&u) != ncclSuccess) return YODA_ERR_HIP;
+  std::memcpy(id, &u, sizeof(u));
+  return YODA_OK;
+}
+
+int yoda_comm_init(yoda_t* h, const uint8_t* id, int rank, int world) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  if (!id || world < 1 || rank < 0 || rank >= world)
+    return fail(h, YODA_ERR_INVALID_ARG, "bad communicator id / rank / world");
+  if (!rccl().load()) return fail(h, YODA_ERR_HIP, rccl().err);
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (h->comm) {
+    (void)rccl().comm_destroy(h->comm);
+    h->comm = nullptr;
+  }
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  const ncclResult_t r = rccl().comm_init_rank(&h->comm, world, u, rank);
+  if (r != ncclSuccess) {
+    h->comm = nullptr;
+    return fail(h, YODA_ERR_HIP, std::string("ncclCommInitRank: ") + rccl().error_string(r));
+  }
+  h->comm_rank = rank;
+  h->comm_world = world;
+  return YODA_OK;
+}
+
+int yoda_comm_run(yoda_t* h, int mode) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  if (!h->comm) return fail(h, YODA_ERR_STATE, "yoda_comm_run before yoda_comm_init");
+  try {
+    yoda_t* hs[1] = {h};
+    return comm_step(hs, 1, h->comm_world, mode, false);
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
+int yoda_comm_run_local(yoda_t* const* hs, int world, int mode) {
+  if (!hs || world < 1 || world > kMaxLocalShards) return YODA_ERR_INVALID_ARG;
+  for (int i = 0; i < world; ++i)
+    if (!hs[i]) return YODA_ERR_INVALID_ARG;
+  for (int i = 1; i < world; ++i)
+    if (hs[i]->device != hs[0]->device)
+      return fail(hs[0], YODA_ERR_INVALID_ARG, "local exchange: shards on different devices");
+  // one stream for every shard of the step, so the device copies order after the kernels
+  std::vector<hipStream_t> saved(world);
+  for (int i = 0; i < world; ++i) {
+    saved[i] = hs[i]->stream;
+    hs[i]->stream = hs[0]->stream;
+  }
+  int rc;
+  try {
+    rc = comm_step(hs, world, world, mode, true);
+  } catch (...) {
+    rc = fail(hs[0], YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+  if (rc == YODA_OK && hipStreamSynchronize(hs[0]->stream) != hipSuccess) rc = YODA_ERR_HIP;
+  for (int i = 0; i < world; ++i) hs[i]->stream = saved[i];
+  return rc;
+}
+
+}  // extern "C"

@@ -979,9 +979,12 @@ __device__ __forceinline__ uint32_t rec_stride(Path p, int K) {
 // score to rows[n][p] (OUT_ROWS, the plugin row mode), or the TOPK best (score, node) per pod
 // sorted by (score desc, node asc) into tk_s/tk_i [C][TOPK][P] (greedy candidates).
 enum K2Out { OUT_ARGMAX = 0, OUT_ROWS = 1, OUT_TOPK = 2 };
-constexpr int kTopK = 16;
+// Candidates per pod: 8 for the reference-faithful greedy, 16 for the capacity mode (whose
+// lists go stale faster: picks also remove nodes).  kTopK is the default.
+constexpr int kTopK = 8;
+constexpr int kTopKCap = 16;
 
-template <int K, Path PATH, int OUT>
+template <int K, Path PATH, int OUT, int TK = kTopK>
 __global__ __launch_bounds__(kBlock) void k2_score(
     const unsigned char* __restrict__ nodes, uint32_t n_nodes, uint32_t chunk_nodes,
     ScoreArgs args, uint32_t n_pods, const MaskSrc ms,
@@ -1004,11 +1007,11 @@ __global__ __launch_bounds__(kBlock) void k2_score(
   constexpr uint32_t stride = PATH == Path::N32 ? n32_stride(K) : node_stride(K);
   double best = -1.0, low = 1.0e300;
   uint32_t idx = 0xffffffffu, ties = 0;
-  double ts[OUT == OUT_TOPK ? kTopK : 1];
-  uint32_t ti[OUT == OUT_TOPK ? kTopK : 1];
+  double ts[OUT == OUT_TOPK ? TK : 1];
+  uint32_t ti[OUT == OUT_TOPK ? TK : 1];
   if constexpr (OUT == OUT_TOPK) {
 #pragma unroll
-    for (int k = 0; k < kTopK; ++k) {
+    for (int k = 0; k < TK; ++k) {
       ts[k] = -1.0;
       ti[k] = 0xffffffffu;
     }
@@ -1019,11 +1022,11 @@ __global__ __launch_bounds__(kBlock) void k2_score(
     if constexpr (OUT == OUT_ROWS) rows[(size_t)n * n_pods + p] = (int64_t)raw;
     if constexpr (OUT == OUT_TOPK) {
       // strict '>' keeps the earlier (lower) node first among equal scores
-      if (raw > ts[kTopK - 1]) {
+      if (raw > ts[TK - 1]) {
         double cs = raw;
         uint32_t ci = n;
 #pragma unroll
-        for (int k = 0; k < kTopK; ++k) {
+        for (int k = 0; k < TK; ++k) {
           // (score desc, node asc): a carried entry that ties a slot must still shift
           const bool gt = cs > ts[k] || (cs == ts[k] && ci < ti[k]);
           const double os = ts[k];
@@ -1079,8 +1082,8 @@ __global__ __launch_bounds__(kBlock) void k2_score(
   if (!live) return;
   if constexpr (OUT == OUT_TOPK) {
 #pragma unroll
-    for (int k = 0; k < kTopK; ++k) {
-      const size_t o = ((size_t)chunk * kTopK + k) * n_pods + p;
+    for (int k = 0; k < TK; ++k) {
+      const size_t o = ((size_t)chunk * TK + k) * n_pods + p;
       tk_s[o] = ts[k];
       tk_i[o] = ti[k];
     }
@@ -1384,6 +1387,7 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
 
 // Merge the per-chunk top-k lists of each pod (chunks in node order, so the strict '>'
 // insertion keeps lower node indices first among equal scores) -> [TOPK][P], global ids.
+template <int TK>
 __global__ __launch_bounds__(kBlock) void k_topk_merge(const double* __restrict__ tk_s,
                                                        const uint32_t* __restrict__ tk_i,
                                                        uint32_t C, uint32_t n_pods,
@@ -1392,22 +1396,22 @@ __global__ __launch_bounds__(kBlock) void k_topk_merge(const double* __restrict_
                                                        uint32_t* __restrict__ out_i) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (p >= n_pods) return;
-  double ts[kTopK];
-  uint32_t ti[kTopK];
+  double ts[TK];
+  uint32_t ti[TK];
 #pragma unroll
-  for (int k = 0; k < kTopK; ++k) {
+  for (int k = 0; k < TK; ++k) {
     ts[k] = -1.0;
     ti[k] = 0xffffffffu;
   }
   for (uint32_t c = 0; c < C; ++c) {
-    for (int e = 0; e < kTopK; ++e) {
-      const size_t o = ((size_t)c * kTopK + e) * n_pods + p;
+    for (int e = 0; e < TK; ++e) {
+      const size_t o = ((size_t)c * TK + e) * n_pods + p;
       double cs = tk_s[o];
       uint32_t ci = tk_i[o];
       // lists are sorted and later chunks hold higher node ids: the rest cannot enter
-      if (!(cs > ts[kTopK - 1])) break;
+      if (!(cs > ts[TK - 1])) break;
 #pragma unroll
-      for (int k = 0; k < kTopK; ++k) {
+      for (int k = 0; k < TK; ++k) {
         const bool gt = cs > ts[k] || (cs == ts[k] && ci < ti[k]);
         const double os = ts[k];
         const uint32_t oi = ti[k];
@@ -1419,7 +1423,7 @@ __global__ __launch_bounds__(kBlock) void k_topk_merge(const double* __restrict_
     }
   }
 #pragma unroll
-  for (int k = 0; k < kTopK; ++k) {
+  for (int k = 0; k < TK; ++k) {
     out_s[(size_t)k * n_pods + p] = ts[k];
     out_i[(size_t)k * n_pods + p] = ti[k] == 0xffffffffu ? ti[k] : ti[k] + node_offset;
   }
@@ -1428,10 +1432,11 @@ __global__ __launch_bounds__(kBlock) void k_topk_merge(const double* __restrict_
 // Wave-per-pod top-k merge: each lane folds a strided subset of chunk lists into its own
 // top-k, then the 64 lists are folded pairwise through shuffles.  The (score desc, node asc)
 // comparison is a total order, so the result does not depend on the folding order.
-__device__ __forceinline__ void topk_insert(double (&ts)[kTopK], uint32_t (&ti)[kTopK],
+template <int TK>
+__device__ __forceinline__ void topk_insert(double (&ts)[TK], uint32_t (&ti)[TK],
                                             double cs, uint32_t ci) {
 #pragma unroll
-  for (int k = 0; k < kTopK; ++k) {
+  for (int k = 0; k < TK; ++k) {
     const bool gt = cs > ts[k] || (cs == ts[k] && ci < ti[k]);
     const double os = ts[k];
     const uint32_t oi = ti[k];
@@ -1442,6 +1447,7 @@ __device__ __forceinline__ void topk_insert(double (&ts)[kTopK], uint32_t (&ti)[
   }
 }
 
+template <int TK>
 __global__ __launch_bounds__(kWave) void k_topk_merge_wave(const double* __restrict__ tk_s,
                                                             const uint32_t* __restrict__ tk_i,
                                                             uint32_t C, uint32_t n_pods,
@@ -1449,36 +1455,36 @@ __global__ __launch_bounds__(kWave) void k_topk_merge_wave(const double* __restr
                                                             double* __restrict__ out_s,
                                                             uint32_t* __restrict__ out_i) {
   const uint32_t p = blockIdx.x, lane = threadIdx.x;
-  double ts[kTopK];
-  uint32_t ti[kTopK];
+  double ts[TK];
+  uint32_t ti[TK];
 #pragma unroll
-  for (int k = 0; k < kTopK; ++k) {
+  for (int k = 0; k < TK; ++k) {
     ts[k] = -1.0;
     ti[k] = 0xffffffffu;
   }
   for (uint32_t c = lane; c < C; c += kWave) {
-    for (int e = 0; e < kTopK; ++e) {
-      const size_t o = ((size_t)c * kTopK + e) * n_pods + p;
+    for (int e = 0; e < TK; ++e) {
+      const size_t o = ((size_t)c * TK + e) * n_pods + p;
       const double cs = tk_s[o];
       const uint32_t ci = tk_i[o];
-      if (!(cs > ts[kTopK - 1] || (cs == ts[kTopK - 1] && ci < ti[kTopK - 1]))) break;
+      if (!(cs > ts[TK - 1] || (cs == ts[TK - 1] && ci < ti[TK - 1]))) break;
       topk_insert(ts, ti, cs, ci);
     }
   }
   for (int o = kWave / 2; o > 0; o >>= 1) {
-    double ps[kTopK];
-    uint32_t pi[kTopK];
+    double ps[TK];
+    uint32_t pi[TK];
 #pragma unroll
-    for (int k = 0; k < kTopK; ++k) {
+    for (int k = 0; k < TK; ++k) {
       ps[k] = __shfl_xor(ts[k], o, kWave);
       pi[k] = __shfl_xor(ti[k], o, kWave);
     }
 #pragma unroll
-    for (int k = 0; k < kTopK; ++k) topk_insert(ts, ti, ps[k], pi[k]);
+    for (int k = 0; k < TK; ++k) topk_insert(ts, ti, ps[k], pi[k]);
   }
   if (lane != 0) return;
 #pragma unroll
-  for (int k = 0; k < kTopK; ++k) {
+  for (int k = 0; k < TK; ++k) {
     out_s[(size_t)k * n_pods + p] = ts[k];
     out_i[(size_t)k * n_pods + p] = ti[k] == 0xffffffffu ? ti[k] : ti[k] + node_offset;
   }
@@ -2450,23 +2456,48 @@ hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t
                           const double* rcp, const float* rcp32, uint32_t n_pods,
                           const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
                           uint32_t bs_stride, const Partials& part, double* tk_s,
-                          uint32_t* tk_i, hipStream_t s) {
-  return launch_k2_t<OUT_TOPK>(K, path, nodes, nullptr, nullptr, 0, n_nodes, chunk_nodes, C, pp, nullptr, rcp,
-                               rcp32,
-                               n_pods, bm, bm_stride, bs, bs_stride, part, nullptr, tk_s, tk_i,
-                               nullptr, s);
+                          uint32_t* tk_i, int tk, hipStream_t s) {
+  if (tk != kTopK && tk != kTopKCap) return hipErrorInvalidValue;
+  dim3 grid((n_pods + kBlock - 1) / kBlock, C);
+  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
+  const MaskSrc ms{bm, bs, bm_stride, bs_stride};
+#define YODA_TOPK(PTH, TKV)                                                                      \
+  YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score<KK, PTH, OUT_TOPK, TKV>), grid, dim3(kBlock), 0, \
+                                      s, nodes, n_nodes, chunk_nodes, a, n_pods, ms, part.best_f, \
+                                      part.idx, part.ties, part.low_f, nullptr, tk_s, tk_i))
+  switch (path) {
+    case Path::N32:
+      if (tk == kTopK) YODA_TOPK(Path::N32, kTopK) else YODA_TOPK(Path::N32, kTopKCap);
+      break;
+    case Path::F64:
+      if (tk == kTopK) YODA_TOPK(Path::F64, kTopK) else YODA_TOPK(Path::F64, kTopKCap);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef YODA_TOPK
+  return hipGetLastError();
 }
 
 hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t C,
                              uint32_t n_pods, uint32_t node_offset, double* out_s,
-                             uint32_t* out_i, hipStream_t s) {
+                             uint32_t* out_i, int tk, hipStream_t s) {
+  if (tk != kTopK && tk != kTopKCap) return hipErrorInvalidValue;
   if (C > 8) {
-    hipLaunchKernelGGL(k_topk_merge_wave, dim3(n_pods), dim3(kWave), 0, s, tk_s, tk_i, C, n_pods,
-                       node_offset, out_s, out_i);
+    if (tk == kTopK)
+      hipLaunchKernelGGL(k_topk_merge_wave<kTopK>, dim3(n_pods), dim3(kWave), 0, s, tk_s, tk_i, C,
+                         n_pods, node_offset, out_s, out_i);
+    else
+      hipLaunchKernelGGL(k_topk_merge_wave<kTopKCap>, dim3(n_pods), dim3(kWave), 0, s, tk_s, tk_i,
+                         C, n_pods, node_offset, out_s, out_i);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_topk_merge, pod_grid(n_pods), dim3(kBlock), 0, s, tk_s, tk_i, C, n_pods,
-                     node_offset, out_s, out_i);
+  if (tk == kTopK)
+    hipLaunchKernelGGL(k_topk_merge<kTopK>, pod_grid(n_pods), dim3(kBlock), 0, s, tk_s, tk_i, C,
+                       n_pods, node_offset, out_s, out_i);
+  else
+    hipLaunchKernelGGL(k_topk_merge<kTopKCap>, pod_grid(n_pods), dim3(kBlock), 0, s, tk_s, tk_i,
+                       C, n_pods, node_offset, out_s, out_i);
   return hipGetLastError();
 }
 
@@ -2481,6 +2512,7 @@ hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32
 }
 
 int topk_k() { return kTopK; }
+int topk_k_capacity() { return kTopKCap; }
 
 // Partials of k_greedy_one: at most this many blocks (grid-stride over the nodes).
 constexpr uint32_t kGreedyOneBlocks = 512;
@@ -2753,6 +2785,128 @@ hipError_t launch_norm_rows(const int64_t* rows, uint32_t n_nodes, uint32_t n_po
   if (total == 0) return hipSuccess;
   hipLaunchKernelGGL(k_norm_rows, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                      s, rows, n_nodes, n_pods, best, lowest, norm);
+  return hipGetLastError();
+}
+
+// ---- the multi-GPU step inside libyoda (yoda_comm_*) ----------------------
+// Exchange 1 is ONE all-reduce(MAX, u64) over [maxima 6P | count slots world x P]: rank r
+// writes (n_feasible << 32 | n_zero_total) into slot r and zeros elsewhere, so the MAX is an
+// all-gather of the counts, summed after.  Exchange 2 is ONE all-gather of ShardRec [P].
+__global__ __launch_bounds__(kBlock) void k_slot_counts(const uint32_t* __restrict__ counts,
+                                                        uint32_t n_pods, uint32_t rank,
+                                                        uint32_t world,
+                                                        uint64_t* __restrict__ slots) {
+  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= (uint64_t)world * n_pods) return;
+  const uint32_t r = (uint32_t)(t / n_pods), p = (uint32_t)(t % n_pods);
+  slots[t] = r == rank ? ((uint64_t)counts[p] << 32) | counts[(size_t)n_pods + p] : 0ull;
+}
+
+__global__ __launch_bounds__(kBlock) void k_unslot_counts(const uint64_t* __restrict__ slots,
+                                                          uint32_t n_pods, uint32_t world,
+                                                          uint32_t* __restrict__ counts) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= n_pods) return;
+  uint32_t nf = 0, nz = 0;
+  for (uint32_t r = 0; r < world; ++r) {
+    const uint64_t v = slots[(size_t)r * n_pods + p];
+    nf += (uint32_t)(v >> 32);
+    nz += (uint32_t)v;
+  }
+  counts[p] = nf;
+  counts[(size_t)n_pods + p] = nz;
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack_rec(const int64_t* __restrict__ best,
+                                                     const uint32_t* __restrict__ idx,
+                                                     const uint32_t* __restrict__ ties,
+                                                     const int64_t* __restrict__ low,
+                                                     uint32_t n_pods, ShardRec* __restrict__ rec) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= n_pods) return;
+  rec[p] = ShardRec{best[p], idx[p], ties[p], low[p]};
+}
+
+// Fold the ranks' records of each pod: the highest best, the lowest node reaching it, the
+// tie counts of the ranks reaching it summed, the lowest low (the merges of merge_phase2).
+__global__ __launch_bounds__(kBlock) void k_merge_rec(const ShardRec* __restrict__ all,
+                                                      uint32_t n_pods, uint32_t world,
+                                                      int64_t* __restrict__ best,
+                                                      uint32_t* __restrict__ idx,
+                                                      uint32_t* __restrict__ ties,
+                                                      int64_t* __restrict__ low) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= n_pods) return;
+  int64_t b = -1, l = kI64Max;
+  uint32_t i = 0xffffffffu, t = 0;
+  for (uint32_t r = 0; r < world; ++r) {
+    const ShardRec x = all[(size_t)r * n_pods + p];
+    l = x.low < l ? x.low : l;
+    if (x.best < 0) continue;
+    if (x.best > b) {
+      b = x.best;
+      i = x.idx;
+      t = x.ties;
+    } else if (x.best == b) {
+      i = min(i, x.idx);
+      t += x.ties;
+    }
+  }
+  best[p] = b;
+  idx[p] = i;
+  ties[p] = t;
+  low[p] = l;
+}
+
+// In-process exchange (several shard handles on one device): elementwise MAX of n u64 over
+// the handles' buffers into dst.
+__global__ __launch_bounds__(kBlock) void k_max_multi(PtrList src, uint32_t k, uint64_t n,
+                                                      uint64_t* __restrict__ dst) {
+  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= n) return;
+  uint64_t m = 0;
+  for (uint32_t j = 0; j < k; ++j) m = umax64(m, static_cast<const uint64_t*>(src.p[j])[t]);
+  dst[t] = m;
+}
+
+hipError_t launch_slot_counts(const uint32_t* counts, uint32_t n_pods, uint32_t rank,
+                              uint32_t world, uint64_t* slots, hipStream_t s) {
+  const uint64_t n = (uint64_t)world * n_pods;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_slot_counts, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     s, counts, n_pods, rank, world, slots);
+  return hipGetLastError();
+}
+
+hipError_t launch_unslot_counts(const uint64_t* slots, uint32_t n_pods, uint32_t world,
+                                uint32_t* counts, hipStream_t s) {
+  if (n_pods == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_unslot_counts, pod_grid(n_pods), dim3(kBlock), 0, s, slots, n_pods, world,
+                     counts);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_rec(const int64_t* best, const uint32_t* idx, const uint32_t* ties,
+                           const int64_t* low, uint32_t n_pods, ShardRec* rec, hipStream_t s) {
+  if (n_pods == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pack_rec, pod_grid(n_pods), dim3(kBlock), 0, s, best, idx, ties, low,
+                     n_pods, rec);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge_rec(const ShardRec* all, uint32_t n_pods, uint32_t world, int64_t* best,
+                            uint32_t* idx, uint32_t* ties, int64_t* low, hipStream_t s) {
+  if (n_pods == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_merge_rec, pod_grid(n_pods), dim3(kBlock), 0, s, all, n_pods, world, best,
+                     idx, ties, low);
+  return hipGetLastError();
+}
+
+hipError_t launch_max_multi(const PtrList& src, uint32_t k, uint64_t n, uint64_t* dst,
+                            hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_max_multi, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                     src, k, n, dst);
   return hipGetLastError();
 }
 

@@ -168,6 +168,20 @@ struct alignas(16) OneOut {
   uint32_t idx, ties;         // lowest node reaching best, nodes reaching it
 };
 
+// Multi-GPU step inside libyoda (yoda_comm_*): a shard's per-pod result of phase 2, all-
+// gathered across ranks (global node index; best / low as int64 raw scores).
+struct alignas(8) ShardRec {
+  int64_t best;       // highest raw score over the shard's feasible nodes (-1: none)
+  uint32_t idx, ties; // lowest global node reaching it, nodes reaching it
+  int64_t low;        // lowest raw score (INT64_MAX: none)
+};
+static_assert(sizeof(ShardRec) == 24, "ShardRec layout");
+// Up to this many handles share one in-process exchange (yoda_comm_run_local).
+constexpr int kMaxLocalShards = 16;
+struct PtrList {
+  const void* p[kMaxLocalShards];
+};
+
 // Per-pod device parameters (struct of arrays, length P each).
 struct PodParams {
   // Filter / card predicate thresholds

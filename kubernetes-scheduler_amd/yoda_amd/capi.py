@@ -71,6 +71,10 @@ _SIGS = {
     "yoda_class_stats_enable": ([_vp, C.c_int], C.c_int),
     "yoda_class_stats_read": ([_vp, _vp], C.c_int),
     "yoda_greedy_restarts": ([_vp, C.POINTER(C.c_uint32)], C.c_int),
+    "yoda_comm_unique_id": ([_vp], C.c_int),
+    "yoda_comm_init": ([_vp, _vp, C.c_int, C.c_int], C.c_int),
+    "yoda_comm_run": ([_vp, C.c_int], C.c_int),
+    "yoda_comm_run_local": ([_vp, C.c_int, C.c_int], C.c_int),
     "yoda_gs_create": ([C.POINTER(CNodeSoA), C.POINTER(CPodSoA), _u32, C.POINTER(_vp)], C.c_int),
     "yoda_gs_destroy": ([_vp], C.c_int),
     "yoda_gs_queue_order": ([_vp, _vp], C.c_int),
@@ -302,6 +306,15 @@ class Yoda:
         return k1.value, k2.value, n.value
 
     # ---- sharded (device pointers as ints) ---------------------------------------------
+    def comm_init(self, comm_id: bytes, rank: int, world: int):
+        """Join an RCCL communicator inside libyoda (yoda_comm_init; collective)."""
+        buf = (C.c_uint8 * 128).from_buffer_copy(comm_id)
+        self._check(lib().yoda_comm_init(self._h, buf, rank, world), "yoda_comm_init")
+
+    def comm_run(self, mode: int = 0):
+        """One sharded step with libyoda's own RCCL exchanges (yoda_comm_run)."""
+        self._check(lib().yoda_comm_run(self._h, mode), "yoda_comm_run")
+
     def shard_phase1(self, mode: int, d_maxima: int, d_counts: int):
         self._check(lib().yoda_shard_phase1(self._h, mode, _vp(d_maxima), _vp(d_counts)),
                     "yoda_shard_phase1")
@@ -365,6 +378,25 @@ class Yoda:
         self._check(lib().yoda_shard_finalize(self._h, mode, _vp(d_counts), _vp(d_best),
                                               _vp(d_idx), _vp(d_ties), _vp(d_lowest)),
                     "yoda_shard_finalize")
+
+
+def comm_unique_id() -> bytes:
+    """RCCL communicator id for Yoda.comm_init (rank 0 makes it, the others receive it)."""
+    buf = (C.c_uint8 * 128)()
+    rc = lib().yoda_comm_unique_id(buf)
+    if rc != 0:
+        raise YodaError(f"yoda_comm_unique_id: {ERRORS.get(rc, rc)}")
+    return bytes(buf)
+
+
+def comm_run_local(handles, mode: int = 0):
+    """One sharded step over several shard handles of this process on one device
+    (yoda_comm_run_local): the libyoda exchange with device copies as the transport."""
+    arr = (C.c_void_p * len(handles))(*[h._h for h in handles])
+    rc = lib().yoda_comm_run_local(arr, len(handles), mode)
+    if rc != 0:
+        raise YodaError(f"yoda_comm_run_local: {ERRORS.get(rc, rc)}: "
+                        f"{lib().yoda_last_error(handles[0]._h).decode()}")
 
 
 def topk_k() -> int:

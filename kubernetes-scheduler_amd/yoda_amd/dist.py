@@ -234,6 +234,33 @@ class ShardExchange:
         return self.handles[0].download()
 
 
+class LibExchange:
+    """Node sharding with libyoda's OWN exchanges (yoda_comm_run, include/yoda.h): one
+    all-reduce(MAX) of the maxima with per-rank count slots and one all-gather of the
+    per-shard (best, index, ties, lowest) records per step, issued by libyoda through RCCL on
+    the handle's stream -- the path a cgo / C caller without torch uses.  torch.distributed
+    here only agrees on the record path and broadcasts the communicator id."""
+
+    def __init__(self, handle, device, shard=None, offset: int = 0, group=None):
+        import torch.distributed as dist
+        from .capi import comm_unique_id
+        if shard is not None:
+            agree_on_path(Reducer(group=group), [handle], [shard], [offset], device)
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        on_dev = dist.get_backend(group) == "nccl"
+        t = torch.zeros(128, dtype=torch.uint8, device=device if on_dev else "cpu")
+        if rank == 0:
+            t.copy_(torch.tensor(list(comm_unique_id()), dtype=torch.uint8))
+        dist.broadcast(t, src=0, group=group)
+        handle.comm_init(bytes(t.cpu().numpy().tobytes()), rank, world)
+        if device.type == "cuda":
+            handle.set_stream(torch.cuda.current_stream(device).cuda_stream)
+        self.handle = handle
+
+    def step(self, mode: int):
+        self.handle.comm_run(mode)
+
+
 def shard_bounds(n_nodes: int, world: int) -> np.ndarray:
     """Contiguous node blocks, one per rank."""
     return np.linspace(0, n_nodes, world + 1).astype(np.int64)

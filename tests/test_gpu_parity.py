@@ -582,3 +582,41 @@ def test_k2_block_scoring(dev, seed):
             dev.upload_nodes(nodes, per_node_k1=k1, per_node_k2=k2)
             assert_same(dev.eval(pods, MODE_SCV), want)
     dev.set_pod_order(True)
+
+
+@pytest.mark.parametrize("mode", [MODE_SCV, MODE_DISKIO])
+@pytest.mark.parametrize("path", ["n32", "f64", "u64"])
+def test_comm_local_matches_unsharded(dev, mode, path):
+    """libyoda's own sharded step (yoda_comm_run_local: the all-reduce with count slots and
+    the all-gather of shard records, device copies as the transport) on 1-4 node shards ==
+    the unsharded evaluation: picks, statuses, feasible counts, ties, top scores, maxima."""
+    from yoda_amd.capi import comm_run_local
+    nodes, pods = synth.make_config(2, pods=700, nodes=3001)
+    nodes.total_memory_sum[17] = 0
+    nodes = nodes.normalized()
+    want = oracle.schedule(nodes, pods, mode, threads=8)
+    for world in (1, 2, 3, 4):
+        b = np.linspace(0, nodes.n_nodes, world + 1).astype(int)
+        hs = [Yoda(0) for _ in range(world)]
+        for r, h in enumerate(hs):
+            h.upload_nodes(nodes.slice(b[r], b[r + 1]), node_offset=int(b[r]),
+                           force_f64=path == "f64", force_generic=path == "u64")
+            h.upload_pods(pods)
+        comm_run_local(hs, mode)
+        for h in hs:
+            assert_same(h.download(), want, mode)
+            h.close()
+
+
+def test_comm_rccl_world1(dev):
+    """The RCCL path of yoda_comm_run (a one-rank communicator on this GPU) == yoda_run."""
+    from yoda_amd.capi import comm_unique_id
+    nodes, pods = synth.make_config(2, pods=500, nodes=4000)
+    y = Yoda(0)
+    y.upload_nodes(nodes)
+    y.upload_pods(pods)
+    y.comm_init(comm_unique_id(), 0, 1)
+    for mode in (MODE_SCV, MODE_DISKIO):
+        y.comm_run(mode)
+        assert_same(y.download(), oracle.schedule(nodes, pods, mode, threads=8), mode)
+    y.close()
