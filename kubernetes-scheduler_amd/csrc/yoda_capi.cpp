@@ -37,7 +37,7 @@ hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigne
                      const double* rcp, const float* rcp32, uint32_t n_pods,
                      const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
                      uint32_t bs_stride, const Partials& part, int64_t* rows,
-                     unsigned long long* stats, hipStream_t s);
+                     unsigned long long* stats, const uint32_t* counts, hipStream_t s);
 hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
                             uint32_t C, const PodParams& pp, uint32_t n_pods, const Partials& part,
                             int64_t* rows, hipStream_t s);
@@ -119,7 +119,8 @@ hipError_t launch_max_multi(const PtrList& src, uint32_t k, uint64_t n, uint64_t
                             hipStream_t s);
 size_t order_scratch_bytes(uint32_t n_pods);
 hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
-                             uint32_t n_pods, const uint32_t key_bits[3], void* scratch,
+                             uint32_t n_pods, const uint32_t key_bits[3],
+                             const uint32_t* groups, uint32_t n_groups, void* scratch,
                              size_t scratch_bytes, uint32_t* perm, hipStream_t s);
 hipError_t launch_permute(const PermTable& t, const uint32_t* perm, uint32_t n_pods, bool scatter,
                           hipStream_t s);
@@ -269,6 +270,10 @@ struct yoda_handle {
   bool ordered = false;
   DevBuf pod_sorted, perm, order_scratch;
   uint32_t key_bits[3] = {24, 8, 32};  // widths of the batch's sort-key fields (c, n, m)
+  // the batch's distinct (clock, number) key groups, ascending (serpentine order, see
+  // yoda_order.hip): host copy kept alive for the async upload
+  DevBuf order_groups;
+  std::vector<uint32_t> order_groups_host;
 
   // state
   DevBuf maxima, counts, rcp, rcp32, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
@@ -332,7 +337,7 @@ struct yoda_handle {
     if (comm && rccl().ok) (void)rccl().comm_destroy(comm);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &pod_blob,   &maxima,       &counts,
-                     &pod_sorted, &perm,     &order_scratch,
+                     &pod_sorted, &perm,     &order_scratch, &order_groups,
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
                      &n_flagged, &bitmask,   &bitmask_t,  &blk,  &bsum, &p_max_u,      &p_cnt,
@@ -523,8 +528,8 @@ int order_pods(yoda_t* h, int mode) {
   HIP_TRY(h, launch_order_pods(reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodNumber]),
                                reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodMU]),
                                reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodCU]), P,
-                               h->key_bits,
-                               h->order_scratch.p, h->order_scratch.bytes,
+                               h->key_bits, h->order_groups.as<uint32_t>(),
+                               (uint32_t)h->order_groups_host.size(), h->order_scratch.p, h->order_scratch.bytes,
                                h->perm.as<uint32_t>(), h->stream));
   PermTable t{};
   for (int a = 0; a < kPodArrays; ++a) {
@@ -638,8 +643,10 @@ int phase1_witness(yoda_t* h, uint64_t* maxima, uint32_t* counts, uint32_t* wit,
 }
 
 // Phase 2: Score over the feasible nodes with the (globally reduced) maxima.
-int phase2(yoda_t* h, int mode, const uint64_t* maxima, int64_t* best, uint32_t* idx,
-           uint32_t* ties, int64_t* low, int64_t* rows = nullptr) {
+// counts: the pods' feasible-node counts ([P] prefix of phase 1's [2][P], local or reduced;
+// NULL: unknown): a pod with none takes no part in the block K2's wave bounds.
+int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, int64_t* best,
+           uint32_t* idx, uint32_t* ties, int64_t* low, int64_t* rows = nullptr) {
   const uint32_t P = h->n_pods;
   if (P == 0) return YODA_OK;
   if (h->n_nodes == 0) {
@@ -669,7 +676,7 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, int64_t* best, uint32_t*
                          h->n_nodes,
                          h->chunk2, h->C2, pod_params(h), maxima, h->rcp.as<double>(),
                          h->rcp32.as<float>(), P, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
-                         h->bs_ptr(), bs_row(h->n_nodes), part, rows, h->stats_ptr(),
+                         h->bs_ptr(), bs_row(h->n_nodes), part, rows, h->stats_ptr(), counts,
                          h->stream));
     if (h->class_stats && h->has_k2sum && !rows)
       h->stats_pairs2 += (uint64_t)(P + 63) / 64 * h->n_nodes;
@@ -1079,6 +1086,33 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     uint32_t* nc = reinterpret_cast<uint32_t*>(st + off[kPodNeedClk]);
     const uint64_t kClamp = 1ull << 53;  // > every F64-path card field (<= 2^44)
     uint64_t key_or[3] = {0, 0, 0};       // OR of the sort key's clamped fields (c, n, m)
+    // distinct (clock, number) key groups: open-addressing set of group + 1 (0 = empty)
+    std::vector<uint32_t> gset(256, 0u);
+    size_t g_n = 0;
+    auto g_insert = [&](uint32_t g) {
+      for (;;) {
+        const size_t mask = gset.size() - 1;
+        size_t i = (size_t)(g * 0x9e3779b1u) & mask;
+        while (gset[i] != 0u && gset[i] != g + 1u) i = (i + 1) & mask;
+        if (gset[i] != 0u) return;
+        if (2 * (g_n + 1) <= gset.size()) {
+          gset[i] = g + 1u;
+          ++g_n;
+          return;
+        }
+        std::vector<uint32_t> old(gset.size() * 2, 0u);  // grow and rehash
+        old.swap(gset);
+        g_n = 0;
+        for (uint32_t v : old)
+          if (v) {
+            size_t j = (size_t)((v - 1u) * 0x9e3779b1u) & (gset.size() - 1);
+            while (gset[j] != 0u) j = (j + 1) & (gset.size() - 1);
+            gset[j] = v;
+            ++g_n;
+          }
+      }
+    };
+    uint32_t g_last = 0xffffffffu;
     for (uint32_t p = 0; p < P; ++p) {
       const uint64_t number = pd->has_number[p] ? pd->number[p] : 1;  // filter.go:12-15
       const uint64_t m = pd->has_memory[p] ? pd->memory[p] : 0;       // filter.go:19,32
@@ -1096,6 +1130,10 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
       key_or[0] |= std::min<uint64_t>(c, 0xffffffull);  // the clamps of k_order_keys
       key_or[1] |= std::min<uint64_t>(number, 0xffull);
       key_or[2] |= std::min<uint64_t>(m, 0xffffffffull);
+      const uint32_t g = (uint32_t)(std::min<uint64_t>(c, 0xffffffull) << 8) |
+                         (uint32_t)std::min<uint64_t>(number, 0xffull);
+      if (g != g_last) g_insert(g);
+      g_last = g;
       al[p] = be[p] = 0.0;
       if (pd->rio && pd->rcpu) {  // algorithm.go:105-106
         const double beta = 1.0 / (1.0 + (double)pd->rcpu[p] / pd->rio[p]);
@@ -1103,7 +1141,17 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
         al[p] = 1 - beta;
       }
     }
+    h->order_groups_host.clear();
+    for (uint32_t v : gset)
+      if (v) h->order_groups_host.push_back(v - 1u);
+    std::sort(h->order_groups_host.begin(), h->order_groups_host.end());
     HIP_TRY(h, hipMemcpyAsync(h->pod_blob.p, st, total, hipMemcpyHostToDevice, h->stream));
+    if (!h->order_groups_host.empty()) {
+      HIP_TRY(h, h->order_groups.ensure(h->order_groups_host.size() * 4));
+      HIP_TRY(h, hipMemcpyAsync(h->order_groups.p, h->order_groups_host.data(),
+                                h->order_groups_host.size() * 4, hipMemcpyHostToDevice,
+                                h->stream));
+    }
     HIP_TRY(h, hipEventRecord(h->stage_event, h->stream));
     h->stage_pending = true;
     for (int a = 0; a < kPodArrays; ++a) h->pod_off[a] = off[a];
@@ -1140,7 +1188,7 @@ int yoda_run(yoda_t* h, int mode, uint32_t flags) {
   try {
     if ((rc = order_pods(h, mode))) return rc;
     if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>()))) return rc;
-    if ((rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->best.as<int64_t>(),
+    if ((rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), h->best.as<int64_t>(),
                      h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>())))
       return rc;
     if ((rc = finalize(h, mode, h->counts.as<uint32_t>(), h->best.as<int64_t>(),
@@ -1248,7 +1296,7 @@ int yoda_score_rows_norm(yoda_t* h, int mode, uint32_t* bitmask_out, uint64_t n_
     }
     if ((rc = order_pods(h, mode))) return rc;
     if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>()))) return rc;
-    if ((rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->best.as<int64_t>(),
+    if ((rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), h->best.as<int64_t>(),
                      h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(),
                      rows)))
       return rc;
@@ -1331,8 +1379,7 @@ int yoda_shard_phase2(yoda_t* h, int mode, const uint64_t* d_maxima, const uint3
     // keep the reduced maxima for download and the generic exact-normalize pass
     if (P) HIP_TRY(h, hipMemcpyAsync(h->maxima.p, d_maxima, 6ull * P * 8, hipMemcpyDeviceToDevice,
                                      h->stream));
-    (void)d_counts;
-    return phase2(h, mode, h->maxima.as<uint64_t>(), d_best, d_idx, d_ties, d_lowest);
+    return phase2(h, mode, h->maxima.as<uint64_t>(), d_counts, d_best, d_idx, d_ties, d_lowest);
   } catch (...) {
     return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
   }
@@ -1395,8 +1442,17 @@ int yoda_class_stats_enable(yoda_t* h, int enable) {
   if (!h) return YODA_ERR_INVALID_ARG;
   HIP_TRY(h, hipSetDevice(h->device));
   if (enable && !h->class_stats) {
-    HIP_TRY(h, h->stats_dev.ensure(8 * 8));
-    HIP_TRY(h, hipMemsetAsync(h->stats_dev.p, 0, 8 * 8, h->stream));
+    // YODA_K2_TRACE=<(wave, chunk) slots>: K2 also records per-(wave, chunk) timings
+    const uint32_t tr = env_u32("YODA_K2_TRACE", 0);
+    const size_t bytes = (16 + 4 * (size_t)tr) * 8;
+    HIP_TRY(h, h->stats_dev.ensure(bytes));
+    HIP_TRY(h, hipMemsetAsync(h->stats_dev.p, 0, bytes, h->stream));
+    if (tr) {
+      const uint64_t one = 1;
+      HIP_TRY(h, hipMemcpyAsync(h->stats_dev.as<uint64_t>() + 15, &one, 8,
+                                hipMemcpyHostToDevice, h->stream));
+      HIP_TRY(h, hipStreamSynchronize(h->stream));
+    }
     h->stats_pairs1 = h->stats_pairs2 = 0;
   }
   h->class_stats = enable != 0;
@@ -1405,11 +1461,11 @@ int yoda_class_stats_enable(yoda_t* h, int enable) {
 
 int yoda_class_stats_read(yoda_t* h, uint64_t* out) {
   if (!h || !out) return YODA_ERR_INVALID_ARG;
-  for (int i = 0; i < 10; ++i) out[i] = 0;
+  for (int i = 0; i < 13; ++i) out[i] = 0;
   if (!h->stats_dev.p) return YODA_OK;
   HIP_TRY(h, hipSetDevice(h->device));
-  uint64_t d[8] = {};
-  HIP_TRY(h, hipMemcpyAsync(d, h->stats_dev.p, 8 * 8, hipMemcpyDeviceToHost, h->stream));
+  uint64_t d[16] = {};
+  HIP_TRY(h, hipMemcpyAsync(d, h->stats_dev.p, 16 * 8, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
   out[0] = d[0];                                                   // K1 ALL
   out[1] = d[1];                                                   // K1 NONE
@@ -1421,8 +1477,21 @@ int yoda_class_stats_read(yoda_t* h, uint64_t* out) {
   out[7] = d[5];                                                   // K2 (wave, chunk)s, uniform
   out[8] = d[6];                                                   // K2 (wave, chunk)s
   out[9] = h->stats_pairs1;
-  HIP_TRY(h, hipMemsetAsync(h->stats_dev.p, 0, 8 * 8, h->stream));
+  out[10] = d[7];                                                  // K2 FAST via node records
+  out[11] = d[8];                                                  // K2 per-pod, non-uniform
+  out[12] = d[9];                                                  // max per-pod nodes/(w, c)
+  HIP_TRY(h, hipMemsetAsync(h->stats_dev.p, 0, 15 * 8, h->stream));
   h->stats_pairs1 = h->stats_pairs2 = 0;
+  return YODA_OK;
+}
+
+int yoda_k2_trace_read(yoda_t* h, uint64_t* out, uint64_t n_slots) {
+  if (!h || !out) return YODA_ERR_INVALID_ARG;
+  if (!h->stats_dev.p || h->stats_dev.bytes < (16 + 4 * n_slots) * 8) return YODA_ERR_INVALID_ARG;
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipMemcpyAsync(out, h->stats_dev.as<uint64_t>() + 16, 4 * n_slots * 8,
+                            hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));
   return YODA_OK;
 }
 
@@ -2909,7 +2978,7 @@ static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local) 
                                     h->counts.as<uint32_t>(), h->stream));
     HIP_TRY(h, hipMemcpyAsync(h->maxima.p, ex, 6 * (size_t)P * 8, hipMemcpyDeviceToDevice,
                               h->stream));
-    int rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->best.as<int64_t>(),
+    int rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), h->best.as<int64_t>(),
                     h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>());
     if (rc) return rc;
     HIP_TRY(h, launch_pack_rec(h->best.as<int64_t>(), h->idx.as<uint32_t>(),

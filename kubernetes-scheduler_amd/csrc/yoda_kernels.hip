@@ -850,6 +850,7 @@ struct ScoreArgs {
   const uint32_t* c_32;
   const double* rcp;    // [5][P] f64: bw, core, power, free, total
   const float* rcp32;   // [3][P] f32: bw, core, power
+  const uint32_t* cnt = nullptr;  // [P] feasible-node counts (phase 1), or none
 };
 
 template <Path P>
@@ -1111,7 +1112,7 @@ __global__ __launch_bounds__(kBlock) void k2_score(
 //   EXACT anything else (mixed-model node, or non-uniform maxima): Scorer<N32>::raw.
 // Every term is an exact integer < 2^52 in each form, so all three give the same raw score.
 template <int K, bool STATS>
-__global__ __launch_bounds__(kBlock) void k2_block_n32(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ? 5 : 1))) void k2_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum2,
     uint32_t n_nodes, uint32_t chunk_nodes, ScoreArgs args, uint32_t n_pods,
     const uint64_t* __restrict__ bm, uint32_t bm_stride, const BlockMask* __restrict__ bs,
@@ -1121,8 +1122,12 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
     unsigned long long* __restrict__ stats) {
   constexpr uint32_t S2 = k2sum_stride(K), NS = n32_stride(K);
   constexpr uint32_t PSW = K + 2;  // LDS words per node: prefix[0..K], shared
-  constexpr uint32_t TAB = kWave * PSW;  // one table: 64 nodes
-  __shared__ uint32_t lds_all[kBlock / kWave][2 * TAB];
+  constexpr uint32_t TAB = kWave * PSW;  // the prefix table: 64 nodes
+  // node records (below): 6 words + (basic at nq_lo, at nq_lo + 1) per reciprocal set
+  constexpr uint32_t kSets = 5, REC = 6 + 2 * kSets;
+  // LDS per wave: prefix table | 64 node records | the sets' reciprocals (8 words each)
+  constexpr uint32_t RECS = TAB, RCPS = TAB + kWave * REC, LDSW = RCPS + 8 * kSets;
+  __shared__ __attribute__((aligned(16))) uint32_t lds_all[kBlock / kWave][LDSW];
   const uint32_t lane = lane_id();
   uint32_t* lds = lds_all[threadIdx.x >> 6];
   const Tile tl = tile();
@@ -1133,46 +1138,71 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
   const bool live = p < n_pods;
   const uint64_t live_mask = ballot(live);
   if (live_mask == 0) return;  // a wave past the batch
+  // STATS with stats[15] set: the timing trace only (no per-block counter atomics)
+  const bool trace = STATS && stats[15] != 0ull;
+  const uint64_t t_start = STATS ? wall_clock64() : 0ull;
   const uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
   const BlockMask* bsw = bs ? bs + (size_t)uniform_u32(p >> 6) * bs_stride : nullptr;
   Scorer<Path::N32> sc;
   if (live) sc.load(args, p, n_pods);
-  // live lanes are a prefix of the wave: lane 0 is live
-  const float u_bw = __int_as_float((int)uniform_u32((uint32_t)__float_as_int(sc.r_bw)));
-  const float u_core = __int_as_float((int)uniform_u32((uint32_t)__float_as_int(sc.r_core)));
-  const float u_pow = __int_as_float((int)uniform_u32((uint32_t)__float_as_int(sc.r_pow)));
-  const double u_free =
-      __longlong_as_double((long long)uniform_u64((uint64_t)__double_as_longlong(sc.r_free)));
-  const double u_tot =
-      __longlong_as_double((long long)uniform_u64((uint64_t)__double_as_longlong(sc.r_tot)));
-  const bool same = sc.r_bw == u_bw && sc.r_core == u_core && sc.r_pow == u_pow &&
-                    sc.r_free == u_free && sc.r_tot == u_tot;
-  const uint64_t same_b = ballot(!live || same);
-  const bool uni_max = same_b == ~0ull;
-  // Otherwise a second reciprocal set (the first lane that differs from lane 0): lanes of
-  // either set read prefix tables from LDS, the rest (grp 2) compute with their own.
-  const int l1 = uni_max ? 0 : __builtin_ctzll(~same_b);
-  auto rl_f = [&](float x) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l1));
+  // A pod feasible on no node has no bit in any mask: it takes no part in the wave's bounds
+  // and reciprocal sets, and its outputs stay "no node".
+  const bool act = live && (args.cnt == nullptr || args.cnt[p] != 0u);
+  const uint64_t act_mask = ballot(act);
+  // Reciprocal sets: active lanes with the same (bw, core, power, free, total) reciprocals,
+  // numbered in order of their first lane; up to kSets, any further lanes "overflow".
+  auto rl_f = [&](float x, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
   };
-  auto rl_d = [&](double x) {
+  auto rl_d = [&](double x, int l) {
     const uint64_t b = (uint64_t)__double_as_longlong(x);
     return __longlong_as_double((long long)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
-        (int)(uint32_t)b, l1) | ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
-        (int)(uint32_t)(b >> 32), l1) << 32)));
+        (int)(uint32_t)b, l) | ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
+        (int)(uint32_t)(b >> 32), l) << 32)));
   };
-  const float v_bw = rl_f(sc.r_bw), v_core = rl_f(sc.r_core), v_pow = rl_f(sc.r_pow);
-  const double v_free = rl_d(sc.r_free), v_tot = rl_d(sc.r_tot);
-  const bool same1 = sc.r_bw == v_bw && sc.r_core == v_core && sc.r_pow == v_pow &&
-                     sc.r_free == v_free && sc.r_tot == v_tot;
-  const uint32_t grp = same ? 0u : (same1 ? 1u : 2u);
-  const uint32_t m_max = wave_max_u32(live ? sc.m : 0u), m_min = wave_min_u32(live ? sc.m : ~0u);
-  const uint32_t c_max = wave_max_u32(live ? sc.c : 0u), c_min = wave_min_u32(live ? sc.c : ~0u);
+  uint32_t set = 0, nsets = 0;
+  uint64_t rem = act_mask;
+  float u_bw = 0.f, u_core = 0.f, u_pow = 0.f;  // set 0's reciprocals (wave-uniform)
+  double u_free = 0.0, u_tot = 0.0;
+  for (; rem != 0ull && nsets < kSets; ++nsets) {
+    const int l = __builtin_ctzll(rem);
+    const float b_bw = rl_f(sc.r_bw, l), b_core = rl_f(sc.r_core, l), b_pow = rl_f(sc.r_pow, l);
+    const double b_free = rl_d(sc.r_free, l), b_tot = rl_d(sc.r_tot, l);
+    const bool in = act && sc.r_bw == b_bw && sc.r_core == b_core && sc.r_pow == b_pow &&
+                    sc.r_free == b_free && sc.r_tot == b_tot;
+    const uint64_t in_b = ballot(in) & rem;
+    if ((in_b >> lane) & 1ull) set = nsets;
+    rem &= ~in_b;
+    if (nsets == 0) {
+      u_bw = b_bw;
+      u_core = b_core;
+      u_pow = b_pow;
+      u_free = b_free;
+      u_tot = b_tot;
+    }
+    if (lane == (uint32_t)l) {
+      uint32_t* r = lds + RCPS + 8 * nsets;
+      r[0] = (uint32_t)__float_as_int(b_bw);
+      r[1] = (uint32_t)__float_as_int(b_core);
+      r[2] = (uint32_t)__float_as_int(b_pow);
+      const uint64_t f = (uint64_t)__double_as_longlong(b_free);
+      const uint64_t t = (uint64_t)__double_as_longlong(b_tot);
+      r[4] = (uint32_t)f;
+      r[5] = (uint32_t)(f >> 32);
+      r[6] = (uint32_t)t;
+      r[7] = (uint32_t)(t >> 32);
+    }
+  }
+  const bool uni_max = nsets <= 1u && rem == 0ull;  // "uniform maxima"
+  const bool rec_ok = rem == 0ull;  // every active lane has a set: node records serve it
+  const uint32_t m_max = wave_max_u32(act ? sc.m : 0u), m_min = wave_min_u32(act ? sc.m : ~0u);
+  const uint32_t c_max = wave_max_u32(act ? sc.c : 0u), c_min = wave_min_u32(act ? sc.c : ~0u);
 
   double best = -1.0, low = 1.0e300;        // pod lane
   uint32_t idx = 0xffffffffu, ties = 0;
   double ubest = -1.0, ulow = 1.0e300;      // node lane (U nodes)
   uint32_t uidx = 0xffffffffu, uties = 0;
+  uint32_t npart = 0;  // STATS: per-pod-pass nodes of this (wave, chunk)
   // One block: the wave's mask of node nb + lane and its summary (kept for the per-pod pass,
   // read back with v_readlane), loaded together: one memory latency per block.
   auto block = [&](uint32_t nb) {
@@ -1202,37 +1232,11 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
       ts.v[t] = s[64 * (kS2Fs + K + t)];
     }
     if (feas_b == 0) return;  // no pod of the wave can use any node of the block
-    uint64_t fast_b = ballot(mask != 0ull && (h0.w & kSumUni4) != 0u), u_b = 0;
-    if (!uni_max) {
-      // prefix tables for both reciprocal sets (no U nodes: scores differ across the wave)
-      const uint32_t ck = h0.z, bw = h1.x, core = h1.y, pw = h1.z;
-      uint32_t a0 = 0, a1 = 0;
-      lds[lane * PSW + 0] = 0u;
-      lds[TAB + lane * PSW + 0] = 0u;
-#pragma unroll
-      for (int t = 0; t < K; ++t) {
-        const double f = (double)fs.v[t], to = (double)ts.v[t];
-        a0 += 3u * (uint32_t)(f * u_free) + (uint32_t)(to * u_tot);
-        a1 += 3u * (uint32_t)(f * v_free) + (uint32_t)(to * v_tot);
-        lds[lane * PSW + t + 1] = a0;
-        lds[TAB + lane * PSW + t + 1] = a1;
-      }
-      lds[lane * PSW + K + 1] = (uint32_t)((float)bw * u_bw) + (uint32_t)((float)ck * u_bw) +
-                                2u * (uint32_t)((float)core * u_core) +
-                                (uint32_t)((float)pw * u_pow);
-      lds[TAB + lane * PSW + K + 1] = (uint32_t)((float)bw * v_bw) +
-                                      (uint32_t)((float)ck * v_bw) +
-                                      2u * (uint32_t)((float)core * v_core) +
-                                      (uint32_t)((float)pw * v_pow);
-    } else {
-      const double stat = __longlong_as_double((long long)((uint64_t)h0.x | ((uint64_t)h0.y << 32)));
+    uint64_t fast_b = ballot(mask != 0ull && (h0.w & kSumUni4) != 0u), u_b = 0, rec_b = 0;
+    {
       const uint32_t ck = h0.z, meta = h0.w, bw = h1.x, core = h1.y, pw = h1.z;
       const uint32_t cnt = (meta >> 8) & 0xffu;
       const bool fast = mask != 0ull && (meta & kSumUni4) != 0u;
-      // CalculateCardScore terms (algorithm.go:280-291) with the wave's reciprocals
-      const uint32_t shared = (uint32_t)((float)bw * u_bw) + (uint32_t)((float)ck * u_bw) +
-                              2u * (uint32_t)((float)core * u_core) +
-                              (uint32_t)((float)pw * u_pow);
       uint32_t nq_lo = 0, nq_hi = 0;  // qualifying cards for the largest / smallest m
 #pragma unroll
       for (int t = 0; t < K; ++t) {
@@ -1241,36 +1245,141 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
       }
       nq_lo = min(nq_lo, cnt);
       nq_hi = min(nq_hi, cnt);
-      uint32_t acc = 0, sel = 0;  // prefix sums of (3 q_free + q_total) in free order
-      lds[lane * PSW + 0] = 0u;
+      uint32_t thr = 0;  // fs[nq_lo]: a pod with m <= thr qualifies one card more (nq_lo + 1)
 #pragma unroll
-      for (int t = 0; t < K; ++t) {
-        acc += 3u * (uint32_t)((double)fs.v[t] * u_free) + (uint32_t)((double)ts.v[t] * u_tot);
-        lds[lane * PSW + t + 1] = acc;
-        sel = (uint32_t)(t + 1) == nq_lo ? acc : sel;
-      }
-      lds[lane * PSW + K + 1] = shared;
-      const bool q_all = ck >= c_max, q_none = ck < c_min;
-      const bool is_u = fast && mask == live_mask && nq_lo == nq_hi && (q_all || q_none);
-      u_b = ballot(is_u);
-      if (is_u) {
-        const uint32_t basic = q_all ? nq_lo * shared + sel : 0u;  // algorithm.go:271
-        const double raw = (double)basic + stat;                   // algorithm.go:96
-        if (raw > ubest) {
-          ubest = raw;
-          uidx = n;
-          uties = 1;
-        } else if (raw == ubest) {
-          ++uties;
+      for (int t = 0; t < K; ++t) thr = (uint32_t)t == nq_lo ? fs.v[t] : thr;
+      // A one-model node whose qualifying-card count takes at most two values over the wave
+      // (nq_lo, or nq_lo + 1 for the pods with m <= fs[nq_lo]: the free order is descending)
+      // gets a record: the threshold, its clock, the wave's mask, the static part and, per
+      // reciprocal set, both basic scores -- the per-pod pass reads it with three LDS loads.
+      const bool two = fast && nq_hi - nq_lo <= 1u;
+      uint32_t* rec = lds + RECS + lane * REC;
+      if (uni_max) {
+        // CalculateCardScore terms (algorithm.go:280-291) with the wave's reciprocals
+        const uint32_t shared = (uint32_t)((float)bw * u_bw) + (uint32_t)((float)ck * u_bw) +
+                                2u * (uint32_t)((float)core * u_core) +
+                                (uint32_t)((float)pw * u_pow);
+        uint32_t acc = 0, sel = 0, sel_hi = 0;  // prefix sums of (3 q_free + q_total)
+        lds[lane * PSW + 0] = 0u;
+#pragma unroll
+        for (int t = 0; t < K; ++t) {
+          acc += 3u * (uint32_t)((double)fs.v[t] * u_free) + (uint32_t)((double)ts.v[t] * u_tot);
+          lds[lane * PSW + t + 1] = acc;
+          sel = (uint32_t)(t + 1) == nq_lo ? acc : sel;
+          sel_hi = (uint32_t)(t + 1) == nq_hi ? acc : sel_hi;
         }
-        ulow = fmin(ulow, raw);
+        lds[lane * PSW + K + 1] = shared;
+        const double stat =
+            __longlong_as_double((long long)((uint64_t)h0.x | ((uint64_t)h0.y << 32)));
+        const bool q_all = ck >= c_max, q_none = ck < c_min;
+        const bool is_u = fast && mask == act_mask && nq_lo == nq_hi && (q_all || q_none);
+        u_b = ballot(is_u);
+        if (is_u) {
+          const uint32_t basic = q_all ? nq_lo * shared + sel : 0u;  // algorithm.go:271
+          const double raw = (double)basic + stat;                   // algorithm.go:96
+          if (raw > ubest) {
+            ubest = raw;
+            uidx = n;
+            uties = 1;
+          } else if (raw == ubest) {
+            ++uties;
+          }
+          ulow = fmin(ulow, raw);
+        }
+        const bool is_rec = two && !is_u;
+        rec_b = ballot(is_rec);
+        if (is_rec) {
+          *reinterpret_cast<uint4*>(rec) = make_uint4(thr, ck, (uint32_t)mask,
+                                                      (uint32_t)(mask >> 32));
+          *reinterpret_cast<uint4*>(rec + 4) = make_uint4(h0.x, h0.y, nq_lo * shared + sel,
+                                                          nq_hi * shared + sel_hi);
+        }
+      } else {
+        // several reciprocal sets: no U nodes (scores differ across the wave), a record per
+        // two-valued node with the basic scores of every set
+        const bool is_rec = rec_ok && two;
+        rec_b = ballot(is_rec);
+        if (rec_b != 0ull) {
+          if (is_rec) {
+            *reinterpret_cast<uint4*>(rec) = make_uint4(thr, ck, (uint32_t)mask,
+                                                        (uint32_t)(mask >> 32));
+            *reinterpret_cast<uint2*>(rec + 4) = make_uint2(h0.x, h0.y);
+          }
+          for (uint32_t q = 0; q < nsets; ++q) {
+            const uint32_t* r = lds + RCPS + 8 * q;  // the set's reciprocals (broadcast)
+            const float v_bw = __int_as_float((int)r[0]), v_core = __int_as_float((int)r[1]);
+            const float v_pow = __int_as_float((int)r[2]);
+            const double v_free =
+                __longlong_as_double((long long)((uint64_t)r[4] | ((uint64_t)r[5] << 32)));
+            const double v_tot =
+                __longlong_as_double((long long)((uint64_t)r[6] | ((uint64_t)r[7] << 32)));
+            const uint32_t shared = (uint32_t)((float)bw * v_bw) + (uint32_t)((float)ck * v_bw) +
+                                    2u * (uint32_t)((float)core * v_core) +
+                                    (uint32_t)((float)pw * v_pow);
+            uint32_t acc = 0, sel = 0, sel_hi = 0;
+#pragma unroll
+            for (int t = 0; t < K; ++t) {
+              acc += 3u * (uint32_t)((double)fs.v[t] * v_free) +
+                     (uint32_t)((double)ts.v[t] * v_tot);
+              sel = (uint32_t)(t + 1) == nq_lo ? acc : sel;
+              sel_hi = (uint32_t)(t + 1) == nq_hi ? acc : sel_hi;
+            }
+            if (is_rec)
+              *reinterpret_cast<uint2*>(rec + 6 + 2 * q) =
+                  make_uint2(nq_lo * shared + sel, nq_hi * shared + sel_hi);
+          }
+        }
       }
     }
     uint64_t part_b = feas_b & ~u_b;
-    if (STATS && lane == 0) {  // (wave, node) pairs: U, FAST, EXACT (skipped = the rest)
+    if (STATS && !trace && lane == 0) {  // (wave, node) pairs: U, FAST, EXACT (skipped: rest)
       atomicAdd(stats + 2, (unsigned long long)__builtin_popcountll(u_b));
       atomicAdd(stats + 3, (unsigned long long)__builtin_popcountll(part_b & fast_b));
       atomicAdd(stats + 4, (unsigned long long)__builtin_popcountll(part_b & ~fast_b));
+      atomicAdd(stats + 7, (unsigned long long)__builtin_popcountll(rec_b));
+      if (!uni_max) atomicAdd(stats + 8, (unsigned long long)__builtin_popcountll(part_b));
+    }
+    if (STATS) npart += (uint32_t)__builtin_popcountll(part_b);
+    // node order is not kept across the two loops: the tie rule keeps the lowest index.
+    // Branch-free (selects, no exec-mask branches): f = this pod lane is feasible on nn.
+    auto take = [&](bool f, double raw, uint32_t nn) {
+      const bool gt = f && raw > best, eq = f && raw == best;
+      idx = gt ? nn : (eq ? min(idx, nn) : idx);
+      ties = gt ? 1u : ties + (eq ? 1u : 0u);
+      best = gt ? raw : best;
+      low = f && raw < low ? raw : low;  // no NaN here: a compare, not fmin's canonicalizes
+    };
+    uint64_t rb = rec_b;
+    part_b &= ~rec_b;
+    while (rb) {  // four records per trip: all twelve LDS loads in flight before the first use
+      constexpr int R = 4;
+      uint32_t jj[R];
+      bool vv[R];
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        vv[k] = rb != 0ull;
+        jj[k] = vv[k] ? (uint32_t)__builtin_ctzll(rb) : 0u;
+        rb &= rb - 1;
+      }
+      uint4 ra[R];
+      uint2 rs[R], rp[R];
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const uint32_t* r = lds + RECS + jj[k] * REC;
+        ra[k] = *reinterpret_cast<const uint4*>(r);
+        rs[k] = *reinterpret_cast<const uint2*>(r + 4);
+        rp[k] = *reinterpret_cast<const uint2*>(r + 6 + 2 * set);
+      }
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        // basic = nq * shared + prefix[nq] if the clock qualifies (algorithm.go:271-291)
+        const uint32_t bsel = sc.m <= ra[k].x ? rp[k].y : rp[k].x;
+        const uint32_t basic = ra[k].y >= sc.c ? bsel : 0u;
+        const double raw = (double)basic + __longlong_as_double((long long)(
+                                               (uint64_t)rs[k].x | ((uint64_t)rs[k].y << 32)));
+        const uint32_t mw = lane < 32u ? ra[k].z : ra[k].w;  // the wave's mask of the node
+        take(vv[k] && ((mw >> (lane & 31u)) & 1u) != 0u, raw, nb + jj[k]);
+      }
     }
     while (part_b) {  // wave-uniform loop over the remaining feasible nodes
       const int j = __builtin_ctzll(part_b);
@@ -1293,11 +1402,11 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
         const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h0.x, j) |
                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h0.y, j) << 32);
         uint32_t basic;
-        if (grp < 2u) {
-          const uint32_t* tab = lds + grp * TAB + (uint32_t)j * PSW;
+        if (uni_max) {
+          const uint32_t* tab = lds + (uint32_t)j * PSW;
           basic = ckj >= sc.c ? nq * tab[K + 1] + tab[nq] : 0u;
         } else {
-          // a pod outside both sets: Scorer<N32>'s one-model branch on the node lane's data,
+          // several reciprocal sets: Scorer<N32>'s one-model branch on the node lane's data,
           // with its own reciprocals (shared quotients f32, memory quotients f64)
           const uint32_t shared =
             (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.x, j) * sc.r_bw) +
@@ -1319,16 +1428,7 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
       } else {
         raw = sc.template raw<K>(nodes + (size_t)nn * NS);
       }
-      if ((mj >> lane) & 1ull) {
-        if (raw > best) {
-          best = raw;
-          idx = nn;
-          ties = 1;
-        } else if (raw == best) {
-          ++ties;
-        }
-        low = fmin(low, raw);
-      }
+      take(((mj >> lane) & 1ull) != 0ull, raw, nn);
     }
   };
   if (blk) {
@@ -1349,9 +1449,19 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
   } else {
     for (uint32_t nb = n0; nb < n1; nb += kWave) block(nb);
   }
-  if (STATS && lane == 0) {  // (wave, chunk)s with uniform maxima / all
+  if (STATS && !trace && lane == 0) {  // (wave, chunk)s with uniform maxima / all
     atomicAdd(stats + 5, uni_max ? 1ull : 0ull);
     atomicAdd(stats + 6, 1ull);
+    atomicMax(stats + 9, (unsigned long long)npart);
+  }
+  if (trace && lane == 0) {
+    {  // per-(wave, chunk) trace: start, end (100 MHz clock), per-pod nodes
+      unsigned long long* tr = stats + 16 + 4 * ((size_t)(p >> 6) * gridDim.y + chunk);
+      tr[0] = t_start;
+      tr[1] = wall_clock64();
+      tr[2] = npart;
+      tr[3] = uni_max ? 1ull : 0ull;
+    }
   }
   // merge the U nodes (the same for every pod lane) into each pod lane
   double wb = ubest;
@@ -1367,7 +1477,7 @@ __global__ __launch_bounds__(kBlock) void k2_block_n32(
     wl = fmin(wl, __shfl_xor(wl, o, kWave));
   }
   if (!live) return;
-  if (wt > 0) {
+  if (act && wt > 0) {
     if (wb > best) {
       best = wb;
       idx = wi;
@@ -2410,9 +2520,9 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
                               uint32_t n_pods, const uint64_t* bm, uint32_t bm_stride,
                               const BlockMask* bs, uint32_t bs_stride, const Partials& part,
                               int64_t* rows, double* tk_s, uint32_t* tk_i,
-                              unsigned long long* stats, hipStream_t s) {
+                              unsigned long long* stats, const uint32_t* counts, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
-  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
+  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts};
   const MaskSrc ms{bm, bs, bm_stride, bs_stride};
   switch (path) {
     case Path::N32:
@@ -2550,14 +2660,14 @@ hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigne
                      const double* rcp, const float* rcp32, uint32_t n_pods,
                      const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
                      uint32_t bs_stride, const Partials& part, int64_t* rows,
-                     unsigned long long* stats, hipStream_t s) {
+                     unsigned long long* stats, const uint32_t* counts, hipStream_t s) {
   if (rows)
     return launch_k2_t<OUT_ROWS>(K, path, nodes, nullptr, nullptr, 0, n_nodes, chunk_nodes, C, pp, maxima, rcp,
                                  rcp32, n_pods, bm, bm_stride, bs, bs_stride, part, rows, nullptr,
-                                 nullptr, stats, s);
+                                 nullptr, stats, counts, s);
   return launch_k2_t<OUT_ARGMAX>(K, path, nodes, sum2, blk, blk_stride, n_nodes, chunk_nodes, C, pp, maxima, rcp,
                                  rcp32, n_pods, bm, bm_stride, bs, bs_stride, part, rows, nullptr,
-                                 nullptr, stats, s);
+                                 nullptr, stats, counts, s);
 }
 
 hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,

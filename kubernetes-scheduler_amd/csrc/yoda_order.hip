@@ -23,18 +23,45 @@ namespace yoda {
 // is just fast.  The fields are packed at the widths the batch actually uses (host: the OR
 // of each clamped field at upload), so the radix sort runs over bn + bm + bc bits only —
 // same order as the full-width key, fewer passes.
+//
+// Serpentine: memory ascends in the even (clock, number) groups and descends in the odd
+// ones (rank among the batch's groups, host-built sorted list `groups`).  A wave that
+// straddles two groups then holds pods of similar memory from both ends instead of the
+// largest requests of one group next to the smallest of the next: its pods qualify the
+// same cards on most nodes, where a straddling ascending wave spans every memory size and
+// leaves the block K2 nothing but per-pod work.
+__device__ __forceinline__ uint64_t order_key(uint64_t number, uint64_t m_u, uint64_t c_u,
+                                              uint32_t n_shift, uint32_t c_shift,
+                                              const uint32_t* __restrict__ groups,
+                                              uint32_t n_groups) {
+  const uint64_t c = c_u < 0xffffffull ? c_u : 0xffffffull;
+  const uint64_t n = number < 0xffull ? number : 0xffull;
+  uint64_t m = m_u < 0xffffffffull ? m_u : 0xffffffffull;
+  if (groups) {
+    const uint32_t g = (uint32_t)(c << 8) | (uint32_t)n;
+    uint32_t lo = 0, hi = n_groups;  // lower_bound: the group's rank
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (groups[mid] < g) lo = mid + 1; else hi = mid;
+    }
+    const uint64_t m_all = n_shift >= 32 ? 0xffffffffull : (1ull << n_shift) - 1ull;
+    if (lo & 1u) m = m_all - m;  // m <= m_all: n_shift is the width of the batch's m field
+  }
+  return (c << c_shift) | (n << n_shift) | m;
+}
+
 __global__ __launch_bounds__(kBlock) void k_order_keys(const uint64_t* __restrict__ number,
                                                        const uint64_t* __restrict__ m_u,
                                                        const uint64_t* __restrict__ c_u,
                                                        uint32_t n_pods, uint32_t n_shift,
-                                                       uint32_t c_shift, uint64_t* __restrict__ keys,
+                                                       uint32_t c_shift,
+                                                       const uint32_t* __restrict__ groups,
+                                                       uint32_t n_groups,
+                                                       uint64_t* __restrict__ keys,
                                                        uint32_t* __restrict__ idx) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (p >= n_pods) return;
-  const uint64_t c = c_u[p] < 0xffffffull ? c_u[p] : 0xffffffull;
-  const uint64_t n = number[p] < 0xffull ? number[p] : 0xffull;
-  const uint64_t m = m_u[p] < 0xffffffffull ? m_u[p] : 0xffffffffull;
-  keys[p] = (c << c_shift) | (n << n_shift) | m;
+  keys[p] = order_key(number[p], m_u[p], c_u[p], n_shift, c_shift, groups, n_groups);
   idx[p] = p;
 }
 
@@ -44,14 +71,14 @@ __global__ __launch_bounds__(kBlock) void k_order_keys32(const uint64_t* __restr
                                                          const uint64_t* __restrict__ m_u,
                                                          const uint64_t* __restrict__ c_u,
                                                          uint32_t n_pods, uint32_t n_shift,
-                                                         uint32_t c_shift, uint32_t* __restrict__ keys,
+                                                         uint32_t c_shift,
+                                                         const uint32_t* __restrict__ groups,
+                                                         uint32_t n_groups,
+                                                         uint32_t* __restrict__ keys,
                                                          uint32_t* __restrict__ idx) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (p >= n_pods) return;
-  const uint64_t c = c_u[p] < 0xffffffull ? c_u[p] : 0xffffffull;
-  const uint64_t n = number[p] < 0xffull ? number[p] : 0xffull;
-  const uint64_t m = m_u[p] < 0xffffffffull ? m_u[p] : 0xffffffffull;
-  keys[p] = (uint32_t)((c << c_shift) | (n << n_shift) | m);
+  keys[p] = (uint32_t)order_key(number[p], m_u[p], c_u[p], n_shift, c_shift, groups, n_groups);
   idx[p] = p;
 }
 
@@ -84,7 +111,8 @@ size_t order_scratch_bytes(uint32_t n_pods) {
 
 // perm[i] = the original index of the i-th pod in sorted order.
 hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
-                             uint32_t n_pods, const uint32_t key_bits[3], void* scratch,
+                             uint32_t n_pods, const uint32_t key_bits[3],
+                             const uint32_t* groups, uint32_t n_groups, void* scratch,
                              size_t scratch_bytes, uint32_t* perm, hipStream_t s) {
   // key_bits = widths of (c, n, m); each <= its clamp (24, 8, 32), so the total is <= 64
   const uint32_t bc = key_bits[0] < 24 ? key_bits[0] : 24;
@@ -102,14 +130,16 @@ hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const 
     uint32_t* k32_in = reinterpret_cast<uint32_t*>(keys_in);
     uint32_t* k32_out = reinterpret_cast<uint32_t*>(keys_out);
     hipLaunchKernelGGL(k_order_keys32, dim3((n_pods + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                       number, m_u, c_u, n_pods, n_shift, c_shift, k32_in, idx_in);
+                       number, m_u, c_u, n_pods, n_shift, c_shift, n_groups ? groups : nullptr,
+                       n_groups, k32_in, idx_in);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k32_in, k32_out, idx_in, perm,
                                               (int)n_pods, 0, end_bit, s);
   }
   hipLaunchKernelGGL(k_order_keys, dim3((n_pods + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                     number, m_u, c_u, n_pods, n_shift, c_shift, keys_in, idx_in);
+                     number, m_u, c_u, n_pods, n_shift, c_shift, n_groups ? groups : nullptr,
+                     n_groups, keys_in, idx_in);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, perm,

@@ -70,6 +70,7 @@ _SIGS = {
     "yoda_shard_witness_download": ([_vp, _vp, _vp, _vp, _vp], C.c_int),
     "yoda_class_stats_enable": ([_vp, C.c_int], C.c_int),
     "yoda_class_stats_read": ([_vp, _vp], C.c_int),
+    "yoda_k2_trace_read": ([_vp, _vp, C.c_uint64], C.c_int),
     "yoda_greedy_restarts": ([_vp, C.POINTER(C.c_uint32)], C.c_int),
     "yoda_comm_unique_id": ([_vp], C.c_int),
     "yoda_comm_init": ([_vp, _vp, C.c_int, C.c_int], C.c_int),
@@ -285,7 +286,7 @@ class Yoda:
             self._check(lib().yoda_class_stats_enable(self._h, 1 if enable else 0),
                         "yoda_class_stats_enable")
             return None
-        out = np.zeros(10, np.uint64)
+        out = np.zeros(13, np.uint64)
         self._check(lib().yoda_class_stats_read(self._h, _np_ptr(out)), "yoda_class_stats_read")
         v = [int(x) for x in out]
         pairs = max(v[9], 1)
@@ -293,7 +294,15 @@ class Yoda:
                 "k2": {"skipped": v[6] / pairs, "u": v[3] / pairs, "fast": v[4] / pairs,
                        "exact": v[5] / pairs},
                 "k2_uniform_maxima_wave_chunks": v[7] / max(v[8], 1),
+                "k2_fast_records": v[10] / pairs, "k2_per_pod_nonuniform": v[11] / pairs,
+                "k2_max_per_pod_nodes_wave_chunk": v[12],
                 "wave_node_pairs": v[9]}
+
+    def k2_trace(self, n_slots: int) -> np.ndarray:
+        """[n_slots, 4] u64 per-(wave, chunk) K2 trace (YODA_K2_TRACE, diagnostic)."""
+        out = np.zeros((n_slots, 4), np.uint64)
+        self._check(lib().yoda_k2_trace_read(self._h, _np_ptr(out), n_slots), "yoda_k2_trace_read")
+        return out
 
     def profile(self, enable: bool = True):
         self._check(lib().yoda_profile(self._h, 1 if enable else 0), "yoda_profile")

@@ -78,6 +78,8 @@ def main():
     mx = res.maxima  # [P][6] in collection.go order: bw, clock, core, free, power, total
     key_m = mx[:, [0, 2, 3, 4, 5]]
     k2 = {"skip": 0, "u": 0, "fast": 0, "exact": 0}
+    extra = {"fast_rec": 0, "nonuni_feasible": 0}
+    per_wave = []
     uni_waves = 0
     for w0 in range(0, P, 64):
         sl = slice(w0, min(w0 + 64, P))
@@ -94,6 +96,8 @@ def main():
         k2["skip"] += int((~anyf).sum())
         if not uni:
             k2["exact"] += int(anyf.sum())
+            extra["nonuni_feasible"] += int(anyf.sum())
+            per_wave.append(int(anyf.sum()))
             continue
         nq_lo = (fs >= mm.max()).sum(axis=1)
         nq_hi = (fs >= mm.min()).sum(axis=1)
@@ -101,9 +105,15 @@ def main():
         u = allf & (nq_lo == nq_hi) & (qall | qnone)
         k2["u"] += int(u.sum())
         k2["fast"] += int((anyf & ~u).sum())
+        extra["fast_rec"] += int((anyf & ~u & (nq_hi - nq_lo <= 1)).sum())
+        per_wave.append(int((anyf & ~u).sum()))
     tot = sum(k2.values())
     print("K2 (wave, node) pairs:", {k: f"{v / tot:.4f}" for k, v in k2.items()},
-          f"uniform-maxima waves {uni_waves}/{(P + 63) // 64}")
+          f"uniform-maxima waves {uni_waves}/{(P + 63) // 64}",
+          {k: f"{v / tot:.4f}" for k, v in extra.items()})
+    pw = np.array(per_wave)
+    print("per-pod nodes per wave: mean %.0f p50 %.0f p90 %.0f p99 %.0f max %d (of %d nodes)" % (
+        pw.mean(), np.percentile(pw, 50), np.percentile(pw, 90), np.percentile(pw, 99), pw.max(), N))
 
 
 if __name__ == "__main__":
