@@ -1447,8 +1447,8 @@ int yoda_class_stats_enable(yoda_t* h, int enable) {
     const size_t bytes = (16 + 4 * (size_t)tr) * 8;
     HIP_TRY(h, h->stats_dev.ensure(bytes));
     HIP_TRY(h, hipMemsetAsync(h->stats_dev.p, 0, bytes, h->stream));
-    if (tr) {
-      const uint64_t one = 1;
+    if (tr) {  // YODA_K1_TRACE set: the K1 records it instead of the K2
+      const uint64_t one = env_u32("YODA_K1_TRACE", 0) ? 2 : 1;
       HIP_TRY(h, hipMemcpyAsync(h->stats_dev.as<uint64_t>() + 15, &one, 8,
                                 hipMemcpyHostToDevice, h->stream));
       HIP_TRY(h, hipStreamSynchronize(h->stream));

@@ -499,7 +499,10 @@ __global__ __launch_bounds__(kWave) void k_reduce_wit(const uint64_t* __restrict
 // approximations: ALL nodes fold their contribution into node-lane maxima that are reduced
 // across the wave once per chunk, and both write their 64-bit masks with one store.
 template <int K, bool STATS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 ? 6 : 8))) void k1_block_n32(
+#ifndef YODA_K1_WAVES
+#define YODA_K1_WAVES 8
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 ? 5 : YODA_K1_WAVES))) void k1_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum,
     uint32_t n_nodes, uint32_t chunk_nodes, const uint32_t* __restrict__ m_in,
     const uint32_t* __restrict__ c_in, const uint64_t* __restrict__ number_in,
@@ -511,7 +514,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
   constexpr uint32_t SS = k1sum_stride(K);
   constexpr uint32_t NS = n32_stride(K);
   constexpr uint32_t HW = K + 1;  // LDS words per node: hfs[0..K-1], 0
-  __shared__ uint32_t lds_all[kBlock / kWave][kWave * HW];
+  // + a 10-word record per one-model PART node (below): the per-pod pass reads it from LDS
+  constexpr uint32_t REC = 10, RECS = kWave * HW;
+  __shared__ __attribute__((aligned(16))) uint32_t lds_all[kBlock / kWave][RECS + kWave * REC];
   uint32_t* lds = lds_all[threadIdx.x >> 6];
   const uint32_t lane = lane_id();
   const Tile tl = tile();
@@ -524,6 +529,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
   if (live_mask == 0) return;  // a wave past the batch: no bitmask row, no partials
   uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
   BlockMask* bsw = bs + (size_t)uniform_u32(p >> 6) * bs_stride;
+  // STATS with stats[15] == 2: per-(wave, chunk) timing trace only (no counter atomics)
+  const bool trace = STATS && stats[15] == 2ull;
+  const uint64_t t_start = STATS ? wall_clock64() : 0ull;
+  uint32_t npart = 0;
 
   uint32_t m = 0, c = 0, need_mem = 0, need_clk = 0;
   uint64_t number = ~0ull;
@@ -614,7 +623,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
         valid && !feas_none && feas_all && uni4 && (qual_none || (qual_all && unit));
     const uint64_t all_b = ballot(is_all), none_b = ballot(is_none);
     uint64_t part_b = ballot(valid) & ~all_b & ~none_b;
-    if (STATS && lane == 0) {  // class counts of (wave, node) pairs: ALL, NONE (PART = rest)
+    if (STATS && !trace && lane == 0) {  // class counts of (wave, node) pairs: ALL, NONE
       atomicAdd(stats + 0, (unsigned long long)__builtin_popcountll(all_b));
       atomicAdd(stats + 1, (unsigned long long)__builtin_popcountll(none_b));
     }
@@ -630,45 +639,78 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
     }
     uint32_t lo = is_all ? (uint32_t)live_mask : 0u;
     uint32_t hi = is_all ? (uint32_t)(live_mask >> 32) : 0u;
-    while (part_b) {  // wave-uniform loop over the nodes the bounds could not decide
+    if (STATS) npart += (uint32_t)__builtin_popcountll(part_b);
+    // One-model PART nodes: a record of the node's facts in LDS -- {CardNumber lo, hi,
+    // clock, meta, max free + 1, hfs[need - 1], bandwidth, core, power, total} -- read by
+    // the per-pod pass with broadcast loads, four nodes per trip, branch-free.
+    const bool one_model = (meta & (kSumUni4 | kSumUniTotal)) == (kSumUni4 | kSumUniTotal);
+    const uint64_t rec_b = part_b & ballot(one_model);
+    if (rec_b != 0ull && ((rec_b >> lane) & 1ull)) {
+      uint32_t* r = lds + RECS + lane * REC;
+      *reinterpret_cast<uint2*>(r + 0) = make_uint2(w0.x, w0.y);
+      *reinterpret_cast<uint2*>(r + 2) = make_uint2(ck, meta);
+      *reinterpret_cast<uint2*>(r + 4) = make_uint2(mrf1, hfs_all_ok ? t_all : 0u);
+      *reinterpret_cast<uint2*>(r + 6) = make_uint2(bw, core);
+      *reinterpret_cast<uint2*>(r + 8) = make_uint2(pw, tot);
+    }
+    // the pod lane's hfs slot of its need (slot K: no such card, 0) for the LDS rows
+    const uint32_t hk = need_mem == 0u ? (uint32_t)K : min(need_mem, (uint32_t)K + 1u) - 1u;
+    uint64_t rb = rec_b;
+    while (rb) {
+#ifndef YODA_K1_R
+#define YODA_K1_R 2
+#endif
+      constexpr int R = YODA_K1_R;
+      uint32_t jj[R];
+      bool vv[R];
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        vv[k] = rb != 0ull;
+        jj[k] = vv[k] ? (uint32_t)__builtin_ctzll(rb) : 0u;
+        rb &= rb - 1;
+      }
+      uint2 r0[R], r1[R], r2[R], r3[R], r4[R];
+      uint32_t th[R];
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const uint32_t* r = lds + RECS + jj[k] * REC;
+        r0[k] = *reinterpret_cast<const uint2*>(r + 0);
+        r1[k] = *reinterpret_cast<const uint2*>(r + 2);
+        r2[k] = *reinterpret_cast<const uint2*>(r + 4);
+        r3[k] = *reinterpret_cast<const uint2*>(r + 6);
+        r4[k] = *reinterpret_cast<const uint2*>(r + 8);
+        // hfs[need-1] of node j: its lane's (uniform need), or the pod's slot of the row
+        th[k] = need_uni ? r2[k].y : lds[jj[k] * HW + hk];
+      }
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const uint64_t cnj = (uint64_t)r0[k].x | ((uint64_t)r0[k].y << 32);
+        const uint32_t ckj = r1[k].x, mj = r1[k].y, mrfj = r2[k].x;
+        // PodFitsNumber / Memory (CardFitsMemory count >= need <=> hfs[need-1] > m) / Clock
+        // (bitwise, not short-circuit: selects, no exec-mask branches)
+        const bool fn = number <= cnj;
+        const bool fm = (need_mem == 0u) | (th[k] > m);
+        const bool fc = (need_clk == 0u) | ((ckj == c) & (((mj >> 8) & 0xffu) >= need_clk));
+        const bool f = vv[k] & live & fn & fm & fc;
+        nf += f ? 1u : 0u;
+        nz += (f & ((mj & kSumZeroTotal) != 0u)) ? 1u : 0u;
+        const bool q = f & (ckj >= c) & (mrfj > m);  // collection.go:46, one-model node
+        mx[kMaxBw] = max(mx[kMaxBw], q ? r3[k].x : 0u);
+        mx[kMaxClock] = max(mx[kMaxClock], q ? ckj : 0u);
+        mx[kMaxCore] = max(mx[kMaxCore], q ? r3[k].y : 0u);
+        mx[kMaxFree] = max(mx[kMaxFree], q ? mrfj - 1u : 0u);
+        mx[kMaxPower] = max(mx[kMaxPower], q ? r4[k].x : 0u);
+        mx[kMaxTotal] = max(mx[kMaxTotal], q ? r4[k].y : 0u);
+        const uint64_t b = ballot(f);
+        if (vv[k]) set_lane(lo, hi, b, jj[k]);
+      }
+    }
+    part_b &= ~rec_b;
+    while (part_b) {  // mixed-model nodes: the exact per-card predicates from the record
       const int j = __builtin_ctzll(part_b);
       part_b &= part_b - 1;
-      const uint32_t mj = (uint32_t)__builtin_amdgcn_readlane((int)meta, j);
-      bool f;
-      if ((mj & (kSumUni4 | kSumUniTotal)) == (kSumUni4 | kSumUniTotal)) {
-        // one-model node: the same predicates from the node lane's summary (no memory
-        // round trip): CardFitsMemory count >= need  <=>  hfs[need-1] > m
-        const uint64_t cnj =
-            (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)w0.x, j) |
-            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)w0.y, j) << 32);
-        const uint32_t ckj = (uint32_t)__builtin_amdgcn_readlane((int)ck, j);
-        const uint32_t mrfj = (uint32_t)__builtin_amdgcn_readlane((int)mrf1, j);
-        uint32_t th;
-        if (need_uni) {  // hfs[need-1] of node j from its lane (a need beyond K: no such card)
-          const uint32_t tj = (uint32_t)__builtin_amdgcn_readlane((int)t_all, j);
-          th = hfs_all_ok ? tj : 0u;
-        } else {
-          const uint32_t hk = need_mem == 0u ? (uint32_t)K : min(need_mem, (uint32_t)K + 1u) - 1u;
-          th = lds[(uint32_t)j * HW + hk];
-        }
-        f = live && number <= cnj && (need_mem == 0u || th > m) &&
-            (need_clk == 0u || (ckj == c && ((mj >> 8) & 0xffu) >= need_clk));
-        if (f) {
-          ++nf;
-          nz += (mj & kSumZeroTotal) ? 1u : 0u;
-          if (ckj >= c && mrfj > m) {  // collection.go:46, one-model node
-            mx[kMaxBw] = max(mx[kMaxBw], (uint32_t)__builtin_amdgcn_readlane((int)bw, j));
-            mx[kMaxClock] = max(mx[kMaxClock], ckj);
-            mx[kMaxCore] = max(mx[kMaxCore], (uint32_t)__builtin_amdgcn_readlane((int)core, j));
-            mx[kMaxFree] = max(mx[kMaxFree], mrfj - 1u);
-            mx[kMaxPower] = max(mx[kMaxPower], (uint32_t)__builtin_amdgcn_readlane((int)pw, j));
-            mx[kMaxTotal] = max(mx[kMaxTotal], (uint32_t)__builtin_amdgcn_readlane((int)tot, j));
-          }
-        }
-      } else {
-        f = k1_node_lean<K>(nodes + (size_t)(nb + (uint32_t)j) * NS, m, c, number, need_mem,
-                            need_clk, mx, nf, nz) && live;
-      }
+      const bool f = k1_node_lean<K>(nodes + (size_t)(nb + (uint32_t)j) * NS, m, c, number,
+                                     need_mem, need_clk, mx, nf, nz) && live;
       const uint64_t b = ballot(f);
       set_lane(lo, hi, b, (uint32_t)j);
     }
@@ -690,6 +732,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
     }
   }
   blk_flush();
+  if (trace && lane == 0) {
+    unsigned long long* tr = stats + 16 + 4 * ((size_t)(p >> 6) * C + chunk);
+    tr[0] = t_start;
+    tr[1] = wall_clock64();
+    tr[2] = npart;
+    tr[3] = 0ull;
+  }
   // fold the ALL nodes into every pod lane
   a_bw = wave_max_u32(a_bw);
   a_ck = wave_max_u32(a_ck);
@@ -1139,7 +1188,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   const uint64_t live_mask = ballot(live);
   if (live_mask == 0) return;  // a wave past the batch
   // STATS with stats[15] set: the timing trace only (no per-block counter atomics)
-  const bool trace = STATS && stats[15] != 0ull;
+  const bool trace = STATS && stats[15] == 1ull;
   const uint64_t t_start = STATS ? wall_clock64() : 0ull;
   const uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
   const BlockMask* bsw = bs ? bs + (size_t)uniform_u32(p >> 6) * bs_stride : nullptr;

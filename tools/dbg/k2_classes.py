@@ -39,7 +39,8 @@ if os.environ.get("YODA_K2_TRACE"):
     y.class_stats(False)
     tr = y.k2_trace(int(os.environ["YODA_K2_TRACE"])).astype(np.int64)
     os.makedirs("gpurun_out", exist_ok=True)
-    np.save("gpurun_out/k2_trace.npy", tr)
+    np.save("gpurun_out/k1_trace.npy" if os.environ.get("YODA_K1_TRACE") else
+            "gpurun_out/k2_trace.npy", tr)
     live = tr[:, 1] > 0
     t = tr[live]
     t0 = t[:, 0].min()
