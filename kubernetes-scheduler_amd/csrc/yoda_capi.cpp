@@ -119,9 +119,14 @@ hipError_t launch_max_multi(const PtrList& src, uint32_t k, uint64_t n, uint64_t
                             hipStream_t s);
 size_t order_scratch_bytes(uint32_t n_pods);
 hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
-                             uint32_t n_pods, const uint32_t key_bits[3],
-                             const uint32_t* groups, uint32_t n_groups, void* scratch,
+                             const uint32_t* need_mem, uint32_t n_pods, const uint32_t key_bits[3],
+                             const uint64_t* groups, uint32_t n_groups, void* scratch,
                              size_t scratch_bytes, uint32_t* perm, hipStream_t s);
+hipError_t launch_order_count(const OrderMeta& o, const uint64_t* number, const uint64_t* m_u,
+                              const uint64_t* c_u, const uint32_t* need_mem, uint32_t n_pods,
+                              uint32_t* hist, uint32_t* bstart, uint32_t* slot, uint32_t* bkt,
+                              const PermTable& t, const uint32_t* pad, uint32_t n_pad,
+                              uint32_t* perm, hipStream_t s);
 hipError_t launch_permute(const PermTable& t, const uint32_t* perm, uint32_t n_pods, bool scatter,
                           hipStream_t s);
 }  // namespace yoda
@@ -270,10 +275,17 @@ struct yoda_handle {
   bool ordered = false;
   DevBuf pod_sorted, perm, order_scratch;
   uint32_t key_bits[3] = {24, 8, 32};  // widths of the batch's sort-key fields (c, n, m)
-  // the batch's distinct (clock, number) key groups, ascending (serpentine order, see
-  // yoda_order.hip): host copy kept alive for the async upload
-  DevBuf order_groups;
-  std::vector<uint32_t> order_groups_host;
+  // Counting-sort order (yoda_order.hip, OrderMeta), built at upload: the batch's distinct
+  // (clock, number, has-memory) groups ascending, their first sorted positions unpadded and
+  // padded to a wave, and the padding slots (dst, src) -- one device blob, host copy kept
+  // for the async upload.  n_work: the sorted positions of this run (n_pad when padded).
+  bool og_ok = false;
+  uint32_t og_groups = 0, og_nb_log2 = 0, og_m_shift = 0, og_n_pad_slots = 0;
+  uint32_t n_pad = 0, n_work = 0;
+  size_t og_off_start = 0, og_off_start_pad = 0, og_off_pad = 0;
+  std::vector<unsigned char> og_host;
+  DevBuf order_meta, order_hist, order_bstart, order_slot, order_bkt;
+  size_t sorted_off[kPodArrays] = {};
 
   // state
   DevBuf maxima, counts, rcp, rcp32, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
@@ -337,7 +349,8 @@ struct yoda_handle {
     if (comm && rccl().ok) (void)rccl().comm_destroy(comm);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &pod_blob,   &maxima,       &counts,
-                     &pod_sorted, &perm,     &order_scratch, &order_groups,
+                     &pod_sorted, &perm,     &order_scratch, &order_meta, &order_hist,
+                     &order_bstart, &order_slot, &order_bkt,
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
                      &n_flagged, &bitmask,   &bitmask_t,  &blk,  &bsum, &p_max_u,      &p_cnt,
@@ -469,18 +482,19 @@ int ensure_state(yoda_t* h, uint32_t P) {
 
 PodParams pod_params(yoda_t* h) {
   unsigned char* b = (h->ordered ? h->pod_sorted : h->pod_blob).as<unsigned char>();
+  const size_t* off = h->ordered ? h->sorted_off : h->pod_off;
   PodParams pp;
-  pp.m_f = reinterpret_cast<double*>(b + h->pod_off[kPodMF]);
-  pp.c_f = reinterpret_cast<double*>(b + h->pod_off[kPodCF]);
-  pp.m_u = reinterpret_cast<uint64_t*>(b + h->pod_off[kPodMU]);
-  pp.c_u = reinterpret_cast<uint64_t*>(b + h->pod_off[kPodCU]);
-  pp.m_32 = reinterpret_cast<uint32_t*>(b + h->pod_off[kPodM32]);
-  pp.c_32 = reinterpret_cast<uint32_t*>(b + h->pod_off[kPodC32]);
-  pp.number = reinterpret_cast<uint64_t*>(b + h->pod_off[kPodNumber]);
-  pp.need_mem = reinterpret_cast<uint32_t*>(b + h->pod_off[kPodNeedMem]);
-  pp.need_clk = reinterpret_cast<uint32_t*>(b + h->pod_off[kPodNeedClk]);
-  pp.alpha = reinterpret_cast<double*>(b + h->pod_off[kPodAlpha]);
-  pp.beta = reinterpret_cast<double*>(b + h->pod_off[kPodBeta]);
+  pp.m_f = reinterpret_cast<double*>(b + off[kPodMF]);
+  pp.c_f = reinterpret_cast<double*>(b + off[kPodCF]);
+  pp.m_u = reinterpret_cast<uint64_t*>(b + off[kPodMU]);
+  pp.c_u = reinterpret_cast<uint64_t*>(b + off[kPodCU]);
+  pp.m_32 = reinterpret_cast<uint32_t*>(b + off[kPodM32]);
+  pp.c_32 = reinterpret_cast<uint32_t*>(b + off[kPodC32]);
+  pp.number = reinterpret_cast<uint64_t*>(b + off[kPodNumber]);
+  pp.need_mem = reinterpret_cast<uint32_t*>(b + off[kPodNeedMem]);
+  pp.need_clk = reinterpret_cast<uint32_t*>(b + off[kPodNeedClk]);
+  pp.alpha = reinterpret_cast<double*>(b + off[kPodAlpha]);
+  pp.beta = reinterpret_cast<double*>(b + off[kPodBeta]);
   return pp;
 }
 
@@ -512,32 +526,76 @@ int check_ready(yoda_t* h, int mode) {
 
 // Batches above this size are sorted (below it a batch fills at most one wave).
 constexpr uint32_t kOrderMinPods = 2 * kWave;
+// Groups x memory buckets of the counting-sort order (its LDS histogram: 64 KiB); a batch
+// with more (clock, number, has-memory) groups takes the radix sort without padding.
+constexpr uint32_t kOrderMaxGroups = 16384;
 
 // Sort the batch by its Filter inputs and gather the pod arrays (yoda_order.hip).  Runs on
-// the device inside every run, so its cost is part of the measured step.
+// the device inside every run, so its cost is part of the measured step.  The counting
+// sort (groups built at upload) fills h->n_work sorted positions: n_pad when the run pads
+// its groups to whole waves (prepare_run), else n_pods; the radix sort is the fallback for
+// batches with too many groups.
 int order_pods(yoda_t* h, int mode) {
-  const uint32_t P = h->n_pods;
+  const uint32_t P = h->n_pods, W = h->n_work;
   h->ordered = false;
   if (!h->order_enabled || mode != YODA_MODE_SCV || P < kOrderMinPods || h->n_nodes == 0)
     return YODA_OK;
   const unsigned char* b = h->pod_blob.as<unsigned char>();
-  const size_t scratch = order_scratch_bytes(P);
-  HIP_TRY(h, h->order_scratch.ensure(scratch));
-  HIP_TRY(h, h->perm.ensure((size_t)P * 4));
-  HIP_TRY(h, h->pod_sorted.ensure(h->pod_blob.bytes));
-  HIP_TRY(h, launch_order_pods(reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodNumber]),
-                               reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodMU]),
-                               reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodCU]), P,
-                               h->key_bits, h->order_groups.as<uint32_t>(),
-                               (uint32_t)h->order_groups_host.size(), h->order_scratch.p, h->order_scratch.bytes,
-                               h->perm.as<uint32_t>(), h->stream));
+  HIP_TRY(h, h->perm.ensure((size_t)W * 4));
+  size_t total = 0;
+  for (int a = 0; a < kPodArrays; ++a) {
+    h->sorted_off[a] = total;
+    total += ((size_t)W * kPodArrayBytes[a] + 255) / 256 * 256;
+  }
+  HIP_TRY(h, h->pod_sorted.ensure(total));
   PermTable t{};
   for (int a = 0; a < kPodArrays; ++a) {
     t.src[t.n] = b + h->pod_off[a];
-    t.dst[t.n] = h->pod_sorted.as<unsigned char>() + h->pod_off[a];
+    t.dst[t.n] = h->pod_sorted.as<unsigned char>() + h->sorted_off[a];
     t.bytes[t.n] = (uint32_t)kPodArrayBytes[a];
     ++t.n;
   }
+  // The counting sort's order inside a bucket follows its atomics (not reproducible from
+  // one run to the next): only the padded single-handle run uses it.  Every other entry
+  // point takes the radix sort, whose order is a function of the batch alone -- shards of
+  // one batch on several GPUs must agree on it.
+  if (h->og_ok && W != P) {
+    const bool padded = true;
+    HIP_TRY(h, h->order_slot.ensure((size_t)P * 4));
+    HIP_TRY(h, h->order_bkt.ensure((size_t)P * 4));
+    const unsigned char* meta = h->order_meta.as<unsigned char>();
+    OrderMeta o;
+    o.groups = reinterpret_cast<const uint64_t*>(meta);
+    o.gstart = reinterpret_cast<const uint32_t*>(meta + (padded ? h->og_off_start_pad
+                                                                : h->og_off_start));
+    o.n_groups = h->og_groups;
+    o.nb_log2 = h->og_nb_log2;
+    o.m_shift = h->og_m_shift;
+    HIP_TRY(h, launch_order_count(o, reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodNumber]),
+                                  reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodMU]),
+                                  reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodCU]),
+                                  reinterpret_cast<const uint32_t*>(b + h->pod_off[kPodNeedMem]),
+                                  P, h->order_hist.as<uint32_t>(), h->order_bstart.as<uint32_t>(),
+                                  h->order_slot.as<uint32_t>(), h->order_bkt.as<uint32_t>(), t,
+                                  reinterpret_cast<const uint32_t*>(meta + h->og_off_pad),
+                                  padded ? h->og_n_pad_slots : 0u, h->perm.as<uint32_t>(),
+                                  h->stream));
+    h->ordered = true;
+    return YODA_OK;
+  }
+  if (W != P) return fail(h, YODA_ERR_STATE, "padded order without its groups");
+  const size_t scratch = order_scratch_bytes(P);
+  HIP_TRY(h, h->order_scratch.ensure(scratch));
+  HIP_TRY(h, launch_order_pods(reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodNumber]),
+                               reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodMU]),
+                               reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodCU]),
+                               reinterpret_cast<const uint32_t*>(b + h->pod_off[kPodNeedMem]), P,
+                               h->key_bits,
+                               h->og_ok ? reinterpret_cast<const uint64_t*>(
+                                              h->order_meta.as<unsigned char>())
+                                        : nullptr,
+                               h->og_ok ? h->og_groups : 0u, h->order_scratch.p,
+                               h->order_scratch.bytes, h->perm.as<uint32_t>(), h->stream));
   HIP_TRY(h, launch_permute(t, h->perm.as<uint32_t>(), P, false, h->stream));
   h->ordered = true;
   return YODA_OK;
@@ -545,7 +603,7 @@ int order_pods(yoda_t* h, int mode) {
 
 // Scatter the per-pod outputs of an ordered run back to the caller's pod order.
 int unpermute_outputs(yoda_t* h) {
-  const uint32_t P = h->n_pods;
+  const uint32_t P = h->n_pods, W = h->n_work;  // W sorted positions (copies: same values)
   if (!h->ordered || P == 0) return YODA_OK;
   // Scatter every row into a second buffer of the same shape, then swap the two: no copy
   // back (the swapped-out buffers become the next scatter's targets).
@@ -560,22 +618,23 @@ int unpermute_outputs(yoda_t* h) {
                       {&h->best, &h->best_alt, 1, 8},         {&h->maxima, &h->maxima_alt, 6, 8}};
   PermTable t{};
   for (const Arr& a : arrs) {
-    HIP_TRY(h, a.alt->ensure((size_t)a.rows * P * a.bytes));
+    // sized like the buffer it is swapped with (no reallocation from one run to the next)
+    HIP_TRY(h, a.alt->ensure(std::max(a.buf->bytes, (size_t)a.rows * W * a.bytes)));
     for (uint32_t r = 0; r < a.rows; ++r) {
-      t.src[t.n] = a.buf->as<unsigned char>() + (size_t)r * P * a.bytes;
+      t.src[t.n] = a.buf->as<unsigned char>() + (size_t)r * W * a.bytes;
       t.dst[t.n] = a.alt->as<unsigned char>() + (size_t)r * P * a.bytes;
       t.bytes[t.n] = a.bytes;
       ++t.n;
     }
   }
-  HIP_TRY(h, launch_permute(t, h->perm.as<uint32_t>(), P, true, h->stream));
+  HIP_TRY(h, launch_permute(t, h->perm.as<uint32_t>(), W, true, h->stream));
   for (const Arr& a : arrs) std::swap(*a.buf, *a.alt);
   return YODA_OK;
 }
 
 // Phase 1: Filter + PreScore maxima (Mode A), or the all-feasible state (Mode B).
 int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts) {
-  const uint32_t P = h->n_pods;
+  const uint32_t P = h->n_work;  // sorted positions of this run
   if (P == 0) return YODA_OK;
   if (mode == YODA_MODE_DISKIO) {
     HIP_TRY(h, launch_fill_diskio_state(P, h->n_nodes, maxima, counts, h->stream));
@@ -647,7 +706,7 @@ int phase1_witness(yoda_t* h, uint64_t* maxima, uint32_t* counts, uint32_t* wit,
 // NULL: unknown): a pod with none takes no part in the block K2's wave bounds.
 int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, int64_t* best,
            uint32_t* idx, uint32_t* ties, int64_t* low, int64_t* rows = nullptr) {
-  const uint32_t P = h->n_pods;
+  const uint32_t P = h->n_work;  // sorted positions of this run
   if (P == 0) return YODA_OK;
   if (h->n_nodes == 0) {
     std::vector<int64_t> neg(P, -1), big(P, INT64_MAX);
@@ -694,7 +753,7 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
 // Finalize into the handle's pick/status/ties; runs K3 for generic-path overflow pods.
 int finalize(yoda_t* h, int mode, const uint32_t* counts, const int64_t* best,
              const uint32_t* idx, const uint32_t* ties, const int64_t* low, bool sharded) {
-  const uint32_t P = h->n_pods;
+  const uint32_t P = h->n_work;  // sorted positions of this run
   if (P == 0) return YODA_OK;
   const bool generic = h->generic && mode == YODA_MODE_SCV;
   HIP_TRY(h, hipMemsetAsync(h->n_flagged.p, 0, 4, h->stream));
@@ -1086,33 +1145,39 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     uint32_t* nc = reinterpret_cast<uint32_t*>(st + off[kPodNeedClk]);
     const uint64_t kClamp = 1ull << 53;  // > every F64-path card field (<= 2^44)
     uint64_t key_or[3] = {0, 0, 0};       // OR of the sort key's clamped fields (c, n, m)
-    // distinct (clock, number) key groups: open-addressing set of group + 1 (0 = empty)
-    std::vector<uint32_t> gset(256, 0u);
+    // distinct (clock, number, has-memory) groups with their pod counts: open addressing on
+    // key + 1 (0 = empty); consecutive pods of one group (the common case) skip the probe
+    std::vector<uint64_t> gkey(256, 0ull);
+    std::vector<uint32_t> gcnt(256, 0u);
     size_t g_n = 0;
-    auto g_insert = [&](uint32_t g) {
-      for (;;) {
-        const size_t mask = gset.size() - 1;
-        size_t i = (size_t)(g * 0x9e3779b1u) & mask;
-        while (gset[i] != 0u && gset[i] != g + 1u) i = (i + 1) & mask;
-        if (gset[i] != 0u) return;
-        if (2 * (g_n + 1) <= gset.size()) {
-          gset[i] = g + 1u;
-          ++g_n;
-          return;
-        }
-        std::vector<uint32_t> old(gset.size() * 2, 0u);  // grow and rehash
-        old.swap(gset);
-        g_n = 0;
-        for (uint32_t v : old)
-          if (v) {
-            size_t j = (size_t)((v - 1u) * 0x9e3779b1u) & (gset.size() - 1);
-            while (gset[j] != 0u) j = (j + 1) & (gset.size() - 1);
-            gset[j] = v;
-            ++g_n;
-          }
-      }
+    auto g_slot = [&](uint64_t k1) {
+      size_t i = (size_t)(k1 * 0x9e3779b97f4a7c15ull >> 40) & (gkey.size() - 1);
+      while (gkey[i] != 0ull && gkey[i] != k1) i = (i + 1) & (gkey.size() - 1);
+      return i;
     };
-    uint32_t g_last = 0xffffffffu;
+    uint64_t g_last = ~0ull;
+    uint32_t g_run = 0;
+    auto g_add = [&](uint64_t g, uint32_t c) {
+      size_t i = g_slot(g + 1);
+      if (gkey[i] == 0ull) {
+        if (2 * (g_n + 1) > gkey.size()) {  // grow and rehash
+          std::vector<uint64_t> ok(gkey.size() * 2, 0ull);
+          std::vector<uint32_t> oc(gcnt.size() * 2, 0u);
+          ok.swap(gkey);
+          oc.swap(gcnt);
+          for (size_t j = 0; j < ok.size(); ++j)
+            if (ok[j]) {
+              const size_t t = g_slot(ok[j]);
+              gkey[t] = ok[j];
+              gcnt[t] = oc[j];
+            }
+          i = g_slot(g + 1);
+        }
+        gkey[i] = g + 1;
+        ++g_n;
+      }
+      gcnt[i] += c;
+    };
     for (uint32_t p = 0; p < P; ++p) {
       const uint64_t number = pd->has_number[p] ? pd->number[p] : 1;  // filter.go:12-15
       const uint64_t m = pd->has_memory[p] ? pd->memory[p] : 0;       // filter.go:19,32
@@ -1130,10 +1195,14 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
       key_or[0] |= std::min<uint64_t>(c, 0xffffffull);  // the clamps of k_order_keys
       key_or[1] |= std::min<uint64_t>(number, 0xffull);
       key_or[2] |= std::min<uint64_t>(m, 0xffffffffull);
-      const uint32_t g = (uint32_t)(std::min<uint64_t>(c, 0xffffffull) << 8) |
-                         (uint32_t)std::min<uint64_t>(number, 0xffull);
-      if (g != g_last) g_insert(g);
-      g_last = g;
+      const uint64_t g = (std::min<uint64_t>(c, 0xffffffull) << 9) |
+                         (std::min<uint64_t>(number, 0xffull) << 1) | (nm[p] != 0u ? 1u : 0u);
+      if (g != g_last) {
+        if (g_run) g_add(g_last, g_run);
+        g_last = g;
+        g_run = 0;
+      }
+      ++g_run;
       al[p] = be[p] = 0.0;
       if (pd->rio && pd->rcpu) {  // algorithm.go:105-106
         const double beta = 1.0 / (1.0 + (double)pd->rcpu[p] / pd->rio[p]);
@@ -1141,16 +1210,60 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
         al[p] = 1 - beta;
       }
     }
-    h->order_groups_host.clear();
-    for (uint32_t v : gset)
-      if (v) h->order_groups_host.push_back(v - 1u);
-    std::sort(h->order_groups_host.begin(), h->order_groups_host.end());
+    if (g_run) g_add(g_last, g_run);
     HIP_TRY(h, hipMemcpyAsync(h->pod_blob.p, st, total, hipMemcpyHostToDevice, h->stream));
-    if (!h->order_groups_host.empty()) {
-      HIP_TRY(h, h->order_groups.ensure(h->order_groups_host.size() * 4));
-      HIP_TRY(h, hipMemcpyAsync(h->order_groups.p, h->order_groups_host.data(),
-                                h->order_groups_host.size() * 4, hipMemcpyHostToDevice,
-                                h->stream));
+    {  // the counting-sort order's groups (yoda_order.hip)
+      std::vector<std::pair<uint64_t, uint32_t>> gs;
+      gs.reserve(g_n);
+      for (size_t i = 0; i < gkey.size(); ++i)
+        if (gkey[i]) gs.emplace_back(gkey[i] - 1, gcnt[i]);
+      std::sort(gs.begin(), gs.end());
+      const uint32_t G = (uint32_t)gs.size();
+      h->og_ok = G > 0 && G <= kOrderMaxGroups;
+      h->n_pad = P;
+      if (h->og_ok) {
+        uint32_t nbl = 8;  // buckets per group: G * NB <= kOrderMaxGroups entries (LDS)
+        while (nbl > 0 && ((size_t)G << nbl) > kOrderMaxGroups) --nbl;
+        uint32_t bm = 0;
+        while (bm < 32 && (key_or[2] >> bm)) ++bm;
+        h->og_groups = G;
+        h->og_nb_log2 = nbl;
+        h->og_m_shift = bm > nbl ? bm - nbl : 0;
+        std::vector<uint32_t> st0(G), stp(G), pad;
+        uint32_t a0 = 0, ap = 0;
+        for (uint32_t g = 0; g < G; ++g) {
+          st0[g] = a0;
+          stp[g] = ap;
+          a0 += gs[g].second;
+          const uint32_t padded = (gs[g].second + kWave - 1) / kWave * kWave;
+          for (uint32_t i = gs[g].second; i < padded; ++i) {  // copies of the group's last
+            pad.push_back(ap + i);                            // pod: the wave's neighbours
+            pad.push_back(ap + gs[g].second - 1);             // in memory order
+          }
+          ap += padded;
+        }
+        h->n_pad = ap;
+        h->og_n_pad_slots = (uint32_t)(pad.size() / 2);
+        h->og_off_start = (size_t)G * 8;
+        h->og_off_start_pad = h->og_off_start + (size_t)G * 4;
+        h->og_off_pad = h->og_off_start_pad + (size_t)G * 4;
+        h->og_host.assign(h->og_off_pad + pad.size() * 4, 0);
+        for (uint32_t g = 0; g < G; ++g)
+          std::memcpy(h->og_host.data() + (size_t)g * 8, &gs[g].first, 8);
+        std::memcpy(h->og_host.data() + h->og_off_start, st0.data(), (size_t)G * 4);
+        std::memcpy(h->og_host.data() + h->og_off_start_pad, stp.data(), (size_t)G * 4);
+        if (!pad.empty())
+          std::memcpy(h->og_host.data() + h->og_off_pad, pad.data(), pad.size() * 4);
+        HIP_TRY(h, h->order_meta.ensure(h->og_host.size()));
+        HIP_TRY(h, hipMemcpyAsync(h->order_meta.p, h->og_host.data(), h->og_host.size(),
+                                  hipMemcpyHostToDevice, h->stream));
+        const size_t nbk = (size_t)G << nbl;
+        if (h->order_hist.bytes < nbk * 4) {  // the scan clears it after each use
+          HIP_TRY(h, h->order_hist.ensure(nbk * 4));
+          HIP_TRY(h, hipMemsetAsync(h->order_hist.p, 0, h->order_hist.bytes, h->stream));
+        }
+        HIP_TRY(h, h->order_bstart.ensure(nbk * 4));
+      }
     }
     HIP_TRY(h, hipEventRecord(h->stage_event, h->stream));
     h->stage_pending = true;
@@ -1161,6 +1274,7 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
       h->key_bits[f] = bits;
     }
     h->n_pods = P;
+    h->n_work = P;
     h->has_pods = true;
     h->ran = false;
     h->phase1_done = false;
@@ -1174,16 +1288,22 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
   }
 }
 
-static int prepare_run(yoda_t* h, int mode) {
+// pad: this run may pad the order's groups to whole waves (yoda_run without the bitmask;
+// every other entry point keeps one sorted position per caller pod).
+static int prepare_run(yoda_t* h, int mode, bool pad = false) {
   int rc = check_ready(h, mode);
   if (rc) return rc;
   h->topk_ready = false;  // this run overwrites the bitmask and reciprocals
-  plan_chunks(h, mode, h->n_pods, h->n_nodes);
-  return ensure_state(h, std::max<uint32_t>(h->n_pods, 1));
+  const bool ordering = h->order_enabled && mode == YODA_MODE_SCV &&
+                        h->n_pods >= kOrderMinPods && h->n_nodes > 0;
+  h->n_work = pad && ordering && h->og_ok && env_u32("YODA_ORDER_PAD", 1) ? h->n_pad
+                                                                         : h->n_pods;
+  plan_chunks(h, mode, h->n_work, h->n_nodes);
+  return ensure_state(h, std::max<uint32_t>(h->n_work, 1));
 }
 
 int yoda_run(yoda_t* h, int mode, uint32_t flags) {
-  int rc = prepare_run(h, mode);
+  int rc = prepare_run(h, mode, (flags & YODA_RUN_BITMASK) == 0);
   if (rc) return rc;
   try {
     if ((rc = order_pods(h, mode))) return rc;

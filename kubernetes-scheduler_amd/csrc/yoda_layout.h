@@ -233,6 +233,15 @@ struct Partials {
 
 // Per-pod array table for the batch permutation (yoda_order.hip).
 constexpr int kPermArrays = 16;
+// Counting-sort pod order (yoda_order.hip): the batch's distinct group keys (ascending;
+// key = clock24 << 9 | number8 << 1 | has-memory), each group's first sorted position, and
+// the memory buckets per group (1 << nb_log2; bucket = min(m, 2^32 - 1) >> m_shift).
+struct OrderMeta {
+  const uint64_t* groups;
+  const uint32_t* gstart;
+  uint32_t n_groups, nb_log2, m_shift;
+};
+
 struct PermTable {
   const void* src[kPermArrays];
   void* dst[kPermArrays];

@@ -18,50 +18,56 @@
 
 namespace yoda {
 
-// key = clock (clamped to 24 bits) | number (8 bits) | memory (32 bits), lexicographic:
-// ascending clock puts the K1 `clock >= c` skips together too.  Any key is correct; this one
-// is just fast.  The fields are packed at the widths the batch actually uses (host: the OR
-// of each clamped field at upload), so the radix sort runs over bn + bm + bc bits only —
-// same order as the full-width key, fewer passes.
+// key = clock (clamped to 24 bits) | number (8 bits) | has-memory (1 bit) | memory (32
+// bits), lexicographic: ascending clock puts the K1 `clock >= c` skips together too.  Any
+// key is correct; this one is just fast.  The fields are packed at the widths the batch
+// actually uses (host: the OR of each clamped field at upload), so the radix sort runs over
+// bc + bn + 1 + bm bits only -- same order as the full-width key, fewer passes.  (Without
+// room for the has-memory bit in 64, it is left out.)
 //
-// Serpentine: memory ascends in the even (clock, number) groups and descends in the odd
-// ones (rank among the batch's groups, host-built sorted list `groups`).  A wave that
-// straddles two groups then holds pods of similar memory from both ends instead of the
+// Serpentine: memory ascends in the even (clock, number, has-memory) groups and descends in
+// the odd ones (rank among the batch's groups, host-built sorted list `groups`).  A wave
+// that straddles two groups then holds pods of similar memory from both ends instead of the
 // largest requests of one group next to the smallest of the next: its pods qualify the
 // same cards on most nodes, where a straddling ascending wave spans every memory size and
 // leaves the block K2 nothing but per-pod work.
+struct KeyShape {
+  uint32_t bm, f_shift, n_shift, c_shift;  // field positions; f_shift == 64: no flag bit
+};
+
 __device__ __forceinline__ uint64_t order_key(uint64_t number, uint64_t m_u, uint64_t c_u,
-                                              uint32_t n_shift, uint32_t c_shift,
-                                              const uint32_t* __restrict__ groups,
+                                              uint32_t need_mem, KeyShape k,
+                                              const uint64_t* __restrict__ groups,
                                               uint32_t n_groups) {
   const uint64_t c = c_u < 0xffffffull ? c_u : 0xffffffull;
   const uint64_t n = number < 0xffull ? number : 0xffull;
+  const uint64_t f = need_mem != 0u ? 1ull : 0ull;
   uint64_t m = m_u < 0xffffffffull ? m_u : 0xffffffffull;
   if (groups) {
-    const uint32_t g = (uint32_t)(c << 8) | (uint32_t)n;
+    const uint64_t g = (c << 9) | (n << 1) | f;
     uint32_t lo = 0, hi = n_groups;  // lower_bound: the group's rank
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
       if (groups[mid] < g) lo = mid + 1; else hi = mid;
     }
-    const uint64_t m_all = n_shift >= 32 ? 0xffffffffull : (1ull << n_shift) - 1ull;
-    if (lo & 1u) m = m_all - m;  // m <= m_all: n_shift is the width of the batch's m field
+    const uint64_t m_all = k.bm >= 32 ? 0xffffffffull : (1ull << k.bm) - 1ull;
+    if (lo & 1u) m = m_all - m;  // m <= m_all: bm is the width of the batch's m field
   }
-  return (c << c_shift) | (n << n_shift) | m;
+  return (c << k.c_shift) | (n << k.n_shift) | (k.f_shift < 64 ? f << k.f_shift : 0ull) | m;
 }
 
 __global__ __launch_bounds__(kBlock) void k_order_keys(const uint64_t* __restrict__ number,
                                                        const uint64_t* __restrict__ m_u,
                                                        const uint64_t* __restrict__ c_u,
-                                                       uint32_t n_pods, uint32_t n_shift,
-                                                       uint32_t c_shift,
-                                                       const uint32_t* __restrict__ groups,
+                                                       const uint32_t* __restrict__ need_mem,
+                                                       uint32_t n_pods, KeyShape k,
+                                                       const uint64_t* __restrict__ groups,
                                                        uint32_t n_groups,
                                                        uint64_t* __restrict__ keys,
                                                        uint32_t* __restrict__ idx) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (p >= n_pods) return;
-  keys[p] = order_key(number[p], m_u[p], c_u[p], n_shift, c_shift, groups, n_groups);
+  keys[p] = order_key(number[p], m_u[p], c_u[p], need_mem[p], k, groups, n_groups);
   idx[p] = p;
 }
 
@@ -70,15 +76,15 @@ __global__ __launch_bounds__(kBlock) void k_order_keys(const uint64_t* __restric
 __global__ __launch_bounds__(kBlock) void k_order_keys32(const uint64_t* __restrict__ number,
                                                          const uint64_t* __restrict__ m_u,
                                                          const uint64_t* __restrict__ c_u,
-                                                         uint32_t n_pods, uint32_t n_shift,
-                                                         uint32_t c_shift,
-                                                         const uint32_t* __restrict__ groups,
+                                                         const uint32_t* __restrict__ need_mem,
+                                                         uint32_t n_pods, KeyShape k,
+                                                         const uint64_t* __restrict__ groups,
                                                          uint32_t n_groups,
                                                          uint32_t* __restrict__ keys,
                                                          uint32_t* __restrict__ idx) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (p >= n_pods) return;
-  keys[p] = (uint32_t)order_key(number[p], m_u[p], c_u[p], n_shift, c_shift, groups, n_groups);
+  keys[p] = (uint32_t)order_key(number[p], m_u[p], c_u[p], need_mem[p], k, groups, n_groups);
   idx[p] = p;
 }
 
@@ -111,15 +117,21 @@ size_t order_scratch_bytes(uint32_t n_pods) {
 
 // perm[i] = the original index of the i-th pod in sorted order.
 hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
-                             uint32_t n_pods, const uint32_t key_bits[3],
-                             const uint32_t* groups, uint32_t n_groups, void* scratch,
+                             const uint32_t* need_mem, uint32_t n_pods, const uint32_t key_bits[3],
+                             const uint64_t* groups, uint32_t n_groups, void* scratch,
                              size_t scratch_bytes, uint32_t* perm, hipStream_t s) {
-  // key_bits = widths of (c, n, m); each <= its clamp (24, 8, 32), so the total is <= 64
+  // key_bits = widths of (c, n, m); each <= its clamp (24, 8, 32)
   const uint32_t bc = key_bits[0] < 24 ? key_bits[0] : 24;
   const uint32_t bn = key_bits[1] < 8 ? key_bits[1] : 8;
   const uint32_t bm = key_bits[2] < 32 ? key_bits[2] : 32;
-  const uint32_t n_shift = bm, c_shift = bm + bn;
-  const int end_bit = (int)(bc + bn + bm) > 0 ? (int)(bc + bn + bm) : 1;
+  const bool flag = bc + bn + 1 + bm <= 64;
+  KeyShape k;
+  k.bm = bm;
+  k.f_shift = flag ? bm : 64;
+  k.n_shift = bm + (flag ? 1 : 0);
+  k.c_shift = k.n_shift + bn;
+  const uint32_t bits = k.c_shift + bc;
+  const int end_bit = bits > 0 ? (int)bits : 1;
   unsigned char* b = static_cast<unsigned char*>(scratch);
   uint64_t* keys_in = reinterpret_cast<uint64_t*>(b);
   uint64_t* keys_out = keys_in + n_pods;
@@ -130,16 +142,14 @@ hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const 
     uint32_t* k32_in = reinterpret_cast<uint32_t*>(keys_in);
     uint32_t* k32_out = reinterpret_cast<uint32_t*>(keys_out);
     hipLaunchKernelGGL(k_order_keys32, dim3((n_pods + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                       number, m_u, c_u, n_pods, n_shift, c_shift, n_groups ? groups : nullptr,
-                       n_groups, k32_in, idx_in);
+                       number, m_u, c_u, need_mem, n_pods, k, groups, n_groups, k32_in, idx_in);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k32_in, k32_out, idx_in, perm,
                                               (int)n_pods, 0, end_bit, s);
   }
   hipLaunchKernelGGL(k_order_keys, dim3((n_pods + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                     number, m_u, c_u, n_pods, n_shift, c_shift, n_groups ? groups : nullptr,
-                     n_groups, keys_in, idx_in);
+                     number, m_u, c_u, need_mem, n_pods, k, groups, n_groups, keys_in, idx_in);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, perm,
@@ -151,6 +161,138 @@ hipError_t launch_permute(const PermTable& t, const uint32_t* perm, uint32_t n_p
   if (t.n == 0 || n_pods == 0) return hipSuccess;
   dim3 grid((n_pods + kBlock - 1) / kBlock, t.n);
   hipLaunchKernelGGL(k_permute, grid, dim3(kBlock), 0, s, t, perm, n_pods, scatter ? 1 : 0);
+  return hipGetLastError();
+}
+
+// ---- counting-sort order with group padding ------------------------------------------
+// The batch's pods fall into a few (clock, number, has-memory) groups (host: the distinct
+// group keys, ascending, and each group's first sorted position).  Within a group the pods
+// are ordered by memory in NB buckets, ascending in even groups and descending in odd ones
+// (serpentine, as above); the order inside one bucket is whatever the atomics give (any
+// order is correct, results do not depend on it).  With padding every group starts on a
+// wave boundary: the free slots at a group's end are filled with copies of its last pod
+// (a sorted position that maps to the same caller pod: identical inputs, identical
+// results, written back twice), so no wave mixes two groups -- a mixed wave leaves the
+// block kernels nothing but per-pod work on every node.
+__device__ __forceinline__ uint32_t order_bucket(const OrderMeta& o, uint64_t number,
+                                                 uint64_t m_u, uint64_t c_u, uint32_t need_mem) {
+  const uint64_t c = c_u < 0xffffffull ? c_u : 0xffffffull;
+  const uint64_t n = number < 0xffull ? number : 0xffull;
+  const uint64_t key = (c << 9) | (n << 1) | (need_mem != 0u ? 1ull : 0ull);
+  uint32_t lo = 0, hi = o.n_groups;  // lower_bound: the group's rank (the key is present)
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (o.groups[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  const uint64_t m = m_u < 0xffffffffull ? m_u : 0xffffffffull;
+  const uint32_t nb = 1u << o.nb_log2;
+  uint32_t b = (uint32_t)(m >> o.m_shift);
+  b = b < nb ? b : nb - 1u;
+  if (lo & 1u) b = nb - 1u - b;
+  return (lo << o.nb_log2) | b;
+}
+
+// Per workgroup: an LDS histogram of the buckets (each pod's rank inside its workgroup's
+// share of the bucket), then one global atomic per (workgroup, bucket): the share's base.
+__global__ __launch_bounds__(1024) void k_order_hist(OrderMeta o, const uint64_t* __restrict__ number,
+                                                     const uint64_t* __restrict__ m_u,
+                                                     const uint64_t* __restrict__ c_u,
+                                                     const uint32_t* __restrict__ need_mem,
+                                                     uint32_t n_pods, uint32_t* __restrict__ hist,
+                                                     uint32_t* __restrict__ slot,
+                                                     uint32_t* __restrict__ bkt) {
+  extern __shared__ uint32_t lh[];
+  const uint32_t nbk = o.n_groups << o.nb_log2;
+  for (uint32_t i = threadIdx.x; i < nbk; i += blockDim.x) lh[i] = 0u;
+  __syncthreads();
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t b = 0, local = 0;
+  if (p < n_pods) {
+    b = order_bucket(o, number[p], m_u[p], c_u[p], need_mem[p]);
+    local = atomicAdd(&lh[b], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nbk; i += blockDim.x) {
+    const uint32_t c = lh[i];
+    if (c) lh[i] = atomicAdd(&hist[i], c);
+  }
+  __syncthreads();
+  if (p < n_pods) {
+    slot[p] = lh[b] + local;
+    bkt[p] = b;
+  }
+}
+
+// One workgroup per group: exclusive scan of its NB bucket counts from the group's first
+// sorted position; the counts are cleared for the next run.
+__global__ __launch_bounds__(256) void k_order_scan(OrderMeta o, uint32_t* __restrict__ hist,
+                                                    uint32_t* __restrict__ bstart) {
+  __shared__ uint32_t sc[256];
+  const uint32_t g = blockIdx.x, t = threadIdx.x, nb = 1u << o.nb_log2;
+  const uint32_t i = (g << o.nb_log2) + t;
+  const uint32_t c = t < nb ? hist[i] : 0u;
+  sc[t] = c;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {  // Hillis-Steele inclusive scan
+    const uint32_t v = t >= d ? sc[t - d] : 0u;
+    __syncthreads();
+    sc[t] += v;
+    __syncthreads();
+  }
+  if (t < nb) {
+    bstart[i] = o.gstart[g] + sc[t] - c;
+    hist[i] = 0u;
+  }
+}
+
+// Sorted position of every pod: perm[pos] = p, and every pod array scattered to pos.
+__global__ __launch_bounds__(kBlock) void k_order_scatter(PermTable t,
+                                                          const uint32_t* __restrict__ slot,
+                                                          const uint32_t* __restrict__ bkt,
+                                                          const uint32_t* __restrict__ bstart,
+                                                          uint32_t n_pods, uint32_t* __restrict__ perm) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= n_pods) return;
+  const uint32_t pos = bstart[bkt[p]] + slot[p];
+  perm[pos] = p;
+  for (uint32_t a = 0; a < t.n; ++a) {
+    if (t.bytes[a] == 8)
+      static_cast<uint64_t*>(t.dst[a])[pos] = static_cast<const uint64_t*>(t.src[a])[p];
+    else
+      static_cast<uint32_t*>(t.dst[a])[pos] = static_cast<const uint32_t*>(t.src[a])[p];
+  }
+}
+
+// The padding slots: a copy of the group's last sorted position (perm and every array).
+__global__ __launch_bounds__(kBlock) void k_order_pad(PermTable t, const uint32_t* __restrict__ pad,
+                                                      uint32_t n_pad, uint32_t* __restrict__ perm) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n_pad) return;
+  const uint32_t d = pad[2 * i], s = pad[2 * i + 1];
+  perm[d] = perm[s];
+  for (uint32_t a = 0; a < t.n; ++a) {
+    if (t.bytes[a] == 8)
+      static_cast<uint64_t*>(t.dst[a])[d] = static_cast<const uint64_t*>(t.dst[a])[s];
+    else
+      static_cast<uint32_t*>(t.dst[a])[d] = static_cast<const uint32_t*>(t.dst[a])[s];
+  }
+}
+
+// t: the pod arrays (src = caller order, dst = sorted order); scratch: slot, bkt [P] u32.
+hipError_t launch_order_count(const OrderMeta& o, const uint64_t* number, const uint64_t* m_u,
+                              const uint64_t* c_u, const uint32_t* need_mem, uint32_t n_pods,
+                              uint32_t* hist, uint32_t* bstart, uint32_t* slot, uint32_t* bkt,
+                              const PermTable& t, const uint32_t* pad, uint32_t n_pad,
+                              uint32_t* perm, hipStream_t s) {
+  const uint32_t nbk = o.n_groups << o.nb_log2;
+  hipLaunchKernelGGL(k_order_hist, dim3((n_pods + 1023) / 1024), dim3(1024), nbk * 4, s, o,
+                     number, m_u, c_u, need_mem, n_pods, hist, slot, bkt);
+  hipLaunchKernelGGL(k_order_scan, dim3(o.n_groups), dim3(256), 0, s, o, hist, bstart);
+  hipLaunchKernelGGL(k_order_scatter, dim3((n_pods + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                     t, slot, bkt, bstart, n_pods, perm);
+  if (n_pad)
+    hipLaunchKernelGGL(k_order_pad, dim3((n_pad + kBlock - 1) / kBlock), dim3(kBlock), 0, s, t,
+                       pad, n_pad, perm);
   return hipGetLastError();
 }
 
