@@ -126,7 +126,7 @@ hipError_t launch_order_count(const OrderMeta& o, const uint64_t* number, const 
                               const uint64_t* c_u, const uint32_t* need_mem, uint32_t n_pods,
                               uint32_t* hist, uint32_t* bstart, uint32_t* slot, uint32_t* bkt,
                               const PermTable& t, const uint32_t* pad, uint32_t n_pad,
-                              uint32_t* perm, hipStream_t s);
+                              uint64_t* zero, uint32_t n_zero, uint32_t* perm, hipStream_t s);
 hipError_t launch_permute(const PermTable& t, const uint32_t* perm, uint32_t n_pods, bool scatter,
                           hipStream_t s);
 }  // namespace yoda
@@ -294,6 +294,8 @@ struct yoda_handle {
   DevBuf bitmask, bitmask_t, rows, rows_t, norm;
   DevBuf blk;               // [wave][node block / 64] u64: blocks with a feasible pod (K1 -> K2)
   bool blk_valid = false;   // the last K1 wrote blk (block-classified K1 on this batch)
+  bool blk_zeroed = false;  // this run's order already cleared blk (no memset in phase 1)
+  bool flagged_dirty = true;  // n_flagged may be nonzero (a generic run since the last clear)
   DevBuf bsum;              // [wave][node block] BlockMask: the block K1's sparse masks
   bool bm_sparse = false;   // the last K1 wrote the sparse form (bsum + partial masks only)
   const BlockMask* bs_ptr() const { return bm_sparse ? bsum.as<BlockMask>() : nullptr; }
@@ -538,6 +540,7 @@ constexpr uint32_t kOrderMaxGroups = 16384;
 int order_pods(yoda_t* h, int mode) {
   const uint32_t P = h->n_pods, W = h->n_work;
   h->ordered = false;
+  h->blk_zeroed = false;
   if (!h->order_enabled || mode != YODA_MODE_SCV || P < kOrderMinPods || h->n_nodes == 0)
     return YODA_OK;
   const unsigned char* b = h->pod_blob.as<unsigned char>();
@@ -561,6 +564,21 @@ int order_pods(yoda_t* h, int mode) {
   // one batch on several GPUs must agree on it.
   if (h->og_ok && W != P) {
     const bool padded = true;
+    // the block kernels (N32 with both summaries) read 5 of the pod arrays; the rest of the
+    // sorted blob is left unwritten and unread
+    if (h->path == Path::N32 && h->has_k1sum && h->has_k2sum) {
+      const int fast[] = {kPodM32, kPodC32, kPodNumber, kPodNeedMem, kPodNeedClk};
+      t.n = 0;
+      for (int a : fast) {
+        t.src[t.n] = b + h->pod_off[a];
+        t.dst[t.n] = h->pod_sorted.as<unsigned char>() + h->sorted_off[a];
+        t.bytes[t.n] = (uint32_t)kPodArrayBytes[a];
+        ++t.n;
+      }
+    }
+    // the K1 block list is cleared here rather than by a memset in phase 1
+    const uint32_t n_zero = h->has_k1sum ? (W + 63) / 64 * blk_row(h->n_nodes) : 0u;
+    h->blk_zeroed = n_zero != 0;
     HIP_TRY(h, h->order_slot.ensure((size_t)P * 4));
     HIP_TRY(h, h->order_bkt.ensure((size_t)P * 4));
     const unsigned char* meta = h->order_meta.as<unsigned char>();
@@ -578,8 +596,8 @@ int order_pods(yoda_t* h, int mode) {
                                   P, h->order_hist.as<uint32_t>(), h->order_bstart.as<uint32_t>(),
                                   h->order_slot.as<uint32_t>(), h->order_bkt.as<uint32_t>(), t,
                                   reinterpret_cast<const uint32_t*>(meta + h->og_off_pad),
-                                  padded ? h->og_n_pad_slots : 0u, h->perm.as<uint32_t>(),
-                                  h->stream));
+                                  padded ? h->og_n_pad_slots : 0u, h->blk.as<uint64_t>(), n_zero,
+                                  h->perm.as<uint32_t>(), h->stream));
     h->ordered = true;
     return YODA_OK;
   }
@@ -654,9 +672,10 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts) {
   if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
   h->blk_valid = h->has_k1sum;
   h->bm_sparse = h->has_k1sum;  // the block K1 writes the sparse form
-  if (h->blk_valid)
+  if (h->blk_valid && !h->blk_zeroed)
     HIP_TRY(h, hipMemsetAsync(h->blk.p, 0, (size_t)(P + 63) / 64 * blk_row(h->n_nodes) * 8,
                               h->stream));
+  h->blk_zeroed = false;
   HIP_TRY(h, launch_k1(h->K, h->path, h->nodes.as<unsigned char>(),
                        h->has_k1sum ? h->k1sum.as<unsigned char>() : nullptr, h->n_nodes,
                        h->chunk1, h->C1, pod_params(h), P, part, h->bitmask.as<uint64_t>(),
@@ -756,7 +775,10 @@ int finalize(yoda_t* h, int mode, const uint32_t* counts, const int64_t* best,
   const uint32_t P = h->n_work;  // sorted positions of this run
   if (P == 0) return YODA_OK;
   const bool generic = h->generic && mode == YODA_MODE_SCV;
-  HIP_TRY(h, hipMemsetAsync(h->n_flagged.p, 0, 4, h->stream));
+  // the overflow count is written by the generic path only: clear it for those runs, and
+  // once after one (yoda_shard_overflow_count reads it)
+  if (generic || h->flagged_dirty) HIP_TRY(h, hipMemsetAsync(h->n_flagged.p, 0, 4, h->stream));
+  h->flagged_dirty = generic;
   HIP_TRY(h, launch_finalize(counts, best, idx, ties, low, P, generic, h->pick.as<int32_t>(),
                              h->status.as<int32_t>(), h->ties_out.as<uint32_t>(),
                              h->flagged.as<uint32_t>(), h->n_flagged.as<uint32_t>(), h->stream));
@@ -1149,6 +1171,8 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     // key + 1 (0 = empty); consecutive pods of one group (the common case) skip the probe
     std::vector<uint64_t> gkey(256, 0ull);
     std::vector<uint32_t> gcnt(256, 0u);
+    // per group: its pods of the largest and of the smallest memory (the padding copies)
+    std::vector<uint64_t> gmax(256, 0ull), gmin(256, ~0ull);  // (m << 32 | pod) extremes
     size_t g_n = 0;
     auto g_slot = [&](uint64_t k1) {
       size_t i = (size_t)(k1 * 0x9e3779b97f4a7c15ull >> 40) & (gkey.size() - 1);
@@ -1157,19 +1181,25 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     };
     uint64_t g_last = ~0ull;
     uint32_t g_run = 0;
-    auto g_add = [&](uint64_t g, uint32_t c) {
+    uint64_t r_max = 0, r_min = ~0ull;  // the current run's extremes
+    auto g_add = [&](uint64_t g, uint32_t c, uint64_t mx, uint64_t mn) {
       size_t i = g_slot(g + 1);
       if (gkey[i] == 0ull) {
         if (2 * (g_n + 1) > gkey.size()) {  // grow and rehash
-          std::vector<uint64_t> ok(gkey.size() * 2, 0ull);
-          std::vector<uint32_t> oc(gcnt.size() * 2, 0u);
+          const size_t n2 = gkey.size() * 2;
+          std::vector<uint64_t> ok(n2, 0ull), omx(n2, 0ull), omn(n2, ~0ull);
+          std::vector<uint32_t> oc(n2, 0u);
           ok.swap(gkey);
           oc.swap(gcnt);
+          omx.swap(gmax);
+          omn.swap(gmin);
           for (size_t j = 0; j < ok.size(); ++j)
             if (ok[j]) {
               const size_t t = g_slot(ok[j]);
               gkey[t] = ok[j];
               gcnt[t] = oc[j];
+              gmax[t] = omx[j];
+              gmin[t] = omn[j];
             }
           i = g_slot(g + 1);
         }
@@ -1177,6 +1207,8 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
         ++g_n;
       }
       gcnt[i] += c;
+      gmax[i] = std::max(gmax[i], mx);
+      gmin[i] = std::min(gmin[i], mn);
     };
     for (uint32_t p = 0; p < P; ++p) {
       const uint64_t number = pd->has_number[p] ? pd->number[p] : 1;  // filter.go:12-15
@@ -1198,11 +1230,16 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
       const uint64_t g = (std::min<uint64_t>(c, 0xffffffull) << 9) |
                          (std::min<uint64_t>(number, 0xffull) << 1) | (nm[p] != 0u ? 1u : 0u);
       if (g != g_last) {
-        if (g_run) g_add(g_last, g_run);
+        if (g_run) g_add(g_last, g_run, r_max, r_min);
         g_last = g;
         g_run = 0;
+        r_max = 0;
+        r_min = ~0ull;
       }
       ++g_run;
+      const uint64_t mp = (std::min<uint64_t>(m, 0xffffffffull) << 32) | p;
+      r_max = std::max(r_max, mp);
+      r_min = std::min(r_min, mp);
       al[p] = be[p] = 0.0;
       if (pd->rio && pd->rcpu) {  // algorithm.go:105-106
         const double beta = 1.0 / (1.0 + (double)pd->rcpu[p] / pd->rio[p]);
@@ -1210,19 +1247,25 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
         al[p] = 1 - beta;
       }
     }
-    if (g_run) g_add(g_last, g_run);
+    if (g_run) g_add(g_last, g_run, r_max, r_min);
     HIP_TRY(h, hipMemcpyAsync(h->pod_blob.p, st, total, hipMemcpyHostToDevice, h->stream));
     {  // the counting-sort order's groups (yoda_order.hip)
-      std::vector<std::pair<uint64_t, uint32_t>> gs;
+      struct Grp {
+        uint64_t key;
+        uint32_t count, pod_max, pod_min;  // pods of the largest / smallest memory
+        bool operator<(const Grp& o) const { return key < o.key; }
+      };
+      std::vector<Grp> gs;
       gs.reserve(g_n);
       for (size_t i = 0; i < gkey.size(); ++i)
-        if (gkey[i]) gs.emplace_back(gkey[i] - 1, gcnt[i]);
+        if (gkey[i])
+          gs.push_back({gkey[i] - 1, gcnt[i], (uint32_t)gmax[i], (uint32_t)gmin[i]});
       std::sort(gs.begin(), gs.end());
       const uint32_t G = (uint32_t)gs.size();
       h->og_ok = G > 0 && G <= kOrderMaxGroups;
       h->n_pad = P;
       if (h->og_ok) {
-        uint32_t nbl = 8;  // buckets per group: G * NB <= kOrderMaxGroups entries (LDS)
+        uint32_t nbl = 10;  // buckets per group: G * NB <= kOrderMaxGroups entries (LDS)
         while (nbl > 0 && ((size_t)G << nbl) > kOrderMaxGroups) --nbl;
         uint32_t bm = 0;
         while (bm < 32 && (key_or[2] >> bm)) ++bm;
@@ -1234,11 +1277,14 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
         for (uint32_t g = 0; g < G; ++g) {
           st0[g] = a0;
           stp[g] = ap;
-          a0 += gs[g].second;
-          const uint32_t padded = (gs[g].second + kWave - 1) / kWave * kWave;
-          for (uint32_t i = gs[g].second; i < padded; ++i) {  // copies of the group's last
-            pad.push_back(ap + i);                            // pod: the wave's neighbours
-            pad.push_back(ap + gs[g].second - 1);             // in memory order
+          a0 += gs[g].count;
+          const uint32_t padded = (gs[g].count + kWave - 1) / kWave * kWave;
+          // copies of the group's last pod in memory order (largest memory in an ascending
+          // -- even -- group, smallest in a descending one): the tail wave's neighbour
+          const uint32_t last = (g & 1u) ? gs[g].pod_min : gs[g].pod_max;
+          for (uint32_t i = gs[g].count; i < padded; ++i) {
+            pad.push_back(ap + i);
+            pad.push_back(last);
           }
           ap += padded;
         }
@@ -1249,7 +1295,7 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
         h->og_off_pad = h->og_off_start_pad + (size_t)G * 4;
         h->og_host.assign(h->og_off_pad + pad.size() * 4, 0);
         for (uint32_t g = 0; g < G; ++g)
-          std::memcpy(h->og_host.data() + (size_t)g * 8, &gs[g].first, 8);
+          std::memcpy(h->og_host.data() + (size_t)g * 8, &gs[g].key, 8);
         std::memcpy(h->og_host.data() + h->og_off_start, st0.data(), (size_t)G * 4);
         std::memcpy(h->og_host.data() + h->og_off_start_pad, stp.data(), (size_t)G * 4);
         if (!pad.empty())

@@ -1160,8 +1160,11 @@ __global__ __launch_bounds__(kBlock) void k2_score(
 //         reads  nq * shared + prefix[nq]  from LDS (the same integers as Scorer<N32>);
 //   EXACT anything else (mixed-model node, or non-uniform maxima): Scorer<N32>::raw.
 // Every term is an exact integer < 2^52 in each form, so all three give the same raw score.
+#ifndef YODA_K2_WAVES
+#define YODA_K2_WAVES 5
+#endif
 template <int K, bool STATS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ? 5 : 1))) void k2_block_n32(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ? YODA_K2_WAVES : 1))) void k2_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum2,
     uint32_t n_nodes, uint32_t chunk_nodes, ScoreArgs args, uint32_t n_pods,
     const uint64_t* __restrict__ bm, uint32_t bm_stride, const BlockMask* __restrict__ bs,
@@ -1172,8 +1175,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   constexpr uint32_t S2 = k2sum_stride(K), NS = n32_stride(K);
   constexpr uint32_t PSW = K + 2;  // LDS words per node: prefix[0..K], shared
   constexpr uint32_t TAB = kWave * PSW;  // the prefix table: 64 nodes
-  // node records (below): 6 words + (basic at nq_lo, at nq_lo + 1) per reciprocal set
-  constexpr uint32_t kSets = 5, REC = 6 + 2 * kSets;
+  // node records (below): 16 words -- 8 of header, then 4 basic scores (uniform maxima) or
+  // the (basic at nq_lo, at nq_lo + 1) pair of each reciprocal set
+  constexpr uint32_t kSets = 4, REC = 16;
   // LDS per wave: prefix table | 64 node records | the sets' reciprocals (8 words each)
   constexpr uint32_t RECS = TAB, RCPS = TAB + kWave * REC, LDSW = RCPS + 8 * kSets;
   __shared__ __attribute__((aligned(16))) uint32_t lds_all[kBlock / kWave][LDSW];
@@ -1251,6 +1255,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   uint32_t idx = 0xffffffffu, ties = 0;
   double ubest = -1.0, ulow = 1.0e300;      // node lane (U nodes)
   uint32_t uidx = 0xffffffffu, uties = 0;
+  uint64_t rbest = 0, rlow = ~0ull;          // pod lane, record nodes (integer scores)
+  uint32_t ridx = 0xffffffffu, rties = 0;
   uint32_t npart = 0;  // STATS: per-pod-pass nodes of this (wave, chunk)
   // One block: the wave's mask of node nb + lane and its summary (kept for the per-pod pass,
   // read back with v_readlane), loaded together: one memory latency per block.
@@ -1294,32 +1300,47 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       }
       nq_lo = min(nq_lo, cnt);
       nq_hi = min(nq_hi, cnt);
-      uint32_t thr = 0;  // fs[nq_lo]: a pod with m <= thr qualifies one card more (nq_lo + 1)
+      // fs[nq_lo + i]: a pod with m <= thr_i qualifies card nq_lo + i too (the free order
+      // is descending); 0 past the node's range (only m == 0 meets it, and then every
+      // lower threshold as well)
+      const uint32_t range = nq_hi - nq_lo;
+      uint32_t thr = 0, thr1 = 0, thr2 = 0;
 #pragma unroll
-      for (int t = 0; t < K; ++t) thr = (uint32_t)t == nq_lo ? fs.v[t] : thr;
-      // A one-model node whose qualifying-card count takes at most two values over the wave
-      // (nq_lo, or nq_lo + 1 for the pods with m <= fs[nq_lo]: the free order is descending)
-      // gets a record: the threshold, its clock, the wave's mask, the static part and, per
-      // reciprocal set, both basic scores -- the per-pod pass reads it with three LDS loads.
-      const bool two = fast && nq_hi - nq_lo <= 1u;
+      for (int t = 0; t < K; ++t) {
+        thr = (uint32_t)t == nq_lo ? fs.v[t] : thr;
+        thr1 = (uint32_t)t == nq_lo + 1u && range > 1u ? fs.v[t] : thr1;
+        thr2 = (uint32_t)t == nq_lo + 2u && range > 2u ? fs.v[t] : thr2;
+      }
+      // the static part as an integer (< 2^52: its f64 bits above 2^52's)
+      const double stat_d =
+          __longlong_as_double((long long)((uint64_t)h0.x | ((uint64_t)h0.y << 32)));
+      const uint64_t stat_u = (uint64_t)__double_as_longlong(stat_d + 4503599627370496.0) -
+                              0x4330000000000000ull;
+      // A one-model node whose qualifying-card count takes at most four values over the
+      // wave (two with several reciprocal sets) gets a record: its clock, the wave's mask,
+      // the thresholds, the static part and the basic scores -- the per-pod pass reads it
+      // with three broadcast LDS loads.
+      const bool two = fast && range <= 1u;
       uint32_t* rec = lds + RECS + lane * REC;
       if (uni_max) {
         // CalculateCardScore terms (algorithm.go:280-291) with the wave's reciprocals
         const uint32_t shared = (uint32_t)((float)bw * u_bw) + (uint32_t)((float)ck * u_bw) +
                                 2u * (uint32_t)((float)core * u_core) +
                                 (uint32_t)((float)pw * u_pow);
-        uint32_t acc = 0, sel = 0, sel_hi = 0;  // prefix sums of (3 q_free + q_total)
+        uint32_t acc = 0, sel = 0;  // prefix sums of (3 q_free + q_total) in free order
         lds[lane * PSW + 0] = 0u;
 #pragma unroll
         for (int t = 0; t < K; ++t) {
+#ifdef YODA_ABL_NOPREFIX
+          acc += fs.v[t] + ts.v[t];
+#else
           acc += 3u * (uint32_t)((double)fs.v[t] * u_free) + (uint32_t)((double)ts.v[t] * u_tot);
+#endif
           lds[lane * PSW + t + 1] = acc;
           sel = (uint32_t)(t + 1) == nq_lo ? acc : sel;
-          sel_hi = (uint32_t)(t + 1) == nq_hi ? acc : sel_hi;
         }
         lds[lane * PSW + K + 1] = shared;
-        const double stat =
-            __longlong_as_double((long long)((uint64_t)h0.x | ((uint64_t)h0.y << 32)));
+        const double stat = stat_d;
         const bool q_all = ck >= c_max, q_none = ck < c_min;
         const bool is_u = fast && mask == act_mask && nq_lo == nq_hi && (q_all || q_none);
         u_b = ballot(is_u);
@@ -1335,13 +1356,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
           }
           ulow = fmin(ulow, raw);
         }
-        const bool is_rec = two && !is_u;
+        const bool is_rec = fast && range <= 3u && !is_u;
         rec_b = ballot(is_rec);
         if (is_rec) {
-          *reinterpret_cast<uint4*>(rec) = make_uint4(thr, ck, (uint32_t)mask,
-                                                      (uint32_t)(mask >> 32));
-          *reinterpret_cast<uint4*>(rec + 4) = make_uint4(h0.x, h0.y, nq_lo * shared + sel,
-                                                          nq_hi * shared + sel_hi);
+          // basic at nq_lo + i (i <= range; repeated past it), from the prefix row
+          const uint32_t* row = lds + lane * PSW;
+          const uint32_t q1 = nq_lo + min(range, 1u), q2 = nq_lo + min(range, 2u);
+          const uint32_t q3 = nq_lo + min(range, 3u);
+          *reinterpret_cast<uint4*>(rec) = make_uint4(ck, (uint32_t)mask, (uint32_t)(mask >> 32),
+                                                      thr);
+          *reinterpret_cast<uint4*>(rec + 4) = make_uint4((uint32_t)stat_u,
+                                                          (uint32_t)(stat_u >> 32), thr1, thr2);
+          *reinterpret_cast<uint4*>(rec + 8) =
+              make_uint4(nq_lo * shared + sel, q1 * shared + row[q1], q2 * shared + row[q2],
+                         q3 * shared + row[q3]);
         }
       } else {
         // several reciprocal sets: no U nodes (scores differ across the wave), a record per
@@ -1350,9 +1378,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         rec_b = ballot(is_rec);
         if (rec_b != 0ull) {
           if (is_rec) {
-            *reinterpret_cast<uint4*>(rec) = make_uint4(thr, ck, (uint32_t)mask,
-                                                        (uint32_t)(mask >> 32));
-            *reinterpret_cast<uint2*>(rec + 4) = make_uint2(h0.x, h0.y);
+            *reinterpret_cast<uint4*>(rec) = make_uint4(ck, (uint32_t)mask,
+                                                        (uint32_t)(mask >> 32), thr);
+            *reinterpret_cast<uint4*>(rec + 4) = make_uint4((uint32_t)stat_u,
+                                                            (uint32_t)(stat_u >> 32), 0u, 0u);
           }
           for (uint32_t q = 0; q < nsets; ++q) {
             const uint32_t* r = lds + RCPS + 8 * q;  // the set's reciprocals (broadcast)
@@ -1374,7 +1403,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
               sel_hi = (uint32_t)(t + 1) == nq_hi ? acc : sel_hi;
             }
             if (is_rec)
-              *reinterpret_cast<uint2*>(rec + 6 + 2 * q) =
+              *reinterpret_cast<uint2*>(rec + 8 + 2 * q) =
                   make_uint2(nq_lo * shared + sel, nq_hi * shared + sel_hi);
           }
         }
@@ -1398,10 +1427,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       best = gt ? raw : best;
       low = f && raw < low ? raw : low;  // no NaN here: a compare, not fmin's canonicalizes
     };
+#ifdef YODA_ABL_NOPOD
+    rec_b = 0;
+    part_b = 0;
+#endif
     uint64_t rb = rec_b;
     part_b &= ~rec_b;
-    while (rb) {  // four records per trip: all twelve LDS loads in flight before the first use
-      constexpr int R = 4;
+    // records: integer scores (static part + basic < 2^53) into the record state
+    auto take_r = [&](bool f, uint64_t raw, uint32_t nn) {
+      const bool gt = f & (raw > rbest), eq = f & (raw == rbest);
+      ridx = gt ? nn : (eq ? min(ridx, nn) : ridx);
+      rties = gt ? 1u : rties + (eq ? 1u : 0u);
+      rbest = gt ? raw : rbest;
+      rlow = (f & (raw < rlow)) ? raw : rlow;
+    };
+    while (rb) {  // R records per trip: all their LDS loads in flight before the first use
+#ifndef YODA_K2_R
+#define YODA_K2_R 2
+#endif
+      constexpr int R = YODA_K2_R;
       uint32_t jj[R];
       bool vv[R];
 #pragma unroll
@@ -1410,24 +1454,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         jj[k] = vv[k] ? (uint32_t)__builtin_ctzll(rb) : 0u;
         rb &= rb - 1;
       }
-      uint4 ra[R];
-      uint2 rs[R], rp[R];
+      uint4 ra[R], rs[R], rp[R];
 #pragma unroll
       for (int k = 0; k < R; ++k) {
         const uint32_t* r = lds + RECS + jj[k] * REC;
         ra[k] = *reinterpret_cast<const uint4*>(r);
-        rs[k] = *reinterpret_cast<const uint2*>(r + 4);
-        rp[k] = *reinterpret_cast<const uint2*>(r + 6 + 2 * set);
+        rs[k] = *reinterpret_cast<const uint4*>(r + 4);
+        if (uni_max) {
+          rp[k] = *reinterpret_cast<const uint4*>(r + 8);
+        } else {
+          const uint2 pr = *reinterpret_cast<const uint2*>(r + 8 + 2 * set);
+          rp[k] = make_uint4(pr.x, pr.y, pr.y, pr.y);
+        }
       }
 #pragma unroll
       for (int k = 0; k < R; ++k) {
-        // basic = nq * shared + prefix[nq] if the clock qualifies (algorithm.go:271-291)
-        const uint32_t bsel = sc.m <= ra[k].x ? rp[k].y : rp[k].x;
-        const uint32_t basic = ra[k].y >= sc.c ? bsel : 0u;
-        const double raw = (double)basic + __longlong_as_double((long long)(
-                                               (uint64_t)rs[k].x | ((uint64_t)rs[k].y << 32)));
-        const uint32_t mw = lane < 32u ? ra[k].z : ra[k].w;  // the wave's mask of the node
-        take(vv[k] && ((mw >> (lane & 31u)) & 1u) != 0u, raw, nb + jj[k]);
+        // nq = nq_lo + #{thresholds >= m}; basic = nq * shared + prefix[nq] if the clock
+        // qualifies (algorithm.go:271-291)
+        const bool c0 = sc.m <= ra[k].w, c1 = sc.m <= rs[k].z, c2 = sc.m <= rs[k].w;
+        const uint32_t bsel = c2 ? rp[k].w : (c1 ? rp[k].z : (c0 ? rp[k].y : rp[k].x));
+        const uint32_t basic = ra[k].x >= sc.c ? bsel : 0u;
+        const uint64_t raw = ((uint64_t)rs[k].x | ((uint64_t)rs[k].y << 32)) + basic;
+        const uint32_t mw = lane < 32u ? ra[k].y : ra[k].z;  // the wave's mask of the node
+        take_r(vv[k] && ((mw >> (lane & 31u)) & 1u) != 0u, raw, nb + jj[k]);
       }
     }
     while (part_b) {  // wave-uniform loop over the remaining feasible nodes
@@ -1526,6 +1575,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     wl = fmin(wl, __shfl_xor(wl, o, kWave));
   }
   if (!live) return;
+  if (rties > 0) {  // the record nodes (exact: every score < 2^53)
+    const double rb_d = (double)rbest;
+    if (rb_d > best) {
+      best = rb_d;
+      idx = ridx;
+      ties = rties;
+    } else if (rb_d == best) {
+      idx = min(idx, ridx);
+      ties += rties;
+    }
+    low = fmin(low, (double)rlow);
+  }
   if (act && wt > 0) {
     if (wb > best) {
       best = wb;

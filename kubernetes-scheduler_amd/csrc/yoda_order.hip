@@ -212,9 +212,21 @@ __global__ __launch_bounds__(1024) void k_order_hist(OrderMeta o, const uint64_t
     local = atomicAdd(&lh[b], 1u);
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nbk; i += blockDim.x) {
-    const uint32_t c = lh[i];
-    if (c) lh[i] = atomicAdd(&hist[i], c);
+  // one global add per (workgroup, bucket) in use: all of a thread's adds in flight at once
+  // (nbk <= 16 * blockDim.x), then their returns -- the shares' bases -- back into LDS
+  constexpr int kAdds = 16;
+  uint32_t base[kAdds];
+#pragma unroll
+  for (int k = 0; k < kAdds; ++k) {
+    const uint32_t i = threadIdx.x + (uint32_t)k * blockDim.x;
+    const uint32_t c = i < nbk ? lh[i] : 0u;
+    base[k] = c ? atomicAdd(&hist[i], c) : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kAdds; ++k) {
+    const uint32_t i = threadIdx.x + (uint32_t)k * blockDim.x;
+    if (i < nbk) lh[i] = base[k];
   }
   __syncthreads();
   if (p < n_pods) {
@@ -225,15 +237,17 @@ __global__ __launch_bounds__(1024) void k_order_hist(OrderMeta o, const uint64_t
 
 // One workgroup per group: exclusive scan of its NB bucket counts from the group's first
 // sorted position; the counts are cleared for the next run.
-__global__ __launch_bounds__(256) void k_order_scan(OrderMeta o, uint32_t* __restrict__ hist,
-                                                    uint32_t* __restrict__ bstart) {
-  __shared__ uint32_t sc[256];
+constexpr uint32_t kOrderMaxBuckets = 1024;  // buckets per group (nb_log2 <= 10)
+__global__ __launch_bounds__(kOrderMaxBuckets) void k_order_scan(OrderMeta o,
+                                                                 uint32_t* __restrict__ hist,
+                                                                 uint32_t* __restrict__ bstart) {
+  __shared__ uint32_t sc[kOrderMaxBuckets];
   const uint32_t g = blockIdx.x, t = threadIdx.x, nb = 1u << o.nb_log2;
   const uint32_t i = (g << o.nb_log2) + t;
   const uint32_t c = t < nb ? hist[i] : 0u;
   sc[t] = c;
   __syncthreads();
-  for (uint32_t d = 1; d < 256; d <<= 1) {  // Hillis-Steele inclusive scan
+  for (uint32_t d = 1; d < nb; d <<= 1) {  // Hillis-Steele inclusive scan
     const uint32_t v = t >= d ? sc[t - d] : 0u;
     __syncthreads();
     sc[t] += v;
@@ -245,15 +259,30 @@ __global__ __launch_bounds__(256) void k_order_scan(OrderMeta o, uint32_t* __res
   }
 }
 
-// Sorted position of every pod: perm[pos] = p, and every pod array scattered to pos.
+// Sorted position of every pod: perm[pos] = p, and every pod array scattered to pos.  The
+// threads past the batch fill the padding slots (pad: (slot, caller pod) pairs, the pod a
+// copy of the group's last in memory order) and clear the `zero` words (the K1 block list).
 __global__ __launch_bounds__(kBlock) void k_order_scatter(PermTable t,
                                                           const uint32_t* __restrict__ slot,
                                                           const uint32_t* __restrict__ bkt,
                                                           const uint32_t* __restrict__ bstart,
-                                                          uint32_t n_pods, uint32_t* __restrict__ perm) {
-  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-  if (p >= n_pods) return;
-  const uint32_t pos = bstart[bkt[p]] + slot[p];
+                                                          uint32_t n_pods,
+                                                          const uint32_t* __restrict__ pad,
+                                                          uint32_t n_pad, uint64_t* __restrict__ zero,
+                                                          uint32_t n_zero,
+                                                          uint32_t* __restrict__ perm) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  for (uint32_t z = i; z < n_zero; z += gridDim.x * kBlock) zero[z] = 0ull;
+  uint32_t p, pos;
+  if (i < n_pods) {
+    p = i;
+    pos = bstart[bkt[p]] + slot[p];
+  } else if (i - n_pods < n_pad) {
+    pos = pad[2 * (i - n_pods)];
+    p = pad[2 * (i - n_pods) + 1];
+  } else {
+    return;
+  }
   perm[pos] = p;
   for (uint32_t a = 0; a < t.n; ++a) {
     if (t.bytes[a] == 8)
@@ -263,36 +292,20 @@ __global__ __launch_bounds__(kBlock) void k_order_scatter(PermTable t,
   }
 }
 
-// The padding slots: a copy of the group's last sorted position (perm and every array).
-__global__ __launch_bounds__(kBlock) void k_order_pad(PermTable t, const uint32_t* __restrict__ pad,
-                                                      uint32_t n_pad, uint32_t* __restrict__ perm) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n_pad) return;
-  const uint32_t d = pad[2 * i], s = pad[2 * i + 1];
-  perm[d] = perm[s];
-  for (uint32_t a = 0; a < t.n; ++a) {
-    if (t.bytes[a] == 8)
-      static_cast<uint64_t*>(t.dst[a])[d] = static_cast<const uint64_t*>(t.dst[a])[s];
-    else
-      static_cast<uint32_t*>(t.dst[a])[d] = static_cast<const uint32_t*>(t.dst[a])[s];
-  }
-}
-
 // t: the pod arrays (src = caller order, dst = sorted order); scratch: slot, bkt [P] u32.
 hipError_t launch_order_count(const OrderMeta& o, const uint64_t* number, const uint64_t* m_u,
                               const uint64_t* c_u, const uint32_t* need_mem, uint32_t n_pods,
                               uint32_t* hist, uint32_t* bstart, uint32_t* slot, uint32_t* bkt,
                               const PermTable& t, const uint32_t* pad, uint32_t n_pad,
-                              uint32_t* perm, hipStream_t s) {
+                              uint64_t* zero, uint32_t n_zero, uint32_t* perm, hipStream_t s) {
   const uint32_t nbk = o.n_groups << o.nb_log2;
+  if (o.nb_log2 > 10 || nbk > 16u * 1024u) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_order_hist, dim3((n_pods + 1023) / 1024), dim3(1024), nbk * 4, s, o,
                      number, m_u, c_u, need_mem, n_pods, hist, slot, bkt);
-  hipLaunchKernelGGL(k_order_scan, dim3(o.n_groups), dim3(256), 0, s, o, hist, bstart);
-  hipLaunchKernelGGL(k_order_scatter, dim3((n_pods + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                     t, slot, bkt, bstart, n_pods, perm);
-  if (n_pad)
-    hipLaunchKernelGGL(k_order_pad, dim3((n_pad + kBlock - 1) / kBlock), dim3(kBlock), 0, s, t,
-                       pad, n_pad, perm);
+  hipLaunchKernelGGL(k_order_scan, dim3(o.n_groups), dim3(1u << o.nb_log2), 0, s, o, hist,
+                     bstart);
+  hipLaunchKernelGGL(k_order_scatter, dim3((n_pods + n_pad + kBlock - 1) / kBlock), dim3(kBlock),
+                     0, s, t, slot, bkt, bstart, n_pods, pad, n_pad, zero, n_zero, perm);
   return hipGetLastError();
 }
 
