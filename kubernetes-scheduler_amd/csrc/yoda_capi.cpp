@@ -28,7 +28,8 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                      BlockMask* bs, uint32_t bs_stride, uint64_t* blk, uint32_t blk_stride,
                      unsigned long long* stats, hipStream_t s);
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool narrow,
-                          uint64_t* maxima, uint32_t* counts, hipStream_t s);
+                          uint64_t* maxima, uint32_t* counts, double* rcp, float* rcp32,
+                          hipStream_t s);
 hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
                         hipStream_t s);
 hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigned char* sum2,
@@ -54,7 +55,8 @@ hipError_t launch_fill_diskio_state(uint32_t n_pods, uint32_t n_nodes, uint64_t*
 hipError_t launch_finalize(const uint32_t* counts, const int64_t* best, const uint32_t* idx,
                            const uint32_t* ties_in, const int64_t* lowest, uint32_t n_pods,
                            bool generic, int32_t* pick, int32_t* status, uint32_t* ties_out,
-                           uint32_t* flagged, uint32_t* n_flagged, hipStream_t s);
+                           uint32_t* flagged, uint32_t* n_flagged, const FinalScatter& sc,
+                           hipStream_t s);
 hipError_t launch_k3(int K, const unsigned char* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
                      uint32_t C, const PodParams& pp, const uint64_t* maxima, uint32_t n_pods,
                      const uint64_t* bm, uint32_t bm_stride, const uint32_t* flagged,
@@ -296,6 +298,8 @@ struct yoda_handle {
   bool blk_valid = false;   // the last K1 wrote blk (block-classified K1 on this batch)
   bool blk_zeroed = false;  // this run's order already cleared blk (no memset in phase 1)
   bool flagged_dirty = true;  // n_flagged may be nonzero (a generic run since the last clear)
+  bool maxima_sorted = false;  // h->maxima still in the last run's sorted order (n_work rows)
+  bool rcp_ready = false;      // phase 1 wrote the reciprocals of its (final) maxima
   DevBuf bsum;              // [wave][node block] BlockMask: the block K1's sparse masks
   bool bm_sparse = false;   // the last K1 wrote the sparse form (bsum + partial masks only)
   const BlockMask* bs_ptr() const { return bm_sparse ? bsum.as<BlockMask>() : nullptr; }
@@ -406,10 +410,11 @@ uint64_t static_score(uint64_t free_sum, uint64_t total_sum, uint64_t alloc, boo
 }
 
 // Node chunking of one kernel: C chunks x ceil(P/256) pod blocks = B workgroups.  B is sized
-// to ~6 full "rounds" of the kernel's resident capacity (occupancy API), so the last round is
-// nearly full (efficiency >= 1 - pod_blocks / (6 cap)) and chunks stay small enough to
+// to ~8 full "rounds" of the kernel's resident capacity (occupancy API), so the last round is
+// nearly full (efficiency >= 1 - pod_blocks / (8 cap)) and chunks stay small enough to
 // balance data-dependent work (K2 skips infeasible nodes).
-// Tuning knobs for A/B runs (tools/ab.sh): YODA_CHUNK_ROUNDS (default 6) and
+// Tuning knobs for A/B runs (tools/ab.sh): YODA_CHUNK_ROUNDS1 / 2 (K1 / K2; defaults 6 / 8;
+// both at once, config 3: 3 1.92 ms, 4 1.87, 6 1.81, 8 1.78, 10 2.02 per step) and
 // YODA_MIN_CHUNK_NODES (default 0 = no floor; a floor keeps the per-(wave, chunk) set-up of
 // the block-classified kernels amortised when few pod blocks would otherwise mean many
 // small chunks, e.g. one rank's pod shard).  Read once per process.
@@ -418,9 +423,8 @@ static uint32_t env_u32(const char* name, uint32_t dflt) {
   return (s && *s) ? (uint32_t)std::strtoul(s, nullptr, 10) : dflt;
 }
 
-void plan_chunks_for(uint32_t cap, uint32_t n_pods, uint32_t n_nodes, uint32_t* C_out,
-                     uint32_t* chunk_out) {
-  static const uint32_t rounds = std::max<uint32_t>(1, env_u32("YODA_CHUNK_ROUNDS", 6));
+void plan_chunks_for(uint32_t cap, uint32_t rounds, uint32_t n_pods, uint32_t n_nodes,
+                     uint32_t* C_out, uint32_t* chunk_out) {
   static const uint32_t min_chunk = env_u32("YODA_MIN_CHUNK_NODES", 0);
   const uint32_t pod_blocks = std::max<uint32_t>(1, (n_pods + kBlock - 1) / kBlock);
   const uint32_t max_chunks = std::max<uint32_t>(1, (n_nodes + kChunkAlign - 1) / kChunkAlign);
@@ -445,8 +449,13 @@ int capacity(yoda_t* h, int which, int mode) {
 }
 
 void plan_chunks(yoda_t* h, int mode, uint32_t n_pods, uint32_t n_nodes) {
-  plan_chunks_for((uint32_t)capacity(h, 1, mode), n_pods, n_nodes, &h->C1, &h->chunk1);
-  plan_chunks_for((uint32_t)capacity(h, 2, mode), n_pods, n_nodes, &h->C2, &h->chunk2);
+  // K1's partials are 32 B a (pod, chunk) and its reduce reads them all: fewer rounds
+  static const uint32_t r1 = std::max<uint32_t>(1, env_u32("YODA_CHUNK_ROUNDS1",
+                                                           env_u32("YODA_CHUNK_ROUNDS", 6)));
+  static const uint32_t r2 = std::max<uint32_t>(1, env_u32("YODA_CHUNK_ROUNDS2",
+                                                           env_u32("YODA_CHUNK_ROUNDS", 8)));
+  plan_chunks_for((uint32_t)capacity(h, 1, mode), r1, n_pods, n_nodes, &h->C1, &h->chunk1);
+  plan_chunks_for((uint32_t)capacity(h, 2, mode), r2, n_pods, n_nodes, &h->C2, &h->chunk2);
 }
 
 int ensure_state(yoda_t* h, uint32_t P) {
@@ -541,6 +550,7 @@ int order_pods(yoda_t* h, int mode) {
   const uint32_t P = h->n_pods, W = h->n_work;
   h->ordered = false;
   h->blk_zeroed = false;
+  h->maxima_sorted = false;
   if (!h->order_enabled || mode != YODA_MODE_SCV || P < kOrderMinPods || h->n_nodes == 0)
     return YODA_OK;
   const unsigned char* b = h->pod_blob.as<unsigned char>();
@@ -651,7 +661,9 @@ int unpermute_outputs(yoda_t* h) {
 }
 
 // Phase 1: Filter + PreScore maxima (Mode A), or the all-feasible state (Mode B).
-int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts) {
+// final_maxima: this handle's maxima are the run's (no exchange follows).
+int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_maxima = false) {
+  h->rcp_ready = false;
   const uint32_t P = h->n_work;  // sorted positions of this run
   if (P == 0) return YODA_OK;
   if (mode == YODA_MODE_DISKIO) {
@@ -686,8 +698,13 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts) {
     HIP_TRY(h, hipEventRecord(e1, h->stream));
     h->ev_k1.emplace_back(e0, e1);
   }
-  // the block-classified K1 (N32) writes u32 maxima partials
-  HIP_TRY(h, launch_reduce1(part, h->C1, P, h->has_k1sum, maxima, counts, h->stream));
+  // the block-classified K1 (N32) writes u32 maxima partials; a single-handle run's maxima
+  // are final, so the reduce writes the reciprocals too (phase 2 then skips k_prep2)
+  const bool rcp = final_maxima && !h->generic;
+  HIP_TRY(h, launch_reduce1(part, h->C1, P, h->has_k1sum, maxima, counts,
+                            rcp ? h->rcp.as<double>() : nullptr,
+                            rcp ? h->rcp32.as<float>() : nullptr, h->stream));
+  h->rcp_ready = rcp;
   return YODA_OK;
 }
 
@@ -741,8 +758,9 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
   bool is_f64 = true;
   hipEvent_t e0 = h->profiling ? h->next_event() : nullptr;
   hipEvent_t e1 = h->profiling ? h->next_event() : nullptr;
-  if (mode == YODA_MODE_SCV && !h->generic)
+  if (mode == YODA_MODE_SCV && !h->generic && !h->rcp_ready)
     HIP_TRY(h, launch_prep2(maxima, P, h->rcp.as<double>(), h->rcp32.as<float>(), h->stream));
+  h->rcp_ready = false;
   if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
   if (mode == YODA_MODE_DISKIO) {
     HIP_TRY(h, launch_k2_diskio(h->nodes_b.as<NodeRecB>(), h->n_nodes, h->chunk2, h->C2,
@@ -779,9 +797,31 @@ int finalize(yoda_t* h, int mode, const uint32_t* counts, const int64_t* best,
   // once after one (yoda_shard_overflow_count reads it)
   if (generic || h->flagged_dirty) HIP_TRY(h, hipMemsetAsync(h->n_flagged.p, 0, 4, h->stream));
   h->flagged_dirty = generic;
+  if (h->ordered && !generic) {
+    // one kernel: the outputs computed and scattered to the caller's pod order into the
+    // *_alt buffers, then swapped in (as unpermute_outputs would)
+    const uint32_t Pc = h->n_pods;
+    // (the maxima -- 48 B a pod, read only by yoda_download -- stay in sorted order until a
+    // download asks for them: h->maxima_sorted)
+    DevBuf* pairs[][2] = {{&h->pick, &h->pick_alt},         {&h->status, &h->status_alt},
+                          {&h->ties_out, &h->ties_out_alt}, {&h->counts, &h->counts_alt},
+                          {&h->best, &h->best_alt}};
+    for (auto& pr : pairs) HIP_TRY(h, pr[1]->ensure(pr[0]->bytes));
+    FinalScatter sc{h->perm.as<uint32_t>(), Pc, h->counts_alt.as<uint32_t>(),
+                    h->best_alt.as<int64_t>(), nullptr, nullptr};
+    HIP_TRY(h, launch_finalize(counts, best, idx, ties, low, P, false, h->pick_alt.as<int32_t>(),
+                               h->status_alt.as<int32_t>(), h->ties_out_alt.as<uint32_t>(),
+                               h->flagged.as<uint32_t>(), h->n_flagged.as<uint32_t>(), sc,
+                               h->stream));
+    for (auto& pr : pairs) std::swap(*pr[0], *pr[1]);
+    h->maxima_sorted = true;
+    return YODA_OK;
+  }
+  const FinalScatter none{};
   HIP_TRY(h, launch_finalize(counts, best, idx, ties, low, P, generic, h->pick.as<int32_t>(),
                              h->status.as<int32_t>(), h->ties_out.as<uint32_t>(),
-                             h->flagged.as<uint32_t>(), h->n_flagged.as<uint32_t>(), h->stream));
+                             h->flagged.as<uint32_t>(), h->n_flagged.as<uint32_t>(), none,
+                             h->stream));
   if (generic) {
     uint32_t nfl = 0;
     HIP_TRY(h, hipMemcpyAsync(&nfl, h->n_flagged.p, 4, hipMemcpyDeviceToHost, h->stream));
@@ -1353,7 +1393,8 @@ int yoda_run(yoda_t* h, int mode, uint32_t flags) {
   if (rc) return rc;
   try {
     if ((rc = order_pods(h, mode))) return rc;
-    if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>()))) return rc;
+    if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), true)))
+      return rc;
     if ((rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), h->best.as<int64_t>(),
                      h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>())))
       return rc;
@@ -1395,6 +1436,20 @@ int yoda_download(yoda_t* h, yoda_eval_out* out) {
       HIP_TRY(h, hipMemcpyAsync(st.data(), h->status.p, P * 4ull, hipMemcpyDeviceToHost, s));
     }
     std::vector<uint64_t> mx;
+    if (out->maxima && h->maxima_sorted) {  // scatter the maxima to the caller's order now
+      const uint32_t W = h->n_work;
+      HIP_TRY(h, h->maxima_alt.ensure(h->maxima.bytes));
+      PermTable t{};
+      for (uint32_t r = 0; r < 6; ++r) {
+        t.src[t.n] = h->maxima.as<unsigned char>() + (size_t)r * W * 8;
+        t.dst[t.n] = h->maxima_alt.as<unsigned char>() + (size_t)r * P * 8;
+        t.bytes[t.n] = 8;
+        ++t.n;
+      }
+      HIP_TRY(h, launch_permute(t, h->perm.as<uint32_t>(), W, true, s));
+      std::swap(h->maxima, h->maxima_alt);
+      h->maxima_sorted = false;
+    }
     if (out->maxima) {
       mx.resize(6 * (size_t)P);
       HIP_TRY(h, hipMemcpyAsync(mx.data(), h->maxima.p, mx.size() * 8, hipMemcpyDeviceToHost, s));

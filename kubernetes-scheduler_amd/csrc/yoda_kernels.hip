@@ -796,12 +796,19 @@ __device__ __forceinline__ uint64_t mask_at(const MaskSrc& m, uint32_t w, uint32
 // Per-pod merge of K1 chunk partials -> maxima [6][P] and counts [2][P].  One thread per
 // (pod, field) (grid.y = the 6 maxima + 2 counts), chunk loads unrolled so each thread keeps
 // several in flight.  NARROW: u32 maxima partials (the N32 K1).
+__device__ __forceinline__ double ru_100_over(double M);
+__device__ __forceinline__ float ru32_100_over(double M);
+
+// rcp != nullptr (a single-handle run, whose maxima are final here): each maxima thread also
+// writes its field's reciprocals (k_prep2's, fused).
 template <bool NARROW>
 __global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__ pmax,
                                                     const uint32_t* __restrict__ pcnt, uint32_t C,
                                                     uint32_t n_pods,
                                                     uint64_t* __restrict__ maxima,
-                                                    uint32_t* __restrict__ counts) {
+                                                    uint32_t* __restrict__ counts,
+                                                    double* __restrict__ rcp,
+                                                    float* __restrict__ rcp32) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t f = blockIdx.y;
   if (p >= n_pods) return;
@@ -819,6 +826,13 @@ __global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__
       for (uint32_t c = 0; c < C; ++c) mx = umax64(mx, src[(size_t)c * n_pods]);
     }
     maxima[(size_t)f * n_pods + p] = mx;
+    // rcp rows: bw, core, power, free, total (k_prep2's order); the clock has none
+    const int k = f == kMaxBw ? 0 : f == kMaxCore ? 1 : f == kMaxPower ? 2 : f == kMaxFree ? 3
+                : f == kMaxTotal ? 4 : -1;
+    if (rcp && k >= 0) {
+      rcp[(size_t)k * n_pods + p] = ru_100_over((double)mx);
+      if (k < 3) rcp32[(size_t)k * n_pods + p] = ru32_100_over((double)mx);
+    }
   } else {
     const uint32_t* src = pcnt + (size_t)(f - 6) * C * n_pods + p;
     uint32_t s = 0;
@@ -2360,37 +2374,52 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const uint32_t* __restrict_
                                                      int32_t* __restrict__ status,
                                                      uint32_t* ties_out,
                                                      uint32_t* __restrict__ flagged,
-                                                     uint32_t* __restrict__ n_flagged) {
+                                                     uint32_t* __restrict__ n_flagged,
+                                                     FinalScatter sc) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (p >= n_pods) return;
+  if (sc.perm) {
+    // ordered run: every per-pod output goes straight to the caller's pod order (a padded
+    // order's copies write the same values twice)
+    const uint32_t q = sc.perm[p];
+    sc.counts[q] = counts[p];
+    sc.counts[(size_t)sc.n_out + q] = counts[(size_t)n_pods + p];
+    sc.best[q] = best[p];
+    if (sc.maxima) {
+#pragma unroll
+      for (int f = 0; f < 6; ++f)
+        sc.maxima[(size_t)f * sc.n_out + q] = sc.maxima_in[(size_t)f * n_pods + p];
+    }
+  }
+  const uint32_t o = sc.perm ? sc.perm[p] : p;  // where this pod's outputs land
   const uint32_t nf = counts[p], nz = counts[(size_t)n_pods + p];
   uint32_t t = ties_io[p];
   if (nf == 0) {
-    pick[p] = -1;
-    status[p] = 1;
+    pick[o] = -1;
+    status[o] = 1;
     t = 0;
   } else if (nf == 1) {  // k8s: the only feasible node is returned without scoring
-    pick[p] = (int32_t)idx[p];
-    status[p] = 0;
+    pick[o] = (int32_t)idx[p];
+    status[o] = 0;
     t = 1;
   } else if (nz > 0) {  // Score would divide by TotalMemorySum == 0: Go panics
-    pick[p] = -2;
-    status[p] = 2;
+    pick[o] = -2;
+    status[o] = 2;
     t = 0;
   } else {
     const int64_t h = best[p];
     int64_t l = lowest[p];
     if (h == l) --l;  // scheduler.go:173-175
     if (generic && (uint64_t)(h - l) > (uint64_t)(kI64Max / 100)) {
-      pick[p] = -3;  // pending: exact normalize (K3)
-      status[p] = -1;
+      pick[o] = -3;  // pending: exact normalize (K3)
+      status[o] = -1;
       flagged[atomicAdd(n_flagged, 1u)] = p;
     } else {
-      pick[p] = (int32_t)idx[p];
-      status[p] = 0;
+      pick[o] = (int32_t)idx[p];
+      status[o] = 0;
     }
   }
-  ties_out[p] = t;
+  ties_out[o] = t;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2594,8 +2623,13 @@ int kernel_capacity(int K, Path path, int which, int mode_diskio) {
 // chunks, one wave per pod (strided over chunks) when there are many.
 constexpr uint32_t kWaveReduceChunks = 48;
 
+hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
+                        hipStream_t s);
+
+// rcp / rcp32 non-null: also the reciprocals (k_prep2 fused; the wave variant runs it after)
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool narrow,
-                          uint64_t* maxima, uint32_t* counts, hipStream_t s) {
+                          uint64_t* maxima, uint32_t* counts, double* rcp, float* rcp32,
+                          hipStream_t s) {
   if (C > kWaveReduceChunks) {
     if (narrow)
       hipLaunchKernelGGL(k_reduce1_wave<true>, dim3(n_pods), dim3(kWave), 0, s, part.max_u,
@@ -2603,14 +2637,15 @@ hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, boo
     else
       hipLaunchKernelGGL(k_reduce1_wave<false>, dim3(n_pods), dim3(kWave), 0, s, part.max_u,
                          part.cnt, C, n_pods, maxima, counts);
+    if (rcp) return launch_prep2(maxima, n_pods, rcp, rcp32, s);
   } else {
     const dim3 grid((n_pods + kBlock - 1) / kBlock, 8);
     if (narrow)
       hipLaunchKernelGGL(k_reduce1<true>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
-                         n_pods, maxima, counts);
+                         n_pods, maxima, counts, rcp, rcp32);
     else
       hipLaunchKernelGGL(k_reduce1<false>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
-                         n_pods, maxima, counts);
+                         n_pods, maxima, counts, rcp, rcp32);
   }
   return hipGetLastError();
 }
@@ -2848,9 +2883,12 @@ hipError_t launch_fill_diskio_state(uint32_t n_pods, uint32_t n_nodes, uint64_t*
 hipError_t launch_finalize(const uint32_t* counts, const int64_t* best, const uint32_t* idx,
                            const uint32_t* ties_in, const int64_t* lowest, uint32_t n_pods,
                            bool generic, int32_t* pick, int32_t* status, uint32_t* ties_out,
-                           uint32_t* flagged, uint32_t* n_flagged, hipStream_t s) {
+                           uint32_t* flagged, uint32_t* n_flagged, const FinalScatter& sc,
+                           hipStream_t s) {
+  if (sc.perm && generic) return hipErrorInvalidValue;  // K3 still needs the sorted outputs
   hipLaunchKernelGGL(k_finalize, pod_grid(n_pods), dim3(kBlock), 0, s, counts, best, idx, ties_in,
-                     lowest, n_pods, generic ? 1 : 0, pick, status, ties_out, flagged, n_flagged);
+                     lowest, n_pods, generic ? 1 : 0, pick, status, ties_out, flagged, n_flagged,
+                     sc);
   return hipGetLastError();
 }
 

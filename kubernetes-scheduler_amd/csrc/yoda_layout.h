@@ -242,6 +242,17 @@ struct OrderMeta {
   uint32_t n_groups, nb_log2, m_shift;
 };
 
+// k_finalize of an ordered run: the caller-order outputs (perm == nullptr: none, the
+// outputs stay in sorted order); n_out = caller pods, the row stride of counts / maxima.
+struct FinalScatter {
+  const uint32_t* perm;
+  uint32_t n_out;
+  uint32_t* counts;          // [2][n_out]
+  int64_t* best;             // [n_out]
+  uint64_t* maxima;          // [6][n_out], or none (left in sorted order)
+  const uint64_t* maxima_in; // [6][n_pods] sorted
+};
+
 struct PermTable {
   const void* src[kPermArrays];
   void* dst[kPermArrays];
