@@ -242,6 +242,11 @@ int yoda_comm_run_local(yoda_t* const* handles, int world, int mode);
  * every output is returned in the caller's pod order, so results never depend on it.
  * enable = 0 turns the ordering off (default on).  Takes effect from the next run. */
 int yoda_set_pod_order(yoda_t* h, int enable);
+/* The batch order (diagnostic): out[4] = {(clock, number, has-memory) groups of the uploaded
+ * batch (0: too many for the counting sort), its sorted positions with every group padded to
+ * a wave, the sorted positions of the last run, how that run was ordered (0 not, 1 radix sort,
+ * 2 counting sort)}. */
+int yoda_order_info(const yoda_t* h, uint32_t* out);
 
 /* ---- kernel timing ----------------------------------------------------------------- */
 /* enable != 0: every subsequent K1 / K2 launch is bracketed by HIP events recorded on the

@@ -300,6 +300,7 @@ struct yoda_handle {
   bool flagged_dirty = true;  // n_flagged may be nonzero (a generic run since the last clear)
   bool maxima_sorted = false;  // h->maxima still in the last run's sorted order (n_work rows)
   bool rcp_ready = false;      // phase 1 wrote the reciprocals of its (final) maxima
+  bool count_order = false;    // this run orders by the counting sort (private runs)
   DevBuf bsum;              // [wave][node block] BlockMask: the block K1's sparse masks
   bool bm_sparse = false;   // the last K1 wrote the sparse form (bsum + partial masks only)
   const BlockMask* bs_ptr() const { return bm_sparse ? bsum.as<BlockMask>() : nullptr; }
@@ -572,8 +573,8 @@ int order_pods(yoda_t* h, int mode) {
   // one run to the next): only the padded single-handle run uses it.  Every other entry
   // point takes the radix sort, whose order is a function of the batch alone -- shards of
   // one batch on several GPUs must agree on it.
-  if (h->og_ok && W != P) {
-    const bool padded = true;
+  if (h->count_order) {
+    const bool padded = W != P;
     // the block kernels (N32 with both summaries) read 5 of the pod arrays; the rest of the
     // sorted blob is left unwritten and unread
     if (h->path == Path::N32 && h->has_k1sum && h->has_k2sum) {
@@ -1374,16 +1375,21 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
   }
 }
 
-// pad: this run may pad the order's groups to whole waves (yoda_run without the bitmask;
-// every other entry point keeps one sorted position per caller pod).
+// pad: a private run (yoda_run without the bitmask) -- it may take the counting sort and pad
+// the order's groups to whole waves; every other entry point keeps the radix order, one
+// sorted position per caller pod, reproducible across the shards of a batch.
 static int prepare_run(yoda_t* h, int mode, bool pad = false) {
   int rc = check_ready(h, mode);
   if (rc) return rc;
   h->topk_ready = false;  // this run overwrites the bitmask and reciprocals
   const bool ordering = h->order_enabled && mode == YODA_MODE_SCV &&
                         h->n_pods >= kOrderMinPods && h->n_nodes > 0;
-  h->n_work = pad && ordering && h->og_ok && env_u32("YODA_ORDER_PAD", 1) ? h->n_pad
-                                                                         : h->n_pods;
+  // a private run takes the counting sort, padded when that adds at most 1/8 of the batch
+  // (many small groups would otherwise multiply the work)
+  h->count_order = pad && ordering && h->og_ok;
+  const bool padded = h->count_order && env_u32("YODA_ORDER_PAD", 1) &&
+                      (uint64_t)h->n_pad * 8 <= (uint64_t)h->n_pods * 9;
+  h->n_work = padded ? h->n_pad : h->n_pods;
   plan_chunks(h, mode, h->n_work, h->n_nodes);
   return ensure_state(h, std::max<uint32_t>(h->n_work, 1));
 }
@@ -1650,6 +1656,15 @@ int yoda_shard_overflow_count(yoda_t* h, uint32_t* n_pods) {
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, hipMemcpyAsync(n_pods, h->n_flagged.p, 4, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
+  return YODA_OK;
+}
+
+int yoda_order_info(const yoda_t* h, uint32_t* out) {
+  if (!h || !out) return YODA_ERR_INVALID_ARG;
+  out[0] = h->og_ok ? h->og_groups : 0u;
+  out[1] = h->n_pad;
+  out[2] = h->n_work;
+  out[3] = h->ordered ? (h->count_order ? 2u : 1u) : 0u;
   return YODA_OK;
 }
 

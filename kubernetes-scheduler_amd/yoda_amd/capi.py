@@ -56,6 +56,7 @@ _SIGS = {
     "yoda_shard_overflow_count": ([_vp, C.POINTER(C.c_uint32)], C.c_int),
     "yoda_profile": ([_vp, C.c_int], C.c_int),
     "yoda_set_pod_order": ([_vp, C.c_int], C.c_int),
+    "yoda_order_info": ([_vp, _vp], C.c_int),
     "yoda_profile_read": ([_vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                            C.POINTER(C.c_uint32)], C.c_int),
     "yoda_greedy": ([_vp, C.POINTER(CPodSoA), C.c_int, _u32, C.POINTER(C.c_int32)], C.c_int),
@@ -273,6 +274,14 @@ class Yoda:
         r = C.c_uint32()
         self._check(lib().yoda_greedy_restarts(self._h, C.byref(r)), "yoda_greedy_restarts")
         return r.value
+
+    def order_info(self) -> dict:
+        """yoda_order_info: the batch's order groups, padded size, last run's sorted size and
+        ordering kind (0 none, 1 radix, 2 counting)."""
+        out = np.zeros(4, np.uint32)
+        self._check(lib().yoda_order_info(self._h, _np_ptr(out)), "yoda_order_info")
+        return {"groups": int(out[0]), "padded": int(out[1]), "work": int(out[2]),
+                "kind": int(out[3])}
 
     def set_pod_order(self, enable: bool = True):
         """Sort Mode-A batches on the device before K1/K2 (default on); results are returned
