@@ -1265,12 +1265,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   const uint32_t m_max = wave_max_u32(act ? sc.m : 0u), m_min = wave_min_u32(act ? sc.m : ~0u);
   const uint32_t c_max = wave_max_u32(act ? sc.c : 0u), c_min = wave_min_u32(act ? sc.c : ~0u);
 
-  double best = -1.0, low = 1.0e300;        // pod lane
-  uint32_t idx = 0xffffffffu, ties = 0;
   double ubest = -1.0, ulow = 1.0e300;      // node lane (U nodes)
   uint32_t uidx = 0xffffffffu, uties = 0;
-  uint64_t rbest = 0, rlow = ~0ull;          // pod lane, record nodes (integer scores)
+  // pod lane, every per-pod node: integer scores (static part + basic, exact below 2^53);
+  // (0, 0 ties) is the empty state -- a first score of 0 counts as a tie of it
+  uint64_t rbest = 0, rlow = ~0ull;
   uint32_t ridx = 0xffffffffu, rties = 0;
+  auto to_u = [](double x) {  // an integer-valued double in [0, 2^52) -> its value
+    return (uint64_t)__double_as_longlong(x + 4503599627370496.0) - 0x4330000000000000ull;
+  };
   uint32_t npart = 0;  // STATS: per-pod-pass nodes of this (wave, chunk)
   // One block: the wave's mask of node nb + lane and its summary (kept for the per-pod pass,
   // read back with v_readlane), loaded together: one memory latency per block.
@@ -1432,22 +1435,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       if (!uni_max) atomicAdd(stats + 8, (unsigned long long)__builtin_popcountll(part_b));
     }
     if (STATS) npart += (uint32_t)__builtin_popcountll(part_b);
-    // node order is not kept across the two loops: the tie rule keeps the lowest index.
+    // node order is not kept across the loops: the tie rule keeps the lowest index.
     // Branch-free (selects, no exec-mask branches): f = this pod lane is feasible on nn.
-    auto take = [&](bool f, double raw, uint32_t nn) {
-      const bool gt = f && raw > best, eq = f && raw == best;
-      idx = gt ? nn : (eq ? min(idx, nn) : idx);
-      ties = gt ? 1u : ties + (eq ? 1u : 0u);
-      best = gt ? raw : best;
-      low = f && raw < low ? raw : low;  // no NaN here: a compare, not fmin's canonicalizes
-    };
-#ifdef YODA_ABL_NOPOD
-    rec_b = 0;
-    part_b = 0;
-#endif
     uint64_t rb = rec_b;
     part_b &= ~rec_b;
-    // records: integer scores (static part + basic < 2^53) into the record state
     auto take_r = [&](bool f, uint64_t raw, uint32_t nn) {
       const bool gt = f & (raw > rbest), eq = f & (raw == rbest);
       ridx = gt ? nn : (eq ? min(ridx, nn) : ridx);
@@ -1520,27 +1511,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         } else {
           // several reciprocal sets: Scorer<N32>'s one-model branch on the node lane's data,
           // with its own reciprocals (shared quotients f32, memory quotients f64)
+          const Scorer<Path::N32>& own = sc;
           const uint32_t shared =
-            (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.x, j) * sc.r_bw) +
-            (uint32_t)((float)ckj * sc.r_bw) +
-            2u * (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.y, j) * sc.r_core) +
-            (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.z, j) * sc.r_pow);
+            (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.x, j) * own.r_bw) +
+            (uint32_t)((float)ckj * own.r_bw) +
+            2u * (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.y, j) * own.r_core) +
+            (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.z, j) * own.r_pow);
           uint32_t mem = 0;
 #pragma unroll
           for (int t = 0; t < K; ++t) {
             const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)fs.v[t], j);
             const uint32_t to = (uint32_t)__builtin_amdgcn_readlane((int)ts.v[t], j);
-            const uint32_t term = 3u * (uint32_t)((double)f * sc.r_free) +
-                                  (uint32_t)((double)to * sc.r_tot);
+            const uint32_t term = 3u * (uint32_t)((double)f * own.r_free) +
+                                  (uint32_t)((double)to * own.r_tot);
             mem += (uint32_t)t < nq ? term : 0u;  // the qualifying cards are a prefix
           }
           basic = ckj >= sc.c ? nq * shared + mem : 0u;  // algorithm.go:271
         }
         raw = (double)basic + __longlong_as_double((long long)sb);
       } else {
-        raw = sc.template raw<K>(nodes + (size_t)nn * NS);
+        raw = sc.template raw<K>(nodes + (size_t)nn * NS);  // a mixed-model node
       }
-      take(((mj >> lane) & 1ull) != 0ull, raw, nn);
+      take_r(((mj >> lane) & 1ull) != 0ull, to_u(raw), nn);
     }
   };
   if (blk) {
@@ -1589,18 +1581,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     wl = fmin(wl, __shfl_xor(wl, o, kWave));
   }
   if (!live) return;
-  if (rties > 0) {  // the record nodes (exact: every score < 2^53)
-    const double rb_d = (double)rbest;
-    if (rb_d > best) {
-      best = rb_d;
-      idx = ridx;
-      ties = rties;
-    } else if (rb_d == best) {
-      idx = min(idx, ridx);
-      ties += rties;
-    }
-    low = fmin(low, (double)rlow);
-  }
+  // the per-pod nodes' state (exact: every score < 2^53), then the U nodes
+  double best = rties > 0 ? (double)rbest : -1.0, low = rties > 0 ? (double)rlow : 1.0e300;
+  uint32_t idx = ridx, ties = rties;
   if (act && wt > 0) {
     if (wb > best) {
       best = wb;
