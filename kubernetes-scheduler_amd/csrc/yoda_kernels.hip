@@ -218,11 +218,22 @@ __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
 struct Tile {
   uint32_t pb, chunk;
 };
+#ifndef YODA_TILE_POD_MAJOR
+#define YODA_TILE_POD_MAJOR 1
+#endif
 __device__ __forceinline__ Tile tile() {
   const uint32_t PB = gridDim.x, C = gridDim.y;
   if ((C & 7u) != 0u) return {blockIdx.x, blockIdx.y};
   const uint32_t L = blockIdx.x + blockIdx.y * PB;
   const uint32_t i = L >> 3;
+  // XCD (L & 7) owns chunks (L & 7) + 8 g.  Pod-major: it takes all its chunks of one pod
+  // block before the next, so the pod block's parameters are read from HBM once per XCD
+  // (its C / 8 chunks' node summaries -- ~1 MB -- stay in the XCD's 4 MB L2 meanwhile);
+  // chunk-major walks one chunk across all pod blocks at a time.
+  if (YODA_TILE_POD_MAJOR) {
+    const uint32_t G = C >> 3;
+    return {i / G, (i % G) * 8u + (L & 7u)};
+  }
   return {i % PB, (i / PB) * 8u + (L & 7u)};
 }
 
