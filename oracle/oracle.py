@@ -39,6 +39,8 @@ def lib():
                                       C.POINTER(CEvalOut)]
         L.oracle_schedule_range.argtypes = [C.POINTER(CNodeSoA), C.POINTER(CPodSoA), C.c_int,
                                             C.c_uint32, C.c_uint32, C.c_int, C.POINTER(CEvalOut)]
+        L.oracle_schedule_memo.argtypes = [C.POINTER(CNodeSoA), C.POINTER(CPodSoA), C.c_uint32,
+                                           C.c_int, C.POINTER(CEvalOut)]
         L.oracle_pod_detail.argtypes = [C.POINTER(CNodeSoA), C.POINTER(CPodSoA), C.c_uint32,
                                         C.c_int, C.POINTER(C.c_uint8), C.POINTER(C.c_int64),
                                         C.POINTER(C.c_int64)]
@@ -59,6 +61,18 @@ def schedule(nodes: NodeSoA, pods: PodSoA, mode: int = 0, threads: int = 1,
     rc = lib().oracle_schedule_range(C.byref(cn), C.byref(cp), mode, p0, p1, threads, C.byref(co))
     if rc != 0:
         raise RuntimeError(f"oracle_schedule rc={rc}")
+    return res
+
+
+def schedule_memo(nodes: NodeSoA, pods: PodSoA, first: int, threads: int = 1) -> EvalResult:
+    """Mode B with the B3 Redis memo quirk, node `first` scored first in every cycle
+    (documentation mode: SURVEY §8a B3; the product path computes the uncached B1)."""
+    nodes, pods = nodes.normalized(), pods.normalized()
+    res = EvalResult.empty(pods.n_pods)
+    cn, cp, co = nodes.c(), pods.c(), res.c()
+    rc = lib().oracle_schedule_memo(C.byref(cn), C.byref(cp), first, threads, C.byref(co))
+    if rc != 0:
+        raise RuntimeError(f"oracle_schedule_memo rc={rc}")
     return res
 
 

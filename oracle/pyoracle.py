@@ -216,6 +216,23 @@ def diskio_score(pod: Pod, s: Scv) -> int:  # algorithm.go:99-119
     return uint64_to_int64(go_float64_to_uint64(si))
 
 
+def diskio_score_memo(pod: Pod, s: Scv, computed: bool) -> int:
+    """B3 memo quirk (algorithm.go:57-63,116): the cycle's first Score call computes and
+    returns uint64(S); later calls read FormatFloat(S, 'f', -1, 64) back through
+    StrToUint64 (filter.go:67-73), so only a finite, integral S >= 0 survives."""
+    if computed:
+        return diskio_score(pod, s)
+    with _fpe_ignored():
+        q = _fdiv(float(pod.rcpu), pod.rio)
+        beta = _fdiv(1.0, 1.0 + q)
+    alpha = 1 - beta
+    li = abs(_fmul(alpha, s.cpu / 100.0) - _fmul(beta, s.disk_io / 50.0))
+    si = 10.0 - _fmul(10.0, li)
+    if math.isnan(si) or math.isinf(si) or si != math.trunc(si) or si < 0 or si >= 2.0 ** 63:
+        return 0
+    return int(si)
+
+
 class _fpe_ignored:
     def __enter__(self):
         return self
@@ -251,8 +268,10 @@ class CycleResult:
     tie_set: List[int] = field(default_factory=list)
 
 
-def schedule_one(pod: Pod, scvs: Sequence[Scv], mode: int = 0) -> CycleResult:
-    """One kube-scheduler v1.22.3 cycle with yoda as the only scorer (see yoda_oracle.c)."""
+def schedule_one(pod: Pod, scvs: Sequence[Scv], mode: int = 0,
+                 memo_first: int | None = None) -> CycleResult:
+    """One kube-scheduler v1.22.3 cycle with yoda as the only scorer (see yoda_oracle.c).
+    memo_first (Mode B only): the B3 memo quirk with that node's Score call first."""
     if mode == 1:
         feasible = list(range(len(scvs)))  # Filter pass-through (scheduler.go:96-99)
         mv = MaxValue()
@@ -266,14 +285,14 @@ def schedule_one(pod: Pod, scvs: Sequence[Scv], mode: int = 0) -> CycleResult:
     if len(feasible) == 1:  # k8s returns the only feasible node without scoring
         r.pick, r.status, r.n_ties, r.tie_set = feasible[0], STATUS_OK, 1, [feasible[0]]
         try:
-            r.top_score = _score(pod, scvs[feasible[0]], mv, mode)
+            r.top_score = _score(pod, scvs[feasible[0]], mv, mode, memo_first, feasible[0])
         except DivideByZero:
             r.top_score = 0
         return r
     scores = []
     try:
         for i in feasible:
-            scores.append(_score(pod, scvs[i], mv, mode))
+            scores.append(_score(pod, scvs[i], mv, mode, memo_first, i))
     except DivideByZero:
         r.pick, r.status = PICK_ERROR, STATUS_DIV_ZERO
         return r
@@ -295,8 +314,10 @@ def schedule_one(pod: Pod, scvs: Sequence[Scv], mode: int = 0) -> CycleResult:
     return r
 
 
-def _score(pod: Pod, s: Scv, mv: MaxValue, mode: int) -> int:
+def _score(pod: Pod, s: Scv, mv: MaxValue, mode: int, memo_first=None, n: int = -1) -> int:
     if mode == 1:
+        if memo_first is not None:
+            return diskio_score_memo(pod, s, n == memo_first)
         return diskio_score(pod, s)
     raw = basic_score(mv, pod, s)
     raw = (raw + allocate_score(s)) & U64

@@ -242,6 +242,31 @@ static int64_t diskio_score(const yoda_pod_soa* pd, uint32_t p, const yoda_node_
   return uint64_to_int64(go_float64_to_uint64(s));
 }
 
+/* B3 documentation mode — the Redis memo quirk of CalculateScore (algorithm.go:57-63,116,
+ * SURVEY §8a B3).  Within one cycle (NormalizeScore flushes the DB, scheduler.go:160) the
+ * first Score call misses "S-<node>", computes every node's S and stores it (:116); it
+ * returns uint64(S) for its own node.  Every later call returns StrToUint64 (filter.go:67-73)
+ * of the stored string: go-redis writes a float64 as FormatFloat(S, 'f', -1, 64), so Atoi
+ * accepts it only when S is finite and integral; a negative integer wraps in uint64() and
+ * then fails Uint64ToInt64 (scheduler.go:154); so the node scores S if S is a non-negative
+ * integer, else 0.  Which call runs first depends on goroutine order: `first` fixes it. */
+static int64_t diskio_score_memo(const yoda_pod_soa* pd, uint32_t p, const yoda_node_soa* nd,
+                                 uint32_t n, int64_t first) {
+  if ((int64_t)n == first) return diskio_score(pd, p, nd, n);
+  double rio = pd->rio[p];
+  double rcpu = (double)pd->rcpu[p];
+  double beta = 1.0 / (1.0 + rcpu / rio);
+  double alpha = 1 - beta;
+  double v = nd->cpu[n] / 100.0;
+  double u = nd->disk_io[n] / 50.0;
+  double a = alpha * v;
+  double b = beta * u;
+  double s = 10.0 - 10.0 * fabs(a - b);
+  if (!isfinite(s) || s != trunc(s)) return 0;           /* "NaN", "+Inf", "9.5": Atoi fails */
+  if (s < 0 || s >= 9223372036854775808.0) return 0;     /* wraps / out of Atoi range -> 0 */
+  return (int64_t)s;
+}
+
 /* Per-pod result of one scheduling cycle. */
 typedef struct {
   int32_t pick, status;
@@ -259,7 +284,7 @@ typedef struct {
  *   the LOWEST node index of the tie set and reports the tie set's size.
  * scratch: >= 2*N int64 + N uint32. */
 static void schedule_one(const yoda_node_soa* nd, const yoda_pod_soa* pd, uint32_t p, int mode,
-                         int64_t* scores, uint32_t* feas, cycle_result* r) {
+                         int64_t memo_first, int64_t* scores, uint32_t* feas, cycle_result* r) {
   uint32_t nf = 0;
   max_value mv = {1, 1, 1, 1, 1, 1};
   memset(r, 0, sizeof(*r));
@@ -289,6 +314,8 @@ static void schedule_one(const yoda_node_soa* nd, const yoda_pod_soa* pd, uint32
       raw += allocate_score(nd, n, &div_zero);
       raw += actual_score(nd, n, &div_zero);
       scores[i] = uint64_to_int64(raw);
+    } else if (memo_first >= 0) {
+      scores[i] = diskio_score_memo(pd, p, nd, n, memo_first);
     } else {
       scores[i] = diskio_score(pd, p, nd, n);
     }
@@ -358,9 +385,9 @@ static void write_result(const cycle_result* r, uint32_t p, yoda_eval_out* out) 
   }
 }
 
-/* Schedule every pod independently against the snapshot (pods [p0, p1)). */
-int oracle_schedule_range(const yoda_node_soa* nd, const yoda_pod_soa* pd, int mode, uint32_t p0,
-                          uint32_t p1, int n_threads, yoda_eval_out* out) {
+static int schedule_range(const yoda_node_soa* nd, const yoda_pod_soa* pd, int mode,
+                          int64_t memo_first, uint32_t p0, uint32_t p1, int n_threads,
+                          yoda_eval_out* out) {
   if (!nd || !pd || !out || p1 > pd->n_pods || p0 > p1) return YODA_ERR_INVALID_ARG;
   if (mode != YODA_MODE_SCV && mode != YODA_MODE_DISKIO) return YODA_ERR_INVALID_ARG;
   if (n_threads < 1) n_threads = 1;
@@ -376,7 +403,7 @@ int oracle_schedule_range(const yoda_node_soa* nd, const yoda_pod_soa* pd, int m
 #pragma omp for schedule(dynamic, 4)
       for (int64_t p = (int64_t)p0; p < (int64_t)p1; ++p) {
         cycle_result r;
-        schedule_one(nd, pd, (uint32_t)p, mode, scores, feas, &r);
+        schedule_one(nd, pd, (uint32_t)p, mode, memo_first, scores, feas, &r);
         write_result(&r, (uint32_t)p, out);
       }
     }
@@ -384,6 +411,21 @@ int oracle_schedule_range(const yoda_node_soa* nd, const yoda_pod_soa* pd, int m
     free(feas);
   }
   return err ? YODA_ERR_INVALID_ARG : YODA_OK;
+}
+
+/* Schedule every pod independently against the snapshot (pods [p0, p1)). */
+int oracle_schedule_range(const yoda_node_soa* nd, const yoda_pod_soa* pd, int mode, uint32_t p0,
+                          uint32_t p1, int n_threads, yoda_eval_out* out) {
+  return schedule_range(nd, pd, mode, -1, p0, p1, n_threads, out);
+}
+
+/* Mode B with the B3 memo quirk (diskio_score_memo): node `first` is the one whose Score
+ * call runs first in every cycle.  Documentation mode only, not a product path. */
+int oracle_schedule_memo(const yoda_node_soa* nd, const yoda_pod_soa* pd, uint32_t first,
+                         int n_threads, yoda_eval_out* out) {
+  if (!nd || first >= nd->n_nodes) return YODA_ERR_INVALID_ARG;
+  return schedule_range(nd, pd, YODA_MODE_DISKIO, (int64_t)first, 0, pd ? pd->n_pods : 0,
+                        n_threads, out);
 }
 
 int oracle_schedule(const yoda_node_soa* nd, const yoda_pod_soa* pd, int mode, int n_threads,
@@ -478,7 +520,7 @@ int oracle_greedy(const yoda_node_soa* nd_in, const yoda_pod_soa* pd, int mode, 
   for (uint32_t i = 0; i < P; ++i) {
     uint32_t p = order[i];
     cycle_result r;
-    schedule_one(&nd, pd, p, mode, scores, feas, &r);
+    schedule_one(&nd, pd, p, mode, -1, scores, feas, &r);
     pick[p] = r.pick;
     if (status) status[p] = r.status;
     if (r.pick >= 0) {

@@ -82,6 +82,53 @@ def test_kat_mode_b(rcpu, rio, cases):
     assert res.pick[0] == want.index(best) and res.n_ties[0] == want.count(best)
 
 
+# KAT B3 (memo quirk, documentation mode): Rcpu 100, Rio 100 -> beta = alpha = 1/2.
+# (cpu%, disk MB/s) -> S = 10 - 10|V/2 - U/2|: 9.5, 9.0, 5.0, 2.5, -5.0.  The node scored first
+# gets trunc(S); the others read FormatFloat(S) back through Atoi: 9.5 -> 0, 2.5 -> 0,
+# -5 -> uint64 wrap -> Uint64ToInt64 -> 0.
+B3_NODES = [(10, 0), (20, 0), (100, 0), (50, 100), (0, 150)]
+B3_CASES = [  # first -> (scores, pick, ties)
+    (None, [9, 9, 5, 2, 0], 0, 2),   # uncached B1 (the product semantics)
+    (0, [9, 9, 5, 0, 0], 0, 2),
+    (1, [0, 9, 5, 0, 0], 1, 1),      # the quirk moves the pick
+    (3, [0, 9, 5, 2, 0], 1, 1),
+    (4, [0, 9, 5, 0, 0], 1, 1),
+]
+
+
+@pytest.mark.parametrize("first,scores,pick,ties", B3_CASES)
+def test_kat_b3_memo_quirk(first, scores, pick, ties):
+    pod = po.Pod(rio=100.0, rcpu=100)
+    scvs = [po.Scv(card_number=0, card_list=[], free_memory_sum=0, total_memory_sum=1,
+                   cpu=float(c), disk_io=float(d)) for c, d in B3_NODES]
+    got = [po._score(pod, s, None, MODE_DISKIO, first, n) for n, s in enumerate(scvs)]
+    assert got == scores
+    r = po.schedule_one(pod, scvs, MODE_DISKIO, memo_first=first)
+    assert (r.pick, r.n_ties) == (pick, ties)
+    nodes, pods = oracle.from_py(scvs, [pod], max_cards=1)
+    res = (oracle.schedule(nodes, pods, MODE_DISKIO) if first is None
+           else oracle.schedule_memo(nodes, pods, first))
+    assert (res.pick[0], res.n_ties[0], res.top_score[0]) == (pick, ties, scores[pick])
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_b3_memo_c_matches_python(seed):
+    nodes = synth.make_nodes(40, 100 + seed)
+    pods = synth.make_pods(48, 200 + seed)
+    # integral S values are what the quirk keeps: give a quarter of the nodes cpu = disk = 0
+    nodes.cpu[::4] = 0.0
+    nodes.disk_io[::4] = 0.0
+    scvs, plist = oracle.to_py(nodes, pods)
+    for first in (0, 7):
+        res = oracle.schedule_memo(nodes, pods, first)
+        for p, pod in enumerate(plist):
+            r = po.schedule_one(pod, scvs, MODE_DISKIO, memo_first=first)
+            assert (res.pick[p], res.n_ties[p], res.top_score[p]) == (r.pick, r.n_ties,
+                                                                      r.top_score)
+    with pytest.raises(RuntimeError):
+        oracle.schedule_memo(nodes, pods, nodes.n_nodes)
+
+
 def test_go_float_to_uint64_edges():
     assert po.go_float64_to_uint64(5.9) == 5
     assert po.go_float64_to_uint64(-0.5) == 0
