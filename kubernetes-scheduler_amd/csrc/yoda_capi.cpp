@@ -80,6 +80,16 @@ hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t
 hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t C,
                              uint32_t n_pods, uint32_t node_offset, double* out_s,
                              uint32_t* out_i, int tk, hipStream_t s);
+hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigned char* sum2,
+                                const uint64_t* blk, uint32_t blk_stride, uint32_t n_nodes,
+                                uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
+                                const double* rcp, const float* rcp32, uint32_t n_pods,
+                                const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
+                                uint32_t bs_stride, const uint32_t* counts, uint64_t* keys,
+                                uint32_t ib, int tk, hipStream_t s);
+hipError_t launch_topk_merge_keys(const uint64_t* keys, uint32_t C, uint32_t n_pods, uint32_t ib,
+                                  uint32_t node_offset, double* out_s, uint32_t* out_i, int tk,
+                                  hipStream_t s);
 hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32_t* node,
                              const uint64_t* value, const uint64_t* card_number, uint32_t count,
                              unsigned char* sum, uint32_t sum_stride, unsigned char* sum2,
@@ -261,6 +271,9 @@ struct yoda_handle {
   std::vector<unsigned char> host_records;  // kept for alloc updates (greedy)
   std::vector<uint32_t> host_k2sum;         // idem (its static score words)
   std::vector<uint64_t> h_total_sum, h_free_sum, h_alloc, h_card_number;
+  // bound on any raw score of this snapshot whatever the allocated memory (Basic + the
+  // largest Allocate 300 + Actual): the packed top-k keys need score < 2^(64 - index bits)
+  uint64_t score_bound = ~0ull;
 
   // pods: one device blob of per-pod arrays (PodArray order), staged through pinned memory
   bool has_pods = false;
@@ -456,6 +469,16 @@ void plan_chunks(yoda_t* h, int mode, uint32_t n_pods, uint32_t n_nodes) {
   static const uint32_t r2 = std::max<uint32_t>(1, env_u32("YODA_CHUNK_ROUNDS2",
                                                            env_u32("YODA_CHUNK_ROUNDS", 8)));
   plan_chunks_for((uint32_t)capacity(h, 1, mode), r1, n_pods, n_nodes, &h->C1, &h->chunk1);
+  // YODA_K1_MAX_CHUNKS (A/B knob, default off): at most that many K1 chunks, so that small
+  // batches keep their partials (and k_reduce1's reads) few
+  static const uint32_t c1_max = env_u32("YODA_K1_MAX_CHUNKS", 0);
+  if (c1_max && h->C1 > c1_max) {
+    h->chunk1 = ((n_nodes + c1_max - 1) / c1_max + kChunkAlign - 1) / kChunkAlign * kChunkAlign;
+    h->C1 = std::max<uint32_t>(1, (n_nodes + h->chunk1 - 1) / h->chunk1);
+    if (h->C1 >= 8) {  // keep a multiple of 8 (XCD tiling); trailing chunks may be empty
+      h->C1 = (h->C1 + 7) / 8 * 8;
+    }
+  }
   plan_chunks_for((uint32_t)capacity(h, 2, mode), r2, n_pods, n_nodes, &h->C2, &h->chunk2);
 }
 
@@ -846,6 +869,58 @@ int finalize(yoda_t* h, int mode, const uint32_t* counts, const int64_t* best,
   return unpermute_outputs(h);
 }
 
+// Top-k candidate lists of the run's P sorted pods (greedy windows, yoda_shard_topk) into
+// h->tk_s / h->tk_i ([KT][P], scores and global node ids, (score desc, node asc)), after
+// phase 1 and the reciprocals.  The block-classified K2 with packed keys whenever the record
+// path and the score bound allow it (its own chunking: one round of workgroups, so that the
+// [C][P][KT] lists stay small); else the per-pair K2 (k2_score OUT_TOPK).
+// YODA_TOPK_PER_PAIR=1 forces the per-pair kernels (A/B, tests).
+int topk_lists(yoda_t* h, uint32_t P, uint32_t KT, const uint32_t* d_counts) {
+  const uint32_t N = h->n_nodes;
+  HIP_TRY(h, h->tk_s.ensure((size_t)KT * P * 8));
+  HIP_TRY(h, h->tk_i.ensure((size_t)KT * P * 4));
+  if (P == 0 || N == 0) return YODA_OK;
+  uint32_t ib = 1;
+  while ((1ull << ib) <= N) ++ib;  // node ids < 2^ib - 1: a real key is never 0
+  static const bool per_pair = std::getenv("YODA_TOPK_PER_PAIR") &&
+                               std::strcmp(std::getenv("YODA_TOPK_PER_PAIR"), "1") == 0;
+  const bool block = !per_pair && h->path == Path::N32 && h->has_k2sum && h->K <= 8 &&
+                     ib <= 40 && h->score_bound < (1ull << (64 - ib));
+  if (block) {
+    uint32_t Ct = 1, cht = 64;
+    // rounds of resident workgroups: 4 for window-sized batches (more, shorter per-(wave,
+    // chunk) lists balance better), 1 below 2048 pods (the capacity windows, where the merge's
+    // reads dominate); A/B in profiles/r02/greedy_topk/
+    static const uint32_t rt_env = env_u32("YODA_TOPK_ROUNDS", 0);
+    const uint32_t rt = rt_env ? rt_env : (P >= 2048 ? 4u : 1u);
+    plan_chunks_for((uint32_t)capacity(h, 2, YODA_MODE_SCV), rt, P, N, &Ct, &cht);
+    HIP_TRY(h, h->tk_s_part.ensure((size_t)Ct * P * KT * 8));
+    HIP_TRY(h, launch_k2_topk_block(h->K, h->nodes.as<unsigned char>(),
+                                    h->k2sum.as<unsigned char>(),
+                                    h->blk_valid ? h->blk.as<uint64_t>() : nullptr, blk_row(N), N,
+                                    cht, Ct, pod_params(h), h->rcp.as<double>(),
+                                    h->rcp32.as<float>(), P, h->bitmask.as<uint64_t>(), bm_row(N),
+                                    h->bs_ptr(), bs_row(N), d_counts,
+                                    h->tk_s_part.as<uint64_t>(), ib, (int)KT, h->stream));
+    HIP_TRY(h, launch_topk_merge_keys(h->tk_s_part.as<uint64_t>(), Ct, P, ib, h->node_offset,
+                                      h->tk_s.as<double>(), h->tk_i.as<uint32_t>(), (int)KT,
+                                      h->stream));
+    return YODA_OK;
+  }
+  const size_t CPk = (size_t)h->C2 * KT * P;
+  HIP_TRY(h, h->tk_s_part.ensure(CPk * 8));
+  HIP_TRY(h, h->tk_i_part.ensure(CPk * 4));
+  HIP_TRY(h, launch_k2_topk(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk2, h->C2,
+                            pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(), P,
+                            h->bitmask.as<uint64_t>(), bm_row(N), h->bs_ptr(), bs_row(N),
+                            partials(h), h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),
+                            (int)KT, h->stream));
+  HIP_TRY(h, launch_topk_merge(h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(), h->C2, P,
+                               h->node_offset, h->tk_s.as<double>(), h->tk_i.as<uint32_t>(),
+                               (int)KT, h->stream));
+  return YODA_OK;
+}
+
 bool is_pow2_le16(uint32_t k) { return k == 1 || k == 2 || k == 4 || k == 8 || k == 16; }
 
 }  // namespace
@@ -956,6 +1031,16 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     const long double score_bound =
         (long double)K * (800.0L + 100.0L * (long double)max_clock) + (long double)max_static;
     const bool f64_ok = max_field <= kFastFieldMax && score_bound < (long double)kFastScoreMax;
+    {
+      uint64_t max_actual = 0;  // Actual does not depend on the allocated memory
+      for (uint32_t i = 0; i < N; ++i)
+        if (nd->total_memory_sum[i] != 0)
+          max_actual = std::max(max_actual,
+                                nd->free_memory_sum[i] * 100u / nd->total_memory_sum[i] * 2u);
+      const long double b = (long double)K * (800.0L + 100.0L * (long double)max_clock) + 300.0L +
+                            (long double)max_actual;
+      h->score_bound = b < 9.0e18L ? (uint64_t)b + 1u : ~0ull;
+    }
     // bandwidth, clock, core and power <= 55738 on EVERY shard keeps 300 x + M < 2^24 for
     // any maxima another shard contributes (all shards run one path: yoda_amd/dist.py).
     const bool n32_ok = f64_ok && max_field <= kN32FieldMax && max_small <= kN32SmallFieldMax;
@@ -2026,25 +2111,12 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
         // sort the window like any batch (whole waves skip nodes); outputs stay in sorted
         // order and are read through pos[i] = sorted position of window pod i
         if ((rc = order_pods(h, YODA_MODE_SCV))) return rc;
-        const size_t CPk = (size_t)h->C2 * KT * wn;
-        HIP_TRY(h, h->tk_s_part.ensure(CPk * 8));
-        HIP_TRY(h, h->tk_i_part.ensure(CPk * 4));
-        HIP_TRY(h, h->tk_s.ensure((size_t)KT * wn * 8));
-        HIP_TRY(h, h->tk_i.ensure((size_t)KT * wn * 4));
         if (N > 0) {
           if ((rc = phase1(h, YODA_MODE_SCV, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>())))
             return rc;
           HIP_TRY(h, launch_prep2(h->maxima.as<uint64_t>(), wn, h->rcp.as<double>(),
                                   h->rcp32.as<float>(), h->stream));
-          HIP_TRY(h, launch_k2_topk(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk2,
-                                    h->C2, pod_params(h), h->rcp.as<double>(),
-                                    h->rcp32.as<float>(), wn, h->bitmask.as<uint64_t>(),
-                                    bm_row(N), h->bs_ptr(), bs_row(N),
-                                    partials(h), h->tk_s_part.as<double>(),
-                                    h->tk_i_part.as<uint32_t>(), (int)KT, h->stream));
-          HIP_TRY(h, launch_topk_merge(h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),
-                                       h->C2, wn, h->node_offset, h->tk_s.as<double>(),
-                                       h->tk_i.as<uint32_t>(), (int)KT, h->stream));
+          if ((rc = topk_lists(h, wn, KT, h->counts.as<uint32_t>()))) return rc;
           HIP_TRY(h, hipMemcpyAsync(counts.data(), h->counts.p, 2ull * wn * 4,
                                     hipMemcpyDeviceToHost, h->stream));
           HIP_TRY(h, hipMemcpyAsync(ts.data(), h->tk_s.p, (size_t)KT * wn * 8,
@@ -2275,21 +2347,9 @@ int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_count
     HIP_TRY(h, hipMemcpyAsync(cnt.data(), d_counts, 2ull * P * 4, hipMemcpyDeviceToHost,
                               h->stream));
     if (N > 0) {
-      const size_t CPk = (size_t)h->C2 * KT * P;
-      HIP_TRY(h, h->tk_s_part.ensure(CPk * 8));
-      HIP_TRY(h, h->tk_i_part.ensure(CPk * 4));
-      HIP_TRY(h, h->tk_s.ensure((size_t)KT * P * 8));
-      HIP_TRY(h, h->tk_i.ensure((size_t)KT * P * 4));
       HIP_TRY(h, launch_prep2(h->maxima.as<uint64_t>(), P, h->rcp.as<double>(),
                               h->rcp32.as<float>(), h->stream));
-      HIP_TRY(h, launch_k2_topk(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk2, h->C2,
-                                pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(), P,
-                                h->bitmask.as<uint64_t>(), bm_row(N), h->bs_ptr(), bs_row(N),
-                                partials(h), h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),
-                                (int)KT, h->stream));
-      HIP_TRY(h, launch_topk_merge(h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(), h->C2,
-                                   P, h->node_offset, h->tk_s.as<double>(),
-                                   h->tk_i.as<uint32_t>(), (int)KT, h->stream));
+      if ((rc = topk_lists(h, P, KT, d_counts))) return rc;
       HIP_TRY(h, hipMemcpyAsync(ts.data(), h->tk_s.p, (size_t)KT * P * 8, hipMemcpyDeviceToHost,
                                 h->stream));
       HIP_TRY(h, hipMemcpyAsync(ti.data(), h->tk_i.p, (size_t)KT * P * 4, hipMemcpyDeviceToHost,
@@ -3024,10 +3084,6 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
     if ((rc = prepare_run(h, YODA_MODE_SCV))) return rc;
     if ((rc = order_pods(h, YODA_MODE_SCV))) return rc;
     HIP_TRY(h, h->wit.ensure(12 * (size_t)wn * 4));
-    HIP_TRY(h, h->tk_s_part.ensure((size_t)h->C2 * KT * wn * 8));
-    HIP_TRY(h, h->tk_i_part.ensure((size_t)h->C2 * KT * wn * 4));
-    HIP_TRY(h, h->tk_s.ensure((size_t)KT * wn * 8));
-    HIP_TRY(h, h->tk_i.ensure((size_t)KT * wn * 4));
     if ((rc = phase1_witness(h, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(),
                              h->wit.as<uint32_t>(), 0)))
       return rc;
@@ -3041,14 +3097,12 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
     if (N > 0) {
       HIP_TRY(h, launch_prep2(h->maxima.as<uint64_t>(), wn, h->rcp.as<double>(),
                               h->rcp32.as<float>(), h->stream));
-      HIP_TRY(h, launch_k2_topk(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk2, h->C2,
-                                pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(), wn,
-                                h->bitmask.as<uint64_t>(), bm_row(N), nullptr, 0, partials(h),
-                                h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(), (int)KT,
-                                h->stream));
-      HIP_TRY(h, launch_topk_merge(h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(), h->C2,
-                                   wn, 0, h->tk_s.as<double>(), h->tk_i.as<uint32_t>(), (int)KT,
-                                   h->stream));
+      // (node ids local here: the session works on this handle's nodes)
+      const uint32_t off = h->node_offset;
+      h->node_offset = 0;
+      rc = topk_lists(h, wn, KT, h->counts.as<uint32_t>());
+      h->node_offset = off;
+      if (rc) return rc;
       HIP_TRY(h, hipMemcpyAsync(st + o_ts, h->tk_s.p, 8 * (size_t)KT * wn, hipMemcpyDeviceToHost,
                                 h->stream));
       HIP_TRY(h, hipMemcpyAsync(st + o_ti, h->tk_i.p, 4 * (size_t)KT * wn, hipMemcpyDeviceToHost,

@@ -879,6 +879,45 @@ __global__ __launch_bounds__(kWave) void k_reduce1_wave(const uint64_t* __restri
   }
 }
 
+// Split variant of k_reduce1 for many chunks (small pod batches: greedy windows): thread =
+// (pod, field) as in k_reduce1 (coalesced over pods), grid.z splits the chunks, and each
+// split folds its share into the outputs with one atomic (maxima and counts zeroed before;
+// every chunk's maxima partial is >= 1, the CollectMaxValues floor).
+template <bool NARROW>
+__global__ __launch_bounds__(kBlock) void k_reduce1_split(const uint64_t* __restrict__ pmax,
+                                                          const uint32_t* __restrict__ pcnt,
+                                                          uint32_t C, uint32_t n_pods,
+                                                          uint64_t* __restrict__ maxima,
+                                                          uint32_t* __restrict__ counts) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x, f = blockIdx.y;
+  if (p >= n_pods) return;
+  const uint32_t S = gridDim.z, per = (C + S - 1) / S;
+  const uint32_t c0 = blockIdx.z * per, c1 = min(C, c0 + per);
+  if (c0 >= c1) return;
+  if (f < 6) {
+    uint64_t mx = 0;
+    if constexpr (NARROW) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(pmax) + (size_t)f * C * n_pods + p;
+      uint32_t m32 = 0;
+#pragma unroll 8
+      for (uint32_t c = c0; c < c1; ++c) m32 = max(m32, src[(size_t)c * n_pods]);
+      mx = m32;
+    } else {
+      const uint64_t* src = pmax + (size_t)f * C * n_pods + p;
+#pragma unroll 8
+      for (uint32_t c = c0; c < c1; ++c) mx = umax64(mx, src[(size_t)c * n_pods]);
+    }
+    atomicMax(reinterpret_cast<unsigned long long*>(maxima + (size_t)f * n_pods + p),
+              (unsigned long long)mx);
+  } else {
+    const uint32_t* src = pcnt + (size_t)(f - 6) * C * n_pods + p;
+    uint32_t sum = 0;
+#pragma unroll 8
+    for (uint32_t c = c0; c < c1; ++c) sum += src[(size_t)c * n_pods];
+    atomicAdd(counts + (size_t)(f - 6) * n_pods + p, sum);
+  }
+}
+
 // RU(100 / M): the smallest double >= 100/M.  With every card field <= 2^44,
 // floor(x * RU(100/M)) == floor(100 x / M) exactly.
 __device__ __forceinline__ double ru_100_over(double M) {
@@ -1185,19 +1224,29 @@ __global__ __launch_bounds__(kBlock) void k2_score(
 //         reads  nq * shared + prefix[nq]  from LDS (the same integers as Scorer<N32>);
 //   EXACT anything else (mixed-model node, or non-uniform maxima): Scorer<N32>::raw.
 // Every term is an exact integer < 2^52 in each form, so all three give the same raw score.
+//
+// TKO > 0 (greedy candidate lists): instead of the argmax, each pod's TKO best (score, node)
+// pairs as packed keys  score << ib | (2^ib - 1 - node)  (a larger key is a higher score, or
+// the same score on a lower node: the (score desc, node asc) order of the per-pair top-k; the
+// host guarantees score < 2^(64 - ib) and n_nodes < 2^ib), sorted descending into
+// tk_keys[chunk][pod][TKO] (0 = no entry).  U nodes go into one wave-uniform list (their score
+// is the same on every active lane), the per-pod nodes into a per-lane list; the two are merged
+// at the end of the chunk.
 #ifndef YODA_K2_WAVES
 #define YODA_K2_WAVES 5
 #endif
-template <int K, bool STATS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ? YODA_K2_WAVES : 1))) void k2_block_n32(
+template <int K, bool STATS, int TKO = 0>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ? (TKO == 0 ? YODA_K2_WAVES : (TKO <= 8 ? 4 : 3)) : 1))) void k2_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum2,
     uint32_t n_nodes, uint32_t chunk_nodes, ScoreArgs args, uint32_t n_pods,
     const uint64_t* __restrict__ bm, uint32_t bm_stride, const BlockMask* __restrict__ bs,
     uint32_t bs_stride, const uint64_t* __restrict__ blk,
     uint32_t blk_stride, double* __restrict__ pbest,
     uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties, double* __restrict__ plow,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats, uint64_t* __restrict__ tk_keys, uint32_t ib) {
   constexpr uint32_t S2 = k2sum_stride(K), NS = n32_stride(K);
+  constexpr bool TOPK = TKO > 0;
+  constexpr int TL = TOPK ? TKO : 1;
   constexpr uint32_t PSW = K + 2;  // LDS words per node: prefix[0..K], shared
   constexpr uint32_t TAB = kWave * PSW;  // the prefix table: 64 nodes
   // node records (below): 16 words -- 8 of header, then 4 basic scores (uniform maxima) or
@@ -1286,6 +1335,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     return (uint64_t)__double_as_longlong(x + 4503599627370496.0) - 0x4330000000000000ull;
   };
   uint32_t npart = 0;  // STATS: per-pod-pass nodes of this (wave, chunk)
+  // TOPK: the lane's list (per-pod nodes) and the wave-uniform list (U nodes), descending
+  uint64_t pl[TL], ul[TL];
+#pragma unroll
+  for (int k = 0; k < TL; ++k) pl[k] = ul[k] = 0ull;
+  const uint32_t imax = TOPK ? (1u << ib) - 1u : 0u;
+  // insert key x into the lane's sorted list (x > pl[TL - 1])
+  auto pl_insert = [&](uint64_t x) {
+#pragma unroll
+    for (int k = 0; k < TL; ++k) {
+      const uint64_t o = pl[k];
+      const bool gt = x > o;
+      pl[k] = gt ? x : o;
+      x = gt ? o : x;
+    }
+  };
   // One block: the wave's mask of node nb + lane and its summary (kept for the per-pod pass,
   // read back with v_readlane), loaded together: one memory latency per block.
   auto block = [&](uint32_t nb) {
@@ -1316,6 +1380,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     }
     if (feas_b == 0) return;  // no pod of the wave can use any node of the block
     uint64_t fast_b = ballot(mask != 0ull && (h0.w & kSumUni4) != 0u), u_b = 0, rec_b = 0;
+    // TOPK: an upper bound on node n's key for every pod of the wave (uniform maxima, one-model
+    // node: every pod qualifies at most the nq_hi cards the smallest scv/memory does); ~0:
+    // no bound
+    uint64_t ub_key = ~0ull;
     {
       const uint32_t ck = h0.z, meta = h0.w, bw = h1.x, core = h1.y, pw = h1.z;
       const uint32_t cnt = (meta >> 8) & 0xffu;
@@ -1355,7 +1423,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         const uint32_t shared = (uint32_t)((float)bw * u_bw) + (uint32_t)((float)ck * u_bw) +
                                 2u * (uint32_t)((float)core * u_core) +
                                 (uint32_t)((float)pw * u_pow);
-        uint32_t acc = 0, sel = 0;  // prefix sums of (3 q_free + q_total) in free order
+        uint32_t acc = 0, sel = 0, sel_hi = 0;  // prefix sums of (3 q_free + q_total), free order
         lds[lane * PSW + 0] = 0u;
 #pragma unroll
         for (int t = 0; t < K; ++t) {
@@ -1366,13 +1434,37 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
 #endif
           lds[lane * PSW + t + 1] = acc;
           sel = (uint32_t)(t + 1) == nq_lo ? acc : sel;
+          if constexpr (TOPK) sel_hi = (uint32_t)(t + 1) == nq_hi ? acc : sel_hi;
+        }
+        if constexpr (TOPK) {
+          // basic = nq * shared + prefix[nq] grows with nq <= nq_hi (0 when the clock fails)
+          const uint64_t ub = stat_u + (ck >= c_min ? nq_hi * shared + sel_hi : 0u);
+          if (fast) ub_key = (ub << ib) | (uint64_t)(imax - n);
         }
         lds[lane * PSW + K + 1] = shared;
         const double stat = stat_d;
         const bool q_all = ck >= c_max, q_none = ck < c_min;
         const bool is_u = fast && mask == act_mask && nq_lo == nq_hi && (q_all || q_none);
         u_b = ballot(is_u);
-        if (is_u) {
+        if constexpr (TOPK) {
+          // the wave's U keys above the uniform list's last one enter it, best first
+          const uint32_t basic = q_all ? nq_lo * shared + sel : 0u;  // algorithm.go:271
+          const uint64_t key =
+              is_u ? ((stat_u + basic) << ib) | (uint64_t)(imax - n) : 0ull;
+          bool cand = key > ul[TL - 1];
+          while (ballot(cand) != 0ull) {
+            uint64_t x = wave_max_u64(cand ? key : 0ull);
+            cand = cand && key != x;
+#pragma unroll
+            for (int k = 0; k < TL; ++k) {
+              const uint64_t o = ul[k];
+              const bool gt = x > o;
+              ul[k] = gt ? x : o;
+              x = gt ? o : x;
+            }
+            cand = cand && key > ul[TL - 1];
+          }
+        } else if (is_u) {
           const uint32_t basic = q_all ? nq_lo * shared + sel : 0u;  // algorithm.go:271
           const double raw = (double)basic + stat;                   // algorithm.go:96
           if (raw > ubest) {
@@ -1438,6 +1530,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       }
     }
     uint64_t part_b = feas_b & ~u_b;
+    if constexpr (TOPK) {
+      // a node whose bound is below every active lane's k-th key cannot enter any list: no
+      // per-pod pass for it (lists fill within the first blocks of a chunk)
+      const uint64_t thr = wave_min_u64(act ? pl[TL - 1] : ~0ull);
+      const uint64_t keep_b = ballot(ub_key > thr);
+      part_b &= keep_b;
+      rec_b &= keep_b;
+    }
     if (STATS && !trace && lane == 0) {  // (wave, node) pairs: U, FAST, EXACT (skipped: rest)
       atomicAdd(stats + 2, (unsigned long long)__builtin_popcountll(u_b));
       atomicAdd(stats + 3, (unsigned long long)__builtin_popcountll(part_b & fast_b));
@@ -1451,6 +1551,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     uint64_t rb = rec_b;
     part_b &= ~rec_b;
     auto take_r = [&](bool f, uint64_t raw, uint32_t nn) {
+      if constexpr (TOPK) {
+        const uint64_t key = f ? (raw << ib) | (uint64_t)(imax - nn) : 0ull;
+        if (key > pl[TL - 1]) pl_insert(key);
+        return;
+      }
       const bool gt = f & (raw > rbest), eq = f & (raw == rbest);
       ridx = gt ? nn : (eq ? min(ridx, nn) : ridx);
       rties = gt ? 1u : rties + (eq ? 1u : 0u);
@@ -1577,6 +1682,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       tr[2] = npart;
       tr[3] = uni_max ? 1ull : 0ull;
     }
+  }
+  if constexpr (TOPK) {
+    // the U list (descending, the same for every active lane) into each active lane's list:
+    // once no lane takes entry k, none takes a later (smaller) one
+#pragma unroll
+    for (int k = 0; k < TL; ++k) {
+      const uint64_t x = act ? ul[k] : 0ull;
+      const bool take = x > pl[TL - 1];
+      if (ballot(take) == 0ull) break;
+      if (take) pl_insert(x);
+    }
+    if (!live) return;
+    uint64_t* o = tk_keys + ((size_t)chunk * n_pods + p) * TL;
+#pragma unroll
+    for (int k = 0; k < TL; k += 2)
+      *reinterpret_cast<ulonglong2*>(o + k) = make_ulonglong2(pl[k], pl[k + 1]);
+    return;
   }
   // merge the U nodes (the same for every pod lane) into each pod lane
   double wb = ubest;
@@ -1715,6 +1837,68 @@ __global__ __launch_bounds__(kWave) void k_topk_merge_wave(const double* __restr
   for (int k = 0; k < TK; ++k) {
     out_s[(size_t)k * n_pods + p] = ts[k];
     out_i[(size_t)k * n_pods + p] = ti[k] == 0xffffffffu ? ti[k] : ti[k] + node_offset;
+  }
+}
+
+// Merge of the block K2's packed top-k lists keys[C][P][TK] (descending, 0 = none): one wave
+// per pod (4 pods a workgroup); lane l folds chunks l, l + 64, ... (each list one contiguous
+// read), then the 64 lane lists are folded through shuffles.  Keys are unique (one node each),
+// so the result is the global top TK whatever the folding order.  Out: [TK][P] scores (-1: no
+// entry) and global node ids (0xFFFFFFFF).
+template <int TK>
+__global__ __launch_bounds__(kBlock) void k_topk_merge_keys(const uint64_t* __restrict__ keys,
+                                                            uint32_t C, uint32_t n_pods,
+                                                            uint32_t ib, uint32_t node_offset,
+                                                            double* __restrict__ out_s,
+                                                            uint32_t* __restrict__ out_i) {
+  const uint32_t p = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6), lane = lane_id();
+  if (p >= n_pods) return;  // wave-uniform
+  uint64_t pl[TK];
+#pragma unroll
+  for (int k = 0; k < TK; ++k) pl[k] = 0ull;
+  auto insert = [&](uint64_t x) {
+#pragma unroll
+    for (int k = 0; k < TK; ++k) {
+      const uint64_t o = pl[k];
+      const bool gt = x > o;
+      pl[k] = gt ? x : o;
+      x = gt ? o : x;
+    }
+  };
+  for (uint32_t c = lane; c < C; c += kWave) {
+    const ulonglong2* l = reinterpret_cast<const ulonglong2*>(keys + ((size_t)c * n_pods + p) * TK);
+    uint64_t v[TK];
+#pragma unroll
+    for (int k = 0; k < TK / 2; ++k) {
+      const ulonglong2 t = l[k];
+      v[2 * k] = t.x;
+      v[2 * k + 1] = t.y;
+    }
+#pragma unroll
+    for (int k = 0; k < TK; ++k) {
+      if (!(v[k] > pl[TK - 1])) break;  // the list is sorted: nothing further enters
+      insert(v[k]);
+    }
+  }
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    uint64_t v[TK];
+#pragma unroll
+    for (int k = 0; k < TK; ++k) v[k] = (uint64_t)__shfl_xor((unsigned long long)pl[k], o, kWave);
+#pragma unroll
+    for (int k = 0; k < TK; ++k) {
+      if (!(v[k] > pl[TK - 1])) break;
+      insert(v[k]);
+    }
+  }
+  if (lane != 0) return;
+  const uint64_t imask = (1ull << ib) - 1ull;
+#pragma unroll
+  for (int k = 0; k < TK; ++k) {
+    const uint64_t x = pl[k];
+    out_s[(size_t)k * n_pods + p] = x ? (double)(x >> ib) : -1.0;
+    out_i[(size_t)k * n_pods + p] =
+        x ? (uint32_t)(imask - (x & imask)) + node_offset : 0xffffffffu;
   }
 }
 
@@ -2624,7 +2808,22 @@ hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, fl
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool narrow,
                           uint64_t* maxima, uint32_t* counts, double* rcp, float* rcp32,
                           hipStream_t s) {
-  if (C > kWaveReduceChunks) {
+  if (C > kWaveReduceChunks && n_pods >= 2 * kBlock) {
+    // split the chunks so that ~64k threads read the partials, then atomics
+    const uint32_t pb = (n_pods + kBlock - 1) / kBlock;
+    const uint32_t S = std::max<uint32_t>(1, std::min<uint32_t>(C / 16, 256 / pb + 1));
+    hipError_t e = hipMemsetAsync(maxima, 0, 6 * (size_t)n_pods * 8, s);
+    if (e == hipSuccess) e = hipMemsetAsync(counts, 0, 2 * (size_t)n_pods * 4, s);
+    if (e != hipSuccess) return e;
+    const dim3 grid(pb, 8, S);
+    if (narrow)
+      hipLaunchKernelGGL(k_reduce1_split<true>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
+                         n_pods, maxima, counts);
+    else
+      hipLaunchKernelGGL(k_reduce1_split<false>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt,
+                         C, n_pods, maxima, counts);
+    if (rcp) return launch_prep2(maxima, n_pods, rcp, rcp32, s);
+  } else if (C > kWaveReduceChunks) {
     if (narrow)
       hipLaunchKernelGGL(k_reduce1_wave<true>, dim3(n_pods), dim3(kWave), 0, s, part.max_u,
                          part.cnt, C, n_pods, maxima, counts);
@@ -2670,12 +2869,14 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
           YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, true>), grid, dim3(kBlock), 0, s,
                                               nodes, sum2, n_nodes, chunk_nodes, a, n_pods, bm,
                                               bm_stride, bs, bs_stride, blk, blk_stride,
-                                              part.best_f, part.idx, part.ties, part.low_f, stats))
+                                              part.best_f, part.idx, part.ties, part.low_f, stats,
+                                              nullptr, 0u))
         else
           YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false>), grid, dim3(kBlock), 0, s,
                                               nodes, sum2, n_nodes, chunk_nodes, a, n_pods, bm,
                                               bm_stride, bs, bs_stride, blk, blk_stride,
-                                              part.best_f, part.idx, part.ties, part.low_f, stats));
+                                              part.best_f, part.idx, part.ties, part.low_f, stats,
+                                              nullptr, 0u));
         break;
       }
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score<KK, Path::N32, OUT>), grid, dim3(kBlock), 0,
@@ -2725,6 +2926,47 @@ hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t
       return hipErrorInvalidValue;
   }
 #undef YODA_TOPK
+  return hipGetLastError();
+}
+
+// The block K2's packed-key top-k (N32 path with node summaries; DESIGN.md §5 greedy):
+// keys [C][P][tk], merged by launch_topk_merge_keys.  counts: the pods' feasible-node counts
+// (a pod with none takes no part in the wave's bounds).
+hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigned char* sum2,
+                                const uint64_t* blk, uint32_t blk_stride, uint32_t n_nodes,
+                                uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
+                                const double* rcp, const float* rcp32, uint32_t n_pods,
+                                const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
+                                uint32_t bs_stride, const uint32_t* counts, uint64_t* keys,
+                                uint32_t ib, int tk, hipStream_t s) {
+  if ((tk != kTopK && tk != kTopKCap) || K > 8 || n_pods == 0) return hipErrorInvalidValue;
+  dim3 grid((n_pods + kBlock - 1) / kBlock, C);
+  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts};
+#define YODA_TOPKB(TKV)                                                                       \
+  YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false, TKV>), grid, dim3(kBlock), 0, s, \
+                                      nodes, sum2, n_nodes, chunk_nodes, a, n_pods, bm,         \
+                                      bm_stride, bs, bs_stride, blk, blk_stride, nullptr,       \
+                                      nullptr, nullptr, nullptr, nullptr, keys, ib))
+  if (tk == kTopK) {
+    YODA_TOPKB(kTopK);
+  } else {
+    YODA_TOPKB(kTopKCap);
+  }
+#undef YODA_TOPKB
+  return hipGetLastError();
+}
+
+hipError_t launch_topk_merge_keys(const uint64_t* keys, uint32_t C, uint32_t n_pods, uint32_t ib,
+                                  uint32_t node_offset, double* out_s, uint32_t* out_i, int tk,
+                                  hipStream_t s) {
+  if (tk != kTopK && tk != kTopKCap) return hipErrorInvalidValue;
+  const dim3 grid((n_pods + (kBlock / kWave) - 1) / (kBlock / kWave));
+  if (tk == kTopK)
+    hipLaunchKernelGGL(k_topk_merge_keys<kTopK>, grid, dim3(kBlock), 0, s, keys, C, n_pods, ib,
+                       node_offset, out_s, out_i);
+  else
+    hipLaunchKernelGGL(k_topk_merge_keys<kTopKCap>, grid, dim3(kBlock), 0, s, keys, C, n_pods, ib,
+                       node_offset, out_s, out_i);
   return hipGetLastError();
 }
 
