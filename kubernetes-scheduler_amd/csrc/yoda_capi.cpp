@@ -94,6 +94,8 @@ hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32
                              const uint64_t* value, const uint64_t* card_number, uint32_t count,
                              unsigned char* sum, uint32_t sum_stride, unsigned char* sum2,
                              uint32_t sum2_stride, hipStream_t s);
+hipError_t launch_gtable(int K, const uint32_t* sum2, uint32_t n_nodes, const uint64_t* g_max,
+                         uint32_t* tab, uint32_t* rcp_out, hipStream_t s);
 int topk_k();
 int topk_k_capacity();
 uint32_t greedy_one_blocks();
@@ -267,6 +269,8 @@ struct yoda_handle {
   DevBuf nodes_b;   // Mode B records
   DevBuf k1sum;     // K1 node summaries (N32 path, yoda_layout.h K1SumWord)
   DevBuf k2sum;     // K2 node summaries (N32 path, yoda_layout.h K2SumWord)
+  DevBuf gtab, gtab_aux;  // the G table (yoda_layout.h GTab) + [G maxima | its reciprocals]
+  GTab g = {};
   bool has_k1sum = false, has_k2sum = false;
   std::vector<unsigned char> host_records;  // kept for alloc updates (greedy)
   std::vector<uint32_t> host_k2sum;         // idem (its static score words)
@@ -515,6 +519,9 @@ int ensure_state(yoda_t* h, uint32_t P) {
   return YODA_OK;
 }
 
+// gtab_aux: [G maxima 6 x u64 | G reciprocals 8 x u32]
+constexpr size_t kGTabAuxBytes = 48 + 32;
+
 PodParams pod_params(yoda_t* h) {
   unsigned char* b = (h->ordered ? h->pod_sorted : h->pod_blob).as<unsigned char>();
   const size_t* off = h->ordered ? h->sorted_off : h->pod_off;
@@ -530,6 +537,7 @@ PodParams pod_params(yoda_t* h) {
   pp.need_clk = reinterpret_cast<uint32_t*>(b + off[kPodNeedClk]);
   pp.alpha = reinterpret_cast<double*>(b + off[kPodAlpha]);
   pp.beta = reinterpret_cast<double*>(b + off[kPodBeta]);
+  pp.g = h->has_k2sum ? h->g : GTab{};
   return pp;
 }
 
@@ -1052,6 +1060,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     std::vector<unsigned char> rec((size_t)std::max<uint32_t>(N, 1) * stride, 0);
     // K1 node summaries (N32 path): the facts the block-classified K1 reads per node
     const bool want_sum = path == Path::N32;
+    uint32_t g_rcp[8] = {};  // the G table's reciprocals, read back from the device
     const size_t sstride = k1sum_stride(K);
     std::vector<uint32_t> sum(want_sum ? (size_t)std::max<uint32_t>(N, 1) * sstride / 4 : 0, 0);
     const size_t s2stride = k2sum_stride(K);
@@ -1175,9 +1184,30 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
       HIP_TRY(h, h->k2sum.ensure(sum2.size() * 4));
       HIP_TRY(h, hipMemcpyAsync(h->k2sum.p, sum2.data(), sum2.size() * 4, hipMemcpyHostToDevice,
                                 h->stream));
+      // the G table: per field the max over every real card (floor 1, collection.go:31-38),
+      // the CollectMaxValues result of any pod feasible on the maximal cards' nodes
+      uint64_t gmax[6] = {1, 1, 1, 1, 1, 1};
+      for (uint32_t i = 0; i < N; ++i)
+        for (uint32_t j = 0; j < nd->card_count[i]; ++j) {
+          const size_t k = (size_t)i * KS + j;
+          gmax[kMaxBw] = std::max(gmax[kMaxBw], nd->card_bandwidth[k]);
+          gmax[kMaxClock] = std::max(gmax[kMaxClock], nd->card_clock[k]);
+          gmax[kMaxCore] = std::max(gmax[kMaxCore], nd->card_core[k]);
+          gmax[kMaxFree] = std::max(gmax[kMaxFree], nd->card_free_memory[k]);
+          gmax[kMaxPower] = std::max(gmax[kMaxPower], nd->card_power[k]);
+          gmax[kMaxTotal] = std::max(gmax[kMaxTotal], nd->card_total_memory[k]);
+        }
+      HIP_TRY(h, h->gtab.ensure(sum_words(std::max<uint32_t>(N, 1), gtab_stride(K)) * 4));
+      HIP_TRY(h, h->gtab_aux.ensure(kGTabAuxBytes));
+      HIP_TRY(h, hipMemcpyAsync(h->gtab_aux.p, gmax, sizeof(gmax), hipMemcpyHostToDevice,
+                                h->stream));
+      uint32_t* rcp_dev = reinterpret_cast<uint32_t*>(h->gtab_aux.as<unsigned char>() + 48);
+      HIP_TRY(h, launch_gtable(K, h->k2sum.as<uint32_t>(), N, h->gtab_aux.as<uint64_t>(),
+                               h->gtab.as<uint32_t>(), rcp_dev, h->stream));
+      HIP_TRY(h, hipMemcpyAsync(g_rcp, rcp_dev, sizeof(g_rcp), hipMemcpyDeviceToHost, h->stream));
     }
     const bool diskio = nd->cpu && nd->disk_io;
-    if (diskio && N > 0) {
+    if (diskio && N > 0) {  // (g_rcp: read back by the synchronize below)
       std::vector<NodeRecB> rb(N);
       for (uint32_t i = 0; i < N; ++i) {
         rb[i].v = nd->cpu[i] / 100.0;     // algorithm.go:73
@@ -1203,6 +1233,16 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     h->path = path;
     h->has_k1sum = want_sum && !(flags & YODA_UPLOAD_PER_NODE_K1);
     h->has_k2sum = want_sum && !(flags & YODA_UPLOAD_PER_NODE_K2);
+    h->g = GTab{};
+    static const bool no_gtab = env_u32("YODA_NO_GTAB", 0) != 0;  // A/B knob
+    if (h->has_k2sum && N > 0 && !no_gtab) {
+      h->g.tab = h->gtab.as<uint32_t>();
+      std::memcpy(&h->g.r_bw, &g_rcp[0], 4);
+      std::memcpy(&h->g.r_core, &g_rcp[1], 4);
+      std::memcpy(&h->g.r_pow, &g_rcp[2], 4);
+      std::memcpy(&h->g.r_free, &g_rcp[4], 8);
+      std::memcpy(&h->g.r_tot, &g_rcp[6], 8);
+    }
     h->generic = path == Path::U64;
     h->has_nodes = true;
     h->ran = false;

@@ -952,6 +952,80 @@ __global__ __launch_bounds__(kBlock) void k_prep2(const uint64_t* __restrict__ m
   }
 }
 
+// The "G table" (N32 block K2): for the snapshot-wide maxima G (per CalculateCardScore field,
+// the max over every real card, floor 1 -- the PreScore maxima of any pod whose feasible
+// nodes include the maximal cards, which is most pods of a large cluster) the per-node terms
+// the block K2 otherwise recomputes in every (wave, block): shared = the node's bandwidth,
+// clock/MaxBandwidth, 2 core and power quotients, and the prefix sums of 3 q_free + q_total
+// over its free-sorted cards, stored as the basic scores B[q] = q shared + prefix[q] of the
+// q = 1..K qualifying-card counts (tile layout, sum_index with gtab_stride).  A wave whose
+// reciprocals equal G's (compared bit for bit) reads them instead.
+// (struct GTab, gtab_stride: yoda_layout.h)
+
+// The terms of one one-model node under reciprocals r (the expressions of k2_block_n32).
+__device__ __forceinline__ uint32_t card_shared_terms(uint32_t bw, uint32_t ck, uint32_t core,
+                                                      uint32_t pw, float r_bw, float r_core,
+                                                      float r_pow) {
+  return (uint32_t)((float)bw * r_bw) + (uint32_t)((float)ck * r_bw) +
+         2u * (uint32_t)((float)core * r_core) + (uint32_t)((float)pw * r_pow);
+}
+__device__ __forceinline__ uint32_t card_mem_term(uint32_t f, uint32_t t, double r_free,
+                                                  double r_tot) {
+  return 3u * (uint32_t)((double)f * r_free) + (uint32_t)((double)t * r_tot);
+}
+
+// Build the G table (GTab above) of the N32 snapshot: g_max = G per maxima field (kMax*
+// order); rcp_out <- G's reciprocals (f32 bw, core, power; f64 free, total) for the host to
+// hand to K2.  One thread per node, tile layout.
+template <int K>
+__global__ __launch_bounds__(kBlock) void k_gtable(const uint32_t* __restrict__ sum2,
+                                                   uint32_t n_nodes, const uint64_t* __restrict__ g_max,
+                                                   uint32_t* __restrict__ tab,
+                                                   uint32_t* __restrict__ rcp_out) {
+  const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
+  const float r_bw = ru32_100_over((double)g_max[kMaxBw]);
+  const float r_core = ru32_100_over((double)g_max[kMaxCore]);
+  const float r_pow = ru32_100_over((double)g_max[kMaxPower]);
+  const double r_free = ru_100_over((double)g_max[kMaxFree]);
+  const double r_tot = ru_100_over((double)g_max[kMaxTotal]);
+  if (n == 0) {
+    rcp_out[0] = (uint32_t)__float_as_int(r_bw);
+    rcp_out[1] = (uint32_t)__float_as_int(r_core);
+    rcp_out[2] = (uint32_t)__float_as_int(r_pow);
+    const uint64_t f = (uint64_t)__double_as_longlong(r_free);
+    const uint64_t t = (uint64_t)__double_as_longlong(r_tot);
+    rcp_out[4] = (uint32_t)f;
+    rcp_out[5] = (uint32_t)(f >> 32);
+    rcp_out[6] = (uint32_t)t;
+    rcp_out[7] = (uint32_t)(t >> 32);
+  }
+  if (n >= ((n_nodes + 63u) & ~63u)) return;  // padded tail lanes: zero summaries
+  constexpr uint32_t S2 = k2sum_stride(K), GS = gtab_stride(K);
+  auto w = [&](uint32_t word) { return sum2[sum_index(n, word, S2)]; };
+  const uint32_t shared =
+      card_shared_terms(w(kS2Bw), w(kS2Clock), w(kS2Core), w(kS2Power), r_bw, r_core, r_pow);
+  uint32_t acc = 0;
+#pragma unroll
+  for (int t = 0; t < K; ++t) {
+    acc += card_mem_term(w(kS2Fs + t), w(kS2Fs + K + t), r_free, r_tot);
+    tab[sum_index(n, t, GS)] = (uint32_t)(t + 1) * shared + acc;  // B[t + 1]
+  }
+}
+
+hipError_t launch_gtable(int K, const uint32_t* sum2, uint32_t n_nodes, const uint64_t* g_max,
+                         uint32_t* tab, uint32_t* rcp_out, hipStream_t s) {
+  const dim3 grid(((n_nodes + 63u) & ~63u) / kBlock + 1);
+  switch (K) {
+    case 1: hipLaunchKernelGGL(k_gtable<1>, grid, dim3(kBlock), 0, s, sum2, n_nodes, g_max, tab, rcp_out); break;
+    case 2: hipLaunchKernelGGL(k_gtable<2>, grid, dim3(kBlock), 0, s, sum2, n_nodes, g_max, tab, rcp_out); break;
+    case 4: hipLaunchKernelGGL(k_gtable<4>, grid, dim3(kBlock), 0, s, sum2, n_nodes, g_max, tab, rcp_out); break;
+    case 8: hipLaunchKernelGGL(k_gtable<8>, grid, dim3(kBlock), 0, s, sum2, n_nodes, g_max, tab, rcp_out); break;
+    case 16: hipLaunchKernelGGL(k_gtable<16>, grid, dim3(kBlock), 0, s, sum2, n_nodes, g_max, tab, rcp_out); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------------
 // K2 on the fast paths: CalculateBasicScore + Allocate + Actual (algorithm.go:96,264-310),
 // exact.  A Scorer holds one pod's thresholds and reciprocals in VGPRs and
@@ -964,6 +1038,7 @@ struct ScoreArgs {
   const double* rcp;    // [5][P] f64: bw, core, power, free, total
   const float* rcp32;   // [3][P] f32: bw, core, power
   const uint32_t* cnt = nullptr;  // [P] feasible-node counts (phase 1), or none
+  GTab g = {};                    // the snapshot-wide maxima's per-node terms (tab: none)
 };
 
 template <Path P>
@@ -1247,7 +1322,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   constexpr uint32_t S2 = k2sum_stride(K), NS = n32_stride(K);
   constexpr bool TOPK = TKO > 0;
   constexpr int TL = TOPK ? TKO : 1;
-  constexpr uint32_t PSW = K + 2;  // LDS words per node: prefix[0..K], shared
+  constexpr uint32_t PSW = K + 2;  // LDS words per node: B[0..K] (B[q] = q shared + prefix[q]), pad
   constexpr uint32_t TAB = kWave * PSW;  // the prefix table: 64 nodes
   // node records (below): 16 words -- 8 of header, then 4 basic scores (uniform maxima) or
   // the (basic at nq_lo, at nq_lo + 1) pair of each reciprocal set
@@ -1322,6 +1397,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   }
   const bool uni_max = nsets <= 1u && rem == 0ull;  // "uniform maxima"
   const bool rec_ok = rem == 0ull;  // every active lane has a set: node records serve it
+  // the wave's reciprocals are the snapshot-wide maxima's: the G table serves its terms
+  const bool use_g = uni_max && args.g.tab != nullptr && u_bw == args.g.r_bw &&
+                     u_core == args.g.r_core && u_pow == args.g.r_pow &&
+                     u_free == args.g.r_free && u_tot == args.g.r_tot;
   const uint32_t m_max = wave_max_u32(act ? sc.m : 0u), m_min = wave_min_u32(act ? sc.m : ~0u);
   const uint32_t c_max = wave_max_u32(act ? sc.c : 0u), c_min = wave_min_u32(act ? sc.c : ~0u);
 
@@ -1372,11 +1451,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     const uint4 h0 = make_uint4(s[64 * kS2Static], s[64 * (kS2Static + 1)], s[64 * kS2Clock],
                                 s[64 * kS2Meta]);
     const uint4 h1 = make_uint4(s[64 * kS2Bw], s[64 * kS2Core], s[64 * kS2Power], 0u);
-    Group<uint32_t, K> fs, ts;
+    Group<uint32_t, K> fs, ts;  // ts: TotalMemory in free order, or (use_g) B[1..K]
 #pragma unroll
-    for (int t = 0; t < K; ++t) {
-      fs.v[t] = s[64 * (kS2Fs + t)];
-      ts.v[t] = s[64 * (kS2Fs + K + t)];
+    for (int t = 0; t < K; ++t) fs.v[t] = s[64 * (kS2Fs + t)];
+    if (use_g) {  // a G wave needs no TotalMemory: the table has the basic scores
+      const uint32_t* gs = args.g.tab + sum_index(nb, 0, gtab_stride(K)) + lane;
+#pragma unroll
+      for (int t = 0; t < K; ++t) ts.v[t] = gs[64 * t];
+    } else {
+#pragma unroll
+      for (int t = 0; t < K; ++t) ts.v[t] = s[64 * (kS2Fs + K + t)];
     }
     if (feas_b == 0) return;  // no pod of the wave can use any node of the block
     uint64_t fast_b = ballot(mask != 0ull && (h0.w & kSumUni4) != 0u), u_b = 0, rec_b = 0;
@@ -1419,36 +1503,48 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       const bool two = fast && range <= 1u;
       uint32_t* rec = lds + RECS + lane * REC;
       if (uni_max) {
-        // CalculateCardScore terms (algorithm.go:280-291) with the wave's reciprocals
-        const uint32_t shared = (uint32_t)((float)bw * u_bw) + (uint32_t)((float)ck * u_bw) +
-                                2u * (uint32_t)((float)core * u_core) +
-                                (uint32_t)((float)pw * u_pow);
-        uint32_t acc = 0, sel = 0, sel_hi = 0;  // prefix sums of (3 q_free + q_total), free order
+        // CalculateCardScore terms (algorithm.go:280-291) with the wave's reciprocals: from
+        // the G table when they are G's (the same integers), else computed
+        // B[q] = q shared + prefix[q]: the basic score with q qualifying cards (prefix: the
+        // sums of 3 q_free + q_total in free order); sel = B[nq_lo], sel_hi = B[nq_hi]
+        uint32_t sel = 0, sel_hi = 0;
         lds[lane * PSW + 0] = 0u;
+        if (use_g) {  // (wave-uniform branch)
 #pragma unroll
-        for (int t = 0; t < K; ++t) {
+          for (int t = 0; t < K; ++t) {
+            const uint32_t b = ts.v[t];
+            lds[lane * PSW + t + 1] = b;
+            sel = (uint32_t)(t + 1) == nq_lo ? b : sel;
+            if constexpr (TOPK) sel_hi = (uint32_t)(t + 1) == nq_hi ? b : sel_hi;
+          }
+        } else {
+          const uint32_t shared = card_shared_terms(bw, ck, core, pw, u_bw, u_core, u_pow);
+          uint32_t acc = 0;
+#pragma unroll
+          for (int t = 0; t < K; ++t) {
 #ifdef YODA_ABL_NOPREFIX
-          acc += fs.v[t] + ts.v[t];
+            acc += fs.v[t] + ts.v[t];
 #else
-          acc += 3u * (uint32_t)((double)fs.v[t] * u_free) + (uint32_t)((double)ts.v[t] * u_tot);
+            acc += card_mem_term(fs.v[t], ts.v[t], u_free, u_tot);
 #endif
-          lds[lane * PSW + t + 1] = acc;
-          sel = (uint32_t)(t + 1) == nq_lo ? acc : sel;
-          if constexpr (TOPK) sel_hi = (uint32_t)(t + 1) == nq_hi ? acc : sel_hi;
+            const uint32_t b = (uint32_t)(t + 1) * shared + acc;
+            lds[lane * PSW + t + 1] = b;
+            sel = (uint32_t)(t + 1) == nq_lo ? b : sel;
+            if constexpr (TOPK) sel_hi = (uint32_t)(t + 1) == nq_hi ? b : sel_hi;
+          }
         }
         if constexpr (TOPK) {
-          // basic = nq * shared + prefix[nq] grows with nq <= nq_hi (0 when the clock fails)
-          const uint64_t ub = stat_u + (ck >= c_min ? nq_hi * shared + sel_hi : 0u);
+          // basic = B[nq] grows with nq <= nq_hi (0 when the clock fails)
+          const uint64_t ub = stat_u + (ck >= c_min ? sel_hi : 0u);
           if (fast) ub_key = (ub << ib) | (uint64_t)(imax - n);
         }
-        lds[lane * PSW + K + 1] = shared;
         const double stat = stat_d;
         const bool q_all = ck >= c_max, q_none = ck < c_min;
         const bool is_u = fast && mask == act_mask && nq_lo == nq_hi && (q_all || q_none);
         u_b = ballot(is_u);
         if constexpr (TOPK) {
           // the wave's U keys above the uniform list's last one enter it, best first
-          const uint32_t basic = q_all ? nq_lo * shared + sel : 0u;  // algorithm.go:271
+          const uint32_t basic = q_all ? sel : 0u;  // algorithm.go:271
           const uint64_t key =
               is_u ? ((stat_u + basic) << ib) | (uint64_t)(imax - n) : 0ull;
           bool cand = key > ul[TL - 1];
@@ -1465,7 +1561,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
             cand = cand && key > ul[TL - 1];
           }
         } else if (is_u) {
-          const uint32_t basic = q_all ? nq_lo * shared + sel : 0u;  // algorithm.go:271
+          const uint32_t basic = q_all ? sel : 0u;  // algorithm.go:271
           const double raw = (double)basic + stat;                   // algorithm.go:96
           if (raw > ubest) {
             ubest = raw;
@@ -1488,8 +1584,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
           *reinterpret_cast<uint4*>(rec + 4) = make_uint4((uint32_t)stat_u,
                                                           (uint32_t)(stat_u >> 32), thr1, thr2);
           *reinterpret_cast<uint4*>(rec + 8) =
-              make_uint4(nq_lo * shared + sel, q1 * shared + row[q1], q2 * shared + row[q2],
-                         q3 * shared + row[q3]);
+              make_uint4(sel, row[q1], row[q2], row[q3]);
         }
       } else {
         // several reciprocal sets: no U nodes (scores differ across the wave), a record per
@@ -1623,7 +1718,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         uint32_t basic;
         if (uni_max) {
           const uint32_t* tab = lds + (uint32_t)j * PSW;
-          basic = ckj >= sc.c ? nq * tab[K + 1] + tab[nq] : 0u;
+          basic = ckj >= sc.c ? tab[nq] : 0u;  // B[nq]
         } else {
           // several reciprocal sets: Scorer<N32>'s one-model branch on the node lane's data,
           // with its own reciprocals (shared quotients f32, memory quotients f64)
@@ -2860,7 +2955,7 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
                               int64_t* rows, double* tk_s, uint32_t* tk_i,
                               unsigned long long* stats, const uint32_t* counts, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
-  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts};
+  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g};
   const MaskSrc ms{bm, bs, bm_stride, bs_stride};
   switch (path) {
     case Path::N32:
@@ -2941,7 +3036,7 @@ hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigne
                                 uint32_t ib, int tk, hipStream_t s) {
   if ((tk != kTopK && tk != kTopKCap) || K > 8 || n_pods == 0) return hipErrorInvalidValue;
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
-  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts};
+  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g};
 #define YODA_TOPKB(TKV)                                                                       \
   YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false, TKV>), grid, dim3(kBlock), 0, s, \
                                       nodes, sum2, n_nodes, chunk_nodes, a, n_pods, bm,         \

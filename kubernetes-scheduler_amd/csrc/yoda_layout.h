@@ -183,6 +183,15 @@ struct PtrList {
 };
 
 // Per-pod device parameters (struct of arrays, length P each).
+// The "G table" of an N32 snapshot (yoda_kernels.hip k_gtable / k2_block_n32): per-node terms
+// under the snapshot-wide maxima G, and G's reciprocals (f32 bw, core, power; f64 free, total).
+struct GTab {
+  const uint32_t* tab;
+  float r_bw, r_core, r_pow;
+  double r_free, r_tot;
+};
+__host__ __device__ constexpr uint32_t gtab_stride(int k) { return 4u * (uint32_t)k; }
+
 struct PodParams {
   // Filter / card predicate thresholds
   double* m_f;         // fast: scv/memory clamped to 2^53 (0 if absent)
@@ -197,6 +206,8 @@ struct PodParams {
   // Mode B
   double* alpha;
   double* beta;
+  // the snapshot's G table (N32 with node summaries; tab == nullptr: none)
+  GTab g = {};
 };
 
 // Per-pod state produced between kernels (length P each unless noted).
