@@ -16,6 +16,8 @@
 #include <new>
 #include <string>
 #include <vector>
+#include <thread>
+#include <array>
 
 #include "../../include/yoda.h"
 #include "yoda_layout.h"
@@ -334,6 +336,8 @@ struct yoda_handle {
   bool topk_ready = false;      // the bitmask / reciprocals of that batch are still valid
   uint32_t greedy_windows = 0, greedy_fallbacks = 0;
   double greedy_window_ms = 0, greedy_fallback_ms = 0, greedy_resolve_ms = 0;
+  double greedy_prep_ms = 0;  // (YODA_GREEDY_DEBUG) the host part of the windows: state push,
+                              // window gather + pod upload + order launches
   DevBuf p_max_u, p_cnt, p_best_f, p_best_i, p_idx, p_ties, p_low_f, p_low_i, p_err;
   uint32_t C1 = 1, chunk1 = 32;  // K1 node chunking
   uint32_t C2 = 1, chunk2 = 32;  // K2 / K3 node chunking
@@ -1333,87 +1337,118 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     uint32_t* nc = reinterpret_cast<uint32_t*>(st + off[kPodNeedClk]);
     const uint64_t kClamp = 1ull << 53;  // > every F64-path card field (<= 2^44)
     uint64_t key_or[3] = {0, 0, 0};       // OR of the sort key's clamped fields (c, n, m)
-    // distinct (clock, number, has-memory) groups with their pod counts: open addressing on
-    // key + 1 (0 = empty); consecutive pods of one group (the common case) skip the probe
-    std::vector<uint64_t> gkey(256, 0ull);
-    std::vector<uint32_t> gcnt(256, 0u);
-    // per group: its pods of the largest and of the smallest memory (the padding copies)
-    std::vector<uint64_t> gmax(256, 0ull), gmin(256, ~0ull);  // (m << 32 | pod) extremes
-    size_t g_n = 0;
-    auto g_slot = [&](uint64_t k1) {
-      size_t i = (size_t)(k1 * 0x9e3779b97f4a7c15ull >> 40) & (gkey.size() - 1);
-      while (gkey[i] != 0ull && gkey[i] != k1) i = (i + 1) & (gkey.size() - 1);
-      return i;
-    };
-    uint64_t g_last = ~0ull;
-    uint32_t g_run = 0;
-    uint64_t r_max = 0, r_min = ~0ull;  // the current run's extremes
-    auto g_add = [&](uint64_t g, uint32_t c, uint64_t mx, uint64_t mn) {
-      size_t i = g_slot(g + 1);
-      if (gkey[i] == 0ull) {
-        if (2 * (g_n + 1) > gkey.size()) {  // grow and rehash
-          const size_t n2 = gkey.size() * 2;
-          std::vector<uint64_t> ok(n2, 0ull), omx(n2, 0ull), omn(n2, ~0ull);
-          std::vector<uint32_t> oc(n2, 0u);
-          ok.swap(gkey);
-          oc.swap(gcnt);
-          omx.swap(gmax);
-          omn.swap(gmin);
-          for (size_t j = 0; j < ok.size(); ++j)
-            if (ok[j]) {
-              const size_t t = g_slot(ok[j]);
-              gkey[t] = ok[j];
-              gcnt[t] = oc[j];
-              gmax[t] = omx[j];
-              gmin[t] = omn[j];
-            }
-          i = g_slot(g + 1);
+    // distinct (clock, number, has-memory) groups with their pod counts and, per group, its
+    // pods of the largest and of the smallest memory (the padding copies) as (m << 32 | pod)
+    // extremes.  The pods are packed by up to 16 host threads over contiguous ranges, each
+    // with its own group table (merged after: counts add, extremes max/min).
+    struct GroupTable {
+      std::vector<uint64_t> key = std::vector<uint64_t>(64, 0ull);  // key + 1 (0 = empty)
+      std::vector<uint32_t> cnt = std::vector<uint32_t>(64, 0u);
+      std::vector<uint64_t> mx = std::vector<uint64_t>(64, 0ull), mn = std::vector<uint64_t>(64, ~0ull);
+      size_t n = 0;
+      size_t slot(uint64_t k1) const {
+        size_t i = (size_t)(k1 * 0x9e3779b97f4a7c15ull >> 40) & (key.size() - 1);
+        while (key[i] != 0ull && key[i] != k1) i = (i + 1) & (key.size() - 1);
+        return i;
+      }
+      void add(uint64_t g, uint32_t c, uint64_t vmax, uint64_t vmin) {
+        size_t i = slot(g + 1);
+        if (key[i] == 0ull) {
+          if (2 * (n + 1) > key.size()) {  // grow and rehash
+            GroupTable o;
+            const size_t n2 = key.size() * 2;
+            o.key.assign(n2, 0ull);
+            o.cnt.assign(n2, 0u);
+            o.mx.assign(n2, 0ull);
+            o.mn.assign(n2, ~0ull);
+            for (size_t j = 0; j < key.size(); ++j)
+              if (key[j]) {
+                const size_t t = o.slot(key[j]);
+                o.key[t] = key[j];
+                o.cnt[t] = cnt[j];
+                o.mx[t] = mx[j];
+                o.mn[t] = mn[j];
+              }
+            o.n = n;
+            *this = std::move(o);
+            i = slot(g + 1);
+          }
+          key[i] = g + 1;
+          ++n;
         }
-        gkey[i] = g + 1;
-        ++g_n;
+        cnt[i] += c;
+        mx[i] = std::max(mx[i], vmax);
+        mn[i] = std::min(mn[i], vmin);
       }
-      gcnt[i] += c;
-      gmax[i] = std::max(gmax[i], mx);
-      gmin[i] = std::min(gmin[i], mn);
     };
-    for (uint32_t p = 0; p < P; ++p) {
-      const uint64_t number = pd->has_number[p] ? pd->number[p] : 1;  // filter.go:12-15
-      const uint64_t m = pd->has_memory[p] ? pd->memory[p] : 0;       // filter.go:19,32
-      const uint64_t c = pd->has_clock[p] ? pd->clock[p] : 0;         // filter.go:36,49
-      const uint32_t need = number > 0xffffffffull ? 0xffffffffu : (uint32_t)number;
-      num[p] = number;
-      nm[p] = pd->has_memory[p] ? need : 0;
-      nc[p] = pd->has_clock[p] ? need : 0;
-      mu[p] = m;
-      cu[p] = c;
-      mf[p] = (double)std::min(m, kClamp);
-      cf[p] = (double)std::min(c, kClamp);
-      m32[p] = (uint32_t)std::min<uint64_t>(m, 0xffffffffull);  // > every N32 field
-      c32[p] = (uint32_t)std::min<uint64_t>(c, 0xffffffffull);
-      key_or[0] |= std::min<uint64_t>(c, 0xffffffull);  // the clamps of k_order_keys
-      key_or[1] |= std::min<uint64_t>(number, 0xffull);
-      key_or[2] |= std::min<uint64_t>(m, 0xffffffffull);
-      const uint64_t g = (std::min<uint64_t>(c, 0xffffffull) << 9) |
-                         (std::min<uint64_t>(number, 0xffull) << 1) | (nm[p] != 0u ? 1u : 0u);
-      if (g != g_last) {
-        if (g_run) g_add(g_last, g_run, r_max, r_min);
-        g_last = g;
-        g_run = 0;
-        r_max = 0;
-        r_min = ~0ull;
+    auto pack_range = [&](uint32_t p0, uint32_t p1, GroupTable& gt, uint64_t* kor) {
+      uint64_t g_last = ~0ull;
+      uint32_t g_run = 0;
+      uint64_t r_max = 0, r_min = ~0ull;  // the current run's extremes
+      for (uint32_t p = p0; p < p1; ++p) {
+        const uint64_t number = pd->has_number[p] ? pd->number[p] : 1;  // filter.go:12-15
+        const uint64_t m = pd->has_memory[p] ? pd->memory[p] : 0;       // filter.go:19,32
+        const uint64_t c = pd->has_clock[p] ? pd->clock[p] : 0;         // filter.go:36,49
+        const uint32_t need = number > 0xffffffffull ? 0xffffffffu : (uint32_t)number;
+        num[p] = number;
+        nm[p] = pd->has_memory[p] ? need : 0;
+        nc[p] = pd->has_clock[p] ? need : 0;
+        mu[p] = m;
+        cu[p] = c;
+        mf[p] = (double)std::min(m, kClamp);
+        cf[p] = (double)std::min(c, kClamp);
+        m32[p] = (uint32_t)std::min<uint64_t>(m, 0xffffffffull);  // > every N32 field
+        c32[p] = (uint32_t)std::min<uint64_t>(c, 0xffffffffull);
+        kor[0] |= std::min<uint64_t>(c, 0xffffffull);  // the clamps of k_order_keys
+        kor[1] |= std::min<uint64_t>(number, 0xffull);
+        kor[2] |= std::min<uint64_t>(m, 0xffffffffull);
+        const uint64_t g = (std::min<uint64_t>(c, 0xffffffull) << 9) |
+                           (std::min<uint64_t>(number, 0xffull) << 1) | (nm[p] != 0u ? 1u : 0u);
+        if (g != g_last) {  // consecutive pods of one group (the common case) skip the probe
+          if (g_run) gt.add(g_last, g_run, r_max, r_min);
+          g_last = g;
+          g_run = 0;
+          r_max = 0;
+          r_min = ~0ull;
+        }
+        ++g_run;
+        const uint64_t mp = (std::min<uint64_t>(m, 0xffffffffull) << 32) | p;
+        r_max = std::max(r_max, mp);
+        r_min = std::min(r_min, mp);
+        al[p] = be[p] = 0.0;
+        if (pd->rio && pd->rcpu) {  // algorithm.go:105-106
+          const double beta = 1.0 / (1.0 + (double)pd->rcpu[p] / pd->rio[p]);
+          be[p] = beta;
+          al[p] = 1 - beta;
+        }
       }
-      ++g_run;
-      const uint64_t mp = (std::min<uint64_t>(m, 0xffffffffull) << 32) | p;
-      r_max = std::max(r_max, mp);
-      r_min = std::min(r_min, mp);
-      al[p] = be[p] = 0.0;
-      if (pd->rio && pd->rcpu) {  // algorithm.go:105-106
-        const double beta = 1.0 / (1.0 + (double)pd->rcpu[p] / pd->rio[p]);
-        be[p] = beta;
-        al[p] = 1 - beta;
-      }
+      if (g_run) gt.add(g_last, g_run, r_max, r_min);
+    };
+    const uint32_t n_thr = std::min<uint32_t>(
+        {16u, std::max(1u, std::thread::hardware_concurrency()), std::max(1u, P / 16384u)});
+    std::vector<GroupTable> tables(n_thr);
+    std::vector<std::array<uint64_t, 3>> kors(n_thr, {0ull, 0ull, 0ull});
+    {
+      std::vector<std::thread> pool;
+      const uint32_t per = (P + n_thr - 1) / n_thr;
+      for (uint32_t t = 1; t < n_thr; ++t)
+        pool.emplace_back(pack_range, std::min(P, t * per), std::min(P, (t + 1) * per),
+                          std::ref(tables[t]), kors[t].data());
+      pack_range(0, std::min(P, per), tables[0], kors[0].data());
+      for (auto& th : pool) th.join();
     }
-    if (g_run) g_add(g_last, g_run, r_max, r_min);
+    GroupTable all = std::move(tables[0]);
+    for (uint32_t t = 1; t < n_thr; ++t)
+      for (size_t j = 0; j < tables[t].key.size(); ++j)
+        if (tables[t].key[j])
+          all.add(tables[t].key[j] - 1, tables[t].cnt[j], tables[t].mx[j], tables[t].mn[j]);
+    for (const auto& k : kors)
+      for (int f = 0; f < 3; ++f) key_or[f] |= k[f];
+    std::vector<uint64_t>& gkey = all.key;
+    std::vector<uint32_t>& gcnt = all.cnt;
+    std::vector<uint64_t>& gmax = all.mx;
+    std::vector<uint64_t>& gmin = all.mn;
+    const size_t g_n = all.n;
     HIP_TRY(h, hipMemcpyAsync(h->pod_blob.p, st, total, hipMemcpyHostToDevice, h->stream));
     {  // the counting-sort order's groups (yoda_order.hip)
       struct Grp {
@@ -2057,6 +2092,7 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
     h->greedy_fallbacks = 0;
     h->greedy_restarts = 0;
     h->greedy_window_ms = h->greedy_fallback_ms = h->greedy_resolve_ms = 0;
+    h->greedy_prep_ms = 0;
     using Clock = std::chrono::steady_clock;
     auto ms_since = [](Clock::time_point t0) {
       return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
@@ -2151,6 +2187,7 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
         // sort the window like any batch (whole waves skip nodes); outputs stay in sorted
         // order and are read through pos[i] = sorted position of window pod i
         if ((rc = order_pods(h, YODA_MODE_SCV))) return rc;
+        h->greedy_prep_ms += ms_since(tw);
         if (N > 0) {
           if ((rc = phase1(h, YODA_MODE_SCV, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>())))
             return rc;
@@ -2235,6 +2272,11 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
         h->greedy_resolve_ms += ms_since(tr) - fb_ms;
       }
     }
+    if (std::getenv("YODA_GREEDY_DEBUG"))
+      std::fprintf(stderr, "greedy: windows %u (%.1f ms, of which host prep %.1f ms), fallbacks %u "
+                   "(%.1f ms), resolve %.1f ms\n", h->greedy_windows, h->greedy_window_ms,
+                   h->greedy_prep_ms, h->greedy_fallbacks, h->greedy_fallback_ms,
+                   h->greedy_resolve_ms);
     // Leave the uploaded snapshot unchanged: restore static score and CardNumber.
     for (uint32_t n : all_touched) {
       g.stat[n] = stat0[n];

@@ -1328,7 +1328,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // the (basic at nq_lo, at nq_lo + 1) pair of each reciprocal set
   constexpr uint32_t kSets = 4, REC = 16;
   // LDS per wave: prefix table | 64 node records | the sets' reciprocals (8 words each)
-  constexpr uint32_t RECS = TAB, RCPS = TAB + kWave * REC, LDSW = RCPS + 8 * kSets;
+  // + each node lane's lowest U score (f64; in LDS, not a register: VGPR pressure)
+  constexpr uint32_t RECS = TAB, RCPS = TAB + kWave * REC, ULOW = RCPS + 8 * kSets,
+                     LDSW = ULOW + 2 * kWave;
   __shared__ __attribute__((aligned(16))) uint32_t lds_all[kBlock / kWave][LDSW];
   const uint32_t lane = lane_id();
   uint32_t* lds = lds_all[threadIdx.x >> 6];
@@ -1404,7 +1406,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   const uint32_t m_max = wave_max_u32(act ? sc.m : 0u), m_min = wave_min_u32(act ? sc.m : ~0u);
   const uint32_t c_max = wave_max_u32(act ? sc.c : 0u), c_min = wave_min_u32(act ? sc.c : ~0u);
 
-  double ubest = -1.0, ulow = 1.0e300;      // node lane (U nodes)
+  double ubest = -1.0;                      // node lane (U nodes)
+  double* ulow = reinterpret_cast<double*>(lds + ULOW) + lane;
+  *ulow = 1.0e300;
   uint32_t uidx = 0xffffffffu, uties = 0;
   // pod lane, every per-pod node: integer scores (static part + basic, exact below 2^53);
   // (0, 0 ties) is the empty state -- a first score of 0 counts as a tie of it
@@ -1570,7 +1574,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
           } else if (raw == ubest) {
             ++uties;
           }
-          ulow = fmin(ulow, raw);
+          *ulow = fmin(*ulow, raw);
         }
         const bool is_rec = fast && range <= 3u && !is_u;
         rec_b = ballot(is_rec);
@@ -1702,6 +1706,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       const uint64_t mj =
           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mask >> 32), j) << 32) |
           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mask, j);
+      if constexpr (TOPK) {
+        // per lane: a node whose bound cannot beat the lane's k-th key is skipped by it;
+        // the node is skipped when no feasible lane can take it
+        const uint64_t ubj =
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ub_key >> 32), j)
+             << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ub_key, j);
+        if (ballot(((mj >> lane) & 1ull) != 0ull && ubj > pl[TL - 1]) == 0ull) continue;
+      }
       double raw;
       if ((fast_b >> j) & 1ull) {
         // one-model node: nq qualifying cards (a prefix of the free order), then
@@ -1801,7 +1814,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   for (int o = kWave / 2; o > 0; o >>= 1) wb = fmax(wb, __shfl_xor(wb, o, kWave));
   const bool top = ubest == wb && uties > 0;
   uint32_t wi = top ? uidx : 0xffffffffu, wt = top ? uties : 0u;
-  double wl = ulow;
+  double wl = *ulow;
 #pragma unroll
   for (int o = kWave / 2; o > 0; o >>= 1) {
     wi = min(wi, (uint32_t)__shfl_xor((int)wi, o, kWave));
@@ -3281,10 +3294,67 @@ hipError_t launch_k1_witness(int K, Path path, const unsigned char* nodes, uint3
   return hipGetLastError();
 }
 
+// Split variant of k_reduce_wit for many chunks: threads = (pod, field) coalesced over pods,
+// grid.z splits the chunks.  PHASE 0 folds the maxima (atomicMax) and the feasible counts
+// (atomicAdd); PHASE 1, once the maxima are final, adds up the witnesses of the chunks that
+// reach a field's maximum and takes their lowest node (atomicMin).  Outputs zeroed before
+// (wnode to 0xFFFFFFFF).
+template <int PHASE>
+__global__ __launch_bounds__(kBlock) void k_reduce_wit_split(
+    const uint64_t* __restrict__ pmax, const uint32_t* __restrict__ pwit,
+    const uint32_t* __restrict__ pcnt, uint32_t C, uint32_t n_pods, uint32_t node_offset,
+    uint64_t* __restrict__ maxima, uint32_t* __restrict__ counts, uint32_t* __restrict__ wcount,
+    uint32_t* __restrict__ wnode) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x, f = blockIdx.y;
+  if (p >= n_pods) return;
+  const uint32_t S = gridDim.z, per = (C + S - 1) / S;
+  const uint32_t c0 = blockIdx.z * per, c1 = min(C, c0 + per);
+  if (c0 >= c1) return;
+  if (PHASE == 0) {
+    if (f < 6) {
+      uint64_t mx = 0;
+      for (uint32_t c = c0; c < c1; ++c) mx = umax64(mx, pmax[((size_t)f * C + c) * n_pods + p]);
+      atomicMax(reinterpret_cast<unsigned long long*>(maxima + (size_t)f * n_pods + p),
+                (unsigned long long)mx);
+    } else {
+      uint32_t sum = 0;
+      for (uint32_t c = c0; c < c1; ++c) sum += pcnt[((size_t)(f - 6) * C + c) * n_pods + p];
+      atomicAdd(counts + (size_t)(f - 6) * n_pods + p, sum);
+    }
+  } else {
+    if (f >= 6) return;
+    const uint64_t mx = maxima[(size_t)f * n_pods + p];
+    uint32_t wc = 0, wn = 0xffffffffu;
+    for (uint32_t c = c0; c < c1; ++c) {
+      const size_t o = ((size_t)f * C + c) * n_pods + p;
+      if (pmax[o] == mx) {
+        wc += pwit[o];
+        wn = min(wn, pwit[(size_t)6 * C * n_pods + o]);
+      }
+    }
+    if (wc) atomicAdd(wcount + (size_t)f * n_pods + p, wc);
+    if (wn != 0xffffffffu) atomicMin(wnode + (size_t)f * n_pods + p, wn + node_offset);
+  }
+}
+
 hipError_t launch_reduce_wit(const uint64_t* pmax, const uint32_t* pwit, const uint32_t* pcnt,
                              uint32_t C, uint32_t n_pods, uint32_t node_offset, uint64_t* maxima,
                              uint32_t* counts, uint32_t* wcount, uint32_t* wnode, hipStream_t s) {
   if (n_pods == 0) return hipSuccess;
+  if (C > kWaveReduceChunks && n_pods >= kBlock) {
+    const uint32_t pb = (n_pods + kBlock - 1) / kBlock;
+    const uint32_t S = std::max<uint32_t>(1, std::min<uint32_t>(C / 16, 256 / pb + 1));
+    hipError_t e = hipMemsetAsync(maxima, 0, 6 * (size_t)n_pods * 8, s);
+    if (e == hipSuccess) e = hipMemsetAsync(counts, 0, 2 * (size_t)n_pods * 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(wcount, 0, 6 * (size_t)n_pods * 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(wnode, 0xff, 6 * (size_t)n_pods * 4, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_reduce_wit_split<0>, dim3(pb, 8, S), dim3(kBlock), 0, s, pmax, pwit,
+                       pcnt, C, n_pods, node_offset, maxima, counts, wcount, wnode);
+    hipLaunchKernelGGL(k_reduce_wit_split<1>, dim3(pb, 6, S), dim3(kBlock), 0, s, pmax, pwit,
+                       pcnt, C, n_pods, node_offset, maxima, counts, wcount, wnode);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_reduce_wit, dim3(n_pods), dim3(kWave), 0, s, pmax, pwit, pcnt, C, n_pods,
                      node_offset, maxima, counts, wcount, wnode);
   return hipGetLastError();

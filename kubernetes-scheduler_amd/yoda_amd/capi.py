@@ -216,6 +216,17 @@ class Yoda:
         self._check(lib().yoda_download(self._h, C.byref(co)), "yoda_download")
         return res
 
+    def download_picks(self):
+        """(pick, status) of the last run -- what a scheduler binds; the other outputs stay on
+        the device (yoda_download with only those two pointers set)."""
+        P = self.n_pods
+        pick = np.full(P, -3, np.int32)
+        status = np.full(P, -1, np.int32)
+        co = CEvalOut(pick=pick.ctypes.data_as(C.POINTER(C.c_int32)),
+                      status=status.ctypes.data_as(C.POINTER(C.c_int32)))
+        self._check(lib().yoda_download(self._h, C.byref(co)), "yoda_download")
+        return pick, status
+
     def download_bitmask(self) -> np.ndarray:
         w = (self.n_nodes + 31) // 32
         words = np.zeros((self.n_pods, w), np.uint32)
