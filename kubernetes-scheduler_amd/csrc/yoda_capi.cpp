@@ -2166,7 +2166,9 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
       // Windowed top-k + certified sequential resolve (greedy).  Within a
       // window only the Allocate term of picked nodes changes, and it never increases
       // (unless alloc wraps around 2^64: then the rest of the window is evaluated exactly).
-      const uint32_t KT = (uint32_t)topk_k();
+      // YODA_GREEDY_TOPK=16 (A/B knob): the capacity mode's deeper lists for this mode too
+      static const uint32_t kt_env = env_u32("YODA_GREEDY_TOPK", 0);
+      const uint32_t KT = kt_env == (uint32_t)topk_k_capacity() ? kt_env : (uint32_t)topk_k();
       // Small windows: the GPU work is the same P x N in total, while fewer nodes are
       // touched per window, so fewer candidate lists lose certification.
       const uint32_t W = std::min<uint32_t>(P, greedy_window());
