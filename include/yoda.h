@@ -155,6 +155,8 @@ int yoda_synchronize(yoda_t* h);
                                         classified one (tests, A/B measurements)      */
 #define YODA_UPLOAD_PER_NODE_K2 16u  /* N32: per-pod K2 scoring instead of the block-
                                         classified one (tests, A/B measurements)      */
+#define YODA_UPLOAD_NO_GTAB 32u      /* N32: no G table (the block K2 computes every
+                                        node's card terms itself; tests, A/B)         */
 int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nodes, uint32_t node_offset,
                       uint32_t flags);
 /* 1 if the uploaded snapshot runs on the generic (u64) path, 0 on a fast path. */

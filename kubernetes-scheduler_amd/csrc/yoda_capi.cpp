@@ -1239,7 +1239,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     h->has_k2sum = want_sum && !(flags & YODA_UPLOAD_PER_NODE_K2);
     h->g = GTab{};
     static const bool no_gtab = env_u32("YODA_NO_GTAB", 0) != 0;  // A/B knob
-    if (h->has_k2sum && N > 0 && !no_gtab) {
+    if (h->has_k2sum && N > 0 && !no_gtab && !(flags & YODA_UPLOAD_NO_GTAB)) {
       h->g.tab = h->gtab.as<uint32_t>();
       std::memcpy(&h->g.r_bw, &g_rcp[0], 4);
       std::memcpy(&h->g.r_core, &g_rcp[1], 4);

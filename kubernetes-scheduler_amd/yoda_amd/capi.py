@@ -172,11 +172,13 @@ class Yoda:
 
     def upload_nodes(self, nodes: NodeSoA, node_offset: int = 0, force_generic: bool = False,
                      force_f64: bool = False, no_uniform: bool = False,
-                     per_node_k1: bool = False, per_node_k2: bool = False):
+                     per_node_k1: bool = False, per_node_k2: bool = False,
+                     no_gtab: bool = False):
         self._nodes = nodes.normalized()
         cn = self._nodes.c()
         flags = ((1 if force_generic else 0) | (2 if force_f64 else 0) | (4 if no_uniform else 0)
-                 | (8 if per_node_k1 else 0) | (16 if per_node_k2 else 0))
+                 | (8 if per_node_k1 else 0) | (16 if per_node_k2 else 0)
+                 | (32 if no_gtab else 0))
         self._check(lib().yoda_upload_nodes(self._h, C.byref(cn), node_offset, flags),
                     "yoda_upload_nodes")
         self.n_nodes = self._nodes.n_nodes
