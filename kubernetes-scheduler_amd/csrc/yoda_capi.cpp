@@ -185,13 +185,15 @@ struct DevBuf {
 struct PinnedBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  void* dp = nullptr;  // the same pages as seen by kernels (hipHostMalloc maps them)
   hipError_t ensure(size_t n) {
     if (n <= bytes) return hipSuccess;
     if (p) (void)hipHostFree(p);
-    p = nullptr;
+    p = dp = nullptr;
     bytes = 0;
     const size_t alloc = std::max<size_t>(n, 4096);
     hipError_t e = hipHostMalloc(&p, alloc, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&dp, p, 0);
     if (e == hipSuccess) bytes = alloc;
     return e;
   }
@@ -1958,7 +1960,6 @@ struct GreedyState {
     const size_t bytes = o_cn + (size_t)cnt * 8;
     if (h->upd_pending) HIP_TRY(h, hipEventSynchronize(h->upd_event));
     HIP_TRY(h, h->upd_stage.ensure(bytes));
-    HIP_TRY(h, h->upd_node.ensure(bytes));
     unsigned char* st = static_cast<unsigned char*>(h->upd_stage.p);
     uint32_t* nd = reinterpret_cast<uint32_t*>(st);
     uint64_t* val = reinterpret_cast<uint64_t*>(st + o_val);
@@ -1968,10 +1969,9 @@ struct GreedyState {
       val[i] = stat_bits(stat[list[i]]);
       cn[i] = card_number[list[i]];
     }
-    HIP_TRY(h, hipMemcpyAsync(h->upd_node.p, st, bytes, hipMemcpyHostToDevice, h->stream));
-    HIP_TRY(h, hipEventRecord(h->upd_event, h->stream));
-    h->upd_pending = true;
-    unsigned char* d = h->upd_node.as<unsigned char>();
+    // k_set_static reads the (mapped) staging pages itself: no copy; the event marks the
+    // end of that read, before which the pages are not rewritten
+    const unsigned char* d = static_cast<const unsigned char*>(h->upd_stage.dp);
     const uint32_t stride = h->path == Path::N32 ? n32_stride(h->K) : node_stride(h->K);
     HIP_TRY(h, launch_set_static(h->nodes.as<unsigned char>(), stride,
                                  reinterpret_cast<const uint32_t*>(d),
@@ -1981,6 +1981,8 @@ struct GreedyState {
                                  k1sum_stride(h->K),
                                  h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr,
                                  k2sum_stride(h->K), h->stream));
+    HIP_TRY(h, hipEventRecord(h->upd_event, h->stream));
+    h->upd_pending = true;
     if (marks)
       for (uint32_t n : list) (*marks)[n] = 0;
     list.clear();
@@ -2062,14 +2064,16 @@ int greedy_eval_fast(GreedyState& g, uint32_t s, int32_t* pick_out) {
   double* ps = h->g1_part.as<double>();
   uint32_t* pi = reinterpret_cast<uint32_t*>(ps + nb);
   uint32_t* done = h->g1_done.as<uint32_t>();
+  // the last block writes the pick straight into mapped pinned memory: no copy
+  HIP_TRY(h, h->pick_stage.ensure(16));
   HIP_TRY(h, launch_greedy_one(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes,
                                pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(),
                                h->n_pods, s, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
-                               h->bs_ptr(), bs_row(h->n_nodes), ps, pi, done, done + 1, h->stream));
-  HIP_TRY(h, h->pick_stage.ensure(16));
-  HIP_TRY(h, hipMemcpyAsync(h->pick_stage.p, done + 1, 4, hipMemcpyDeviceToHost, h->stream));
+                               h->bs_ptr(), bs_row(h->n_nodes), ps, pi, done,
+                               static_cast<uint32_t*>(h->pick_stage.dp) + 1, h->stream));
   HIP_TRY(h, hipStreamSynchronize(h->stream));
-  const uint32_t n = *static_cast<uint32_t*>(h->pick_stage.p);
+  // (word 1: the kernel's out[0]; its f64 score follows 8-byte aligned at word 2)
+  const uint32_t n = static_cast<const volatile uint32_t*>(h->pick_stage.p)[1];
   if (n == 0xffffffffu) return fail(h, YODA_ERR_INVALID_ARG, "greedy: no feasible node found");
   *pick_out = (int32_t)(n + h->node_offset);
   return YODA_OK;
