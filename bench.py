@@ -412,7 +412,8 @@ def main():
                          "per rank on one MI355X, profiles/r01/current/shard_timing.txt)")
     ap.add_argument("--exchange", choices=["torch", "libyoda"], default="torch",
                     help="--shard nodes: torch = RCCL all-reduces through torch.distributed "
-                         "(yoda_amd/dist.py ShardExchange, 5 collectives per step); libyoda = "
+                         "(yoda_amd/dist.py ShardExchange: int32 maxima MAX + counts SUM, the "
+                         "packed (score, node) key MAX + ties SUM; 4.4 MB at 100k pods); libyoda = "
                          "libyoda's own RCCL exchanges (yoda_comm_run, 2 collectives per step)")
     ap.add_argument("--no-balance", action="store_true",
                     help="--shard nodes: keep equal node blocks (default: re-cut them once "

@@ -167,6 +167,10 @@ int yoda_uses_generic_path(const yoda_t* h);
 #define YODA_PATH_F64 1
 #define YODA_PATH_U64 2
 int yoda_record_path(const yoda_t* h);
+/* An upper bound on every raw Score of the uploaded snapshot whatever its allocated memory
+ * (Basic at the largest clock + the largest Allocate 300 + Actual); ~0 when unbounded.  The
+ * sharded merge packs (score, node) into one 64-bit key when it fits (yoda_amd/dist.py). */
+uint64_t yoda_score_bound(const yoda_t* h);
 /* Replace alloc_memory (the Allocate-score input) without re-uploading the cards. */
 int yoda_update_alloc(yoda_t* h, const uint64_t* alloc_memory);
 

@@ -1266,6 +1266,8 @@ int yoda_uses_generic_path(const yoda_t* h) { return h ? (h->generic ? 1 : 0) : 
 
 int yoda_record_path(const yoda_t* h) { return h ? (int)h->path : -1; }
 
+uint64_t yoda_score_bound(const yoda_t* h) { return h && h->has_nodes ? h->score_bound : ~0ull; }
+
 int yoda_update_alloc(yoda_t* h, const uint64_t* alloc) {
   if (!h) return YODA_ERR_INVALID_ARG;
   if (!h->has_nodes) return fail(h, YODA_ERR_NO_NODES, "no node snapshot uploaded");

@@ -39,6 +39,7 @@ _SIGS = {
     "yoda_upload_nodes": ([_vp, C.POINTER(CNodeSoA), _u32, _u32], C.c_int),
     "yoda_uses_generic_path": ([_vp], C.c_int),
     "yoda_record_path": ([_vp], C.c_int),
+    "yoda_score_bound": ([_vp], C.c_uint64),
     "yoda_update_alloc": ([_vp, C.POINTER(C.c_uint64)], C.c_int),
     "yoda_eval": ([_vp, C.POINTER(CPodSoA), C.c_int, C.POINTER(CEvalOut)], C.c_int),
     "yoda_upload_pods": ([_vp, C.POINTER(CPodSoA)], C.c_int),
@@ -192,6 +193,11 @@ class Yoda:
     def path_code(self) -> int:
         """0 = N32, 1 = F64, 2 = U64 (include/yoda.h YODA_PATH_*)."""
         return int(lib().yoda_record_path(self._h))
+
+    @property
+    def score_bound(self) -> int:
+        """Upper bound on any raw Score of the snapshot (yoda_score_bound; 2^64-1: none)."""
+        return int(lib().yoda_score_bound(self._h))
 
     @property
     def path(self) -> str:
@@ -530,5 +536,5 @@ def header_symbols(path: str = HEADER_PATH):
     """Entry points declared in include/yoda.h."""
     import re
     text = open(path).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(yoda_[a-z0-9_]+)\s*\(", text,
+    return sorted(set(re.findall(r"^\s*(?:int|uint64_t|const char\*)\s+(yoda_[a-z0-9_]+)\s*\(", text,
                                  re.M)))

@@ -114,8 +114,19 @@ class Reducer:
         return [o.cpu().numpy() for o in out]
 
 
-def merge_phase1(reduce: Reducer, bufs: List[ShardBuffers]):
-    """Global maxima (MAX, unsigned) and feasible / zero-total counts (SUM)."""
+def merge_phase1(reduce: Reducer, bufs: List[ShardBuffers], narrow: bool = False):
+    """Global maxima (MAX, unsigned) and feasible / zero-total counts (SUM).
+
+    narrow: every maxima value is below 2^32 (the N32 record path: card fields <= 2^32 - 2),
+    so the MAX runs on int32 values offset by 2^31 -- half the bytes on the wire."""
+    if narrow:
+        for b in bufs:
+            b.max32 = (b.maxima - (1 << 31)).to(torch.int32)
+        reduce([b.max32 for b in bufs], "max")
+        for b in bufs:
+            b.maxima.copy_(b.max32.to(torch.int64) + (1 << 31))
+        reduce([b.counts for b in bufs], "sum")
+        return
     flip = any(b.unsigned_maxima for b in bufs)
     if flip:
         for b in bufs:
@@ -141,6 +152,34 @@ def merge_phase2(reduce: Reducer, bufs: List[ShardBuffers],
     reduce([b.mins for b in bufs], "min")         # lowest and idx together
     for b in bufs:
         b.idx.copy_(b.mins[b.lowest.numel():])    # back to the u32 bit pattern
+    reduce([b.ties for b in bufs], "sum")
+
+
+def merge_phase2_packed(reduce: Reducer, bufs: List[ShardBuffers], ib: int):
+    """The fast record paths' phase-2 merge (north_star: "per-shard winners merged by an RCCL
+    all-reduce(max) on the packed key"): each shard's (best raw score, lowest node reaching
+    it) becomes ONE int64 key  score << ib | (2^ib - 1 - node)  -- a larger key is a higher
+    score or, on equal scores, a lower node (the selectHost tie rule of DESIGN.md §2) -- and a
+    MAX all-reduce of the keys gives the global winner; the shards holding it then SUM their
+    tie counts.  Requires every node id < 2^ib - 1 and every score < 2^(63 - ib) (checked by
+    the caller from yoda_score_bound).  `lowest` (only the U64 path's normalize check reads
+    it) is set to the winning score."""
+    imax = (1 << ib) - 1
+    for b in bufs:
+        idx64 = b.idx.to(torch.int64) & 0xFFFFFFFF
+        key = (b.best << ib) | (imax - idx64)
+        b.best_g.copy_(torch.where(b.best >= 0, key, torch.zeros_like(key)))
+    reduce([b.best_g for b in bufs], "max")
+    for b in bufs:
+        key = b.best_g
+        won = key > 0
+        best_g = torch.where(won, key >> ib, torch.full_like(key, -1))
+        idx_g = torch.where(won, imax - (key & imax), torch.full_like(key, 0xFFFFFFFF))
+        keep = won & (b.best == best_g)
+        b.ties.copy_(torch.where(keep, b.ties, torch.zeros_like(b.ties)))
+        b.best_g.copy_(best_g)
+        b.idx.copy_(idx_g.to(torch.int32))  # the u32 bit pattern
+        b.lowest.copy_(best_g)
     reduce([b.ties for b in bufs], "sum")
 
 
@@ -179,7 +218,7 @@ def agree_on_path(reduce: Reducer, handles, shards, offsets, device):
 class ShardExchange:
     """Drives libyoda handles (one per shard) through the sharded entry points."""
 
-    def __init__(self, handles, reducer: Reducer, device, path_code=None):
+    def __init__(self, handles, reducer: Reducer, device, path_code=None, compact: bool = True):
         self.handles = list(handles)
         self.reduce = reducer
         self.device = device
@@ -187,19 +226,31 @@ class ShardExchange:
         if path_code is not None and path_code != 2:  # agreed fast path: maxima < 2^63
             for b in self.bufs:
                 b.unsigned_maxima = False
+        # compact exchange (agreed fast path): int32 maxima on N32, and the packed-key phase-2
+        # merge when the global node count and score bound fit one int64 key
+        self.narrow, self.ib = False, None
+        if compact and path_code in (0, 1):
+            lim = [torch.tensor([min(h.score_bound, (1 << 63) - 1), h.node_offset + h.n_nodes],
+                                dtype=torch.int64, device=device) for h in self.handles]
+            reducer(lim, "max")
+            bound, n_total = (int(x) for x in lim[0].tolist())
+            ib = max(1, (n_total + 1).bit_length())  # node ids < 2^ib - 1
+            if ib <= 40 and bound < (1 << (63 - ib)):
+                self.ib = ib
+            self.narrow = path_code == 0
         stream = torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0
         for h in self.handles:
             h.set_stream(stream)
 
     @classmethod
-    def local(cls, handles, device, shards=None, offsets=None):
+    def local(cls, handles, device, shards=None, offsets=None, compact: bool = True):
         """Several shards in one process (single-GPU testing).  Pass the node shards to
         enforce a common record path."""
         red = Reducer(local=True)
         path = None
         if shards is not None:
             path = agree_on_path(red, handles, shards, offsets, device)
-        return cls(handles, red, device, path)
+        return cls(handles, red, device, path, compact=compact)
 
     @classmethod
     def distributed(cls, handle, device, shard=None, offset=0, group=None):
@@ -219,12 +270,16 @@ class ShardExchange:
         p = ShardBuffers.ptr
         for h, b in zip(self.handles, self.bufs):
             h.shard_phase1(mode, p(b.maxima), p(b.counts))
-        merge_phase1(self.reduce, self.bufs)
+        scv = mode == 0
+        merge_phase1(self.reduce, self.bufs, narrow=self.narrow and scv)
         for h, b in zip(self.handles, self.bufs):
             h.shard_phase2(mode, p(b.maxima), p(b.counts), p(b.best), p(b.idx), p(b.ties),
                            p(b.lowest))
-        hb = dict(zip(map(id, self.bufs), self.handles))
-        merge_phase2(self.reduce, self.bufs, lambda b: self._prepare(hb[id(b)], b))
+        if self.ib is not None and scv:
+            merge_phase2_packed(self.reduce, self.bufs, self.ib)
+        else:
+            hb = dict(zip(map(id, self.bufs), self.handles))
+            merge_phase2(self.reduce, self.bufs, lambda b: self._prepare(hb[id(b)], b))
         for h, b in zip(self.handles, self.bufs):
             h.shard_finalize(mode, p(b.counts), p(b.best_g), p(b.idx), p(b.ties), p(b.lowest))
 

@@ -13,17 +13,27 @@ import torch.multiprocessing as mp
 
 import oracle
 from yoda_amd import synth
-from yoda_amd.dist import Reducer, ShardBuffers, merge_phase1, merge_phase2, shard_bounds
+from yoda_amd.dist import (Reducer, ShardBuffers, merge_phase1, merge_phase2,
+                           merge_phase2_packed, shard_bounds)
 from yoda_amd.soa import MODE_SCV
 
 P, N = 24, 90
 
 
-def _cluster():
+def _cluster(compact=False):
     nodes = synth.make_nodes(N, seed=314)
     pods = synth.make_pods(P, seed=271)
-    # unsigned values above 2^63 exercise the sign-flip MAX
-    nodes.card_bandwidth[5, :] = np.uint64((1 << 64) - 3)
+    if not compact:
+        # unsigned values above 2^63 exercise the sign-flip MAX
+        nodes.card_bandwidth[5, :] = np.uint64((1 << 64) - 3)
+    else:
+        # N32 range (the narrow int32 MAX): fields up to 2^32 - 2 and equal-score nodes
+        nodes.card_free_memory[3, 0] = np.uint64(0xFFFFFFFE)
+        nodes.card_total_memory[3, 0] = np.uint64(0xFFFFFFFE)
+        for f in ("card_free_memory", "card_total_memory", "card_clock", "card_bandwidth",
+                  "card_core", "card_power", "card_healthy", "card_number", "card_count",
+                  "free_memory_sum", "total_memory_sum", "alloc_memory"):
+            getattr(nodes, f)[60] = getattr(nodes, f)[10]  # a tie across the shards
     nodes.total_memory_sum[7] = 0
     return nodes.normalized(), pods
 
@@ -81,16 +91,20 @@ def _prepare_cpu(b: ShardBuffers):
     b.ties.copy_(torch.where(keep, b.ties, torch.zeros_like(b.ties)))
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, compact=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        nodes, pods = _cluster()
+        nodes, pods = _cluster(compact)
         bnd = shard_bounds(N, world)
         b = _shard_buffers(nodes, pods, int(bnd[rank]), int(bnd[rank + 1]))
         red = Reducer()
-        merge_phase1(red, [b])
-        merge_phase2(red, [b], _prepare_cpu)
+        if compact:  # int32 maxima + the packed (score, node) key merge
+            merge_phase1(red, [b], narrow=True)
+            merge_phase2_packed(red, [b], ib=(N + 1).bit_length())
+        else:
+            merge_phase1(red, [b])
+            merge_phase2(red, [b], _prepare_cpu)
         q.put((rank, b.maxima.numpy().view(np.uint64).copy(), b.counts.numpy().copy(),
                b.best_g.numpy().copy(), b.idx.numpy().view(np.uint32).copy(),
                b.ties.numpy().copy(), b.lowest.numpy().copy()))
@@ -106,20 +120,22 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_shard_merge(world):
+@pytest.mark.parametrize("world,compact", [(2, False), (3, False), (2, True), (3, True)])
+def test_gloo_shard_merge(world, compact):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, PORTS[world],
-                                                q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, PORTS[(world, compact)], q, compact))
+             for r in range(world)]
     for p in procs:
         p.start()
     outs = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    nodes, pods = _cluster()
+    nodes, pods = _cluster(compact)
     exp = _expected(nodes, pods)
+    if compact:  # the packed merge leaves lowest = the winning score (fast paths only)
+        exp["low"] = exp["best"]
     for rank, mx, cnt, best, idx, ties, low in outs:
         np.testing.assert_array_equal(mx.reshape(6, P), exp["maxima"], err_msg=f"rank {rank}")
         np.testing.assert_array_equal(cnt[:P], exp["nf"])
@@ -130,7 +146,7 @@ def test_gloo_shard_merge(world):
         np.testing.assert_array_equal(low, exp["low"])
 
 
-PORTS = {2: _free_port(), 3: _free_port()}
+PORTS = {(w, c): _free_port() for w in (2, 3) for c in (False, True)}
 
 
 @pytest.mark.parametrize("by_key", [True, False])

@@ -318,7 +318,9 @@ def test_sharded_merge_on_one_gpu(dev):
             y.upload_pods(pods)
             handles.append(y)
         ex = ShardExchange.local(handles, torch.device("cuda:0"), shards,
-                                 [int(b) for b in bounds[:-1]])
+                                 [int(b) for b in bounds[:-1]], compact=G == 2)
+        # G = 2: int32 maxima + the packed (score, node) key merge; G = 3: the 64-bit merge
+        assert (ex.ib is not None and ex.narrow) == (G == 2)
         for mode in (MODE_SCV, MODE_DISKIO):
             res = ex.run(mode)
             w = want if mode == MODE_SCV else oracle.schedule(nodes, pods, mode, threads=8)
