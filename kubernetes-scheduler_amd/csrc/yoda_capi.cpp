@@ -447,6 +447,8 @@ static uint32_t env_u32(const char* name, uint32_t dflt) {
   return (s && *s) ? (uint32_t)std::strtoul(s, nullptr, 10) : dflt;
 }
 
+constexpr uint32_t kMinChunkNodes = 1536;
+
 void plan_chunks_for(uint32_t cap, uint32_t rounds, uint32_t n_pods, uint32_t n_nodes,
                      uint32_t* C_out, uint32_t* chunk_out) {
   static const uint32_t min_chunk = env_u32("YODA_MIN_CHUNK_NODES", 0);
@@ -455,7 +457,16 @@ void plan_chunks_for(uint32_t cap, uint32_t rounds, uint32_t n_pods, uint32_t n_
   if (cap == 0) cap = 2048;
   uint32_t C = std::max<uint32_t>(1, (uint32_t)(((uint64_t)rounds * cap) / pod_blocks));
   C = std::min(C, max_chunks);
-  if (min_chunk) C = std::min(C, std::max<uint32_t>(1, (n_nodes + min_chunk - 1) / min_chunk));
+  if (min_chunk) {
+    C = std::min(C, std::max<uint32_t>(1, (n_nodes + min_chunk - 1) / min_chunk));
+  } else if (pod_blocks >= 64) {
+    // a large pod batch over few nodes (one rank of a node-sharded batch): chunks of at least
+    // kMinChunkNodes amortise the per-(wave, chunk) set-up of the block kernels, as long as
+    // the grid keeps two rounds of resident workgroups (A/B in profiles/r02/final/)
+    const uint32_t c_nodes = (n_nodes + kMinChunkNodes - 1) / kMinChunkNodes;
+    const uint32_t c_rounds = (uint32_t)((2ull * cap + pod_blocks - 1) / pod_blocks);
+    C = std::min(C, std::max<uint32_t>({1u, c_nodes, c_rounds}));
+  }
   // a multiple of 8 chunks lets the kernels give each XCD whole chunks (tile() in
   // yoda_kernels.hip); trailing chunks may then be empty (they write identity partials)
   const bool xcd = C >= 8;

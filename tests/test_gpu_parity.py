@@ -555,6 +555,22 @@ def test_uniform_node_factoring(dev):
             np.testing.assert_array_equal(rows[p][f], raw[f])
 
 
+def test_large_batch_few_nodes(dev):
+    """One rank of a node-sharded batch: many pods over few nodes, where the chunk plan keeps
+    chunks of >= 1536 nodes (plan_chunks_for); a pod sample against the oracle and the
+    invariants for every pod."""
+    nodes, pods = synth.make_config(3, pods=24000, nodes=7000)
+    got = dev.eval(pods, MODE_SCV) if dev.upload_nodes(nodes) is None else None
+    rng = np.random.default_rng(9)
+    sample = np.sort(rng.choice(pods.n_pods, size=600, replace=False))
+    want = oracle.schedule(nodes, pods.take(sample), MODE_SCV, threads=16)
+    sub = type(got)(**{f: getattr(got, f)[sample] for f in got.__dataclass_fields__})
+    assert_same(sub, want)
+    ok = got.status == 0
+    assert ((got.pick >= 0) == ok).all() and (got.pick[ok] < nodes.n_nodes).all()
+    assert (got.n_ties[ok] >= 1).all() and (got.n_ties[ok] <= got.n_feasible[ok]).all()
+
+
 @pytest.mark.parametrize("cfg", [2, 3])
 def test_g_table_on_off(dev, cfg):
     """The K2 G table (per-node basic scores under the snapshot-wide maxima, read by waves
