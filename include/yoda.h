@@ -230,10 +230,13 @@ int yoda_shard_overflow_count(yoda_t* h, uint32_t* n_pods);
  * GPU holds a node shard (yoda_upload_nodes with its node_offset) and the same pod batch.
  * Rank 0 calls yoda_comm_unique_id and hands the id to the other ranks out of band (a file,
  * the k8s API, MPI ...); every rank then calls yoda_comm_init (collective).  yoda_comm_run is
- * one whole sharded step on the handle's stream -- phase 1, ONE all-reduce(MAX) of the maxima
- * with the per-rank count slots, phase 2, ONE all-gather of the per-shard (best, index, ties,
- * lowest) records, the merge, finalize -- and leaves the picks for yoda_download, like
- * yoda_run.  librccl.so.1 is opened at the first call (not a link dependency).
+ * one whole sharded step on the handle's stream -- phase 1; ONE group of all-reduces: MAX of
+ * the maxima (+ two agreement words: score bits, node-id bits) and SUM of the counts; phase 2;
+ * on the fast record paths the packed-key merge: all-reduce(MAX) of each shard's
+ * (best << ib | 2^ib - 1 - node) key, then all-reduce(SUM) of the winners' tie counts (the
+ * U64 path in Mode A all-gathers (best, index, ties, lowest) records instead); finalize --
+ * and leaves the picks for yoda_download, like yoda_run.  All shards must run the same
+ * record path.  librccl.so.1 is opened at the first call (not a link dependency).
  * yoda_comm_run_local runs the same step for `world` shard handles of ONE process on one
  * device, with device copies as the transport (tests, single-process use). */
 #define YODA_COMM_ID_BYTES 128

@@ -131,6 +131,12 @@ hipError_t launch_pack_rec(const int64_t* best, const uint32_t* idx, const uint3
                            const int64_t* low, uint32_t n_pods, ShardRec* rec, hipStream_t s);
 hipError_t launch_merge_rec(const ShardRec* all, uint32_t n_pods, uint32_t world, int64_t* best,
                             uint32_t* idx, uint32_t* ties, int64_t* low, hipStream_t s);
+hipError_t launch_sum_multi_u32(const PtrList& src, uint32_t k, uint64_t n, uint32_t* dst,
+                                hipStream_t s);
+hipError_t launch_pack_key(const int64_t* best, const uint32_t* idx, uint32_t n_pods, uint32_t ib,
+                           uint64_t* key, hipStream_t s);
+hipError_t launch_unpack_key(const uint64_t* key, uint32_t n_pods, uint32_t ib, int64_t* best,
+                             uint32_t* idx, uint32_t* ties, int64_t* low, hipStream_t s);
 hipError_t launch_max_multi(const PtrList& src, uint32_t k, uint64_t n, uint64_t* dst,
                             hipStream_t s);
 size_t order_scratch_bytes(uint32_t n_pods);
@@ -216,6 +222,8 @@ struct RcclApi {
   ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t,
                              hipStream_t) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
   bool load() {
     if (tried) return ok;
@@ -236,9 +244,11 @@ struct RcclApi {
     all_reduce = reinterpret_cast<decltype(all_reduce)>(sym("ncclAllReduce"));
     all_gather = reinterpret_cast<decltype(all_gather)>(sym("ncclAllGather"));
     comm_destroy = reinterpret_cast<decltype(comm_destroy)>(sym("ncclCommDestroy"));
+    group_start = reinterpret_cast<decltype(group_start)>(sym("ncclGroupStart"));
+    group_end = reinterpret_cast<decltype(group_end)>(sym("ncclGroupEnd"));
     error_string = reinterpret_cast<decltype(error_string)>(sym("ncclGetErrorString"));
     ok = get_unique_id && comm_init_rank && all_reduce && all_gather && comm_destroy &&
-         error_string;
+         group_start && group_end && error_string;
     return ok;
   }
 };
@@ -3316,83 +3326,163 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
 
 // ---- multi-GPU step inside libyoda (RCCL, no torch) ---------------------------------------
 // One node shard per handle; a step is the sharded evaluation of yoda_shard_* with the
-// exchanges done here, two collectives per step:
-//   1. all-reduce(MAX, u64) over [maxima 6P | count slots world x P] -- the maxima of
-//      CollectMaxValues are a reduction over all nodes; the counts ride along as one slot per
-//      rank (an all-gather inside the MAX), summed after;
-//   2. all-gather of each shard's ShardRec [P] (best, lowest index reaching it, ties, lowest),
-//      folded per pod by k_merge_rec.
+// exchanges done here:
+//   1. one group of two all-reduces: MAX (u64) over [maxima 6P | score bits, node-id bits]
+//      -- CollectMaxValues is a reduction over all nodes; the two trailing words make every
+//      shard take the same phase-2 form -- and SUM (u32) over the feasible / zero-total
+//      counts [2P];
+//   2. fast record paths (and Mode B): the packed-key merge -- each shard's (best score,
+//      lowest node reaching it) as one u64 key, all-reduce(MAX) [P], then the winners' tie
+//      counts all-reduce(SUM) [P] (k_pack_key / k_unpack_key); the U64 path in Mode A, whose
+//      normalize check needs the lowest score too, all-gathers each shard's ShardRec [P]
+//      (best, lowest index reaching it, ties, lowest) and folds them (k_merge_rec).
 // `hs` are the shards this process drives: one handle with an RCCL communicator
 // (yoda_comm_run), or every shard of the batch on one device with device copies as the
 // transport (yoda_comm_run_local, for tests and single-process use).
+static uint32_t bit_length(uint64_t v) {
+  uint32_t b = 0;
+  while (b < 64 && (v >> b)) ++b;
+  return b;
+}
+
 static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local) {
   yoda_t* h0 = hs[0];
   const uint32_t P = h0->n_pods;
+  const size_t n1 = 6 * (size_t)P + 2;  // maxima | agreement words
   for (int i = 0; i < n; ++i) {
     yoda_t* h = hs[i];
     if (h->n_pods != P) return fail(h0, YODA_ERR_INVALID_ARG, "shards hold different batches");
     int rc = prepare_run(h, mode);
     if (rc) return rc;
     if ((rc = order_pods(h, mode))) return rc;
-    HIP_TRY(h, h->ex1.ensure((6 + (size_t)world) * std::max<uint32_t>(P, 1) * 8));
+    HIP_TRY(h, h->ex1.ensure(n1 * 8));
     HIP_TRY(h, h->rec.ensure((size_t)std::max<uint32_t>(P, 1) * sizeof(ShardRec)));
     HIP_TRY(h, h->rec_all.ensure((size_t)world * std::max<uint32_t>(P, 1) * sizeof(ShardRec)));
     if (P == 0) continue;
     uint64_t* ex = h->ex1.as<uint64_t>();
     if ((rc = phase1(h, mode, ex, h->counts.as<uint32_t>()))) return rc;
-    HIP_TRY(h, launch_slot_counts(h->counts.as<uint32_t>(), P, local ? (uint32_t)i
-                                                                      : (uint32_t)h->comm_rank,
-                                  (uint32_t)world, ex + 6 * (size_t)P, h->stream));
+    // agreement words: the score bits and node-id bits this shard needs (pinned staging,
+    // one slot per shard; the previous step's copies finished before its read-back below)
+    const uint64_t agree[2] = {h->generic && mode == YODA_MODE_SCV ? 64u
+                                                                    : bit_length(h->score_bound),
+                               bit_length((uint64_t)h->node_offset + h->n_nodes + 1)};
+    HIP_TRY(h0, h0->win_stage.ensure(16 * ((size_t)n + 1)));
+    unsigned char* slot = static_cast<unsigned char*>(h0->win_stage.p) + 16 * ((size_t)i + 1);
+    std::memcpy(slot, agree, 16);
+    HIP_TRY(h, hipMemcpyAsync(ex + 6 * (size_t)P, slot, 16, hipMemcpyHostToDevice, h->stream));
   }
   if (P == 0) {
     for (int i = 0; i < n; ++i) hs[i]->ran = true;
     return YODA_OK;
   }
-  const size_t n1 = (6 + (size_t)world) * P;
-  if (local) {  // exchange 1: elementwise MAX over the shards, back to each
-    PtrList l{};
-    for (int i = 0; i < n; ++i) l.p[i] = hs[i]->ex1.p;
+  if (local) {  // exchange 1: elementwise MAX / SUM over the shards, back to each
+    PtrList l{}, c{};
+    for (int i = 0; i < n; ++i) {
+      l.p[i] = hs[i]->ex1.p;
+      c.p[i] = hs[i]->counts.p;
+    }
+    HIP_TRY(h0, h0->rec.ensure(std::max<size_t>(2 * (size_t)P * 4, (size_t)P * sizeof(ShardRec))));
     HIP_TRY(h0, launch_max_multi(l, (uint32_t)n, n1, h0->ex1.as<uint64_t>(), h0->stream));
-    for (int i = 1; i < n; ++i)
-      HIP_TRY(h0, hipMemcpyAsync(hs[i]->ex1.p, h0->ex1.p, n1 * 8, hipMemcpyDeviceToDevice,
-                                 h0->stream));
+    HIP_TRY(h0, launch_sum_multi_u32(c, (uint32_t)n, 2 * (uint64_t)P, h0->rec.as<uint32_t>(),
+                                     h0->stream));
+    for (int i = 0; i < n; ++i) {
+      if (i > 0)
+        HIP_TRY(h0, hipMemcpyAsync(hs[i]->ex1.p, h0->ex1.p, n1 * 8, hipMemcpyDeviceToDevice,
+                                   h0->stream));
+      HIP_TRY(h0, hipMemcpyAsync(hs[i]->counts.p, h0->rec.p, 2 * (size_t)P * 4,
+                                 hipMemcpyDeviceToDevice, h0->stream));
+    }
   } else {
-    const ncclResult_t r = rccl().all_reduce(h0->ex1.p, h0->ex1.p, n1, ncclUint64, ncclMax,
-                                             h0->comm, h0->stream);
+    rccl().group_start();
+    ncclResult_t r = rccl().all_reduce(h0->ex1.p, h0->ex1.p, n1, ncclUint64, ncclMax, h0->comm,
+                                       h0->stream);
+    const ncclResult_t r2 = rccl().all_reduce(h0->counts.p, h0->counts.p, 2 * (size_t)P,
+                                              ncclUint32, ncclSum, h0->comm, h0->stream);
+    const ncclResult_t r3 = rccl().group_end();
+    if (r == ncclSuccess) r = r2;
+    if (r == ncclSuccess) r = r3;
     if (r != ncclSuccess)
       return fail(h0, YODA_ERR_HIP, std::string("ncclAllReduce: ") + rccl().error_string(r));
   }
+  // the agreed phase-2 form (every shard reads the same reduced words; one host wait per step)
+  uint64_t agreed[2] = {64, 64};
+  HIP_TRY(h0, hipMemcpyAsync(h0->win_stage.p, h0->ex1.as<uint64_t>() + 6 * (size_t)P, 16,
+                             hipMemcpyDeviceToHost, h0->stream));
+  HIP_TRY(h0, hipStreamSynchronize(h0->stream));
+  std::memcpy(agreed, h0->win_stage.p, 16);
+  const uint32_t ib = (uint32_t)std::max<uint64_t>(1, agreed[1]);
+  const bool packed = agreed[0] + ib <= 63 && ib <= 40;
   for (int i = 0; i < n; ++i) {
     yoda_t* h = hs[i];
     uint64_t* ex = h->ex1.as<uint64_t>();
-    HIP_TRY(h, launch_unslot_counts(ex + 6 * (size_t)P, P, (uint32_t)world,
-                                    h->counts.as<uint32_t>(), h->stream));
     HIP_TRY(h, hipMemcpyAsync(h->maxima.p, ex, 6 * (size_t)P * 8, hipMemcpyDeviceToDevice,
                               h->stream));
     int rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), h->best.as<int64_t>(),
                     h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>());
     if (rc) return rc;
-    HIP_TRY(h, launch_pack_rec(h->best.as<int64_t>(), h->idx.as<uint32_t>(),
-                               h->ties.as<uint32_t>(), h->lowest.as<int64_t>(), P,
-                               h->rec.as<ShardRec>(), h->stream));
+    if (packed)
+      HIP_TRY(h, launch_pack_key(h->best.as<int64_t>(), h->idx.as<uint32_t>(), P, ib,
+                                 h->rec.as<uint64_t>(), h->stream));
+    else
+      HIP_TRY(h, launch_pack_rec(h->best.as<int64_t>(), h->idx.as<uint32_t>(),
+                                 h->ties.as<uint32_t>(), h->lowest.as<int64_t>(), P,
+                                 h->rec.as<ShardRec>(), h->stream));
   }
-  const size_t rb = (size_t)P * sizeof(ShardRec);
-  if (local) {  // exchange 2: every shard's records to every shard
-    for (int r = 0; r < n; ++r)
+  if (packed) {  // exchange 2: MAX of the keys, then SUM of the winners' ties
+    if (local) {
+      PtrList l{};
+      for (int i = 0; i < n; ++i) l.p[i] = hs[i]->rec.p;
+      HIP_TRY(h0, launch_max_multi(l, (uint32_t)n, P, h0->rec_all.as<uint64_t>(), h0->stream));
       for (int i = 0; i < n; ++i)
-        HIP_TRY(h0, hipMemcpyAsync(hs[i]->rec_all.as<unsigned char>() + r * rb, hs[r]->rec.p, rb,
+        HIP_TRY(h0, hipMemcpyAsync(hs[i]->rec.p, h0->rec_all.p, (size_t)P * 8,
                                    hipMemcpyDeviceToDevice, h0->stream));
+    } else {
+      const ncclResult_t r = rccl().all_reduce(h0->rec.p, h0->rec.p, P, ncclUint64, ncclMax,
+                                               h0->comm, h0->stream);
+      if (r != ncclSuccess)
+        return fail(h0, YODA_ERR_HIP, std::string("ncclAllReduce: ") + rccl().error_string(r));
+    }
+    for (int i = 0; i < n; ++i) {
+      yoda_t* h = hs[i];
+      HIP_TRY(h, launch_unpack_key(h->rec.as<uint64_t>(), P, ib, h->best.as<int64_t>(),
+                                   h->idx.as<uint32_t>(), h->ties.as<uint32_t>(),
+                                   h->lowest.as<int64_t>(), h->stream));
+    }
+    if (local) {
+      PtrList t{};
+      for (int i = 0; i < n; ++i) t.p[i] = hs[i]->ties.p;
+      HIP_TRY(h0, launch_sum_multi_u32(t, (uint32_t)n, P, h0->rec_all.as<uint32_t>(), h0->stream));
+      for (int i = 0; i < n; ++i)
+        HIP_TRY(h0, hipMemcpyAsync(hs[i]->ties.p, h0->rec_all.p, (size_t)P * 4,
+                                   hipMemcpyDeviceToDevice, h0->stream));
+    } else {
+      const ncclResult_t r = rccl().all_reduce(h0->ties.p, h0->ties.p, P, ncclUint32, ncclSum,
+                                               h0->comm, h0->stream);
+      if (r != ncclSuccess)
+        return fail(h0, YODA_ERR_HIP, std::string("ncclAllReduce: ") + rccl().error_string(r));
+    }
   } else {
-    const ncclResult_t r = rccl().all_gather(h0->rec.p, h0->rec_all.p, rb / 8, ncclUint64,
-                                             h0->comm, h0->stream);
-    if (r != ncclSuccess)
-      return fail(h0, YODA_ERR_HIP, std::string("ncclAllGather: ") + rccl().error_string(r));
+    const size_t rb = (size_t)P * sizeof(ShardRec);
+    if (local) {  // exchange 2: every shard's records to every shard
+      for (int r = 0; r < n; ++r)
+        for (int i = 0; i < n; ++i)
+          HIP_TRY(h0, hipMemcpyAsync(hs[i]->rec_all.as<unsigned char>() + r * rb, hs[r]->rec.p,
+                                     rb, hipMemcpyDeviceToDevice, h0->stream));
+    } else {
+      const ncclResult_t r = rccl().all_gather(h0->rec.p, h0->rec_all.p, rb / 8, ncclUint64,
+                                               h0->comm, h0->stream);
+      if (r != ncclSuccess)
+        return fail(h0, YODA_ERR_HIP, std::string("ncclAllGather: ") + rccl().error_string(r));
+    }
+    for (int i = 0; i < n; ++i) {
+      yoda_t* h = hs[i];
+      HIP_TRY(h, launch_merge_rec(h->rec_all.as<ShardRec>(), P, (uint32_t)world,
+                                  h->best.as<int64_t>(), h->idx.as<uint32_t>(),
+                                  h->ties.as<uint32_t>(), h->lowest.as<int64_t>(), h->stream));
+    }
   }
   for (int i = 0; i < n; ++i) {
     yoda_t* h = hs[i];
-    HIP_TRY(h, launch_merge_rec(h->rec_all.as<ShardRec>(), P, (uint32_t)world,
-                                h->best.as<int64_t>(), h->idx.as<uint32_t>(),
-                                h->ties.as<uint32_t>(), h->lowest.as<int64_t>(), h->stream));
     int rc = finalize(h, mode, h->counts.as<uint32_t>(), h->best.as<int64_t>(),
                       h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(),
                       true);

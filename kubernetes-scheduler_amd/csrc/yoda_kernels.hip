@@ -3561,6 +3561,70 @@ hipError_t launch_merge_rec(const ShardRec* all, uint32_t n_pods, uint32_t world
   return hipGetLastError();
 }
 
+// In-process exchange: elementwise SUM of n u32 over the handles' buffers into dst.
+__global__ __launch_bounds__(kBlock) void k_sum_multi_u32(PtrList src, uint32_t k, uint64_t n,
+                                                          uint32_t* __restrict__ dst) {
+  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= n) return;
+  uint32_t a = 0;
+  for (uint32_t j = 0; j < k; ++j) a += static_cast<const uint32_t*>(src.p[j])[t];
+  dst[t] = a;
+}
+
+// Packed-key merge of the sharded phase 2 (fast record paths): each shard's
+// (best score, lowest node reaching it) as one u64  best << ib | (2^ib - 1 - node)  (0: none),
+// MAX-reduced across the shards; then every shard reads the winner back and keeps its tie
+// count only if it holds the winning score (SUM-reduced after).  lowest := the winning score
+// (only the U64 path's normalize check reads it, and that path keeps the record merge).
+__global__ __launch_bounds__(kBlock) void k_pack_key(const int64_t* __restrict__ best,
+                                                     const uint32_t* __restrict__ idx,
+                                                     uint32_t n_pods, uint32_t ib,
+                                                     uint64_t* __restrict__ key) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= n_pods) return;
+  const uint64_t imax = (1ull << ib) - 1ull;
+  key[p] = best[p] < 0 ? 0ull : ((uint64_t)best[p] << ib) | (imax - (uint64_t)idx[p]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_unpack_key(const uint64_t* __restrict__ key,
+                                                       uint32_t n_pods, uint32_t ib,
+                                                       int64_t* __restrict__ best,
+                                                       uint32_t* __restrict__ idx,
+                                                       uint32_t* __restrict__ ties,
+                                                       int64_t* __restrict__ low) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= n_pods) return;
+  const uint64_t imax = (1ull << ib) - 1ull, k = key[p];
+  const int64_t bg = k ? (int64_t)(k >> ib) : -1;
+  ties[p] = (k && best[p] == bg) ? ties[p] : 0u;
+  best[p] = bg;
+  idx[p] = k ? (uint32_t)(imax - (k & imax)) : 0xffffffffu;
+  low[p] = bg;
+}
+
+hipError_t launch_sum_multi_u32(const PtrList& src, uint32_t k, uint64_t n, uint32_t* dst,
+                                hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sum_multi_u32, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock),
+                     0, s, src, k, n, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_key(const int64_t* best, const uint32_t* idx, uint32_t n_pods, uint32_t ib,
+                           uint64_t* key, hipStream_t s) {
+  if (n_pods == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pack_key, pod_grid(n_pods), dim3(kBlock), 0, s, best, idx, n_pods, ib, key);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack_key(const uint64_t* key, uint32_t n_pods, uint32_t ib, int64_t* best,
+                             uint32_t* idx, uint32_t* ties, int64_t* low, hipStream_t s) {
+  if (n_pods == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_unpack_key, pod_grid(n_pods), dim3(kBlock), 0, s, key, n_pods, ib, best,
+                     idx, ties, low);
+  return hipGetLastError();
+}
+
 hipError_t launch_max_multi(const PtrList& src, uint32_t k, uint64_t n, uint64_t* dst,
                             hipStream_t s) {
   if (n == 0) return hipSuccess;

@@ -630,9 +630,10 @@ def test_k2_block_scoring(dev, seed):
 @pytest.mark.parametrize("mode", [MODE_SCV, MODE_DISKIO])
 @pytest.mark.parametrize("path", ["n32", "f64", "u64"])
 def test_comm_local_matches_unsharded(dev, mode, path):
-    """libyoda's own sharded step (yoda_comm_run_local: the all-reduce with count slots and
-    the all-gather of shard records, device copies as the transport) on 1-4 node shards ==
-    the unsharded evaluation: picks, statuses, feasible counts, ties, top scores, maxima."""
+    """libyoda's own sharded step (yoda_comm_run_local: the grouped MAX/SUM exchange of phase 1,
+    then the packed-key merge on the fast paths or the record all-gather on the U64 path in
+    Mode A; device copies as the transport) on 1-4 node shards == the unsharded evaluation:
+    picks, statuses, feasible counts, ties, top scores, maxima."""
     from yoda_amd.capi import comm_run_local
     nodes, pods = synth.make_config(2, pods=700, nodes=3001)
     nodes.total_memory_sum[17] = 0
