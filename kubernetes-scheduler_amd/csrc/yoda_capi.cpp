@@ -123,10 +123,6 @@ hipError_t launch_one(int K, Path path, const unsigned char* nodes, uint32_t n_n
 hipError_t launch_norm_rows(const int64_t* rows, uint32_t n_nodes, uint32_t n_pods,
                             const int64_t* best, const int64_t* lowest, int64_t* norm,
                             hipStream_t s);
-hipError_t launch_slot_counts(const uint32_t* counts, uint32_t n_pods, uint32_t rank,
-                              uint32_t world, uint64_t* slots, hipStream_t s);
-hipError_t launch_unslot_counts(const uint64_t* slots, uint32_t n_pods, uint32_t world,
-                                uint32_t* counts, hipStream_t s);
 hipError_t launch_pack_rec(const int64_t* best, const uint32_t* idx, const uint32_t* ties,
                            const int64_t* low, uint32_t n_pods, ShardRec* rec, hipStream_t s);
 hipError_t launch_merge_rec(const ShardRec* all, uint32_t n_pods, uint32_t world, int64_t* best,

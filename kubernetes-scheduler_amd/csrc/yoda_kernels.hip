@@ -3447,35 +3447,6 @@ hipError_t launch_norm_rows(const int64_t* rows, uint32_t n_nodes, uint32_t n_po
   return hipGetLastError();
 }
 
-// ---- the multi-GPU step inside libyoda (yoda_comm_*) ----------------------
-// Exchange 1 is ONE all-reduce(MAX, u64) over [maxima 6P | count slots world x P]: rank r
-// writes (n_feasible << 32 | n_zero_total) into slot r and zeros elsewhere, so the MAX is an
-// all-gather of the counts, summed after.  Exchange 2 is ONE all-gather of ShardRec [P].
-__global__ __launch_bounds__(kBlock) void k_slot_counts(const uint32_t* __restrict__ counts,
-                                                        uint32_t n_pods, uint32_t rank,
-                                                        uint32_t world,
-                                                        uint64_t* __restrict__ slots) {
-  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (t >= (uint64_t)world * n_pods) return;
-  const uint32_t r = (uint32_t)(t / n_pods), p = (uint32_t)(t % n_pods);
-  slots[t] = r == rank ? ((uint64_t)counts[p] << 32) | counts[(size_t)n_pods + p] : 0ull;
-}
-
-__global__ __launch_bounds__(kBlock) void k_unslot_counts(const uint64_t* __restrict__ slots,
-                                                          uint32_t n_pods, uint32_t world,
-                                                          uint32_t* __restrict__ counts) {
-  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-  if (p >= n_pods) return;
-  uint32_t nf = 0, nz = 0;
-  for (uint32_t r = 0; r < world; ++r) {
-    const uint64_t v = slots[(size_t)r * n_pods + p];
-    nf += (uint32_t)(v >> 32);
-    nz += (uint32_t)v;
-  }
-  counts[p] = nf;
-  counts[(size_t)n_pods + p] = nz;
-}
-
 __global__ __launch_bounds__(kBlock) void k_pack_rec(const int64_t* __restrict__ best,
                                                      const uint32_t* __restrict__ idx,
                                                      const uint32_t* __restrict__ ties,
@@ -3526,23 +3497,6 @@ __global__ __launch_bounds__(kBlock) void k_max_multi(PtrList src, uint32_t k, u
   uint64_t m = 0;
   for (uint32_t j = 0; j < k; ++j) m = umax64(m, static_cast<const uint64_t*>(src.p[j])[t]);
   dst[t] = m;
-}
-
-hipError_t launch_slot_counts(const uint32_t* counts, uint32_t n_pods, uint32_t rank,
-                              uint32_t world, uint64_t* slots, hipStream_t s) {
-  const uint64_t n = (uint64_t)world * n_pods;
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_slot_counts, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                     s, counts, n_pods, rank, world, slots);
-  return hipGetLastError();
-}
-
-hipError_t launch_unslot_counts(const uint64_t* slots, uint32_t n_pods, uint32_t world,
-                                uint32_t* counts, hipStream_t s) {
-  if (n_pods == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_unslot_counts, pod_grid(n_pods), dim3(kBlock), 0, s, slots, n_pods, world,
-                     counts);
-  return hipGetLastError();
 }
 
 hipError_t launch_pack_rec(const int64_t* best, const uint32_t* idx, const uint32_t* ties,
