@@ -1451,12 +1451,20 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     std::vector<std::array<uint64_t, 3>> kors(n_thr, {0ull, 0ull, 0ull});
     {
       std::vector<std::thread> pool;
+      std::vector<uint8_t> thr_failed(n_thr, 0);  // a worker's exception (bad_alloc) -> rethrown
       const uint32_t per = (P + n_thr - 1) / n_thr;
-      for (uint32_t t = 1; t < n_thr; ++t)
-        pool.emplace_back(pack_range, std::min(P, t * per), std::min(P, (t + 1) * per),
-                          std::ref(tables[t]), kors[t].data());
-      pack_range(0, std::min(P, per), tables[0], kors[0].data());
+      auto worker = [&](uint32_t t) {
+        try {
+          pack_range(std::min(P, t * per), std::min(P, (t + 1) * per), tables[t], kors[t].data());
+        } catch (...) {
+          thr_failed[t] = 1;
+        }
+      };
+      for (uint32_t t = 1; t < n_thr; ++t) pool.emplace_back(worker, t);
+      worker(0);
       for (auto& th : pool) th.join();
+      for (uint8_t f : thr_failed)
+        if (f) throw std::bad_alloc();
     }
     GroupTable all = std::move(tables[0]);
     for (uint32_t t = 1; t < n_thr; ++t)
