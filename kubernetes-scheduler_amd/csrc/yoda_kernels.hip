@@ -511,7 +511,7 @@ __global__ __launch_bounds__(kWave) void k_reduce_wit(const uint64_t* __restrict
 // across the wave once per chunk, and both write their 64-bit masks with one store.
 template <int K, bool STATS>
 #ifndef YODA_K1_WAVES
-#define YODA_K1_WAVES 8
+#define YODA_K1_WAVES 7
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 ? 5 : YODA_K1_WAVES))) void k1_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum,
@@ -563,14 +563,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
   const uint64_t num_min = wave_min_u64(live ? number : ~0ull);
   const uint32_t nm_max = wave_max_u32(pm ? need_mem : 0u);
   const uint32_t nm_min = wave_min_u32(pm ? need_mem : ~0u);
-  const uint32_t mpm_max = wave_max_u32(pm ? m : 0u);
-  const uint32_t mpm_min = wave_min_u32(pm ? m : ~0u);
+  // (bounds compared only against node-lane values stay in VGPRs: fewer SGPR spills, whose
+  // v_readlane reloads cost issue slots in every block; profiles/r02/final/k1_occupancy_ab.txt)
+  const uint32_t mpm_max = wave_max_u32v(pm ? m : 0u);
+  const uint32_t mpm_min = wave_min_u32v(pm ? m : ~0u);
   const uint32_t nc_max = wave_max_u32(pc ? need_clk : 0u);
   const uint32_t nc_min = wave_min_u32(pc ? need_clk : ~0u);
   const uint32_t cpc_max = wave_max_u32(pc ? c : 0u);
   const uint32_t cpc_min = wave_min_u32(pc ? c : ~0u);
-  const uint32_t m_max = wave_max_u32(live ? m : 0u), m_min = wave_min_u32(live ? m : ~0u);
-  const uint32_t c_max = wave_max_u32(live ? c : 0u), c_min = wave_min_u32(live ? c : ~0u);
+  const uint32_t m_max = wave_max_u32v(live ? m : 0u), m_min = wave_min_u32v(live ? m : ~0u);
+  const uint32_t c_max = wave_max_u32v(live ? c : 0u), c_min = wave_min_u32v(live ? c : ~0u);
   const bool c_uni = cpc_min == cpc_max;
   // hfs slot of the (1-based) need; a need beyond the K slots has no such card (hfs = 0)
   const bool hfs_all_ok = nm_max <= (uint32_t)K, hfs_none_ok = nm_min <= (uint32_t)K;
