@@ -101,7 +101,8 @@ hipError_t launch_gtable(int K, const uint32_t* sum2, uint32_t n_nodes, const ui
 int topk_k();
 int topk_k_capacity();
 uint32_t greedy_one_blocks();
-hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
+hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes,
+                             const unsigned char* sum2, uint32_t n_nodes,
                              const PodParams& pp, const double* rcp, const float* rcp32,
                              uint32_t n_pods, uint32_t s, const uint64_t* bm, uint32_t bm_stride,
                              const BlockMask* bs, uint32_t bs_stride,
@@ -2093,7 +2094,8 @@ int greedy_eval_fast(GreedyState& g, uint32_t s, int32_t* pick_out) {
   uint32_t* done = h->g1_done.as<uint32_t>();
   // the last block writes the pick straight into mapped pinned memory: no copy
   HIP_TRY(h, h->pick_stage.ensure(16));
-  HIP_TRY(h, launch_greedy_one(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes,
+  HIP_TRY(h, launch_greedy_one(h->K, h->path, h->nodes.as<unsigned char>(),
+                               h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr, h->n_nodes,
                                pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(),
                                h->n_pods, s, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
                                h->bs_ptr(), bs_row(h->n_nodes), ps, pi, done,
@@ -2568,7 +2570,8 @@ int yoda_shard_best_one(yoda_t* h, uint32_t pod, double* score, int32_t* node) {
   double* ps = h->g1_part.as<double>();
   uint32_t* pi = reinterpret_cast<uint32_t*>(ps + nb);
   uint32_t* done = h->g1_done.as<uint32_t>();
-  HIP_TRY(h, launch_greedy_one(h->K, h->path, h->nodes.as<unsigned char>(), h->n_nodes,
+  HIP_TRY(h, launch_greedy_one(h->K, h->path, h->nodes.as<unsigned char>(),
+                               h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr, h->n_nodes,
                                pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(),
                                h->n_pods, s, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
                                h->bs_ptr(), bs_row(h->n_nodes), ps, pi, done, done + 1, h->stream));

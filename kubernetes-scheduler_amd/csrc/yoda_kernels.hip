@@ -1950,19 +1950,26 @@ __global__ __launch_bounds__(kWave) void k_topk_merge_wave(const double* __restr
   }
 }
 
-// Merge of the block K2's packed top-k lists keys[C][P][TK] (descending, 0 = none): one wave
-// per pod (4 pods a workgroup); lane l folds chunks l, l + 64, ... (each list one contiguous
-// read), then the 64 lane lists are folded through shuffles.  Keys are unique (one node each),
-// so the result is the global top TK whatever the folding order.  Out: [TK][P] scores (-1: no
-// entry) and global node ids (0xFFFFFFFF).
+// Merge of the block K2's packed top-k lists keys[C][P][TK] (descending, 0 = none): one
+// workgroup per pod.  Thread t folds chunks t, t + 256, ... into its own sorted list (the
+// first list copied, then insertions until a key falls below the list's tail; each list one
+// contiguous read); each wave then extracts its top TK by TK rounds of wave max over the lane
+// heads (the winning lane shifts its list), and wave 0 the pod's top TK from the four wave
+// lists the same way.  Keys are unique (one node each), so the result is the global top TK
+// whatever the folding order.  Out: [TK][P] scores (-1: no entry) and global node ids
+// (0xFFFFFFFF).  (One workgroup per pod: the capacity windows' 256-1024 pods still fill the
+// chip, and no thread walks more than a few of the C <= 1568 chunks.)
 template <int TK>
 __global__ __launch_bounds__(kBlock) void k_topk_merge_keys(const uint64_t* __restrict__ keys,
                                                             uint32_t C, uint32_t n_pods,
                                                             uint32_t ib, uint32_t node_offset,
                                                             double* __restrict__ out_s,
                                                             uint32_t* __restrict__ out_i) {
-  const uint32_t p = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6), lane = lane_id();
-  if (p >= n_pods) return;  // wave-uniform
+  constexpr uint32_t NW = kBlock / kWave;
+  static_assert(NW * TK <= kWave, "wave 0 holds every wave's list, one key a lane");
+  __shared__ uint64_t lst[NW * TK];
+  const uint32_t p = blockIdx.x, lane = lane_id(), wv = threadIdx.x >> 6;
+  if (p >= n_pods) return;  // workgroup-uniform
   uint64_t pl[TK];
 #pragma unroll
   for (int k = 0; k < TK; ++k) pl[k] = 0ull;
@@ -1975,7 +1982,8 @@ __global__ __launch_bounds__(kBlock) void k_topk_merge_keys(const uint64_t* __re
       x = gt ? o : x;
     }
   };
-  for (uint32_t c = lane; c < C; c += kWave) {
+  bool empty = true;
+  for (uint32_t c = threadIdx.x; c < C; c += kBlock) {
     const ulonglong2* l = reinterpret_cast<const ulonglong2*>(keys + ((size_t)c * n_pods + p) * TK);
     uint64_t v[TK];
 #pragma unroll
@@ -1984,32 +1992,47 @@ __global__ __launch_bounds__(kBlock) void k_topk_merge_keys(const uint64_t* __re
       v[2 * k] = t.x;
       v[2 * k + 1] = t.y;
     }
+    if (empty) {  // the thread's first list: already sorted
+#pragma unroll
+      for (int k = 0; k < TK; ++k) pl[k] = v[k];
+      empty = false;
+      continue;
+    }
 #pragma unroll
     for (int k = 0; k < TK; ++k) {
       if (!(v[k] > pl[TK - 1])) break;  // the list is sorted: nothing further enters
       insert(v[k]);
     }
   }
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) {
-    uint64_t v[TK];
-#pragma unroll
-    for (int k = 0; k < TK; ++k) v[k] = (uint64_t)__shfl_xor((unsigned long long)pl[k], o, kWave);
-#pragma unroll
-    for (int k = 0; k < TK; ++k) {
-      if (!(v[k] > pl[TK - 1])) break;
-      insert(v[k]);
-    }
-  }
-  if (lane != 0) return;
-  const uint64_t imask = (1ull << ib) - 1ull;
+  // the wave's top TK: round k takes the largest lane head (one lane holds it) and that lane
+  // moves on to its next key
+  uint64_t mine = 0ull;
 #pragma unroll
   for (int k = 0; k < TK; ++k) {
-    const uint64_t x = pl[k];
-    out_s[(size_t)k * n_pods + p] = x ? (double)(x >> ib) : -1.0;
-    out_i[(size_t)k * n_pods + p] =
-        x ? (uint32_t)(imask - (x & imask)) + node_offset : 0xffffffffu;
+    const uint64_t m = wave_max_u64v(pl[0]);
+    mine = lane == (uint32_t)k ? m : mine;
+    if (pl[0] == m) {
+#pragma unroll
+      for (int j = 0; j + 1 < TK; ++j) pl[j] = pl[j + 1];
+      pl[TK - 1] = 0ull;
+    }
   }
+  if (lane < (uint32_t)TK) lst[wv * TK + lane] = mine;
+  __syncthreads();
+  if (wv != 0) return;
+  uint64_t x = lane < NW * TK ? lst[lane] : 0ull;
+  mine = 0ull;
+#pragma unroll
+  for (int k = 0; k < TK; ++k) {
+    const uint64_t m = wave_max_u64v(x);
+    mine = lane == (uint32_t)k ? m : mine;
+    x = x == m ? 0ull : x;
+  }
+  if (lane >= (uint32_t)TK) return;
+  const uint64_t imask = (1ull << ib) - 1ull;
+  out_s[(size_t)lane * n_pods + p] = mine ? (double)(mine >> ib) : -1.0;
+  out_i[(size_t)lane * n_pods + p] =
+      mine ? (uint32_t)(imask - (mine & imask)) + node_offset : 0xffffffffu;
 }
 
 // Greedy: overwrite the static score (record header offset 0) of a few nodes.
@@ -2049,9 +2072,15 @@ __global__ __launch_bounds__(kBlock) void k_set_static(unsigned char* __restrict
 // out[1..2] = its raw score as f64 (-1: no feasible node).  One launch: every block
 // writes its (best, index) partial and the last block to finish merges them (the counter is
 // reset for the next call).
+// N32 with the K2 summary (sum2): a one-model node is scored from its summary tile (static
+// part, clock, free-sorted cards; the basic score B[nq] from the G table when the pod's
+// reciprocals are G's, else the k2_block_n32 terms) -- ~50 coalesced bytes instead of the
+// ~250-byte record; other nodes read the record.  The same integers either way (K2's U/FAST
+// classes rely on it).
 template <int K, Path PATH>
 __global__ __launch_bounds__(kBlock) void k_greedy_one(
-    const unsigned char* __restrict__ nodes, uint32_t n_nodes, ScoreArgs args, uint32_t n_pods,
+    const unsigned char* __restrict__ nodes, const uint32_t* __restrict__ sum2,
+    uint32_t n_nodes, ScoreArgs args, uint32_t n_pods,
     uint32_t s, const MaskSrc ms, double* __restrict__ part_s,
     uint32_t* __restrict__ part_i, uint32_t* __restrict__ done, uint32_t* __restrict__ out) {
   constexpr uint32_t stride = PATH == Path::N32 ? n32_stride(K) : node_stride(K);
@@ -2060,12 +2089,53 @@ __global__ __launch_bounds__(kBlock) void k_greedy_one(
   __shared__ bool last;
   Scorer<PATH> sc;
   sc.load(args, s, n_pods);  // the same pod on every lane
+  bool use_g = false;
+  if constexpr (PATH == Path::N32)
+    use_g = args.g.tab != nullptr && sc.r_bw == args.g.r_bw && sc.r_core == args.g.r_core &&
+            sc.r_pow == args.g.r_pow && sc.r_free == args.g.r_free && sc.r_tot == args.g.r_tot;
   const uint32_t bit = s & 63u;
   double best = -1.0;
   uint32_t idx = 0xffffffffu;
   for (uint32_t n = blockIdx.x * kBlock + threadIdx.x; n < n_nodes; n += gridDim.x * kBlock) {
     if ((mask_at(ms, s >> 6, n, n_pods) >> bit) & 1ull) {
-      const double raw = sc.template raw<K>(nodes + (size_t)n * stride);
+      double raw = -1.0;
+      bool done_raw = false;
+      if constexpr (PATH == Path::N32) {
+        if (sum2) {
+          constexpr uint32_t S2 = k2sum_stride(K);
+          auto w = [&](uint32_t word) { return sum2[sum_index(n, word, S2)]; };
+          const uint32_t meta = w(kS2Meta);
+          if (meta & kSumUni4) {
+            const uint32_t cnt = (meta >> 8) & 0xffu;
+            uint32_t nq = 0;
+#pragma unroll
+            for (int t = 0; t < K; ++t) nq += (uint32_t)(w(kS2Fs + t) >= sc.m);
+            nq = min(nq, cnt);
+            uint32_t basic = 0;
+            if (nq) {
+              if (use_g) {
+                basic = args.g.tab[sum_index(n, nq - 1u, gtab_stride(K))];  // B[nq]
+              } else {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int t = 0; t < K; ++t)
+                  acc += (uint32_t)t < nq
+                             ? card_mem_term(w(kS2Fs + t), w(kS2Fs + K + t), sc.r_free, sc.r_tot)
+                             : 0u;
+                basic = nq * card_shared_terms(w(kS2Bw), w(kS2Clock), w(kS2Core), w(kS2Power),
+                                               sc.r_bw, sc.r_core, sc.r_pow) +
+                        acc;
+              }
+            }
+            basic = w(kS2Clock) >= sc.c ? basic : 0u;  // algorithm.go:271
+            const double stat = __longlong_as_double(
+                (long long)((uint64_t)w(kS2Static) | ((uint64_t)w(kS2Static + 1) << 32)));
+            raw = (double)basic + stat;
+            done_raw = true;
+          }
+        }
+      }
+      if (!done_raw) raw = sc.template raw<K>(nodes + (size_t)n * stride);
       if (raw > best) {  // n grows along the thread's sweep: the first maximum is the lowest
         best = raw;
         idx = n;
@@ -3070,7 +3140,8 @@ hipError_t launch_topk_merge_keys(const uint64_t* keys, uint32_t C, uint32_t n_p
                                   uint32_t node_offset, double* out_s, uint32_t* out_i, int tk,
                                   hipStream_t s) {
   if (tk != kTopK && tk != kTopKCap) return hipErrorInvalidValue;
-  const dim3 grid((n_pods + (kBlock / kWave) - 1) / (kBlock / kWave));
+  const dim3 grid(n_pods);  // one workgroup per pod
+  if (n_pods == 0) return hipSuccess;
   if (tk == kTopK)
     hipLaunchKernelGGL(k_topk_merge_keys<kTopK>, grid, dim3(kBlock), 0, s, keys, C, n_pods, ib,
                        node_offset, out_s, out_i);
@@ -3119,24 +3190,27 @@ int topk_k_capacity() { return kTopKCap; }
 constexpr uint32_t kGreedyOneBlocks = 512;
 uint32_t greedy_one_blocks() { return kGreedyOneBlocks; }
 
-hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
+hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes,
+                             const unsigned char* sum2, uint32_t n_nodes,
                              const PodParams& pp, const double* rcp, const float* rcp32,
                              uint32_t n_pods, uint32_t s, const uint64_t* bm, uint32_t bm_stride,
                              const BlockMask* bs, uint32_t bs_stride, double* part_s, uint32_t* part_i, uint32_t* done, uint32_t* out,
                              hipStream_t st) {
-  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
+  ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
+  a.g = pp.g;
   const MaskSrc ms{bm, bs, bm_stride, bs_stride};
+  const uint32_t* s2 = reinterpret_cast<const uint32_t*>(sum2);
   const dim3 grid(std::max<uint32_t>(1, std::min<uint32_t>(kGreedyOneBlocks,
                                                            (n_nodes + kBlock - 1) / kBlock)));
   switch (path) {
     case Path::N32:
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k_greedy_one<KK, Path::N32>), grid, dim3(kBlock), 0,
-                                          st, nodes, n_nodes, a, n_pods, s, ms, part_s,
+                                          st, nodes, s2, n_nodes, a, n_pods, s, ms, part_s,
                                           part_i, done, out));
       break;
     case Path::F64:
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k_greedy_one<KK, Path::F64>), grid, dim3(kBlock), 0,
-                                          st, nodes, n_nodes, a, n_pods, s, ms, part_s,
+                                          st, nodes, nullptr, n_nodes, a, n_pods, s, ms, part_s,
                                           part_i, done, out));
       break;
     default:
