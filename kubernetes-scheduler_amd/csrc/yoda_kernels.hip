@@ -395,7 +395,55 @@ __global__ __launch_bounds__(kBlock) void k1_witness(
     }
     const bool feas =
         live && (number <= hd.card_number) & (cm >= need_mem) & (cc >= need_clk);
-    if (feas) {
+    bool uniform = false;  // one GPU model (scalar flag: a wave-uniform branch)
+    if constexpr (PATH == Path::N32) uniform = (hd.flags & kNodeUniform4) != 0u;
+    if (feas && uniform) {
+      ++nf;
+      nz += hd.zero_total;
+      // the qualifying cards (collection.go:46) are the real cards with free >= m when the
+      // common clock is >= c (padding slots hold zeros: they never raise a maximum, as in
+      // k1_node); the four per-model fields are then the node's own, or 0 with no card
+      auto vmax = [](T x, T y) { return x > y ? x : y; };  // per-lane operands
+      T v[6] = {T(0), T(0), T(0), T(0), T(0), T(0)};
+      uint32_t any = 0;
+      if (ck.v[0] >= c) {
+        const T* g = reinterpret_cast<const T*>(rec);
+        if (hd.flags & kNodeUniformTotal) {
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            const uint32_t q = ((hd.real_mask >> j) & 1u) & (uint32_t)(fr.v[j] >= m);
+            v[kMaxFree] = vmax(v[kMaxFree], q ? fr.v[j] : T(0));
+            any |= q;
+          }
+          v[kMaxTotal] = any ? g[R::off(kTotal, K) / sizeof(T)] : T(0);
+        } else {
+          const Group<T, K> to = load_group<T, K>(rec + R::off(kTotal, K));
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            const uint32_t q = ((hd.real_mask >> j) & 1u) & (uint32_t)(fr.v[j] >= m);
+            v[kMaxFree] = vmax(v[kMaxFree], q ? fr.v[j] : T(0));
+            v[kMaxTotal] = vmax(v[kMaxTotal], q ? to.v[j] : T(0));
+            any |= q;
+          }
+        }
+        v[kMaxBw] = any ? g[R::off(kBandwidth, K) / sizeof(T)] : T(0);
+        v[kMaxClock] = any ? ck.v[0] : T(0);
+        v[kMaxCore] = any ? g[R::off(kCore, K) / sizeof(T)] : T(0);
+        v[kMaxPower] = any ? g[R::off(kPower, K) / sizeof(T)] : T(0);
+      }
+      if (any) {
+#pragma unroll
+        for (int f = 0; f < 6; ++f) {
+          if (v[f] > mx[f]) {  // nodes in increasing order: the first witness is the lowest
+            mx[f] = v[f];
+            wc[f] = 1u;
+            wn[f] = n;
+          } else if (v[f] == mx[f]) {
+            ++wc[f];
+          }
+        }
+      }
+    } else if (feas) {
       ++nf;
       nz += hd.zero_total;
       const Group<T, K> bw = load_group<T, K>(rec + R::off(kBandwidth, K));
