@@ -91,3 +91,14 @@ def test_topk_lists_ties_and_empty():
     pods.has_number[:50] = 1
     (counts, ts, ti), _ = _lists(many, pods)
     _check(many, pods, counts, ts, ti, range(pods.n_pods))
+
+
+def test_topk_lists_many_chunks():
+    """A small batch over many nodes: hundreds of chunk lists per pod, so every thread of the
+    merge (k_topk_merge_keys: one workgroup per pod) folds several lists before the wave and
+    workgroup extraction rounds."""
+    nodes, pods = synth.make_config(3, pods=128, nodes=40000)
+    (counts, ts, ti), path = _lists(nodes, pods)
+    assert path == "n32"
+    rng = np.random.default_rng(11)
+    _check(nodes, pods, counts, ts, ti, rng.choice(pods.n_pods, 40, replace=False))
