@@ -2048,7 +2048,9 @@ struct PodGather {
   }
 };
 
-constexpr uint32_t kGreedyWindow = 4096;
+// 6144 pods: larger windows cost fewer, longer GPU windows but more exact fallbacks (touched
+// nodes invalidate more candidate lists); profiles/r02/final/greedy_window_ab.txt
+constexpr uint32_t kGreedyWindow = 6144;
 // A/B knob: YODA_GREEDY_WINDOW overrides the window size (pods per GPU window).
 uint32_t greedy_window() {
   static const uint32_t w = [] {

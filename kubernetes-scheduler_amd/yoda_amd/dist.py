@@ -447,7 +447,7 @@ def merge_topk(ts_list: Sequence[np.ndarray], ti_list: Sequence[np.ndarray], k: 
             np.take_along_axis(I, o, axis=0).astype(np.uint32))
 
 
-def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window: int = 4096,
+def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window: int = 6144,
                    stats: dict | None = None) -> np.ndarray:
     """Greedy batch assignment (yoda_greedy's semantics: sort.go:8-10 queue order, each pick
     adding the pod's scv/memory to the node, algorithm.go:299-303) over node shards.

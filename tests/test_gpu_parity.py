@@ -472,9 +472,9 @@ def test_greedy_matches_sequential_oracle(dev, flags, path):
 
 @pytest.mark.parametrize("path", ["n32", "f64"])
 def test_greedy_several_sorted_windows(dev, path):
-    """Several 4096-pod windows (each sorted on the device, outputs read through the
+    """Several 6144-pod windows (each sorted on the device, outputs read through the
     permutation) with exact single-pod fallbacks (k_greedy_one) == the sequential oracle."""
-    nodes, pods = synth.make_config(5, pods=9000, nodes=300)
+    nodes, pods = synth.make_config(5, pods=13000, nodes=300)
     dev.upload_nodes(nodes, force_f64=path == "f64")
     got = dev.greedy(pods, MODE_SCV, 0)
     want, _ = oracle.greedy(nodes, pods, MODE_SCV, 0)
