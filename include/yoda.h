@@ -157,6 +157,8 @@ int yoda_synchronize(yoda_t* h);
                                         classified one (tests, A/B measurements)      */
 #define YODA_UPLOAD_NO_GTAB 32u      /* N32: no G table (the block K2 computes every
                                         node's card terms itself; tests, A/B)         */
+#define YODA_UPLOAD_MEM_RANKS 64u    /* N32: memory ranks even when every memory field
+                                        fits 32 bits (tests, A/B)                     */
 int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nodes, uint32_t node_offset,
                       uint32_t flags);
 /* 1 if the uploaded snapshot runs on the generic (u64) path, 0 on a fast path. */
@@ -167,6 +169,11 @@ int yoda_uses_generic_path(const yoda_t* h);
 #define YODA_PATH_F64 1
 #define YODA_PATH_U64 2
 int yoda_record_path(const yoda_t* h);
+/* 1 if the N32 snapshot holds its FreeMemory / TotalMemory as ranks (fields beyond 32 bits,
+ * e.g. bytes: the u32 fields keep every comparison and maximum, value tables give the
+ * quotients and the maxima -- DESIGN.md §3), 0 if as values; -1 for a NULL handle.  The
+ * PreScore maxima returned and exchanged are values either way. */
+int yoda_memory_ranks(const yoda_t* h);
 /* An upper bound on every raw Score of the uploaded snapshot whatever its allocated memory
  * (Basic at the largest clock + the largest Allocate 300 + Actual); ~0 when unbounded.  The
  * sharded merge packs (score, node) into one 64-bit key when it fits (yoda_amd/dist.py). */

@@ -25,13 +25,16 @@
 namespace yoda {
 // launchers (yoda_kernels.hip)
 hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigned char* sum,
+                     const unsigned char* sum2, const unsigned char* mix,
                      uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                      uint32_t n_pods, const Partials& part, uint64_t* bm, uint32_t bm_stride,
                      BlockMask* bs, uint32_t bs_stride, uint64_t* blk, uint32_t blk_stride,
                      unsigned long long* stats, hipStream_t s);
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool narrow,
                           uint64_t* maxima, uint32_t* counts, double* rcp, float* rcp32,
-                          hipStream_t s);
+                          const MemTab& mt, hipStream_t s);
+hipError_t launch_mem_rank(const uint64_t* m_u, uint32_t n_pods, const MemTab& mt, uint32_t* m32,
+                           hipStream_t s);
 hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
                         hipStream_t s);
 hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigned char* sum2,
@@ -96,8 +99,9 @@ hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32
                              const uint64_t* value, const uint64_t* card_number, uint32_t count,
                              unsigned char* sum, uint32_t sum_stride, unsigned char* sum2,
                              uint32_t sum2_stride, hipStream_t s);
-hipError_t launch_gtable(int K, const uint32_t* sum2, uint32_t n_nodes, const uint64_t* g_max,
-                         uint32_t* tab, uint32_t* rcp_out, hipStream_t s);
+hipError_t launch_gtable(int K, const uint32_t* sum2, const uint32_t* mix, uint32_t n_nodes,
+                         const uint64_t* g_max,
+                         uint32_t* tab, uint32_t* rcp_out, MemTab mt, hipStream_t s);
 int topk_k();
 int topk_k_capacity();
 uint32_t greedy_one_blocks();
@@ -114,13 +118,13 @@ hipError_t launch_k1_witness(int K, Path path, const unsigned char* nodes, uint3
                              uint64_t* bm, uint32_t bm_stride, hipStream_t s);
 hipError_t launch_reduce_wit(const uint64_t* pmax, const uint32_t* pwit, const uint32_t* pcnt,
                              uint32_t C, uint32_t n_pods, uint32_t node_offset, uint64_t* maxima,
-                             uint32_t* counts, uint32_t* wcount, uint32_t* wnode, hipStream_t s);
+                             uint32_t* counts, uint32_t* wcount, uint32_t* wnode, const MemTab& mt, hipStream_t s);
 hipError_t launch_wit_prepare(const uint64_t* gmax, const uint64_t* lmax, uint32_t n_pods,
                               uint32_t* wit, hipStream_t s);
 uint32_t one_blocks();
 hipError_t launch_one(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                       const OnePod& pod, uint64_t* feas, void* part, uint32_t* done,
-                      OneOut* out, hipStream_t s);
+                      OneOut* out, const MemTab& mt, hipStream_t s);
 hipError_t launch_norm_rows(const int64_t* rows, uint32_t n_nodes, uint32_t n_pods,
                             const int64_t* best, const int64_t* lowest, int64_t* norm,
                             hipStream_t s);
@@ -140,7 +144,7 @@ size_t order_scratch_bytes(uint32_t n_pods);
 hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
                              const uint32_t* need_mem, uint32_t n_pods, const uint32_t key_bits[3],
                              const uint64_t* groups, uint32_t n_groups, void* scratch,
-                             size_t scratch_bytes, uint32_t* perm, hipStream_t s);
+                             size_t scratch_bytes, uint32_t* perm, const uint32_t* m32, hipStream_t s);
 hipError_t launch_order_count(const OrderMeta& o, const uint64_t* number, const uint64_t* m_u,
                               const uint64_t* c_u, const uint32_t* need_mem, uint32_t n_pods,
                               uint32_t* hist, uint32_t* bstart, uint32_t* slot, uint32_t* bkt,
@@ -280,6 +284,12 @@ struct yoda_handle {
   DevBuf nodes_b;   // Mode B records
   DevBuf k1sum;     // K1 node summaries (N32 path, yoda_layout.h K1SumWord)
   DevBuf k2sum;     // K2 node summaries (N32 path, yoda_layout.h K2SumWord)
+  DevBuf kmix;      // per-card GPU models in free order (N32 path, yoda_layout.h MixWord)
+  // memory ranks (yoda_layout.h MemTab): the N32 memory fields are ranks; value tables
+  bool mem_ranks = false;
+  DevBuf memtab;
+  MemTab mt = {};
+  std::vector<uint64_t> h_frees;  // the distinct card frees, ascending (pod thresholds)
   DevBuf gtab, gtab_aux;  // the G table (yoda_layout.h GTab) + [G maxima | its reciprocals]
   GTab g = {};
   bool has_k1sum = false, has_k2sum = false;
@@ -385,7 +395,7 @@ struct yoda_handle {
   ~yoda_handle() {
     if (comm && rccl().ok) (void)rccl().comm_destroy(comm);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &pod_blob,   &maxima,       &counts,
+    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &memtab,    &pod_blob,   &maxima,       &counts,
                      &pod_sorted, &perm,     &order_scratch, &order_meta, &order_hist,
                      &order_bstart, &order_slot, &order_bkt,
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
@@ -562,6 +572,8 @@ PodParams pod_params(yoda_t* h) {
   pp.alpha = reinterpret_cast<double*>(b + off[kPodAlpha]);
   pp.beta = reinterpret_cast<double*>(b + off[kPodBeta]);
   pp.g = h->has_k2sum ? h->g : GTab{};
+  pp.mix = h->path == Path::N32 ? h->kmix.as<uint32_t>() : nullptr;
+  pp.mt = h->mem_ranks ? h->mt : MemTab{};
   return pp;
 }
 
@@ -655,6 +667,12 @@ int order_pods(yoda_t* h, int mode) {
     o.n_groups = h->og_groups;
     o.nb_log2 = h->og_nb_log2;
     o.m_shift = h->og_m_shift;
+    if (h->mem_ranks) {  // bucket the rank thresholds (< nf + 3) instead of the values
+      uint32_t bits = 0;
+      while (bits < 32 && ((uint64_t)(h->mt.nf + 2) >> bits)) ++bits;
+      o.m_shift = bits > h->og_nb_log2 ? bits - h->og_nb_log2 : 0;
+      o.m32 = reinterpret_cast<const uint32_t*>(b + h->pod_off[kPodM32]);
+    }
     HIP_TRY(h, launch_order_count(o, reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodNumber]),
                                   reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodMU]),
                                   reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodCU]),
@@ -668,18 +686,27 @@ int order_pods(yoda_t* h, int mode) {
     return YODA_OK;
   }
   if (W != P) return fail(h, YODA_ERR_STATE, "padded order without its groups");
+  uint32_t kb[3] = {h->key_bits[0], h->key_bits[1], h->key_bits[2]};
+  if (h->mem_ranks) {  // the rank thresholds' width (< nf + 3)
+    kb[2] = 0;
+    while (kb[2] < 32 && ((uint64_t)(h->mt.nf + 2) >> kb[2])) ++kb[2];
+  }
   const size_t scratch = order_scratch_bytes(P);
   HIP_TRY(h, h->order_scratch.ensure(scratch));
   HIP_TRY(h, launch_order_pods(reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodNumber]),
                                reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodMU]),
                                reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodCU]),
                                reinterpret_cast<const uint32_t*>(b + h->pod_off[kPodNeedMem]), P,
-                               h->key_bits,
+                               kb,
                                h->og_ok ? reinterpret_cast<const uint64_t*>(
                                               h->order_meta.as<unsigned char>())
                                         : nullptr,
                                h->og_ok ? h->og_groups : 0u, h->order_scratch.p,
-                               h->order_scratch.bytes, h->perm.as<uint32_t>(), h->stream));
+                               h->order_scratch.bytes, h->perm.as<uint32_t>(),
+                               h->mem_ranks ? reinterpret_cast<const uint32_t*>(
+                                                  b + h->pod_off[kPodM32])
+                                            : nullptr,
+                               h->stream));
   HIP_TRY(h, launch_permute(t, h->perm.as<uint32_t>(), P, false, h->stream));
   h->ordered = true;
   return YODA_OK;
@@ -745,7 +772,8 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_m
                               h->stream));
   h->blk_zeroed = false;
   HIP_TRY(h, launch_k1(h->K, h->path, h->nodes.as<unsigned char>(),
-                       h->has_k1sum ? h->k1sum.as<unsigned char>() : nullptr, h->n_nodes,
+                       h->has_k1sum ? h->k1sum.as<unsigned char>() : nullptr,
+                       h->k2sum.as<unsigned char>(), h->kmix.as<unsigned char>(), h->n_nodes,
                        h->chunk1, h->C1, pod_params(h), P, part, h->bitmask.as<uint64_t>(),
                        bm_row(h->n_nodes), h->bsum.as<BlockMask>(), bs_row(h->n_nodes),
                        h->blk.as<uint64_t>(), blk_row(h->n_nodes), h->stats_ptr(), h->stream));
@@ -759,7 +787,7 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_m
   const bool rcp = final_maxima && !h->generic;
   HIP_TRY(h, launch_reduce1(part, h->C1, P, h->has_k1sum, maxima, counts,
                             rcp ? h->rcp.as<double>() : nullptr,
-                            rcp ? h->rcp32.as<float>() : nullptr, h->stream));
+                            rcp ? h->rcp32.as<float>() : nullptr, pod_params(h).mt, h->stream));
   h->rcp_ready = rcp;
   return YODA_OK;
 }
@@ -789,7 +817,7 @@ int phase1_witness(yoda_t* h, uint64_t* maxima, uint32_t* counts, uint32_t* wit,
                                pod_params(h), P, part.max_u, h->p_wit.as<uint32_t>(), part.cnt,
                                h->bitmask.as<uint64_t>(), bm_row(N), h->stream));
   HIP_TRY(h, launch_reduce_wit(part.max_u, h->p_wit.as<uint32_t>(), part.cnt, h->C1, P,
-                               node_offset, maxima, counts, wit, wit + 6 * (size_t)P, h->stream));
+                               node_offset, maxima, counts, wit, wit + 6 * (size_t)P, pod_params(h).mt, h->stream));
   return YODA_OK;
 }
 
@@ -1042,7 +1070,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     // Record format: the narrowest exact one.
     std::vector<uint64_t> stat(N);
     std::vector<uint8_t> zt(N);
-    uint64_t max_field = 0, max_small = 0, max_clock = 0, max_static = 0;
+    uint64_t max_field = 0, max_small = 0, max_clock = 0, max_static = 0, max_mem = 0;
     for (uint32_t i = 0; i < N; ++i) {
       bool z = false;
       const uint64_t alloc = nd->alloc_memory ? nd->alloc_memory[i] : 0;
@@ -1056,6 +1084,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
                               nd->card_power[k]});
         max_small = std::max({max_small, nd->card_bandwidth[k], nd->card_core[k],
                               nd->card_power[k], nd->card_clock[k]});
+        max_mem = std::max({max_mem, nd->card_free_memory[k], nd->card_total_memory[k]});
         max_clock = std::max(max_clock, nd->card_clock[k]);
       }
     }
@@ -1075,10 +1104,36 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     }
     // bandwidth, clock, core and power <= 55738 on EVERY shard keeps 300 x + M < 2^24 for
     // any maxima another shard contributes (all shards run one path: yoda_amd/dist.py).
-    const bool n32_ok = f64_ok && max_field <= kN32FieldMax && max_small <= kN32SmallFieldMax;
+    // Memory fields beyond 32 bits (e.g. bytes) keep the N32 path with memory RANKS in the u32
+    // fields (yoda_layout.h MemTab): every compare and max is unchanged, the values come back
+    // for the quotients and the maxima (all <= 2^44: exact in f64).
+    const bool n32_ok = f64_ok && max_small <= kN32SmallFieldMax;
     Path path = n32_ok ? Path::N32 : (f64_ok ? Path::F64 : Path::U64);
     if ((flags & YODA_UPLOAD_FORCE_F64) && path == Path::N32) path = Path::F64;
     if (flags & YODA_UPLOAD_FORCE_GENERIC) path = Path::U64;
+    const bool ranks = path == Path::N32 &&
+                       (max_mem > kN32FieldMax || (flags & YODA_UPLOAD_MEM_RANKS) != 0u);
+    std::vector<uint64_t> frees, totals;  // distinct values, ascending (ranks)
+    if (ranks) {
+      for (uint32_t i = 0; i < N; ++i)
+        for (uint32_t j = 0; j < nd->card_count[i]; ++j) {
+          frees.push_back(nd->card_free_memory[(size_t)i * KS + j]);
+          totals.push_back(nd->card_total_memory[(size_t)i * KS + j]);
+        }
+      for (auto* v : {&frees, &totals}) {
+        std::sort(v->begin(), v->end());
+        v->erase(std::unique(v->begin(), v->end()), v->end());
+      }
+    }
+    // the u32 code of a card's FreeMemory / TotalMemory: its value, or 2 + its rank
+    auto code_f = [&](uint64_t x) -> uint32_t {
+      if (!ranks) return (uint32_t)x;
+      return 2u + (uint32_t)(std::lower_bound(frees.begin(), frees.end(), x) - frees.begin());
+    };
+    auto code_t = [&](uint64_t x) -> uint32_t {
+      if (!ranks) return (uint32_t)x;
+      return 2u + (uint32_t)(std::lower_bound(totals.begin(), totals.end(), x) - totals.begin());
+    };
     // Build records.
     const size_t stride = path == Path::N32 ? n32_stride(K) : node_stride(K);
     std::vector<unsigned char> rec((size_t)std::max<uint32_t>(N, 1) * stride, 0);
@@ -1089,6 +1144,8 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     std::vector<uint32_t> sum(want_sum ? (size_t)std::max<uint32_t>(N, 1) * sstride / 4 : 0, 0);
     const size_t s2stride = k2sum_stride(K);
     std::vector<uint32_t> sum2(want_sum ? (size_t)std::max<uint32_t>(N, 1) * s2stride / 4 : 0, 0);
+    const size_t mstride = mix_stride(K);
+    std::vector<uint32_t> mix(want_sum ? (size_t)std::max<uint32_t>(N, 1) * mstride / 4 : 0, 0);
     for (uint32_t i = 0; i < N; ++i) {
       unsigned char* r = rec.data() + (size_t)i * stride;
       uint32_t hm = 0;
@@ -1131,7 +1188,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
                       (zt[i] ? kSumZeroTotal : 0u) | ((uint32_t)__builtin_popcount(hm) << 8);
         if (cnt > 0) {  // the model values of card 0 (all cards under kSumUni4)
           s[kSumClock] = (uint32_t)nd->card_clock[a];
-          s[kSumTotal] = (uint32_t)nd->card_total_memory[a];
+          s[kSumTotal] = code_t(nd->card_total_memory[a]);
           s[kSumBw] = (uint32_t)nd->card_bandwidth[a];
           s[kSumCore] = (uint32_t)nd->card_core[a];
           s[kSumPower] = (uint32_t)nd->card_power[a];
@@ -1139,7 +1196,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
         uint32_t mrf1 = 0, nhf = 0;
         uint32_t hfs[YODA_MAX_CARDS];
         for (uint32_t j = 0; j < cnt; ++j) {  // N32: free <= 0xFFFFFFFE, so free + 1 fits
-          const uint32_t f1 = (uint32_t)nd->card_free_memory[a + j] + 1u;
+          const uint32_t f1 = code_f(nd->card_free_memory[a + j]) + 1u;
           mrf1 = std::max(mrf1, f1);
           if (nd->card_healthy[a + j]) hfs[nhf++] = f1;
         }
@@ -1159,10 +1216,22 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
         std::stable_sort(ord, ord + cnt, [&](uint32_t x, uint32_t y) {
           return nd->card_free_memory[a + x] > nd->card_free_memory[a + y];
         });
+        uint32_t* mx = mix.data() + (size_t)i * mstride / 4;
+        uint32_t minclk = 0xffffffffu, hmf = 0;
         for (uint32_t j = 0; j < cnt; ++j) {
-          s2[kS2Fs + j] = (uint32_t)nd->card_free_memory[a + ord[j]];
-          s2[kS2Fs + K + j] = (uint32_t)nd->card_total_memory[a + ord[j]];
+          const size_t b = a + ord[j];
+          s2[kS2Fs + j] = code_f(nd->card_free_memory[b]);
+          s2[kS2Fs + K + j] = code_t(nd->card_total_memory[b]);
+          // the per-card models in the same order (nodes without kSumUni4 read them)
+          mx[mix_word(kMixCk, (int)j, K)] = (uint32_t)nd->card_clock[b];
+          mx[mix_word(kMixBw, (int)j, K)] = (uint32_t)nd->card_bandwidth[b];
+          mx[mix_word(kMixCo, (int)j, K)] = (uint32_t)nd->card_core[b];
+          mx[mix_word(kMixPw, (int)j, K)] = (uint32_t)nd->card_power[b];
+          if (nd->card_healthy[b]) hmf |= 1u << j;
+          minclk = std::min(minclk, (uint32_t)nd->card_clock[b]);
         }
+        mx[mix_hm(K)] = hmf;
+        s2[kS2MinClk] = minclk;
       }
       for (uint32_t j = 0; j < nd->card_count[i]; ++j) {
         const size_t k = (size_t)i * KS + j;
@@ -1172,6 +1241,8 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
         if (path == Path::N32) {
           uint32_t* u = reinterpret_cast<uint32_t*>(r + 32);
           for (int f = 0; f < kCardFields; ++f) u[f * K + j] = (uint32_t)v[f];
+          u[kFree * K + j] = code_f(v[kFree]);
+          u[kTotal * K + j] = code_t(v[kTotal]);
           float* g = reinterpret_cast<float*>(r + n32_f32_off(0, K));
           g[kF32Bandwidth * K + j] = (float)v[kBandwidth];
           g[kF32Clock * K + j] = (float)v[kClock];
@@ -1202,6 +1273,10 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
       };
       sum = tiles(sum, (uint32_t)sstride);
       sum2 = tiles(sum2, (uint32_t)s2stride);
+      mix = tiles(mix, (uint32_t)mstride);
+      HIP_TRY(h, h->kmix.ensure(mix.size() * 4));
+      HIP_TRY(h, hipMemcpyAsync(h->kmix.p, mix.data(), mix.size() * 4, hipMemcpyHostToDevice,
+                                h->stream));
       HIP_TRY(h, h->k1sum.ensure(sum.size() * 4));
       HIP_TRY(h, hipMemcpyAsync(h->k1sum.p, sum.data(), sum.size() * 4, hipMemcpyHostToDevice,
                                 h->stream));
@@ -1226,8 +1301,21 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
       HIP_TRY(h, hipMemcpyAsync(h->gtab_aux.p, gmax, sizeof(gmax), hipMemcpyHostToDevice,
                                 h->stream));
       uint32_t* rcp_dev = reinterpret_cast<uint32_t*>(h->gtab_aux.as<unsigned char>() + 48);
-      HIP_TRY(h, launch_gtable(K, h->k2sum.as<uint32_t>(), N, h->gtab_aux.as<uint64_t>(),
-                               h->gtab.as<uint32_t>(), rcp_dev, h->stream));
+      MemTab mt{};
+      if (ranks) {  // value tables: v[0] = v[1] = 0, v[2 + i] = the i-th distinct value
+        std::vector<double> vt(4 + frees.size() + totals.size(), 0.0);
+        for (size_t i = 0; i < frees.size(); ++i) vt[2 + i] = (double)frees[i];
+        for (size_t i = 0; i < totals.size(); ++i) vt[4 + frees.size() + i] = (double)totals[i];
+        HIP_TRY(h, h->memtab.ensure(vt.size() * 8));
+        HIP_TRY(h, hipMemcpy(h->memtab.p, vt.data(), vt.size() * 8, hipMemcpyHostToDevice));
+        mt.vf = h->memtab.as<double>();
+        mt.vt = h->memtab.as<double>() + 2 + frees.size();
+        mt.nf = (uint32_t)frees.size();
+      }
+      h->mt = mt;
+      HIP_TRY(h, launch_gtable(K, h->k2sum.as<uint32_t>(), h->kmix.as<uint32_t>(), N,
+                               h->gtab_aux.as<uint64_t>(),
+                               h->gtab.as<uint32_t>(), rcp_dev, mt, h->stream));
       HIP_TRY(h, hipMemcpyAsync(g_rcp, rcp_dev, sizeof(g_rcp), hipMemcpyDeviceToHost, h->stream));
     }
     const bool diskio = nd->cpu && nd->disk_io;
@@ -1268,7 +1356,18 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
       std::memcpy(&h->g.r_tot, &g_rcp[6], 8);
     }
     h->generic = path == Path::U64;
+    h->mem_ranks = ranks;
+    if (!ranks) h->mt = MemTab{};
+    h->h_frees.swap(frees);
     h->has_nodes = true;
+    // the uploaded pods' N32 memory thresholds follow the snapshot (ranks or the clamp)
+    if (h->has_pods && path == Path::N32) {
+      unsigned char* b = h->pod_blob.as<unsigned char>();
+      HIP_TRY(h, launch_mem_rank(reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodMU]),
+                                 h->n_pods, pod_params(h).mt,
+                                 reinterpret_cast<uint32_t*>(b + h->pod_off[kPodM32]), h->stream));
+      HIP_TRY(h, hipStreamSynchronize(h->stream));
+    }
     h->ran = false;
     h->phase1_done = false;
     if (!is_pow2_le16((uint32_t)K)) return fail(h, YODA_ERR_INVALID_ARG, "bad K");
@@ -1283,6 +1382,8 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
 int yoda_uses_generic_path(const yoda_t* h) { return h ? (h->generic ? 1 : 0) : -1; }
 
 int yoda_record_path(const yoda_t* h) { return h ? (int)h->path : -1; }
+
+int yoda_memory_ranks(const yoda_t* h) { return h ? (h->mem_ranks ? 1 : 0) : -1; }
 
 uint64_t yoda_score_bound(const yoda_t* h) { return h && h->has_nodes ? h->score_bound : ~0ull; }
 
@@ -1480,6 +1581,13 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     std::vector<uint64_t>& gmin = all.mn;
     const size_t g_n = all.n;
     HIP_TRY(h, hipMemcpyAsync(h->pod_blob.p, st, total, hipMemcpyHostToDevice, h->stream));
+    if (h->has_nodes && h->mem_ranks)  // scv/memory -> its rank threshold, on the device
+      HIP_TRY(h, launch_mem_rank(reinterpret_cast<const uint64_t*>(
+                                     h->pod_blob.as<unsigned char>() + off[kPodMU]),
+                                 P, h->mt,
+                                 reinterpret_cast<uint32_t*>(h->pod_blob.as<unsigned char>() +
+                                                             off[kPodM32]),
+                                 h->stream));
     {  // the counting-sort order's groups (yoda_order.hip)
       struct Grp {
         uint64_t key;
@@ -3091,6 +3199,9 @@ static int greedy_eval_exact(yoda_t* h, const yoda_pod_soa* pods, uint32_t p, in
   op.need_mem = pods->has_memory[p] ? need : 0;
   op.need_clk = pods->has_clock[p] ? need : 0;
   op.m32 = (uint32_t)std::min<uint64_t>(m, 0xffffffffull);
+  if (h->mem_ranks)  // the rank threshold (yoda_layout.h MemTab)
+    op.m32 = 2u + (uint32_t)(std::lower_bound(h->h_frees.begin(), h->h_frees.end(), m) -
+                             h->h_frees.begin());
   op.c32 = (uint32_t)std::min<uint64_t>(c, 0xffffffffull);
   op.mf = (double)std::min<uint64_t>(m, 1ull << 53);
   op.cf = (double)std::min<uint64_t>(c, 1ull << 53);
@@ -3103,7 +3214,7 @@ static int greedy_eval_exact(yoda_t* h, const yoda_pod_soa* pods, uint32_t p, in
   }
   HIP_TRY(h, launch_one(h->K, h->path, h->nodes.as<unsigned char>(), N, op,
                         h->one_feas.as<uint64_t>(), h->one_part.p, h->one_done.as<uint32_t>(),
-                        h->one_out.as<OneOut>(), h->stream));
+                        h->one_out.as<OneOut>(), pod_params(h).mt, h->stream));
   HIP_TRY(h, h->pick_stage.ensure(sizeof(OneOut)));
   HIP_TRY(h, hipMemcpyAsync(h->pick_stage.p, h->one_out.p, sizeof(OneOut), hipMemcpyDeviceToHost,
                             h->stream));
@@ -3160,6 +3271,12 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
             h->path == Path::N32
                 ? reinterpret_cast<const uint32_t*>(r + n32_u32_off(f, h->K))[j]
                 : (uint64_t) reinterpret_cast<const double*>(r + 32 + 8 * (size_t)f * K)[j];
+      if (h->path == Path::N32) {  // memory values from the f64 groups (the u32 ones may be ranks)
+        fld[kFree][(size_t)n * K + j] =
+            (uint64_t) reinterpret_cast<const double*>(r + n32_f64_off(kF64Free, h->K))[j];
+        fld[kTotal][(size_t)n * K + j] =
+            (uint64_t) reinterpret_cast<const double*>(r + n32_f64_off(kF64Total, h->K))[j];
+      }
     }
   }
   nv.max_cards = K;

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "yoda_layout.h"
@@ -25,6 +26,8 @@
 namespace yoda {
 
 constexpr int64_t kI64Max = 0x7fffffffffffffffll;
+
+static inline dim3 pod_grid(uint32_t n) { return dim3((n + kBlock - 1) / kBlock); }
 
 // Record policies (yoda_layout.h): field type of the K1 sweep and where its groups live.
 template <Path P>
@@ -60,6 +63,13 @@ __device__ __forceinline__ Group<T, K> load_group(const unsigned char* p) {
 }
 
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
+// Memory ranks (yoda_layout.h MemTab): a maximum in rank space -> its value: max(1, v[r]), the CollectMaxValues floor for r < 2.
+__device__ __forceinline__ uint64_t rank_value(uint64_t r, const double* v) {
+  if (r < 2u) return 1u;
+  const uint64_t x = (uint64_t)v[r];
+  return x > 1u ? x : 1u;
+}
 
 // max of two non-NaN doubles in ONE v_max_f64.  fmax() under the default IEEE mode first
 // canonicalizes both operands (two extra v_max_f64 per call); card fields and maxima are
@@ -505,7 +515,7 @@ __global__ __launch_bounds__(kWave) void k_reduce_wit(const uint64_t* __restrict
                                                        uint64_t* __restrict__ maxima,
                                                        uint32_t* __restrict__ counts,
                                                        uint32_t* __restrict__ wcount,
-                                                       uint32_t* __restrict__ wnode) {
+                                                       uint32_t* __restrict__ wnode, MemTab mt) {
   const uint32_t p = blockIdx.x, lane = threadIdx.x;
   for (int f = 0; f < 6; ++f) {
     uint64_t mx = 1;
@@ -529,6 +539,8 @@ __global__ __launch_bounds__(kWave) void k_reduce_wit(const uint64_t* __restrict
       const uint32_t c2 = __shfl_xor(wc, o, kWave), n2 = __shfl_xor(wn, o, kWave);
       merge(m2, c2, n2);
     }
+    if (mt.vf && f == kMaxFree) mx = rank_value(mx, mt.vf);  // memory ranks -> values
+    if (mt.vf && f == kMaxTotal) mx = rank_value(mx, mt.vt);
     if (lane == 0) {
       maxima[(size_t)f * n_pods + p] = mx;
       wcount[(size_t)f * n_pods + p] = wc;
@@ -563,6 +575,7 @@ template <int K, bool STATS>
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 ? 5 : YODA_K1_WAVES))) void k1_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum,
+    const uint32_t* __restrict__ sum2w, const uint32_t* __restrict__ mixw,
     uint32_t n_nodes, uint32_t chunk_nodes, const uint32_t* __restrict__ m_in,
     const uint32_t* __restrict__ c_in, const uint64_t* __restrict__ number_in,
     const uint32_t* __restrict__ need_mem_in, const uint32_t* __restrict__ need_clk_in,
@@ -572,6 +585,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
     unsigned long long* __restrict__ stats) {
   constexpr uint32_t SS = k1sum_stride(K);
   constexpr uint32_t NS = n32_stride(K);
+  constexpr uint32_t S2 = k2sum_stride(K), MS = mix_stride(K);
   constexpr uint32_t HW = K + 1;  // LDS words per node: hfs[0..K-1], 0
   // + a 10-word record per one-model PART node (below): the per-pod pass reads it from LDS
   constexpr uint32_t REC = 10, RECS = kWave * HW;
@@ -657,7 +671,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
                                 s[64 * kSumMeta]);
     const uint4 w1 = make_uint4(s[64 * kSumMrf1], s[64 * kSumTotal], s[64 * kSumBw],
                                 s[64 * kSumCore]);
-    const uint32_t pw = s[64 * kSumPower];
+    const uint32_t pw0 = s[64 * kSumPower];
     const uint32_t t_all = s[64 * hfs_all], t_none = s[64 * hfs_none];
     if (!need_uni) {  // the node's healthy frees for the per-pod pass: lds[node][need - 1] (slot K: 0)
 #pragma unroll
@@ -665,23 +679,90 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
       lds[lane * HW + K] = 0u;
     }
     const uint64_t cn = (uint64_t)w0.x | ((uint64_t)w0.y << 32);
-    const uint32_t ck = w0.z, meta = w0.w, mrf1 = w1.x, tot = w1.y, bw = w1.z, core = w1.w;
+    const uint32_t meta = w0.w;
+    // the node's model values; for the per-card nodes below, overwritten with their maxima
+    // contribution (those nodes never take the one-model record path, the only other reader)
+    uint32_t ck = w0.z, mrf1 = w1.x, tot = w1.y, bw = w1.z, core = w1.w, pw = pw0;
     const bool uni4 = (meta & kSumUni4) != 0u, unit = (meta & kSumUniTotal) != 0u;
+    const bool one_model = uni4 && unit;
     const uint32_t nh = (meta >> 8) & 0xffu;
-    // PodFitsNumber / PodFitsMemory / PodFitsClock for every pod of the wave at once
+    // PodFitsNumber / PodFitsMemory for every pod of the wave at once
     const bool mem_all = !any_pm || (hfs_all_ok && t_all > mpm_max);
     const bool mem_none = all_pm && (!hfs_none_ok || t_none <= mpm_min);
-    const bool clk_all = !any_pc || (c_uni && uni4 && ck == cpc_max && nh >= nc_max);
-    const bool clk_none = all_pc && c_uni && uni4 && (ck != cpc_max || nh < nc_min);
+    const bool num_none = num_min > cn;
+    // hc: the node's healthy cards whose clock is the wave's scv/clock (PodFitsClock's count,
+    // filter.go:56-58; meaningful when every pod with the label asks for one clock, c_uni)
+    uint32_t hc = (uni4 && ck == cpc_max) ? nh : 0u;
+    // mixed-model nodes: count hc over the per-card clocks (free order, with health bits),
+    // only when it decides something (some pod has the label, all of them one clock) and
+    // the number / memory bounds leave the node open
+    const uint32_t* mxw = mixw + sum_index(nb, 0, MS) + lane;
+    if (any_pc && c_uni) {
+      const bool cnt_clk = valid && !uni4 && !num_none && !mem_none;
+      if (ballot(cnt_clk) != 0ull) {
+        if (cnt_clk) {
+          const uint32_t hm = mxw[64 * mix_hm(K)];
+#pragma unroll
+          for (int t = 0; t < K; ++t)
+            hc += ((hm >> t) & 1u) & (uint32_t)(mxw[64 * mix_word(kMixCk, t, K)] == cpc_max);
+        }
+      }
+    }
+    // PodFitsClock for every pod of the wave at once
+    const bool clk_all = !any_pc || (c_uni && hc >= nc_max);
+    const bool clk_none = all_pc && c_uni && hc < nc_min;
     const bool feas_all = (num_max <= cn) && mem_all && clk_all;
-    const bool feas_none = (num_min > cn) || mem_none || clk_none;
-    // CollectMaxValues card predicate (collection.go:46) on a one-model node:
-    // some card qualifies  <=>  clock >= c  and  max free >= m
-    const bool qual_all = ck >= c_max && mrf1 > m_max;
-    const bool qual_none = ck < c_min || mrf1 <= m_min;
+    const bool feas_none = num_none || mem_none || clk_none;
+    // The node's CollectMaxValues contribution (collection.go:46: cards with free >= m and
+    // clock >= c, no health check) is the same for every pod of the wave when the SMALLEST
+    // qualifying set (the wave's largest m and c) and the LARGEST (its smallest m and c) give
+    // the same six maxima: every pod's set lies between the two.  One-model node with one
+    // TotalMemory: some card qualifies  <=>  clock >= c  and  max free >= m, and then the
+    // maxima are the node's own model values.
+    bool qual = ck >= c_max && mrf1 > m_max;
+    bool same = qual || ck < c_min || mrf1 <= m_min;
+    // Any other node (mixed GPU models, or per-card TotalMemory) that every pod of the wave
+    // passes: a loop over its free-ordered cards (K2 summary frees / totals, per-card models),
+    // lane = node -- the smallest set's maxima, then whether a card of the largest set but
+    // not the smallest raises one of them.
+    const bool gen = valid && !one_model && feas_all && !feas_none;
+    if (ballot(gen) != 0ull) {
+      if (gen) {
+        const uint32_t* s2 = sum2w + sum_index(nb, 0, S2) + lane;
+        bw = ck = core = mrf1 = pw = tot = 0u;  // mrf1: 1 + the free maximum (0: none)
+        bool unc = false;
+#pragma unroll 1
+        for (int t = 0; t < K; ++t) {
+          const uint32_t f = s2[64 * (kS2Fs + t)], cj = mxw[64 * mix_word(kMixCk, t, K)];
+          const bool qs = (f >= m_max) & (cj >= c_max), ql = (f >= m_min) & (cj >= c_min);
+          unc = unc || (ql && !qs);
+          bw = max(bw, qs ? mxw[64 * mix_word(kMixBw, t, K)] : 0u);
+          ck = max(ck, qs ? cj : 0u);
+          core = max(core, qs ? mxw[64 * mix_word(kMixCo, t, K)] : 0u);
+          mrf1 = max(mrf1, qs ? f + 1u : 0u);
+          pw = max(pw, qs ? mxw[64 * mix_word(kMixPw, t, K)] : 0u);
+          tot = max(tot, qs ? s2[64 * (kS2Fs + K + t)] : 0u);
+        }
+        qual = true;
+        same = true;
+        if (unc) {
+#pragma unroll 1
+          for (int t = 0; t < K; ++t) {
+            const uint32_t f = s2[64 * (kS2Fs + t)], cj = mxw[64 * mix_word(kMixCk, t, K)];
+            const bool d = (f >= m_min) & (cj >= c_min) & !((f >= m_max) & (cj >= c_max));
+            const uint32_t raises = (uint32_t)(mxw[64 * mix_word(kMixBw, t, K)] > bw) |
+                                    (uint32_t)(cj > ck) |
+                                    (uint32_t)(mxw[64 * mix_word(kMixCo, t, K)] > core) |
+                                    (uint32_t)(f >= mrf1) |
+                                    (uint32_t)(mxw[64 * mix_word(kMixPw, t, K)] > pw) |
+                                    (uint32_t)(s2[64 * (kS2Fs + K + t)] > tot);
+            same = same && !(d && raises != 0u);
+          }
+        }
+      }
+    }
     const bool is_none = valid && feas_none;
-    const bool is_all =
-        valid && !feas_none && feas_all && uni4 && (qual_none || (qual_all && unit));
+    const bool is_all = valid && !feas_none && feas_all && same;
     const uint64_t all_b = ballot(is_all), none_b = ballot(is_none);
     uint64_t part_b = ballot(valid) & ~all_b & ~none_b;
     if (STATS && !trace && lane == 0) {  // class counts of (wave, node) pairs: ALL, NONE
@@ -690,11 +771,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
     }
     nf_all += (uint32_t)__builtin_popcountll(all_b);
     nz_all += (uint32_t)__builtin_popcountll(ballot(is_all && (meta & kSumZeroTotal)));
-    if (is_all && qual_all) {
+    if (is_all && qual) {
       a_bw = max(a_bw, bw);
       a_ck = max(a_ck, ck);
       a_core = max(a_core, core);
-      a_free = max(a_free, mrf1 - 1u);
+      a_free = max(a_free, mrf1 - (mrf1 != 0u ? 1u : 0u));
       a_pw = max(a_pw, pw);
       a_tot = max(a_tot, tot);
     }
@@ -704,7 +785,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
     // One-model PART nodes: a record of the node's facts in LDS -- {CardNumber lo, hi,
     // clock, meta, max free + 1, hfs[need - 1], bandwidth, core, power, total} -- read by
     // the per-pod pass with broadcast loads, four nodes per trip, branch-free.
-    const bool one_model = (meta & (kSumUni4 | kSumUniTotal)) == (kSumUni4 | kSumUniTotal);
     const uint64_t rec_b = part_b & ballot(one_model);
     if (rec_b != 0ull && ((rec_b >> lane) & 1ull)) {
       uint32_t* r = lds + RECS + lane * REC;
@@ -869,7 +949,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__
                                                     uint64_t* __restrict__ maxima,
                                                     uint32_t* __restrict__ counts,
                                                     double* __restrict__ rcp,
-                                                    float* __restrict__ rcp32) {
+                                                    float* __restrict__ rcp32, MemTab mt) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t f = blockIdx.y;
   if (p >= n_pods) return;
@@ -886,6 +966,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__
 #pragma unroll 8
       for (uint32_t c = 0; c < C; ++c) mx = umax64(mx, src[(size_t)c * n_pods]);
     }
+    if (mt.vf && f == kMaxFree) mx = rank_value(mx, mt.vf);  // memory ranks -> values
+    if (mt.vf && f == kMaxTotal) mx = rank_value(mx, mt.vt);
     maxima[(size_t)f * n_pods + p] = mx;
     // rcp rows: bw, core, power, free, total (k_prep2's order); the clock has none
     const int k = f == kMaxBw ? 0 : f == kMaxCore ? 1 : f == kMaxPower ? 2 : f == kMaxFree ? 3
@@ -910,7 +992,8 @@ __global__ __launch_bounds__(kWave) void k_reduce1_wave(const uint64_t* __restri
                                                          const uint32_t* __restrict__ pcnt,
                                                          uint32_t C, uint32_t n_pods,
                                                          uint64_t* __restrict__ maxima,
-                                                         uint32_t* __restrict__ counts) {
+                                                         uint32_t* __restrict__ counts,
+                                                         MemTab mt) {
   const uint32_t p = blockIdx.x, lane = threadIdx.x;
   for (int f = 0; f < 6; ++f) {
     uint64_t mx = 1;
@@ -919,6 +1002,8 @@ __global__ __launch_bounds__(kWave) void k_reduce1_wave(const uint64_t* __restri
       mx = umax64(mx, NARROW ? (uint64_t)reinterpret_cast<const uint32_t*>(pmax)[o] : pmax[o]);
     }
     for (int o = kWave / 2; o > 0; o >>= 1) mx = umax64(mx, __shfl_xor(mx, o, kWave));
+    if (mt.vf && f == kMaxFree) mx = rank_value(mx, mt.vf);  // memory ranks -> values
+    if (mt.vf && f == kMaxTotal) mx = rank_value(mx, mt.vt);
     if (lane == 0) maxima[(size_t)f * n_pods + p] = mx;
   }
   for (int f = 0; f < 2; ++f) {
@@ -966,6 +1051,47 @@ __global__ __launch_bounds__(kBlock) void k_reduce1_split(const uint64_t* __rest
     for (uint32_t c = c0; c < c1; ++c) sum += src[(size_t)c * n_pods];
     atomicAdd(counts + (size_t)(f - 6) * n_pods + p, sum);
   }
+}
+
+// Memory ranks: scv/memory -> its rank threshold 2 + #{distinct card frees < m} (binary search
+// in mt.vf[2 .. nf + 1], ascending; the frees are <= 2^44, so the f64 compares are exact), or,
+// without ranks (mt.vf == nullptr), the plain N32 clamp min(m, 2^32 - 1).
+__global__ __launch_bounds__(kBlock) void k_mem_rank(const uint64_t* __restrict__ m_u,
+                                                     uint32_t n_pods, MemTab mt,
+                                                     uint32_t* __restrict__ m32) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= n_pods) return;
+  const uint64_t m = m_u[p];
+  if (!mt.vf) {
+    m32[p] = m > 0xffffffffull ? 0xffffffffu : (uint32_t)m;
+    return;
+  }
+  const double md = (double)(m < (1ull << 53) ? m : (1ull << 53));
+  uint32_t lo = 0, hi = mt.nf;  // first index with value >= m
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (mt.vf[2u + mid] < md) lo = mid + 1u; else hi = mid;
+  }
+  m32[p] = 2u + lo;
+}
+
+hipError_t launch_mem_rank(const uint64_t* m_u, uint32_t n_pods, const MemTab& mt, uint32_t* m32,
+                           hipStream_t s) {
+  if (n_pods == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mem_rank, pod_grid(n_pods), dim3(kBlock), 0, s, m_u, n_pods, mt, m32);
+  return hipGetLastError();
+}
+
+// Memory ranks: the free / total rows of maxima [6][P] reduced in rank space (the split
+// reductions' atomics) -> values.
+__global__ __launch_bounds__(kBlock) void k_rank_maxima(uint64_t* __restrict__ maxima,
+                                                        uint32_t n_pods, MemTab mt) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= n_pods) return;
+  uint64_t* f = maxima + (size_t)kMaxFree * n_pods + p;
+  uint64_t* t = maxima + (size_t)kMaxTotal * n_pods + p;
+  *f = rank_value(*f, mt.vf);
+  *t = rank_value(*t, mt.vt);
 }
 
 // RU(100 / M): the smallest double >= 100/M.  With every card field <= 2^44,
@@ -1023,15 +1149,31 @@ __device__ __forceinline__ uint32_t card_mem_term(uint32_t f, uint32_t t, double
                                                   double r_tot) {
   return 3u * (uint32_t)((double)f * r_free) + (uint32_t)((double)t * r_tot);
 }
+// With memory ranks (RK, yoda_layout.h MemTab) f and t are ranks: their values from the tables.
+// The block K2 takes RK as a template parameter (a kernel of its own for rank snapshots: the
+// gathers' registers never reach the plain kernel).
+template <bool RK>
+__device__ __forceinline__ uint32_t mem_term(uint32_t f, uint32_t t, double r_free, double r_tot,
+                                             const MemTab& mt) {
+  if constexpr (RK) return 3u * (uint32_t)(mt.vf[f] * r_free) + (uint32_t)(mt.vt[t] * r_tot);
+  return 3u * (uint32_t)((double)f * r_free) + (uint32_t)((double)t * r_tot);
+}
+// the same with a run-time test (mt.vf: wave-uniform) for the sites outside the block kernels
+__device__ __forceinline__ uint32_t card_mem_term(uint32_t f, uint32_t t, double r_free,
+                                                  double r_tot, const MemTab& mt) {
+  const double fv = mt.vf ? mt.vf[f] : (double)f, tv = mt.vf ? mt.vt[t] : (double)t;
+  return 3u * (uint32_t)(fv * r_free) + (uint32_t)(tv * r_tot);
+}
 
 // Build the G table (GTab above) of the N32 snapshot: g_max = G per maxima field (kMax*
 // order); rcp_out <- G's reciprocals (f32 bw, core, power; f64 free, total) for the host to
 // hand to K2.  One thread per node, tile layout.
 template <int K>
 __global__ __launch_bounds__(kBlock) void k_gtable(const uint32_t* __restrict__ sum2,
+                                                   const uint32_t* __restrict__ mix,
                                                    uint32_t n_nodes, const uint64_t* __restrict__ g_max,
                                                    uint32_t* __restrict__ tab,
-                                                   uint32_t* __restrict__ rcp_out) {
+                                                   uint32_t* __restrict__ rcp_out, MemTab mt) {
   const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
   const float r_bw = ru32_100_over((double)g_max[kMaxBw]);
   const float r_core = ru32_100_over((double)g_max[kMaxCore]);
@@ -1050,27 +1192,36 @@ __global__ __launch_bounds__(kBlock) void k_gtable(const uint32_t* __restrict__ 
     rcp_out[7] = (uint32_t)(t >> 32);
   }
   if (n >= ((n_nodes + 63u) & ~63u)) return;  // padded tail lanes: zero summaries
-  constexpr uint32_t S2 = k2sum_stride(K), GS = gtab_stride(K);
+  constexpr uint32_t S2 = k2sum_stride(K), GS = gtab_stride(K), MS = mix_stride(K);
   auto w = [&](uint32_t word) { return sum2[sum_index(n, word, S2)]; };
+  auto x = [&](uint32_t word) { return mix[sum_index(n, word, MS)]; };
+  const bool uni = (w(kS2Meta) & kSumUni4) != 0u;
   const uint32_t shared =
       card_shared_terms(w(kS2Bw), w(kS2Clock), w(kS2Core), w(kS2Power), r_bw, r_core, r_pow);
   uint32_t acc = 0;
 #pragma unroll
   for (int t = 0; t < K; ++t) {
-    acc += card_mem_term(w(kS2Fs + t), w(kS2Fs + K + t), r_free, r_tot);
-    tab[sum_index(n, t, GS)] = (uint32_t)(t + 1) * shared + acc;  // B[t + 1]
+    // a mixed-model node: each card's own model terms (every card counted: the row a wave
+    // uses when the node's lowest clock passes every pod's scv/clock)
+    const uint32_t sh = uni ? shared
+                            : card_shared_terms(x(mix_word(kMixBw, t, K)), x(mix_word(kMixCk, t, K)),
+                                                x(mix_word(kMixCo, t, K)), x(mix_word(kMixPw, t, K)),
+                                                r_bw, r_core, r_pow);
+    acc += card_mem_term(w(kS2Fs + t), w(kS2Fs + K + t), r_free, r_tot, mt) + (uni ? 0u : sh);
+    tab[sum_index(n, t, GS)] = (uni ? (uint32_t)(t + 1) * shared : 0u) + acc;  // B[t + 1]
   }
 }
 
-hipError_t launch_gtable(int K, const uint32_t* sum2, uint32_t n_nodes, const uint64_t* g_max,
-                         uint32_t* tab, uint32_t* rcp_out, hipStream_t s) {
+hipError_t launch_gtable(int K, const uint32_t* sum2, const uint32_t* mix, uint32_t n_nodes,
+                         const uint64_t* g_max, uint32_t* tab, uint32_t* rcp_out, MemTab mt,
+                         hipStream_t s) {
   const dim3 grid(((n_nodes + 63u) & ~63u) / kBlock + 1);
   switch (K) {
-    case 1: hipLaunchKernelGGL(k_gtable<1>, grid, dim3(kBlock), 0, s, sum2, n_nodes, g_max, tab, rcp_out); break;
-    case 2: hipLaunchKernelGGL(k_gtable<2>, grid, dim3(kBlock), 0, s, sum2, n_nodes, g_max, tab, rcp_out); break;
-    case 4: hipLaunchKernelGGL(k_gtable<4>, grid, dim3(kBlock), 0, s, sum2, n_nodes, g_max, tab, rcp_out); break;
-    case 8: hipLaunchKernelGGL(k_gtable<8>, grid, dim3(kBlock), 0, s, sum2, n_nodes, g_max, tab, rcp_out); break;
-    case 16: hipLaunchKernelGGL(k_gtable<16>, grid, dim3(kBlock), 0, s, sum2, n_nodes, g_max, tab, rcp_out); break;
+    case 1: hipLaunchKernelGGL(k_gtable<1>, grid, dim3(kBlock), 0, s, sum2, mix, n_nodes, g_max, tab, rcp_out, mt); break;
+    case 2: hipLaunchKernelGGL(k_gtable<2>, grid, dim3(kBlock), 0, s, sum2, mix, n_nodes, g_max, tab, rcp_out, mt); break;
+    case 4: hipLaunchKernelGGL(k_gtable<4>, grid, dim3(kBlock), 0, s, sum2, mix, n_nodes, g_max, tab, rcp_out, mt); break;
+    case 8: hipLaunchKernelGGL(k_gtable<8>, grid, dim3(kBlock), 0, s, sum2, mix, n_nodes, g_max, tab, rcp_out, mt); break;
+    case 16: hipLaunchKernelGGL(k_gtable<16>, grid, dim3(kBlock), 0, s, sum2, mix, n_nodes, g_max, tab, rcp_out, mt); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1089,6 +1240,8 @@ struct ScoreArgs {
   const float* rcp32;   // [3][P] f32: bw, core, power
   const uint32_t* cnt = nullptr;  // [P] feasible-node counts (phase 1), or none
   GTab g = {};                    // the snapshot-wide maxima's per-node terms (tab: none)
+  const uint32_t* mix = nullptr;  // per-card models in free order (yoda_layout.h MixWord)
+  MemTab mt = {};                 // memory ranks (yoda_layout.h MemTab)
 };
 
 template <Path P>
@@ -1360,7 +1513,7 @@ __global__ __launch_bounds__(kBlock) void k2_score(
 #ifndef YODA_K2_WAVES
 #define YODA_K2_WAVES 5
 #endif
-template <int K, bool STATS, int TKO = 0>
+template <int K, bool STATS, int TKO = 0, bool RK = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ? (TKO == 0 ? YODA_K2_WAVES : (TKO <= 8 ? 4 : 3)) : 1))) void k2_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum2,
     uint32_t n_nodes, uint32_t chunk_nodes, ScoreArgs args, uint32_t n_pods,
@@ -1369,7 +1522,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     uint32_t blk_stride, double* __restrict__ pbest,
     uint32_t* __restrict__ pidx, uint32_t* __restrict__ pties, double* __restrict__ plow,
     unsigned long long* __restrict__ stats, uint64_t* __restrict__ tk_keys, uint32_t ib) {
-  constexpr uint32_t S2 = k2sum_stride(K), NS = n32_stride(K);
+  constexpr uint32_t S2 = k2sum_stride(K), NS = n32_stride(K), MS = mix_stride(K);
   constexpr bool TOPK = TKO > 0;
   constexpr int TL = TOPK ? TKO : 1;
   constexpr uint32_t PSW = K + 2;  // LDS words per node: B[0..K] (B[q] = q shared + prefix[q]), pad
@@ -1504,7 +1657,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     const uint32_t* s = reinterpret_cast<const uint32_t*>(sum2) + sum_index(nb, 0, S2) + lane;
     const uint4 h0 = make_uint4(s[64 * kS2Static], s[64 * (kS2Static + 1)], s[64 * kS2Clock],
                                 s[64 * kS2Meta]);
-    const uint4 h1 = make_uint4(s[64 * kS2Bw], s[64 * kS2Core], s[64 * kS2Power], 0u);
+    const uint4 h1 = make_uint4(s[64 * kS2Bw], s[64 * kS2Core], s[64 * kS2Power],
+                                s[64 * kS2MinClk]);
     Group<uint32_t, K> fs, ts;  // ts: TotalMemory in free order, or (use_g) B[1..K]
 #pragma unroll
     for (int t = 0; t < K; ++t) fs.v[t] = s[64 * (kS2Fs + t)];
@@ -1517,15 +1671,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       for (int t = 0; t < K; ++t) ts.v[t] = s[64 * (kS2Fs + K + t)];
     }
     if (feas_b == 0) return;  // no pod of the wave can use any node of the block
-    uint64_t fast_b = ballot(mask != 0ull && (h0.w & kSumUni4) != 0u), u_b = 0, rec_b = 0;
+    uint64_t fast_b = 0, u_b = 0, rec_b = 0;
+    // the clock the per-pod passes compare with the pods' scv/clock (algorithm.go:271): the
+    // node's one model, or ~0 for a mixed-model node whose clock test is folded into its row
+    uint32_t ck = h0.z;
+    bool fast = mask != 0ull && (h0.w & kSumUni4) != 0u;
     // TOPK: an upper bound on node n's key for every pod of the wave (uniform maxima, one-model
     // node: every pod qualifies at most the nq_hi cards the smallest scv/memory does); ~0:
     // no bound
     uint64_t ub_key = ~0ull;
     {
-      const uint32_t ck = h0.z, meta = h0.w, bw = h1.x, core = h1.y, pw = h1.z;
+      const uint32_t meta = h0.w, bw = h1.x, core = h1.y, pw = h1.z;
       const uint32_t cnt = (meta >> 8) & 0xffu;
-      const bool fast = mask != 0ull && (meta & kSumUni4) != 0u;
       uint32_t nq_lo = 0, nq_hi = 0;  // qualifying cards for the largest / smallest m
 #pragma unroll
       for (int t = 0; t < K; ++t) {
@@ -1554,7 +1711,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       // wave (two with several reciprocal sets) gets a record: its clock, the wave's mask,
       // the thresholds, the static part and the basic scores -- the per-pod pass reads it
       // with three broadcast LDS loads.
-      const bool two = fast && range <= 1u;
       uint32_t* rec = lds + RECS + lane * REC;
       if (uni_max) {
         // CalculateCardScore terms (algorithm.go:280-291) with the wave's reciprocals: from
@@ -1573,18 +1729,58 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
           }
         } else {
           const uint32_t shared = card_shared_terms(bw, ck, core, pw, u_bw, u_core, u_pow);
-          uint32_t acc = 0;
+          auto row = [&](auto rk) {
+            uint32_t acc = 0;
 #pragma unroll
-          for (int t = 0; t < K; ++t) {
-#ifdef YODA_ABL_NOPREFIX
-            acc += fs.v[t] + ts.v[t];
-#else
-            acc += card_mem_term(fs.v[t], ts.v[t], u_free, u_tot);
-#endif
-            const uint32_t b = (uint32_t)(t + 1) * shared + acc;
-            lds[lane * PSW + t + 1] = b;
-            sel = (uint32_t)(t + 1) == nq_lo ? b : sel;
-            if constexpr (TOPK) sel_hi = (uint32_t)(t + 1) == nq_hi ? b : sel_hi;
+            for (int t = 0; t < K; ++t) {
+              acc += mem_term<decltype(rk)::value>(fs.v[t], ts.v[t], u_free, u_tot, args.mt);
+              const uint32_t b = (uint32_t)(t + 1) * shared + acc;
+              lds[lane * PSW + t + 1] = b;
+              sel = (uint32_t)(t + 1) == nq_lo ? b : sel;
+              if constexpr (TOPK) sel_hi = (uint32_t)(t + 1) == nq_hi ? b : sel_hi;
+            }
+          };
+          row(std::integral_constant<bool, RK>{});
+        }
+        // Mixed-model nodes (cards of several GPU models): when every card's clock test
+        // (clock >= c, algorithm.go:271) comes out the same for every pod of the wave, the
+        // basic score with the first q free-ordered cards qualifying on memory is
+        // B'[q] = the sum of CalculateCardScore over those of them whose clock passes --
+        // a row like the one-model B[q], with the clock test folded in (ck := ~0).  The G
+        // row is B' when every card passes (the node's lowest clock >= the wave's
+        // largest scv/clock).  Otherwise the node stays on the exact per-pod path.
+        const bool mixn = mask != 0ull && (meta & kSumUni4) == 0u;
+        if (ballot(mixn) != 0ull) {
+          if (mixn) {
+            bool ok = use_g && h1.w >= c_max;
+            if (!ok) {
+              const uint32_t* mxw = args.mix + sum_index(nb, 0, MS) + lane;
+              bool cu = true;
+              sel = 0u;
+              sel_hi = 0u;
+              auto row = [&](auto rk) {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int t = 0; t < K; ++t) {
+                  const uint32_t cj = mxw[64 * mix_word(kMixCk, t, K)];
+                  const uint32_t to = use_g ? s[64 * (kS2Fs + K + t)] : ts.v[t];
+                  cu = cu && ((cj >= c_max) || (cj < c_min));
+                  const uint32_t term =
+                      card_shared_terms(mxw[64 * mix_word(kMixBw, t, K)], cj,
+                                        mxw[64 * mix_word(kMixCo, t, K)],
+                                        mxw[64 * mix_word(kMixPw, t, K)], u_bw, u_core, u_pow) +
+                      mem_term<decltype(rk)::value>(fs.v[t], to, u_free, u_tot, args.mt);
+                  acc += cj >= c_max ? term : 0u;
+                  lds[lane * PSW + t + 1] = acc;
+                  sel = (uint32_t)(t + 1) == nq_lo ? acc : sel;
+                  if constexpr (TOPK) sel_hi = (uint32_t)(t + 1) == nq_hi ? acc : sel_hi;
+                }
+              };
+              row(std::integral_constant<bool, RK>{});
+              ok = cu;
+            }
+            fast = ok;
+            ck = ~0u;
           }
         }
         if constexpr (TOPK) {
@@ -1642,10 +1838,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         }
       } else {
         // several reciprocal sets: no U nodes (scores differ across the wave), a record per
-        // two-valued node with the basic scores of every set
-        const bool is_rec = rec_ok && two;
+        // two-valued one-model node with the basic scores of every set (not with memory ranks,
+        // RK: the per-set loop's table gathers would spill the kernel; those nodes take the
+        // per-pod pass)
+        const bool is_rec = !RK && rec_ok && fast && range <= 1u;
         rec_b = ballot(is_rec);
-        if (rec_b != 0ull) {
+        if (!RK && rec_b != 0ull) {
           if (is_rec) {
             *reinterpret_cast<uint4*>(rec) = make_uint4(ck, (uint32_t)mask,
                                                         (uint32_t)(mask >> 32), thr);
@@ -1663,14 +1861,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
             const uint32_t shared = (uint32_t)((float)bw * v_bw) + (uint32_t)((float)ck * v_bw) +
                                     2u * (uint32_t)((float)core * v_core) +
                                     (uint32_t)((float)pw * v_pow);
-            uint32_t acc = 0, sel = 0, sel_hi = 0;
+            uint32_t sel = 0, sel_hi = 0;
+            auto row = [&](auto rk) {
+              uint32_t acc = 0;
 #pragma unroll
-            for (int t = 0; t < K; ++t) {
-              acc += 3u * (uint32_t)((double)fs.v[t] * v_free) +
-                     (uint32_t)((double)ts.v[t] * v_tot);
-              sel = (uint32_t)(t + 1) == nq_lo ? acc : sel;
-              sel_hi = (uint32_t)(t + 1) == nq_hi ? acc : sel_hi;
-            }
+              for (int t = 0; t < K; ++t) {
+                acc += mem_term<decltype(rk)::value>(fs.v[t], ts.v[t], v_free, v_tot, args.mt);
+                sel = (uint32_t)(t + 1) == nq_lo ? acc : sel;
+                sel_hi = (uint32_t)(t + 1) == nq_hi ? acc : sel_hi;
+              }
+            };
+            row(std::integral_constant<bool, RK>{});
             if (is_rec)
               *reinterpret_cast<uint2*>(rec + 8 + 2 * q) =
                   make_uint2(nq_lo * shared + sel, nq_hi * shared + sel_hi);
@@ -1678,6 +1879,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         }
       }
     }
+    fast_b = ballot(fast);
     uint64_t part_b = feas_b & ~u_b;
     if constexpr (TOPK) {
       // a node whose bound is below every active lane's k-th key cannot enter any list: no
@@ -1775,7 +1977,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         for (int t = 0; t < K; ++t)
           nq += (uint32_t)((uint32_t)__builtin_amdgcn_readlane((int)fs.v[t], j) >= sc.m);
         nq = min(nq, cnt);
-        const uint32_t ckj = (uint32_t)__builtin_amdgcn_readlane((int)h0.z, j);
+        const uint32_t ckj = (uint32_t)__builtin_amdgcn_readlane((int)ck, j);
         const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h0.x, j) |
                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)h0.y, j) << 32);
         uint32_t basic;
@@ -1792,14 +1994,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
             2u * (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.y, j) * own.r_core) +
             (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.z, j) * own.r_pow);
           uint32_t mem = 0;
+          auto terms = [&](auto rk) {
 #pragma unroll
-          for (int t = 0; t < K; ++t) {
-            const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)fs.v[t], j);
-            const uint32_t to = (uint32_t)__builtin_amdgcn_readlane((int)ts.v[t], j);
-            const uint32_t term = 3u * (uint32_t)((double)f * own.r_free) +
-                                  (uint32_t)((double)to * own.r_tot);
-            mem += (uint32_t)t < nq ? term : 0u;  // the qualifying cards are a prefix
-          }
+            for (int t = 0; t < K; ++t) {
+              const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)fs.v[t], j);
+              const uint32_t to = (uint32_t)__builtin_amdgcn_readlane((int)ts.v[t], j);
+              const uint32_t term =
+                  mem_term<decltype(rk)::value>(f, to, own.r_free, own.r_tot, args.mt);
+              mem += (uint32_t)t < nq ? term : 0u;  // the qualifying cards are a prefix
+            }
+          };
+          terms(std::integral_constant<bool, RK>{});
           basic = ckj >= sc.c ? nq * shared + mem : 0u;  // algorithm.go:271
         }
         raw = (double)basic + __longlong_as_double((long long)sb);
@@ -2168,7 +2373,8 @@ __global__ __launch_bounds__(kBlock) void k_greedy_one(
 #pragma unroll
                 for (int t = 0; t < K; ++t)
                   acc += (uint32_t)t < nq
-                             ? card_mem_term(w(kS2Fs + t), w(kS2Fs + K + t), sc.r_free, sc.r_tot)
+                             ? card_mem_term(w(kS2Fs + t), w(kS2Fs + K + t), sc.r_free, sc.r_tot,
+                                             args.mt)
                              : 0u;
                 basic = nq * card_shared_terms(w(kS2Bw), w(kS2Clock), w(kS2Core), w(kS2Power),
                                                sc.r_bw, sc.r_core, sc.r_pow) +
@@ -2249,7 +2455,7 @@ __global__ __launch_bounds__(kBlock) void k_one_filter(const unsigned char* __re
                                                        uint64_t* __restrict__ feas,
                                                        uint64_t* __restrict__ part,
                                                        uint32_t* __restrict__ done,
-                                                       OneOut* __restrict__ out) {
+                                                       OneOut* __restrict__ out, MemTab mt) {
   using R = Rec<PATH>;
   using T = typename R::T;
   __shared__ uint64_t red[kBlock / kWave][9];
@@ -2372,6 +2578,10 @@ __global__ __launch_bounds__(kBlock) void k_one_filter(const unsigned char* __re
     acc[6] += red[k][6];
     acc[7] += red[k][7];
     acc[8] = acc[8] < red[k][8] ? acc[8] : red[k][8];
+  }
+  if (mt.vf) {  // memory ranks -> values
+    acc[kMaxFree] = rank_value(acc[kMaxFree], mt.vf);
+    acc[kMaxTotal] = rank_value(acc[kMaxTotal], mt.vt);
   }
   for (int f = 0; f < 6; ++f) out->maxima[f] = acc[f];
   out->nf = (uint32_t)acc[6];
@@ -2947,11 +3157,10 @@ __global__ __launch_bounds__(kBlock) void k_bitmask_transpose(const MaskSrc ms,
     default: return hipErrorInvalidValue;           \
   }
 
-static inline dim3 pod_grid(uint32_t n) { return dim3((n + kBlock - 1) / kBlock); }
 
 
 hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigned char* sum,
-                     uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
+                     const unsigned char* sum2, const unsigned char* mix, uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                      uint32_t n_pods, const Partials& part, uint64_t* bm, uint32_t bm_stride,
                      BlockMask* bs, uint32_t bs_stride, uint64_t* blk, uint32_t blk_stride,
                      unsigned long long* stats, hipStream_t s) {
@@ -2961,13 +3170,17 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
       if (sum) {
         if (stats)
           YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK, true>), grid, dim3(kBlock), 0, s,
-                                              nodes, sum, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
+                                              nodes, sum, reinterpret_cast<const uint32_t*>(sum2),
+                                              reinterpret_cast<const uint32_t*>(mix), n_nodes,
+                                              chunk_nodes, pp.m_32, pp.c_32,
                                               pp.number, pp.need_mem, pp.need_clk, n_pods,
                                               part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,
                                               blk, blk_stride, stats))
         else
           YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK, false>), grid, dim3(kBlock), 0, s,
-                                              nodes, sum, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
+                                              nodes, sum, reinterpret_cast<const uint32_t*>(sum2),
+                                              reinterpret_cast<const uint32_t*>(mix), n_nodes,
+                                              chunk_nodes, pp.m_32, pp.c_32,
                                               pp.number, pp.need_mem, pp.need_clk, n_pods,
                                               part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,
                                               blk, blk_stride, stats));
@@ -3035,7 +3248,7 @@ hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, fl
 // rcp / rcp32 non-null: also the reciprocals (k_prep2 fused; the wave variant runs it after)
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool narrow,
                           uint64_t* maxima, uint32_t* counts, double* rcp, float* rcp32,
-                          hipStream_t s) {
+                          const MemTab& mt, hipStream_t s) {
   if (C > kWaveReduceChunks && n_pods >= 2 * kBlock) {
     // split the chunks so that ~64k threads read the partials, then atomics
     const uint32_t pb = (n_pods + kBlock - 1) / kBlock;
@@ -3050,23 +3263,25 @@ hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, boo
     else
       hipLaunchKernelGGL(k_reduce1_split<false>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt,
                          C, n_pods, maxima, counts);
+    if (mt.vf)  // the atomics ran in rank space
+      hipLaunchKernelGGL(k_rank_maxima, pod_grid(n_pods), dim3(kBlock), 0, s, maxima, n_pods, mt);
     if (rcp) return launch_prep2(maxima, n_pods, rcp, rcp32, s);
   } else if (C > kWaveReduceChunks) {
     if (narrow)
       hipLaunchKernelGGL(k_reduce1_wave<true>, dim3(n_pods), dim3(kWave), 0, s, part.max_u,
-                         part.cnt, C, n_pods, maxima, counts);
+                         part.cnt, C, n_pods, maxima, counts, mt);
     else
       hipLaunchKernelGGL(k_reduce1_wave<false>, dim3(n_pods), dim3(kWave), 0, s, part.max_u,
-                         part.cnt, C, n_pods, maxima, counts);
+                         part.cnt, C, n_pods, maxima, counts, mt);
     if (rcp) return launch_prep2(maxima, n_pods, rcp, rcp32, s);
   } else {
     const dim3 grid((n_pods + kBlock - 1) / kBlock, 8);
     if (narrow)
       hipLaunchKernelGGL(k_reduce1<true>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
-                         n_pods, maxima, counts, rcp, rcp32);
+                         n_pods, maxima, counts, rcp, rcp32, mt);
     else
       hipLaunchKernelGGL(k_reduce1<false>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
-                         n_pods, maxima, counts, rcp, rcp32);
+                         n_pods, maxima, counts, rcp, rcp32, mt);
   }
   return hipGetLastError();
 }
@@ -3088,23 +3303,23 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
                               int64_t* rows, double* tk_s, uint32_t* tk_i,
                               unsigned long long* stats, const uint32_t* counts, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
-  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g};
+  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g, pp.mix, pp.mt};
   const MaskSrc ms{bm, bs, bm_stride, bs_stride};
   switch (path) {
     case Path::N32:
       if (OUT == OUT_ARGMAX && sum2) {
-        if (stats)
-          YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, true>), grid, dim3(kBlock), 0, s,
-                                              nodes, sum2, n_nodes, chunk_nodes, a, n_pods, bm,
-                                              bm_stride, bs, bs_stride, blk, blk_stride,
-                                              part.best_f, part.idx, part.ties, part.low_f, stats,
-                                              nullptr, 0u))
-        else
-          YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false>), grid, dim3(kBlock), 0, s,
-                                              nodes, sum2, n_nodes, chunk_nodes, a, n_pods, bm,
-                                              bm_stride, bs, bs_stride, blk, blk_stride,
-                                              part.best_f, part.idx, part.ties, part.low_f, stats,
-                                              nullptr, 0u));
+#define YODA_K2B(ST, RKV)                                                                        \
+  YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, ST, 0, RKV>), grid, dim3(kBlock), 0, s,  \
+                                      nodes, sum2, n_nodes, chunk_nodes, a, n_pods, bm, bm_stride, \
+                                      bs, bs_stride, blk, blk_stride, part.best_f, part.idx,      \
+                                      part.ties, part.low_f, stats, nullptr, 0u))
+        // memory ranks: the kernel of its own (RK = true)
+        if (stats) {
+          if (a.mt.vf) YODA_K2B(true, true) else YODA_K2B(true, false);
+        } else {
+          if (a.mt.vf) YODA_K2B(false, true) else YODA_K2B(false, false);
+        }
+#undef YODA_K2B
         break;
       }
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score<KK, Path::N32, OUT>), grid, dim3(kBlock), 0,
@@ -3169,16 +3384,16 @@ hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigne
                                 uint32_t ib, int tk, hipStream_t s) {
   if ((tk != kTopK && tk != kTopKCap) || K > 8 || n_pods == 0) return hipErrorInvalidValue;
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
-  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g};
-#define YODA_TOPKB(TKV)                                                                       \
-  YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false, TKV>), grid, dim3(kBlock), 0, s, \
-                                      nodes, sum2, n_nodes, chunk_nodes, a, n_pods, bm,         \
-                                      bm_stride, bs, bs_stride, blk, blk_stride, nullptr,       \
+  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g, pp.mix, pp.mt};
+#define YODA_TOPKB(TKV, RKV)                                                                    \
+  YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false, TKV, RKV>), grid, dim3(kBlock), 0, \
+                                      s, nodes, sum2, n_nodes, chunk_nodes, a, n_pods, bm,        \
+                                      bm_stride, bs, bs_stride, blk, blk_stride, nullptr,         \
                                       nullptr, nullptr, nullptr, nullptr, keys, ib))
   if (tk == kTopK) {
-    YODA_TOPKB(kTopK);
+    if (a.mt.vf) YODA_TOPKB(kTopK, true) else YODA_TOPKB(kTopK, false);
   } else {
-    YODA_TOPKB(kTopKCap);
+    if (a.mt.vf) YODA_TOPKB(kTopKCap, true) else YODA_TOPKB(kTopKCap, false);
   }
 #undef YODA_TOPKB
   return hipGetLastError();
@@ -3246,6 +3461,7 @@ hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes,
                              hipStream_t st) {
   ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
   a.g = pp.g;
+  a.mt = pp.mt;
   const MaskSrc ms{bm, bs, bm_stride, bs_stride};
   const uint32_t* s2 = reinterpret_cast<const uint32_t*>(sum2);
   const dim3 grid(std::max<uint32_t>(1, std::min<uint32_t>(kGreedyOneBlocks,
@@ -3478,7 +3694,8 @@ __global__ __launch_bounds__(kBlock) void k_init_wit(uint64_t* __restrict__ maxi
 
 hipError_t launch_reduce_wit(const uint64_t* pmax, const uint32_t* pwit, const uint32_t* pcnt,
                              uint32_t C, uint32_t n_pods, uint32_t node_offset, uint64_t* maxima,
-                             uint32_t* counts, uint32_t* wcount, uint32_t* wnode, hipStream_t s) {
+                             uint32_t* counts, uint32_t* wcount, uint32_t* wnode, const MemTab& mt,
+                             hipStream_t s) {
   if (n_pods == 0) return hipSuccess;
   if (C > kWaveReduceChunks && n_pods >= kBlock) {
     const uint32_t pb = (n_pods + kBlock - 1) / kBlock;
@@ -3489,10 +3706,12 @@ hipError_t launch_reduce_wit(const uint64_t* pmax, const uint32_t* pwit, const u
                        pcnt, C, n_pods, node_offset, maxima, counts, wcount, wnode);
     hipLaunchKernelGGL(k_reduce_wit_split<1>, dim3(pb, 6, S), dim3(kBlock), 0, s, pmax, pwit,
                        pcnt, C, n_pods, node_offset, maxima, counts, wcount, wnode);
+    if (mt.vf)  // both phases ran in rank space
+      hipLaunchKernelGGL(k_rank_maxima, pod_grid(n_pods), dim3(kBlock), 0, s, maxima, n_pods, mt);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_reduce_wit, dim3(n_pods), dim3(kWave), 0, s, pmax, pwit, pcnt, C, n_pods,
-                     node_offset, maxima, counts, wcount, wnode);
+                     node_offset, maxima, counts, wcount, wnode, mt);
   return hipGetLastError();
 }
 
@@ -3524,7 +3743,7 @@ uint32_t one_blocks() { return kOneBlocks; }
 
 hipError_t launch_one(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                       const OnePod& pod, uint64_t* feas, void* part, uint32_t* done,
-                      OneOut* out, hipStream_t s) {
+                      OneOut* out, const MemTab& mt, hipStream_t s) {
   const dim3 grid(std::max<uint32_t>(1, std::min<uint32_t>(kOneBlocks,
                                                            (n_nodes + kBlock - 1) / kBlock)));
   uint64_t* p1 = static_cast<uint64_t*>(part);
@@ -3532,13 +3751,13 @@ hipError_t launch_one(int K, Path path, const unsigned char* nodes, uint32_t n_n
   switch (path) {
     case Path::N32:
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k_one_filter<KK, Path::N32>), grid, dim3(kBlock), 0, s,
-                                          nodes, n_nodes, pod, feas, p1, done, out);
+                                          nodes, n_nodes, pod, feas, p1, done, out, mt);
                     hipLaunchKernelGGL((k_one_score<KK, Path::N32>), grid, dim3(kBlock), 0, s,
                                        nodes, n_nodes, pod, feas, p2, done + 1, out));
       break;
     case Path::F64:
       YODA_K_SWITCH(K, hipLaunchKernelGGL((k_one_filter<KK, Path::F64>), grid, dim3(kBlock), 0, s,
-                                          nodes, n_nodes, pod, feas, p1, done, out);
+                                          nodes, n_nodes, pod, feas, p1, done, out, MemTab{});
                     hipLaunchKernelGGL((k_one_score<KK, Path::F64>), grid, dim3(kBlock), 0, s,
                                        nodes, n_nodes, pod, feas, p2, done + 1, out));
       break;

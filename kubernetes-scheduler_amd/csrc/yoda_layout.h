@@ -106,9 +106,23 @@ __host__ __device__ constexpr uint32_t k1sum_stride(int k) {
 //   ts[K]   TotalMemory of the same cards, in the same order
 // The qualifying cards of a one-model node (algorithm.go:271) are then a prefix of that
 // order: nq(m) = #{fs >= m} (capped at len(CardList)).
+//   minclk  the lowest clock over the REAL cards (0xFFFFFFFF: empty CardList)
 enum K2SumWord { kS2Static = 0, kS2Clock = 2, kS2Meta = 3, kS2Bw = 4, kS2Core = 5, kS2Power = 6,
-                 kS2Fs = 8 };
+                 kS2MinClk = 7, kS2Fs = 8 };
 __host__ __device__ constexpr uint32_t k2sum_stride(int k) { return 32u + 8u * (uint32_t)k; }
+
+// Per-card GPU models of every node (N32 path), in the K2 summary's descending-free card order,
+// read with lane = node by the block kernels for the nodes whose cards are not all one model
+// (no kSumUni4): u32 words
+//   ck[K], bw[K], co[K], pw[K]   Clock, Bandwidth, Core, Power of the j-th card in free order
+//   hm                           bit j: that card is Healthy
+// (zeros past len(CardList)).  Tile layout like the summaries (sum_index).
+enum MixWord { kMixCk = 0, kMixBw = 1, kMixCo = 2, kMixPw = 3 };
+__host__ __device__ constexpr uint32_t mix_word(int field, int j, int k) {
+  return (uint32_t)(field * k + j);
+}
+__host__ __device__ constexpr uint32_t mix_hm(int k) { return 4u * (uint32_t)k; }
+__host__ __device__ constexpr uint32_t mix_stride(int k) { return 4u * (4u * (uint32_t)k + 1u); }
 
 // Both summaries are stored in tiles of 64 nodes, word-major inside a tile (AoSoA): word w
 // of node n is u32 number sum_index(n, w, stride).  The block kernels read them with
@@ -192,6 +206,20 @@ struct GTab {
 };
 __host__ __device__ constexpr uint32_t gtab_stride(int k) { return 4u * (uint32_t)k; }
 
+// Memory ranks (N32 snapshots whose FreeMemory / TotalMemory exceed 32 bits, e.g. bytes): the
+// u32 memory fields of the records and summaries hold RANKS instead of values -- free ->
+// 2 + its index among the snapshot's distinct card frees (ascending), total -> 2 + its index
+// among the distinct totals -- and scv/memory becomes 2 + #{distinct frees < m}, so every
+// comparison free >= m, every max and every sort order is unchanged.  vf[r] / vt[r] give the
+// value of rank r (index 0, 1: 0).  Values are needed only for the quotients (CalculateCard
+// Score) and the maxima themselves: a maximum of rank r is max(1, v[r]) (r < 2: the floor
+// 1 of collection.go:31-38).  vf == nullptr: plain values.
+struct MemTab {
+  const double* vf = nullptr;
+  const double* vt = nullptr;
+  uint32_t nf = 0;  // distinct card frees (vf[2 .. nf + 1])
+};
+
 struct PodParams {
   // Filter / card predicate thresholds
   double* m_f;         // fast: scv/memory clamped to 2^53 (0 if absent)
@@ -208,6 +236,10 @@ struct PodParams {
   double* beta;
   // the snapshot's G table (N32 with node summaries; tab == nullptr: none)
   GTab g = {};
+  // the snapshot's per-card models in free order (N32; yoda_layout.h MixWord)
+  const uint32_t* mix = nullptr;
+  // the snapshot's memory ranks (MemTab; vf == nullptr: none)
+  MemTab mt = {};
 };
 
 // Per-pod state produced between kernels (length P each unless noted).
@@ -251,6 +283,7 @@ struct OrderMeta {
   const uint64_t* groups;
   const uint32_t* gstart;
   uint32_t n_groups, nb_log2, m_shift;
+  const uint32_t* m32 = nullptr;  // memory ranks: the pods' rank thresholds (MemTab)
 };
 
 // k_finalize of an ordered run: the caller-order outputs (perm == nullptr: none, the

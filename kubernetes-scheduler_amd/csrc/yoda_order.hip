@@ -35,14 +35,16 @@ struct KeyShape {
   uint32_t bm, f_shift, n_shift, c_shift;  // field positions; f_shift == 64: no flag bit
 };
 
+// m32 (memory ranks, yoda_layout.h MemTab): the pods' rank thresholds, monotone in scv/memory,
+// stand in for the 32-bit clamp of the value.
 __device__ __forceinline__ uint64_t order_key(uint64_t number, uint64_t m_u, uint64_t c_u,
                                               uint32_t need_mem, KeyShape k,
                                               const uint64_t* __restrict__ groups,
-                                              uint32_t n_groups) {
+                                              uint32_t n_groups, const uint32_t* m32, uint32_t p) {
   const uint64_t c = c_u < 0xffffffull ? c_u : 0xffffffull;
   const uint64_t n = number < 0xffull ? number : 0xffull;
   const uint64_t f = need_mem != 0u ? 1ull : 0ull;
-  uint64_t m = m_u < 0xffffffffull ? m_u : 0xffffffffull;
+  uint64_t m = m32 ? (uint64_t)m32[p] : (m_u < 0xffffffffull ? m_u : 0xffffffffull);
   if (groups) {
     const uint64_t g = (c << 9) | (n << 1) | f;
     uint32_t lo = 0, hi = n_groups;  // lower_bound: the group's rank
@@ -64,10 +66,11 @@ __global__ __launch_bounds__(kBlock) void k_order_keys(const uint64_t* __restric
                                                        const uint64_t* __restrict__ groups,
                                                        uint32_t n_groups,
                                                        uint64_t* __restrict__ keys,
-                                                       uint32_t* __restrict__ idx) {
+                                                       uint32_t* __restrict__ idx,
+                                                       const uint32_t* __restrict__ m32) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (p >= n_pods) return;
-  keys[p] = order_key(number[p], m_u[p], c_u[p], need_mem[p], k, groups, n_groups);
+  keys[p] = order_key(number[p], m_u[p], c_u[p], need_mem[p], k, groups, n_groups, m32, p);
   idx[p] = p;
 }
 
@@ -81,10 +84,12 @@ __global__ __launch_bounds__(kBlock) void k_order_keys32(const uint64_t* __restr
                                                          const uint64_t* __restrict__ groups,
                                                          uint32_t n_groups,
                                                          uint32_t* __restrict__ keys,
-                                                         uint32_t* __restrict__ idx) {
+                                                         uint32_t* __restrict__ idx,
+                                                         const uint32_t* __restrict__ m32) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (p >= n_pods) return;
-  keys[p] = (uint32_t)order_key(number[p], m_u[p], c_u[p], need_mem[p], k, groups, n_groups);
+  keys[p] = (uint32_t)order_key(number[p], m_u[p], c_u[p], need_mem[p], k, groups, n_groups,
+                                m32, p);
   idx[p] = p;
 }
 
@@ -119,7 +124,8 @@ size_t order_scratch_bytes(uint32_t n_pods) {
 hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const uint64_t* c_u,
                              const uint32_t* need_mem, uint32_t n_pods, const uint32_t key_bits[3],
                              const uint64_t* groups, uint32_t n_groups, void* scratch,
-                             size_t scratch_bytes, uint32_t* perm, hipStream_t s) {
+                             size_t scratch_bytes, uint32_t* perm, const uint32_t* m32,
+                             hipStream_t s) {
   // key_bits = widths of (c, n, m); each <= its clamp (24, 8, 32)
   const uint32_t bc = key_bits[0] < 24 ? key_bits[0] : 24;
   const uint32_t bn = key_bits[1] < 8 ? key_bits[1] : 8;
@@ -142,14 +148,14 @@ hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const 
     uint32_t* k32_in = reinterpret_cast<uint32_t*>(keys_in);
     uint32_t* k32_out = reinterpret_cast<uint32_t*>(keys_out);
     hipLaunchKernelGGL(k_order_keys32, dim3((n_pods + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                       number, m_u, c_u, need_mem, n_pods, k, groups, n_groups, k32_in, idx_in);
+                       number, m_u, c_u, need_mem, n_pods, k, groups, n_groups, k32_in, idx_in, m32);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k32_in, k32_out, idx_in, perm,
                                               (int)n_pods, 0, end_bit, s);
   }
   hipLaunchKernelGGL(k_order_keys, dim3((n_pods + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                     number, m_u, c_u, need_mem, n_pods, k, groups, n_groups, keys_in, idx_in);
+                     number, m_u, c_u, need_mem, n_pods, k, groups, n_groups, keys_in, idx_in, m32);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, perm,
@@ -175,7 +181,8 @@ hipError_t launch_permute(const PermTable& t, const uint32_t* perm, uint32_t n_p
 // results, written back twice), so no wave mixes two groups -- a mixed wave leaves the
 // block kernels nothing but per-pod work on every node.
 __device__ __forceinline__ uint32_t order_bucket(const OrderMeta& o, uint64_t number,
-                                                 uint64_t m_u, uint64_t c_u, uint32_t need_mem) {
+                                                 uint64_t m_u, uint64_t c_u, uint32_t need_mem,
+                                                 uint32_t p) {
   const uint64_t c = c_u < 0xffffffull ? c_u : 0xffffffull;
   const uint64_t n = number < 0xffull ? number : 0xffull;
   const uint64_t key = (c << 9) | (n << 1) | (need_mem != 0u ? 1ull : 0ull);
@@ -184,7 +191,8 @@ __device__ __forceinline__ uint32_t order_bucket(const OrderMeta& o, uint64_t nu
     const uint32_t mid = (lo + hi) >> 1;
     if (o.groups[mid] < key) lo = mid + 1; else hi = mid;
   }
-  const uint64_t m = m_u < 0xffffffffull ? m_u : 0xffffffffull;
+  // memory ranks: the rank thresholds (monotone in scv/memory) instead of the 32-bit clamp
+  const uint64_t m = o.m32 ? (uint64_t)o.m32[p] : (m_u < 0xffffffffull ? m_u : 0xffffffffull);
   const uint32_t nb = 1u << o.nb_log2;
   uint32_t b = (uint32_t)(m >> o.m_shift);
   b = b < nb ? b : nb - 1u;
@@ -208,7 +216,7 @@ __global__ __launch_bounds__(1024) void k_order_hist(OrderMeta o, const uint64_t
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t b = 0, local = 0;
   if (p < n_pods) {
-    b = order_bucket(o, number[p], m_u[p], c_u[p], need_mem[p]);
+    b = order_bucket(o, number[p], m_u[p], c_u[p], need_mem[p], p);
     local = atomicAdd(&lh[b], 1u);
   }
   __syncthreads();

@@ -230,14 +230,16 @@ class ShardExchange:
         # merge when the global node count and score bound fit one int64 key
         self.narrow, self.ib = False, None
         if compact and path_code in (0, 1):
-            lim = [torch.tensor([min(h.score_bound, (1 << 63) - 1), h.node_offset + h.n_nodes],
+            lim = [torch.tensor([min(h.score_bound, (1 << 63) - 1), h.node_offset + h.n_nodes,
+                                 int(h.memory_ranks)],
                                 dtype=torch.int64, device=device) for h in self.handles]
             reducer(lim, "max")
-            bound, n_total = (int(x) for x in lim[0].tolist())
+            bound, n_total, ranks = (int(x) for x in lim[0].tolist())
             ib = max(1, (n_total + 1).bit_length())  # node ids < 2^ib - 1
             if ib <= 40 and bound < (1 << (63 - ib)):
                 self.ib = ib
-            self.narrow = path_code == 0
+            # int32 maxima need every field < 2^32: not with memory ranks (values beyond 32 bits)
+            self.narrow = path_code == 0 and ranks == 0
         stream = torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0
         for h in self.handles:
             h.set_stream(stream)

@@ -108,6 +108,39 @@ def test_pod(p: int = 1) -> PodSoA:
                   ).normalized()
 
 
+def _copy(soa):
+    return type(soa)(**{f: np.array(getattr(soa, f)) for f in soa.__dataclass_fields__})
+
+
+def mixed_models(nodes: NodeSoA, frac: float = 0.5, seed: int = 12) -> NodeSoA:
+    """The same fleet with a fraction `frac` of its nodes holding a mix of GPU models: each
+    real card of such a node draws its own (clock, bandwidth, cores, power) model, so the
+    one-model shortcuts of the block kernels do not apply to it."""
+    out = _copy(nodes)
+    rng = np.random.default_rng(seed)
+    pick = rng.random(out.n_nodes) < frac
+    k = out.card_clock.shape[1]
+    models = rng.integers(0, 3, size=(int(pick.sum()), k))
+    real = np.arange(k)[None, :] < out.card_count[pick][:, None]
+    for arr, table in ((out.card_clock, CLOCKS), (out.card_bandwidth, BANDWIDTHS),
+                       (out.card_core, CORES), (out.card_power, POWERS)):
+        arr[pick] = np.where(real, table[models], 0)
+    return out.normalized()
+
+
+def memory_in_bytes(nodes: NodeSoA, pods: PodSoA):
+    """The same workload with every memory quantity in bytes instead of MiB (card free/total,
+    the sums, the allocated memory, scv/memory): fields above 2^32, the F64 record path."""
+    mib = np.uint64(1 << 20)
+    n = _copy(nodes)
+    for f in ("card_free_memory", "card_total_memory", "free_memory_sum", "total_memory_sum",
+              "alloc_memory"):
+        setattr(n, f, getattr(n, f) * mib)
+    p = _copy(pods)
+    p.memory = p.memory * mib
+    return n.normalized(), p.normalized()
+
+
 CONFIGS = {
     1: dict(pods=1, nodes=100, seed=1, desc="example/test-pod.yaml x 100 synthetic nodes"),
     2: dict(pods=1000, nodes=5000, seed=42, desc="1k pods x 5k nodes"),

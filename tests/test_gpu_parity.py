@@ -89,14 +89,19 @@ def test_every_record_path(dev, path):
     assert_same(got, want)
 
 
-def test_f64_path_chosen_for_wide_fields(dev):
-    # free memory in bytes (> 2^32) leaves the narrow path but stays exact in f64
+def test_wide_memory_fields(dev):
+    # free memory in bytes (> 2^32): the N32 kernels with memory ranks (yoda_layout.h MemTab);
+    # a wide small field (bandwidth > 55738) takes the F64 per-pair kernels instead
     nodes, pods = synth.make_config(2, pods=200, nodes=1500)
     nodes.card_free_memory[:] *= np.uint64(1 << 20)
     nodes.card_total_memory[:] *= np.uint64(1 << 20)
     pods.memory[:] *= np.uint64(1 << 20)
     got, want = run_both(dev, nodes, pods)
-    assert dev.path == "f64"
+    assert dev.path == "n32" and dev.memory_ranks
+    assert_same(got, want)
+    nodes.card_bandwidth[7, 0] = np.uint64(70000)
+    got, want = run_both(dev, nodes, pods)
+    assert dev.path == "f64" and not dev.memory_ranks
     assert_same(got, want)
 
 
