@@ -229,8 +229,17 @@ int yoda_shard_prepare_merge(yoda_t* h, const int64_t* d_best_global, const int6
 int yoda_shard_finalize(yoda_t* h, int mode, const uint32_t* d_counts, const int64_t* d_best,
                         const uint32_t* d_idx, const uint32_t* d_ties, const int64_t* d_lowest);
 /* Generic path only: pods whose NormalizeScore can overflow int64 are re-evaluated with
- * the exact normalize (scheduler.go:176-179).  Returns the number of such pods in *n_pods. */
+ * the exact normalize (scheduler.go:176-179).  Returns the number of such pods in *n_pods
+ * (after yoda_shard_finalize: nonzero means the exchange below is needed). */
 int yoda_shard_overflow_count(yoda_t* h, uint32_t* n_pods);
+/* When yoda_shard_overflow_count reports pods after yoda_shard_finalize, their exact normalize
+ * is split across the shards: yoda_shard_exact_records writes this shard's per-pod records
+ * (d_rec: [P] x 24 bytes, device), the caller ALL-GATHERS them over the ranks in rank order
+ * (d_all: [world][P] x 24 bytes) and yoda_shard_exact_merge folds them into the picks (best
+ * normalized score, lowest node, ties summed, a score outside [0, 100] -> STATUS_SCORE_RANGE),
+ * completing the step.  yoda_comm_run does this itself. */
+int yoda_shard_exact_records(yoda_t* h, void* d_rec);
+int yoda_shard_exact_merge(yoda_t* h, const void* d_all, int world);
 
 /* ---- multi-GPU without a host framework: RCCL inside libyoda ------------------------
  * For callers that have no torch.distributed (the Go plugin through cgo, C).  One handle per
@@ -251,6 +260,19 @@ int yoda_comm_unique_id(uint8_t* id);
 int yoda_comm_init(yoda_t* h, const uint8_t* id, int rank, int world);
 int yoda_comm_run(yoda_t* h, int mode);
 int yoda_comm_run_local(yoda_t* const* handles, int world, int mode);
+/* The greedy batch (yoda_greedy's semantics) over the ranks' node shards, driven inside libyoda
+ * (collective: every rank passes the same pods and the SAME full snapshot `all_nodes`, which the
+ * host-side resolve reads; its handle holds this rank's shard).  Per window the maxima / counts
+ * (capacity mode: and the maxima witnesses) are all-reduced and the shards' top-k candidate
+ * lists all-gathered; an uncertified pod is scored on every shard and the (score, node)
+ * candidates all-gathered.  U64 snapshots: every pod one sharded exact step.  pick [P]: global
+ * node ids in input order.  The shards' node state is restored at the end.  The C/cgo twin of
+ * the Python driver dist.sharded_greedy (the Go plugin's ShardedGreedy calls it).
+ * _local: the same over `world` handles of this process on one device (tests). */
+int yoda_comm_greedy(yoda_t* h, const yoda_node_soa* all_nodes, const yoda_pod_soa* pods,
+                     int mode, uint32_t flags, int32_t* pick);
+int yoda_comm_greedy_local(yoda_t* const* handles, int world, const yoda_node_soa* all_nodes,
+                           const yoda_pod_soa* pods, int mode, uint32_t flags, int32_t* pick);
 
 /* ---- batch ordering ---------------------------------------------------------------- */
 /* Mode A runs of more than 128 pods (yoda_run, yoda_score_rows, yoda_shard_phase1) sort the

@@ -68,6 +68,12 @@ hipError_t launch_k3(int K, const unsigned char* nodes, uint32_t n_nodes, uint32
                      const uint32_t* n_flagged,
                      const int64_t* best, const int64_t* low, const Partials& part,
                      uint32_t max_flagged, hipStream_t s);
+hipError_t launch_reduce3_rec(const Partials& part, uint32_t C, const uint32_t* flagged,
+                              const uint32_t* n_flagged, uint32_t max_flagged,
+                              uint32_t node_offset, ShardRec* rec, hipStream_t s);
+hipError_t launch_merge3(const ShardRec* all, uint32_t n_pods, uint32_t world,
+                         const uint32_t* flagged, const uint32_t* n_flagged, uint32_t max_flagged,
+                         int32_t* pick, int32_t* status, uint32_t* ties, hipStream_t s);
 hipError_t launch_reduce3(const Partials& part, uint32_t C, const uint32_t* flagged,
                           const uint32_t* n_flagged, uint32_t max_flagged, uint32_t node_offset,
                           int32_t* pick, int32_t* status, uint32_t* ties, hipStream_t s);
@@ -377,6 +383,12 @@ struct yoda_handle {
   ncclComm_t comm = nullptr;
   int comm_rank = 0, comm_world = 1;
   DevBuf ex1, rec, rec_all;  // [maxima 6P | count slots world x P] u64; ShardRec [P], [world][P]
+  DevBuf cg_max, cg_cnt, cg_wit, cg_gather;  // yoda_comm_greedy: exchange buffers
+  // sharded exact normalize (K3 over a shard): per-pod records of the flagged pods, pending
+  // until the shards' records are merged (yoda_shard_exact_merge)
+  DevBuf k3rec, k3all;
+  bool k3_pending = false;
+  uint32_t k3_nfl = 0;
   // profiling: event pairs around K1 / K2
   bool profiling = false;
   std::vector<hipEvent_t> ev_pool;
@@ -406,7 +418,7 @@ struct yoda_handle {
                      &p_best_f,  &p_best_i,  &p_idx,      &p_ties,       &p_low_f,
                      &p_low_i,   &p_err,     &pick_alt,   &status_alt,   &ties_out_alt,
                      &p_wit,     &wit,       &stats_dev, &one_feas,  &one_part,  &one_done,
-                     &ex1,       &rec,       &rec_all,
+                     &ex1,       &rec,       &rec_all,   &cg_max,    &cg_cnt,    &cg_wit,    &cg_gather, &k3rec,     &k3all,
                      &one_out,
                      &counts_alt, &best_alt, &maxima_alt};
     for (DevBuf* b : all) b->release();
@@ -875,6 +887,7 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
 int finalize(yoda_t* h, int mode, const uint32_t* counts, const int64_t* best,
              const uint32_t* idx, const uint32_t* ties, const int64_t* low, bool sharded) {
   const uint32_t P = h->n_work;  // sorted positions of this run
+  h->k3_pending = false;
   if (P == 0) return YODA_OK;
   const bool generic = h->generic && mode == YODA_MODE_SCV;
   // the overflow count is written by the generic path only: clear it for those runs, and
@@ -911,16 +924,24 @@ int finalize(yoda_t* h, int mode, const uint32_t* counts, const int64_t* best,
     HIP_TRY(h, hipMemcpyAsync(&nfl, h->n_flagged.p, 4, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     if (nfl > 0) {
-      if (sharded)
-        return fail(h, YODA_ERR_STATE,
-                    "exact-normalize pods (int64 overflow in NormalizeScore) are not supported "
-                    "on the sharded path yet; evaluate on a single handle");
       Partials part = partials(h);
       HIP_TRY(h, launch_k3(h->K, h->nodes.as<unsigned char>(), h->n_nodes, h->chunk2, h->C2,
                            pod_params(h), h->maxima.as<uint64_t>(), P, h->bitmask.as<uint64_t>(),
                            bm_row(h->n_nodes),
                            h->flagged.as<uint32_t>(), h->n_flagged.as<uint32_t>(), best, low,
                            part, nfl, h->stream));
+      if (sharded) {
+        // over this shard's nodes only: per-pod records, merged across the shards by
+        // yoda_shard_exact_merge (the flagged set is the same on every shard: it depends on
+        // the reduced counts, best and lowest only)
+        HIP_TRY(h, h->k3rec.ensure((size_t)P * sizeof(ShardRec)));
+        HIP_TRY(h, launch_reduce3_rec(part, h->C2, h->flagged.as<uint32_t>(),
+                                      h->n_flagged.as<uint32_t>(), nfl, h->node_offset,
+                                      h->k3rec.as<ShardRec>(), h->stream));
+        h->k3_pending = true;
+        h->k3_nfl = nfl;
+        return YODA_OK;  // outputs stay in sorted order until the merge
+      }
       HIP_TRY(h, launch_reduce3(part, h->C2, h->flagged.as<uint32_t>(), h->n_flagged.as<uint32_t>(),
                                 nfl, h->node_offset, h->pick.as<int32_t>(), h->status.as<int32_t>(),
                                 h->ties_out.as<uint32_t>(), h->stream));
@@ -1942,6 +1963,31 @@ int yoda_shard_finalize(yoda_t* h, int mode, const uint32_t* d_counts, const int
     h->ran_bitmask = false;
     h->last_mode = mode;
     return YODA_OK;
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
+int yoda_shard_exact_records(yoda_t* h, void* d_rec) {
+  if (!h || !d_rec) return YODA_ERR_INVALID_ARG;
+  if (!h->k3_pending) return fail(h, YODA_ERR_STATE, "no exact-normalize pods pending");
+  HIP_TRY(h, hipSetDevice(h->device));
+  HIP_TRY(h, hipMemcpyAsync(d_rec, h->k3rec.p, (size_t)h->n_work * sizeof(ShardRec),
+                            hipMemcpyDeviceToDevice, h->stream));
+  return YODA_OK;
+}
+
+int yoda_shard_exact_merge(yoda_t* h, const void* d_all, int world) {
+  if (!h || !d_all || world < 1) return YODA_ERR_INVALID_ARG;
+  if (!h->k3_pending) return fail(h, YODA_ERR_STATE, "no exact-normalize pods pending");
+  try {
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, launch_merge3(static_cast<const ShardRec*>(d_all), h->n_work, (uint32_t)world,
+                             h->flagged.as<uint32_t>(), h->n_flagged.as<uint32_t>(), h->k3_nfl,
+                             h->pick.as<int32_t>(), h->status.as<int32_t>(),
+                             h->ties_out.as<uint32_t>(), h->stream));
+    h->k3_pending = false;
+    return unpermute_outputs(h);
   } catch (...) {
     return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
   }
@@ -3617,11 +3663,334 @@ static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local) 
     h->ran_bitmask = false;
     h->last_mode = mode;
   }
+  // exchange 3 (rare: U64 pods whose NormalizeScore can overflow int64, scheduler.go:176-179):
+  // every shard's exact-normalize records to every shard, then the merge (all shards flag the
+  // same pods, so all of them take this branch)
+  if (h0->k3_pending) {
+    const size_t rb = (size_t)h0->n_work * sizeof(ShardRec);
+    for (int i = 0; i < n; ++i) HIP_TRY(hs[i], hs[i]->k3all.ensure(rb * (size_t)world));
+    if (local) {
+      for (int r = 0; r < n; ++r)
+        for (int i = 0; i < n; ++i)
+          HIP_TRY(h0, hipMemcpyAsync(hs[i]->k3all.as<unsigned char>() + r * rb, hs[r]->k3rec.p,
+                                     rb, hipMemcpyDeviceToDevice, h0->stream));
+    } else {
+      const ncclResult_t r = rccl().all_gather(h0->k3rec.p, h0->k3all.p, rb / 8, ncclUint64,
+                                               h0->comm, h0->stream);
+      if (r != ncclSuccess)
+        return fail(h0, YODA_ERR_HIP, std::string("ncclAllGather: ") + rccl().error_string(r));
+    }
+    for (int i = 0; i < n; ++i) {
+      int rc = yoda_shard_exact_merge(hs[i], hs[i]->k3all.p, world);
+      if (rc) return rc;
+    }
+  }
   return YODA_OK;
 }
 
-extern "C" {
+// Collectives of the libyoda-driven multi-GPU paths: over RCCL (one handle per process, the
+// handle's communicator) or, for tests on one device, over the `n` handles of this process
+// (host-staged: every handle's buffer read back, reduced or concatenated, written back).
+struct Coll {
+  yoda_t* const* hs;
+  int n, world;
+  bool local;
+  int nccl(ncclResult_t r, const char* what) const {
+    if (r == ncclSuccess) return YODA_OK;
+    return fail(hs[0], YODA_ERR_HIP, std::string(what) + ": " + rccl().error_string(r));
+  }
+  // in-place elementwise all-reduce of `count` u64 or u32 device words (MAX / SUM / MIN)
+  int allreduce(const std::vector<void*>& bufs, size_t count, bool u64, ncclRedOp_t op) const {
+    if (count == 0) return YODA_OK;
+    if (!local)
+      return nccl(rccl().all_reduce(bufs[0], bufs[0], count, u64 ? ncclUint64 : ncclUint32, op,
+                                    hs[0]->comm, hs[0]->stream),
+                  "ncclAllReduce");
+    const size_t w = u64 ? 8 : 4;
+    std::vector<unsigned char> acc(count * w), one(count * w);
+    for (int i = 0; i < n; ++i) {
+      HIP_TRY(hs[i], hipMemcpyAsync(i ? one.data() : acc.data(), bufs[i], count * w,
+                                    hipMemcpyDeviceToHost, hs[i]->stream));
+      HIP_TRY(hs[i], hipStreamSynchronize(hs[i]->stream));
+      if (i == 0) continue;
+      for (size_t e = 0; e < count; ++e) {
+        if (u64) {
+          uint64_t& a = reinterpret_cast<uint64_t*>(acc.data())[e];
+          const uint64_t b = reinterpret_cast<const uint64_t*>(one.data())[e];
+          a = op == ncclMax ? std::max(a, b) : op == ncclMin ? std::min(a, b) : a + b;
+        } else {
+          uint32_t& a = reinterpret_cast<uint32_t*>(acc.data())[e];
+          const uint32_t b = reinterpret_cast<const uint32_t*>(one.data())[e];
+          a = op == ncclMax ? std::max(a, b) : op == ncclMin ? std::min(a, b) : a + b;
+        }
+      }
+    }
+    for (int i = 0; i < n; ++i) {
+      HIP_TRY(hs[i], hipMemcpyAsync(bufs[i], acc.data(), count * w, hipMemcpyHostToDevice,
+                                    hs[i]->stream));
+      HIP_TRY(hs[i], hipStreamSynchronize(hs[i]->stream));
+    }
+    return YODA_OK;
+  }
+  // all-gather of host blocks: out = the world's `bytes`-byte blocks in rank order (RCCL:
+  // staged through the first handle's device scratch)
+  int allgather(const std::vector<const void*>& in, size_t bytes,
+                std::vector<unsigned char>& out) const {
+    out.resize((size_t)world * bytes);
+    if (local) {
+      for (int i = 0; i < n; ++i) std::memcpy(out.data() + (size_t)i * bytes, in[i], bytes);
+      return YODA_OK;
+    }
+    yoda_t* h = hs[0];
+    const size_t b8 = (bytes + 7) / 8 * 8;
+    HIP_TRY(h, h->cg_gather.ensure(b8 * ((size_t)world + 1)));
+    unsigned char* d = h->cg_gather.as<unsigned char>();
+    HIP_TRY(h, hipMemcpyAsync(d, in[0], bytes, hipMemcpyHostToDevice, h->stream));
+    int rc = nccl(rccl().all_gather(d, d + b8, b8 / 8, ncclUint64, h->comm, h->stream),
+                  "ncclAllGather");
+    if (rc) return rc;
+    for (int r = 0; r < world; ++r)
+      HIP_TRY(h, hipMemcpyAsync(out.data() + (size_t)r * bytes, d + b8 * ((size_t)r + 1), bytes,
+                                hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    return YODA_OK;
+  }
+};
 
+static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local);
+
+// Greedy batch over node shards, inside libyoda ("Across GPUs"): the protocol of
+// dist.sharded_greedy with RCCL (or the in-process transport): per window, K1 on every shard,
+// maxima MAX / counts SUM (capacity mode: + the witnesses), the shards' candidate lists
+// all-gathered and merged, the host session (identical on every rank, over `all`, the FULL
+// snapshot) resolves the window; an uncertified pod is scored exactly on every shard and the
+// (score, node) candidates all-gathered (capacity mode: it opens the next window).  The U64
+// record path has no candidate lists: every pod is a sharded exact step (comm_step) against
+// the current state.  The shards' node state is restored at the end.
+static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yoda_node_soa* all,
+                       const yoda_pod_soa* pods, int mode, uint32_t flags, int32_t* pick) {
+  yoda_t* h0 = hs[0];
+  const Coll co{hs, n, world, local};
+  const uint32_t P = pods->n_pods;
+  for (int i = 0; i < n; ++i)
+    if (!hs[i]->has_nodes) return fail(h0, YODA_ERR_NO_NODES, "no node snapshot uploaded");
+  if (P == 0) return YODA_OK;
+  int rc;
+  PodGather win;
+  if (mode == YODA_MODE_DISKIO) {  // Mode B reads no assumed-pod state: independent cycles
+    std::vector<uint32_t> idx(P);
+    for (uint32_t i = 0; i < P; ++i) idx[i] = i;
+    win.build(pods, idx.data(), P);
+    for (int i = 0; i < n; ++i)
+      if ((rc = yoda_upload_pods(hs[i], &win.soa))) return rc;
+    if ((rc = comm_step(hs, n, world, mode, local))) return rc;
+    HIP_TRY(h0, hipMemcpyAsync(pick, h0->pick.p, (size_t)P * 4, hipMemcpyDeviceToHost,
+                               h0->stream));
+    HIP_TRY(h0, hipStreamSynchronize(h0->stream));
+    return YODA_OK;
+  }
+  yoda_gs_t* g = nullptr;
+  if ((rc = yoda_gs_create(all, pods, flags, &g))) return fail(h0, rc, "greedy: session setup");
+  struct Guard {
+    yoda_gs_t* g;
+    ~Guard() { yoda_gs_destroy(g); }
+  } guard{g};
+  const bool capacity = (flags & YODA_GREEDY_CARD_CAPACITY) != 0;
+  const bool generic = h0->generic;
+  for (int i = 0; i < n; ++i)
+    if (hs[i]->generic != generic)
+      return fail(h0, YODA_ERR_STATE, "shards on different record paths");
+  std::vector<uint32_t> ids;
+  std::vector<uint64_t> al, cn;
+  auto push = [&](bool original) -> int {  // the session's node changes -> every shard
+    const uint32_t cap = std::max<uint32_t>(g->N, 1);
+    ids.resize(cap), al.resize(cap), cn.resize(cap);
+    uint32_t got = 0;
+    int r = original ? yoda_gs_touched_original(g, cap, ids.data(), al.data(), cn.data(), &got)
+                     : yoda_gs_take_dirty(g, cap, ids.data(), al.data(), cn.data(), &got);
+    if (r) return fail(h0, r, "greedy: node state");
+    if (got == 0) return YODA_OK;
+    for (int i = 0; i < n; ++i)
+      if ((r = yoda_set_node_state(hs[i], got, ids.data(), al.data(), cn.data()))) return r;
+    return YODA_OK;
+  };
+  auto run = [&]() -> int {
+    if (generic) {  // every pod exactly, in queue order, against the current state
+      for (uint32_t q = 0; q < P; ++q) {
+        if ((rc = push(false))) return rc;
+        win.build(pods, g->order.data() + q, 1);
+        for (int i = 0; i < n; ++i)
+          if ((rc = yoda_upload_pods(hs[i], &win.soa))) return rc;
+        if ((rc = comm_step(hs, n, world, YODA_MODE_SCV, local))) return rc;
+        int32_t pk = 0;
+        HIP_TRY(h0, hipMemcpyAsync(&pk, h0->pick.p, 4, hipMemcpyDeviceToHost, h0->stream));
+        HIP_TRY(h0, hipStreamSynchronize(h0->stream));
+        if ((rc = yoda_gs_assign(g, q, pk))) return fail(h0, rc, "greedy: assign");
+        ++h0->greedy_fallbacks;
+      }
+      return push(false);
+    }
+    const uint32_t K = (uint32_t)topk_k(), W0 = std::min<uint32_t>(P, greedy_window());
+    std::vector<uint32_t> counts, ti, wit_h;
+    std::vector<double> ts;
+    std::vector<uint64_t> mx_h;
+    std::vector<unsigned char> gathered, mine, one;
+    std::vector<std::pair<double, uint32_t>> cand;
+    uint32_t ws = 0, W = W0;
+    while (ws < P) {
+      const uint32_t wn = std::min(W, P - ws);
+      if ((rc = push(false))) return rc;
+      win.build(pods, g->order.data() + ws, wn);
+      std::vector<void*> bmax, bcnt, bwc, bwn;
+      for (int i = 0; i < n; ++i) {
+        yoda_t* h = hs[i];
+        if ((rc = yoda_upload_pods(h, &win.soa))) return rc;
+        HIP_TRY(h, h->cg_max.ensure(12ull * wn * 8));  // the maxima, and a local copy
+        HIP_TRY(h, h->cg_cnt.ensure(2ull * wn * 4));
+        HIP_TRY(h, h->cg_wit.ensure(12ull * wn * 4));
+        uint64_t* dmax = h->cg_max.as<uint64_t>();
+        if (capacity) {
+          if ((rc = yoda_shard_phase1_witness(h, dmax, h->cg_cnt.as<uint32_t>(),
+                                              h->cg_wit.as<uint32_t>())))
+            return rc;
+          HIP_TRY(h, hipMemcpyAsync(dmax + 6ull * wn, dmax, 6ull * wn * 8,
+                                    hipMemcpyDeviceToDevice, h->stream));
+        } else if ((rc = yoda_shard_phase1(h, YODA_MODE_SCV, dmax, h->cg_cnt.as<uint32_t>()))) {
+          return rc;
+        }
+        bmax.push_back(dmax);
+        bcnt.push_back(h->cg_cnt.p);
+        bwc.push_back(h->cg_wit.p);
+        bwn.push_back(h->cg_wit.as<uint32_t>() + 6ull * wn);
+      }
+      if (!local) rccl().group_start();
+      rc = co.allreduce(bmax, 6ull * wn, true, ncclMax);
+      const int rc2 = co.allreduce(bcnt, 2ull * wn, false, ncclSum);
+      if (!local) {
+        const int rc3 = co.nccl(rccl().group_end(), "ncclGroupEnd");
+        if (!rc) rc = rc3;
+      }
+      if (rc || (rc = rc2)) return rc;
+      if (capacity) {
+        for (int i = 0; i < n; ++i) {
+          uint64_t* dmax = hs[i]->cg_max.as<uint64_t>();
+          if ((rc = yoda_shard_witness_prepare(hs[i], dmax, dmax + 6ull * wn,
+                                               hs[i]->cg_wit.as<uint32_t>())))
+            return rc;
+        }
+        if ((rc = co.allreduce(bwc, 6ull * wn, false, ncclSum))) return rc;
+        if ((rc = co.allreduce(bwn, 6ull * wn, false, ncclMin))) return rc;
+      }
+      // the shards' candidate lists, all-gathered and merged: the first K of the union in
+      // (score desc, node asc) order contain the global top K
+      counts.resize(2ull * wn);
+      const size_t lb = (size_t)K * wn * 12;  // per shard: K x wn scores (f64) + nodes (u32)
+      mine.resize((size_t)n * lb);
+      for (int i = 0; i < n; ++i) {
+        unsigned char* m = mine.data() + (size_t)i * lb;
+        if ((rc = yoda_shard_topk(hs[i], hs[i]->cg_max.as<uint64_t>(),
+                                  hs[i]->cg_cnt.as<uint32_t>(), counts.data(),
+                                  reinterpret_cast<double*>(m),
+                                  reinterpret_cast<uint32_t*>(m + (size_t)K * wn * 8))))
+          return rc;
+      }
+      std::vector<const void*> ins;
+      for (int i = 0; i < n; ++i) ins.push_back(mine.data() + (size_t)i * lb);
+      if ((rc = co.allgather(ins, lb, gathered))) return rc;
+      ts.assign((size_t)K * wn, -1.0);
+      ti.assign((size_t)K * wn, 0xffffffffu);
+      for (uint32_t p = 0; p < wn; ++p) {
+        cand.clear();
+        for (int r = 0; r < world; ++r) {
+          const unsigned char* b = gathered.data() + (size_t)r * lb;
+          const double* sc = reinterpret_cast<const double*>(b);
+          const uint32_t* nd = reinterpret_cast<const uint32_t*>(b + (size_t)K * wn * 8);
+          for (uint32_t k = 0; k < K; ++k)
+            if (nd[(size_t)k * wn + p] != 0xffffffffu)
+              cand.emplace_back(sc[(size_t)k * wn + p], nd[(size_t)k * wn + p]);
+        }
+        std::sort(cand.begin(), cand.end(), [](const std::pair<double, uint32_t>& a,
+                                               const std::pair<double, uint32_t>& b) {
+          return a.first > b.first || (a.first == b.first && a.second < b.second);
+        });
+        for (uint32_t k = 0; k < K && k < cand.size(); ++k) {
+          ts[(size_t)k * wn + p] = cand[k].first;
+          ti[(size_t)k * wn + p] = cand[k].second;
+        }
+      }
+      if ((rc = yoda_gs_begin_window(g, ws, wn, K, counts.data(), ts.data(), ti.data())))
+        return fail(h0, rc, "greedy: begin window");
+      ++h0->greedy_windows;
+      if (capacity) {
+        mx_h.resize(6ull * wn);
+        wit_h.resize(12ull * wn);
+        if ((rc = yoda_shard_witness_download(h0, h0->cg_max.as<uint64_t>(),
+                                              h0->cg_wit.as<uint32_t>(), mx_h.data(),
+                                              wit_h.data())))
+          return rc;
+        if ((rc = yoda_gs_set_witness(g, mx_h.data(), wit_h.data(), wit_h.data() + 6ull * wn)))
+          return fail(h0, rc, "greedy: witnesses");
+        uint32_t nxt = 0;
+        if ((rc = yoda_gs_resolve(g, &nxt))) return fail(h0, rc, "greedy: resolve");
+        if (nxt < wn) {  // the uncertified pod opens the next window (sized as dist.py does)
+          ++h0->greedy_restarts;
+          ws += nxt;
+          uint32_t b = 0;
+          while ((1ull << b) < 2ull * std::max<uint32_t>(nxt, 1)) ++b;
+          W = std::min<uint32_t>(W0, std::max<uint32_t>(64, 1u << b));
+        } else {
+          ws += wn;
+          W = std::min<uint32_t>(W0, 2 * W);
+        }
+        continue;
+      }
+      for (;;) {
+        uint32_t nxt = 0;
+        if ((rc = yoda_gs_resolve(g, &nxt))) return fail(h0, rc, "greedy: resolve");
+        if (nxt >= wn) break;
+        if ((rc = push(false))) return rc;
+        one.resize((size_t)n * 16);
+        for (int i = 0; i < n; ++i) {
+          double sc = -1.0;
+          int32_t nd = -1;
+          if ((rc = yoda_shard_best_one(hs[i], nxt, &sc, &nd))) return rc;
+          const int64_t nd64 = nd;
+          std::memcpy(one.data() + 16 * (size_t)i, &sc, 8);
+          std::memcpy(one.data() + 16 * (size_t)i + 8, &nd64, 8);
+        }
+        std::vector<const void*> in1;
+        for (int i = 0; i < n; ++i) in1.push_back(one.data() + 16 * (size_t)i);
+        if ((rc = co.allgather(in1, 16, gathered))) return rc;
+        double bs = -1.0;
+        int64_t bn = -1;
+        for (int r = 0; r < world; ++r) {
+          double sc;
+          int64_t nd;
+          std::memcpy(&sc, gathered.data() + 16 * (size_t)r, 8);
+          std::memcpy(&nd, gathered.data() + 16 * (size_t)r + 8, 8);
+          if (nd >= 0 && (sc > bs || (sc == bs && nd < bn))) {
+            bs = sc;
+            bn = nd;
+          }
+        }
+        if (bn < 0) return fail(h0, YODA_ERR_STATE, "greedy: no feasible node for a window pod");
+        if ((rc = yoda_gs_assign(g, ws + nxt, (int32_t)bn))) return fail(h0, rc, "greedy: assign");
+        ++h0->greedy_fallbacks;
+      }
+      ws += wn;
+    }
+    return push(false);
+  };
+  h0->greedy_windows = h0->greedy_fallbacks = h0->greedy_restarts = 0;
+  rc = run();
+  const int rr = push(true);  // restore the shards' original node state
+  if (rc) return rc;
+  if (rr) return rr;
+  uint32_t resolved = 0, assigned = 0;
+  return yoda_gs_picks(g, pick, &resolved, &assigned);
+}
+
+extern "C" {
 int yoda_comm_unique_id(uint8_t* id) {
   if (!id) return YODA_ERR_INVALID_ARG;
   if (!rccl().load()) return YODA_ERR_HIP;
@@ -3662,6 +4031,48 @@ int yoda_comm_run(yoda_t* h, int mode) {
   } catch (...) {
     return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
   }
+}
+
+int yoda_comm_greedy(yoda_t* h, const yoda_node_soa* all_nodes, const yoda_pod_soa* pods,
+                     int mode, uint32_t flags, int32_t* pick) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  if (!all_nodes || !pods || !pick) return fail(h, YODA_ERR_INVALID_ARG, "NULL argument");
+  if (!h->comm) return fail(h, YODA_ERR_STATE, "yoda_comm_greedy before yoda_comm_init");
+  try {
+    HIP_TRY(h, hipSetDevice(h->device));
+    yoda_t* hs[1] = {h};
+    return comm_greedy(hs, 1, h->comm_world, false, all_nodes, pods, mode, flags, pick);
+  } catch (const std::bad_alloc&) {
+    return fail(h, YODA_ERR_INVALID_ARG, "host allocation failed");
+  } catch (...) {
+    return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+}
+
+int yoda_comm_greedy_local(yoda_t* const* hs, int world, const yoda_node_soa* all_nodes,
+                           const yoda_pod_soa* pods, int mode, uint32_t flags, int32_t* pick) {
+  if (!hs || world < 1 || world > kMaxLocalShards || !all_nodes || !pods || !pick)
+    return YODA_ERR_INVALID_ARG;
+  for (int i = 0; i < world; ++i)
+    if (!hs[i]) return YODA_ERR_INVALID_ARG;
+  for (int i = 1; i < world; ++i)
+    if (hs[i]->device != hs[0]->device)
+      return fail(hs[0], YODA_ERR_INVALID_ARG, "local exchange: shards on different devices");
+  std::vector<hipStream_t> saved(world);
+  for (int i = 0; i < world; ++i) {
+    saved[i] = hs[i]->stream;
+    hs[i]->stream = hs[0]->stream;
+  }
+  int rc;
+  try {
+    rc = hipSetDevice(hs[0]->device) == hipSuccess
+             ? comm_greedy(hs, world, world, true, all_nodes, pods, mode, flags, pick)
+             : YODA_ERR_HIP;
+  } catch (...) {
+    rc = fail(hs[0], YODA_ERR_INVALID_ARG, "unexpected exception");
+  }
+  for (int i = 0; i < world; ++i) hs[i]->stream = saved[i];
+  return rc;
 }
 
 int yoda_comm_run_local(yoda_t* const* hs, int world, int mode) {

@@ -569,6 +569,9 @@ __global__ __launch_bounds__(kWave) void k_reduce_wit(const uint64_t* __restrict
 // NONE and ALL are exact statements about every (pod, node) pair of the block, not
 // approximations: ALL nodes fold their contribution into node-lane maxima that are reduced
 // across the wave once per chunk, and both write their 64-bit masks with one store.
+#ifndef YODA_K1_GEN_UNROLL
+#define YODA_K1_GEN_UNROLL 1
+#endif
 template <int K, bool STATS>
 #ifndef YODA_K1_WAVES
 #define YODA_K1_WAVES 7
@@ -662,17 +665,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
       atomicOr(reinterpret_cast<unsigned long long*>(blkw + blk_wi), (unsigned long long)blk_bits);
   };
 
+#ifndef YODA_K1_PF
+#define YODA_K1_PF 0
+#endif
+  // the summary words a block's classification reads (YODA_K1_PF: the next block's are loaded
+  // while this one is classified -- the loop is otherwise one memory latency per block)
+  uint4 pf0 = make_uint4(0u, 0u, 0u, 0u), pf1 = pf0;
+  uint32_t pf_pw = 0, pf_ta = 0, pf_tn = 0;
+  auto load_sum = [&](uint32_t nb) {
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(sum) + sum_index(nb, 0, SS) + lane;
+    pf0 = make_uint4(s[64 * kSumCnLo], s[64 * kSumCnHi], s[64 * kSumClock], s[64 * kSumMeta]);
+    pf1 = make_uint4(s[64 * kSumMrf1], s[64 * kSumTotal], s[64 * kSumBw], s[64 * kSumCore]);
+    pf_pw = s[64 * kSumPower];
+    pf_ta = s[64 * hfs_all];
+    pf_tn = s[64 * hfs_none];
+  };
+  if (YODA_K1_PF && n0 < n1) load_sum(n0);
   for (uint32_t nb = n0; nb < n1; nb += kWave) {
     const uint32_t n = nb + lane;
     const bool valid = n < n1;
     // this block's tile of summaries (nb is a multiple of 64): word w at s[64 w]
     const uint32_t* s = reinterpret_cast<const uint32_t*>(sum) + sum_index(nb, 0, SS) + lane;
-    const uint4 w0 = make_uint4(s[64 * kSumCnLo], s[64 * kSumCnHi], s[64 * kSumClock],
-                                s[64 * kSumMeta]);
-    const uint4 w1 = make_uint4(s[64 * kSumMrf1], s[64 * kSumTotal], s[64 * kSumBw],
-                                s[64 * kSumCore]);
-    const uint32_t pw0 = s[64 * kSumPower];
-    const uint32_t t_all = s[64 * hfs_all], t_none = s[64 * hfs_none];
+    if (!YODA_K1_PF) load_sum(nb);
+    const uint4 w0 = pf0, w1 = pf1;
+    const uint32_t pw0 = pf_pw, t_all = pf_ta, t_none = pf_tn;
+    if (YODA_K1_PF && nb + kWave < n1) load_sum(nb + kWave);
     if (!need_uni) {  // the node's healthy frees for the per-pod pass: lds[node][need - 1] (slot K: 0)
 #pragma unroll
       for (int t = 0; t < K; ++t) lds[lane * HW + t] = s[64 * (kSumHfs + t)];
@@ -698,7 +715,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
     // the number / memory bounds leave the node open
     const uint32_t* mxw = mixw + sum_index(nb, 0, MS) + lane;
     if (any_pc && c_uni) {
+#ifdef YODA_ABL_K1_NOHC
+      const bool cnt_clk = false;
+#else
       const bool cnt_clk = valid && !uni4 && !num_none && !mem_none;
+#endif
       if (ballot(cnt_clk) != 0ull) {
         if (cnt_clk) {
           const uint32_t hm = mxw[64 * mix_hm(K)];
@@ -725,13 +746,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
     // passes: a loop over its free-ordered cards (K2 summary frees / totals, per-card models),
     // lane = node -- the smallest set's maxima, then whether a card of the largest set but
     // not the smallest raises one of them.
+#ifdef YODA_ABL_K1_NOGEN
+    const bool gen = false;
+#else
     const bool gen = valid && !one_model && feas_all && !feas_none;
+#endif
     if (ballot(gen) != 0ull) {
       if (gen) {
         const uint32_t* s2 = sum2w + sum_index(nb, 0, S2) + lane;
         bw = ck = core = mrf1 = pw = tot = 0u;  // mrf1: 1 + the free maximum (0: none)
         bool unc = false;
-#pragma unroll 1
+#pragma unroll YODA_K1_GEN_UNROLL
         for (int t = 0; t < K; ++t) {
           const uint32_t f = s2[64 * (kS2Fs + t)], cj = mxw[64 * mix_word(kMixCk, t, K)];
           const bool qs = (f >= m_max) & (cj >= c_max), ql = (f >= m_min) & (cj >= c_min);
@@ -746,7 +771,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
         qual = true;
         same = true;
         if (unc) {
-#pragma unroll 1
+#pragma unroll YODA_K1_GEN_UNROLL
           for (int t = 0; t < K; ++t) {
             const uint32_t f = s2[64 * (kS2Fs + t)], cj = mxw[64 * mix_word(kMixCk, t, K)];
             const bool d = (f >= m_min) & (cj >= c_min) & !((f >= m_max) & (cj >= c_max));
@@ -850,8 +875,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
     while (part_b) {  // mixed-model nodes: the exact per-card predicates from the record
       const int j = __builtin_ctzll(part_b);
       part_b &= part_b - 1;
+#ifdef YODA_ABL_K1_NOLEAN
+      const bool f = false;
+#else
       const bool f = k1_node_lean<K>(nodes + (size_t)(nb + (uint32_t)j) * NS, m, c, number,
                                      need_mem, need_clk, mx, nf, nz) && live;
+#endif
       const uint64_t b = ballot(f);
       set_lane(lo, hi, b, (uint32_t)j);
     }
@@ -3125,6 +3154,95 @@ __global__ __launch_bounds__(kBlock) void k_reduce3(const int64_t* __restrict__ 
     status[p] = 0;
     ties_out[p] = ties;
   }
+}
+
+// Sharded K3 (several node shards): each shard folds its chunk partials of the flagged pods
+// into one record per pod -- {best normalized score, lowest GLOBAL node reaching it, ties,
+// low := 1 if a score left [0, 100]} at rec[p] -- the records are all-gathered across the
+// shards and k_merge3 folds them (best MAX, lowest node among the shards reaching it, ties
+// summed over those, range errors OR-ed) into the picks as k_reduce3 would.
+__global__ __launch_bounds__(kBlock) void k_reduce3_rec(const int64_t* __restrict__ pbest,
+                                                        const uint32_t* __restrict__ pidx,
+                                                        const uint32_t* __restrict__ pties,
+                                                        const uint32_t* __restrict__ perr,
+                                                        uint32_t C,
+                                                        const uint32_t* __restrict__ flagged,
+                                                        const uint32_t* __restrict__ n_flagged_p,
+                                                        uint32_t max_flagged, uint32_t node_offset,
+                                                        ShardRec* __restrict__ rec) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= min(*n_flagged_p, max_flagged)) return;
+  const uint32_t p = flagged[i];
+  int64_t best = -1;
+  uint32_t idx = 0xffffffffu, ties = 0, err = 0;
+  for (uint32_t c = 0; c < C; ++c) {
+    const size_t o = (size_t)c * max_flagged + i;
+    err |= perr[o];
+    const int64_t b = pbest[o];
+    if (b < 0) continue;
+    if (b > best) {
+      best = b;
+      idx = pidx[o];
+      ties = pties[o];
+    } else if (b == best) {
+      ties += pties[o];
+    }
+  }
+  rec[p] = ShardRec{best, idx == 0xffffffffu ? idx : idx + node_offset, ties, (int64_t)err};
+}
+
+__global__ __launch_bounds__(kBlock) void k_merge3(const ShardRec* __restrict__ all,
+                                                   uint32_t n_pods, uint32_t world,
+                                                   const uint32_t* __restrict__ flagged,
+                                                   const uint32_t* __restrict__ n_flagged_p,
+                                                   uint32_t max_flagged,
+                                                   int32_t* __restrict__ pick,
+                                                   int32_t* __restrict__ status,
+                                                   uint32_t* __restrict__ ties_out) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= min(*n_flagged_p, max_flagged)) return;
+  const uint32_t p = flagged[i];
+  int64_t best = -1;
+  uint32_t idx = 0xffffffffu, ties = 0, err = 0;
+  for (uint32_t r = 0; r < world; ++r) {
+    const ShardRec x = all[(size_t)r * n_pods + p];
+    err |= x.low != 0 ? 1u : 0u;
+    if (x.best < 0) continue;
+    if (x.best > best) {
+      best = x.best;
+      idx = x.idx;
+      ties = x.ties;
+    } else if (x.best == best) {
+      idx = min(idx, x.idx);
+      ties += x.ties;
+    }
+  }
+  if (err) {
+    pick[p] = -2;
+    status[p] = 3;
+    ties_out[p] = 0;
+  } else {
+    pick[p] = (int32_t)idx;
+    status[p] = 0;
+    ties_out[p] = ties;
+  }
+}
+
+hipError_t launch_reduce3_rec(const Partials& part, uint32_t C, const uint32_t* flagged,
+                              const uint32_t* n_flagged, uint32_t max_flagged,
+                              uint32_t node_offset, ShardRec* rec, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce3_rec, pod_grid(max_flagged), dim3(kBlock), 0, s, part.best_i,
+                     part.idx, part.ties, part.err, C, flagged, n_flagged, max_flagged,
+                     node_offset, rec);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge3(const ShardRec* all, uint32_t n_pods, uint32_t world,
+                         const uint32_t* flagged, const uint32_t* n_flagged, uint32_t max_flagged,
+                         int32_t* pick, int32_t* status, uint32_t* ties, hipStream_t s) {
+  hipLaunchKernelGGL(k_merge3, pod_grid(max_flagged), dim3(kBlock), 0, s, all, n_pods, world,
+                     flagged, n_flagged, max_flagged, pick, status, ties);
+  return hipGetLastError();
 }
 
 // Bitmask [wave][node] u64 (device, yoda_layout.h) -> [P][W] u32 words (host API layout:

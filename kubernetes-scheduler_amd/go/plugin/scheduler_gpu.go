@@ -19,6 +19,7 @@ import (
 	"strconv"
 	"sync"
 	"sync/atomic"
+	"time"
 
 	scv "github.com/NJUPT-ISL/SCV/api/v1"
 	v1 "k8s.io/api/core/v1"
@@ -76,13 +77,15 @@ type SnapshotSource interface {
 type Yoda struct {
 	handle framework.Handle
 	gpu    *yodagpu.Handle
-	source SnapshotSource
+	source SnapshotSource // SCV records (Mode A); nil in Mode B
 	mode   yodagpu.Mode
 	mu     sync.Mutex // one scheduling cycle at a time uses the GPU handle
 
 	loaded     bool
 	gen        uint64   // generation of the uploaded SCV records
+	names      []string // the uploaded node order
 	alloc      []uint64 // allocated scv/memory per node as on the device
+	nodeGen    []int64  // framework.NodeInfo.Generation each alloc[i] was summed at (-1: none)
 	cardNumber []uint64
 }
 
@@ -103,12 +106,19 @@ func New(obj runtime.Object, h framework.Handle) (framework.Plugin, error) {
 		}
 	}
 	klog.V(3).Infof("yoda (GPU) plugin args: %+v", args)
-	src, err := NewInformerSource(h)
+	if args.Mode == "diskio" { // Mode B scores the snapshot's nodes: no SCV records needed
+		return NewWithSource(args, h, nil)
+	}
+	src, err := NewInformerSource(h, cacheSyncTimeout)
 	if err != nil {
 		return nil, err
 	}
 	return NewWithSource(args, h, src)
 }
+
+// cacheSyncTimeout bounds the wait for the SCV informer's first list: a missing CRD or RBAC
+// that denies list/watch then fails the plugin factory instead of hanging the scheduler.
+const cacheSyncTimeout = 60 * time.Second
 
 // NewWithSource builds the plugin over any SnapshotSource (tests, file-backed snapshots).
 func NewWithSource(args *Args, h framework.Handle, src SnapshotSource) (*Yoda, error) {
@@ -138,8 +148,9 @@ type informerSource struct {
 }
 
 // NewInformerSource watches the SCV custom resources through a dynamic shared informer
-// (the RBAC of deploy/yoda-scheduler.yaml:225-236 already grants get/list/watch on them).
-func NewInformerSource(h framework.Handle) (SnapshotSource, error) {
+// (the RBAC of deploy/yoda-scheduler.yaml:225-236 already grants get/list/watch on them).  It
+// returns an error when the informer has not synced within `timeout`.
+func NewInformerSource(h framework.Handle, timeout time.Duration) (SnapshotSource, error) {
 	dc, err := dynamic.NewForConfig(h.KubeConfig())
 	if err != nil {
 		return nil, err
@@ -155,7 +166,16 @@ func NewInformerSource(h framework.Handle) (SnapshotSource, error) {
 	})
 	stop := make(chan struct{}) // lives as long as the scheduler process
 	f.Start(stop)
-	f.WaitForCacheSync(stop)
+	wait := make(chan struct{}) // closes at the deadline: WaitForCacheSync gives up then
+	timer := time.AfterFunc(timeout, func() { close(wait) })
+	defer timer.Stop()
+	for gvr, ok := range f.WaitForCacheSync(wait) {
+		if !ok {
+			close(stop)
+			return nil, fmt.Errorf("yoda: the %s informer did not sync within %v (is the SCV CRD "+
+				"installed, and may the scheduler list/watch it?)", gvr.Resource, timeout)
+		}
+	}
 	return s, nil
 }
 
@@ -187,24 +207,58 @@ func (s *informerSource) SCVs() ([]string, []*scv.Scv, uint64, error) {
 
 // ---- the device snapshot --------------------------------------------------------------------
 
-// allocated returns, per snapshot node, the sum of the scv/memory labels of the pods the
-// scheduler's snapshot has on it -- assumed pods included, as in CalculateAllocateScore's
-// loop over nodeInfo.Pods (algorithm.go:299-303).
-func (y *Yoda) allocated(names []string) []uint64 {
+// podMemory is CalculateAllocateScore's sum for one node: the scv/memory labels of the pods
+// the scheduler's snapshot has on it, assumed pods included (algorithm.go:299-303).
+func podMemory(ni *framework.NodeInfo) uint64 {
+	var sum uint64
+	for _, pi := range ni.Pods {
+		if mem, ok := pi.Pod.GetLabels()["scv/memory"]; ok {
+			sum += filter.StrToUint64(mem) // uint64 wrap, as the reference
+		}
+	}
+	return sum
+}
+
+// allocated returns, per node of `names`, podMemory of its snapshot NodeInfo, and the
+// NodeInfo generations it was summed at.  prev/prevGen (same node order, may be nil): a node
+// whose generation did not move keeps its previous sum -- the framework bumps
+// NodeInfo.Generation on every pod added to or removed from the node, so a cycle walks the
+// pods of the changed nodes only, not every pod of the cluster.
+func (y *Yoda) allocated(names []string, prev []uint64, prevGen []int64) ([]uint64, []int64) {
 	alloc := make([]uint64, len(names))
+	gens := make([]int64, len(names))
 	infos := y.handle.SnapshotSharedLister().NodeInfos()
 	for i, n := range names {
+		gens[i] = -1
 		ni, err := infos.Get(n)
 		if err != nil {
 			continue // an SCV record without a schedulable node: nothing allocated on it
 		}
-		for _, pi := range ni.Pods {
-			if mem, ok := pi.Pod.GetLabels()["scv/memory"]; ok {
-				alloc[i] += filter.StrToUint64(mem)
-			}
+		gens[i] = ni.Generation
+		if prev != nil && prevGen[i] == ni.Generation {
+			alloc[i] = prev[i]
+			continue
+		}
+		alloc[i] = podMemory(ni)
+	}
+	return alloc, gens
+}
+
+// snapshotNodes is Mode B's node set: every node of the scheduler's snapshot (the reference's
+// Filter passes them all and PreScore scores NodeInfos().List(), scheduler.go:96-99,122).
+func (y *Yoda) snapshotNodes() ([]string, error) {
+	infos, err := y.handle.SnapshotSharedLister().NodeInfos().List()
+	if err != nil {
+		return nil, err
+	}
+	names := make([]string, 0, len(infos))
+	for _, ni := range infos {
+		if ni.Node() != nil {
+			names = append(names, ni.Node().GetName())
 		}
 	}
-	return alloc
+	sort.Strings(names)
+	return names, nil
 }
 
 // refresh brings the device snapshot up to date: a full upload when the SCV records
@@ -212,38 +266,45 @@ func (y *Yoda) allocated(names []string) []uint64 {
 // the reference's PreScore, scheduler.go:101-114); otherwise only the nodes whose allocated
 // memory moved since the last cycle (the scheduler's assumes and binds) are pushed.
 func (y *Yoda) refresh() error {
+	if y.mode == yodagpu.ModeDiskIO {
+		// Mode B: the snapshot's nodes, each with the advisor's metrics; a snapshot node the
+		// advisor does not report is the reference's nil dereference (algorithm.go:70,73)
+		names, err := y.snapshotNodes()
+		if err != nil {
+			return err
+		}
+		info, err := advisor.Result{}.Init() // advisor.go:149-265
+		if err != nil {
+			return err
+		}
+		cpu, disk := make([]float64, len(names)), make([]float64, len(names))
+		for i, n := range names {
+			ni, ok := info.Info[n]
+			if !ok {
+				return fmt.Errorf("node %q missing from the advisor's metrics", n)
+			}
+			cpu[i], disk[i] = ni.Cpu, ni.DiskIO
+		}
+		y.names = names
+		return y.gpu.UploadNodes(names, nil, nil, cpu, disk)
+	}
 	names, scvs, gen, err := y.source.SCVs()
 	if err != nil {
 		return err
 	}
-	alloc := y.allocated(names)
-	if y.mode == yodagpu.ModeDiskIO || !y.loaded || gen != y.gen {
-		var cpu, disk []float64
-		if y.mode == yodagpu.ModeDiskIO {
-			info, err := advisor.Result{}.Init() // advisor.go:149-265
-			if err != nil {
-				return err
-			}
-			cpu, disk = make([]float64, len(names)), make([]float64, len(names))
-			for i, n := range names {
-				ni, ok := info.Info[n]
-				if !ok {
-					// the reference dereferences a nil NodeInfo here (algorithm.go:70,73)
-					return fmt.Errorf("node %q missing from the advisor's metrics", n)
-				}
-				cpu[i], disk[i] = ni.Cpu, ni.DiskIO
-			}
-		}
-		if err := y.gpu.UploadNodes(names, scvs, alloc, cpu, disk); err != nil {
+	if !y.loaded || gen != y.gen {
+		alloc, gens := y.allocated(names, nil, nil)
+		if err := y.gpu.UploadNodes(names, scvs, alloc, nil, nil); err != nil {
 			return err
 		}
-		y.loaded, y.gen, y.alloc = true, gen, alloc
+		y.loaded, y.gen, y.names, y.alloc, y.nodeGen = true, gen, names, alloc, gens
 		y.cardNumber = make([]uint64, len(scvs))
 		for i, s := range scvs {
 			y.cardNumber[i] = uint64(s.Status.CardNumber)
 		}
 		return nil
 	}
+	alloc, gens := y.allocated(y.names, y.alloc, y.nodeGen)
 	var idx []uint32
 	var al, cn []uint64
 	for i := range alloc {
@@ -256,7 +317,7 @@ func (y *Yoda) refresh() error {
 	if err := y.gpu.SetNodeState(idx, al, cn); err != nil {
 		return err
 	}
-	y.alloc = alloc
+	y.alloc, y.nodeGen = alloc, gens
 	return nil
 }
 

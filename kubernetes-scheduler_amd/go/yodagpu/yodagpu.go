@@ -146,11 +146,10 @@ func (g *Handle) Close() {
 		C.yoda_destroy(g.h)
 		g.h = nil
 	}
-	for _, a := range []*cArray{&g.na.cardNumber, &g.na.freeSum, &g.na.totalSum, &g.na.alloc,
-		&g.na.free, &g.na.total, &g.na.clock, &g.na.bw, &g.na.core, &g.na.power,
-		&g.na.cardCount, &g.na.healthy, &g.na.cpu, &g.na.disk, &g.pa.hasNumber, &g.pa.hasMemory,
-		&g.pa.hasClock, &g.pa.number, &g.pa.memory, &g.pa.clock, &g.pa.priority, &g.pa.rio,
-		&g.pa.rcpu, &g.pa.pick, &g.pa.status} {
+	g.na.release()
+	for _, a := range []*cArray{&g.pa.hasNumber, &g.pa.hasMemory, &g.pa.hasClock, &g.pa.number,
+		&g.pa.memory, &g.pa.clock, &g.pa.priority, &g.pa.rio, &g.pa.rcpu, &g.pa.pick,
+		&g.pa.status} {
 		a.free()
 	}
 }
@@ -159,14 +158,52 @@ func (g *Handle) Close() {
 // struct-of-arrays of yoda_node_soa and uploads them.  allocMemory[i] is the sum of the
 // scv/memory labels of pods already on node i (score.CalculateAllocateScore's loop,
 // algorithm.go:299-303); cpu/diskIO are advisor.NodeInfo values (Mode B, may be nil).
+// scvs == nil: nodes without SCV records (Mode B, which reads none of them).
 func (g *Handle) UploadNodes(names []string, scvs []*scv.Scv, allocMemory []uint64,
 	cpu, diskIO []float64) error {
-	n := len(scvs)
-	if len(names) != n || (allocMemory != nil && len(allocMemory) != n) {
+	return g.UploadShard(names, scvs, allocMemory, cpu, diskIO, 0)
+}
+
+// UploadShard is UploadNodes for one node shard of a multi-GPU snapshot: offset is the global
+// index of names[0] (picks and node ids are global; see CommInit).
+func (g *Handle) UploadShard(names []string, scvs []*scv.Scv, allocMemory []uint64,
+	cpu, diskIO []float64, offset uint32) error {
+	n := len(names)
+	if (scvs != nil && len(scvs) != n) || (allocMemory != nil && len(allocMemory) != n) {
 		return errors.New("yodagpu: names/allocMemory do not match the SCV list")
 	}
+	if scvs == nil {
+		scvs = make([]*scv.Scv, n)
+		for i := range scvs {
+			scvs[i] = &scv.Scv{}
+		}
+	}
+	soa, zero, err := g.na.pack(scvs, allocMemory, cpu, diskIO)
+	if err != nil {
+		return err
+	}
+	// &soa is a Go pointer to memory holding only C pointers: allowed
+	if err := check(g.h, C.yoda_upload_nodes(g.h, &soa, C.uint32_t(offset), 0),
+		"yoda_upload_nodes"); err != nil {
+		return err
+	}
+	g.nodes = names
+	g.zeroTotal = zero
+	g.index = make(map[string]int, len(names))
+	for i, name := range names {
+		g.index[name] = i
+	}
+	return nil
+}
+
+// pack fills the C-side arrays of yoda_node_soa from the SCV records; zero[i]: node i has
+// TotalMemorySum == 0.
+func (a *nodeArrays) pack(scvs []*scv.Scv, allocMemory []uint64, cpu, diskIO []float64) (
+	C.yoda_node_soa, []bool, error) {
+	n := len(scvs)
 	if (cpu == nil) != (diskIO == nil) || (cpu != nil && (len(cpu) != n || len(diskIO) != n)) {
-		return errors.New("yodagpu: cpu/diskIO must both be nil or both have one value per node")
+		return C.yoda_node_soa{}, nil,
+			errors.New("yodagpu: cpu/diskIO must both be nil or both have one value per node")
 	}
 	k := 1
 	for _, s := range scvs {
@@ -175,9 +212,8 @@ func (g *Handle) UploadNodes(names []string, scvs []*scv.Scv, allocMemory []uint
 		}
 	}
 	if k > C.YODA_MAX_CARDS {
-		return errors.New("yodagpu: more than YODA_MAX_CARDS cards on a node")
+		return C.yoda_node_soa{}, nil, errors.New("yodagpu: more than YODA_MAX_CARDS cards on a node")
 	}
-	a := &g.na
 	cardNumber, cardCount := u64s(&a.cardNumber, n), u32s(&a.cardCount, n)
 	freeSum, totalSum, alloc := u64s(&a.freeSum, n), u64s(&a.totalSum, n), u64s(&a.alloc, n)
 	free, total, clock := u64s(&a.free, n*k), u64s(&a.total, n*k), u64s(&a.clock, n*k)
@@ -226,17 +262,14 @@ func (g *Handle) UploadNodes(names []string, scvs []*scv.Scv, allocMemory []uint
 		soa.cpu = (*C.double)(a.cpu.p)
 		soa.disk_io = (*C.double)(a.disk.p)
 	}
-	// &soa is a Go pointer to memory holding only C pointers: allowed
-	if err := check(g.h, C.yoda_upload_nodes(g.h, &soa, 0, 0), "yoda_upload_nodes"); err != nil {
-		return err
+	return soa, zero, nil
+}
+
+func (a *nodeArrays) release() {
+	for _, x := range []*cArray{&a.cardNumber, &a.freeSum, &a.totalSum, &a.alloc, &a.free,
+		&a.total, &a.clock, &a.bw, &a.core, &a.power, &a.cardCount, &a.healthy, &a.cpu, &a.disk} {
+		x.free()
 	}
-	g.nodes = names
-	g.zeroTotal = zero
-	g.index = make(map[string]int, len(names))
-	for i, name := range names {
-		g.index[name] = i
-	}
-	return nil
 }
 
 // SetNodeState updates the allocated scv/memory (and CardNumber) of a few nodes on the
@@ -347,6 +380,77 @@ func (g *Handle) Greedy(pods []*v1.Pod, mode Mode, cardCapacity bool) ([]int32, 
 	}
 	rc := C.yoda_greedy(g.h, &s, C.int(mode), flags, (*C.int32_t)(unsafe.Pointer(&picks[0])))
 	return picks, check(g.h, rc, "yoda_greedy")
+}
+
+// ---- several GPUs: libyoda's own RCCL exchange (include/yoda.h yoda_comm_*) --------------
+
+// CommUniqueID makes the communicator id on rank 0; hand it to the other ranks out of band
+// (a file, a ConfigMap, the k8s API ...).
+func CommUniqueID() ([]byte, error) {
+	id := make([]byte, C.YODA_COMM_ID_BYTES)
+	if err := check(nil, C.yoda_comm_unique_id((*C.uint8_t)(unsafe.Pointer(&id[0]))),
+		"yoda_comm_unique_id"); err != nil {
+		return nil, err
+	}
+	return id, nil
+}
+
+// CommInit joins this handle (one GPU holding the node shard uploaded with UploadShard) to the
+// communicator of `world` ranks; collective: every rank calls it.
+func (g *Handle) CommInit(id []byte, rank, world int) error {
+	if len(id) != C.YODA_COMM_ID_BYTES {
+		return errors.New("yodagpu: communicator id of the wrong size")
+	}
+	return check(g.h, C.yoda_comm_init(g.h, (*C.uint8_t)(unsafe.Pointer(&id[0])), C.int(rank),
+		C.int(world)), "yoda_comm_init")
+}
+
+// ShardedBatch schedules the pods against the node shards of every rank (collective: every
+// rank passes the same pods): yoda_comm_run's maxima / packed-key all-reduces.  Picks are
+// global node indices.
+func (g *Handle) ShardedBatch(pods []*v1.Pod, mode Mode) (picks []int32, statuses []int32, err error) {
+	if len(pods) == 0 {
+		return nil, nil, nil
+	}
+	s := g.packPods(pods)
+	n := len(pods)
+	if err = check(g.h, C.yoda_upload_pods(g.h, &s), "yoda_upload_pods"); err != nil {
+		return nil, nil, err
+	}
+	if err = check(g.h, C.yoda_comm_run(g.h, C.int(mode)), "yoda_comm_run"); err != nil {
+		return nil, nil, err
+	}
+	pk, st := i32s(&g.pa.pick, n), i32s(&g.pa.status, n)
+	out := C.yoda_eval_out{pick: (*C.int32_t)(g.pa.pick.p), status: (*C.int32_t)(g.pa.status.p)}
+	if err = check(g.h, C.yoda_download(g.h, &out), "yoda_download"); err != nil {
+		return nil, nil, err
+	}
+	return append([]int32(nil), pk...), append([]int32(nil), st...), nil
+}
+
+// ShardedGreedy is Greedy across the ranks' node shards (collective; every rank passes the
+// same pods and the same full snapshot `all`, which the host-side resolve reads): the windows'
+// maxima and candidate lists merged over RCCL inside libyoda (yoda_comm_greedy).
+func (g *Handle) ShardedGreedy(all []*scv.Scv, allAlloc []uint64, pods []*v1.Pod, mode Mode,
+	cardCapacity bool) ([]int32, error) {
+	if len(pods) == 0 {
+		return nil, nil
+	}
+	var full nodeArrays // the full snapshot's C arrays (host only)
+	defer full.release()
+	soa, _, err := full.pack(all, allAlloc, nil, nil)
+	if err != nil {
+		return nil, err
+	}
+	s := g.packPods(pods)
+	picks := make([]int32, len(pods))
+	flags := C.uint32_t(0)
+	if cardCapacity {
+		flags = C.YODA_GREEDY_CARD_CAPACITY
+	}
+	rc := C.yoda_comm_greedy(g.h, &soa, &s, C.int(mode), flags,
+		(*C.int32_t)(unsafe.Pointer(&picks[0])))
+	return picks, check(g.h, rc, "yoda_comm_greedy")
 }
 
 // NodeIndex maps a node name to its row position.

@@ -56,6 +56,12 @@ _SIGS = {
     "yoda_shard_prepare_merge": ([_vp, _vp, _vp, _vp, _vp], C.c_int),
     "yoda_shard_finalize": ([_vp, C.c_int, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "yoda_shard_overflow_count": ([_vp, C.POINTER(C.c_uint32)], C.c_int),
+    "yoda_shard_exact_records": ([_vp, _vp], C.c_int),
+    "yoda_shard_exact_merge": ([_vp, _vp, C.c_int], C.c_int),
+    "yoda_comm_greedy": ([_vp, C.POINTER(CNodeSoA), C.POINTER(CPodSoA), C.c_int, _u32,
+                          C.POINTER(C.c_int32)], C.c_int),
+    "yoda_comm_greedy_local": ([_vp, C.c_int, C.POINTER(CNodeSoA), C.POINTER(CPodSoA), C.c_int,
+                                _u32, C.POINTER(C.c_int32)], C.c_int),
     "yoda_profile": ([_vp, C.c_int], C.c_int),
     "yoda_set_pod_order": ([_vp, C.c_int], C.c_int),
     "yoda_order_info": ([_vp, _vp], C.c_int),
@@ -417,6 +423,30 @@ class Yoda:
                     "yoda_shard_best_one")
         return s.value, n.value
 
+    def shard_overflow_count(self) -> int:
+        """Pods of the last (sharded) finalize whose NormalizeScore needs the exact path."""
+        n = C.c_uint32()
+        self._check(lib().yoda_shard_overflow_count(self._h, C.byref(n)),
+                    "yoda_shard_overflow_count")
+        return n.value
+
+    def shard_exact_records(self, d_rec: int):
+        self._check(lib().yoda_shard_exact_records(self._h, _vp(d_rec)), "yoda_shard_exact_records")
+
+    def shard_exact_merge(self, d_all: int, world: int):
+        self._check(lib().yoda_shard_exact_merge(self._h, _vp(d_all), world),
+                    "yoda_shard_exact_merge")
+
+    def comm_greedy(self, all_nodes, pods, mode: int = 0, flags: int = 0) -> np.ndarray:
+        """yoda_comm_greedy: the greedy batch over the ranks' node shards (collective)."""
+        n, p = all_nodes.normalized(), pods.normalized()
+        cn, cp = n.c(), p.c()
+        pick = np.full(p.n_pods, -3, np.int32)
+        self._check(lib().yoda_comm_greedy(self._h, C.byref(cn), C.byref(cp), mode, flags,
+                                           pick.ctypes.data_as(C.POINTER(C.c_int32))),
+                    "yoda_comm_greedy")
+        return pick
+
     def shard_finalize(self, mode, d_counts, d_best, d_idx, d_ties, d_lowest):
         self._check(lib().yoda_shard_finalize(self._h, mode, _vp(d_counts), _vp(d_best),
                                               _vp(d_idx), _vp(d_ties), _vp(d_lowest)),
@@ -440,6 +470,21 @@ def comm_run_local(handles, mode: int = 0):
     if rc != 0:
         raise YodaError(f"yoda_comm_run_local: {ERRORS.get(rc, rc)}: "
                         f"{lib().yoda_last_error(handles[0]._h).decode()}")
+
+
+def comm_greedy_local(handles, all_nodes, pods, mode: int = 0, flags: int = 0) -> np.ndarray:
+    """yoda_comm_greedy_local: the libyoda sharded greedy over several shard handles of this
+    process on one device (in-process transport)."""
+    n, p = all_nodes.normalized(), pods.normalized()
+    cn, cp = n.c(), p.c()
+    pick = np.full(p.n_pods, -3, np.int32)
+    arr = (C.c_void_p * len(handles))(*[h._h for h in handles])
+    rc = lib().yoda_comm_greedy_local(arr, len(handles), C.byref(cn), C.byref(cp), mode, flags,
+                                      pick.ctypes.data_as(C.POINTER(C.c_int32)))
+    if rc != 0:
+        raise YodaError(f"yoda_comm_greedy_local: {ERRORS.get(rc, rc)}: "
+                        f"{lib().yoda_last_error(handles[0]._h).decode()}")
+    return pick
 
 
 def topk_k() -> int:

@@ -99,6 +99,19 @@ class Reducer:
         for t in ts:
             dist.all_reduce(t, op=rop, group=self.group)
 
+    def gather_tensors(self, ts: Sequence[torch.Tensor]) -> List[torch.Tensor]:
+        """All-gather of one device tensor per local shard -> for each local shard, the
+        concatenation of every shard's tensor in rank order."""
+        if self.local:
+            cat = torch.cat(list(ts))
+            return [cat for _ in ts]
+        import torch.distributed as dist
+        t = ts[0]
+        out = torch.empty(dist.get_world_size(self.group) * t.numel(), dtype=t.dtype,
+                          device=t.device)
+        dist.all_gather_into_tensor(out, t, group=self.group)
+        return [out]
+
     def gather(self, arrays: Sequence[np.ndarray]) -> List[np.ndarray]:
         """All-gather of one float64 array per local shard -> every shard's array (rank order).
         Local mode: the arrays themselves.  RCCL needs device tensors, gloo host tensors."""
@@ -284,6 +297,18 @@ class ShardExchange:
             merge_phase2(self.reduce, self.bufs, lambda b: self._prepare(hb[id(b)], b))
         for h, b in zip(self.handles, self.bufs):
             h.shard_finalize(mode, p(b.counts), p(b.best_g), p(b.idx), p(b.ties), p(b.lowest))
+        if scv and self.handles[0].generic and self.handles[0].shard_overflow_count():
+            # U64 pods whose NormalizeScore can overflow int64 (scheduler.go:176-179): every
+            # shard's exact-normalize records all-gathered, then merged (the same pods are
+            # flagged on every shard: the flags read only the reduced buffers)
+            recs = [torch.empty(24 * max(h.n_pods, 1), dtype=torch.uint8, device=self.device)
+                    for h in self.handles]
+            for h, r in zip(self.handles, recs):
+                h.shard_exact_records(r.data_ptr())
+            world = (len(self.handles) if self.reduce.local
+                     else torch.distributed.get_world_size(self.reduce.group))
+            for h, a in zip(self.handles, self.reduce.gather_tensors(recs)):
+                h.shard_exact_merge(a.data_ptr(), world)
 
     def run(self, mode: int) -> EvalResult:
         self.step(mode)
@@ -464,9 +489,6 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
     `shards`: this process's shards (HandleShard); `nodes`: the FULL snapshot.  The shards'
     node state is restored at the end."""
     from .capi import GreedySession, topk_k
-    if any(s.generic for s in shards):
-        raise ValueError("sharded greedy needs a fast record path (N32/F64); the U64 path is "
-                         "served by the single-handle yoda_greedy")
     k = topk_k()
     gs = GreedySession(nodes, pods, flags)
     order = gs.queue_order()
@@ -481,8 +503,24 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
                 s.set_node_state(n, a, c)
 
     windows = exact = restarts = 0
+    generic = any(s.generic for s in shards)
     try:
-        if capacity:
+        if generic:
+            # the U64 record path has no candidate lists: every pod in queue order is one exact
+            # sharded step (ShardExchange) against the current node state
+            ex = ShardExchange([s.h for s in shards], reduce, shards[0].device, path_code=2)
+            from .soa import MODE_SCV
+            ex.bufs = [ShardBuffers(1, shards[0].device) for _ in shards]
+            for q in range(P):
+                push()
+                one = pods.take(order[q:q + 1])
+                for s in shards:
+                    s.upload_pods(one)
+                ex.step(MODE_SCV)
+                gs.assign(q, int(shards[0].h.download_picks()[0][0]))
+                exact += 1
+            push()
+        if capacity and not generic:
             ws, Wc = 0, W
             while ws < P:
                 wn = min(Wc, P - ws)
@@ -508,7 +546,7 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
                 else:
                     ws += wn
                     Wc = min(W, 2 * Wc)
-        for ws in (range(0, P, W) if not capacity else ()):
+        for ws in (range(0, P, W) if not capacity and not generic else ()):
             wn = min(W, P - ws)
             push()
             win = pods.take(order[ws:ws + wn])
