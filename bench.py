@@ -82,8 +82,8 @@ def cpu_model() -> str:
 
 def kernel_names(path: str, mode: int):
     """(K1, K2) kernel names of a record path, as rocprofv3 / tools/pmc_summary.py name them."""
-    if mode == MODE_DISKIO:
-        return "k_fill_diskio_state", "k2_diskio"
+    if mode == MODE_DISKIO:  # the batch path (lane = class; lane = node for <= 64 classes)
+        return "k_fill_diskio_state", "k2b_class_lanes"
     return {"n32": ("k1_block_n32", "k2_block_n32"),
             "f64": ("k1_filter_maxima", "k2_score"),
             "u64": ("k1_filter_maxima", "k2_score_generic")}[path]
@@ -332,56 +332,66 @@ def row_latency(dev_index: int, node_counts=(5000, 100000), cycles: int = 60) ->
     return out
 
 
+def diskio_classes(pods) -> int:
+    """Distinct Mode-B pod classes of a batch: (alpha, beta) bit pairs (algorithm.go:105-106,
+    the grouping libyoda's Mode-B batch path evaluates once per class)."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        beta = 1.0 / (1.0 + pods.rcpu.astype(np.float64) / pods.rio)
+    alpha = 1 - beta
+    key = np.stack([alpha.view(np.uint64), beta.view(np.uint64)], axis=1)
+    return int(np.unique(key, axis=0).shape[0])
+
+
 def disclosure(y, nodes, pods, step, barrier, args) -> dict:
-    """What the headline depends on, measured after the timed region on
-    the same GPU: the block kernels' work classes for this batch (device counters), the step
-    time of the per-pair kernels on the same workload, of a variant whose nodes mix GPU models
-    (half the nodes, so the one-model shortcuts apply less), and of the F64 record path
-    (memory fields in bytes instead of MiB)."""
+    """What the headline depends on, measured after the
+    timed region on the same GPU: the block kernels' work classes for this batch (device
+    counters), the per-pair kernels on the same workload, and the workloads the headline does
+    not cover (synth.VARIANTS): mixed-model nodes, memory in bytes, the U64 record path,
+    config 4 at its declared size and at 100k x 100k, and Mode B with the pods as generated
+    and with a distinct request per pod -- each with its K1/K2 HIP-event times and class
+    fractions."""
     out = {}
     y.class_stats(True)
     step()
     barrier()
     y.class_stats(False)
     out["classes"] = y.class_stats()
-    P, N = pods.n_pods, nodes.n_nodes
-    variants = {}
-    rng = np.random.default_rng(12)
-    copy = lambda soa: type(soa)(**{f: np.array(getattr(soa, f))  # noqa: E731
-                                    for f in soa.__dataclass_fields__})
-    mixed = copy(nodes)
-    pick = rng.random(N) < 0.5
-    k = mixed.card_clock.shape[1]
-    models = rng.integers(0, 3, size=(int(pick.sum()), k))
-    real = np.arange(k)[None, :] < mixed.card_count[pick][:, None]
-    for arr, table in ((mixed.card_clock, synth.CLOCKS), (mixed.card_bandwidth, synth.BANDWIDTHS),
-                       (mixed.card_core, synth.CORES), (mixed.card_power, synth.POWERS)):
-        arr[pick] = np.where(real, table[models], 0)
-    mib = 1 << 20
-    f64n = copy(nodes)
-    for f in ("card_free_memory", "card_total_memory", "free_memory_sum", "total_memory_sum",
-              "alloc_memory"):
-        setattr(f64n, f, getattr(f64n, f) * np.uint64(mib))
-    f64p = copy(pods)
-    f64p.memory = f64p.memory * np.uint64(mib)
-    cases = (("per_pair_kernels", nodes, pods, dict(per_node_k1=True, per_node_k2=True)),
-             ("mixed_model_nodes_50pct", mixed.normalized(), pods, {}),
-             ("f64_path_memory_in_bytes", f64n.normalized(), f64p.normalized(), {}))
     dev_index = torch.cuda.current_device()
-    for name, nd, pd, kw in cases:
+    variants = {}
+
+    def timed(name, nd, pd, mode, kw, steps):
         z = Yoda(dev_index)
         z.upload_nodes(nd, **kw)
         z.upload_pods(pd)
         z.set_stream(torch.cuda.current_stream().cuda_stream)
-        ms = _timed_steps(lambda: z.run(MODE_SCV), barrier, 3)
-        variants[name] = {"ms_per_step": ms, "pairs_per_s": P * N / (ms / 1e3), "path": z.path}
-        if name == "mixed_model_nodes_50pct":
+        z.run(mode)
+        barrier()
+        z.profile(True)
+        ms = _timed_steps(lambda: z.run(mode), barrier, steps)
+        z.profile(False)
+        k1, k2, nl = z.profile_read()
+        v = {"desc": synth.VARIANTS.get(name, name), "pods": pd.n_pods, "nodes": nd.n_nodes,
+             "mode": "diskio" if mode == MODE_DISKIO else "scv", "path": z.path,
+             "ms_per_step": ms, "pairs_per_s": pd.n_pods * nd.n_nodes / (ms / 1e3),
+             "k1_ms": k1 / max(nl, 1), "k2_ms": k2 / max(nl, 1)}
+        if mode == MODE_SCV and z.path == "n32":
             z.class_stats(True)
-            z.run(MODE_SCV)
+            z.run(mode)
             barrier()
             z.class_stats(False)
-            variants[name]["classes"] = z.class_stats()
+            v["classes"] = z.class_stats()
+        if mode == MODE_DISKIO:
+            v["pod_classes"] = diskio_classes(pd)
+            # K2B: 16 B of node record per node and class, 24 B out per pod; f64 work per pair
+            v["k2b_unique_bytes"] = nd.n_nodes * 16 + pd.n_pods * 24
+        variants[name] = v
         z.close()
+
+    timed("per_pair_kernels", nodes, pods, MODE_SCV, dict(per_node_k1=True, per_node_k2=True), 3)
+    variants["per_pair_kernels"]["desc"] = "config 3 on the per-pair kernels (no block classes)"
+    for name, nd, pd, mode, kw in synth.variant_workloads(
+            ["mixed50", "bytes", "u64", "c4", "het100k", "diskio", "diskio_distinct"]):
+        timed(name, nd, pd, mode, kw, 3 if name == "u64" else 5)
     out["variants"] = variants
     out["plugin_row_latency"] = row_latency(dev_index)
     return out

@@ -47,6 +47,14 @@ hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigne
 hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
                             uint32_t C, const PodParams& pp, uint32_t n_pods, const Partials& part,
                             int64_t* rows, hipStream_t s);
+DiskPlan diskio_plan(uint32_t n_nodes, uint32_t n_cls);
+hipError_t launch_k2b(const NodeRecB* nodes, uint32_t n_nodes, const double* cab,
+                      uint32_t n_cls, const DiskLevels& lv, const DiskPlan& pl, uint32_t* plc,
+                      uint32_t* pidx, hipStream_t s);
+hipError_t launch_reduce2b(const uint32_t* plc, const uint32_t* pidx, uint32_t C, uint32_t n_cls,
+                           const uint32_t* cls, uint32_t n_pods, uint32_t node_offset,
+                           int64_t* best, uint32_t* idx, uint32_t* ties, int64_t* low,
+                           hipStream_t s);
 hipError_t launch_rows_transpose(const int64_t* in, uint32_t n_nodes, uint32_t n_pods,
                                  const uint32_t* perm,
                                  int64_t* out, hipStream_t s);
@@ -388,6 +396,12 @@ struct yoda_handle {
   // until the shards' records are merged (yoda_shard_exact_merge)
   DevBuf k3rec, k3all;
   bool k3_pending = false;
+  // Mode B batch path: the batch's pod classes (distinct (alpha, beta) bit pairs), built on
+  // the first Mode B run after an upload: device [2][D] f64 (alpha, beta) + [P] u32 class
+  // of each pod; chunk partials [2][C][D] u32
+  bool b_cls_ready = false;
+  uint32_t b_ncls = 0;
+  DevBuf b_cab, b_cls, b_part;
   uint32_t k3_nfl = 0;
   // profiling: event pairs around K1 / K2
   bool profiling = false;
@@ -419,7 +433,7 @@ struct yoda_handle {
                      &p_low_i,   &p_err,     &pick_alt,   &status_alt,   &ties_out_alt,
                      &p_wit,     &wit,       &stats_dev, &one_feas,  &one_part,  &one_done,
                      &ex1,       &rec,       &rec_all,   &cg_max,    &cg_cnt,    &cg_wit,    &cg_gather, &k3rec,     &k3all,
-                     &one_out,
+                     &one_out,   &b_cab,     &b_cls,     &b_part,
                      &counts_alt, &best_alt, &maxima_alt};
     for (DevBuf* b : all) b->release();
     pod_stage.release();
@@ -755,6 +769,76 @@ int unpermute_outputs(yoda_t* h) {
   return YODA_OK;
 }
 
+// Mode B score levels (yoda_layout.h DiskLevels): t[k] = the largest |d| >= 0 whose score
+// trunc(10 - 10*|d|) (algorithm.go:110-111, no FMA: this file builds with -ffp-contract=off)
+// is >= k, by bisection over the bit patterns of the non-negative doubles (ordered like their
+// values); the score is non-increasing in |d|, so the set is [0, t[k]].
+static double diskio_score(double l) {
+  volatile double t = 10.0 * l;
+  volatile double s = 10.0 - t;
+  return s >= 1.0 ? std::trunc((double)s) : 0.0;
+}
+
+static const DiskLevels& diskio_levels() {
+  static const DiskLevels lv = [] {
+    DiskLevels d{};
+    d.t[0] = HUGE_VAL;
+    d.t[11] = -1.0;
+    for (int k = 1; k <= 10; ++k) {
+      uint64_t lo = 0, hi = 0x7ff0000000000000ull;  // score(+0) = 10 >= k, score(inf) = 0 < k
+      while (hi - lo > 1) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        double x;
+        std::memcpy(&x, &mid, 8);
+        if (diskio_score(x) >= (double)k) lo = mid; else hi = mid;
+      }
+      std::memcpy(&d.t[k], &lo, 8);
+    }
+    return d;
+  }();
+  return lv;
+}
+
+// The batch's Mode B pod classes, from the staged (alpha, beta) of the last upload: pods with
+// bit-identical (alpha, beta) score every node alike (algorithm.go:105-111).
+int ensure_diskio_classes(yoda_t* h) {
+  if (h->b_cls_ready) return YODA_OK;
+  const uint32_t P = h->n_pods;
+  const unsigned char* st = static_cast<const unsigned char*>(h->pod_stage.p);
+  const uint64_t* al = reinterpret_cast<const uint64_t*>(st + h->pod_off[kPodAlpha]);
+  const uint64_t* be = reinterpret_cast<const uint64_t*>(st + h->pod_off[kPodBeta]);
+  size_t cap = 64;
+  while (cap < 2 * (size_t)P) cap <<= 1;
+  std::vector<uint32_t> slot(cap, 0xffffffffu);  // class id, or empty
+  std::vector<uint64_t> ca, cb;
+  std::vector<uint32_t> cls(P);
+  for (uint32_t p = 0; p < P; ++p) {
+    const uint64_t a = al[p], b = be[p];
+    size_t i = (size_t)((a * 0x9e3779b97f4a7c15ull ^ b * 0xc2b2ae3d27d4eb4full) >> 20) & (cap - 1);
+    while (slot[i] != 0xffffffffu && !(ca[slot[i]] == a && cb[slot[i]] == b)) i = (i + 1) & (cap - 1);
+    if (slot[i] == 0xffffffffu) {
+      slot[i] = (uint32_t)ca.size();
+      ca.push_back(a);
+      cb.push_back(b);
+    }
+    cls[p] = slot[i];
+  }
+  const uint32_t D = (uint32_t)ca.size();
+  std::vector<uint64_t> cab(2 * (size_t)D);
+  std::copy(ca.begin(), ca.end(), cab.begin());
+  std::copy(cb.begin(), cb.end(), cab.begin() + D);
+  HIP_TRY(h, h->b_cab.ensure(std::max<size_t>(cab.size(), 1) * 8));
+  HIP_TRY(h, h->b_cls.ensure(std::max<size_t>(P, 1) * 4));
+  HIP_TRY(h, hipMemcpyAsync(h->b_cab.p, cab.data(), cab.size() * 8, hipMemcpyHostToDevice,
+                            h->stream));
+  HIP_TRY(h, hipMemcpyAsync(h->b_cls.p, cls.data(), (size_t)P * 4, hipMemcpyHostToDevice,
+                            h->stream));
+  HIP_TRY(h, hipStreamSynchronize(h->stream));  // the host vectors go out of scope
+  h->b_ncls = D;
+  h->b_cls_ready = true;
+  return YODA_OK;
+}
+
 // Phase 1: Filter + PreScore maxima (Mode A), or the all-feasible state (Mode B).
 // final_maxima: this handle's maxima are the run's (no exchange follows).
 int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_maxima = false) {
@@ -857,6 +941,29 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
   if (mode == YODA_MODE_SCV && !h->generic && !h->rcp_ready)
     HIP_TRY(h, launch_prep2(maxima, P, h->rcp.as<double>(), h->rcp32.as<float>(), h->stream));
   h->rcp_ready = false;
+  if (mode == YODA_MODE_DISKIO && !rows) {
+    // batch path: over the batch's pod classes, then each pod takes its class's outcome
+    // (Mode B runs are never reordered: P == n_pods, caller order)
+    int rc = ensure_diskio_classes(h);
+    if (rc) return rc;
+    if ((uint64_t)h->n_nodes >> kDiskCountBits)
+      return fail(h, YODA_ERR_INVALID_ARG, "Mode B batch: more than 2^28 nodes");
+    const uint32_t D = h->b_ncls;
+    const DiskPlan pl = diskio_plan(h->n_nodes, D);
+    HIP_TRY(h, h->b_part.ensure(2 * (size_t)pl.C * D * 4));
+    uint32_t* plc = h->b_part.as<uint32_t>();
+    uint32_t* pix = plc + (size_t)pl.C * D;
+    if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
+    HIP_TRY(h, launch_k2b(h->nodes_b.as<NodeRecB>(), h->n_nodes, h->b_cab.as<double>(), D,
+                          diskio_levels(), pl, plc, pix, h->stream));
+    if (e1) {
+      HIP_TRY(h, hipEventRecord(e1, h->stream));
+      h->ev_k2.emplace_back(e0, e1);
+    }
+    HIP_TRY(h, launch_reduce2b(plc, pix, pl.C, D, h->b_cls.as<uint32_t>(), P, h->node_offset,
+                               best, idx, ties, low, h->stream));
+    return YODA_OK;
+  }
   if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
   if (mode == YODA_MODE_DISKIO) {
     HIP_TRY(h, launch_k2_diskio(h->nodes_b.as<NodeRecB>(), h->n_nodes, h->chunk2, h->C2,
@@ -1457,6 +1564,7 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
                   !pd->has_clock || !pd->clock))
       return fail(h, YODA_ERR_INVALID_ARG, "a required pod array is NULL");
     h->topk_ready = false;
+    h->b_cls_ready = false;
     HIP_TRY(h, hipSetDevice(h->device));
     // One blob of per-pod arrays, staged in pinned memory and sent with ONE copy.
     size_t off[kPodArrays], total = 0;

@@ -2875,6 +2875,205 @@ __global__ __launch_bounds__(kBlock) void k2_diskio(const NodeRecB* __restrict__
   plow[o] = low;
 }
 
+// ---------------------------------------------------------------------------------------
+// K2B batch path (Mode B): the same score over pod CLASSES -- the distinct
+// (alpha, beta) bit pairs of the batch (algorithm.go:105-106).  Pods of one class score every
+// node alike, so their outcome is the class's.  Per pair: a = alpha*V, b = beta*U, d = a - b
+// (:109), and the level of |d| against DiskLevels (score >= k <=> |d| <= t[k]): three f64
+// operations, two compares.  A lane keeps, over nodes in increasing order, the best level
+// seen, its node count and its first (lowest) node; level 0 counts nothing while running
+// (every node is >= 0, NaN included) and is settled at the end.
+struct DiskAcc {
+  uint32_t lev, cnt, idx;
+  double tc, tu;  // count threshold of the current level (-1 at level 0), the next level's
+};
+
+__device__ __forceinline__ void disk_init(DiskAcc& s, const double* lv) {
+  s.lev = 0;
+  s.cnt = 0;
+  s.idx = 0xffffffffu;
+  s.tc = -1.0;
+  s.tu = lv[1];
+}
+
+__device__ __forceinline__ void disk_step(DiskAcc& s, double ad, uint32_t n, const double* lv) {
+  s.cnt += (ad <= s.tc) ? 1u : 0u;
+  if (ad <= s.tu) {  // a higher level (rare once the first nodes are seen)
+    uint32_t L = 1;  // the levels are nested: |d| <= t[k] for every k up to its level
+#pragma unroll
+    for (int k = 2; k <= 10; ++k) L += (ad <= lv[k]) ? 1u : 0u;
+    s.lev = L;
+    s.cnt = 1;
+    s.idx = n;
+    s.tc = lv[L];
+    s.tu = lv[L + 1];
+  }
+}
+
+// Lane = class: each lane runs CPL classes over the chunk's nodes, one node record per
+// iteration read by a scalar (wave-uniform) load.
+template <int CPL>
+__global__ __launch_bounds__(kBlock) void k2b_class_lanes(const NodeRecB* __restrict__ nodes,
+                                                          uint32_t n_nodes, uint32_t chunk_nodes,
+                                                          const double* __restrict__ cab,
+                                                          uint32_t n_cls, DiskLevels lvs,
+                                                          uint32_t* __restrict__ plc,
+                                                          uint32_t* __restrict__ pidx) {
+#pragma clang fp contract(off)
+  __shared__ double lv[12];
+  if (threadIdx.x < 12) lv[threadIdx.x] = lvs.t[threadIdx.x];
+  __syncthreads();
+  const uint32_t chunk = blockIdx.y;
+  const uint32_t n0 = chunk * chunk_nodes;
+  const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
+  const uint32_t c0 = blockIdx.x * (kBlock * CPL) + threadIdx.x;
+  double al[CPL], be[CPL];
+  DiskAcc s[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const uint32_t c = c0 + j * kBlock;
+    al[j] = c < n_cls ? cab[c] : 0.0;
+    be[j] = c < n_cls ? cab[(size_t)n_cls + c] : 0.0;
+    disk_init(s[j], lv);
+  }
+  // 8 node records per trip: the scalar loads are issued together, one wait per trip
+  constexpr int kTrip = 8;
+  uint32_t n = n0;
+  for (; n + kTrip <= n1; n += kTrip) {
+    NodeRecB r[kTrip];
+#pragma unroll
+    for (int i = 0; i < kTrip; ++i) r[i] = nodes[n + i];
+#pragma unroll
+    for (int i = 0; i < kTrip; ++i) {
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        const double a = al[j] * r[i].v;
+        const double b = be[j] * r[i].u;
+        disk_step(s[j], fabs(a - b), n + i, lv);
+      }
+    }
+  }
+  for (; n < n1; ++n) {
+    const NodeRecB r = nodes[n];
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const double a = al[j] * r.v;
+      const double b = be[j] * r.u;
+      disk_step(s[j], fabs(a - b), n, lv);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const uint32_t c = c0 + j * kBlock;
+    if (c >= n_cls) continue;
+    uint32_t cnt = s[j].cnt, idx = s[j].idx;
+    if (s[j].lev == 0u) {
+      cnt = n1 - n0;
+      idx = n0;
+    }
+    plc[(size_t)chunk * n_cls + c] = (s[j].lev << kDiskCountBits) | cnt;
+    pidx[(size_t)chunk * n_cls + c] = idx;
+  }
+}
+
+// Lane = node, one class per workgroup (batches of few classes, e.g. one pod spec): each
+// thread strides over the chunk's nodes, then the workgroup merges (max level; at it, count
+// sum and lowest node).
+__global__ __launch_bounds__(kBlock) void k2b_node_lanes(const NodeRecB* __restrict__ nodes,
+                                                         uint32_t n_nodes, uint32_t chunk_nodes,
+                                                         const double* __restrict__ cab,
+                                                         uint32_t n_cls, DiskLevels lvs,
+                                                         uint32_t* __restrict__ plc,
+                                                         uint32_t* __restrict__ pidx) {
+#pragma clang fp contract(off)
+  __shared__ double lv[12];
+  __shared__ uint32_t red[3][kBlock / kWave];
+  if (threadIdx.x < 12) lv[threadIdx.x] = lvs.t[threadIdx.x];
+  __syncthreads();
+  const uint32_t chunk = blockIdx.x, c = blockIdx.y;
+  const uint32_t n0 = chunk * chunk_nodes;
+  const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
+  const double al = cab[c], be = cab[(size_t)n_cls + c];
+  DiskAcc s;
+  disk_init(s, lv);
+  uint32_t seen = 0;
+  for (uint32_t n = n0 + threadIdx.x; n < n1; n += kBlock, ++seen) {
+    const NodeRecB r = nodes[n];
+    const double a = al * r.v;
+    const double b = be * r.u;
+    disk_step(s, fabs(a - b), n, lv);
+  }
+  if (s.lev == 0u) {
+    s.cnt = seen;
+    s.idx = seen ? n0 + threadIdx.x : 0xffffffffu;
+  }
+  const uint32_t L = wave_max_u32(s.lev);
+  uint32_t cnt = s.lev == L ? s.cnt : 0u;
+  uint32_t idx = s.lev == L ? s.idx : 0xffffffffu;
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    cnt += (uint32_t)__shfl_xor((int)cnt, o, kWave);
+    idx = min(idx, (uint32_t)__shfl_xor((int)idx, o, kWave));
+  }
+  const uint32_t w = threadIdx.x / kWave;
+  if (lane_id() == 0) {
+    red[0][w] = L;
+    red[1][w] = cnt;
+    red[2][w] = idx;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  uint32_t bl = 0, bc = 0, bi = 0xffffffffu;
+  for (int i = 0; i < kBlock / kWave; ++i) {
+    if (red[1][i] == 0u) continue;  // a wave with no node of this chunk
+    if (red[0][i] > bl) {
+      bl = red[0][i];
+      bc = red[1][i];
+      bi = red[2][i];
+    } else if (red[0][i] == bl) {
+      bc += red[1][i];
+      bi = min(bi, red[2][i]);
+    }
+  }
+  plc[(size_t)chunk * n_cls + c] = (bl << kDiskCountBits) | bc;
+  pidx[(size_t)chunk * n_cls + c] = bi;
+}
+
+// Per pod: its class's chunk partials (chunks in node order: the first chunk reaching the best
+// level holds the lowest node) -> best level, lowest node (+ node_offset), count.  Mode B
+// scores lie in [0, 10], so NormalizeScore cannot overflow and the lowest score is not needed
+// (written as 0).
+__global__ __launch_bounds__(kBlock) void k_reduce2b(const uint32_t* __restrict__ plc,
+                                                     const uint32_t* __restrict__ pidx,
+                                                     uint32_t C, uint32_t n_cls,
+                                                     const uint32_t* __restrict__ cls,
+                                                     uint32_t n_pods, uint32_t node_offset,
+                                                     int64_t* __restrict__ best_out,
+                                                     uint32_t* __restrict__ idx_out,
+                                                     uint32_t* __restrict__ ties_out,
+                                                     int64_t* __restrict__ low_out) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= n_pods) return;
+  const uint32_t c = cls[p];
+  int64_t bl = -1;
+  uint32_t bc = 0, bi = 0xffffffffu;
+  for (uint32_t k = 0; k < C; ++k) {
+    const uint32_t w = plc[(size_t)k * n_cls + c];
+    const int64_t L = (int64_t)(w >> kDiskCountBits);
+    if (L > bl) {
+      bl = L;
+      bc = w & ((1u << kDiskCountBits) - 1u);
+      bi = pidx[(size_t)k * n_cls + c];
+    } else if (L == bl) {
+      bc += w & ((1u << kDiskCountBits) - 1u);
+    }
+  }
+  best_out[p] = bl;
+  idx_out[p] = bi == 0xffffffffu ? bi : bi + node_offset;
+  ties_out[p] = bc;
+  low_out[p] = 0;
+}
+
 // Per-pod merge of K2 chunk partials.  Chunks are in node order, so on equal scores the
 // earlier chunk's index (lower) is kept.
 __global__ __launch_bounds__(kBlock) void k_reduce2(const double* __restrict__ pbest_f,
@@ -3629,6 +3828,53 @@ hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t ch
     hipLaunchKernelGGL(k2_diskio<false>, grid, dim3(kBlock), 0, s, nodes, n_nodes, chunk_nodes,
                        pp.alpha, pp.beta, n_pods, part.best_f, part.idx, part.ties, part.low_f,
                        rows);
+  return hipGetLastError();
+}
+
+// Mode B batch plan: few classes (<= 64) run lane = node in chunks of 2048 nodes, one
+// workgroup per (chunk, class); more run lane = class (4 per lane) in enough node chunks for
+// ~8 resident waves per SIMD.
+constexpr uint32_t kDiskNodeLaneMaxCls = 64;
+constexpr uint32_t kDiskNodeLaneChunk = 2048;
+constexpr int kDiskCPL = 4;
+
+DiskPlan diskio_plan(uint32_t n_nodes, uint32_t n_cls) {
+  DiskPlan pl{};
+  if (n_nodes == 0 || n_cls == 0) return pl;
+  pl.node_lanes = n_cls <= kDiskNodeLaneMaxCls;
+  if (pl.node_lanes) {
+    pl.chunk = kDiskNodeLaneChunk;
+  } else {
+    const uint32_t waves = (n_cls + kWave * kDiskCPL - 1) / (kWave * kDiskCPL);
+    uint32_t C = (8192u + waves - 1) / waves;
+    C = std::max(1u, std::min(C, (n_nodes + 63u) / 64u));
+    pl.chunk = (n_nodes + C - 1) / C;
+  }
+  pl.C = (n_nodes + pl.chunk - 1) / pl.chunk;
+  return pl;
+}
+
+hipError_t launch_k2b(const NodeRecB* nodes, uint32_t n_nodes, const double* cab,
+                      uint32_t n_cls, const DiskLevels& lv, const DiskPlan& pl, uint32_t* plc,
+                      uint32_t* pidx, hipStream_t s) {
+  if (pl.C == 0) return hipSuccess;
+  if (pl.node_lanes) {
+    hipLaunchKernelGGL(k2b_node_lanes, dim3(pl.C, n_cls), dim3(kBlock), 0, s, nodes, n_nodes,
+                       pl.chunk, cab, n_cls, lv, plc, pidx);
+  } else {
+    const uint32_t cb = (n_cls + kBlock * kDiskCPL - 1) / (kBlock * kDiskCPL);
+    hipLaunchKernelGGL(k2b_class_lanes<kDiskCPL>, dim3(cb, pl.C), dim3(kBlock), 0, s, nodes,
+                       n_nodes, pl.chunk, cab, n_cls, lv, plc, pidx);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce2b(const uint32_t* plc, const uint32_t* pidx, uint32_t C, uint32_t n_cls,
+                           const uint32_t* cls, uint32_t n_pods, uint32_t node_offset,
+                           int64_t* best, uint32_t* idx, uint32_t* ties, int64_t* low,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce2b, pod_grid(n_pods), dim3(kBlock), 0, s, plc, pidx, C, n_cls, cls,
+                     n_pods, node_offset, best, idx, ties, low);
   return hipGetLastError();
 }
 

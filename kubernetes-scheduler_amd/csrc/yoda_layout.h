@@ -164,6 +164,22 @@ struct alignas(16) NodeRecB {
   double v, u;
 };
 
+// Mode B score levels.  With d = alpha*V - beta*U (algorithm.go:109), the score
+// trunc(10 - 10*|d|) (>= 1, else 0; :110-111 then Uint64ToInt64) is a non-increasing function
+// of |d| under IEEE rounding (each operation is monotone), so score >= k  <=>  |d| <= t[k] for
+// k = 1..10; t[11] = -1 (no level above 10), t[0] unused.  Computed once on the host by
+// bisection over the double bit patterns (yoda_capi.cpp diskio_levels).
+struct DiskLevels {
+  double t[12];
+};
+// Mode B per (node chunk, pod class) partial: level << 28 | nodes at that level in the chunk.
+constexpr uint32_t kDiskCountBits = 28;
+// Mode B batch launch plan (yoda_kernels.hip diskio_plan): C chunks of `chunk` nodes.
+struct DiskPlan {
+  uint32_t chunk, C;
+  bool node_lanes;
+};
+
 // One pod evaluated alone against the CURRENT node state (greedy fallbacks), lane = node:
 // its Filter / card-predicate operands, passed by value (yoda_kernels.hip k_one_*).
 struct OnePod {

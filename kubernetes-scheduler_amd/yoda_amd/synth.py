@@ -141,6 +141,17 @@ def memory_in_bytes(nodes: NodeSoA, pods: PodSoA):
     return n.normalized(), p.normalized()
 
 
+def distinct_diskio(pods: PodSoA, seed: int = 11) -> PodSoA:
+    """The same pods with a distinct Mode-B request each: diskIO annotation U(0.5, 100) and a
+    CPU request U{50..4000} millicores, so no two pods share (alpha, beta) and the Mode-B batch
+    path evaluates every (pod, node) pair (algorithm.go:105-106)."""
+    p = _copy(pods)
+    rng = np.random.default_rng(seed)
+    p.rio = 0.5 + rng.random(p.n_pods) * 99.5
+    p.rcpu = rng.integers(50, 4001, p.n_pods).astype(np.int64)
+    return p.normalized()
+
+
 CONFIGS = {
     1: dict(pods=1, nodes=100, seed=1, desc="example/test-pod.yaml x 100 synthetic nodes"),
     2: dict(pods=1000, nodes=5000, seed=42, desc="1k pods x 5k nodes"),
@@ -161,3 +172,55 @@ def make_config(cfg: int, pods: int | None = None, nodes: int | None = None):
     het = cfg == 4
     return (make_nodes(n, seed, heterogeneous=het),
             make_pods(p, seed + 1000, heterogeneous=het, priorities=(cfg == 5)))
+
+
+# Workloads the headline does not cover (bench.py `extra.variants`, tools/variants.py):
+# name -> description.  Mode 0 = SCV (Mode A), 1 = diskIO (Mode B), as yoda_amd.soa.
+VARIANTS = {
+    "c3": "config 3 as generated (the headline workload)",
+    "mixed50": "config 3 with 50% of the nodes holding mixed GPU models",
+    "mixed100": "config 3 with every node holding mixed GPU models",
+    "bytes": "config 3 with memory in bytes instead of MiB (fields above 2^32: memory ranks)",
+    "u64": "config 3 forced onto the U64 record path (the reference's uint64 arithmetic)",
+    "c4": "config 4 at its declared size (10k pods x 20k nodes, heterogeneous fleet)",
+    "het100k": "config-4 generator at 100k pods x 100k nodes",
+    "diskio": "config 3, Mode B (BalancedCpuDiskIOPriority), pods as generated (one spec)",
+    "diskio_distinct": "config 3, Mode B, a distinct diskIO/CPU request per pod",
+    "c4diskio": "config 4, Mode B",
+}
+
+
+def variant_workloads(names):
+    """Yield (name, nodes, pods, mode, upload kwargs) for the VARIANTS names (config 3 built
+    once and shared)."""
+    c3 = None
+
+    def get_c3():
+        nonlocal c3
+        if c3 is None:
+            c3 = make_config(3)
+        return c3
+
+    for name in names:
+        if name not in VARIANTS:
+            raise ValueError(f"unknown variant {name}")
+        mode, kw = 0, {}
+        if name in ("c4", "c4diskio"):
+            n, p = make_config(4)
+        elif name == "het100k":
+            n, p = make_config(4, pods=100_000, nodes=100_000)
+        else:
+            n, p = get_c3()
+        if name == "mixed50":
+            n = mixed_models(n, 0.5)
+        elif name == "mixed100":
+            n = mixed_models(n, 1.0)
+        elif name == "bytes":
+            n, p = memory_in_bytes(n, p)
+        elif name == "u64":
+            kw = {"force_generic": True}
+        elif name == "diskio_distinct":
+            p = distinct_diskio(p)
+        if name.startswith("diskio") or name == "c4diskio":
+            mode = 1
+        yield name, n, p, mode, kw

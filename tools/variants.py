@@ -6,7 +6,7 @@ with the class counters on, and optionally the first `--check` pods against the 
 (picks, statuses, ties, feasible counts).  One JSON object per variant on stdout.
 
     python tools/variants.py [names...] [--steps 5] [--check 256]
-names: c3 mixed50 bytes u64 c4 het100k diskio (default: all)
+names: yoda_amd/synth.py VARIANTS (default: all but mixed100 and c4diskio)
 """
 from __future__ import annotations
 
@@ -28,48 +28,6 @@ from yoda_amd.capi import Yoda  # noqa: E402
 from yoda_amd.soa import MODE_DISKIO, MODE_SCV  # noqa: E402
 
 
-def workloads(names):
-    c3 = None
-
-    def get_c3():
-        nonlocal c3
-        if c3 is None:
-            c3 = synth.make_config(3)
-        return c3
-
-    for name in names:
-        if name == "c3":
-            n, p = get_c3()
-            yield name, n, p, MODE_SCV, {}
-        elif name == "mixed50":
-            n, p = get_c3()
-            yield name, synth.mixed_models(n, 0.5), p, MODE_SCV, {}
-        elif name == "mixed100":
-            n, p = get_c3()
-            yield name, synth.mixed_models(n, 1.0), p, MODE_SCV, {}
-        elif name == "bytes":
-            n, p = get_c3()
-            nb, pb = synth.memory_in_bytes(n, p)
-            yield name, nb, pb, MODE_SCV, {}
-        elif name == "u64":
-            n, p = get_c3()
-            yield name, n, p, MODE_SCV, {"force_generic": True}
-        elif name == "c4":
-            n, p = synth.make_config(4)
-            yield name, n, p, MODE_SCV, {}
-        elif name == "het100k":
-            n, p = synth.make_config(4, pods=100_000, nodes=100_000)
-            yield name, n, p, MODE_SCV, {}
-        elif name == "diskio":
-            n, p = get_c3()
-            yield name, n, p, MODE_DISKIO, {}
-        elif name == "c4diskio":
-            n, p = synth.make_config(4)
-            yield name, n, p, MODE_DISKIO, {}
-        else:
-            raise SystemExit(f"unknown variant {name}")
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("names", nargs="*")
@@ -77,10 +35,11 @@ def main():
     ap.add_argument("--check", type=int, default=0)
     ap.add_argument("--threads", type=int, default=16)
     args = ap.parse_args()
-    names = args.names or ["c3", "mixed50", "bytes", "u64", "c4", "het100k", "diskio"]
+    names = args.names or ["c3", "mixed50", "bytes", "u64", "c4", "het100k", "diskio",
+                          "diskio_distinct"]
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
-    for name, nodes, pods, mode, kw in workloads(names):
+    for name, nodes, pods, mode, kw in synth.variant_workloads(names):
         y = Yoda(0)
         y.upload_nodes(nodes, **kw)
         y.upload_pods(pods)
