@@ -138,7 +138,9 @@ int yoda_destroy(yoda_t* h);
 const char* yoda_last_error(const yoda_t* h);
 /* Launch all work on this HIP stream (hipStream_t passed as void*; NULL = the HIP null
  * stream, e.g. PyTorch's default stream).  Until called, the handle uses a non-blocking
- * stream of its own; yoda_use_own_stream switches back to it. */
+ * stream of its own; yoda_use_own_stream switches back to it.  Work the handle already
+ * queued on its previous stream (e.g. an upload's copies) is ordered before the new
+ * stream's next work (an event wait on the device, no host synchronization). */
 int yoda_set_stream(yoda_t* h, void* hip_stream);
 int yoda_use_own_stream(yoda_t* h);
 int yoda_synchronize(yoda_t* h);
@@ -324,8 +326,10 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
 int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks,
                       double* times_ms);
 /* YODA_GREEDY_CARD_CAPACITY: windows of the last yoda_greedy that ended early at a pod the
- * capacity certificate could not clear (that pod then opened the next window); isolated
- * uncertified pods are scheduled one by one instead (counted as fallbacks). */
+ * capacity certificate could not clear (that pod then opens the next window).  The capacity
+ * mode restarts on every uncertified pod by default (no exact fallbacks: the fallback count
+ * stays 0); the YODA_GREEDY_FAIL_DIV environment knob re-enables one-by-one fallbacks for
+ * A/B runs. */
 int yoda_greedy_restarts(const yoda_t* h, uint32_t* restarts);
 
 /* ---- sharded greedy batch (node shards on several GPUs) ------------------------------

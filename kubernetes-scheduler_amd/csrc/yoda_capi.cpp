@@ -299,6 +299,7 @@ struct yoda_handle {
   DevBuf k1sum;     // K1 node summaries (N32 path, yoda_layout.h K1SumWord)
   DevBuf k2sum;     // K2 node summaries (N32 path, yoda_layout.h K2SumWord)
   DevBuf kmix;      // per-card GPU models in free order (N32 path, yoda_layout.h MixWord)
+  DevBuf kx1;       // K1's tile of the mixed-model nodes (N32 path, yoda_layout.h K1MixWord)
   // memory ranks (yoda_layout.h MemTab): the N32 memory fields are ranks; value tables
   bool mem_ranks = false;
   DevBuf memtab;
@@ -320,6 +321,7 @@ struct yoda_handle {
   DevBuf pod_blob;
   PinnedBuf pod_stage;
   hipEvent_t stage_event = nullptr;
+  hipEvent_t switch_event = nullptr;  // yoda_set_stream: the old stream's work, waited on
   bool stage_pending = false;
   size_t pod_off[kPodArrays] = {};
   // batch ordering (yoda_order.hip): when `ordered`, the kernels of this run read the pods
@@ -421,7 +423,7 @@ struct yoda_handle {
   ~yoda_handle() {
     if (comm && rccl().ok) (void)rccl().comm_destroy(comm);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &memtab,    &pod_blob,   &maxima,       &counts,
+    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &pod_blob,   &maxima,       &counts,
                      &pod_sorted, &perm,     &order_scratch, &order_meta, &order_hist,
                      &order_bstart, &order_slot, &order_bkt,
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
@@ -441,6 +443,7 @@ struct yoda_handle {
     pick_stage.release();
     win_stage.release();
     if (stage_event) (void)hipEventDestroy(stage_event);
+    if (switch_event) (void)hipEventDestroy(switch_event);
     if (upd_event) (void)hipEventDestroy(upd_event);
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
@@ -599,6 +602,7 @@ PodParams pod_params(yoda_t* h) {
   pp.beta = reinterpret_cast<double*>(b + off[kPodBeta]);
   pp.g = h->has_k2sum ? h->g : GTab{};
   pp.mix = h->path == Path::N32 ? h->kmix.as<uint32_t>() : nullptr;
+  pp.x1 = h->path == Path::N32 ? h->kx1.as<uint32_t>() : nullptr;
   pp.mt = h->mem_ranks ? h->mt : MemTab{};
   return pp;
 }
@@ -1154,16 +1158,27 @@ const char* yoda_last_error(const yoda_t* h) {
   return h ? h->last_error.c_str() : "null handle";
 }
 
+// Switch the handle's stream: work already queued on the old stream (an upload's copies and
+// kernels) is ordered before anything queued on the new one (an event wait, no host sync).
+static int switch_stream(yoda_t* h, hipStream_t ns) {
+  if (ns == h->stream) return YODA_OK;
+  HIP_TRY(h, hipSetDevice(h->device));
+  if (!h->switch_event)
+    HIP_TRY(h, hipEventCreateWithFlags(&h->switch_event, hipEventDisableTiming));
+  HIP_TRY(h, hipEventRecord(h->switch_event, h->stream));
+  HIP_TRY(h, hipStreamWaitEvent(ns, h->switch_event, 0));
+  h->stream = ns;
+  return YODA_OK;
+}
+
 int yoda_set_stream(yoda_t* h, void* hip_stream) {
   if (!h) return YODA_ERR_INVALID_ARG;
-  h->stream = static_cast<hipStream_t>(hip_stream);
-  return YODA_OK;
+  return switch_stream(h, static_cast<hipStream_t>(hip_stream));
 }
 
 int yoda_use_own_stream(yoda_t* h) {
   if (!h) return YODA_ERR_INVALID_ARG;
-  h->stream = h->own_stream;
-  return YODA_OK;
+  return switch_stream(h, h->own_stream);
 }
 
 int yoda_synchronize(yoda_t* h) {
@@ -1274,6 +1289,8 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     std::vector<uint32_t> sum2(want_sum ? (size_t)std::max<uint32_t>(N, 1) * s2stride / 4 : 0, 0);
     const size_t mstride = mix_stride(K);
     std::vector<uint32_t> mix(want_sum ? (size_t)std::max<uint32_t>(N, 1) * mstride / 4 : 0, 0);
+    const size_t xstride = x1_stride(K);
+    std::vector<uint32_t> x1m(want_sum ? (size_t)std::max<uint32_t>(N, 1) * xstride / 4 : 0, 0);
     for (uint32_t i = 0; i < N; ++i) {
       unsigned char* r = rec.data() + (size_t)i * stride;
       uint32_t hm = 0;
@@ -1360,6 +1377,43 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
         }
         mx[mix_hm(K)] = hmf;
         s2[kS2MinClk] = minclk;
+        // K1 tile (K1MixWord): prefix maxima per 16-bit half, their change bits, the cards
+        // packed, the healthy-card counts per distinct clock
+        uint32_t* x = x1m.data() + (size_t)i * xstride / 4;
+        uint32_t pa = 0, pb = 0, pt = 0, chg = 0, nch = 0;
+        auto hmax = [](uint32_t u, uint32_t v) {
+          return std::max(u & 0xffffu, v & 0xffffu) | (std::max(u >> 16, v >> 16) << 16);
+        };
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const size_t b = a + ord[j];
+          const uint32_t ca = (uint32_t)nd->card_clock[b] | ((uint32_t)nd->card_bandwidth[b] << 16);
+          const uint32_t cb = (uint32_t)nd->card_core[b] | ((uint32_t)nd->card_power[b] << 16);
+          const uint32_t na = hmax(pa, ca), nb2 = hmax(pb, cb);
+          const uint32_t nt = std::max(pt, s2[kS2Fs + K + j]);
+          if (j == 0 || na != pa || nb2 != pb || nt != pt) chg |= 1u << (j + 1);
+          pa = na;
+          pb = nb2;
+          pt = nt;
+          x[x1_pm((int)j, 0)] = pa;
+          x[x1_pm((int)j, 1)] = pb;
+          x[x1_pm((int)j, 2)] = pt;
+          x[x1_cd((int)j, 0, K)] = ca;
+          x[x1_cd((int)j, 1, K)] = cb;
+          if (nd->card_healthy[b]) {
+            const uint32_t ck = (uint32_t)nd->card_clock[b];
+            uint32_t e = 0;
+            while (e < nch && (x[kX1Ch + e] & 0xffffu) != ck) ++e;
+            if (e == nch) {
+              if (nch == 4) {
+                chg |= kX1ChgMany;
+                continue;
+              }
+              x[kX1Ch + nch++] = ck;
+            }
+            x[kX1Ch + e] += 1u << 16;
+          }
+        }
+        x[kX1Chg] = chg;
       }
       for (uint32_t j = 0; j < nd->card_count[i]; ++j) {
         const size_t k = (size_t)i * KS + j;
@@ -1402,6 +1456,10 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
       sum = tiles(sum, (uint32_t)sstride);
       sum2 = tiles(sum2, (uint32_t)s2stride);
       mix = tiles(mix, (uint32_t)mstride);
+      x1m = tiles(x1m, (uint32_t)xstride);
+      HIP_TRY(h, h->kx1.ensure(x1m.size() * 4));
+      HIP_TRY(h, hipMemcpyAsync(h->kx1.p, x1m.data(), x1m.size() * 4, hipMemcpyHostToDevice,
+                                h->stream));
       HIP_TRY(h, h->kmix.ensure(mix.size() * 4));
       HIP_TRY(h, hipMemcpyAsync(h->kmix.p, mix.data(), mix.size() * 4, hipMemcpyHostToDevice,
                                 h->stream));

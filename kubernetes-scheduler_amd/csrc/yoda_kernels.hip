@@ -213,6 +213,12 @@ __device__ __forceinline__ bool k1_node_lean(const unsigned char* rec, uint32_t 
 }
 
 __device__ __forceinline__ uint64_t ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+// per-16-bit-half maximum of two packed pairs (v_pk_max_u16)
+__device__ __forceinline__ uint32_t max16x2(uint32_t a, uint32_t b) {
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  const us2 m = __builtin_elementwise_max(__builtin_bit_cast(us2, a), __builtin_bit_cast(us2, b));
+  return __builtin_bit_cast(uint32_t, m);
+}
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & (kWave - 1); }
 __device__ __forceinline__ uint32_t uniform_u32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
@@ -579,6 +585,7 @@ template <int K, bool STATS>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 ? 5 : YODA_K1_WAVES))) void k1_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum,
     const uint32_t* __restrict__ sum2w, const uint32_t* __restrict__ mixw,
+    const uint32_t* __restrict__ x1w,
     uint32_t n_nodes, uint32_t chunk_nodes, const uint32_t* __restrict__ m_in,
     const uint32_t* __restrict__ c_in, const uint64_t* __restrict__ number_in,
     const uint32_t* __restrict__ need_mem_in, const uint32_t* __restrict__ need_clk_in,
@@ -588,7 +595,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
     unsigned long long* __restrict__ stats) {
   constexpr uint32_t SS = k1sum_stride(K);
   constexpr uint32_t NS = n32_stride(K);
-  constexpr uint32_t S2 = k2sum_stride(K), MS = mix_stride(K);
+  constexpr uint32_t S2 = k2sum_stride(K), MS = mix_stride(K), XS = x1_stride(K);
   constexpr uint32_t HW = K + 1;  // LDS words per node: hfs[0..K-1], 0
   // + a 10-word record per one-model PART node (below): the per-pod pass reads it from LDS
   constexpr uint32_t REC = 10, RECS = kWave * HW;
@@ -713,7 +720,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
     // mixed-model nodes: count hc over the per-card clocks (free order, with health bits),
     // only when it decides something (some pod has the label, all of them one clock) and
     // the number / memory bounds leave the node open
-    const uint32_t* mxw = mixw + sum_index(nb, 0, MS) + lane;
+    const uint32_t* xw = x1w + sum_index(nb, 0, XS) + lane;
     if (any_pc && c_uni) {
 #ifdef YODA_ABL_K1_NOHC
       const bool cnt_clk = false;
@@ -721,11 +728,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
       const bool cnt_clk = valid && !uni4 && !num_none && !mem_none;
 #endif
       if (ballot(cnt_clk) != 0ull) {
-        if (cnt_clk) {
-          const uint32_t hm = mxw[64 * mix_hm(K)];
+        if (cnt_clk) {  // the node's healthy-card count per distinct clock (K1MixWord ch)
+          if ((xw[64 * kX1Chg] & kX1ChgMany) == 0u) {
 #pragma unroll
-          for (int t = 0; t < K; ++t)
-            hc += ((hm >> t) & 1u) & (uint32_t)(mxw[64 * mix_word(kMixCk, t, K)] == cpc_max);
+            for (int e = 0; e < 4; ++e) {
+              const uint32_t w = xw[64 * (kX1Ch + e)];
+              hc += (w & 0xffffu) == cpc_max ? w >> 16 : 0u;
+            }
+          } else {  // more than 4 distinct clocks: the cards one by one
+            const uint32_t* mxw = mixw + sum_index(nb, 0, MS) + lane;
+            const uint32_t hm = mxw[64 * mix_hm(K)];
+#pragma unroll
+            for (int t = 0; t < K; ++t)
+              hc += ((hm >> t) & 1u) & (uint32_t)(mxw[64 * mix_word(kMixCk, t, K)] == cpc_max);
+          }
         }
       }
     }
@@ -753,37 +769,65 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
 #endif
     if (ballot(gen) != 0ull) {
       if (gen) {
+        // The cards in free order (K2 summary): the smallest set is {t < qs, clock >= c_max},
+        // the largest {t < ql, clock >= c_min}, qs / ql = cards with free >= m_max / m_min.
         const uint32_t* s2 = sum2w + sum_index(nb, 0, S2) + lane;
-        bw = ck = core = mrf1 = pw = tot = 0u;  // mrf1: 1 + the free maximum (0: none)
-        bool unc = false;
-#pragma unroll YODA_K1_GEN_UNROLL
+        const uint32_t cnt = (s2[64 * kS2Meta] >> 8) & 0xffu, minclk = s2[64 * kS2MinClk];
+        uint32_t qs = 0, ql = 0;
+#pragma unroll
         for (int t = 0; t < K; ++t) {
-          const uint32_t f = s2[64 * (kS2Fs + t)], cj = mxw[64 * mix_word(kMixCk, t, K)];
-          const bool qs = (f >= m_max) & (cj >= c_max), ql = (f >= m_min) & (cj >= c_min);
-          unc = unc || (ql && !qs);
-          bw = max(bw, qs ? mxw[64 * mix_word(kMixBw, t, K)] : 0u);
-          ck = max(ck, qs ? cj : 0u);
-          core = max(core, qs ? mxw[64 * mix_word(kMixCo, t, K)] : 0u);
-          mrf1 = max(mrf1, qs ? f + 1u : 0u);
-          pw = max(pw, qs ? mxw[64 * mix_word(kMixPw, t, K)] : 0u);
-          tot = max(tot, qs ? s2[64 * (kS2Fs + K + t)] : 0u);
+          const uint32_t f = s2[64 * (kS2Fs + t)];
+          qs += (uint32_t)(f >= m_max);
+          ql += (uint32_t)(f >= m_min);
         }
-        qual = true;
-        same = true;
-        if (unc) {
+        qs = min(qs, cnt);
+        ql = min(ql, cnt);
+        if (c_max <= minclk) {
+          // every card passes every pod's clock test: both sets are prefixes, whose maxima
+          // are tabled (K1MixWord pm) with the cards where they change (chg)
+          const uint32_t chg = xw[64 * kX1Chg];
+          same = ((chg >> (qs + 1u)) & ((1u << (ql - qs)) - 1u)) == 0u;
+          bw = ck = core = mrf1 = pw = tot = 0u;
+          if (qs > 0u) {
+            const uint32_t* pm = xw + 64 * x1_pm((int)qs - 1, 0);
+            const uint32_t a = pm[0], b = pm[64], t = pm[128];
+            ck = a & 0xffffu;
+            bw = a >> 16;
+            core = b & 0xffffu;
+            pw = b >> 16;
+            tot = t;
+            mrf1 = s2[64 * kS2Fs] + 1u;  // the first card has the largest free
+          }
+        } else {
+          // per card, both sets' maxima at once (clock|bandwidth and core|power per 16-bit
+          // half); the contribution is the same for every pod iff they are equal
+          uint32_t sa = 0, sb = 0, st = 0, sf = 0, la = 0, lb = 0, lt = 0, lf = 0;
 #pragma unroll YODA_K1_GEN_UNROLL
           for (int t = 0; t < K; ++t) {
-            const uint32_t f = s2[64 * (kS2Fs + t)], cj = mxw[64 * mix_word(kMixCk, t, K)];
-            const bool d = (f >= m_min) & (cj >= c_min) & !((f >= m_max) & (cj >= c_max));
-            const uint32_t raises = (uint32_t)(mxw[64 * mix_word(kMixBw, t, K)] > bw) |
-                                    (uint32_t)(cj > ck) |
-                                    (uint32_t)(mxw[64 * mix_word(kMixCo, t, K)] > core) |
-                                    (uint32_t)(f >= mrf1) |
-                                    (uint32_t)(mxw[64 * mix_word(kMixPw, t, K)] > pw) |
-                                    (uint32_t)(s2[64 * (kS2Fs + K + t)] > tot);
-            same = same && !(d && raises != 0u);
+            const uint32_t f = s2[64 * (kS2Fs + t)], to = s2[64 * (kS2Fs + K + t)];
+            const uint32_t a = xw[64 * x1_cd(t, 0, K)], b = xw[64 * x1_cd(t, 1, K)];
+            const uint32_t cj = a & 0xffffu;
+            const bool real = (uint32_t)t < cnt;
+            const bool in_s = real & (f >= m_max) & (cj >= c_max);
+            const bool in_l = real & (f >= m_min) & (cj >= c_min);
+            sa = max16x2(sa, in_s ? a : 0u);
+            sb = max16x2(sb, in_s ? b : 0u);
+            st = max(st, in_s ? to : 0u);
+            sf = max(sf, in_s ? f + 1u : 0u);
+            la = max16x2(la, in_l ? a : 0u);
+            lb = max16x2(lb, in_l ? b : 0u);
+            lt = max(lt, in_l ? to : 0u);
+            lf = max(lf, in_l ? f + 1u : 0u);
           }
+          same = (sa == la) & (sb == lb) & (st == lt) & (sf == lf);
+          ck = sa & 0xffffu;
+          bw = sa >> 16;
+          core = sb & 0xffffu;
+          pw = sb >> 16;
+          tot = st;
+          mrf1 = sf;
         }
+        qual = true;
       }
     }
     const bool is_none = valid && feas_none;
@@ -3488,7 +3532,7 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
         if (stats)
           YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK, true>), grid, dim3(kBlock), 0, s,
                                               nodes, sum, reinterpret_cast<const uint32_t*>(sum2),
-                                              reinterpret_cast<const uint32_t*>(mix), n_nodes,
+                                              reinterpret_cast<const uint32_t*>(mix), pp.x1, n_nodes,
                                               chunk_nodes, pp.m_32, pp.c_32,
                                               pp.number, pp.need_mem, pp.need_clk, n_pods,
                                               part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,
@@ -3496,7 +3540,7 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
         else
           YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK, false>), grid, dim3(kBlock), 0, s,
                                               nodes, sum, reinterpret_cast<const uint32_t*>(sum2),
-                                              reinterpret_cast<const uint32_t*>(mix), n_nodes,
+                                              reinterpret_cast<const uint32_t*>(mix), pp.x1, n_nodes,
                                               chunk_nodes, pp.m_32, pp.c_32,
                                               pp.number, pp.need_mem, pp.need_clk, n_pods,
                                               part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,

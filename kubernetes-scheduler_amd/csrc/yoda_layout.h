@@ -124,6 +124,24 @@ __host__ __device__ constexpr uint32_t mix_word(int field, int j, int k) {
 __host__ __device__ constexpr uint32_t mix_hm(int k) { return 4u * (uint32_t)k; }
 __host__ __device__ constexpr uint32_t mix_stride(int k) { return 4u * (4u * (uint32_t)k + 1u); }
 
+// K1 tile of the nodes whose cards are not all one model (N32 path; read by k1_block_n32 with
+// lane = node), REAL cards in the K2 summary's descending-free order, u32 words:
+//   chg      bit q (1..K): the prefix maxima below differ between q - 1 and q cards (bit 1
+//            whenever a card exists); bit 31: more than 4 distinct healthy-card clocks
+//   ch[4]    clock | (healthy cards with that clock << 16), distinct clocks (0: unused)
+//   pm[q-1]  for q = 1..K, the maxima over the first q cards of (clock | bandwidth << 16)
+//            and (core | power << 16) per 16-bit half, and of TotalMemory (K2 summary code)
+//   cd[t]    card t's (clock | bandwidth << 16), (core | power << 16)
+// (N32: clock, bandwidth, core and power are <= 55738, so each fits 16 bits.)  Tile layout
+// like the summaries (sum_index).
+enum K1MixWord { kX1Chg = 0, kX1Ch = 1, kX1Pm = 5 };
+__host__ __device__ constexpr uint32_t x1_pm(int q1, int f) { return kX1Pm + 3u * (uint32_t)q1 + (uint32_t)f; }
+__host__ __device__ constexpr uint32_t x1_cd(int t, int f, int k) {
+  return kX1Pm + 3u * (uint32_t)k + 2u * (uint32_t)t + (uint32_t)f;
+}
+__host__ __device__ constexpr uint32_t x1_stride(int k) { return 4u * (kX1Pm + 5u * (uint32_t)k); }
+constexpr uint32_t kX1ChgMany = 1u << 31;
+
 // Both summaries are stored in tiles of 64 nodes, word-major inside a tile (AoSoA): word w
 // of node n is u32 number sum_index(n, w, stride).  The block kernels read them with
 // lane = node, so loading one word for 64 nodes is one contiguous 256-B access (2 cache
@@ -254,6 +272,8 @@ struct PodParams {
   GTab g = {};
   // the snapshot's per-card models in free order (N32; yoda_layout.h MixWord)
   const uint32_t* mix = nullptr;
+  // the snapshot's K1 tile of mixed-model nodes (N32; yoda_layout.h K1MixWord)
+  const uint32_t* x1 = nullptr;
   // the snapshot's memory ranks (MemTab; vf == nullptr: none)
   MemTab mt = {};
 };

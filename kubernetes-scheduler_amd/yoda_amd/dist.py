@@ -317,11 +317,15 @@ class ShardExchange:
 
 
 class LibExchange:
-    """Node sharding with libyoda's OWN exchanges (yoda_comm_run, include/yoda.h): one
-    all-reduce(MAX) of the maxima with per-rank count slots and one all-gather of the
-    per-shard (best, index, ties, lowest) records per step, issued by libyoda through RCCL on
-    the handle's stream -- the path a cgo / C caller without torch uses.  torch.distributed
-    here only agrees on the record path and broadcasts the communicator id."""
+    """Node sharding with libyoda's OWN exchanges (yoda_comm_run, include/yoda.h, DESIGN.md
+    §7), issued by libyoda through RCCL on the handle's stream -- the path a cgo / C caller
+    without torch uses.  Per step: after K1 one grouped all-reduce, MAX over [maxima 6P |
+    2 agreement words] and SUM over the counts [2P]; after K2, on the fast record paths, the
+    packed (score << ib | ~node) key MAX then the tie-count SUM of the shards holding the
+    winner.  Only the U64 path in Mode A all-gathers the per-shard (best, index, ties,
+    lowest) records instead (its NormalizeScore check needs the lowest score), plus the
+    exact-normalize records when K3 flags pods.  torch.distributed here only agrees on the
+    record path and broadcasts the communicator id."""
 
     def __init__(self, handle, device, shard=None, offset: int = 0, group=None):
         import torch.distributed as dist
