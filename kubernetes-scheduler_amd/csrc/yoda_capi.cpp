@@ -308,6 +308,8 @@ struct yoda_handle {
   DevBuf gtab, gtab_aux;  // the G table (yoda_layout.h GTab) + [G maxima | its reciprocals]
   GTab g = {};
   bool has_k1sum = false, has_k2sum = false;
+  bool all_one_model = false;  // every node: one GPU model, one TotalMemory (kNodeUniform4|Total)
+  bool all_uni4 = false;       // every node: one GPU model (kNodeUniform4)
   std::vector<unsigned char> host_records;  // kept for alloc updates (greedy)
   std::vector<uint32_t> host_k2sum;         // idem (its static score words)
   std::vector<uint64_t> h_total_sum, h_free_sum, h_alloc, h_card_number;
@@ -603,6 +605,8 @@ PodParams pod_params(yoda_t* h) {
   pp.g = h->has_k2sum ? h->g : GTab{};
   pp.mix = h->path == Path::N32 ? h->kmix.as<uint32_t>() : nullptr;
   pp.x1 = h->path == Path::N32 ? h->kx1.as<uint32_t>() : nullptr;
+  pp.one_model = h->path == Path::N32 && h->all_one_model;
+  pp.all_uni4 = h->path == Path::N32 && h->all_uni4;
   pp.mt = h->mem_ranks ? h->mt : MemTab{};
   return pp;
 }
@@ -1289,6 +1293,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     std::vector<uint32_t> sum2(want_sum ? (size_t)std::max<uint32_t>(N, 1) * s2stride / 4 : 0, 0);
     const size_t mstride = mix_stride(K);
     std::vector<uint32_t> mix(want_sum ? (size_t)std::max<uint32_t>(N, 1) * mstride / 4 : 0, 0);
+    uint32_t n_one_model = 0, n_uni4 = 0;
     const size_t xstride = x1_stride(K);
     std::vector<uint32_t> x1m(want_sum ? (size_t)std::max<uint32_t>(N, 1) * xstride / 4 : 0, 0);
     for (uint32_t i = 0; i < N; ++i) {
@@ -1316,6 +1321,9 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
       hd.flags = 0u;
       if (uni && !(flags & YODA_UPLOAD_NO_UNIFORM))
         hd.flags = kNodeUniform4 | (uni_total ? kNodeUniformTotal : 0u);
+      n_one_model += (hd.flags & (kNodeUniform4 | kNodeUniformTotal)) ==
+                     (kNodeUniform4 | kNodeUniformTotal);
+      n_uni4 += (hd.flags & kNodeUniform4) != 0u;
       if (path == Path::U64) {
         hd.static_score = stat[i];
       } else {
@@ -1530,6 +1538,8 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     h->K = K;
     h->path = path;
     h->has_k1sum = want_sum && !(flags & YODA_UPLOAD_PER_NODE_K1);
+    h->all_one_model = n_one_model == N;
+    h->all_uni4 = n_uni4 == N;
     h->has_k2sum = want_sum && !(flags & YODA_UPLOAD_PER_NODE_K2);
     h->g = GTab{};
     static const bool no_gtab = env_u32("YODA_NO_GTAB", 0) != 0;  // A/B knob

@@ -578,7 +578,9 @@ __global__ __launch_bounds__(kWave) void k_reduce_wit(const uint64_t* __restrict
 #ifndef YODA_K1_GEN_UNROLL
 #define YODA_K1_GEN_UNROLL 1
 #endif
-template <int K, bool STATS>
+// MIX = false: a snapshot whose every node is one GPU model with one TotalMemory (no per-card
+// work in K1 at all): the same kernel with the per-card branches compiled out.
+template <int K, bool STATS, bool MIX = true>
 #ifndef YODA_K1_WAVES
 #define YODA_K1_WAVES 7
 #endif
@@ -725,7 +727,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
 #ifdef YODA_ABL_K1_NOHC
       const bool cnt_clk = false;
 #else
-      const bool cnt_clk = valid && !uni4 && !num_none && !mem_none;
+      const bool cnt_clk = MIX && valid && !uni4 && !num_none && !mem_none;
 #endif
       if (ballot(cnt_clk) != 0ull) {
         if (cnt_clk) {  // the node's healthy-card count per distinct clock (K1MixWord ch)
@@ -765,7 +767,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
 #ifdef YODA_ABL_K1_NOGEN
     const bool gen = false;
 #else
-    const bool gen = valid && !one_model && feas_all && !feas_none;
+    const bool gen = MIX && valid && !one_model && feas_all && !feas_none;
 #endif
     if (ballot(gen) != 0ull) {
       if (gen) {
@@ -916,7 +918,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
       }
     }
     part_b &= ~rec_b;
-    while (part_b) {  // mixed-model nodes: the exact per-card predicates from the record
+    while (MIX && part_b) {  // mixed-model nodes: the exact per-card predicates from the record
       const int j = __builtin_ctzll(part_b);
       part_b &= part_b - 1;
 #ifdef YODA_ABL_K1_NOLEAN
@@ -1586,7 +1588,9 @@ __global__ __launch_bounds__(kBlock) void k2_score(
 #ifndef YODA_K2_WAVES
 #define YODA_K2_WAVES 5
 #endif
-template <int K, bool STATS, int TKO = 0, bool RK = false>
+// MIX = false: a snapshot whose every node is one GPU model (kSumUni4): no mixed-model rows
+// and no exact per-pod Scorer in the kernel.
+template <int K, bool STATS, int TKO = 0, bool RK = false, bool MIX = true>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ? (TKO == 0 ? YODA_K2_WAVES : (TKO <= 8 ? 4 : 3)) : 1))) void k2_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum2,
     uint32_t n_nodes, uint32_t chunk_nodes, ScoreArgs args, uint32_t n_pods,
@@ -1748,7 +1752,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     // the clock the per-pod passes compare with the pods' scv/clock (algorithm.go:271): the
     // node's one model, or ~0 for a mixed-model node whose clock test is folded into its row
     uint32_t ck = h0.z;
-    bool fast = mask != 0ull && (h0.w & kSumUni4) != 0u;
+    bool fast = mask != 0ull && (!MIX || (h0.w & kSumUni4) != 0u);
     // TOPK: an upper bound on node n's key for every pod of the wave (uniform maxima, one-model
     // node: every pod qualifies at most the nq_hi cards the smallest scv/memory does); ~0:
     // no bound
@@ -1822,7 +1826,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         // a row like the one-model B[q], with the clock test folded in (ck := ~0).  The G
         // row is B' when every card passes (the node's lowest clock >= the wave's
         // largest scv/clock).  Otherwise the node stays on the exact per-pod path.
-        const bool mixn = mask != 0ull && (meta & kSumUni4) == 0u;
+        const bool mixn = MIX && mask != 0ull && (meta & kSumUni4) == 0u;
         if (ballot(mixn) != 0ull) {
           if (mixn) {
             bool ok = use_g && h1.w >= c_max;
@@ -2041,7 +2045,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         if (ballot(((mj >> lane) & 1ull) != 0ull && ubj > pl[TL - 1]) == 0ull) continue;
       }
       double raw;
-      if ((fast_b >> j) & 1ull) {
+      if (!MIX || ((fast_b >> j) & 1ull)) {
         // one-model node: nq qualifying cards (a prefix of the free order), then
         // nq * shared + prefix[nq] from LDS -- the node's facts come from its lane
         const uint32_t cnt = ((uint32_t)__builtin_amdgcn_readlane((int)h0.w, j) >> 8) & 0xffu;
@@ -3537,6 +3541,14 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                                               pp.number, pp.need_mem, pp.need_clk, n_pods,
                                               part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,
                                               blk, blk_stride, stats))
+        else if (pp.one_model)
+          YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK, false, false>), grid, dim3(kBlock), 0, s,
+                                              nodes, sum, reinterpret_cast<const uint32_t*>(sum2),
+                                              reinterpret_cast<const uint32_t*>(mix), pp.x1, n_nodes,
+                                              chunk_nodes, pp.m_32, pp.c_32,
+                                              pp.number, pp.need_mem, pp.need_clk, n_pods,
+                                              part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,
+                                              blk, blk_stride, stats))
         else
           YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK, false>), grid, dim3(kBlock), 0, s,
                                               nodes, sum, reinterpret_cast<const uint32_t*>(sum2),
@@ -3677,6 +3689,12 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
         // memory ranks: the kernel of its own (RK = true)
         if (stats) {
           if (a.mt.vf) YODA_K2B(true, true) else YODA_K2B(true, false);
+        } else if (pp.all_uni4 && !a.mt.vf) {
+          YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false, 0, false, false>), grid,
+                                              dim3(kBlock), 0, s, nodes, sum2, n_nodes,
+                                              chunk_nodes, a, n_pods, bm, bm_stride, bs,
+                                              bs_stride, blk, blk_stride, part.best_f, part.idx,
+                                              part.ties, part.low_f, stats, nullptr, 0u));
         } else {
           if (a.mt.vf) YODA_K2B(false, true) else YODA_K2B(false, false);
         }

@@ -274,6 +274,11 @@ struct PodParams {
   const uint32_t* mix = nullptr;
   // the snapshot's K1 tile of mixed-model nodes (N32; yoda_layout.h K1MixWord)
   const uint32_t* x1 = nullptr;
+  // every node of the snapshot is one GPU model with one TotalMemory (N32: the K1 without
+  // per-card branches serves it)
+  bool one_model = false;
+  // every node of the snapshot is one GPU model (kSumUni4; N32: the K2 without mixed rows)
+  bool all_uni4 = false;
   // the snapshot's memory ranks (MemTab; vf == nullptr: none)
   MemTab mt = {};
 };
