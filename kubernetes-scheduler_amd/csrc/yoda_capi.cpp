@@ -993,7 +993,11 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
     HIP_TRY(h, hipEventRecord(e1, h->stream));
     h->ev_k2.emplace_back(e0, e1);
   }
-  HIP_TRY(h, launch_reduce2(part, h->C2, P, is_f64, h->node_offset, best, idx, ties, low,
+  // the block K2 (N32 with summaries, argmax) writes no lowest scores: the
+  // merge reports each pod's best in their place
+  Partials pr = part;
+  if (mode == YODA_MODE_SCV && h->path == Path::N32 && h->has_k2sum && !rows) pr.low_f = nullptr;
+  HIP_TRY(h, launch_reduce2(pr, h->C2, P, is_f64, h->node_offset, best, idx, ties, low,
                             h->stream));
   return YODA_OK;
 }

@@ -1607,10 +1607,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // node records (below): 16 words -- 8 of header, then 4 basic scores (uniform maxima) or
   // the (basic at nq_lo, at nq_lo + 1) pair of each reciprocal set
   constexpr uint32_t kSets = 4, REC = 16;
-  // LDS per wave: prefix table | 64 node records | the sets' reciprocals (8 words each)
-  // + each node lane's lowest U score (f64; in LDS, not a register: VGPR pressure)
-  constexpr uint32_t RECS = TAB, RCPS = TAB + kWave * REC, ULOW = RCPS + 8 * kSets,
-                     LDSW = ULOW + 2 * kWave;
+  // LDS per wave: prefix table | 64 node records | the sets' reciprocals (8 words each).
+  // No lowest score: on this path NormalizeScore cannot overflow, so the
+  // lowest raw score is never read (the chunk merge reports the best in its place).
+  constexpr uint32_t RECS = TAB, RCPS = TAB + kWave * REC, LDSW = RCPS + 8 * kSets;
   __shared__ __attribute__((aligned(16))) uint32_t lds_all[kBlock / kWave][LDSW];
   const uint32_t lane = lane_id();
   uint32_t* lds = lds_all[threadIdx.x >> 6];
@@ -1687,12 +1687,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   const uint32_t c_max = wave_max_u32(act ? sc.c : 0u), c_min = wave_min_u32(act ? sc.c : ~0u);
 
   double ubest = -1.0;                      // node lane (U nodes)
-  double* ulow = reinterpret_cast<double*>(lds + ULOW) + lane;
-  *ulow = 1.0e300;
   uint32_t uidx = 0xffffffffu, uties = 0;
   // pod lane, every per-pod node: integer scores (static part + basic, exact below 2^53);
   // (0, 0 ties) is the empty state -- a first score of 0 counts as a tie of it
-  uint64_t rbest = 0, rlow = ~0ull;
+  uint64_t rbest = 0;
   uint32_t ridx = 0xffffffffu, rties = 0;
   auto to_u = [](double x) {  // an integer-valued double in [0, 2^52) -> its value
     return (uint64_t)__double_as_longlong(x + 4503599627370496.0) - 0x4330000000000000ull;
@@ -1770,15 +1768,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       nq_hi = min(nq_hi, cnt);
       // fs[nq_lo + i]: a pod with m <= thr_i qualifies card nq_lo + i too (the free order
       // is descending); 0 past the node's range (only m == 0 meets it, and then every
-      // lower threshold as well)
+      // lower threshold as well).  Read back by index from the lane's record slot, where
+      // the frees are staged (the slot is overwritten by a record further down).
       const uint32_t range = nq_hi - nq_lo;
-      uint32_t thr = 0, thr1 = 0, thr2 = 0;
+      uint32_t* rec = lds + RECS + lane * REC;
+      if constexpr (K >= 4) {
 #pragma unroll
-      for (int t = 0; t < K; ++t) {
-        thr = (uint32_t)t == nq_lo ? fs.v[t] : thr;
-        thr1 = (uint32_t)t == nq_lo + 1u && range > 1u ? fs.v[t] : thr1;
-        thr2 = (uint32_t)t == nq_lo + 2u && range > 2u ? fs.v[t] : thr2;
+        for (int t = 0; t < K; t += 4)
+          *reinterpret_cast<uint4*>(rec + t) =
+              make_uint4(fs.v[t], fs.v[t + 1], fs.v[t + 2], fs.v[t + 3]);
+      } else {
+#pragma unroll
+        for (int t = 0; t < K; ++t) rec[t] = fs.v[t];
       }
+      const uint32_t thr = nq_lo < (uint32_t)K ? rec[nq_lo] : 0u;
+      const uint32_t thr1 = range > 1u && nq_lo + 1u < (uint32_t)K ? rec[nq_lo + 1u] : 0u;
+      const uint32_t thr2 = range > 2u && nq_lo + 2u < (uint32_t)K ? rec[nq_lo + 2u] : 0u;
       // the static part as an integer (< 2^52: its f64 bits above 2^52's)
       const double stat_d =
           __longlong_as_double((long long)((uint64_t)h0.x | ((uint64_t)h0.y << 32)));
@@ -1788,7 +1793,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       // wave (two with several reciprocal sets) gets a record: its clock, the wave's mask,
       // the thresholds, the static part and the basic scores -- the per-pod pass reads it
       // with three broadcast LDS loads.
-      uint32_t* rec = lds + RECS + lane * REC;
       if (uni_max) {
         // CalculateCardScore terms (algorithm.go:280-291) with the wave's reciprocals: from
         // the G table when they are G's (the same integers), else computed
@@ -1801,9 +1805,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
           for (int t = 0; t < K; ++t) {
             const uint32_t b = ts.v[t];
             lds[lane * PSW + t + 1] = b;
-            sel = (uint32_t)(t + 1) == nq_lo ? b : sel;
             if constexpr (TOPK) sel_hi = (uint32_t)(t + 1) == nq_hi ? b : sel_hi;
           }
+          sel = lds[lane * PSW + nq_lo];  // B[nq_lo], read back
         } else {
           const uint32_t shared = card_shared_terms(bw, ck, core, pw, u_bw, u_core, u_pow);
           auto row = [&](auto rk) {
@@ -1813,11 +1817,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
               acc += mem_term<decltype(rk)::value>(fs.v[t], ts.v[t], u_free, u_tot, args.mt);
               const uint32_t b = (uint32_t)(t + 1) * shared + acc;
               lds[lane * PSW + t + 1] = b;
-              sel = (uint32_t)(t + 1) == nq_lo ? b : sel;
               if constexpr (TOPK) sel_hi = (uint32_t)(t + 1) == nq_hi ? b : sel_hi;
             }
           };
           row(std::integral_constant<bool, RK>{});
+          sel = lds[lane * PSW + nq_lo];  // B[nq_lo], read back
         }
         // Mixed-model nodes (cards of several GPU models): when every card's clock test
         // (clock >= c, algorithm.go:271) comes out the same for every pod of the wave, the
@@ -1897,7 +1901,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
           } else if (raw == ubest) {
             ++uties;
           }
-          *ulow = fmin(*ulow, raw);
         }
         const bool is_rec = fast && range <= 3u && !is_u;
         rec_b = ballot(is_rec);
@@ -1988,7 +1991,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       ridx = gt ? nn : (eq ? min(ridx, nn) : ridx);
       rties = gt ? 1u : rties + (eq ? 1u : 0u);
       rbest = gt ? raw : rbest;
-      rlow = (f & (raw < rlow)) ? raw : rlow;
     };
     while (rb) {  // R records per trip: all their LDS loads in flight before the first use
 #ifndef YODA_K2_R
@@ -2146,16 +2148,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   for (int o = kWave / 2; o > 0; o >>= 1) wb = fmax(wb, __shfl_xor(wb, o, kWave));
   const bool top = ubest == wb && uties > 0;
   uint32_t wi = top ? uidx : 0xffffffffu, wt = top ? uties : 0u;
-  double wl = *ulow;
 #pragma unroll
   for (int o = kWave / 2; o > 0; o >>= 1) {
     wi = min(wi, (uint32_t)__shfl_xor((int)wi, o, kWave));
     wt += (uint32_t)__shfl_xor((int)wt, o, kWave);
-    wl = fmin(wl, __shfl_xor(wl, o, kWave));
   }
   if (!live) return;
   // the per-pod nodes' state (exact: every score < 2^53), then the U nodes
-  double best = rties > 0 ? (double)rbest : -1.0, low = rties > 0 ? (double)rlow : 1.0e300;
+  double best = rties > 0 ? (double)rbest : -1.0;
   uint32_t idx = ridx, ties = rties;
   if (act && wt > 0) {
     if (wb > best) {
@@ -2166,13 +2166,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       idx = min(idx, wi);
       ties += wt;
     }
-    low = fmin(low, wl);
   }
   const size_t o = (size_t)chunk * n_pods + p;
   pbest[o] = best;
   pidx[o] = idx;
   pties[o] = ties;
-  plow[o] = low;
 }
 
 // Merge the per-chunk top-k lists of each pod (chunks in node order, so the strict '>'
@@ -3144,7 +3142,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce2(const double* __restrict__ p
     const size_t o = (size_t)c * n_pods + p;
     int64_t b, l;
     if (is_f64) {
-      const double bf = pbest_f[o], lf = plow_f[o];
+      const double bf = pbest_f[o], lf = plow_f ? plow_f[o] : 1.0e300;
       b = bf < 0.0 ? -1 : (int64_t)bf;
       l = lf > 9.0e18 ? kI64Max : (int64_t)lf;
     } else {
@@ -3164,7 +3162,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce2(const double* __restrict__ p
   best_out[p] = best;
   idx_out[p] = idx == 0xffffffffu ? idx : idx + node_offset;
   ties_out[p] = ties;
-  low_out[p] = low;
+  low_out[p] = (is_f64 && !plow_f) ? best : low;  // no lowest scores: the best in its place
 }
 
 // Wave-per-pod variant of k_reduce2 (many chunks).  Each lane merges a strided subset of
@@ -3188,7 +3186,7 @@ __global__ __launch_bounds__(kWave) void k_reduce2_wave(const double* __restrict
     const size_t o = (size_t)c * n_pods + p;
     int64_t b, l;
     if (is_f64) {
-      const double bf = pbest_f[o], lf = plow_f[o];
+      const double bf = pbest_f[o], lf = plow_f ? plow_f[o] : 1.0e300;
       b = bf < 0.0 ? -1 : (int64_t)bf;
       l = lf > 9.0e18 ? kI64Max : (int64_t)lf;
     } else {
@@ -3225,7 +3223,7 @@ __global__ __launch_bounds__(kWave) void k_reduce2_wave(const double* __restrict
   best_out[p] = best;
   idx_out[p] = idx == 0xffffffffu ? idx : idx + node_offset;
   ties_out[p] = ties;
-  low_out[p] = low;
+  low_out[p] = (is_f64 && !plow_f) ? best : low;  // no lowest scores: the best in its place
 }
 
 // Multi-GPU: after the MAX all-reduce of best, keep idx/ties only on shards that reach the
