@@ -17,6 +17,10 @@
 #include <string>
 #include <vector>
 #include <thread>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <array>
 
 #include "../../include/yoda.h"
@@ -490,6 +494,85 @@ uint64_t static_score(uint64_t free_sum, uint64_t total_sum, uint64_t alloc, boo
 // YODA_MIN_CHUNK_NODES (default 0 = no floor; a floor keeps the per-(wave, chunk) set-up of
 // the block-classified kernels amortised when few pod blocks would otherwise mean many
 // small chunks, e.g. one rank's pod shard).  Read once per process.
+// Host worker pool for the packing loops (pod upload): threads created once per process and
+// parked on a condition variable between calls -- spawning 15 threads per upload cost more
+// than the packing itself.  run(n, fn) calls fn(0..n-1) once each, the caller taking part;
+// calls are serialised (one batch at a time).
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool pool;
+    return pool;
+  }
+  uint32_t size() const { return (uint32_t)threads_.size() + 1u; }
+  void run(uint32_t n, const std::function<void(uint32_t)>& fn) {
+    if (n == 0) return;
+    if (n == 1 || threads_.empty()) {
+      for (uint32_t i = 0; i < n; ++i) fn(i);
+      return;
+    }
+    std::lock_guard<std::mutex> serial(call_mu_);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &fn;
+      n_ = n;
+      next_.store(0);
+      left_ = n;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return left_ == 0; });
+    fn_ = nullptr;
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : threads_) t.join();
+  }
+
+ private:
+  HostPool() {
+    const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const uint32_t n = std::min(16u, hw) - 1u;  // + the calling thread
+    for (uint32_t i = 0; i < n; ++i) threads_.emplace_back([this] { loop(); });
+  }
+  void work() {
+    for (;;) {
+      const uint32_t i = next_.fetch_add(1);
+      if (i >= n_) return;
+      (*fn_)(i);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--left_ == 0) done_cv_.notify_one();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  std::vector<std::thread> threads_;
+  std::mutex mu_, call_mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(uint32_t)>* fn_ = nullptr;
+  uint32_t n_ = 0, left_ = 0;
+  std::atomic<uint32_t> next_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 static uint32_t env_u32(const char* name, uint32_t dflt) {
   const char* s = std::getenv(name);
   return (s && *s) ? (uint32_t)std::strtoul(s, nullptr, 10) : dflt;
@@ -1644,6 +1727,12 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
       off[a] = total;
       total += ((size_t)std::max<uint32_t>(P, 1) * kPodArrayBytes[a] + 255) / 256 * 256;
     }
+    static const bool dbg = std::getenv("YODA_UPLOAD_DEBUG") != nullptr;
+    auto now_ms = [] {
+      return std::chrono::duration<double, std::milli>(
+                 std::chrono::steady_clock::now().time_since_epoch()).count();
+    };
+    const double t_start = dbg ? now_ms() : 0.0;
     if (h->stage_pending) HIP_TRY(h, hipEventSynchronize(h->stage_event));  // staging reuse
     HIP_TRY(h, h->pod_stage.ensure(total));
     HIP_TRY(h, h->pod_blob.ensure(total));
@@ -1705,7 +1794,9 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
         mn[i] = std::min(mn[i], vmin);
       }
     };
-    auto pack_range = [&](uint32_t p0, uint32_t p1, GroupTable& gt, uint64_t* kor) {
+    auto pack_range = [&](uint32_t p0, uint32_t p1, GroupTable& gt, uint64_t* kor_out) {
+      // (ORs accumulated locally: the per-thread outputs share cache lines)
+      uint64_t kor[3] = {0ull, 0ull, 0ull};
       uint64_t g_last = ~0ull;
       uint32_t g_run = 0;
       uint64_t r_max = 0, r_min = ~0ull;  // the current run's extremes
@@ -1747,28 +1838,28 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
         }
       }
       if (g_run) gt.add(g_last, g_run, r_max, r_min);
+      for (int f = 0; f < 3; ++f) kor_out[f] = kor[f];
     };
-    const uint32_t n_thr = std::min<uint32_t>(
-        {16u, std::max(1u, std::thread::hardware_concurrency()), std::max(1u, P / 16384u)});
+    // ranges of >= 4096 pods over the process's worker pool (HostPool)
+    static const uint32_t thr_cap = env_u32("YODA_UPLOAD_THREADS", 16);
+    const uint32_t n_thr = std::min<uint32_t>({HostPool::get().size(), std::max(1u, thr_cap),
+                                               std::max(1u, P / 4096u)});
     std::vector<GroupTable> tables(n_thr);
     std::vector<std::array<uint64_t, 3>> kors(n_thr, {0ull, 0ull, 0ull});
     {
-      std::vector<std::thread> pool;
       std::vector<uint8_t> thr_failed(n_thr, 0);  // a worker's exception (bad_alloc) -> rethrown
       const uint32_t per = (P + n_thr - 1) / n_thr;
-      auto worker = [&](uint32_t t) {
+      HostPool::get().run(n_thr, [&](uint32_t t) {
         try {
           pack_range(std::min(P, t * per), std::min(P, (t + 1) * per), tables[t], kors[t].data());
         } catch (...) {
           thr_failed[t] = 1;
         }
-      };
-      for (uint32_t t = 1; t < n_thr; ++t) pool.emplace_back(worker, t);
-      worker(0);
-      for (auto& th : pool) th.join();
+      });
       for (uint8_t f : thr_failed)
         if (f) throw std::bad_alloc();
     }
+    const double t_packed = dbg ? now_ms() : 0.0;
     GroupTable all = std::move(tables[0]);
     for (uint32_t t = 1; t < n_thr; ++t)
       for (size_t j = 0; j < tables[t].key.size(); ++j)
@@ -1781,7 +1872,9 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     std::vector<uint64_t>& gmax = all.mx;
     std::vector<uint64_t>& gmin = all.mn;
     const size_t g_n = all.n;
+    const double t_merged = dbg ? now_ms() : 0.0;
     HIP_TRY(h, hipMemcpyAsync(h->pod_blob.p, st, total, hipMemcpyHostToDevice, h->stream));
+    const double t_copied = dbg ? now_ms() : 0.0;
     if (h->has_nodes && h->mem_ranks)  // scv/memory -> its rank threshold, on the device
       HIP_TRY(h, launch_mem_rank(reinterpret_cast<const uint64_t*>(
                                      h->pod_blob.as<unsigned char>() + off[kPodMU]),
@@ -1866,6 +1959,10 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     h->phase1_done = false;
     h->ordered = false;
     h->pods_diskio = pd->rio != nullptr && pd->rcpu != nullptr;
+    if (dbg)
+      std::fprintf(stderr, "yoda_upload_pods: %u pods, %u threads: pack %.3f merge %.3f copy %.3f "
+                   "groups %.3f ms\n", P, n_thr, t_packed - t_start, t_merged - t_packed,
+                   t_copied - t_merged, now_ms() - t_copied);
     return YODA_OK;
   } catch (const std::bad_alloc&) {
     return fail(h, YODA_ERR_INVALID_ARG, "host allocation failed");
