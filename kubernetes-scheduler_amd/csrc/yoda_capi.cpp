@@ -134,6 +134,13 @@ hipError_t launch_k1_witness(int K, Path path, const unsigned char* nodes, uint3
                              uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                              uint32_t n_pods, uint64_t* pmax, uint32_t* pwit, uint32_t* pcnt,
                              uint64_t* bm, uint32_t bm_stride, hipStream_t s);
+hipError_t launch_k1_block_witness(int K, const unsigned char* nodes, const unsigned char* sum,
+                                   const unsigned char* sum2, const unsigned char* mix,
+                                   uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C,
+                                   const PodParams& pp, uint32_t n_pods, uint64_t* pmax,
+                                   uint32_t* pwit, uint32_t* pcnt, uint64_t* bm,
+                                   uint32_t bm_stride, BlockMask* bs, uint32_t bs_stride,
+                                   uint64_t* blk, uint32_t blk_stride, hipStream_t s);
 hipError_t launch_reduce_wit(const uint64_t* pmax, const uint32_t* pwit, const uint32_t* pcnt,
                              uint32_t C, uint32_t n_pods, uint32_t node_offset, uint64_t* maxima,
                              uint32_t* counts, uint32_t* wcount, uint32_t* wnode, const MemTab& mt, hipStream_t s);
@@ -1000,9 +1007,24 @@ int phase1_witness(yoda_t* h, uint64_t* maxima, uint32_t* counts, uint32_t* wit,
   }
   HIP_TRY(h, h->p_wit.ensure(12 * (size_t)h->C1 * P * 4));
   Partials part = partials(h);
-  HIP_TRY(h, launch_k1_witness(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk1, h->C1,
-                               pod_params(h), P, part.max_u, h->p_wit.as<uint32_t>(), part.cnt,
-                               h->bitmask.as<uint64_t>(), bm_row(N), h->stream));
+  static const bool block_wit = env_u32("YODA_BLOCK_WITNESS", 1) != 0;
+  if (block_wit && h->path == Path::N32 && h->has_k1sum && h->has_k2sum && h->all_one_model) {
+    // block-classified, like phase 1's K1: sparse masks and the block list for the window's K2
+    h->bm_sparse = true;
+    h->blk_valid = true;
+    HIP_TRY(h, hipMemsetAsync(h->blk.p, 0, (size_t)(P + 63) / 64 * blk_row(N) * 8, h->stream));
+    HIP_TRY(h, launch_k1_block_witness(h->K, h->nodes.as<unsigned char>(),
+                                       h->k1sum.as<unsigned char>(), h->k2sum.as<unsigned char>(),
+                                       h->kmix.as<unsigned char>(), N, h->chunk1, h->C1,
+                                       pod_params(h), P, part.max_u, h->p_wit.as<uint32_t>(),
+                                       part.cnt, h->bitmask.as<uint64_t>(), bm_row(N),
+                                       h->bsum.as<BlockMask>(), bs_row(N), h->blk.as<uint64_t>(),
+                                       blk_row(N), h->stream));
+  } else {
+    HIP_TRY(h, launch_k1_witness(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk1, h->C1,
+                                 pod_params(h), P, part.max_u, h->p_wit.as<uint32_t>(), part.cnt,
+                                 h->bitmask.as<uint64_t>(), bm_row(N), h->stream));
+  }
   HIP_TRY(h, launch_reduce_wit(part.max_u, h->p_wit.as<uint32_t>(), part.cnt, h->C1, P,
                                node_offset, maxima, counts, wit, wit + 6 * (size_t)P, pod_params(h).mt, h->stream));
   return YODA_OK;

@@ -580,11 +580,14 @@ __global__ __launch_bounds__(kWave) void k_reduce_wit(const uint64_t* __restrict
 #endif
 // MIX = false: a snapshot whose every node is one GPU model with one TotalMemory (no per-card
 // work in K1 at all): the same kernel with the per-card branches compiled out.
-template <int K, bool STATS, bool MIX = true>
+// WIT (capacity greedy windows, with MIX = false): also the witnesses of every maximum (how
+// many nodes reach it, the lowest one; k1_witness's outputs), in k1_witness's partial layout:
+// pmax [6][C][P] u64, pwit [2][6][C][P], pcnt [2][C][P].
+template <int K, bool STATS, bool MIX = true, bool WIT = false>
 #ifndef YODA_K1_WAVES
 #define YODA_K1_WAVES 7
 #endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 ? 5 : YODA_K1_WAVES))) void k1_block_n32(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 : (K >= 16 ? 5 : YODA_K1_WAVES)))) void k1_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum,
     const uint32_t* __restrict__ sum2w, const uint32_t* __restrict__ mixw,
     const uint32_t* __restrict__ x1w,
@@ -594,7 +597,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
     uint32_t n_pods, uint64_t* __restrict__ pmax, uint32_t* __restrict__ pcnt,
     uint64_t* __restrict__ bm, uint32_t bm_stride, BlockMask* __restrict__ bs,
     uint32_t bs_stride, uint64_t* __restrict__ blk, uint32_t blk_stride,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats, uint32_t* __restrict__ pwit = nullptr) {
+  static_assert(!(WIT && MIX), "the witness K1 serves one-model snapshots");
   constexpr uint32_t SS = k1sum_stride(K);
   constexpr uint32_t NS = n32_stride(K);
   constexpr uint32_t S2 = k2sum_stride(K), MS = mix_stride(K), XS = x1_stride(K);
@@ -664,6 +668,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
   // node-lane maxima of the ALL nodes (their contribution is the same for every pod lane)
   uint32_t a_bw = 0, a_ck = 0, a_core = 0, a_free = 0, a_pw = 0, a_tot = 0;
   uint32_t nf_all = 0, nz_all = 0;
+  // WIT: per field, the pod lane's witness count / lowest witness of mx (per-pod nodes), and
+  // the node lane's maximum / count / lowest node over the ALL nodes it holds
+  uint32_t wc[WIT ? 6 : 1], wn[WIT ? 6 : 1], aw[WIT ? 6 : 1], ac[WIT ? 6 : 1], al[WIT ? 6 : 1];
+  if constexpr (WIT) {
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+      wc[f] = ac[f] = 0u;
+      wn[f] = al[f] = 0xffffffffu;
+      aw[f] = 1u;
+    }
+  }
   // blocks with a feasible pod of this wave, for K2 (bit b of word b/64; flushed with an
   // atomic OR when the word changes -- neighbouring chunks may share a word)
   uint64_t* blkw = blk + (size_t)uniform_u32(p >> 6) * blk_stride;
@@ -849,6 +864,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
       a_free = max(a_free, mrf1 - (mrf1 != 0u ? 1u : 0u));
       a_pw = max(a_pw, pw);
       a_tot = max(a_tot, tot);
+      if constexpr (WIT) {  // nodes in increasing order per lane: the first witness is lowest
+        const uint32_t v[6] = {bw, ck, core, mrf1 - (mrf1 != 0u ? 1u : 0u), pw, tot};
+#pragma unroll
+        for (int f = 0; f < 6; ++f) {
+          const bool gt = v[f] > aw[f], eq = v[f] == aw[f];
+          ac[f] = gt ? 1u : ac[f] + (eq ? 1u : 0u);
+          al[f] = gt ? nb + lane : al[f];
+          aw[f] = gt ? v[f] : aw[f];
+        }
+      }
     }
     uint32_t lo = is_all ? (uint32_t)live_mask : 0u;
     uint32_t hi = is_all ? (uint32_t)(live_mask >> 32) : 0u;
@@ -907,12 +932,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
         nf += f ? 1u : 0u;
         nz += (f & ((mj & kSumZeroTotal) != 0u)) ? 1u : 0u;
         const bool q = f & (ckj >= c) & (mrfj > m);  // collection.go:46, one-model node
-        mx[kMaxBw] = max(mx[kMaxBw], q ? r3[k].x : 0u);
-        mx[kMaxClock] = max(mx[kMaxClock], q ? ckj : 0u);
-        mx[kMaxCore] = max(mx[kMaxCore], q ? r3[k].y : 0u);
-        mx[kMaxFree] = max(mx[kMaxFree], q ? mrfj - 1u : 0u);
-        mx[kMaxPower] = max(mx[kMaxPower], q ? r4[k].x : 0u);
-        mx[kMaxTotal] = max(mx[kMaxTotal], q ? r4[k].y : 0u);
+        if constexpr (WIT) {  // the node's values against the lane's maxima and witnesses
+          const uint32_t v[6] = {r3[k].x, ckj, r3[k].y, mrfj - 1u, r4[k].x, r4[k].y};
+#pragma unroll
+          for (int g = 0; g < 6; ++g) {
+            const bool gt = q & (v[g] > mx[g]), eq = q & (v[g] == mx[g]);
+            wc[g] = gt ? 1u : wc[g] + (eq ? 1u : 0u);
+            wn[g] = gt ? nb + jj[k] : wn[g];
+            mx[g] = gt ? v[g] : mx[g];
+          }
+        } else {
+          mx[kMaxBw] = max(mx[kMaxBw], q ? r3[k].x : 0u);
+          mx[kMaxClock] = max(mx[kMaxClock], q ? ckj : 0u);
+          mx[kMaxCore] = max(mx[kMaxCore], q ? r3[k].y : 0u);
+          mx[kMaxFree] = max(mx[kMaxFree], q ? mrfj - 1u : 0u);
+          mx[kMaxPower] = max(mx[kMaxPower], q ? r4[k].x : 0u);
+          mx[kMaxTotal] = max(mx[kMaxTotal], q ? r4[k].y : 0u);
+        }
         const uint64_t b = ballot(f);
         if (vv[k]) set_lane(lo, hi, b, jj[k]);
       }
@@ -954,6 +990,39 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K >= 16 
     tr[1] = wall_clock64();
     tr[2] = npart;
     tr[3] = 0ull;
+  }
+  if constexpr (WIT) {
+    // the ALL nodes' maxima, witness counts and lowest witnesses, folded into every pod lane
+    // (the same rule as a node's: a larger maximum replaces, an equal one adds)
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+      const uint32_t M = wave_max_u32(aw[f]);
+      uint32_t cnt = aw[f] == M ? ac[f] : 0u, low = aw[f] == M ? al[f] : 0xffffffffu;
+#pragma unroll
+      for (int o = kWave / 2; o > 0; o >>= 1) {
+        cnt += (uint32_t)__shfl_xor((int)cnt, o, kWave);
+        low = min(low, (uint32_t)__shfl_xor((int)low, o, kWave));
+      }
+      if (M > mx[f]) {
+        mx[f] = M;
+        wc[f] = cnt;
+        wn[f] = low;
+      } else if (M == mx[f]) {
+        wc[f] += cnt;
+        wn[f] = min(wn[f], low);
+      }
+    }
+    if (!live) return;
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+      const size_t o = ((size_t)f * C + chunk) * n_pods + p;
+      pmax[o] = (uint64_t)mx[f];
+      pwit[o] = wc[f];
+      pwit[(size_t)6 * C * n_pods + o] = wn[f];
+    }
+    pcnt[((size_t)0 * C + chunk) * n_pods + p] = nf + nf_all;
+    pcnt[((size_t)1 * C + chunk) * n_pods + p] = nz + nz_all;
+    return;
   }
   // fold the ALL nodes into every pod lane
   a_bw = wave_max_u32(a_bw);
@@ -4031,6 +4100,24 @@ hipError_t launch_bitmask_transpose(const uint64_t* bm, uint32_t bm_stride, cons
   const MaskSrc ms{bm, bs, bm_stride, bs_stride};
   hipLaunchKernelGGL(k_bitmask_transpose, grid, dim3(kBlock), 0, s, ms, n_nodes, W,
                      n_pods, perm, out);
+  return hipGetLastError();
+}
+
+// The block K1 with witnesses (one-model N32 snapshots with summaries): sparse masks, blk.
+hipError_t launch_k1_block_witness(int K, const unsigned char* nodes, const unsigned char* sum,
+                                   const unsigned char* sum2, const unsigned char* mix,
+                                   uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C,
+                                   const PodParams& pp, uint32_t n_pods, uint64_t* pmax,
+                                   uint32_t* pwit, uint32_t* pcnt, uint64_t* bm,
+                                   uint32_t bm_stride, BlockMask* bs, uint32_t bs_stride,
+                                   uint64_t* blk, uint32_t blk_stride, hipStream_t s) {
+  dim3 grid((n_pods + kBlock - 1) / kBlock, C);
+  YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK, false, false, true>), grid, dim3(kBlock),
+                                      0, s, nodes, sum, reinterpret_cast<const uint32_t*>(sum2),
+                                      reinterpret_cast<const uint32_t*>(mix), pp.x1, n_nodes,
+                                      chunk_nodes, pp.m_32, pp.c_32, pp.number, pp.need_mem,
+                                      pp.need_clk, n_pods, pmax, pcnt, bm, bm_stride, bs,
+                                      bs_stride, blk, blk_stride, nullptr, pwit));
   return hipGetLastError();
 }
 
