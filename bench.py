@@ -381,9 +381,22 @@ def disclosure(y, nodes, pods, step, barrier, args) -> dict:
             z.class_stats(False)
             v["classes"] = z.class_stats()
         if mode == MODE_DISKIO:
-            v["pod_classes"] = diskio_classes(pd)
-            # K2B: 16 B of node record per node and class, 24 B out per pod; f64 work per pair
-            v["k2b_unique_bytes"] = nd.n_nodes * 16 + pd.n_pods * 24
+            D = diskio_classes(pd)
+            v["pod_classes"] = D
+            # K2B roofline (Mode B): D x N class-node pairs, each 3 f64 VALU ops
+            # (a = alpha V, b = beta U, d = a - b) + 2 compares + a carry-add = 6 VALU
+            # instructions per 64 pairs on one SIMD (4 cycles each, full rate) -- issue-bound;
+            # bytes: 16 B per node record and 24 B out per pod
+            cn_pairs = D * nd.n_nodes
+            simd_rate = 1024 * 2.4e9 / 4  # wave instructions / s: 256 CUs x 4 SIMDs, 2.4 GHz
+            ideal_ms = cn_pairs * 6 / 64 / simd_rate * 1e3
+            k2 = v["k2_ms"]
+            v["k2b_roofline"] = {
+                "bound": "valu_issue", "class_node_pairs": cn_pairs, "valu_per_pair": 6,
+                "ideal_ms": ideal_ms, "frac": ideal_ms / k2 if k2 > 0 else None,
+                "unique_bytes": nd.n_nodes * 16 + pd.n_pods * 24,
+                "hbm_frac": ((nd.n_nodes * 16 + pd.n_pods * 24) / (k2 / 1e3) / 1e9 / HBM_PEAK_GBS
+                             if k2 > 0 else None)}
         variants[name] = v
         z.close()
 

@@ -218,13 +218,14 @@ struct PinnedBuf {
   void* p = nullptr;
   size_t bytes = 0;
   void* dp = nullptr;  // the same pages as seen by kernels (hipHostMalloc maps them)
+  unsigned flags = hipHostMallocDefault;  // hipHostMallocCoherent: polled by the host
   hipError_t ensure(size_t n) {
     if (n <= bytes) return hipSuccess;
     if (p) (void)hipHostFree(p);
     p = dp = nullptr;
     bytes = 0;
     const size_t alloc = std::max<size_t>(n, 4096);
-    hipError_t e = hipHostMalloc(&p, alloc, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&p, alloc, flags);
     if (e == hipSuccess) e = hipHostGetDevicePointer(&dp, p, 0);
     if (e == hipSuccess) bytes = alloc;
     return e;
@@ -377,6 +378,7 @@ struct yoda_handle {
   DevBuf p_wit, wit;        // capacity greedy: witness partials [2][6][C][P], merged [2][6][P]
   DevBuf one_feas, one_part, one_done, one_out;  // k_one_*: a pod against the current state
   PinnedBuf upd_stage, pick_stage, win_stage;
+  PinnedBuf poll_stage;  // coherent: the greedy fallback's pick, polled by the host
   uint32_t greedy_restarts = 0;
   hipEvent_t upd_event = nullptr;
   bool upd_pending = false;
@@ -454,6 +456,7 @@ struct yoda_handle {
     pod_stage.release();
     upd_stage.release();
     pick_stage.release();
+    poll_stage.release();
     win_stage.release();
     if (stage_event) (void)hipEventDestroy(stage_event);
     if (switch_event) (void)hipEventDestroy(switch_event);
@@ -1008,14 +1011,25 @@ int phase1_witness(yoda_t* h, uint64_t* maxima, uint32_t* counts, uint32_t* wit,
   HIP_TRY(h, h->p_wit.ensure(12 * (size_t)h->C1 * P * 4));
   Partials part = partials(h);
   static const bool block_wit = env_u32("YODA_BLOCK_WITNESS", 1) != 0;
+  uint32_t C = h->C1;
   if (block_wit && h->path == Path::N32 && h->has_k1sum && h->has_k2sum && h->all_one_model) {
-    // block-classified, like phase 1's K1: sparse masks and the block list for the window's K2
+    // block-classified, like phase 1's K1: sparse masks and the block list for the window's K2.
+    // Its per-(wave, chunk) epilogue (18 wave reductions, 104 B of partials a pod) is the
+    // cost that grows with the chunk count: chunks of >= YODA_WIT_CHUNK_NODES nodes
+    static const uint32_t wit_chunk = std::max<uint32_t>(
+        kChunkAlign, env_u32("YODA_WIT_CHUNK_NODES", 512) / kChunkAlign * kChunkAlign);
+    uint32_t chunk = h->chunk1;
+    if (chunk < wit_chunk) {
+      chunk = wit_chunk;
+      C = std::max<uint32_t>(1, (N + chunk - 1) / chunk);
+      if (C >= 8) C = (C + 7) / 8 * 8;  // XCD tiling; trailing chunks may be empty
+    }
     h->bm_sparse = true;
     h->blk_valid = true;
     HIP_TRY(h, hipMemsetAsync(h->blk.p, 0, (size_t)(P + 63) / 64 * blk_row(N) * 8, h->stream));
     HIP_TRY(h, launch_k1_block_witness(h->K, h->nodes.as<unsigned char>(),
                                        h->k1sum.as<unsigned char>(), h->k2sum.as<unsigned char>(),
-                                       h->kmix.as<unsigned char>(), N, h->chunk1, h->C1,
+                                       h->kmix.as<unsigned char>(), N, chunk, C,
                                        pod_params(h), P, part.max_u, h->p_wit.as<uint32_t>(),
                                        part.cnt, h->bitmask.as<uint64_t>(), bm_row(N),
                                        h->bsum.as<BlockMask>(), bs_row(N), h->blk.as<uint64_t>(),
@@ -1025,7 +1039,7 @@ int phase1_witness(yoda_t* h, uint64_t* maxima, uint32_t* counts, uint32_t* wit,
                                  pod_params(h), P, part.max_u, h->p_wit.as<uint32_t>(), part.cnt,
                                  h->bitmask.as<uint64_t>(), bm_row(N), h->stream));
   }
-  HIP_TRY(h, launch_reduce_wit(part.max_u, h->p_wit.as<uint32_t>(), part.cnt, h->C1, P,
+  HIP_TRY(h, launch_reduce_wit(part.max_u, h->p_wit.as<uint32_t>(), part.cnt, C, P,
                                node_offset, maxima, counts, wit, wit + 6 * (size_t)P, pod_params(h).mt, h->stream));
   return YODA_OK;
 }
@@ -1199,6 +1213,14 @@ int topk_lists(yoda_t* h, uint32_t P, uint32_t KT, const uint32_t* d_counts) {
     static const uint32_t rt_env = env_u32("YODA_TOPK_ROUNDS", 0);
     const uint32_t rt = rt_env ? rt_env : (P >= 2048 ? 4u : 1u);
     plan_chunks_for((uint32_t)capacity(h, 2, YODA_MODE_SCV), rt, P, N, &Ct, &cht);
+    // YODA_TOPK_MIN_CHUNK (A/B knob): chunks of at least that many nodes -- fewer per-(wave,
+    // chunk) lists to write and merge in small windows
+    static const uint32_t tk_min = env_u32("YODA_TOPK_MIN_CHUNK", 0);
+    if (tk_min && cht < tk_min) {
+      cht = (tk_min + kChunkAlign - 1) / kChunkAlign * kChunkAlign;
+      Ct = std::max<uint32_t>(1, (N + cht - 1) / cht);
+      if (Ct >= 8) Ct = (Ct + 7) / 8 * 8;
+    }
     HIP_TRY(h, h->tk_s_part.ensure((size_t)Ct * P * KT * 8));
     HIP_TRY(h, launch_k2_topk_block(h->K, h->nodes.as<unsigned char>(),
                                     h->k2sum.as<unsigned char>(),
@@ -2547,17 +2569,37 @@ int greedy_eval_fast(GreedyState& g, uint32_t s, int32_t* pick_out) {
   double* ps = h->g1_part.as<double>();
   uint32_t* pi = reinterpret_cast<uint32_t*>(ps + nb);
   uint32_t* done = h->g1_done.as<uint32_t>();
-  // the last block writes the pick straight into mapped pinned memory: no copy
-  HIP_TRY(h, h->pick_stage.ensure(16));
+  // the last block writes the pick straight into mapped (coherent) pinned memory: no copy,
+  // and the host polls the node word instead of synchronising the stream (the next device
+  // work is stream-ordered after this kernel anyway)
+  h->poll_stage.flags = hipHostMallocCoherent;
+  HIP_TRY(h, h->poll_stage.ensure(16));
+  volatile uint32_t* res = static_cast<volatile uint32_t*>(h->poll_stage.p) + 1;
+  constexpr uint32_t kPending = 0xfffffffeu;  // never a node index (N < 2^31)
+  *res = kPending;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
   HIP_TRY(h, launch_greedy_one(h->K, h->path, h->nodes.as<unsigned char>(),
                                h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr, h->n_nodes,
                                pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(),
                                h->n_pods, s, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
                                h->bs_ptr(), bs_row(h->n_nodes), ps, pi, done,
-                               static_cast<uint32_t*>(h->pick_stage.dp) + 1, h->stream));
-  HIP_TRY(h, hipStreamSynchronize(h->stream));
+                               static_cast<uint32_t*>(h->poll_stage.dp) + 1, h->stream));
+  {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0; *res == kPending; ++spin) {
+      // past a generous bound (a stalled device, or memory the device cannot reach coherently
+      // on this system) the stream synchronisation decides
+      if ((spin & 1023u) == 0u &&
+          std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+        HIP_TRY(h, hipStreamSynchronize(h->stream));
+        break;
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  }
   // (word 1: the kernel's out[0]; its f64 score follows 8-byte aligned at word 2)
-  const uint32_t n = static_cast<const volatile uint32_t*>(h->pick_stage.p)[1];
+  const uint32_t n = *res;
+  if (n == kPending) return fail(h, YODA_ERR_STATE, "greedy: the fallback's result never arrived");
   if (n == 0xffffffffu) return fail(h, YODA_ERR_INVALID_ARG, "greedy: no feasible node found");
   *pick_out = (int32_t)(n + h->node_offset);
   return YODA_OK;

@@ -1801,8 +1801,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     const uint32_t* s = reinterpret_cast<const uint32_t*>(sum2) + sum_index(nb, 0, S2) + lane;
     const uint4 h0 = make_uint4(s[64 * kS2Static], s[64 * (kS2Static + 1)], s[64 * kS2Clock],
                                 s[64 * kS2Meta]);
-    const uint4 h1 = make_uint4(s[64 * kS2Bw], s[64 * kS2Core], s[64 * kS2Power],
-                                s[64 * kS2MinClk]);
+    // (bandwidth, core, power: only waves that compute their own card terms read them, i.e.
+    // not the G waves of a one-model snapshot; minclk: the mixed-model rows)
+    uint4 h1 = make_uint4(0u, 0u, 0u, 0u);
+    if (MIX || !use_g)
+      h1 = make_uint4(s[64 * kS2Bw], s[64 * kS2Core], s[64 * kS2Power], s[64 * kS2MinClk]);
     Group<uint32_t, K> fs, ts;  // ts: TotalMemory in free order, or (use_g) B[1..K]
 #pragma unroll
     for (int t = 0; t < K; ++t) fs.v[t] = s[64 * (kS2Fs + t)];
@@ -2579,8 +2582,11 @@ __global__ __launch_bounds__(kBlock) void k_greedy_one(
   __syncthreads();
   if (threadIdx.x == 0) {
     for (uint32_t k = 1; k < kBlock / kWave; ++k) merge(best, idx, red_s[k], red_i[k]);
-    out[0] = idx;
+    // the score first, then the node: a host polling out[0] (mapped memory) reads a complete
+    // result once the node word changes
     *reinterpret_cast<double*>(out + 1) = best;  // 8-byte aligned: out = done + 1 (sharded merge)
+    __threadfence_system();
+    __hip_atomic_store(out, idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     *done = 0u;
   }
 }
@@ -3831,15 +3837,21 @@ hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigne
   if ((tk != kTopK && tk != kTopKCap) || K > 8 || n_pods == 0) return hipErrorInvalidValue;
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g, pp.mix, pp.mt};
-#define YODA_TOPKB(TKV, RKV)                                                                    \
-  YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false, TKV, RKV>), grid, dim3(kBlock), 0, \
-                                      s, nodes, sum2, n_nodes, chunk_nodes, a, n_pods, bm,        \
-                                      bm_stride, bs, bs_stride, blk, blk_stride, nullptr,         \
-                                      nullptr, nullptr, nullptr, nullptr, keys, ib))
+#define YODA_TOPKB(TKV, RKV, MIXV)                                                              \
+  YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false, TKV, RKV, MIXV>), grid,            \
+                                      dim3(kBlock), 0, s, nodes, sum2, n_nodes, chunk_nodes, a,   \
+                                      n_pods, bm, bm_stride, bs, bs_stride, blk, blk_stride,      \
+                                      nullptr, nullptr, nullptr, nullptr, nullptr, keys, ib))
+  // one-model snapshots without memory ranks: the kernel without the mixed-model rows
+  const bool lean = pp.all_uni4 && !a.mt.vf;
   if (tk == kTopK) {
-    if (a.mt.vf) YODA_TOPKB(kTopK, true) else YODA_TOPKB(kTopK, false);
+    if (a.mt.vf) YODA_TOPKB(kTopK, true, true)
+    else if (lean) YODA_TOPKB(kTopK, false, false)
+    else YODA_TOPKB(kTopK, false, true);
   } else {
-    if (a.mt.vf) YODA_TOPKB(kTopKCap, true) else YODA_TOPKB(kTopKCap, false);
+    if (a.mt.vf) YODA_TOPKB(kTopKCap, true, true)
+    else if (lean) YODA_TOPKB(kTopKCap, false, false)
+    else YODA_TOPKB(kTopKCap, false, true);
   }
 #undef YODA_TOPKB
   return hipGetLastError();

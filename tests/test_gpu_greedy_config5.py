@@ -88,7 +88,10 @@ def test_config5_full_size(cfg5, flags):
 
     # 2. replay: one independent cycle at sampled queue positions across the batch
     rng = np.random.default_rng(17 + flags)
-    qs = np.unique(np.concatenate([[0, 2000, P // 2, P - 1],
+    # window boundaries (6144-pod windows) and their neighbours, where a window's candidate
+    # lists give way to the next window's
+    wb = np.array([6144 * k + d for k in (1, 40, 120) for d in (-1, 0, 1)])
+    qs = np.unique(np.concatenate([[0, 2000, P // 2, P - 1], wb[wb < P],
                                    rng.integers(0, P, size=8)]))
     two = Yoda(0)
     for q in qs:
@@ -105,4 +108,20 @@ def test_config5_full_size(cfg5, flags):
     sub = pods.slice(0, 64)
     np.testing.assert_array_equal(y.eval(sub, MODE_SCV).pick,
                                   oracle.schedule(nodes, sub, MODE_SCV, threads=8).pick)
+    y.close()
+
+
+@pytest.mark.parametrize("flags", [0, CAP])
+def test_config5_generator_several_windows_vs_oracle(flags):
+    """The config-5 generator at 14,000 pods x 8,000 nodes: more than two 6144-pod windows
+    (window boundaries, exact fallbacks / capacity restarts across them), every pick against
+    the sequential oracle."""
+    nodes, pods = synth.make_config(5, pods=14_000, nodes=8_000)
+    y = Yoda(0)
+    y.upload_nodes(nodes)
+    pick = y.greedy(pods, MODE_SCV, flags)
+    windows, _ = y.greedy_stats()
+    assert windows >= 3
+    want, _ = oracle.greedy(nodes, pods, MODE_SCV, flags)
+    np.testing.assert_array_equal(pick, want)
     y.close()
