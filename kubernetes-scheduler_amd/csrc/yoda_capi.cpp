@@ -1017,7 +1017,7 @@ int phase1_witness(yoda_t* h, uint64_t* maxima, uint32_t* counts, uint32_t* wit,
     // Its per-(wave, chunk) epilogue (18 wave reductions, 104 B of partials a pod) is the
     // cost that grows with the chunk count: chunks of >= YODA_WIT_CHUNK_NODES nodes
     static const uint32_t wit_chunk = std::max<uint32_t>(
-        kChunkAlign, env_u32("YODA_WIT_CHUNK_NODES", 512) / kChunkAlign * kChunkAlign);
+        kChunkAlign, env_u32("YODA_WIT_CHUNK_NODES", 64) / kChunkAlign * kChunkAlign);
     uint32_t chunk = h->chunk1;
     if (chunk < wit_chunk) {
       chunk = wit_chunk;
