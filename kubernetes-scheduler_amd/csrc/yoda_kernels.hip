@@ -3213,6 +3213,9 @@ __global__ __launch_bounds__(kBlock) void k_reduce2(const double* __restrict__ p
   if (p >= n_pods) return;
   int64_t best = -1, low = kI64Max;
   uint32_t idx = 0xffffffffu, ties = 0;
+  // branch-free, unrolled: every chunk's four words are loaded up front (several chunks in
+  // flight), then folded with selects; equal bests keep the earlier chunk's (lower) index
+#pragma unroll 4
   for (uint32_t c = 0; c < C; ++c) {
     const size_t o = (size_t)c * n_pods + p;
     int64_t b, l;
@@ -3224,15 +3227,12 @@ __global__ __launch_bounds__(kBlock) void k_reduce2(const double* __restrict__ p
       b = pbest_i[o];
       l = plow_i[o];
     }
-    if (b < 0) continue;
-    if (b > best) {
-      best = b;
-      idx = pidx[o];
-      ties = pties[o];
-    } else if (b == best) {
-      ties += pties[o];
-    }
-    low = l < low ? l : low;
+    const uint32_t ix = pidx[o], tt = pties[o];
+    const bool v = b >= 0, gt = v && b > best, eq = v && b == best;
+    idx = gt ? ix : idx;
+    ties = gt ? tt : (eq ? ties + tt : ties);
+    best = gt ? b : best;
+    low = (v && l < low) ? l : low;
   }
   best_out[p] = best;
   idx_out[p] = idx == 0xffffffffu ? idx : idx + node_offset;
