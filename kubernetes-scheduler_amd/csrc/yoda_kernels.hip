@@ -1963,16 +1963,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
             }
             cand = cand && key > ul[TL - 1];
           }
-        } else if (is_u) {
+        } else {
+          // (branch-free: selects instead of exec-mask branches around the update)
           const uint32_t basic = q_all ? sel : 0u;  // algorithm.go:271
           const double raw = (double)basic + stat;                   // algorithm.go:96
-          if (raw > ubest) {
-            ubest = raw;
-            uidx = n;
-            uties = 1;
-          } else if (raw == ubest) {
-            ++uties;
-          }
+          const bool gt = is_u && raw > ubest, eq = is_u && raw == ubest;
+          uidx = gt ? n : uidx;
+          uties = gt ? 1u : uties + (eq ? 1u : 0u);
+          ubest = gt ? raw : ubest;
         }
         const bool is_rec = fast && range <= 3u && !is_u;
         rec_b = ballot(is_rec);
