@@ -116,7 +116,7 @@ hipError_t launch_topk_merge_keys(const uint64_t* keys, uint32_t C, uint32_t n_p
 hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32_t* node,
                              const uint64_t* value, const uint64_t* card_number, uint32_t count,
                              unsigned char* sum, uint32_t sum_stride, unsigned char* sum2,
-                             uint32_t sum2_stride, hipStream_t s);
+                             uint32_t sum2_stride, const PermCopy& pc, hipStream_t s);
 hipError_t launch_gtable(int K, const uint32_t* sum2, const uint32_t* mix, uint32_t n_nodes,
                          const uint64_t* g_max,
                          uint32_t* tab, uint32_t* rcp_out, MemTab mt, hipStream_t s);
@@ -321,6 +321,21 @@ struct yoda_handle {
   GTab g = {};
   bool has_k1sum = false, has_k2sum = false;
   bool all_one_model = false;  // every node: one GPU model, one TotalMemory (kNodeUniform4|Total)
+  // block-grouped node order of the private batch runs (node_perm at upload): copies of the
+  // K1 / K2 summaries and the G table in that order, the local id of each position, and each
+  // node's position (k_set_static keeps the copies current)
+  bool perm_on = false;
+  DevBuf k1sum_p, k2sum_p, gtab_p, perm_ids, perm_inv;
+  PermCopy perm_copy() const {
+    PermCopy pc;
+    if (perm_on) {
+      pc.inv = perm_inv.as<uint32_t>();
+      pc.sum = k1sum_p.as<unsigned char>();
+      pc.sum2 = k2sum_p.as<unsigned char>();
+    }
+    return pc;
+  }
+  bool perm_run() const { return perm_on && count_order; }  // this run is block-grouped
   bool all_uni4 = false;       // every node: one GPU model (kNodeUniform4)
   std::vector<unsigned char> host_records;  // kept for alloc updates (greedy)
   std::vector<uint32_t> host_k2sum;         // idem (its static score words)
@@ -438,7 +453,7 @@ struct yoda_handle {
   ~yoda_handle() {
     if (comm && rccl().ok) (void)rccl().comm_destroy(comm);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &pod_blob,   &maxima,       &counts,
+    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &k1sum_p,   &k2sum_p,   &gtab_p,    &perm_ids,  &perm_inv,    &pod_blob,   &maxima,       &counts,
                      &pod_sorted, &perm,     &order_scratch, &order_meta, &order_hist,
                      &order_bstart, &order_slot, &order_bkt,
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
@@ -700,6 +715,10 @@ PodParams pod_params(yoda_t* h) {
   pp.x1 = h->path == Path::N32 ? h->kx1.as<uint32_t>() : nullptr;
   pp.one_model = h->path == Path::N32 && h->all_one_model;
   pp.all_uni4 = h->path == Path::N32 && h->all_uni4;
+  if (h->perm_run()) {
+    pp.ids = h->perm_ids.as<uint32_t>();
+    if (pp.g.tab) pp.g.tab = h->gtab_p.as<uint32_t>();
+  }
   pp.mt = h->mem_ranks ? h->mt : MemTab{};
   return pp;
 }
@@ -968,9 +987,11 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_m
     HIP_TRY(h, hipMemsetAsync(h->blk.p, 0, (size_t)(P + 63) / 64 * blk_row(h->n_nodes) * 8,
                               h->stream));
   h->blk_zeroed = false;
+  const bool pr = h->perm_run();  // block-grouped node order (upload's node_perm)
   HIP_TRY(h, launch_k1(h->K, h->path, h->nodes.as<unsigned char>(),
-                       h->has_k1sum ? h->k1sum.as<unsigned char>() : nullptr,
-                       h->k2sum.as<unsigned char>(), h->kmix.as<unsigned char>(), h->n_nodes,
+                       h->has_k1sum ? (pr ? h->k1sum_p : h->k1sum).as<unsigned char>() : nullptr,
+                       (pr ? h->k2sum_p : h->k2sum).as<unsigned char>(),
+                       h->kmix.as<unsigned char>(), h->n_nodes,
                        h->chunk1, h->C1, pod_params(h), P, part, h->bitmask.as<uint64_t>(),
                        bm_row(h->n_nodes), h->bsum.as<BlockMask>(), bs_row(h->n_nodes),
                        h->blk.as<uint64_t>(), blk_row(h->n_nodes), h->stats_ptr(), h->stream));
@@ -1097,7 +1118,9 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
                                 pod_params(h), P, part, rows, h->stream));
   } else {
     HIP_TRY(h, launch_k2(h->K, h->path, h->nodes.as<unsigned char>(),
-                         h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr,
+                         h->has_k2sum ? (h->perm_run() ? h->k2sum_p : h->k2sum)
+                                            .as<unsigned char>()
+                                      : nullptr,
                          h->blk_valid ? h->blk.as<uint64_t>() : nullptr, blk_row(h->n_nodes),
                          h->n_nodes,
                          h->chunk2, h->C2, pod_params(h), maxima, h->rcp.as<double>(),
@@ -1592,6 +1615,79 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
           for (uint32_t w = 0; w < W; ++w) t[sum_index(i, w, stride)] = v[(size_t)i * W + w];
         return t;
       };
+      // Block-grouped node order for the private batch runs (node order): a
+      // snapshot of one-model nodes is dealt into 64-node blocks of one clock each (PodFitsClock
+      // then rules whole blocks out for a clock-labelled wave, and K2 skips them), whole blocks
+      // round-robin in proportion to each clock's block count so that every node chunk keeps
+      // the snapshot's mix, the groups' remainders last.  Copies of the K1 / K2 summaries in
+      // that order; the kernels compare the nodes' local ids (perm_ids) on score ties.
+      h->perm_on = false;
+      static const bool perm_env = env_u32("YODA_NODE_PERM", 1) != 0;
+      std::vector<uint32_t> nperm;
+      if (perm_env && path == Path::N32 && n_one_model == N && N >= 4096 &&
+          !(flags & YODA_UPLOAD_PER_NODE_K1) && !(flags & YODA_UPLOAD_PER_NODE_K2)) {
+        const uint32_t SW = (uint32_t)(sstride / 4);
+        std::vector<uint32_t> keys;
+        std::vector<std::vector<uint32_t>> grp;
+        bool ok = true;
+        for (uint32_t i = 0; i < N && ok; ++i) {
+          const uint32_t ck = sum[(size_t)i * SW + kSumClock];
+          size_t g = 0;
+          while (g < keys.size() && keys[g] != ck) ++g;
+          if (g == keys.size()) {
+            if (keys.size() == 64) ok = false;  // too many clocks to group usefully
+            keys.push_back(ck);
+            grp.emplace_back();
+          }
+          if (ok) grp[g].push_back(i);
+        }
+        const size_t G = grp.size();
+        if (ok && G >= 2) {
+          std::vector<size_t> nb(G), done(G, 0);
+          size_t total = 0;
+          for (size_t g = 0; g < G; ++g) total += (nb[g] = grp[g].size() / 64);
+          nperm.reserve(N);
+          for (size_t b = 0; b < total; ++b) {
+            size_t best = G;
+            double bt = 0.0;
+            for (size_t g = 0; g < G; ++g) {
+              if (done[g] == nb[g]) continue;
+              const double t = (done[g] + 0.5) / (double)nb[g];
+              if (best == G || t < bt) best = g, bt = t;
+            }
+            const size_t o = done[best]++ * 64;
+            nperm.insert(nperm.end(), grp[best].begin() + o, grp[best].begin() + o + 64);
+          }
+          for (size_t g = 0; g < G; ++g)
+            nperm.insert(nperm.end(), grp[g].begin() + done[g] * 64, grp[g].end());
+          h->perm_on = nperm.size() == N;
+        }
+      }
+      if (h->perm_on) {
+        const uint32_t SW = (uint32_t)(sstride / 4), S2W = (uint32_t)(s2stride / 4);
+        std::vector<uint32_t> sp((size_t)N * SW), s2p((size_t)N * S2W), inv(N);
+        for (uint32_t q = 0; q < N; ++q) {
+          const uint32_t i = nperm[q];
+          std::memcpy(sp.data() + (size_t)q * SW, sum.data() + (size_t)i * SW, SW * 4);
+          std::memcpy(s2p.data() + (size_t)q * S2W, sum2.data() + (size_t)i * S2W, S2W * 4);
+          inv[i] = q;
+        }
+        sp = tiles(sp, (uint32_t)sstride);
+        s2p = tiles(s2p, (uint32_t)s2stride);
+        HIP_TRY(h, h->k1sum_p.ensure(sp.size() * 4));
+        HIP_TRY(h, h->k2sum_p.ensure(s2p.size() * 4));
+        HIP_TRY(h, h->perm_ids.ensure((size_t)N * 4));
+        HIP_TRY(h, h->perm_inv.ensure((size_t)N * 4));
+        HIP_TRY(h, hipMemcpyAsync(h->k1sum_p.p, sp.data(), sp.size() * 4, hipMemcpyHostToDevice,
+                                  h->stream));
+        HIP_TRY(h, hipMemcpyAsync(h->k2sum_p.p, s2p.data(), s2p.size() * 4,
+                                  hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(h, hipMemcpyAsync(h->perm_ids.p, nperm.data(), (size_t)N * 4,
+                                  hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(h, hipMemcpyAsync(h->perm_inv.p, inv.data(), (size_t)N * 4,
+                                  hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(h, hipStreamSynchronize(h->stream));  // (the host copies go out of scope)
+      }
       sum = tiles(sum, (uint32_t)sstride);
       sum2 = tiles(sum2, (uint32_t)s2stride);
       mix = tiles(mix, (uint32_t)mstride);
@@ -1641,6 +1737,12 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
       HIP_TRY(h, launch_gtable(K, h->k2sum.as<uint32_t>(), h->kmix.as<uint32_t>(), N,
                                h->gtab_aux.as<uint64_t>(),
                                h->gtab.as<uint32_t>(), rcp_dev, mt, h->stream));
+      if (h->perm_on) {  // the G table of the block-grouped copy (the same rows, reordered)
+        HIP_TRY(h, h->gtab_p.ensure(sum_words(std::max<uint32_t>(N, 1), gtab_stride(K)) * 4));
+        HIP_TRY(h, launch_gtable(K, h->k2sum_p.as<uint32_t>(), h->kmix.as<uint32_t>(), N,
+                                 h->gtab_aux.as<uint64_t>(), h->gtab_p.as<uint32_t>(), rcp_dev,
+                                 mt, h->stream));
+      }
       HIP_TRY(h, hipMemcpyAsync(g_rcp, rcp_dev, sizeof(g_rcp), hipMemcpyDeviceToHost, h->stream));
     }
     const bool diskio = nd->cpu && nd->disk_io;
@@ -2483,7 +2585,7 @@ struct GreedyState {
                                  h->has_k1sum ? h->k1sum.as<unsigned char>() : nullptr,
                                  k1sum_stride(h->K),
                                  h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr,
-                                 k2sum_stride(h->K), h->stream));
+                                 k2sum_stride(h->K), h->perm_copy(), h->stream));
     HIP_TRY(h, hipEventRecord(h->upd_event, h->stream));
     h->upd_pending = true;
     if (marks)
@@ -2882,7 +2984,7 @@ int push_node_state(yoda_t* h, const std::vector<uint32_t>& loc, const std::vect
                                h->has_k1sum ? h->k1sum.as<unsigned char>() : nullptr,
                                k1sum_stride(h->K),
                                h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr,
-                               k2sum_stride(h->K), h->stream));
+                               k2sum_stride(h->K), h->perm_copy(), h->stream));
   return YODA_OK;
 }
 

@@ -1386,6 +1386,7 @@ struct ScoreArgs {
   GTab g = {};                    // the snapshot-wide maxima's per-node terms (tab: none)
   const uint32_t* mix = nullptr;  // per-card models in free order (yoda_layout.h MixWord)
   MemTab mt = {};                 // memory ranks (yoda_layout.h MemTab)
+  const uint32_t* ids = nullptr;  // block-grouped node order: the local id of each position
 };
 
 template <Path P>
@@ -1679,7 +1680,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // LDS per wave: prefix table | 64 node records | the sets' reciprocals (8 words each).
   // No lowest score: on this path NormalizeScore cannot overflow, so the
   // lowest raw score is never read (the chunk merge reports the best in its place).
-  constexpr uint32_t RECS = TAB, RCPS = TAB + kWave * REC, LDSW = RCPS + 8 * kSets;
+  // + the nodes' local ids of a block-grouped run (args.ids)
+  constexpr uint32_t RECS = TAB, RCPS = TAB + kWave * REC, IDW = RCPS + 8 * kSets,
+                     LDSW = IDW + kWave;
   __shared__ __attribute__((aligned(16))) uint32_t lds_all[kBlock / kWave][LDSW];
   const uint32_t lane = lane_id();
   uint32_t* lds = lds_all[threadIdx.x >> 6];
@@ -1784,6 +1787,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // read back with v_readlane), loaded together: one memory latency per block.
   auto block = [&](uint32_t nb) {
     const uint32_t n = nb + lane;
+    const bool valid0 = n < n1;
+    const uint32_t nid = (args.ids && valid0) ? args.ids[n] : n;
+    if (args.ids) lds[IDW + lane] = nid;
     const bool valid = n < n1;
     // the wave's mask of node n: from the block's (nz, full) words, and a load of its own
     // only for a partial node (sparse form); or the dense [wave][node] array
@@ -1968,7 +1974,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
           const uint32_t basic = q_all ? sel : 0u;  // algorithm.go:271
           const double raw = (double)basic + stat;                   // algorithm.go:96
           const bool gt = is_u && raw > ubest, eq = is_u && raw == ubest;
-          uidx = gt ? n : uidx;
+          uidx = gt ? nid : (eq ? min(uidx, nid) : uidx);
           uties = gt ? 1u : uties + (eq ? 1u : 0u);
           ubest = gt ? raw : ubest;
         }
@@ -2097,13 +2103,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         const uint32_t basic = ra[k].x >= sc.c ? bsel : 0u;
         const uint64_t raw = ((uint64_t)rs[k].x | ((uint64_t)rs[k].y << 32)) + basic;
         const uint32_t mw = lane < 32u ? ra[k].y : ra[k].z;  // the wave's mask of the node
-        take_r(vv[k] && ((mw >> (lane & 31u)) & 1u) != 0u, raw, nb + jj[k]);
+        take_r(vv[k] && ((mw >> (lane & 31u)) & 1u) != 0u, raw,
+               args.ids ? lds[IDW + jj[k]] : nb + jj[k]);
       }
     }
     while (part_b) {  // wave-uniform loop over the remaining feasible nodes
       const int j = __builtin_ctzll(part_b);
       part_b &= part_b - 1;
-      const uint32_t nn = nb + (uint32_t)j;
+      // the node's local id (its position, unless the run is block-grouped)
+      const uint32_t nn =
+          args.ids ? (uint32_t)__builtin_amdgcn_readlane((int)nid, j) : nb + (uint32_t)j;
       const uint64_t mj =
           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mask >> 32), j) << 32) |
           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mask, j);
@@ -2443,9 +2452,18 @@ __global__ __launch_bounds__(kBlock) void k_set_static(unsigned char* __restrict
                                                        unsigned char* __restrict__ sum,
                                                        uint32_t sum_stride,
                                                        unsigned char* __restrict__ sum2,
-                                                       uint32_t sum2_stride) {
+                                                       uint32_t sum2_stride, PermCopy pc) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= count) return;
+  if (pc.inv) {  // the block-grouped copies (private runs) at the node's internal position
+    const uint32_t q = pc.inv[node[t]];
+    uint32_t* s1 = reinterpret_cast<uint32_t*>(pc.sum);
+    s1[sum_index(q, kSumCnLo, sum_stride)] = (uint32_t)card_number[t];
+    s1[sum_index(q, kSumCnHi, sum_stride)] = (uint32_t)(card_number[t] >> 32);
+    uint32_t* s2 = reinterpret_cast<uint32_t*>(pc.sum2);
+    s2[sum_index(q, kS2Static, sum2_stride)] = (uint32_t)value[t];
+    s2[sum_index(q, kS2Static + 1, sum2_stride)] = (uint32_t)(value[t] >> 32);
+  }
   uint64_t* hdr = reinterpret_cast<uint64_t*>(nodes + (size_t)node[t] * stride);
   hdr[0] = value[t];        // static_score bits (f64 on the fast paths, u64 on U64)
   hdr[1] = card_number[t];  // CardNumber
@@ -3227,7 +3245,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce2(const double* __restrict__ p
     }
     const uint32_t ix = pidx[o], tt = pties[o];
     const bool v = b >= 0, gt = v && b > best, eq = v && b == best;
-    idx = gt ? ix : idx;
+    // (equal bests: the lower node -- chunks need not be in node order, block-grouped runs)
+    idx = gt ? ix : (eq ? min(idx, ix) : idx);
     ties = gt ? tt : (eq ? ties + tt : ties);
     best = gt ? b : best;
     low = (v && l < low) ? l : low;
@@ -3747,7 +3766,8 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
                               int64_t* rows, double* tk_s, uint32_t* tk_i,
                               unsigned long long* stats, const uint32_t* counts, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
-  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g, pp.mix, pp.mt};
+  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g, pp.mix, pp.mt,
+                    pp.ids};
   const MaskSrc ms{bm, bs, bm_stride, bs_stride};
   switch (path) {
     case Path::N32:
@@ -3895,10 +3915,10 @@ hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t 
 hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32_t* node,
                              const uint64_t* value, const uint64_t* card_number, uint32_t count,
                              unsigned char* sum, uint32_t sum_stride, unsigned char* sum2,
-                             uint32_t sum2_stride, hipStream_t s) {
+                             uint32_t sum2_stride, const PermCopy& pc, hipStream_t s) {
   if (count == 0) return hipSuccess;
   hipLaunchKernelGGL(k_set_static, pod_grid(count), dim3(kBlock), 0, s, nodes, stride, node,
-                     value, card_number, count, sum, sum_stride, sum2, sum2_stride);
+                     value, card_number, count, sum, sum_stride, sum2, sum2_stride, pc);
   return hipGetLastError();
 }
 

@@ -177,6 +177,14 @@ __host__ __device__ constexpr uint32_t blk_row(uint32_t n_nodes) {
   return ((n_nodes + 63u) / 64u + 63u) / 64u;
 }
 
+// The block-grouped copies of the node summaries (private batch runs) that k_set_static keeps
+// current with the originals: inv[node] = its internal position.
+struct PermCopy {
+  const uint32_t* inv = nullptr;
+  unsigned char* sum = nullptr;
+  unsigned char* sum2 = nullptr;
+};
+
 // Mode B node record: V = Cpu/100, U = DiskIO/50 (algorithm.go:71,73).
 struct alignas(16) NodeRecB {
   double v, u;
@@ -279,6 +287,9 @@ struct PodParams {
   bool one_model = false;
   // every node of the snapshot is one GPU model (kSumUni4; N32: the K2 without mixed rows)
   bool all_uni4 = false;
+  // private runs over the block-grouped node order (yoda_capi.cpp node_perm): the local node
+  // id of each internal position (the argmax ties compare these, not positions); nullptr: none
+  const uint32_t* ids = nullptr;
   // the snapshot's memory ranks (MemTab; vf == nullptr: none)
   MemTab mt = {};
 };
