@@ -287,6 +287,10 @@ int yoda_set_pod_order(yoda_t* h, int enable);
  * a wave, the sorted positions of the last run, how that run was ordered (0 not, 1 radix sort,
  * 2 counting sort)}. */
 int yoda_order_info(const yoda_t* h, uint32_t* out);
+/* The node snapshot's order in private runs (diagnostic): *grouped = 1 when its one-model nodes
+ * are dealt into 64-node blocks of one clock for yoda_run (copies of the summaries in that
+ * order; YODA_NODE_PERM=0 disables), 0 when the upload order is used. */
+int yoda_node_order(const yoda_t* h, uint32_t* grouped);
 
 /* ---- kernel timing ----------------------------------------------------------------- */
 /* enable != 0: every subsequent K1 / K2 launch is bracketed by HIP events recorded on the

@@ -2435,6 +2435,12 @@ int yoda_order_info(const yoda_t* h, uint32_t* out) {
   return YODA_OK;
 }
 
+int yoda_node_order(const yoda_t* h, uint32_t* grouped) {
+  if (!h || !grouped) return YODA_ERR_INVALID_ARG;
+  *grouped = h->perm_on ? 1u : 0u;
+  return YODA_OK;
+}
+
 int yoda_set_pod_order(yoda_t* h, int enable) {
   if (!h) return YODA_ERR_INVALID_ARG;
   h->order_enabled = enable != 0;

@@ -65,6 +65,7 @@ _SIGS = {
     "yoda_profile": ([_vp, C.c_int], C.c_int),
     "yoda_set_pod_order": ([_vp, C.c_int], C.c_int),
     "yoda_order_info": ([_vp, _vp], C.c_int),
+    "yoda_node_order": ([_vp, _vp], C.c_int),
     "yoda_profile_read": ([_vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                            C.POINTER(C.c_uint32)], C.c_int),
     "yoda_greedy": ([_vp, C.POINTER(CPodSoA), C.c_int, _u32, C.POINTER(C.c_int32)], C.c_int),
@@ -313,6 +314,13 @@ class Yoda:
         self._check(lib().yoda_order_info(self._h, _np_ptr(out)), "yoda_order_info")
         return {"groups": int(out[0]), "padded": int(out[1]), "work": int(out[2]),
                 "kind": int(out[3])}
+
+    @property
+    def node_order_grouped(self) -> bool:
+        """yoda_node_order: private runs use the block-grouped node order."""
+        g = C.c_uint32(0)
+        self._check(lib().yoda_node_order(self._h, C.byref(g)), "yoda_node_order")
+        return bool(g.value)
 
     def set_pod_order(self, enable: bool = True):
         """Sort Mode-A batches on the device before K1/K2 (default on); results are returned
