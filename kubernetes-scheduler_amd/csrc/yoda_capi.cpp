@@ -41,6 +41,9 @@ hipError_t launch_mem_rank(const uint64_t* m_u, uint32_t n_pods, const MemTab& m
                            hipStream_t s);
 hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
                         hipStream_t s);
+hipError_t launch_window_out(const uint32_t* counts, const uint64_t* maxima, const uint32_t* wit,
+                             const double* tk_s, const uint32_t* tk_i, const uint32_t* perm,
+                             uint32_t wn, uint32_t kt, unsigned char* out, hipStream_t s);
 hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigned char* sum2,
                      const uint64_t* blk, uint32_t blk_stride, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
@@ -3392,8 +3395,18 @@ bool yoda_greedy_session::resolve_capacity(uint32_t i, uint32_t p, int32_t* pk) 
       bi = n;
     }
   }
-  uint64_t lf, lz, lw[6];
-  const bool exact = scan_lost(i, p, q, lq, &lf, &lz, lw);
+  uint64_t lf = 0, lz = 0, lw[6] = {};
+  // The bounds-only certificate first (no card scan): whatever it certifies, the exact one
+  // certifies with the same outcome (nf0 >= 2 + lq leaves >= 2 feasible nodes; a field with
+  // more witnesses than lost nodes, or an unlost single witness, keeps its maximum since
+  // lw[f] <= lq).  The lost nodes' cards are examined only when it fails.
+  bool exact = false;
+  if (!whole && lq > 0 && nf0 >= 2 + lq && nz0 == 0 && bi != 0xffffffffu &&
+      maxima_kept(i, q, lq, false, lw)) {
+    // (falls through to the list certificate below with exact == false)
+  } else {
+    exact = scan_lost(i, p, q, lq, &lf, &lz, lw);
+  }
   if (whole) {
     if (alive == 0) {
       *pk = YODA_PICK_NONE;
@@ -3734,6 +3747,14 @@ static int greedy_eval_exact(yoda_t* h, const yoda_pod_soa* pods, uint32_t p, in
 // (yoda_greedy_session::resolve_capacity).  A pod it cannot certify starts the next window,
 // so it is evaluated against the current state; the window size adapts to how far the last
 // window got.  Node ids inside are local; picks are returned global.
+static FILE* greedy_trace_file() {
+  static FILE* f = [] {
+    const char* p = std::getenv("YODA_GREEDY_TRACE");
+    return p && *p ? std::fopen(p, "w") : nullptr;
+  }();
+  return f;
+}
+
 static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
   using Clock = std::chrono::steady_clock;
   auto ms_since = [](Clock::time_point t0) {
@@ -3813,19 +3834,24 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
     const uint32_t wn = std::min(W, P - ws);
     win.build(pods, g->order.data() + ws, wn);
     if ((rc = yoda_upload_pods(h, &win.soa))) return rc;
+    const double t_up = ms_since(tw);
     if ((rc = prepare_run(h, YODA_MODE_SCV))) return rc;
     if ((rc = order_pods(h, YODA_MODE_SCV))) return rc;
     HIP_TRY(h, h->wit.ensure(12 * (size_t)wn * 4));
     if ((rc = phase1_witness(h, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(),
                              h->wit.as<uint32_t>(), 0)))
       return rc;
-    // pinned staging of the window's outputs (sorted order): counts | maxima | wit |
-    // top scores | top nodes | perm
+    // pinned staging of the window's outputs, in window order (k_window_out writes them there
+    // from the sorted order in one launch): counts | maxima | wit | top scores | top nodes
     const size_t o_cnt = 0, o_mx = o_cnt + 8 * (size_t)wn, o_wit = o_mx + 48 * (size_t)wn,
                  o_ts = o_wit + 48 * (size_t)wn, o_ti = o_ts + 8 * (size_t)KT * wn,
-                 o_perm = o_ti + 4 * (size_t)KT * wn, total = o_perm + 4 * (size_t)wn;
+                 total = o_ti + 4 * (size_t)KT * wn;
     HIP_TRY(h, h->win_stage.ensure(total));
     unsigned char* st = static_cast<unsigned char*>(h->win_stage.p);
+    const uint32_t *cnt_p, *wc_p, *ti_p;
+    const uint64_t* mx_p;
+    const double* ts_p;
+    double t_issued, t_sync;
     if (N > 0) {
       HIP_TRY(h, launch_prep2(h->maxima.as<uint64_t>(), wn, h->rcp.as<double>(),
                               h->rcp32.as<float>(), h->stream));
@@ -3835,64 +3861,45 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
       rc = topk_lists(h, wn, KT, h->counts.as<uint32_t>());
       h->node_offset = off;
       if (rc) return rc;
-      HIP_TRY(h, hipMemcpyAsync(st + o_ts, h->tk_s.p, 8 * (size_t)KT * wn, hipMemcpyDeviceToHost,
-                                h->stream));
-      HIP_TRY(h, hipMemcpyAsync(st + o_ti, h->tk_i.p, 4 * (size_t)KT * wn, hipMemcpyDeviceToHost,
-                                h->stream));
-    } else {
-      for (size_t t = 0; t < (size_t)KT * wn; ++t) {
-        reinterpret_cast<double*>(st + o_ts)[t] = -1.0;
-        reinterpret_cast<uint32_t*>(st + o_ti)[t] = 0xffffffffu;
-      }
-    }
-    HIP_TRY(h, hipMemcpyAsync(st + o_cnt, h->counts.p, 8 * (size_t)wn, hipMemcpyDeviceToHost,
-                              h->stream));
-    HIP_TRY(h, hipMemcpyAsync(st + o_mx, h->maxima.p, 48 * (size_t)wn, hipMemcpyDeviceToHost,
-                              h->stream));
-    HIP_TRY(h, hipMemcpyAsync(st + o_wit, h->wit.p, 48 * (size_t)wn, hipMemcpyDeviceToHost,
-                              h->stream));
-    if (h->ordered)
-      HIP_TRY(h, hipMemcpyAsync(st + o_perm, h->perm.p, 4 * (size_t)wn, hipMemcpyDeviceToHost,
-                                h->stream));
-    HIP_TRY(h, hipStreamSynchronize(h->stream));
-    // sorted position -> window order
-    pos.resize(wn);
-    for (uint32_t i = 0; i < wn; ++i) pos[i] = i;
-    if (h->ordered) {
-      const uint32_t* perm = reinterpret_cast<const uint32_t*>(st + o_perm);
-      for (uint32_t q = 0; q < wn; ++q) pos[perm[q]] = q;
-    }
-    cnt_w.resize(2 * (size_t)wn), mx_w.resize(6 * (size_t)wn), wc_w.resize(12 * (size_t)wn);
-    ts_w.resize((size_t)KT * wn), ti_w.resize((size_t)KT * wn);
-    const uint32_t* cnt_s = reinterpret_cast<const uint32_t*>(st + o_cnt);
-    const uint64_t* mx_s = reinterpret_cast<const uint64_t*>(st + o_mx);
-    const uint32_t* wit_s = reinterpret_cast<const uint32_t*>(st + o_wit);
-    const double* ts_s = reinterpret_cast<const double*>(st + o_ts);
-    const uint32_t* ti_s = reinterpret_cast<const uint32_t*>(st + o_ti);
-    for (uint32_t i = 0; i < wn; ++i) {
-      const uint32_t q = pos[i];
-      cnt_w[i] = cnt_s[q];
-      cnt_w[(size_t)wn + i] = cnt_s[(size_t)wn + q];
-      for (int f = 0; f < 6; ++f) {
-        mx_w[(size_t)f * wn + i] = mx_s[(size_t)f * wn + q];
-        wc_w[(size_t)f * wn + i] = wit_s[(size_t)f * wn + q];
-        wc_w[(size_t)(6 + f) * wn + i] = wit_s[(size_t)(6 + f) * wn + q];
-      }
-      for (uint32_t kk = 0; kk < KT; ++kk) {
-        ts_w[(size_t)kk * wn + i] = ts_s[(size_t)kk * wn + q];
-        ti_w[(size_t)kk * wn + i] = ti_s[(size_t)kk * wn + q];
-      }
+      HIP_TRY(h, launch_window_out(h->counts.as<uint32_t>(), h->maxima.as<uint64_t>(),
+                                   h->wit.as<uint32_t>(), h->tk_s.as<double>(),
+                                   h->tk_i.as<uint32_t>(),
+                                   h->ordered ? h->perm.as<uint32_t>() : nullptr, wn, KT,
+                                   static_cast<unsigned char*>(h->win_stage.dp), h->stream));
+      t_issued = ms_since(tw);
+      HIP_TRY(h, hipStreamSynchronize(h->stream));
+      t_sync = ms_since(tw);
+      cnt_p = reinterpret_cast<const uint32_t*>(st + o_cnt);
+      mx_p = reinterpret_cast<const uint64_t*>(st + o_mx);
+      wc_p = reinterpret_cast<const uint32_t*>(st + o_wit);
+      ts_p = reinterpret_cast<const double*>(st + o_ts);
+      ti_p = reinterpret_cast<const uint32_t*>(st + o_ti);
+    } else {  // no nodes: every pod infeasible
+      t_issued = ms_since(tw);
+      HIP_TRY(h, hipStreamSynchronize(h->stream));
+      t_sync = ms_since(tw);
+      cnt_w.assign(2 * (size_t)wn, 0u);
+      mx_w.assign(6 * (size_t)wn, 1ull);
+      wc_w.assign(12 * (size_t)wn, 0u);
+      for (size_t t = 6 * (size_t)wn; t < 12 * (size_t)wn; ++t) wc_w[t] = 0xffffffffu;
+      ts_w.assign((size_t)KT * wn, -1.0);
+      ti_w.assign((size_t)KT * wn, 0xffffffffu);
+      cnt_p = cnt_w.data(), mx_p = mx_w.data(), wc_p = wc_w.data();
+      ts_p = ts_w.data(), ti_p = ti_w.data();
     }
     ++h->greedy_windows;
-    h->greedy_window_ms += ms_since(tw);
+    const double t_win = ms_since(tw);
+    h->greedy_window_ms += t_win;
     const auto tr = Clock::now();
-    if ((rc = yoda_gs_begin_window(g, ws, wn, KT, cnt_w.data(), ts_w.data(), ti_w.data())) ||
-        (rc = yoda_gs_set_witness(g, mx_w.data(), wc_w.data(), wc_w.data() + 6 * (size_t)wn)))
+    if ((rc = yoda_gs_begin_window(g, ws, wn, KT, cnt_p, ts_p, ti_p)) ||
+        (rc = yoda_gs_set_witness(g, mx_p, wc_p, wc_p + 6 * (size_t)wn)))
       return fail(h, rc, "greedy: session window");
     // resolve; an uncertified pod is scheduled exactly against the current state (k_one_*)
     // while such pods stay rare in the window, else it opens the next window
     uint32_t next = 0, fails = 0;
     double fb_ms = 0;
+    uint64_t why0[6];
+    std::copy(std::begin(g->why), std::end(g->why), why0);
     for (;;) {
       if ((rc = yoda_gs_resolve(g, &next))) return fail(h, rc, "greedy: resolve");
       // YODA_GREEDY_FAIL_DIV (A/B knob): one exact evaluation allowed per that many resolved pods
@@ -3908,6 +3915,26 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
     }
     h->greedy_fallback_ms += fb_ms;
     h->greedy_resolve_ms += ms_since(tr) - fb_ms;
+    // YODA_GREEDY_TRACE=<file> (diagnostic): one line per window -- start, size, pods
+    // resolved, the failed certificate (index into why[], -1 = none), pods assigned so far
+    if (FILE* tf = greedy_trace_file()) {
+      int reason = -1;
+      for (int r = 0; r < 6; ++r)
+        if (g->why[r] != why0[r]) reason = r;
+      uint32_t placed = 0;
+      for (uint32_t t = 0; t < next; ++t) placed += g->pick[g->order[ws + t]] >= 0 ? 1u : 0u;
+      uint64_t q = 0, nf0 = 0, lq = 0;
+      if (next < wn) {
+        q = g->need_cards(g->order[ws + next]);
+        nf0 = g->counts[next];
+        lq = g->lost(q);
+      }
+      std::fprintf(tf, "%u %u %u %d %u %llu %llu %llu %.1f %.1f %.1f %.1f %.1f\n", ws, wn, next,
+                   reason, placed, (unsigned long long)q, (unsigned long long)nf0,
+                   (unsigned long long)lq, 1e3 * ms_since(tw), 1e3 * t_up, 1e3 * t_issued,
+                   1e3 * t_sync, 1e3 * t_win);
+      std::fflush(tf);
+    }
     if (next < wn) {
       // pod ws + next could not be certified: it opens the next window (evaluated against the
       // current state, so it is always resolved there); size it after this one's progress

@@ -1272,6 +1272,42 @@ __global__ __launch_bounds__(kBlock) void k_prep2(const uint64_t* __restrict__ m
   }
 }
 
+// A capacity greedy window's outputs, from the batch's sorted order into window order, written
+// straight into the host's mapped staging pages in one launch (instead of five copies and a
+// host-side permutation): out = counts [2][wn] u32 | maxima [6][wn] u64 | witnesses [12][wn]
+// u32 | top scores [kt][wn] f64 | top nodes [kt][wn] u32.  perm[q] = window index of sorted
+// position q (nullptr: unsorted); each workgroup inverts it for its own 256 window slots, so the
+// writes to host memory are coalesced and the gathers stay on the device.
+__global__ __launch_bounds__(kBlock) void k_window_out(
+    const uint32_t* __restrict__ counts, const uint64_t* __restrict__ maxima,
+    const uint32_t* __restrict__ wit, const double* __restrict__ tk_s,
+    const uint32_t* __restrict__ tk_i, const uint32_t* __restrict__ perm, uint32_t wn,
+    uint32_t kt, unsigned char* __restrict__ out) {
+  __shared__ uint32_t inv[kBlock];
+  const uint32_t w0 = blockIdx.x * kBlock, w = w0 + threadIdx.x;
+  if (perm) {
+    for (uint32_t q = threadIdx.x; q < wn; q += kBlock) {
+      const uint32_t x = perm[q];
+      if (x >= w0 && x < w0 + kBlock) inv[x - w0] = q;
+    }
+    __syncthreads();
+  }
+  if (w >= wn) return;
+  const uint32_t q = perm ? inv[threadIdx.x] : w;
+  uint32_t* o_cnt = reinterpret_cast<uint32_t*>(out);
+  uint64_t* o_mx = reinterpret_cast<uint64_t*>(out + 8 * (size_t)wn);
+  uint32_t* o_wit = reinterpret_cast<uint32_t*>(out + 56 * (size_t)wn);
+  double* o_ts = reinterpret_cast<double*>(out + 104 * (size_t)wn);
+  uint32_t* o_ti = reinterpret_cast<uint32_t*>(out + (104 + 8 * (size_t)kt) * wn);
+  for (uint32_t f = 0; f < 2; ++f) o_cnt[(size_t)f * wn + w] = counts[(size_t)f * wn + q];
+  for (uint32_t f = 0; f < 6; ++f) o_mx[(size_t)f * wn + w] = maxima[(size_t)f * wn + q];
+  for (uint32_t f = 0; f < 12; ++f) o_wit[(size_t)f * wn + w] = wit[(size_t)f * wn + q];
+  for (uint32_t k = 0; k < kt; ++k) {
+    o_ts[(size_t)k * wn + w] = tk_s[(size_t)k * wn + q];
+    o_ti[(size_t)k * wn + w] = tk_i[(size_t)k * wn + q];
+  }
+}
+
 // The "G table" (N32 block K2): for the snapshot-wide maxima G (per CalculateCardScore field,
 // the max over every real card, floor 1 -- the PreScore maxima of any pod whose feasible
 // nodes include the maximal cards, which is most pods of a large cluster) the per-node terms
@@ -3752,6 +3788,15 @@ hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, boo
 hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
                         hipStream_t s) {
   hipLaunchKernelGGL(k_prep2, pod_grid(n_pods), dim3(kBlock), 0, s, maxima, n_pods, rcp, rcp32);
+  return hipGetLastError();
+}
+
+hipError_t launch_window_out(const uint32_t* counts, const uint64_t* maxima, const uint32_t* wit,
+                             const double* tk_s, const uint32_t* tk_i, const uint32_t* perm,
+                             uint32_t wn, uint32_t kt, unsigned char* out, hipStream_t s) {
+  if (wn == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_window_out, pod_grid(wn), dim3(kBlock), 0, s, counts, maxima, wit, tk_s,
+                     tk_i, perm, wn, kt, out);
   return hipGetLastError();
 }
 
