@@ -1717,8 +1717,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // No lowest score: on this path NormalizeScore cannot overflow, so the
   // lowest raw score is never read (the chunk merge reports the best in its place).
   // + the nodes' local ids of a block-grouped run (args.ids)
+  // TT > 1 (top-k lists, whose small diverse windows have several reciprocal sets per wave):
+  // prefix rows B_q[0..K] of every one-model node for each of the first TT sets (row 0 in the
+  // table above, the others after the ids), so the per-pod pass reads a lane's basic score as
+  // in a uniform wave instead of computing its card terms per node
+  constexpr uint32_t TT = (TOPK && !RK) ? (TKO > 8 ? 3u : 2u) : 1u;
   constexpr uint32_t RECS = TAB, RCPS = TAB + kWave * REC, IDW = RCPS + 8 * kSets,
-                     LDSW = IDW + kWave;
+                     XTAB = IDW + kWave, LDSW = XTAB + (TT - 1) * TAB;
+  auto row_base = [&](uint32_t q) -> uint32_t { return q == 0 ? 0u : XTAB + (q - 1u) * TAB; };
   __shared__ __attribute__((aligned(16))) uint32_t lds_all[kBlock / kWave][LDSW];
   const uint32_t lane = lane_id();
   uint32_t* lds = lds_all[threadIdx.x >> 6];
@@ -1753,6 +1759,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         (int)(uint32_t)(b >> 32), l) << 32)));
   };
   uint32_t set = 0, nsets = 0;
+  bool has_set = false;  // this lane is in one of the sets (else it overflowed them)
   uint64_t rem = act_mask;
   float u_bw = 0.f, u_core = 0.f, u_pow = 0.f;  // set 0's reciprocals (wave-uniform)
   double u_free = 0.0, u_tot = 0.0;
@@ -1763,7 +1770,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     const bool in = act && sc.r_bw == b_bw && sc.r_core == b_core && sc.r_pow == b_pow &&
                     sc.r_free == b_free && sc.r_tot == b_tot;
     const uint64_t in_b = ballot(in) & rem;
-    if ((in_b >> lane) & 1ull) set = nsets;
+    if ((in_b >> lane) & 1ull) {
+      set = nsets;
+      has_set = true;
+    }
     rem &= ~in_b;
     if (nsets == 0) {
       u_bw = b_bw;
@@ -2035,7 +2045,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         // per-pod pass)
         const bool is_rec = !RK && rec_ok && fast && range <= 1u;
         rec_b = ballot(is_rec);
-        if (!RK && rec_b != 0ull) {
+        if (!RK && (rec_b != 0ull || (TT > 1u && ballot(fast && !is_rec) != 0ull))) {
           if (is_rec) {
             *reinterpret_cast<uint4*>(rec) = make_uint4(ck, (uint32_t)mask,
                                                         (uint32_t)(mask >> 32), thr);
@@ -2054,6 +2064,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
                                     2u * (uint32_t)((float)core * v_core) +
                                     (uint32_t)((float)pw * v_pow);
             uint32_t sel = 0, sel_hi = 0;
+            // the set's prefix row of this node lane (TT > 1, the first TT sets)
+            uint32_t* trow = lds + row_base(q < TT ? q : 0u) + lane * PSW;
+            const bool wrow = TT > 1u && q < TT;
+            if (wrow) trow[0] = 0u;
             auto row = [&](auto rk) {
               uint32_t acc = 0;
 #pragma unroll
@@ -2061,6 +2075,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
                 acc += mem_term<decltype(rk)::value>(fs.v[t], ts.v[t], v_free, v_tot, args.mt);
                 sel = (uint32_t)(t + 1) == nq_lo ? acc : sel;
                 sel_hi = (uint32_t)(t + 1) == nq_hi ? acc : sel_hi;
+                if (wrow) trow[t + 1] = (uint32_t)(t + 1) * shared + acc;
               }
             };
             row(std::integral_constant<bool, RK>{});
@@ -2178,6 +2193,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         if (uni_max) {
           const uint32_t* tab = lds + (uint32_t)j * PSW;
           basic = ckj >= sc.c ? tab[nq] : 0u;  // B[nq]
+        } else if (TT > 1u &&
+                   ballot(((mj >> lane) & 1ull) != 0ull && !(has_set && set < TT)) == 0ull) {
+          // several reciprocal sets, every lane in a tabled one: its set's row of the node
+          const uint32_t* tab = lds + row_base(set) + (uint32_t)j * PSW;
+          basic = ckj >= sc.c ? tab[nq] : 0u;
         } else {
           // several reciprocal sets: Scorer<N32>'s one-model branch on the node lane's data,
           // with its own reciprocals (shared quotients f32, memory quotients f64)
