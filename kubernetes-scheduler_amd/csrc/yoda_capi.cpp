@@ -3939,8 +3939,19 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
       // pod ws + next could not be certified: it opens the next window (evaluated against the
       // current state, so it is always resolved there); size it after this one's progress
       ++h->greedy_restarts;
+      // the next window holds 130 % of this one's progress, in whole waves: small windows cost
+      // less (K1 / K2 time grows with the pods) and most restart near where the last one did;
+      // profiles/r03/greedy_capacity/grow_ab.txt (1.81-1.91 s with the earlier power of two >=
+      // twice the progress, 1.57-1.64 s at 130 %).  YODA_GREEDY_GROW_PCT: A/B knob (0: that
+      // power of two)
+      static const uint32_t grow = env_u32("YODA_GREEDY_GROW_PCT", 130);
       uint32_t w2 = 64;
-      while (w2 < 2 * next && w2 < Wmax) w2 <<= 1;
+      if (grow) {
+        const uint64_t t = (uint64_t)next * grow / 100;
+        w2 = (uint32_t)std::min<uint64_t>(Wmax, std::max<uint64_t>(64, (t + 63) / 64 * 64));
+      } else {
+        while (w2 < 2 * next && w2 < Wmax) w2 <<= 1;
+      }
       W = std::min(w2, Wmax);
       ws += next;
     } else {
