@@ -2634,6 +2634,32 @@ struct PodGather {
   }
 };
 
+// Queue order (sort.go:8-10): scv/priority descending, then input index.  A counting sort
+// when the priorities span < 2^16 values (the usual small integers), else a stable sort.
+void queue_order(const int64_t* prio, uint32_t P, std::vector<uint32_t>& order) {
+  order.resize(P);
+  if (!prio || P == 0) {
+    for (uint32_t i = 0; i < P; ++i) order[i] = i;
+    return;
+  }
+  int64_t lo = prio[0], hi = prio[0];
+  for (uint32_t i = 1; i < P; ++i) {
+    lo = std::min(lo, prio[i]);
+    hi = std::max(hi, prio[i]);
+  }
+  if ((uint64_t)hi - (uint64_t)lo < (1u << 16)) {
+    const uint32_t R = (uint32_t)((uint64_t)hi - (uint64_t)lo) + 1;
+    std::vector<uint32_t> start(R + 1, 0);
+    for (uint32_t i = 0; i < P; ++i) ++start[(uint32_t)((uint64_t)hi - (uint64_t)prio[i]) + 1];
+    for (uint32_t r = 0; r < R; ++r) start[r + 1] += start[r];
+    for (uint32_t i = 0; i < P; ++i) order[start[(uint32_t)((uint64_t)hi - (uint64_t)prio[i])]++] = i;
+    return;
+  }
+  for (uint32_t i = 0; i < P; ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(),
+                   [prio](uint32_t a, uint32_t b) { return prio[a] > prio[b]; });
+}
+
 // 6144 pods: larger windows cost fewer, longer GPU windows but more exact fallbacks (touched
 // nodes invalidate more candidate lists); profiles/r02/final/greedy_window_ab.txt
 constexpr uint32_t kGreedyWindow = 6144;
@@ -2741,13 +2767,8 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
     if (P == 0) return YODA_OK;
     int rc;
     // Queue order: sort.Less (sort.go:8-10) -- scv/priority descending, then input index.
-    std::vector<uint32_t> order(P);
-    for (uint32_t i = 0; i < P; ++i) order[i] = i;
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-      const int64_t pa = pods->priority ? pods->priority[a] : 0;
-      const int64_t pb = pods->priority ? pods->priority[b] : 0;
-      return pa > pb;
-    });
+    std::vector<uint32_t> order;
+    queue_order(pods->priority, P, order);
     if (mode == YODA_MODE_DISKIO) {  // Mode B reads no assumed-pod state: independent cycles
       PodGather all;
       all.build(pods, order.data(), P);
@@ -3527,12 +3548,7 @@ int yoda_gs_create(const yoda_node_soa* nodes, const yoda_pod_soa* pods, uint32_
     }
     g->pick.assign(P, YODA_PICK_NONE);
     // queue order: sort.Less (sort.go:8-10), scv/priority descending, then input index
-    g->order.resize(P);
-    for (uint32_t i = 0; i < P; ++i) g->order[i] = i;
-    const int64_t* pr = pods->priority;
-    std::stable_sort(g->order.begin(), g->order.end(), [pr](uint32_t a, uint32_t b) {
-      return (pr ? pr[a] : 0) > (pr ? pr[b] : 0);
-    });
+    queue_order(pods->priority, P, g->order);
     *out = g;
     return YODA_OK;
   } catch (...) {
