@@ -2781,6 +2781,7 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
       return YODA_OK;
     }
     if ((flags & YODA_GREEDY_CARD_CAPACITY) && !h->generic) return greedy_capacity(h, pods, pick);
+    uint64_t spec_n = 0, spec_sum = 0, spec_big = 0, spec_waves = 0;  // YODA_GREEDY_SPEC
     GreedyState g;
     g.h = h;
     g.alloc = h->h_alloc;
@@ -2879,6 +2880,7 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
         const auto tr = Clock::now();
         double fb_ms = 0;
         bool wrapped = false;
+        static const bool spec_dbg = std::getenv("YODA_GREEDY_SPEC") != nullptr;
         for (uint32_t i = 0; i < wn; ++i) {
           const uint32_t p = order[ws + i];
           const uint32_t q = pos[i];  // sorted position: the device outputs' index
@@ -2918,6 +2920,29 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
             if (certified) {
               pk = (int32_t)bi;
             } else {
+              if (spec_dbg) {  // diagnostic: later window pods already uncertified now
+                uint64_t c = 0, lastw = ~0ull, wv = 0;
+                for (uint32_t j = i + 1; j < wn; ++j) {
+                  const uint32_t qj = pos[j];
+                  const uint32_t nfj = counts[qj];
+                  if (nfj < 2 || nfj <= KT || counts[(size_t)wn + qj] > 0) continue;
+                  double b = -1.0;
+                  uint32_t bj = 0xffffffffu;
+                  for (uint32_t k = 0; k < KT; ++k) {
+                    const uint32_t node = ti[(size_t)k * wn + qj];
+                    const uint32_t n = node - h->node_offset;
+                    double cur = ts[(size_t)k * wn + qj];
+                    if (g.touched_w[n]) cur = cur - (double)g.stat_w[n] + (double)g.stat[n];
+                    if (cur > b || (cur == b && node < bj)) b = cur, bj = node;
+                  }
+                  const double Tj = ts[(size_t)(KT - 1) * wn + qj];
+                  if (!(b > Tj || (b == Tj && bj <= ti[(size_t)(KT - 1) * wn + qj]))) {
+                    ++c;
+                    if ((qj >> 6) != lastw) ++wv, lastw = qj >> 6;
+                  }
+                }
+                spec_n += 1, spec_sum += c, spec_big += c >= 4 ? 1 : 0, spec_waves += wv;
+              }
               const auto tf = Clock::now();
               if ((rc = greedy_eval_fast(g, q, &pk))) return rc;
               ++h->greedy_fallbacks;
@@ -2941,6 +2966,11 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
                    "(%.1f ms), resolve %.1f ms\n", h->greedy_windows, h->greedy_window_ms,
                    h->greedy_prep_ms, h->greedy_fallbacks, h->greedy_fallback_ms,
                    h->greedy_resolve_ms);
+    if (std::getenv("YODA_GREEDY_SPEC"))
+      std::fprintf(stderr, "greedy spec: fallbacks %llu, later uncertified per fallback %.2f, "
+                   ">= 4: %llu, distinct waves %.2f\n", (unsigned long long)spec_n,
+                   spec_n ? (double)spec_sum / spec_n : 0.0, (unsigned long long)spec_big,
+                   spec_n ? (double)spec_waves / spec_n : 0.0);
     // Leave the uploaded snapshot unchanged: restore static score and CardNumber.
     for (uint32_t n : all_touched) {
       g.stat[n] = stat0[n];
