@@ -398,6 +398,7 @@ struct yoda_handle {
   PinnedBuf upd_stage, pick_stage, win_stage;
   PinnedBuf poll_stage;  // coherent: the greedy fallback's pick, polled by the host
   uint32_t greedy_restarts = 0;
+  uint32_t greedy_refreshes = 0;  // flags-0 mid-window list refreshes (last yoda_greedy)
   hipEvent_t upd_event = nullptr;
   bool upd_pending = false;
   std::vector<uint32_t> h_pos;  // yoda_shard_topk: caller pod index -> sorted position
@@ -2758,6 +2759,7 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
     h->greedy_windows = 0;
     h->greedy_fallbacks = 0;
     h->greedy_restarts = 0;
+    h->greedy_refreshes = 0;
     h->greedy_window_ms = h->greedy_fallback_ms = h->greedy_resolve_ms = 0;
     h->greedy_prep_ms = 0;
     using Clock = std::chrono::steady_clock;
@@ -2781,7 +2783,6 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
       return YODA_OK;
     }
     if ((flags & YODA_GREEDY_CARD_CAPACITY) && !h->generic) return greedy_capacity(h, pods, pick);
-    uint64_t spec_n = 0, spec_sum = 0, spec_big = 0, spec_waves = 0;  // YODA_GREEDY_SPEC
     GreedyState g;
     g.h = h;
     g.alloc = h->h_alloc;
@@ -2839,7 +2840,8 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
       std::vector<uint32_t> counts(2 * (size_t)W);
       std::vector<double> ts((size_t)KT * W);
       std::vector<uint32_t> ti((size_t)KT * W);
-      std::vector<uint32_t> perm(W), pos(W);
+      std::vector<uint32_t> perm(W), pos(W), Tidx, ti2;
+      std::vector<double> Tw, ts2;
       for (uint32_t ws = 0; ws < P; ws += W) {
         const uint32_t wn = std::min(W, P - ws);
         const auto tw = Clock::now();
@@ -2875,12 +2877,90 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
         for (uint32_t i = 0; i < wn; ++i) pos[i] = i;
         if (h->ordered)
           for (uint32_t q = 0; q < wn; ++q) pos[perm[q]] = q;
+        // each list's certificate threshold: its last entry's window-start (or refresh-time)
+        // score and node
+        Tw.resize(wn), Tidx.resize(wn);
+        auto set_thresholds = [&](uint32_t q) {
+          const uint32_t len = std::max<uint32_t>(1, std::min<uint32_t>(counts[q], KT));
+          Tw[q] = ts[(size_t)(len - 1) * wn + q];
+          Tidx[q] = ti[(size_t)(len - 1) * wn + q];
+        };
+        for (uint32_t q = 0; q < wn; ++q) set_thresholds(q);
         ++h->greedy_windows;
         h->greedy_window_ms += ms_since(tw);
         const auto tr = Clock::now();
         double fb_ms = 0;
         bool wrapped = false;
-        static const bool spec_dbg = std::getenv("YODA_GREEDY_SPEC") != nullptr;
+        // the best current candidate of sorted position q (window-start score - old static +
+        // new static) and whether it is certified: every node outside the list scored <= T at
+        // window start (ties: higher index) and its score can only have dropped since
+        auto certify = [&](uint32_t q, uint32_t* best_node) {
+          const uint32_t nf = counts[q];
+          const uint32_t len = std::min<uint32_t>(nf, KT);
+          double bs = -1.0;
+          uint32_t bi = 0xffffffffu;
+          for (uint32_t k = 0; k < len; ++k) {
+            const uint32_t node = ti[(size_t)k * wn + q];
+            const uint32_t n = node - h->node_offset;
+            double cur = ts[(size_t)k * wn + q];
+            if (g.touched_w[n]) cur = cur - (double)g.stat_w[n] + (double)g.stat[n];
+            if (cur > bs || (cur == bs && node < bi)) {
+              bs = cur;
+              bi = node;
+            }
+          }
+          *best_node = bi;
+          return nf <= KT || bs > Tw[q] || (bs == Tw[q] && bi <= Tidx[q]);
+        };
+        // Mid-window list refresh: a window whose lists went stale (similar pods took their
+        // shared top nodes) would otherwise send each of its remaining similar pods to an
+        // exact fallback.  Every kFbCheck fallbacks the next kScan window pods are checked; if
+        // at least kScanMin of them are uncertified already (they stay so: scores only drop),
+        // the window's top-k K2 runs again against the current state (the window's K1 masks
+        // and maxima stay valid: only static scores change in this mode).  A refreshed entry
+        // is stored as  score + old static - current static  of its node, so the certificate
+        // above yields its current score from then on; the threshold is the refresh-time
+        // score (unlisted nodes scored at most that then and only dropped since).
+        // YODA_GREEDY_REFRESH=0: off (A/B knob).
+        static const bool refresh_on = env_u32("YODA_GREEDY_REFRESH", 1) != 0;
+        constexpr uint32_t kFbCheck = 16, kScan = 256, kScanMin = 32;
+        uint32_t fb_since = 0;
+        auto maybe_refresh = [&](uint32_t i) -> int {
+          if (!refresh_on || wrapped || N == 0 || ++fb_since < kFbCheck || wn - i < 2 * kScan)
+            return YODA_OK;
+          fb_since = 0;
+          uint32_t unc = 0, bj;
+          for (uint32_t j = i + 1; j < std::min(wn, i + 1 + kScan); ++j) {
+            const uint32_t qj = pos[j];
+            if (counts[qj] >= 2 && counts[(size_t)wn + qj] == 0 && !certify(qj, &bj)) ++unc;
+          }
+          if (unc < kScanMin) return YODA_OK;
+          int r = g.push_dirty();
+          if (r) return r;
+          if ((r = topk_lists(h, wn, KT, h->counts.as<uint32_t>()))) return r;
+          ts2.resize((size_t)KT * wn), ti2.resize((size_t)KT * wn);
+          HIP_TRY(h, hipMemcpyAsync(ts2.data(), h->tk_s.p, (size_t)KT * wn * 8,
+                                    hipMemcpyDeviceToHost, h->stream));
+          HIP_TRY(h, hipMemcpyAsync(ti2.data(), h->tk_i.p, (size_t)KT * wn * 4,
+                                    hipMemcpyDeviceToHost, h->stream));
+          HIP_TRY(h, hipStreamSynchronize(h->stream));
+          for (uint32_t j = i; j < wn; ++j) {
+            const uint32_t qj = pos[j];
+            const uint32_t len = std::min<uint32_t>(counts[qj], KT);
+            for (uint32_t k = 0; k < len; ++k) {
+              const size_t o = (size_t)k * wn + qj;
+              const uint32_t n = ti2[o] - h->node_offset;
+              ti[o] = ti2[o];
+              ts[o] = g.touched_w[n] ? ts2[o] + (double)g.stat_w[n] - (double)g.stat[n] : ts2[o];
+            }
+            if (len) {
+              Tw[qj] = ts2[(size_t)(len - 1) * wn + qj];
+              Tidx[qj] = ti2[(size_t)(len - 1) * wn + qj];
+            }
+          }
+          ++h->greedy_refreshes;
+          return YODA_OK;
+        };
         for (uint32_t i = 0; i < wn; ++i) {
           const uint32_t p = order[ws + i];
           const uint32_t q = pos[i];  // sorted position: the device outputs' index
@@ -2898,56 +2978,20 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
             ++h->greedy_fallbacks;
             fb_ms += ms_since(tf);
           } else {
-            // current score of each candidate: window-start score - old static + new static
-            const uint32_t len = std::min<uint32_t>(nf, KT);
-            double bs = -1.0;
-            uint32_t bi = 0xffffffffu;
-            for (uint32_t k = 0; k < len; ++k) {
-              const uint32_t node = ti[(size_t)k * wn + q];
-              const uint32_t n = node - h->node_offset;
-              double cur = ts[(size_t)k * wn + q];
-              if (g.touched_w[n]) cur = cur - (double)g.stat_w[n] + (double)g.stat[n];
-              if (cur > bs || (cur == bs && node < bi)) {
-                bs = cur;
-                bi = node;
-              }
-            }
-            // every node outside the list scored <= T at window start (ties: higher index)
-            // and its score can only have dropped since
-            const double T = ts[(size_t)(len - 1) * wn + q];
-            const uint32_t tidx = ti[(size_t)(len - 1) * wn + q];
-            const bool certified = nf <= KT || bs > T || (bs == T && bi <= tidx);
-            if (certified) {
-              pk = (int32_t)bi;
-            } else {
-              if (spec_dbg) {  // diagnostic: later window pods already uncertified now
-                uint64_t c = 0, lastw = ~0ull, wv = 0;
-                for (uint32_t j = i + 1; j < wn; ++j) {
-                  const uint32_t qj = pos[j];
-                  const uint32_t nfj = counts[qj];
-                  if (nfj < 2 || nfj <= KT || counts[(size_t)wn + qj] > 0) continue;
-                  double b = -1.0;
-                  uint32_t bj = 0xffffffffu;
-                  for (uint32_t k = 0; k < KT; ++k) {
-                    const uint32_t node = ti[(size_t)k * wn + qj];
-                    const uint32_t n = node - h->node_offset;
-                    double cur = ts[(size_t)k * wn + qj];
-                    if (g.touched_w[n]) cur = cur - (double)g.stat_w[n] + (double)g.stat[n];
-                    if (cur > b || (cur == b && node < bj)) b = cur, bj = node;
-                  }
-                  const double Tj = ts[(size_t)(KT - 1) * wn + qj];
-                  if (!(b > Tj || (b == Tj && bj <= ti[(size_t)(KT - 1) * wn + qj]))) {
-                    ++c;
-                    if ((qj >> 6) != lastw) ++wv, lastw = qj >> 6;
-                  }
-                }
-                spec_n += 1, spec_sum += c, spec_big += c >= 4 ? 1 : 0, spec_waves += wv;
-              }
+            uint32_t bi;
+            bool certified = certify(q, &bi);
+            if (!certified) {
               const auto tf = Clock::now();
-              if ((rc = greedy_eval_fast(g, q, &pk))) return rc;
-              ++h->greedy_fallbacks;
+              const uint32_t before = h->greedy_refreshes;
+              if ((rc = maybe_refresh(i))) return rc;
+              if (h->greedy_refreshes != before) certified = certify(q, &bi);
+              if (!certified) {
+                if ((rc = greedy_eval_fast(g, q, &pk))) return rc;
+                ++h->greedy_fallbacks;
+              }
               fb_ms += ms_since(tf);
             }
+            if (certified) pk = (int32_t)bi;
           }
           pick[p] = pk;
           if (pk >= 0) {
@@ -2966,11 +3010,8 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
                    "(%.1f ms), resolve %.1f ms\n", h->greedy_windows, h->greedy_window_ms,
                    h->greedy_prep_ms, h->greedy_fallbacks, h->greedy_fallback_ms,
                    h->greedy_resolve_ms);
-    if (std::getenv("YODA_GREEDY_SPEC"))
-      std::fprintf(stderr, "greedy spec: fallbacks %llu, later uncertified per fallback %.2f, "
-                   ">= 4: %llu, distinct waves %.2f\n", (unsigned long long)spec_n,
-                   spec_n ? (double)spec_sum / spec_n : 0.0, (unsigned long long)spec_big,
-                   spec_n ? (double)spec_waves / spec_n : 0.0);
+    if (std::getenv("YODA_GREEDY_DEBUG"))
+      std::fprintf(stderr, "greedy: mid-window list refreshes %u\n", h->greedy_refreshes);
     // Leave the uploaded snapshot unchanged: restore static score and CardNumber.
     for (uint32_t n : all_touched) {
       g.stat[n] = stat0[n];
