@@ -3991,7 +3991,25 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
       if ((rc = yoda_gs_resolve(g, &next))) return fail(h, rc, "greedy: resolve");
       // YODA_GREEDY_FAIL_DIV (A/B knob): one exact evaluation allowed per that many resolved pods
       static const uint32_t rate = env_u32("YODA_GREEDY_FAIL_DIV", 0);
-      if (next >= wn || ++fails > (rate ? next / rate : 0)) break;
+      // YODA_GREEDY_CAP_SCAN=<n> (A/B knob): fall back exactly (instead of restarting) when at
+      // most YODA_GREEDY_CAP_SCAN_MAX of the next n window pods are uncertified already
+      static const uint32_t scan_n = env_u32("YODA_GREEDY_CAP_SCAN", 0);
+      static const uint32_t scan_max = env_u32("YODA_GREEDY_CAP_SCAN_MAX", 1);
+      if (next >= wn) break;
+      bool fallback = false;
+      if (rate) {
+        fallback = ++fails <= next / rate;
+      } else if (scan_n && wn - next > scan_n) {
+        uint64_t saved[6];
+        std::copy(std::begin(g->why), std::end(g->why), saved);
+        uint32_t unc = 0;
+        int32_t dummy;
+        for (uint32_t j = next + 1; j <= next + scan_n && unc <= scan_max; ++j)
+          unc += g->resolve_capacity(j, g->order[ws + j], &dummy) ? 0u : 1u;
+        std::copy(std::begin(saved), std::end(saved), std::begin(g->why));
+        fallback = unc <= scan_max;
+      }
+      if (!fallback) break;
       const auto tf = Clock::now();
       if ((rc = push())) return rc;
       int32_t pk = YODA_PICK_NONE;
