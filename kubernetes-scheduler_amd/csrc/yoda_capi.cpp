@@ -2914,8 +2914,9 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
         };
         // Mid-window list refresh: a window whose lists went stale (similar pods took their
         // shared top nodes) would otherwise send each of its remaining similar pods to an
-        // exact fallback.  Every kFbCheck fallbacks the next kScan window pods are checked; if
-        // at least kScanMin of them are uncertified already (they stay so: scores only drop),
+        // exact fallback.  Every kFbCheck (8) fallbacks the next kScan (256) window pods are
+        // checked; if at least kScanMin (16) of them are uncertified already (they stay so:
+        // scores only drop),
         // the window's top-k K2 runs again against the current state (the window's K1 masks
         // and maxima stay valid: only static scores change in this mode).  A refreshed entry
         // is stored as  score + old static - current static  of its node, so the certificate
@@ -2923,7 +2924,11 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
         // score (unlisted nodes scored at most that then and only dropped since).
         // YODA_GREEDY_REFRESH=0: off (A/B knob).
         static const bool refresh_on = env_u32("YODA_GREEDY_REFRESH", 1) != 0;
-        constexpr uint32_t kFbCheck = 16, kScan = 256, kScanMin = 32;
+        // (YODA_GREEDY_REFRESH_EVERY / _MIN: A/B knobs for the check period and the bar)
+        static const uint32_t kFbCheck =
+            std::max<uint32_t>(1, env_u32("YODA_GREEDY_REFRESH_EVERY", 8));
+        static const uint32_t kScanMin = env_u32("YODA_GREEDY_REFRESH_MIN", 16);
+        constexpr uint32_t kScan = 256;
         uint32_t fb_since = 0;
         auto maybe_refresh = [&](uint32_t i) -> int {
           if (!refresh_on || wrapped || N == 0 || ++fb_since < kFbCheck || wn - i < 2 * kScan)
@@ -3847,7 +3852,11 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
   auto ms_since = [](Clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
   };
-  const uint32_t P = pods->n_pods, N = h->n_nodes, KT = (uint32_t)topk_k_capacity();
+  // YODA_GREEDY_CAP_TOPK=8 (A/B knob): the shorter lists of the flags-0 mode
+  static const uint32_t kt_cap =
+      env_u32("YODA_GREEDY_CAP_TOPK", 0) == (uint32_t)topk_k() ? (uint32_t)topk_k()
+                                                               : (uint32_t)topk_k_capacity();
+  const uint32_t P = pods->n_pods, N = h->n_nodes, KT = kt_cap;
   yoda_node_soa nv{};
   nv.n_nodes = N;
   nv.max_cards = 1;
