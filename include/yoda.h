@@ -335,6 +335,10 @@ int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks,
  * stays 0); the YODA_GREEDY_FAIL_DIV environment knob re-enables one-by-one fallbacks for
  * A/B runs. */
 int yoda_greedy_restarts(const yoda_t* h, uint32_t* restarts);
+/* flags == 0: mid-window list refreshes of the last yoda_greedy (the window's top-k lists
+ * recomputed against the current state once many of its remaining pods had gone uncertified;
+ * DESIGN.md §5). */
+int yoda_greedy_refreshes(const yoda_t* h, uint32_t* refreshes);
 
 /* ---- sharded greedy batch (node shards on several GPUs) ------------------------------
  * yoda_greedy's windowed algorithm split at its exchange points, so each rank's handle holds

@@ -3039,6 +3039,12 @@ int yoda_greedy_restarts(const yoda_t* h, uint32_t* restarts) {
   return YODA_OK;
 }
 
+int yoda_greedy_refreshes(const yoda_t* h, uint32_t* refreshes) {
+  if (!h || !refreshes) return YODA_ERR_INVALID_ARG;
+  *refreshes = h->greedy_refreshes;
+  return YODA_OK;
+}
+
 int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks,
                       double* times_ms) {
   if (!h) return YODA_ERR_INVALID_ARG;

@@ -82,6 +82,7 @@ _SIGS = {
     "yoda_class_stats_read": ([_vp, _vp], C.c_int),
     "yoda_k2_trace_read": ([_vp, _vp, C.c_uint64], C.c_int),
     "yoda_greedy_restarts": ([_vp, C.POINTER(C.c_uint32)], C.c_int),
+    "yoda_greedy_refreshes": ([_vp, C.POINTER(C.c_uint32)], C.c_int),
     "yoda_comm_unique_id": ([_vp], C.c_int),
     "yoda_comm_init": ([_vp, _vp, C.c_int, C.c_int], C.c_int),
     "yoda_comm_run": ([_vp, C.c_int], C.c_int),
@@ -305,6 +306,12 @@ class Yoda:
         """Capacity greedy: windows that ended early at an uncertified pod."""
         r = C.c_uint32()
         self._check(lib().yoda_greedy_restarts(self._h, C.byref(r)), "yoda_greedy_restarts")
+        return r.value
+
+    def greedy_refreshes(self) -> int:
+        """Flags-0 greedy: mid-window top-k list refreshes of the last greedy()."""
+        r = C.c_uint32()
+        self._check(lib().yoda_greedy_refreshes(self._h, C.byref(r)), "yoda_greedy_refreshes")
         return r.value
 
     def order_info(self) -> dict:

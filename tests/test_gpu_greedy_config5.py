@@ -60,6 +60,9 @@ def test_config5_full_size(cfg5, flags):
     pick = y.greedy(pods, MODE_SCV, flags)
     windows, restarts = y.greedy_stats()
     assert windows >= P // 6144  # windows of at most kGreedyWindow pods (yoda_capi.cpp)
+    if flags == 0:
+        # the mid-window list refresh ran (the replays below sample the windows it served)
+        assert y.greedy_refreshes() > 0
 
     # 1. exact prefix against the sequential oracle
     pre = order[:2000]
@@ -91,8 +94,9 @@ def test_config5_full_size(cfg5, flags):
     # window boundaries (6144-pod windows) and their neighbours, where a window's candidate
     # lists give way to the next window's
     wb = np.array([6144 * k + d for k in (1, 40, 120) for d in (-1, 0, 1)])
+    # and the first two windows, where the flags-0 fallbacks and list refreshes cluster
     qs = np.unique(np.concatenate([[0, 2000, P // 2, P - 1], wb[wb < P],
-                                   rng.integers(0, P, size=8)]))
+                                   rng.integers(0, P, size=8), rng.integers(0, 2 * 6144, size=12)]))
     two = Yoda(0)
     for q in qs:
         alloc, cnq = _replay_state(nodes, pods, order, pick, int(q), flags)
