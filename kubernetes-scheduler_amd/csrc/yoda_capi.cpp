@@ -3915,7 +3915,7 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
   } guard{g};
   const uint32_t Wmax = greedy_window();
   uint32_t W = Wmax;
-  std::vector<uint32_t> ids, cnt_w, ti_w, wc_w, pos;
+  std::vector<uint32_t> ids, cnt_w, ti_w, wc_w;
   std::vector<uint64_t> al, cn, mx_w;
   std::vector<double> ts_w;
   auto push = [&]() -> int {  // nodes the session changed -> the device
