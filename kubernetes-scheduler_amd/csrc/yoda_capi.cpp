@@ -1990,10 +1990,12 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
       if (g_run) gt.add(g_last, g_run, r_max, r_min);
       for (int f = 0; f < 3; ++f) kor_out[f] = kor[f];
     };
-    // ranges of >= 4096 pods over the process's worker pool (HostPool)
+    // ranges of >= YODA_UPLOAD_MIN_RANGE (default 4096) pods over the process's worker pool
+    // (HostPool); A/B knob for the greedy windows' 6144-pod uploads
     static const uint32_t thr_cap = env_u32("YODA_UPLOAD_THREADS", 16);
+    static const uint32_t min_range = std::max<uint32_t>(256, env_u32("YODA_UPLOAD_MIN_RANGE", 4096));
     const uint32_t n_thr = std::min<uint32_t>({HostPool::get().size(), std::max(1u, thr_cap),
-                                               std::max(1u, P / 4096u)});
+                                               std::max(1u, P / min_range)});
     std::vector<GroupTable> tables(n_thr);
     std::vector<std::array<uint64_t, 3>> kors(n_thr, {0ull, 0ull, 0ull});
     {
