@@ -280,7 +280,9 @@ int yoda_comm_greedy_local(yoda_t* const* handles, int world, const yoda_node_so
 /* Mode A runs of more than 128 pods (yoda_run, yoda_score_rows, yoda_shard_phase1) sort the
  * batch on the device by the Filter's inputs so that whole wavefronts skip infeasible nodes;
  * every output is returned in the caller's pod order, so results never depend on it.
- * enable = 0 turns the ordering off (default on).  Takes effect from the next run. */
+ * enable = 0 turns the ordering off; 1 (default) orders, a private run (yoda_run) padding each
+ * (clock, number, has-memory) group to a wave boundary when that adds at most 1/8 of the
+ * batch; 2 orders without the padding.  Takes effect from the next run. */
 int yoda_set_pod_order(yoda_t* h, int enable);
 /* The batch order (diagnostic): out[4] = {(clock, number, has-memory) groups of the uploaded
  * batch (0: too many for the counting sort), its sorted positions with every group padded to

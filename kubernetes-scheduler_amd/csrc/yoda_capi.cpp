@@ -360,6 +360,7 @@ struct yoda_handle {
   // from pod_sorted (sorted position i = original pod perm[i]); bitmask/rows stay in sorted
   // order and are un-permuted by their transposes, the per-pod outputs by finalize().
   bool order_enabled = true;
+  bool order_pad = true;  // yoda_set_pod_order(h, 1): pad private runs' groups to waves
   bool ordered = false;
   DevBuf pod_sorted, perm, order_scratch;
   uint32_t key_bits[3] = {24, 8, 32};  // widths of the batch's sort-key fields (c, n, m)
@@ -602,7 +603,21 @@ class HostPool {
   bool stop_ = false;
 };
 
-static uint32_t env_u32(const char* name, uint32_t dflt) {
+// Tuning knobs of the A/B harness (tools/ab_lib.sh).  Only the A/B build reads them from
+// the environment (`make ab` -> libyoda_ab.so, -DYODA_AB_KNOBS); in the release library
+// YODA_KNOB(name, default) is the default itself and the name is not even in the binary, so
+// a scheduler process's environment cannot change kernel choice, chunking or greedy policy.
+#ifdef YODA_AB_KNOBS
+static uint32_t knob_env(const char* name, uint32_t dflt) {
+  const char* s = std::getenv(name);
+  return (s && *s) ? (uint32_t)std::strtoul(s, nullptr, 10) : dflt;
+}
+#define YODA_KNOB(name, dflt) knob_env(name, dflt)
+#else
+#define YODA_KNOB(name, dflt) ((uint32_t)(dflt))
+#endif
+// Diagnostics (*_TRACE, *_DEBUG): counters, timings and traces only, never results or policy.
+static uint32_t diag_env(const char* name, uint32_t dflt) {
   const char* s = std::getenv(name);
   return (s && *s) ? (uint32_t)std::strtoul(s, nullptr, 10) : dflt;
 }
@@ -611,7 +626,7 @@ constexpr uint32_t kMinChunkNodes = 1536;
 
 void plan_chunks_for(uint32_t cap, uint32_t rounds, uint32_t n_pods, uint32_t n_nodes,
                      uint32_t* C_out, uint32_t* chunk_out) {
-  static const uint32_t min_chunk = env_u32("YODA_MIN_CHUNK_NODES", 0);
+  static const uint32_t min_chunk = YODA_KNOB("YODA_MIN_CHUNK_NODES", 0);
   const uint32_t pod_blocks = std::max<uint32_t>(1, (n_pods + kBlock - 1) / kBlock);
   const uint32_t max_chunks = std::max<uint32_t>(1, (n_nodes + kChunkAlign - 1) / kChunkAlign);
   if (cap == 0) cap = 2048;
@@ -645,14 +660,14 @@ int capacity(yoda_t* h, int which, int mode) {
 
 void plan_chunks(yoda_t* h, int mode, uint32_t n_pods, uint32_t n_nodes) {
   // K1's partials are 32 B a (pod, chunk) and its reduce reads them all: fewer rounds
-  static const uint32_t r1 = std::max<uint32_t>(1, env_u32("YODA_CHUNK_ROUNDS1",
-                                                           env_u32("YODA_CHUNK_ROUNDS", 6)));
-  static const uint32_t r2 = std::max<uint32_t>(1, env_u32("YODA_CHUNK_ROUNDS2",
-                                                           env_u32("YODA_CHUNK_ROUNDS", 8)));
+  static const uint32_t r1 = std::max<uint32_t>(1, YODA_KNOB("YODA_CHUNK_ROUNDS1",
+                                                           YODA_KNOB("YODA_CHUNK_ROUNDS", 6)));
+  static const uint32_t r2 = std::max<uint32_t>(1, YODA_KNOB("YODA_CHUNK_ROUNDS2",
+                                                           YODA_KNOB("YODA_CHUNK_ROUNDS", 8)));
   plan_chunks_for((uint32_t)capacity(h, 1, mode), r1, n_pods, n_nodes, &h->C1, &h->chunk1);
   // YODA_K1_MAX_CHUNKS (A/B knob, default off): at most that many K1 chunks, so that small
   // batches keep their partials (and k_reduce1's reads) few
-  static const uint32_t c1_max = env_u32("YODA_K1_MAX_CHUNKS", 0);
+  static const uint32_t c1_max = YODA_KNOB("YODA_K1_MAX_CHUNKS", 0);
   if (c1_max && h->C1 > c1_max) {
     h->chunk1 = ((n_nodes + c1_max - 1) / c1_max + kChunkAlign - 1) / kChunkAlign * kChunkAlign;
     h->C1 = std::max<uint32_t>(1, (n_nodes + h->chunk1 - 1) / h->chunk1);
@@ -1035,14 +1050,14 @@ int phase1_witness(yoda_t* h, uint64_t* maxima, uint32_t* counts, uint32_t* wit,
   }
   HIP_TRY(h, h->p_wit.ensure(12 * (size_t)h->C1 * P * 4));
   Partials part = partials(h);
-  static const bool block_wit = env_u32("YODA_BLOCK_WITNESS", 1) != 0;
+  static const bool block_wit = YODA_KNOB("YODA_BLOCK_WITNESS", 1) != 0;
   uint32_t C = h->C1;
   if (block_wit && h->path == Path::N32 && h->has_k1sum && h->has_k2sum && h->all_one_model) {
     // block-classified, like phase 1's K1: sparse masks and the block list for the window's K2.
     // Its per-(wave, chunk) epilogue (18 wave reductions, 104 B of partials a pod) is the
     // cost that grows with the chunk count: chunks of >= YODA_WIT_CHUNK_NODES nodes
     static const uint32_t wit_chunk = std::max<uint32_t>(
-        kChunkAlign, env_u32("YODA_WIT_CHUNK_NODES", 64) / kChunkAlign * kChunkAlign);
+        kChunkAlign, YODA_KNOB("YODA_WIT_CHUNK_NODES", 64) / kChunkAlign * kChunkAlign);
     uint32_t chunk = h->chunk1;
     if (chunk < wit_chunk) {
       chunk = wit_chunk;
@@ -1228,8 +1243,7 @@ int topk_lists(yoda_t* h, uint32_t P, uint32_t KT, const uint32_t* d_counts) {
   if (P == 0 || N == 0) return YODA_OK;
   uint32_t ib = 1;
   while ((1ull << ib) <= N) ++ib;  // node ids < 2^ib - 1: a real key is never 0
-  static const bool per_pair = std::getenv("YODA_TOPK_PER_PAIR") &&
-                               std::strcmp(std::getenv("YODA_TOPK_PER_PAIR"), "1") == 0;
+  static const bool per_pair = YODA_KNOB("YODA_TOPK_PER_PAIR", 0) == 1;
   const bool block = !per_pair && h->path == Path::N32 && h->has_k2sum && h->K <= 8 &&
                      ib <= 40 && h->score_bound < (1ull << (64 - ib));
   if (block) {
@@ -1237,12 +1251,12 @@ int topk_lists(yoda_t* h, uint32_t P, uint32_t KT, const uint32_t* d_counts) {
     // rounds of resident workgroups: 4 for window-sized batches (more, shorter per-(wave,
     // chunk) lists balance better), 1 below 2048 pods (the capacity windows, where the merge's
     // reads dominate); A/B in profiles/r02/greedy_topk/
-    static const uint32_t rt_env = env_u32("YODA_TOPK_ROUNDS", 0);
+    static const uint32_t rt_env = YODA_KNOB("YODA_TOPK_ROUNDS", 0);
     const uint32_t rt = rt_env ? rt_env : (P >= 2048 ? 4u : 1u);
     plan_chunks_for((uint32_t)capacity(h, 2, YODA_MODE_SCV), rt, P, N, &Ct, &cht);
     // YODA_TOPK_MIN_CHUNK (A/B knob): chunks of at least that many nodes -- fewer per-(wave,
     // chunk) lists to write and merge in small windows
-    static const uint32_t tk_min = env_u32("YODA_TOPK_MIN_CHUNK", 0);
+    static const uint32_t tk_min = YODA_KNOB("YODA_TOPK_MIN_CHUNK", 0);
     if (tk_min && cht < tk_min) {
       cht = (tk_min + kChunkAlign - 1) / kChunkAlign * kChunkAlign;
       Ct = std::max<uint32_t>(1, (N + cht - 1) / cht);
@@ -1626,7 +1640,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
       // the snapshot's mix, the groups' remainders last.  Copies of the K1 / K2 summaries in
       // that order; the kernels compare the nodes' local ids (perm_ids) on score ties.
       h->perm_on = false;
-      static const bool perm_env = env_u32("YODA_NODE_PERM", 1) != 0;
+      static const bool perm_env = YODA_KNOB("YODA_NODE_PERM", 1) != 0;
       std::vector<uint32_t> nperm;
       if (perm_env && path == Path::N32 && n_one_model == N && N >= 4096 &&
           !(flags & YODA_UPLOAD_PER_NODE_K1) && !(flags & YODA_UPLOAD_PER_NODE_K2)) {
@@ -1779,7 +1793,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     h->all_uni4 = n_uni4 == N;
     h->has_k2sum = want_sum && !(flags & YODA_UPLOAD_PER_NODE_K2);
     h->g = GTab{};
-    static const bool no_gtab = env_u32("YODA_NO_GTAB", 0) != 0;  // A/B knob
+    static const bool no_gtab = YODA_KNOB("YODA_NO_GTAB", 0) != 0;  // A/B knob
     if (h->has_k2sum && N > 0 && !no_gtab && !(flags & YODA_UPLOAD_NO_GTAB)) {
       h->g.tab = h->gtab.as<uint32_t>();
       std::memcpy(&h->g.r_bw, &g_rcp[0], 4);
@@ -1825,36 +1839,19 @@ int yoda_update_alloc(yoda_t* h, const uint64_t* alloc) {
   if (!h->has_nodes) return fail(h, YODA_ERR_NO_NODES, "no node snapshot uploaded");
   if (!alloc && h->n_nodes) return fail(h, YODA_ERR_INVALID_ARG, "alloc is NULL");
   try {
-    HIP_TRY(h, hipSetDevice(h->device));
-    const size_t stride = h->path == Path::N32 ? n32_stride(h->K) : node_stride(h->K);
-    uint64_t max_static = 0;
-    for (uint32_t i = 0; i < h->n_nodes; ++i) {
-      bool z = false;
-      const uint64_t s = static_score(h->h_free_sum[i], h->h_total_sum[i], alloc[i], &z);
-      unsigned char* r = h->host_records.data() + (size_t)i * stride;
-      if (h->generic) {
-        reinterpret_cast<NodeHdrG*>(r)->static_score = s;
-      } else {
-        reinterpret_cast<NodeHdrF*>(r)->static_score = (double)s;
-        max_static = std::max(max_static, s);
-        if (h->has_k2sum) {
-          const double sd = (double)s;
-          uint64_t sb;
-          std::memcpy(&sb, &sd, 8);
-          h->host_k2sum[sum_index(i, kS2Static, k2sum_stride(h->K))] = (uint32_t)sb;
-          h->host_k2sum[sum_index(i, kS2Static + 1, k2sum_stride(h->K))] = (uint32_t)(sb >> 32);
-        }
-      }
-    }
-    if (!h->generic && max_static >= (1ull << 51))
-      return fail(h, YODA_ERR_RANGE, "static score leaves the fast path; re-upload the nodes");
-    HIP_TRY(h, hipMemcpyAsync(h->nodes.p, h->host_records.data(), h->host_records.size(),
-                              hipMemcpyHostToDevice, h->stream));
-    if (h->has_k2sum)
-      HIP_TRY(h, hipMemcpyAsync(h->k2sum.p, h->host_k2sum.data(), h->host_k2sum.size() * 4,
-                                hipMemcpyHostToDevice, h->stream));
+    // Every node through the sparse node-state push: the records, the K2 summaries, their
+    // block-grouped copies (perm_on) and the host copies (h_alloc, host_records) all change
+    // together -- k_set_static is the one writer of a node's static score.
+    const uint32_t N = h->n_nodes;
+    std::vector<uint32_t> ids(N);
+    for (uint32_t i = 0; i < N; ++i) ids[i] = h->node_offset + i;
+    const std::vector<uint64_t> cn(h->h_card_number);
+    int rc = yoda_set_node_state(h, N, ids.data(), alloc, cn.data());
+    if (rc) return rc;
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     return YODA_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(h, YODA_ERR_INVALID_ARG, "host allocation failed");
   } catch (...) {
     return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
   }
@@ -1992,8 +1989,8 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     };
     // ranges of >= YODA_UPLOAD_MIN_RANGE (default 4096) pods over the process's worker pool
     // (HostPool); A/B knob for the greedy windows' 6144-pod uploads
-    static const uint32_t thr_cap = env_u32("YODA_UPLOAD_THREADS", 16);
-    static const uint32_t min_range = std::max<uint32_t>(256, env_u32("YODA_UPLOAD_MIN_RANGE", 4096));
+    static const uint32_t thr_cap = YODA_KNOB("YODA_UPLOAD_THREADS", 16);
+    static const uint32_t min_range = std::max<uint32_t>(256, YODA_KNOB("YODA_UPLOAD_MIN_RANGE", 4096));
     const uint32_t n_thr = std::min<uint32_t>({HostPool::get().size(), std::max(1u, thr_cap),
                                                std::max(1u, P / min_range)});
     std::vector<GroupTable> tables(n_thr);
@@ -2135,7 +2132,7 @@ static int prepare_run(yoda_t* h, int mode, bool pad = false) {
   // a private run takes the counting sort, padded when that adds at most 1/8 of the batch
   // (many small groups would otherwise multiply the work)
   h->count_order = pad && ordering && h->og_ok;
-  const bool padded = h->count_order && env_u32("YODA_ORDER_PAD", 1) &&
+  const bool padded = h->count_order && h->order_pad && YODA_KNOB("YODA_ORDER_PAD", 1) &&
                       (uint64_t)h->n_pad * 8 <= (uint64_t)h->n_pods * 9;
   h->n_work = padded ? h->n_pad : h->n_pods;
   plan_chunks(h, mode, h->n_work, h->n_nodes);
@@ -2168,6 +2165,9 @@ int yoda_run(yoda_t* h, int mode, uint32_t flags) {
 int yoda_download(yoda_t* h, yoda_eval_out* out) {
   if (!h || !out) return YODA_ERR_INVALID_ARG;
   if (!h->ran) return fail(h, YODA_ERR_STATE, "yoda_download before yoda_run/finalize");
+  if (h->k3_pending)  // picks of the flagged pods unresolved, outputs still in sorted order
+    return fail(h, YODA_ERR_STATE,
+                "exact normalize pending: run yoda_shard_exact_records / yoda_shard_exact_merge");
   try {
     HIP_TRY(h, hipSetDevice(h->device));
     const uint32_t P = h->n_pods;
@@ -2449,7 +2449,9 @@ int yoda_node_order(const yoda_t* h, uint32_t* grouped) {
 
 int yoda_set_pod_order(yoda_t* h, int enable) {
   if (!h) return YODA_ERR_INVALID_ARG;
+  if (enable < 0 || enable > 2) return fail(h, YODA_ERR_INVALID_ARG, "enable must be 0, 1 or 2");
   h->order_enabled = enable != 0;
+  h->order_pad = enable == 1;
   return YODA_OK;
 }
 
@@ -2458,12 +2460,12 @@ int yoda_class_stats_enable(yoda_t* h, int enable) {
   HIP_TRY(h, hipSetDevice(h->device));
   if (enable && !h->class_stats) {
     // YODA_K2_TRACE=<(wave, chunk) slots>: K2 also records per-(wave, chunk) timings
-    const uint32_t tr = env_u32("YODA_K2_TRACE", 0);
+    const uint32_t tr = diag_env("YODA_K2_TRACE", 0);
     const size_t bytes = (16 + 4 * (size_t)tr) * 8;
     HIP_TRY(h, h->stats_dev.ensure(bytes));
     HIP_TRY(h, hipMemsetAsync(h->stats_dev.p, 0, bytes, h->stream));
     if (tr) {  // YODA_K1_TRACE set: the K1 records it instead of the K2
-      const uint64_t one = env_u32("YODA_K1_TRACE", 0) ? 2 : 1;
+      const uint64_t one = diag_env("YODA_K1_TRACE", 0) ? 2 : 1;
       HIP_TRY(h, hipMemcpyAsync(h->stats_dev.as<uint64_t>() + 15, &one, 8,
                                 hipMemcpyHostToDevice, h->stream));
       HIP_TRY(h, hipStreamSynchronize(h->stream));
@@ -2669,9 +2671,8 @@ constexpr uint32_t kGreedyWindow = 6144;
 // A/B knob: YODA_GREEDY_WINDOW overrides the window size (pods per GPU window).
 uint32_t greedy_window() {
   static const uint32_t w = [] {
-    const char* s = std::getenv("YODA_GREEDY_WINDOW");
-    const unsigned long v = (s && *s) ? std::strtoul(s, nullptr, 10) : 0;
-    return v >= 64 && v <= (1u << 20) ? (uint32_t)v : kGreedyWindow;
+    const uint32_t v = YODA_KNOB("YODA_GREEDY_WINDOW", 0);
+    return v >= 64 && v <= (1u << 20) ? v : kGreedyWindow;
   }();
   return w;
 }
@@ -2833,7 +2834,7 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
       // window only the Allocate term of picked nodes changes, and it never increases
       // (unless alloc wraps around 2^64: then the rest of the window is evaluated exactly).
       // YODA_GREEDY_TOPK=16 (A/B knob): the capacity mode's deeper lists for this mode too
-      static const uint32_t kt_env = env_u32("YODA_GREEDY_TOPK", 0);
+      static const uint32_t kt_env = YODA_KNOB("YODA_GREEDY_TOPK", 0);
       const uint32_t KT = kt_env == (uint32_t)topk_k_capacity() ? kt_env : (uint32_t)topk_k();
       // Small windows: the GPU work is the same P x N in total, while fewer nodes are
       // touched per window, so fewer candidate lists lose certification.
@@ -2925,11 +2926,11 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
         // above yields its current score from then on; the threshold is the refresh-time
         // score (unlisted nodes scored at most that then and only dropped since).
         // YODA_GREEDY_REFRESH=0: off (A/B knob).
-        static const bool refresh_on = env_u32("YODA_GREEDY_REFRESH", 1) != 0;
+        static const bool refresh_on = YODA_KNOB("YODA_GREEDY_REFRESH", 1) != 0;
         // (YODA_GREEDY_REFRESH_EVERY / _MIN: A/B knobs for the check period and the bar)
         static const uint32_t kFbCheck =
-            std::max<uint32_t>(1, env_u32("YODA_GREEDY_REFRESH_EVERY", 8));
-        static const uint32_t kScanMin = env_u32("YODA_GREEDY_REFRESH_MIN", 16);
+            std::max<uint32_t>(1, YODA_KNOB("YODA_GREEDY_REFRESH_EVERY", 8));
+        static const uint32_t kScanMin = YODA_KNOB("YODA_GREEDY_REFRESH_MIN", 16);
         constexpr uint32_t kScan = 256;
         uint32_t fb_since = 0;
         auto maybe_refresh = [&](uint32_t i) -> int {
@@ -3862,7 +3863,7 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
   };
   // YODA_GREEDY_CAP_TOPK=8 (A/B knob): the shorter lists of the flags-0 mode
   static const uint32_t kt_cap =
-      env_u32("YODA_GREEDY_CAP_TOPK", 0) == (uint32_t)topk_k() ? (uint32_t)topk_k()
+      YODA_KNOB("YODA_GREEDY_CAP_TOPK", 0) == (uint32_t)topk_k() ? (uint32_t)topk_k()
                                                                : (uint32_t)topk_k_capacity();
   const uint32_t P = pods->n_pods, N = h->n_nodes, KT = kt_cap;
   yoda_node_soa nv{};
@@ -4007,11 +4008,11 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
     for (;;) {
       if ((rc = yoda_gs_resolve(g, &next))) return fail(h, rc, "greedy: resolve");
       // YODA_GREEDY_FAIL_DIV (A/B knob): one exact evaluation allowed per that many resolved pods
-      static const uint32_t rate = env_u32("YODA_GREEDY_FAIL_DIV", 0);
+      static const uint32_t rate = YODA_KNOB("YODA_GREEDY_FAIL_DIV", 0);
       // YODA_GREEDY_CAP_SCAN=<n> (A/B knob): fall back exactly (instead of restarting) when at
       // most YODA_GREEDY_CAP_SCAN_MAX of the next n window pods are uncertified already
-      static const uint32_t scan_n = env_u32("YODA_GREEDY_CAP_SCAN", 0);
-      static const uint32_t scan_max = env_u32("YODA_GREEDY_CAP_SCAN_MAX", 1);
+      static const uint32_t scan_n = YODA_KNOB("YODA_GREEDY_CAP_SCAN", 0);
+      static const uint32_t scan_max = YODA_KNOB("YODA_GREEDY_CAP_SCAN_MAX", 1);
       if (next >= wn) break;
       bool fallback = false;
       if (rate) {
@@ -4066,7 +4067,7 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
       // profiles/r03/greedy_capacity/grow_ab.txt (1.81-1.91 s with the earlier power of two >=
       // twice the progress, 1.57-1.64 s at 130 %).  YODA_GREEDY_GROW_PCT: A/B knob (0: that
       // power of two)
-      static const uint32_t grow = env_u32("YODA_GREEDY_GROW_PCT", 130);
+      static const uint32_t grow = YODA_KNOB("YODA_GREEDY_GROW_PCT", 130);
       uint32_t w2 = 64;
       if (grow) {
         const uint64_t t = (uint64_t)next * grow / 100;

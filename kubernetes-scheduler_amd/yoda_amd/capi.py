@@ -329,10 +329,12 @@ class Yoda:
         self._check(lib().yoda_node_order(self._h, C.byref(g)), "yoda_node_order")
         return bool(g.value)
 
-    def set_pod_order(self, enable: bool = True):
-        """Sort Mode-A batches on the device before K1/K2 (default on); results are returned
-        in the caller's pod order either way."""
-        self._check(lib().yoda_set_pod_order(self._h, 1 if enable else 0), "yoda_set_pod_order")
+    def set_pod_order(self, enable: bool = True, pad: bool = True):
+        """Sort Mode-A batches on the device before K1/K2 (default on; pad=False: without
+        padding the groups of a private run to wave boundaries); results are returned in the
+        caller's pod order either way."""
+        v = (1 if pad else 2) if enable else 0
+        self._check(lib().yoda_set_pod_order(self._h, v), "yoda_set_pod_order")
 
     def class_stats(self, enable: bool | None = None):
         """Block-kernel work classes (yoda_class_stats_*).  enable=True/False switches the

@@ -47,6 +47,10 @@ def lib():
         L.oracle_greedy.argtypes = [C.POINTER(CNodeSoA), C.POINTER(CPodSoA), C.c_int, C.c_uint32,
                                     C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         L.oracle_queue_order.argtypes = [C.POINTER(CPodSoA), C.POINTER(C.c_uint32)]
+        L.oracle_greedy_mt.argtypes = [C.POINTER(CNodeSoA), C.POINTER(CPodSoA), C.c_uint32,
+                                       C.c_uint32, C.c_uint32, C.c_int, C.POINTER(C.c_int32),
+                                       C.POINTER(C.c_int32), C.POINTER(C.c_int64),
+                                       C.POINTER(C.c_uint32)]
         _lib = L
     return _lib
 
@@ -101,6 +105,29 @@ def greedy(nodes: NodeSoA, pods: PodSoA, mode: int = 0, flags: int = 0):
     if rc != 0:
         raise RuntimeError(f"oracle_greedy rc={rc}")
     return pick, status
+
+
+def greedy_mt(nodes: NodeSoA, pods: PodSoA, flags: int = 0, q0: int = 0, q1: int | None = None,
+              threads: int = 8):
+    """Mode-A greedy with node-parallel cycles (oracle_greedy_mt): queue positions [q0, q1)
+    from the node state given.  Returns (pick, status, top_score, n_ties) over all pods
+    (pods outside the range keep pick -3)."""
+    nodes, pods = nodes.normalized(), pods.normalized()
+    P = pods.n_pods
+    q1 = P if q1 is None else q1
+    pick = np.full(P, -3, np.int32)
+    status = np.full(P, -1, np.int32)
+    top = np.zeros(P, np.int64)
+    ties = np.zeros(P, np.uint32)
+    cn, cp = nodes.c(), pods.c()
+    rc = lib().oracle_greedy_mt(C.byref(cn), C.byref(cp), flags, q0, q1, threads,
+                                pick.ctypes.data_as(C.POINTER(C.c_int32)),
+                                status.ctypes.data_as(C.POINTER(C.c_int32)),
+                                top.ctypes.data_as(C.POINTER(C.c_int64)),
+                                ties.ctypes.data_as(C.POINTER(C.c_uint32)))
+    if rc != 0:
+        raise RuntimeError(f"oracle_greedy_mt rc={rc}")
+    return pick, status, top, ties
 
 
 def queue_order(pods: PodSoA) -> np.ndarray:

@@ -535,4 +535,204 @@ int oracle_greedy(const yoda_node_soa* nd_in, const yoda_pod_soa* pd, int mode, 
   return YODA_OK;
 }
 
+/* ---- node-parallel cycle (full-size fixtures) -----------------------------------------
+ * schedule_one with its node loops split over OpenMP threads, for the full-size greedy
+ * fixtures (config 5: 1M sequential cycles over 100k nodes).  Same functions, same order of
+ * decisions: Filter per node (collection.go:41-44), the maxima over the feasible nodes'
+ * cards (collection.go:46; MAX is order-free), the raw score per feasible node
+ * (algorithm.go:96, scheduler.go:154), NormalizeScore's highest (init 0) and lowest (a
+ * member of the list, so a plain MIN) (scheduler.go:162-175), the per-node normalized score
+ * and range check (:178), and selectHost's maximum with the lowest node index and the tie
+ * count.  Every reduction is MAX / MIN / SUM / lowest-index, so the result does not depend
+ * on the thread count or schedule.  Scratch: raw[N] int64, ok[N] uint8. */
+
+/* CalculateBasicScore's card loop (algorithm.go:270-276) for a node already known feasible */
+static uint64_t basic_score_fit(const max_value* v, uint64_t memory, uint64_t clock,
+                                const yoda_node_soa* nd, uint32_t n) {
+  uint64_t s = 0;
+  for (uint32_t j = 0; j < nd->card_count[n]; ++j) {
+    card_t c = get_card(nd, n, j);
+    if (c.free_memory >= memory && c.clock >= clock) s += card_score(v, &c);
+  }
+  return s;
+}
+
+static void schedule_one_par(const yoda_node_soa* nd, const yoda_pod_soa* pd, uint32_t p,
+                             int n_threads, int64_t* raw, uint8_t* ok, cycle_result* r) {
+  const int64_t N = nd->n_nodes;
+  memset(r, 0, sizeof(*r));
+  max_value mv = {1, 1, 1, 1, 1, 1};
+  uint32_t nf = 0;
+  int64_t first = -1;
+  /* Filter + CollectMaxValues: one pass (the predicate is a pure function of the pair) */
+#pragma omp parallel num_threads(n_threads)
+  {
+    max_value lv = {1, 1, 1, 1, 1, 1};
+    uint32_t lnf = 0;
+    int64_t lfirst = -1;
+#pragma omp for schedule(static)
+    for (int64_t n = 0; n < N; ++n) {
+      uint64_t m, c;
+      ok[n] = (uint8_t)pod_fits_node(pd, p, nd, (uint32_t)n, &m, &c);
+      if (!ok[n]) continue;
+      if (lfirst < 0) lfirst = n;
+      lnf++;
+      for (uint32_t j = 0; j < nd->card_count[n]; ++j) {
+        card_t cd = get_card(nd, (uint32_t)n, j);
+        if (cd.free_memory >= m && cd.clock >= c) process_max_value_with_card(&cd, &lv);
+      }
+    }
+#pragma omp critical
+    {
+      nf += lnf;
+      if (lfirst >= 0 && (first < 0 || lfirst < first)) first = lfirst;
+      if (lv.bandwidth > mv.bandwidth) mv.bandwidth = lv.bandwidth;
+      if (lv.clock > mv.clock) mv.clock = lv.clock;
+      if (lv.core > mv.core) mv.core = lv.core;
+      if (lv.free_memory > mv.free_memory) mv.free_memory = lv.free_memory;
+      if (lv.power > mv.power) mv.power = lv.power;
+      if (lv.total_memory > mv.total_memory) mv.total_memory = lv.total_memory;
+    }
+  }
+  r->n_feasible = nf;
+  r->maxima = mv;
+  if (nf == 0) {
+    r->pick = YODA_PICK_NONE;
+    r->status = YODA_STATUS_UNSCHEDULABLE;
+    return;
+  }
+  /* Score per feasible node (algorithm.go:96, left to right; Uint64ToInt64).  The card
+   * predicate's thresholds are what pod_fits_node reports for any feasible node: the pod's
+   * scv/memory and scv/clock, 0 when the label is absent (filter.go:18-50). */
+  const uint64_t m_thr = pd->has_memory[p] ? pd->memory[p] : 0;
+  const uint64_t c_thr = pd->has_clock[p] ? pd->clock[p] : 0;
+  int div_zero = 0;
+  int64_t highest = 0, lowest = INT64_MAX;
+#pragma omp parallel num_threads(n_threads)
+  {
+    int ldz = 0;
+    int64_t lhi = 0, llo = INT64_MAX;
+#pragma omp for schedule(static)
+    for (int64_t n = 0; n < N; ++n) {
+      if (!ok[n]) continue;
+      uint64_t s = basic_score_fit(&mv, m_thr, c_thr, nd, (uint32_t)n);
+      s += allocate_score(nd, (uint32_t)n, &ldz);
+      s += actual_score(nd, (uint32_t)n, &ldz);
+      raw[n] = uint64_to_int64(s);
+      if (raw[n] > lhi) lhi = raw[n];
+      if (raw[n] < llo) llo = raw[n];
+    }
+#pragma omp critical
+    {
+      div_zero |= ldz;
+      if (lhi > highest) highest = lhi;
+      if (llo < lowest) lowest = llo;
+    }
+  }
+  if (nf == 1) {
+    r->pick = (int32_t)first;
+    r->status = YODA_STATUS_OK;
+    r->n_ties = 1;
+    r->top_score = raw[first];
+    return;
+  }
+  if (div_zero) {
+    r->pick = YODA_PICK_ERROR;
+    r->status = YODA_STATUS_DIV_ZERO;
+    return;
+  }
+  if (highest == lowest) lowest--;
+  int range_err = 0;
+  int64_t best = -1, bi = -1;
+  uint32_t ties = 0;
+#pragma omp parallel num_threads(n_threads)
+  {
+    int lerr = 0;
+    int64_t lbest = -1, lbi = -1;
+    uint32_t lties = 0;
+#pragma omp for schedule(static)
+    for (int64_t n = 0; n < N; ++n) {
+      if (!ok[n]) continue;
+      uint64_t prod = (uint64_t)(raw[n] - lowest) * 100u;
+      int64_t norm = (int64_t)prod / (highest - lowest);
+      if (norm > 100 || norm < 0) lerr = 1;
+      if (norm > lbest) {
+        lbest = norm;
+        lbi = n;
+        lties = 1;
+      } else if (norm == lbest) {
+        lties++;
+      }
+    }
+#pragma omp critical
+    {
+      range_err |= lerr;
+      if (lbest > best) {
+        best = lbest;
+        bi = lbi;
+        ties = lties;
+      } else if (lbest == best && lbest >= 0) {
+        if (lbi < bi) bi = lbi;
+        ties += lties;
+      }
+    }
+  }
+  if (range_err) {
+    r->pick = YODA_PICK_ERROR;
+    r->status = YODA_STATUS_SCORE_RANGE;
+    return;
+  }
+  r->pick = (int32_t)bi;
+  r->status = YODA_STATUS_OK;
+  r->n_ties = ties;
+  r->top_score = raw[bi];
+}
+
+/* oracle_greedy with node-parallel cycles, for the full-size fixtures.  Pods in queue order
+ * [q0, q1) only (q0 = 0, q1 = P: the whole batch), starting from the node state given (its
+ * alloc_memory and card_number: a replayed state for a later block).  top_score / n_ties
+ * optional. */
+int oracle_greedy_mt(const yoda_node_soa* nd_in, const yoda_pod_soa* pd, uint32_t flags,
+                     uint32_t q0, uint32_t q1, int n_threads, int32_t* pick, int32_t* status,
+                     int64_t* top_score, uint32_t* n_ties) {
+  if (!nd_in || !pd || !pick || q0 > q1 || q1 > pd->n_pods) return YODA_ERR_INVALID_ARG;
+  if (n_threads < 1) n_threads = 1;
+  uint32_t N = nd_in->n_nodes, P = pd->n_pods;
+  yoda_node_soa nd = *nd_in;
+  uint64_t* alloc = (uint64_t*)calloc((size_t)N + 1, sizeof(uint64_t));
+  uint64_t* cardn = (uint64_t*)malloc(sizeof(uint64_t) * ((size_t)N + 1));
+  int64_t* raw = (int64_t*)malloc(sizeof(int64_t) * ((size_t)N + 1));
+  uint8_t* ok = (uint8_t*)malloc((size_t)N + 1);
+  uint32_t* order = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)P + 1));
+  if (!alloc || !cardn || !raw || !ok || !order) {
+    free(alloc); free(cardn); free(raw); free(ok); free(order);
+    return YODA_ERR_INVALID_ARG;
+  }
+  for (uint32_t n = 0; n < N; ++n) {
+    alloc[n] = nd_in->alloc_memory ? nd_in->alloc_memory[n] : 0;
+    cardn[n] = nd_in->card_number[n];
+  }
+  nd.alloc_memory = alloc;
+  nd.card_number = cardn;
+  oracle_queue_order(pd, order);
+  for (uint32_t i = q0; i < q1; ++i) {
+    uint32_t p = order[i];
+    cycle_result r;
+    schedule_one_par(&nd, pd, p, n_threads, raw, ok, &r);
+    pick[p] = r.pick;
+    if (status) status[p] = r.status;
+    if (top_score) top_score[p] = r.top_score;
+    if (n_ties) n_ties[p] = r.n_ties;
+    if (r.pick >= 0) { /* the assume of oracle_greedy */
+      if (pd->has_memory[p]) alloc[r.pick] += pd->memory[p];
+      if (flags & YODA_GREEDY_CARD_CAPACITY) {
+        uint64_t num = pd->has_number[p] ? pd->number[p] : 1;
+        cardn[r.pick] = cardn[r.pick] >= num ? cardn[r.pick] - num : 0;
+      }
+    }
+  }
+  free(alloc); free(cardn); free(raw); free(ok); free(order);
+  return YODA_OK;
+}
+
 int oracle_abi_version(void) { return YODA_ABI_VERSION; }

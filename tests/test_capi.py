@@ -51,3 +51,23 @@ def test_struct_layouts_match_header():
         body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), text, re.S).group(1)
         fields = re.findall(r"^\s*(?:const\s+)?[a-z0-9_]+\*?\s*\*?\s*([a-z_0-9]+);", body, re.M)
         assert fields == [f for f, _ in pystruct._fields_], cname
+
+
+# Policy knobs of the A/B harness: read from the environment only by libyoda_ab.so
+# (`make -C kubernetes-scheduler_amd/csrc ab`, -DYODA_AB_KNOBS).  The release library must
+# ignore them -- a scheduler inherits its environment -- so their names are not even in it.
+AB_KNOBS = ("YODA_NODE_PERM", "YODA_ORDER_PAD", "YODA_NO_GTAB", "YODA_CHUNK_ROUNDS",
+            "YODA_MIN_CHUNK_NODES", "YODA_K1_MAX_CHUNKS", "YODA_BLOCK_WITNESS",
+            "YODA_TOPK_PER_PAIR", "YODA_TOPK_ROUNDS", "YODA_UPLOAD_THREADS",
+            "YODA_GREEDY_WINDOW", "YODA_GREEDY_TOPK", "YODA_GREEDY_REFRESH",
+            "YODA_GREEDY_GROW_PCT", "YODA_GREEDY_CAP_TOPK", "YODA_GREEDY_CAP_SCAN",
+            "YODA_GREEDY_FAIL_DIV")
+
+
+def test_release_library_ignores_ab_knobs():
+    data = open(capi.LIB_PATH if "libyoda_ab" not in capi.LIB_PATH else
+                capi.LIB_PATH.replace("libyoda_ab", "libyoda"), "rb").read()
+    found = [k for k in AB_KNOBS if k.encode() in data]
+    assert not found, f"release libyoda.so reads tuning knobs from the environment: {found}"
+    # the diagnostics may (traces and counters, never results or policy)
+    assert b"YODA_K2_TRACE" in data

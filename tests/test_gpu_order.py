@@ -75,18 +75,16 @@ def test_too_many_groups_radix(dev):
     assert_same(got, oracle.schedule(nodes, pods, MODE_SCV, threads=8))
 
 
-@pytest.mark.parametrize("env", [{"YODA_ORDER_PAD": "0"}, {}])
-def test_order_modes_agree(dev, env, monkeypatch):
+@pytest.mark.parametrize("pad", [False, True])
+def test_order_modes_agree(dev, pad):
     """Padded and unpadded counting order, and no order: identical outputs."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     nodes, pods = synth.make_config(2, pods=20000, nodes=1500)
     dev.upload_nodes(nodes)
-    dev.set_pod_order(True)
+    dev.set_pod_order(True, pad=pad)
     a = dev.eval(pods, MODE_SCV)
     info = dev.order_info()
     assert info["kind"] == 2
-    assert (info["work"] > pods.n_pods) == ("YODA_ORDER_PAD" not in env)
+    assert (info["work"] > pods.n_pods) == pad
     dev.set_pod_order(False)
     b = dev.eval(pods, MODE_SCV)
     dev.set_pod_order(True)
