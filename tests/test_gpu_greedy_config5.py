@@ -1,9 +1,12 @@
 """Config 5 at its full size (BASELINE.json: 1M pods x 100k nodes greedy), both greedy modes.
 
-The sequential oracle cannot run 1M x 100k in test time, so the check is three-fold:
-  1. exact picks against oracle_greedy (sort.go:8-10 order, algorithm.go:299-303 assume,
-     plus the CardNumber decrement with YODA_GREEDY_CARD_CAPACITY) on a queue-order prefix of
-     2,000 pods -- a prefix in queue order is an exact sub-problem;
+  0. EVERY pick against the sequential C oracle (sort.go:8-10 order, algorithm.go:299-303
+     assume, plus the CardNumber decrement with YODA_GREEDY_CARD_CAPACITY): the oracle's 1M
+     cycles run in the build container (tests/golden/make_fullsize.py, ~35 min per flag on 8
+     cores); tests/golden/fullsize.json holds one digest per 6,144-pod queue window, which the
+     GPU's picks must reproduce window by window;
+  1. exact picks against oracle_greedy run here on a queue-order prefix of 2,000 pods -- a
+     prefix in queue order is an exact sub-problem;
   2. replay at sampled queue positions across the whole batch: the node state just before
      position q is rebuilt from the earlier picks (allocated memory += scv/memory, CardNumber
      -= the pod's number), uploaded to a second handle, and that pod alone is scheduled on it
@@ -63,6 +66,14 @@ def test_config5_full_size(cfg5, flags):
     if flags == 0:
         # the mid-window list refresh ran (the replays below sample the windows it served)
         assert y.greedy_refreshes() > 0
+
+    # 0. every pick, window by window, against the oracle's digests
+    import fullsize_check as fc
+    fx = fc.load(f"config5_{flags}")
+    fc.check_inputs(fx, nodes, pods)
+    bad = fc.greedy_mismatch(fx, pick, nodes, pods, order, oracle)
+    assert bad is None, bad
+    assert int((pick >= 0).sum()) == fx["placed"]
 
     # 1. exact prefix against the sequential oracle
     pre = order[:2000]

@@ -119,3 +119,20 @@ def test_greedy_then_private_run(dev):
                                       oracle.greedy(nodes, pods, MODE_SCV, flags)[0])
     sub = pods.slice(0, 800)
     assert_same(dev.eval(sub, MODE_SCV), oracle.schedule(nodes, sub, MODE_SCV, threads=8))
+
+
+def test_update_alloc_reaches_the_grouped_copies(dev):
+    """yoda_update_alloc (every node's allocated memory) then a private run over the grouped
+    copies: the same as a fresh upload with that allocated memory (the copies used
+    to keep the old static scores), and a later greedy starts from the new state."""
+    nodes, pods = synth.make_config(2, pods=700, nodes=5000)
+    dev.upload_nodes(nodes)
+    assert dev.node_order_grouped
+    rng = np.random.default_rng(9)
+    alloc = (nodes.alloc_memory + rng.integers(0, 300000, nodes.n_nodes)).astype(np.uint64)
+    dev.update_alloc(alloc)
+    mod = nodes.slice(0, nodes.n_nodes)
+    mod.alloc_memory = alloc
+    assert_same(dev.eval(pods, MODE_SCV), oracle.schedule(mod, pods, MODE_SCV, threads=8))
+    np.testing.assert_array_equal(dev.greedy(pods, MODE_SCV, 0),
+                                  oracle.greedy(mod, pods, MODE_SCV, 0)[0])
