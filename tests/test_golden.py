@@ -57,3 +57,26 @@ def test_gpu_reproduces_golden(path):
             y.upload_nodes(nodes, force_f64=rec == "f64", force_generic=rec == "u64")
             for mode in (0, 1):
                 check(y.eval(pods, mode), z, mode)
+
+
+def test_fullsize_fixture_pins_the_oracle():
+    """tests/golden/fullsize.json (the every-pod digests the GPU suite checks at full size):
+    the generator still makes the inputs it was computed on, and the C oracle reproduces its
+    first and last config-3 blocks here (2 x 1,024 pods x 100k nodes)."""
+    import fullsize_check as fc
+    from yoda_amd import synth
+    fx = fc.load("config3")
+    nodes, pods = synth.make_config(3)
+    fc.check_inputs(fx, nodes, pods)
+    B, nb = fx["block"], len(fx["digests"])
+    for b in (0, nb - 1):
+        sel = np.arange(b * B, min(pods.n_pods, (b + 1) * B))
+        res = oracle.schedule(nodes, pods.take(sel), 0, threads=8)
+        assert fc.mf.config3_digests(res, B)[0] == fx["digests"][b], b
+    for key in ("config5_0", "config5_1"):
+        try:
+            g = fc.load(key)
+        except KeyError:
+            continue
+        fc.check_inputs(g, *synth.make_config(5))
+        assert len(g["digests"]) == -(-g["pods"] // g["window"])
