@@ -2478,7 +2478,7 @@ int yoda_class_stats_enable(yoda_t* h, int enable) {
 
 int yoda_class_stats_read(yoda_t* h, uint64_t* out) {
   if (!h || !out) return YODA_ERR_INVALID_ARG;
-  for (int i = 0; i < 13; ++i) out[i] = 0;
+  for (int i = 0; i < 16; ++i) out[i] = 0;
   if (!h->stats_dev.p) return YODA_OK;
   HIP_TRY(h, hipSetDevice(h->device));
   uint64_t d[16] = {};
@@ -2497,6 +2497,9 @@ int yoda_class_stats_read(yoda_t* h, uint64_t* out) {
   out[10] = d[7];                                                  // K2 FAST via node records
   out[11] = d[8];                                                  // K2 per-pod, non-uniform
   out[12] = d[9];                                                  // max per-pod nodes/(w, c)
+  out[13] = d[10];                                                 // K1 (w, block)s all NONE
+  out[14] = d[11];                                                 // K1 (w, block)s all ALL
+  out[15] = d[12];                                                 // K1 (w, block)s
   HIP_TRY(h, hipMemsetAsync(h->stats_dev.p, 0, 15 * 8, h->stream));
   h->stats_pairs1 = h->stats_pairs2 = 0;
   return YODA_OK;

@@ -851,9 +851,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     const bool is_all = valid && !feas_none && feas_all && same;
     const uint64_t all_b = ballot(is_all), none_b = ballot(is_none);
     uint64_t part_b = ballot(valid) & ~all_b & ~none_b;
-    if (STATS && !trace && lane == 0) {  // class counts of (wave, node) pairs: ALL, NONE
-      atomicAdd(stats + 0, (unsigned long long)__builtin_popcountll(all_b));
-      atomicAdd(stats + 1, (unsigned long long)__builtin_popcountll(none_b));
+    if (STATS && !trace) {  // class counts of (wave, node) pairs: ALL, NONE; whole blocks
+      const uint64_t vb = ballot(valid);
+      if (lane == 0) {
+        atomicAdd(stats + 0, (unsigned long long)__builtin_popcountll(all_b));
+        atomicAdd(stats + 1, (unsigned long long)__builtin_popcountll(none_b));
+        atomicAdd(stats + 10, none_b == vb ? 1ull : 0ull);
+        atomicAdd(stats + 11, all_b == vb ? 1ull : 0ull);
+        atomicAdd(stats + 12, 1ull);
+      }
     }
     nf_all += (uint32_t)__builtin_popcountll(all_b);
     nz_all += (uint32_t)__builtin_popcountll(ballot(is_all && (meta & kSumZeroTotal)));

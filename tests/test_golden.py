@@ -74,9 +74,9 @@ def test_fullsize_fixture_pins_the_oracle():
         res = oracle.schedule(nodes, pods.take(sel), 0, threads=8)
         assert fc.mf.config3_digests(res, B)[0] == fx["digests"][b], b
     for key in ("config5_0", "config5_1"):
-        try:
-            g = fc.load(key)
-        except KeyError:
+        import json
+        if key not in json.load(open(fc.FIXTURE)):
             continue
+        g = fc.load(key)
         fc.check_inputs(g, *synth.make_config(5))
         assert len(g["digests"]) == -(-g["pods"] // g["window"])

@@ -69,7 +69,8 @@ def test_config5_full_size(cfg5, flags):
 
     # 0. every pick, window by window, against the oracle's digests
     import fullsize_check as fc
-    fx = fc.load(f"config5_{flags}")
+    fx = fc.load_optional(f"config5_{flags}")
+    assert fx is not None, f"config5_{flags} digests missing: tests/golden/make_fullsize.py"
     fc.check_inputs(fx, nodes, pods)
     bad = fc.greedy_mismatch(fx, pick, nodes, pods, order, oracle)
     assert bad is None, bad
