@@ -120,6 +120,8 @@ hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32
                              const uint64_t* value, const uint64_t* card_number, uint32_t count,
                              unsigned char* sum, uint32_t sum_stride, unsigned char* sum2,
                              uint32_t sum2_stride, const PermCopy& pc, hipStream_t s);
+hipError_t launch_bsum_cn(const unsigned char* sum, uint32_t sum_stride, uint32_t n_nodes,
+                          uint32_t* bsum, uint32_t bsw, hipStream_t s);
 hipError_t launch_gtable(int K, const uint32_t* sum2, const uint32_t* mix, uint32_t n_nodes,
                          const uint64_t* g_max,
                          uint32_t* tab, uint32_t* rcp_out, MemTab mt, hipStream_t s);
@@ -329,13 +331,22 @@ struct yoda_handle {
   // node's position (k_set_static keeps the copies current)
   bool perm_on = false;
   DevBuf k1sum_p, k2sum_p, gtab_p, perm_ids, perm_inv;
+  // 64-node block summaries (yoda_layout.h BlockSumWord) of the snapshot order and of the
+  // block-grouped copy's; loose: node-state pushes left their CardNumber bounds valid but not
+  // tight (k_set_static's atomics), recomputed before the next private run
+  DevBuf blksum, blksum_p;
+  bool blksum_loose = false;
+  bool greedy_active = false;  // inside a greedy batch (its pushes keep the bounds valid)
   PermCopy perm_copy() const {
     PermCopy pc;
     if (perm_on) {
       pc.inv = perm_inv.as<uint32_t>();
       pc.sum = k1sum_p.as<unsigned char>();
       pc.sum2 = k2sum_p.as<unsigned char>();
+      pc.bsum_p = blksum_p.p ? blksum_p.as<uint32_t>() : nullptr;
     }
+    pc.bsum = blksum.p && path == Path::N32 ? blksum.as<uint32_t>() : nullptr;
+    pc.bsum_words = bsum_stride(K) / 4u;
     return pc;
   }
   bool perm_run() const { return perm_on && count_order; }  // this run is block-grouped
@@ -458,7 +469,7 @@ struct yoda_handle {
   ~yoda_handle() {
     if (comm && rccl().ok) (void)rccl().comm_destroy(comm);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &k1sum_p,   &k2sum_p,   &gtab_p,    &perm_ids,  &perm_inv,    &pod_blob,   &maxima,       &counts,
+    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &k1sum_p,   &k2sum_p,   &gtab_p, &blksum, &blksum_p,    &perm_ids,  &perm_inv,    &pod_blob,   &maxima,       &counts,
                      &pod_sorted, &perm,     &order_scratch, &order_meta, &order_hist,
                      &order_bstart, &order_slot, &order_bkt,
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
@@ -734,9 +745,11 @@ PodParams pod_params(yoda_t* h) {
   pp.x1 = h->path == Path::N32 ? h->kx1.as<uint32_t>() : nullptr;
   pp.one_model = h->path == Path::N32 && h->all_one_model;
   pp.all_uni4 = h->path == Path::N32 && h->all_uni4;
+  if (h->path == Path::N32 && h->has_k1sum && h->blksum.p) pp.bsum = h->blksum.as<uint32_t>();
   if (h->perm_run()) {
     pp.ids = h->perm_ids.as<uint32_t>();
     if (pp.g.tab) pp.g.tab = h->gtab_p.as<uint32_t>();
+    pp.bsum = h->blksum_p.p ? h->blksum_p.as<uint32_t>() : nullptr;
   }
   pp.mt = h->mem_ranks ? h->mt : MemTab{};
   return pp;
@@ -978,6 +991,29 @@ int ensure_diskio_classes(yoda_t* h) {
   return YODA_OK;
 }
 
+// Inside a greedy batch: its node-state pushes leave the block summaries' bounds valid (the
+// atomics of k_set_static), so its windows do not tighten them; the next private run does.
+struct GreedyScope {
+  yoda_t* h;
+  bool prev;
+  explicit GreedyScope(yoda_t* x) : h(x), prev(x->greedy_active) { h->greedy_active = true; }
+  ~GreedyScope() { h->greedy_active = prev; }
+};
+
+// The block summaries' CardNumber bounds, tight again after node-state pushes.
+hipError_t tighten_block_sums(yoda_t* h) {
+  hipError_t e = hipSuccess;
+  const uint32_t bsw = bsum_stride(h->K) / 4u;
+  if (h->path == Path::N32 && h->has_k1sum && h->blksum.p)
+    e = launch_bsum_cn(h->k1sum.as<unsigned char>(), k1sum_stride(h->K), h->n_nodes,
+                       h->blksum.as<uint32_t>(), bsw, h->stream);
+  if (e == hipSuccess && h->perm_on && h->blksum_p.p)
+    e = launch_bsum_cn(h->k1sum_p.as<unsigned char>(), k1sum_stride(h->K), h->n_nodes,
+                       h->blksum_p.as<uint32_t>(), bsw, h->stream);
+  if (e == hipSuccess) h->blksum_loose = false;
+  return e;
+}
+
 // Phase 1: Filter + PreScore maxima (Mode A), or the all-feasible state (Mode B).
 // final_maxima: this handle's maxima are the run's (no exchange follows).
 int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_maxima = false) {
@@ -1007,6 +1043,7 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_m
                               h->stream));
   h->blk_zeroed = false;
   const bool pr = h->perm_run();  // block-grouped node order (upload's node_perm)
+  if (h->blksum_loose && !h->greedy_active) HIP_TRY(h, tighten_block_sums(h));
   HIP_TRY(h, launch_k1(h->K, h->path, h->nodes.as<unsigned char>(),
                        h->has_k1sum ? (pr ? h->k1sum_p : h->k1sum).as<unsigned char>() : nullptr,
                        (pr ? h->k2sum_p : h->k2sum).as<unsigned char>(),
@@ -1466,6 +1503,8 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     const size_t mstride = mix_stride(K);
     std::vector<uint32_t> mix(want_sum ? (size_t)std::max<uint32_t>(N, 1) * mstride / 4 : 0, 0);
     uint32_t n_one_model = 0, n_uni4 = 0;
+    // per node: the clocks of its real cards and of its healthy cards, min / max (block sums)
+    std::vector<uint32_t> clk_rng(want_sum ? 4 * (size_t)N : 0);
     const size_t xstride = x1_stride(K);
     std::vector<uint32_t> x1m(want_sum ? (size_t)std::max<uint32_t>(N, 1) * xstride / 4 : 0, 0);
     for (uint32_t i = 0; i < N; ++i) {
@@ -1594,6 +1633,18 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
           }
         }
         x[kX1Chg] = chg;
+        uint32_t* cr = clk_rng.data() + 4 * (size_t)i;
+        cr[0] = cr[2] = 0xffffffffu;
+        cr[1] = cr[3] = 0u;
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const uint32_t ck = (uint32_t)nd->card_clock[a + j];
+          cr[0] = std::min(cr[0], ck);
+          cr[1] = std::max(cr[1], ck);
+          if (nd->card_healthy[a + j]) {
+            cr[2] = std::min(cr[2], ck);
+            cr[3] = std::max(cr[3], ck);
+          }
+        }
       }
       for (uint32_t j = 0; j < nd->card_count[i]; ++j) {
         const size_t k = (size_t)i * KS + j;
@@ -1705,6 +1756,97 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
         HIP_TRY(h, hipMemcpyAsync(h->perm_inv.p, inv.data(), (size_t)N * 4,
                                   hipMemcpyHostToDevice, h->stream));
         HIP_TRY(h, hipStreamSynchronize(h->stream));  // (the host copies go out of scope)
+      }
+      // block summaries of the snapshot order and of the block-grouped copy's (BlockSumWord)
+      {
+        const uint32_t SW = (uint32_t)(sstride / 4);
+        auto bsums = [&](const uint32_t* order) {
+          const uint32_t nb = (N + 63) / 64, BW = bsum_stride(K) / 4;
+          std::vector<uint32_t> b((size_t)std::max<uint32_t>(nb, 1) * BW, 0u);
+          for (uint32_t blk = 0; blk < nb; ++blk) {
+            uint32_t* o = b.data() + (size_t)blk * BW;
+            uint64_t cmin = ~0ull, cmax = 0;
+            uint32_t fl = kBsOneModel | kBsUni4, ckmin = ~0u, ckmax = 0, hmin = ~0u, hmax = 0;
+            uint32_t nhmin = ~0u, nhmax = 0, mrmin = ~0u, mrmax = 0, nreal = 0, nzt = 0;
+            uint32_t mx[6] = {0, 0, 0, 0, 0, 0}, wc[6] = {0, 0, 0, 0, 0, 0};
+            uint32_t wl[6] = {~0u, ~0u, ~0u, ~0u, ~0u, ~0u};
+            uint32_t tmin[YODA_MAX_CARDS], tmax[YODA_MAX_CARDS];
+            for (int t = 0; t < K; ++t) tmin[t] = ~0u, tmax[t] = 0;
+            for (uint32_t l = 0; l < 64 && blk * 64 + l < N; ++l) {
+              const uint32_t i = order ? order[blk * 64 + l] : blk * 64 + l;
+              const uint32_t* w = sum.data() + (size_t)i * SW;
+              const uint64_t cn = (uint64_t)w[kSumCnLo] | ((uint64_t)w[kSumCnHi] << 32);
+              const uint32_t meta = w[kSumMeta], nh = (meta >> 8) & 0xffu;
+              const uint32_t* cr = clk_rng.data() + 4 * (size_t)i;
+              ++nreal;
+              cmin = std::min(cmin, cn);
+              cmax = std::max(cmax, cn);
+              if (!(meta & kSumUni4)) fl &= ~(kBsUni4 | kBsOneModel);
+              if (!(meta & kSumUniTotal)) fl &= ~kBsOneModel;
+              if (meta & kSumZeroTotal) ++nzt;
+              ckmin = std::min(ckmin, cr[0]);
+              ckmax = std::max(ckmax, cr[1]);
+              hmin = std::min(hmin, cr[2]);
+              hmax = std::max(hmax, cr[3]);
+              nhmin = std::min(nhmin, nh);
+              nhmax = std::max(nhmax, nh);
+              mrmin = std::min(mrmin, w[kSumMrf1]);
+              mrmax = std::max(mrmax, w[kSumMrf1]);
+              const uint32_t mr = w[kSumMrf1];
+              const uint32_t v[6] = {w[kSumBw], w[kSumClock], w[kSumCore], mr - (mr != 0u ? 1u : 0u),
+                                     w[kSumPower], w[kSumTotal]};  // kMax* order
+              for (int f = 0; f < 6; ++f) {
+                if (wc[f] == 0 || v[f] > mx[f]) {
+                  mx[f] = v[f];
+                  wc[f] = 1;
+                  wl[f] = l;
+                } else if (v[f] == mx[f]) {
+                  ++wc[f];
+                }
+              }
+              for (int t = 0; t < K; ++t) {
+                tmin[t] = std::min(tmin[t], w[kSumHfs + t]);
+                tmax[t] = std::max(tmax[t], w[kSumHfs + t]);
+              }
+            }
+            if (nreal == 0) continue;
+            std::memcpy(o + kBsCnMin, &cmin, 8);
+            std::memcpy(o + kBsCnMax, &cmax, 8);
+            o[kBsFlags] = fl;
+            o[kBsCkMin] = ckmin;
+            o[kBsCkMax] = ckmax;
+            o[kBsHckMin] = hmin;
+            o[kBsHckMax] = hmax;
+            o[kBsNhMin] = nhmin;
+            o[kBsNhMax] = nhmax;
+            o[kBsMrfMin] = mrmin;
+            o[kBsMrfMax] = mrmax;
+            o[kBsNReal] = nreal;
+            o[kBsNzt] = nzt;
+            for (int f = 0; f < 6; ++f) {
+              o[kBsMx + f] = mx[f];
+              o[kBsWc + f] = wc[f];
+              o[kBsWl + f] = wl[f];
+            }
+            for (int t = 0; t < K; ++t) {
+              o[kBsT + t] = tmin[t];
+              o[kBsT + K + t] = tmax[t];
+            }
+          }
+          return b;
+        };
+        const std::vector<uint32_t> bo = bsums(nullptr);
+        HIP_TRY(h, h->blksum.ensure(bo.size() * 4));
+        HIP_TRY(h, hipMemcpyAsync(h->blksum.p, bo.data(), bo.size() * 4, hipMemcpyHostToDevice,
+                                  h->stream));
+        if (h->perm_on) {
+          const std::vector<uint32_t> bp = bsums(nperm.data());
+          HIP_TRY(h, h->blksum_p.ensure(bp.size() * 4));
+          HIP_TRY(h, hipMemcpyAsync(h->blksum_p.p, bp.data(), bp.size() * 4,
+                                    hipMemcpyHostToDevice, h->stream));
+        }
+        HIP_TRY(h, hipStreamSynchronize(h->stream));  // (the host copies go out of scope)
+        h->blksum_loose = false;
       }
       sum = tiles(sum, (uint32_t)sstride);
       sum2 = tiles(sum2, (uint32_t)s2stride);
@@ -2761,6 +2903,7 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
   if (!h->has_nodes) return fail(h, YODA_ERR_NO_NODES, "no node snapshot uploaded");
   try {
     HIP_TRY(h, hipSetDevice(h->device));
+    GreedyScope scope(h);
     const uint32_t P = pods->n_pods, N = h->n_nodes;
     h->greedy_windows = 0;
     h->greedy_fallbacks = 0;
@@ -3095,6 +3238,7 @@ int push_node_state(yoda_t* h, const std::vector<uint32_t>& loc, const std::vect
   h->upd_pending = true;
   unsigned char* d = h->upd_node.as<unsigned char>();
   const uint32_t stride = h->path == Path::N32 ? n32_stride(h->K) : node_stride(h->K);
+  h->blksum_loose = true;  // (the atomics keep the block bounds valid, not tight)
   HIP_TRY(h, launch_set_static(h->nodes.as<unsigned char>(), stride,
                                reinterpret_cast<const uint32_t*>(d),
                                reinterpret_cast<const uint64_t*>(d + o_val),

@@ -597,7 +597,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     uint32_t n_pods, uint64_t* __restrict__ pmax, uint32_t* __restrict__ pcnt,
     uint64_t* __restrict__ bm, uint32_t bm_stride, BlockMask* __restrict__ bs,
     uint32_t bs_stride, uint64_t* __restrict__ blk, uint32_t blk_stride,
-    unsigned long long* __restrict__ stats, uint32_t* __restrict__ pwit = nullptr) {
+    unsigned long long* __restrict__ stats, uint32_t* __restrict__ pwit = nullptr,
+    const uint32_t* __restrict__ bsm = nullptr) {
   static_assert(!(WIT && MIX), "the witness K1 serves one-model snapshots");
   constexpr uint32_t SS = k1sum_stride(K);
   constexpr uint32_t NS = n32_stride(K);
@@ -705,7 +706,82 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     pf_tn = s[64 * hfs_none];
   };
   if (YODA_K1_PF && n0 < n1) load_sum(n0);
+  // Whole-block decisions from the block summaries (BlockSumWord, scalar reads): the bounds
+  // of the block's nodes against the wave's bounds prove every node NONE, or every node ALL
+  // with one contribution (all qualifying: the block's maxima; none qualifying: nothing).
+  // Sufficient conditions of the per-node tests below, so the outcome is the same.
+  constexpr uint32_t BSW = bsum_stride(K) / 4u;
+  const uint32_t s_mpm_max = uniform_u32(mpm_max), s_mpm_min = uniform_u32(mpm_min);
+  const uint32_t s_m_max = uniform_u32(m_max), s_m_min = uniform_u32(m_min);
+  const uint32_t s_c_max = uniform_u32(c_max), s_c_min = uniform_u32(c_min);
+  const uint32_t bs_tn = kBsT + (uint32_t)K + (hfs_none_ok && nm_min > 0u ? nm_min - 1u : 0u);
+  const uint32_t bs_ta = kBsT + (any_pm && hfs_all_ok && nm_max > 0u ? nm_max - 1u : 0u);
   for (uint32_t nb = n0; nb < n1; nb += kWave) {
+    if (bsm != nullptr) {
+      const uint32_t* B = bsm + (size_t)(nb >> 6) * BSW;
+      const uint64_t bcn_min = (uint64_t)B[kBsCnMin] | ((uint64_t)B[kBsCnMin + 1] << 32);
+      const uint64_t bcn_max = (uint64_t)B[kBsCnMax] | ((uint64_t)B[kBsCnMax + 1] << 32);
+      const uint32_t bfl = B[kBsFlags], ckmin = B[kBsCkMin], ckmax = B[kBsCkMax];
+      const uint32_t nreal = B[kBsNReal];
+      // every node NONE: PodFitsNumber, PodFitsMemory or PodFitsClock fails on all of them
+      bool bnone = num_min > bcn_max;
+      bnone = bnone || (all_pm && (!hfs_none_ok || B[bs_tn] <= s_mpm_min));
+      if (all_pc && c_uni) {
+        // no healthy card of the block has the wave's clock (hc = 0 < need), or one-model
+        // nodes of that clock with too few healthy cards
+        bnone = bnone || cpc_max < B[kBsHckMin] || cpc_max > B[kBsHckMax] ||
+                ((bfl & kBsUni4) && ckmin == ckmax && ckmin == cpc_max && B[kBsNhMax] < nc_min);
+      }
+      // every node ALL: feasible for every pod, one-model, and all or none qualifying
+      bool ball = (bfl & kBsOneModel) && num_max <= bcn_min;
+      ball = ball && (!any_pm || (hfs_all_ok && B[bs_ta] > s_mpm_max));
+      ball = ball && (!any_pc || (c_uni && ckmin == ckmax && ckmin == cpc_max &&
+                                  B[kBsNhMin] >= nc_max));
+      const bool allq = ckmin >= s_c_max && B[kBsMrfMin] > s_m_max;
+      const bool noq = ckmax < s_c_min || B[kBsMrfMax] <= s_m_min;
+      ball = ball && (allq || noq) && !bnone;
+      if (bnone || ball) {
+        const uint64_t vb = nreal >= 64u ? ~0ull : ((1ull << nreal) - 1ull);
+        if (STATS && !trace && lane == 0) {
+          atomicAdd(stats + (ball ? 0 : 1), (unsigned long long)nreal);
+          atomicAdd(stats + (ball ? 11 : 10), 1ull);
+          atomicAdd(stats + 12, 1ull);
+        }
+        if (lane == 0) bsw[nb >> 6] = ball ? BlockMask{vb, vb} : BlockMask{0ull, 0ull};
+        if (bnone) continue;
+        nf_all += nreal;
+        nz_all += B[kBsNzt];
+        if (allq) {
+          if constexpr (WIT) {  // one lane folds the block's witnesses (the reduce sums lanes)
+            if (lane == 0) {
+#pragma unroll
+              for (int f = 0; f < 6; ++f) {
+                const uint32_t v = B[kBsMx + f], cnt = B[kBsWc + f], low = nb + B[kBsWl + f];
+                const bool gt = v > aw[f], eq = v == aw[f];
+                ac[f] = gt ? cnt : ac[f] + (eq ? cnt : 0u);
+                al[f] = gt ? low : (eq ? min(al[f], low) : al[f]);
+                aw[f] = gt ? v : aw[f];
+              }
+            }
+          } else {
+            a_bw = max(a_bw, B[kBsMx + kMaxBw]);
+            a_ck = max(a_ck, B[kBsMx + kMaxClock]);
+            a_core = max(a_core, B[kBsMx + kMaxCore]);
+            a_free = max(a_free, B[kBsMx + kMaxFree]);
+            a_pw = max(a_pw, B[kBsMx + kMaxPower]);
+            a_tot = max(a_tot, B[kBsMx + kMaxTotal]);
+          }
+        }
+        const uint32_t bi = nb >> 6;
+        if ((bi >> 6) != blk_wi) {
+          blk_flush();
+          blk_wi = bi >> 6;
+          blk_bits = 0;
+        }
+        blk_bits |= 1ull << (bi & 63u);
+        continue;
+      }
+    }
     const uint32_t n = nb + lane;
     const bool valid = n < n1;
     // this block's tile of summaries (nb is a multiple of 64): word w at s[64 w]
@@ -2526,6 +2602,22 @@ __global__ __launch_bounds__(kBlock) void k_set_static(unsigned char* __restrict
     s2[sum_index(q, kS2Static, sum2_stride)] = (uint32_t)value[t];
     s2[sum_index(q, kS2Static + 1, sum2_stride)] = (uint32_t)(value[t] >> 32);
   }
+  if (pc.bsum || pc.bsum_p) {  // widen the blocks' CardNumber bounds to the new value
+    const uint32_t bsw = pc.bsum_words;
+    const unsigned long long cn = (unsigned long long)card_number[t];
+    if (pc.bsum) {
+      unsigned long long* b = reinterpret_cast<unsigned long long*>(
+          pc.bsum + (size_t)(node[t] >> 6) * bsw);
+      atomicMin(b + kBsCnMin / 2, cn);
+      atomicMax(b + kBsCnMax / 2, cn);
+    }
+    if (pc.bsum_p) {
+      unsigned long long* b = reinterpret_cast<unsigned long long*>(
+          pc.bsum_p + (size_t)(pc.inv[node[t]] >> 6) * bsw);
+      atomicMin(b + kBsCnMin / 2, cn);
+      atomicMax(b + kBsCnMax / 2, cn);
+    }
+  }
   uint64_t* hdr = reinterpret_cast<uint64_t*>(nodes + (size_t)node[t] * stride);
   hdr[0] = value[t];        // static_score bits (f64 on the fast paths, u64 on U64)
   hdr[1] = card_number[t];  // CardNumber
@@ -3692,7 +3784,7 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                                               chunk_nodes, pp.m_32, pp.c_32,
                                               pp.number, pp.need_mem, pp.need_clk, n_pods,
                                               part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,
-                                              blk, blk_stride, stats))
+                                              blk, blk_stride, stats, nullptr, pp.bsum))
         else if (pp.one_model)
           YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK, false, false>), grid, dim3(kBlock), 0, s,
                                               nodes, sum, reinterpret_cast<const uint32_t*>(sum2),
@@ -3700,7 +3792,7 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                                               chunk_nodes, pp.m_32, pp.c_32,
                                               pp.number, pp.need_mem, pp.need_clk, n_pods,
                                               part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,
-                                              blk, blk_stride, stats))
+                                              blk, blk_stride, stats, nullptr, pp.bsum))
         else
           YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK, false>), grid, dim3(kBlock), 0, s,
                                               nodes, sum, reinterpret_cast<const uint32_t*>(sum2),
@@ -3708,7 +3800,7 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                                               chunk_nodes, pp.m_32, pp.c_32,
                                               pp.number, pp.need_mem, pp.need_clk, n_pods,
                                               part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,
-                                              blk, blk_stride, stats));
+                                              blk, blk_stride, stats, nullptr, pp.bsum));
       } else {
         YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_filter_maxima<KK, Path::N32>), grid, dim3(kBlock),
                                             0, s, nodes, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
@@ -3983,6 +4075,33 @@ hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t 
   return hipGetLastError();
 }
 
+// Tighten the blocks' CardNumber bounds again (BlockSumWord cn_min / cn_max) from the K1
+// summaries' current values, one wave per 64-node block.
+__global__ __launch_bounds__(kWave) void k_bsum_cn(const uint32_t* __restrict__ sum,
+                                                   uint32_t sum_stride, uint32_t n_nodes,
+                                                   uint32_t* __restrict__ bsum, uint32_t bsw) {
+  const uint32_t b = blockIdx.x, n = b * 64u + threadIdx.x;
+  const bool v = n < n_nodes;
+  uint64_t cn = 0;
+  if (v)
+    cn = (uint64_t)sum[sum_index(n, kSumCnLo, sum_stride)] |
+         ((uint64_t)sum[sum_index(n, kSumCnHi, sum_stride)] << 32);
+  const uint64_t lo = wave_min_u64(v ? cn : ~0ull), hi = wave_max_u64(v ? cn : 0ull);
+  if (threadIdx.x == 0) {
+    uint64_t* o = reinterpret_cast<uint64_t*>(bsum + (size_t)b * bsw);
+    o[kBsCnMin / 2] = lo;
+    o[kBsCnMax / 2] = hi;
+  }
+}
+
+hipError_t launch_bsum_cn(const unsigned char* sum, uint32_t sum_stride, uint32_t n_nodes,
+                          uint32_t* bsum, uint32_t bsw, hipStream_t s) {
+  if (n_nodes == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bsum_cn, dim3((n_nodes + 63) / 64), dim3(kWave), 0, s,
+                     reinterpret_cast<const uint32_t*>(sum), sum_stride, n_nodes, bsum, bsw);
+  return hipGetLastError();
+}
+
 hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32_t* node,
                              const uint64_t* value, const uint64_t* card_number, uint32_t count,
                              unsigned char* sum, uint32_t sum_stride, unsigned char* sum2,
@@ -4218,7 +4337,7 @@ hipError_t launch_k1_block_witness(int K, const unsigned char* nodes, const unsi
                                       reinterpret_cast<const uint32_t*>(mix), pp.x1, n_nodes,
                                       chunk_nodes, pp.m_32, pp.c_32, pp.number, pp.need_mem,
                                       pp.need_clk, n_pods, pmax, pcnt, bm, bm_stride, bs,
-                                      bs_stride, blk, blk_stride, nullptr, pwit));
+                                      bs_stride, blk, blk_stride, nullptr, pwit, pp.bsum));
   return hipGetLastError();
 }
 

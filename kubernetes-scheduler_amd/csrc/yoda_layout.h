@@ -111,6 +111,33 @@ enum K2SumWord { kS2Static = 0, kS2Clock = 2, kS2Meta = 3, kS2Bw = 4, kS2Core = 
                  kS2MinClk = 7, kS2Fs = 8 };
 __host__ __device__ constexpr uint32_t k2sum_stride(int k) { return 32u + 8u * (uint32_t)k; }
 
+// Block summary (N32 path): bounds over the REAL nodes of one 64-node block of a summary
+// order (the snapshot order, or the block-grouped copy's), so that the block K1 can decide a
+// whole block for a wave from one scalar read -- every node NONE, or every node ALL with one
+// maxima contribution -- before any per-node work.  u32 words, bsum_stride(K) bytes a block:
+//   cn_min, cn_max (u64, words 0-3)   CardNumber bounds (k_set_static keeps them valid bounds
+//                                     with atomics; a recompute makes them tight again)
+//   flags    kBsOneModel: every node one GPU model with one TotalMemory (kSumUni4|UniTotal);
+//            kBsUni4: every node kSumUni4
+//   ck_min, ck_max      the nodes' clock (one-model nodes) / card clocks (others)
+//   hck_min, hck_max    the clocks of the HEALTHY cards (~0 / 0: none)
+//   nh_min, nh_max      healthy cards per node
+//   mrf_min, mrf_max    1 + max FreeMemory per node (K1Sum mrf1)
+//   nreal, nzt          real nodes in the block, of them TotalMemorySum == 0
+//   mx[6]   per MaxValue field (kMax* order) the max over the nodes of the contribution a
+//           one-model node makes when some card qualifies (its model values, max free)
+//   wc[6]   nodes reaching mx[f];  wl[6]  the lowest of them (offset in the block)
+//   tmin[K], tmax[K]    bounds of hfs[k] (K1Sum: 1 + free of the k-th healthy card by free)
+enum BlockSumWord {
+  kBsCnMin = 0, kBsCnMax = 2, kBsFlags = 4, kBsCkMin = 5, kBsCkMax = 6, kBsHckMin = 7,
+  kBsHckMax = 8, kBsNhMin = 9, kBsNhMax = 10, kBsMrfMin = 11, kBsMrfMax = 12, kBsNReal = 13,
+  kBsNzt = 14, kBsMx = 16, kBsWc = 22, kBsWl = 28, kBsT = 34
+};
+constexpr uint32_t kBsOneModel = 1u, kBsUni4 = 2u;
+__host__ __device__ constexpr uint32_t bsum_stride(int k) {
+  return 4u * ((kBsT + 2u * (uint32_t)k + 3u) & ~3u);
+}
+
 // Per-card GPU models of every node (N32 path), in the K2 summary's descending-free card order,
 // read with lane = node by the block kernels for the nodes whose cards are not all one model
 // (no kSumUni4): u32 words
@@ -183,6 +210,11 @@ struct PermCopy {
   const uint32_t* inv = nullptr;
   unsigned char* sum = nullptr;
   unsigned char* sum2 = nullptr;
+  // and the block summaries' CardNumber bounds (BlockSumWord), of the snapshot order and of
+  // the block-grouped order, widened with atomics so that they stay valid bounds
+  uint32_t* bsum = nullptr;
+  uint32_t* bsum_p = nullptr;
+  uint32_t bsum_words = 0;  // bsum_stride(K) / 4
 };
 
 // Mode B node record: V = Cpu/100, U = DiskIO/50 (algorithm.go:71,73).
@@ -292,6 +324,8 @@ struct PodParams {
   const uint32_t* ids = nullptr;
   // the snapshot's memory ranks (MemTab; vf == nullptr: none)
   MemTab mt = {};
+  // 64-node block summaries of the order the run visits (BlockSumWord; nullptr: none)
+  const uint32_t* bsum = nullptr;
 };
 
 // Per-pod state produced between kernels (length P each unless noted).
