@@ -273,6 +273,10 @@ int yoda_comm_run_local(yoda_t* const* handles, int world, int mode);
  * _local: the same over `world` handles of this process on one device (tests). */
 int yoda_comm_greedy(yoda_t* h, const yoda_node_soa* all_nodes, const yoda_pod_soa* pods,
                      int mode, uint32_t flags, int32_t* pick);
+/* Work counters of the last yoda_comm_greedy[_local] on this handle (the first handle for
+ * _local): out[5] = {windows, pods evaluated one by one (exchanges), capacity restarts,
+ * mid-window list refreshes, collective calls}. */
+int yoda_comm_greedy_stats(const yoda_t* h, uint32_t* out);
 int yoda_comm_greedy_local(yoda_t* const* handles, int world, const yoda_node_soa* all_nodes,
                            const yoda_pod_soa* pods, int mode, uint32_t flags, int32_t* pick);
 
@@ -353,12 +357,18 @@ int yoda_greedy_refreshes(const yoda_t* h, uint32_t* refreshes);
  *     window's pod order ;
  *   merge the shards' lists (keep the first yoda_topk_k() of their union in that order) ;
  *   yoda_gs_begin_window ; loop { yoda_gs_resolve -> next ; if next == W break ;
+ *     [mid-window refresh, every 8th such pod: when yoda_gs_uncertified(next + 1, 256) >= 16,
+ *      push yoda_gs_take_dirty, yoda_shard_topk again on every shard (the window's phase-1
+ *      masks and maxima stay valid: only static scores change), merge as above and
+ *      yoda_gs_refresh(next, merged) -- then resolve again] ;
  *     push yoda_gs_take_dirty to every shard (yoda_set_node_state) ;
  *     yoda_shard_best_one(next) on every shard ; pick = max score, lowest node ;
  *     yoda_gs_assign(ws + next, pick) } ; push yoda_gs_take_dirty.
- * Fast record paths (N32 / F64) and flags == 0 only: with YODA_GREEDY_CARD_CAPACITY or the
- * U64 path, evaluate each pod exactly with the sharded yoda_shard_* sequence instead and
- * feed the pick to yoda_gs_assign. */
+ * That is the flags == 0 protocol on the fast record paths (N32 / F64).  With
+ * YODA_GREEDY_CARD_CAPACITY each window runs the witness phase 1 below instead, and the first
+ * pod the session cannot certify opens the next window (sized by yoda_greedy_next_window);
+ * no pod is evaluated one by one.  On the U64 path every pod is one exact sharded step
+ * (yoda_shard_phase1 / phase2 / finalize over a one-pod batch) fed to yoda_gs_assign. */
 int yoda_topk_k(void);
 /* Set the allocated memory (and CardNumber) of the listed nodes (GLOBAL ids; ids outside
  * this handle's shard are ignored) and refresh their static score on the device. */
@@ -417,6 +427,18 @@ int yoda_gs_set_witness(yoda_gs_t* g, const uint64_t* maxima, const uint32_t* wi
  * also tracks CardNumber decrements: feasibility and, through the witnesses, the maxima). */
 int yoda_gs_resolve(yoda_gs_t* g, uint32_t* next);
 int yoda_gs_assign(yoda_gs_t* g, uint32_t queue_pos, int32_t pick);
+/* flags == 0: *count = window pods [from, from + scan) with >= 2 feasible nodes whose lists no
+ * longer certify them (they stay so: scores only drop) -- the refresh trigger. */
+int yoda_gs_uncertified(const yoda_gs_t* g, uint32_t from, uint32_t scan, uint32_t* count);
+/* flags == 0: new candidate lists for window pods [from, wn) ([k][wn] in window order, as
+ * yoda_gs_begin_window's, scored against the CURRENT node state): each list's threshold
+ * becomes its refresh-time k-th score. */
+int yoda_gs_refresh(yoda_gs_t* g, uint32_t from, const double* top_score,
+                    const uint32_t* top_node);
+/* YODA_GREEDY_CARD_CAPACITY: the size of the window that a restart at window index `progress`
+ * opens (130 % of the progress in whole waves, at least 64, at most wmax) -- the one rule of
+ * yoda_greedy, yoda_comm_greedy and the Python driver. */
+uint32_t yoda_greedy_next_window(uint32_t progress, uint32_t wmax);
 /* Nodes whose state changed since the last call (at most cap), with their current state. */
 int yoda_gs_take_dirty(yoda_gs_t* g, uint32_t cap, uint32_t* nodes, uint64_t* alloc,
                        uint64_t* card_number, uint32_t* count);

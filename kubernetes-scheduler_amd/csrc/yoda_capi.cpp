@@ -440,6 +440,7 @@ struct yoda_handle {
   int comm_rank = 0, comm_world = 1;
   DevBuf ex1, rec, rec_all;  // [maxima 6P | count slots world x P] u64; ShardRec [P], [world][P]
   DevBuf cg_max, cg_cnt, cg_wit, cg_gather;  // yoda_comm_greedy: exchange buffers
+  uint32_t comm_greedy_stats[5] = {};          // yoda_comm_greedy_stats
   // sharded exact normalize (K3 over a shard): per-pod records of the flagged pods, pending
   // until the shards' records are merged (yoda_shard_exact_merge)
   DevBuf k3rec, k3all;
@@ -2737,6 +2738,7 @@ struct GreedyState {
     // end of that read, before which the pages are not rewritten
     const unsigned char* d = static_cast<const unsigned char*>(h->upd_stage.dp);
     const uint32_t stride = h->path == Path::N32 ? n32_stride(h->K) : node_stride(h->K);
+    h->blksum_loose = true;  // (the atomics keep the block bounds valid, not tight)
     HIP_TRY(h, launch_set_static(h->nodes.as<unsigned char>(), stride,
                                  reinterpret_cast<const uint32_t*>(d),
                                  reinterpret_cast<const uint64_t*>(d + o_val),
@@ -3471,10 +3473,14 @@ struct yoda_greedy_session {
   std::vector<uint32_t> order, touched_list, dirty_list, ever_list;
   std::vector<int32_t> pick;
   // current window (queue positions [ws, ws + wn)), inputs in window order
-  uint32_t ws = 0, wn = 0, k = 0, next = 0, resolved = 0, assigned = 0;
+  uint32_t ws = 0, wn = 0, k = 0, next = 0, resolved = 0, assigned = 0, refreshes = 0;
   bool in_window = false, wrapped = false;
   std::vector<uint32_t> counts, ti;
   std::vector<double> ts;
+  // each list's certificate threshold (flags 0): its last entry's window-start -- or, after a
+  // mid-window refresh (yoda_gs_refresh), refresh-time -- score and node
+  std::vector<double> Tw;
+  std::vector<uint32_t> Tix;
   // YODA_GREEDY_CARD_CAPACITY (greedy): cross[q] = window-touched nodes whose
   // CardNumber has dropped from >= q (window start) to < q, i.e. nodes a pod needing q cards
   // has lost since its candidate list was made; and the window's PreScore maxima with their
@@ -3615,6 +3621,25 @@ struct yoda_greedy_session {
   }
   // Capacity-mode resolve of window pod i (input pod p): true with *pk when certified.
   bool resolve_capacity(uint32_t i, uint32_t p, int32_t* pk);
+  // flags 0: window pod i's best current candidate (window-start score - old static + new
+  // static) and whether the list certifies it: every unlisted node scored <= T at the window
+  // start or last refresh (ties: higher index) and its score can only have dropped since
+  bool certify0(uint32_t i, uint32_t* best) const {
+    const uint32_t nf = counts[i], len = std::min<uint32_t>(nf, k);
+    double bs = -1.0;
+    uint32_t bi = 0xffffffffu;
+    for (uint32_t kk = 0; kk < len; ++kk) {
+      const uint32_t n = ti[(size_t)kk * wn + i];
+      double cur = ts[(size_t)kk * wn + i];
+      if (touched_w[n]) cur = cur - (double)stat_w[n] + (double)stat[n];
+      if (cur > bs || (cur == bs && n < bi)) {
+        bs = cur;
+        bi = n;
+      }
+    }
+    *best = bi;
+    return nf <= k || bs > Tw[i] || (bs == Tw[i] && bi <= Tix[i]);
+  }
   // why capacity certificates failed: wrap, few feasible left, zero-total, maxima, list
   // exhausted, below the threshold
   uint64_t why[6] = {};
@@ -3819,6 +3844,13 @@ int yoda_gs_begin_window(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
     g->counts.assign(counts, counts + 2 * (size_t)wn);
     g->ts.assign(top_score, top_score + (size_t)k * wn);
     g->ti.assign(top_node, top_node + (size_t)k * wn);
+    g->Tw.resize(wn);
+    g->Tix.resize(wn);
+    for (uint32_t i = 0; i < wn; ++i) {
+      const uint32_t len = std::max<uint32_t>(1, std::min<uint32_t>(counts[i], k));
+      g->Tw[i] = top_score[(size_t)(len - 1) * wn + i];
+      g->Tix[i] = top_node[(size_t)(len - 1) * wn + i];
+    }
     return YODA_OK;
   } catch (...) {
     return YODA_ERR_INVALID_ARG;
@@ -3845,7 +3877,7 @@ int yoda_gs_set_witness(yoda_gs_t* g, const uint64_t* maxima, const uint32_t* wi
 // (greedy): *next = its window index, or wn when the window is done.
 int yoda_gs_resolve(yoda_gs_t* g, uint32_t* next) {
   if (!g || !next || !g->in_window) return YODA_ERR_INVALID_ARG;
-  const uint32_t wn = g->wn, KT = g->k;
+  const uint32_t wn = g->wn;
   const bool capacity = (g->flags & YODA_GREEDY_CARD_CAPACITY) != 0;
   while (g->next < wn) {
     const uint32_t i = g->next;
@@ -3863,21 +3895,8 @@ int yoda_gs_resolve(yoda_gs_t* g, uint32_t* next) {
     } else if (g->wrapped) {
       break;
     } else {
-      const uint32_t len = std::min<uint32_t>(nf, KT);
-      double bs = -1.0;
-      uint32_t bi = 0xffffffffu;
-      for (uint32_t k = 0; k < len; ++k) {
-        const uint32_t n = g->ti[(size_t)k * wn + i];
-        double cur = g->ts[(size_t)k * wn + i];
-        if (g->touched_w[n]) cur = cur - (double)g->stat_w[n] + (double)g->stat[n];
-        if (cur > bs || (cur == bs && n < bi)) {
-          bs = cur;
-          bi = n;
-        }
-      }
-      const double T = g->ts[(size_t)(len - 1) * wn + i];
-      const uint32_t tidx = g->ti[(size_t)(len - 1) * wn + i];
-      if (!(nf <= KT || bs > T || (bs == T && bi <= tidx))) break;
+      uint32_t bi;
+      if (!g->certify0(i, &bi)) break;
       pk = (int32_t)bi;
     }
     g->pick[p] = pk;
@@ -3886,6 +3905,61 @@ int yoda_gs_resolve(yoda_gs_t* g, uint32_t* next) {
     ++g->resolved;
   }
   *next = g->next;
+  return YODA_OK;
+}
+
+uint32_t yoda_greedy_next_window(uint32_t progress, uint32_t wmax) {
+  // the next window holds 130 % of this one's progress, in whole waves: small windows cost
+  // less (K1 / K2 time grows with the pods) and most restart near where the last one did;
+  // profiles/r03/greedy_capacity/grow_ab.txt (1.81-1.91 s with the earlier power of two >=
+  // twice the progress, 1.57-1.64 s at 130 %).  YODA_GREEDY_GROW_PCT: A/B knob (0: that
+  // power of two)
+  static const uint32_t grow = YODA_KNOB("YODA_GREEDY_GROW_PCT", 130);
+  wmax = std::max<uint32_t>(wmax, 1);
+  uint32_t w2 = 64;
+  if (grow) {
+    const uint64_t t = (uint64_t)progress * grow / 100;
+    w2 = (uint32_t)std::min<uint64_t>(wmax, std::max<uint64_t>(64, (t + 63) / 64 * 64));
+  } else {
+    while (w2 < 2 * progress && w2 < wmax) w2 <<= 1;
+  }
+  return std::min(w2, wmax);
+}
+
+int yoda_gs_uncertified(const yoda_gs_t* g, uint32_t from, uint32_t scan, uint32_t* count) {
+  if (!g || !count || !g->in_window) return YODA_ERR_INVALID_ARG;
+  if (g->flags & YODA_GREEDY_CARD_CAPACITY) return YODA_ERR_STATE;
+  uint32_t c = 0, bi;
+  const uint32_t end = (uint32_t)std::min<uint64_t>(g->wn, (uint64_t)from + scan);
+  for (uint32_t i = from; i < end; ++i)
+    if (g->counts[i] >= 2 && g->counts[(size_t)g->wn + i] == 0 && !g->certify0(i, &bi)) ++c;
+  *count = c;
+  return YODA_OK;
+}
+
+int yoda_gs_refresh(yoda_gs_t* g, uint32_t from, const double* top_score,
+                    const uint32_t* top_node) {
+  if (!g || !g->in_window || !top_score || !top_node || from > g->wn) return YODA_ERR_INVALID_ARG;
+  if (g->flags & YODA_GREEDY_CARD_CAPACITY) return YODA_ERR_STATE;
+  const uint32_t wn = g->wn, k = g->k;
+  for (uint32_t i = from; i < wn; ++i) {
+    const uint32_t len = std::min<uint32_t>(g->counts[i], k);
+    for (uint32_t kk = 0; kk < len; ++kk) {
+      const size_t o = (size_t)kk * wn + i;
+      const uint32_t n = top_node[o];
+      if (n >= g->N) return YODA_ERR_RANGE;
+      // stored so that the certificate's  stored - old static + current static  is its
+      // current score (the refresh scored it with the current static)
+      g->ti[o] = n;
+      g->ts[o] = g->touched_w[n] ? top_score[o] + (double)g->stat_w[n] - (double)g->stat[n]
+                                 : top_score[o];
+    }
+    if (len) {
+      g->Tw[i] = top_score[(size_t)(len - 1) * wn + i];
+      g->Tix[i] = top_node[(size_t)(len - 1) * wn + i];
+    }
+  }
+  ++g->refreshes;
   return YODA_OK;
 }
 
@@ -4214,15 +4288,7 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
       // profiles/r03/greedy_capacity/grow_ab.txt (1.81-1.91 s with the earlier power of two >=
       // twice the progress, 1.57-1.64 s at 130 %).  YODA_GREEDY_GROW_PCT: A/B knob (0: that
       // power of two)
-      static const uint32_t grow = YODA_KNOB("YODA_GREEDY_GROW_PCT", 130);
-      uint32_t w2 = 64;
-      if (grow) {
-        const uint64_t t = (uint64_t)next * grow / 100;
-        w2 = (uint32_t)std::min<uint64_t>(Wmax, std::max<uint64_t>(64, (t + 63) / 64 * 64));
-      } else {
-        while (w2 < 2 * next && w2 < Wmax) w2 <<= 1;
-      }
-      W = std::min(w2, Wmax);
+      W = yoda_greedy_next_window(next, Wmax);
       ws += next;
     } else {
       ws += wn;
@@ -4452,6 +4518,7 @@ struct Coll {
   yoda_t* const* hs;
   int n, world;
   bool local;
+  uint32_t* calls = nullptr;  // collective calls made (yoda_comm_greedy_stats)
   int nccl(ncclResult_t r, const char* what) const {
     if (r == ncclSuccess) return YODA_OK;
     return fail(hs[0], YODA_ERR_HIP, std::string(what) + ": " + rccl().error_string(r));
@@ -4459,6 +4526,7 @@ struct Coll {
   // in-place elementwise all-reduce of `count` u64 or u32 device words (MAX / SUM / MIN)
   int allreduce(const std::vector<void*>& bufs, size_t count, bool u64, ncclRedOp_t op) const {
     if (count == 0) return YODA_OK;
+    if (calls) ++*calls;
     if (!local)
       return nccl(rccl().all_reduce(bufs[0], bufs[0], count, u64 ? ncclUint64 : ncclUint32, op,
                                     hs[0]->comm, hs[0]->stream),
@@ -4494,6 +4562,7 @@ struct Coll {
   int allgather(const std::vector<const void*>& in, size_t bytes,
                 std::vector<unsigned char>& out) const {
     out.resize((size_t)world * bytes);
+    if (calls) ++*calls;
     if (local) {
       for (int i = 0; i < n; ++i) std::memcpy(out.data() + (size_t)i * bytes, in[i], bytes);
       return YODA_OK;
@@ -4527,7 +4596,10 @@ static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local);
 static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yoda_node_soa* all,
                        const yoda_pod_soa* pods, int mode, uint32_t flags, int32_t* pick) {
   yoda_t* h0 = hs[0];
-  const Coll co{hs, n, world, local};
+  Coll co{hs, n, world, local};
+  uint32_t* st = h0->comm_greedy_stats;  // windows, exact pods, restarts, refreshes, collectives
+  std::fill(st, st + 5, 0u);
+  co.calls = st + 4;
   const uint32_t P = pods->n_pods;
   for (int i = 0; i < n; ++i)
     if (!hs[i]->has_nodes) return fail(h0, YODA_ERR_NO_NODES, "no node snapshot uploaded");
@@ -4584,6 +4656,7 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
         HIP_TRY(h0, hipStreamSynchronize(h0->stream));
         if ((rc = yoda_gs_assign(g, q, pk))) return fail(h0, rc, "greedy: assign");
         ++h0->greedy_fallbacks;
+        ++st[1];
       }
       return push(false);
     }
@@ -4639,45 +4712,51 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
         if ((rc = co.allreduce(bwn, 6ull * wn, false, ncclMin))) return rc;
       }
       // the shards' candidate lists, all-gathered and merged: the first K of the union in
-      // (score desc, node asc) order contain the global top K
+      // (score desc, node asc) order contain the global top K (window pods [from, wn) only)
       counts.resize(2ull * wn);
-      const size_t lb = (size_t)K * wn * 12;  // per shard: K x wn scores (f64) + nodes (u32)
-      mine.resize((size_t)n * lb);
-      for (int i = 0; i < n; ++i) {
-        unsigned char* m = mine.data() + (size_t)i * lb;
-        if ((rc = yoda_shard_topk(hs[i], hs[i]->cg_max.as<uint64_t>(),
+      auto merged_lists = [&](uint32_t from) -> int {
+        const size_t lb = (size_t)K * wn * 12;  // per shard: K x wn scores (f64) + nodes (u32)
+        mine.resize((size_t)n * lb);
+        for (int i = 0; i < n; ++i) {
+          unsigned char* m = mine.data() + (size_t)i * lb;
+          int r = yoda_shard_topk(hs[i], hs[i]->cg_max.as<uint64_t>(),
                                   hs[i]->cg_cnt.as<uint32_t>(), counts.data(),
                                   reinterpret_cast<double*>(m),
-                                  reinterpret_cast<uint32_t*>(m + (size_t)K * wn * 8))))
-          return rc;
-      }
-      std::vector<const void*> ins;
-      for (int i = 0; i < n; ++i) ins.push_back(mine.data() + (size_t)i * lb);
-      if ((rc = co.allgather(ins, lb, gathered))) return rc;
-      ts.assign((size_t)K * wn, -1.0);
-      ti.assign((size_t)K * wn, 0xffffffffu);
-      for (uint32_t p = 0; p < wn; ++p) {
-        cand.clear();
-        for (int r = 0; r < world; ++r) {
-          const unsigned char* b = gathered.data() + (size_t)r * lb;
-          const double* sc = reinterpret_cast<const double*>(b);
-          const uint32_t* nd = reinterpret_cast<const uint32_t*>(b + (size_t)K * wn * 8);
-          for (uint32_t k = 0; k < K; ++k)
-            if (nd[(size_t)k * wn + p] != 0xffffffffu)
-              cand.emplace_back(sc[(size_t)k * wn + p], nd[(size_t)k * wn + p]);
+                                  reinterpret_cast<uint32_t*>(m + (size_t)K * wn * 8));
+          if (r) return r;
         }
-        std::sort(cand.begin(), cand.end(), [](const std::pair<double, uint32_t>& a,
-                                               const std::pair<double, uint32_t>& b) {
-          return a.first > b.first || (a.first == b.first && a.second < b.second);
-        });
-        for (uint32_t k = 0; k < K && k < cand.size(); ++k) {
-          ts[(size_t)k * wn + p] = cand[k].first;
-          ti[(size_t)k * wn + p] = cand[k].second;
+        std::vector<const void*> ins;
+        for (int i = 0; i < n; ++i) ins.push_back(mine.data() + (size_t)i * lb);
+        int r = co.allgather(ins, lb, gathered);
+        if (r) return r;
+        ts.assign((size_t)K * wn, -1.0);
+        ti.assign((size_t)K * wn, 0xffffffffu);
+        for (uint32_t p = from; p < wn; ++p) {
+          cand.clear();
+          for (int rk = 0; rk < world; ++rk) {
+            const unsigned char* b = gathered.data() + (size_t)rk * lb;
+            const double* sc = reinterpret_cast<const double*>(b);
+            const uint32_t* nd = reinterpret_cast<const uint32_t*>(b + (size_t)K * wn * 8);
+            for (uint32_t k = 0; k < K; ++k)
+              if (nd[(size_t)k * wn + p] != 0xffffffffu)
+                cand.emplace_back(sc[(size_t)k * wn + p], nd[(size_t)k * wn + p]);
+          }
+          std::sort(cand.begin(), cand.end(), [](const std::pair<double, uint32_t>& a,
+                                                 const std::pair<double, uint32_t>& b) {
+            return a.first > b.first || (a.first == b.first && a.second < b.second);
+          });
+          for (uint32_t k = 0; k < K && k < cand.size(); ++k) {
+            ts[(size_t)k * wn + p] = cand[k].first;
+            ti[(size_t)k * wn + p] = cand[k].second;
+          }
         }
-      }
+        return YODA_OK;
+      };
+      if ((rc = merged_lists(0))) return rc;
       if ((rc = yoda_gs_begin_window(g, ws, wn, K, counts.data(), ts.data(), ti.data())))
         return fail(h0, rc, "greedy: begin window");
       ++h0->greedy_windows;
+      ++st[0];
       if (capacity) {
         mx_h.resize(6ull * wn);
         wit_h.resize(12ull * wn);
@@ -4689,22 +4768,43 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
           return fail(h0, rc, "greedy: witnesses");
         uint32_t nxt = 0;
         if ((rc = yoda_gs_resolve(g, &nxt))) return fail(h0, rc, "greedy: resolve");
-        if (nxt < wn) {  // the uncertified pod opens the next window (sized as dist.py does)
+        if (nxt < wn) {  // the uncertified pod opens the next window (yoda_greedy's rule)
           ++h0->greedy_restarts;
+          ++st[2];
           ws += nxt;
-          uint32_t b = 0;
-          while ((1ull << b) < 2ull * std::max<uint32_t>(nxt, 1)) ++b;
-          W = std::min<uint32_t>(W0, std::max<uint32_t>(64, 1u << b));
+          W = yoda_greedy_next_window(nxt, W0);
         } else {
           ws += wn;
           W = std::min<uint32_t>(W0, 2 * W);
         }
         continue;
       }
+      // mid-window list refresh (yoda_greedy's): every kFbCheck exact pods,
+      // when >= kScanMin of the next kScan window pods are uncertified already, every shard's
+      // top-k runs again against the current state and the merged lists replace the old ones
+      constexpr uint32_t kFbCheck = 8, kScan = 256, kScanMin = 16;
+      uint32_t fb_since = 0;
       for (;;) {
         uint32_t nxt = 0;
         if ((rc = yoda_gs_resolve(g, &nxt))) return fail(h0, rc, "greedy: resolve");
         if (nxt >= wn) break;
+        if (++fb_since >= kFbCheck && wn - nxt >= 2 * kScan && !g->wrapped) {
+          fb_since = 0;
+          uint32_t unc = 0;
+          if ((rc = yoda_gs_uncertified(g, nxt + 1, kScan, &unc))) return fail(h0, rc, "greedy");
+          if (unc >= kScanMin) {
+            if ((rc = push(false))) return rc;
+            if ((rc = merged_lists(nxt))) return rc;
+            if ((rc = yoda_gs_refresh(g, nxt, ts.data(), ti.data())))
+              return fail(h0, rc, "greedy: refresh");
+            ++h0->greedy_refreshes;
+            ++st[3];
+            uint32_t again = 0;
+            if ((rc = yoda_gs_resolve(g, &again))) return fail(h0, rc, "greedy: resolve");
+            if (again >= wn) break;
+            nxt = again;
+          }
+        }
         if ((rc = push(false))) return rc;
         one.resize((size_t)n * 16);
         for (int i = 0; i < n; ++i) {
@@ -4733,12 +4833,13 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
         if (bn < 0) return fail(h0, YODA_ERR_STATE, "greedy: no feasible node for a window pod");
         if ((rc = yoda_gs_assign(g, ws + nxt, (int32_t)bn))) return fail(h0, rc, "greedy: assign");
         ++h0->greedy_fallbacks;
+        ++st[1];
       }
       ws += wn;
     }
     return push(false);
   };
-  h0->greedy_windows = h0->greedy_fallbacks = h0->greedy_restarts = 0;
+  h0->greedy_windows = h0->greedy_fallbacks = h0->greedy_restarts = h0->greedy_refreshes = 0;
   rc = run();
   const int rr = push(true);  // restore the shards' original node state
   if (rc) return rc;
@@ -4748,6 +4849,12 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
 }
 
 extern "C" {
+int yoda_comm_greedy_stats(const yoda_t* h, uint32_t* out) {
+  if (!h || !out) return YODA_ERR_INVALID_ARG;
+  std::copy(h->comm_greedy_stats, h->comm_greedy_stats + 5, out);
+  return YODA_OK;
+}
+
 int yoda_comm_unique_id(uint8_t* id) {
   if (!id) return YODA_ERR_INVALID_ARG;
   if (!rccl().load()) return YODA_ERR_HIP;
@@ -4815,10 +4922,15 @@ int yoda_comm_greedy_local(yoda_t* const* hs, int world, const yoda_node_soa* al
   for (int i = 1; i < world; ++i)
     if (hs[i]->device != hs[0]->device)
       return fail(hs[0], YODA_ERR_INVALID_ARG, "local exchange: shards on different devices");
+  // one stream for every shard (the device copies order after the kernels); a shard's own
+  // queued work is ordered before it (switch_stream), and the shared stream's after it on exit
   std::vector<hipStream_t> saved(world);
   for (int i = 0; i < world; ++i) {
     saved[i] = hs[i]->stream;
-    hs[i]->stream = hs[0]->stream;
+    if (switch_stream(hs[i], hs[0]->stream) != YODA_OK) {
+      for (int j = 0; j < i; ++j) (void)switch_stream(hs[j], saved[j]);
+      return YODA_ERR_HIP;
+    }
   }
   int rc;
   try {
@@ -4828,7 +4940,8 @@ int yoda_comm_greedy_local(yoda_t* const* hs, int world, const yoda_node_soa* al
   } catch (...) {
     rc = fail(hs[0], YODA_ERR_INVALID_ARG, "unexpected exception");
   }
-  for (int i = 0; i < world; ++i) hs[i]->stream = saved[i];
+  for (int i = 0; i < world; ++i)
+    if (switch_stream(hs[i], saved[i]) != YODA_OK && rc == YODA_OK) rc = YODA_ERR_HIP;
   return rc;
 }
 
@@ -4839,11 +4952,15 @@ int yoda_comm_run_local(yoda_t* const* hs, int world, int mode) {
   for (int i = 1; i < world; ++i)
     if (hs[i]->device != hs[0]->device)
       return fail(hs[0], YODA_ERR_INVALID_ARG, "local exchange: shards on different devices");
-  // one stream for every shard of the step, so the device copies order after the kernels
+  // one stream for every shard (the device copies order after the kernels); a shard's own
+  // queued work is ordered before it (switch_stream), and the shared stream's after it on exit
   std::vector<hipStream_t> saved(world);
   for (int i = 0; i < world; ++i) {
     saved[i] = hs[i]->stream;
-    hs[i]->stream = hs[0]->stream;
+    if (switch_stream(hs[i], hs[0]->stream) != YODA_OK) {
+      for (int j = 0; j < i; ++j) (void)switch_stream(hs[j], saved[j]);
+      return YODA_ERR_HIP;
+    }
   }
   int rc;
   try {
@@ -4852,7 +4969,8 @@ int yoda_comm_run_local(yoda_t* const* hs, int world, int mode) {
     rc = fail(hs[0], YODA_ERR_INVALID_ARG, "unexpected exception");
   }
   if (rc == YODA_OK && hipStreamSynchronize(hs[0]->stream) != hipSuccess) rc = YODA_ERR_HIP;
-  for (int i = 0; i < world; ++i) hs[i]->stream = saved[i];
+  for (int i = 0; i < world; ++i)
+    if (switch_stream(hs[i], saved[i]) != YODA_OK && rc == YODA_OK) rc = YODA_ERR_HIP;
   return rc;
 }
 

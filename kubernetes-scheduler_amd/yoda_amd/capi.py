@@ -97,6 +97,10 @@ _SIGS = {
     "yoda_gs_take_dirty": ([_vp, _u32, _vp, _vp, _vp, C.POINTER(C.c_uint32)], C.c_int),
     "yoda_gs_touched_original": ([_vp, _u32, _vp, _vp, _vp, C.POINTER(C.c_uint32)], C.c_int),
     "yoda_gs_picks": ([_vp, _vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)], C.c_int),
+    "yoda_gs_uncertified": ([_vp, _u32, _u32, C.POINTER(C.c_uint32)], C.c_int),
+    "yoda_gs_refresh": ([_vp, _u32, _vp, _vp], C.c_int),
+    "yoda_greedy_next_window": ([_u32, _u32], C.c_uint32),
+    "yoda_comm_greedy_stats": ([_vp, _vp], C.c_int),
 }
 
 
@@ -466,6 +470,13 @@ class Yoda:
                     "yoda_comm_greedy")
         return pick
 
+    def comm_greedy_stats(self) -> dict:
+        """yoda_comm_greedy_stats of the last comm_greedy on this handle."""
+        out = np.zeros(5, np.uint32)
+        self._check(lib().yoda_comm_greedy_stats(self._h, _np_ptr(out)), "yoda_comm_greedy_stats")
+        return dict(zip(("windows", "exact_pods", "restarts", "refreshes", "collectives"),
+                        map(int, out)))
+
     def shard_finalize(self, mode, d_counts, d_best, d_idx, d_ties, d_lowest):
         self._check(lib().yoda_shard_finalize(self._h, mode, _vp(d_counts), _vp(d_best),
                                               _vp(d_idx), _vp(d_ties), _vp(d_lowest)),
@@ -509,6 +520,12 @@ def comm_greedy_local(handles, all_nodes, pods, mode: int = 0, flags: int = 0) -
 def topk_k() -> int:
     """Candidates per pod in the greedy top-k lists (yoda_topk_k)."""
     return int(lib().yoda_topk_k())
+
+
+def next_window(progress: int, wmax: int) -> int:
+    """Capacity greedy: the window a restart at window index `progress` opens
+    (yoda_greedy_next_window, the rule every driver shares)."""
+    return int(lib().yoda_greedy_next_window(progress, wmax))
 
 
 def _np_ptr(a: np.ndarray) -> int:
@@ -578,6 +595,20 @@ class GreedySession:
     def assign(self, queue_pos: int, pick: int):
         self._check(lib().yoda_gs_assign(self._g, queue_pos, pick), "yoda_gs_assign")
 
+    def uncertified(self, start: int, scan: int) -> int:
+        """Window pods [start, start + scan) whose lists no longer certify them (flags 0)."""
+        c = C.c_uint32()
+        self._check(lib().yoda_gs_uncertified(self._g, start, scan, C.byref(c)),
+                    "yoda_gs_uncertified")
+        return c.value
+
+    def refresh(self, start: int, top_score, top_node):
+        """New lists for window pods [start, wn), scored against the current state."""
+        s = np.ascontiguousarray(top_score, np.float64)
+        i = np.ascontiguousarray(top_node, np.uint32)
+        self._check(lib().yoda_gs_refresh(self._g, start, _np_ptr(s), _np_ptr(i)),
+                    "yoda_gs_refresh")
+
     def _nodes_call(self, fn, what):
         cnt = C.c_uint32()
         self._check(fn(self._g, self._buf_n.size, _np_ptr(self._buf_n), _np_ptr(self._buf_a),
@@ -606,5 +637,5 @@ def header_symbols(path: str = HEADER_PATH):
     """Entry points declared in include/yoda.h."""
     import re
     text = open(path).read()
-    return sorted(set(re.findall(r"^\s*(?:int|uint64_t|const char\*)\s+(yoda_[a-z0-9_]+)\s*\(", text,
+    return sorted(set(re.findall(r"^\s*(?:int|uint32_t|uint64_t|const char\*)\s+(yoda_[a-z0-9_]+)\s*\(", text,
                                  re.M)))

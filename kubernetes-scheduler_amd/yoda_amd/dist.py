@@ -492,7 +492,7 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
     how far the last one got), as the single-handle yoda_greedy does.
     `shards`: this process's shards (HandleShard); `nodes`: the FULL snapshot.  The shards'
     node state is restored at the end."""
-    from .capi import GreedySession, topk_k
+    from .capi import GreedySession, next_window, topk_k
     k = topk_k()
     gs = GreedySession(nodes, pods, flags)
     order = gs.queue_order()
@@ -506,7 +506,13 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
             for s in shards:
                 s.set_node_state(n, a, c)
 
-    windows = exact = restarts = 0
+    windows = exact = restarts = refreshes = 0
+
+    def merged_lists():
+        lists = [s.topk() for s in shards]
+        g = reduce.gather([np.stack([ts, ti.astype(np.float64)]) for _, ts, ti in lists])
+        ts, ti = merge_topk([x[0] for x in g], [x[1].astype(np.uint64) for x in g], k)
+        return lists[0][0], ts, ti
     generic = any(s.generic for s in shards)
     try:
         if generic:
@@ -543,10 +549,10 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
                 gs.set_witness(mx, wit[:6], wit[6:])
                 nxt = gs.resolve()
                 windows += 1
-                if nxt < wn:  # the uncertified pod opens the next window
+                if nxt < wn:  # the uncertified pod opens the next window (yoda_greedy's rule)
                     restarts += 1
                     ws += nxt
-                    Wc = min(W, max(64, 1 << int(2 * max(nxt, 1) - 1).bit_length()))
+                    Wc = next_window(nxt, W)
                 else:
                     ws += wn
                     Wc = min(W, 2 * Wc)
@@ -557,14 +563,27 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
             for s in shards:
                 s.upload_pods(win)
             merge_phase1(reduce, [s.phase1() for s in shards])
-            lists = [s.topk() for s in shards]
-            g = reduce.gather([np.stack([ts, ti.astype(np.float64)]) for _, ts, ti in lists])
-            ts, ti = merge_topk([x[0] for x in g], [x[1].astype(np.uint64) for x in g], k)
-            gs.begin_window(ws, k, lists[0][0], ts, ti)
+            counts, ts, ti = merged_lists()
+            gs.begin_window(ws, k, counts, ts, ti)
+            # mid-window list refresh (yoda_greedy's): every 8 exact pods, when
+            # >= 16 of the next 256 window pods are uncertified, every shard's top-k runs again
+            # against the current state (phase 1's masks and maxima stay valid)
+            fb_since = 0
             while True:
                 i = gs.resolve()
                 if i >= wn:
                     break
+                fb_since += 1
+                if fb_since >= 8 and wn - i >= 512:
+                    fb_since = 0
+                    if gs.uncertified(i + 1, 256) >= 16:
+                        push()
+                        _, ts, ti = merged_lists()
+                        gs.refresh(i, ts, ti)
+                        refreshes += 1
+                        i = gs.resolve()
+                        if i >= wn:
+                            break
                 push()
                 cands = reduce.gather([np.array(s.best_one(i), np.float64) for s in shards])
                 bs, bn = -1.0, -1
@@ -586,6 +605,6 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
     pick, resolved, assigned = gs.picks()
     if stats is not None:
         stats.update(windows=windows, exact_pods=exact, certified_pods=resolved,
-                     restarts=restarts)
+                     restarts=restarts, refreshes=refreshes)
     gs.close()
     return pick

@@ -199,3 +199,28 @@ def test_sharded_greedy_gloo(flags, contended):
     want = _want(nodes, pods, flags)
     for rank, got in outs:
         np.testing.assert_array_equal(got, want, err_msg=f"rank {rank}")
+
+
+def test_sharded_greedy_refresh():
+    """A 1,100-pod window of a contended fleet (identical pods and nodes: each list's nodes are
+    used up by the pods before it): the driver's mid-window list refresh (yoda_gs_uncertified /
+    yoda_gs_refresh, as yoda_greedy's) runs, and the picks are still the sequential oracle's."""
+    big = 1100
+    nodes = synth.make_nodes(N, seed=5)
+    pods = synth.make_pods(big, seed=6, priorities=True)
+    for f in ("card_number", "card_count", "free_memory_sum", "total_memory_sum",
+              "alloc_memory"):
+        getattr(nodes, f)[:] = getattr(nodes, f)[0]
+    for f in ("card_free_memory", "card_total_memory", "card_clock", "card_bandwidth",
+              "card_core", "card_power", "card_healthy"):
+        getattr(nodes, f)[:] = getattr(nodes, f)[0]
+    pods.has_number[:], pods.number[:] = 1, 1
+    pods.has_memory[:], pods.memory[:] = 1, 300
+    pods.has_clock[:] = 0
+    nodes, pods = nodes.normalized(), pods.normalized()
+    b = shard_bounds(N, 2)
+    shards = [OracleShard(nodes, int(b[r]), int(b[r + 1])) for r in range(2)]
+    stats = {}
+    got = sharded_greedy(shards, Reducer(local=True), nodes, pods, 0, 4096, stats)
+    np.testing.assert_array_equal(got, _want(nodes, pods, 0))
+    assert stats["refreshes"] > 0 and stats["exact_pods"] > 0, stats
