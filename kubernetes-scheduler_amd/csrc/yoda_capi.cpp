@@ -122,6 +122,8 @@ hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32
                              uint32_t sum2_stride, const PermCopy& pc, hipStream_t s);
 hipError_t launch_bsum_cn(const unsigned char* sum, uint32_t sum_stride, uint32_t n_nodes,
                           uint32_t* bsum, uint32_t bsw, hipStream_t s);
+hipError_t launch_block_ub(int K, const uint32_t* sum2, const uint32_t* tab, uint32_t n_nodes,
+                           uint32_t* out, hipStream_t s);
 hipError_t launch_gtable(int K, const uint32_t* sum2, const uint32_t* mix, uint32_t n_nodes,
                          const uint64_t* g_max,
                          uint32_t* tab, uint32_t* rcp_out, MemTab mt, hipStream_t s);
@@ -337,6 +339,9 @@ struct yoda_handle {
   DevBuf blksum, blksum_p;
   bool blksum_loose = false;
   bool greedy_active = false;  // inside a greedy batch (its pushes keep the bounds valid)
+  // K2 block bounds (yoda_layout.h kbub_*) of both orders; dirty: static scores changed since
+  DevBuf kbub, kbub_p;
+  bool kbub_dirty = true;
   PermCopy perm_copy() const {
     PermCopy pc;
     if (perm_on) {
@@ -470,7 +475,7 @@ struct yoda_handle {
   ~yoda_handle() {
     if (comm && rccl().ok) (void)rccl().comm_destroy(comm);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &k1sum_p,   &k2sum_p,   &gtab_p, &blksum, &blksum_p,    &perm_ids,  &perm_inv,    &pod_blob,   &maxima,       &counts,
+    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &k1sum_p,   &k2sum_p,   &gtab_p, &blksum, &blksum_p, &kbub, &kbub_p,    &perm_ids,  &perm_inv,    &pod_blob,   &maxima,       &counts,
                      &pod_sorted, &perm,     &order_scratch, &order_meta, &order_hist,
                      &order_bstart, &order_slot, &order_bkt,
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
@@ -747,10 +752,13 @@ PodParams pod_params(yoda_t* h) {
   pp.one_model = h->path == Path::N32 && h->all_one_model;
   pp.all_uni4 = h->path == Path::N32 && h->all_uni4;
   if (h->path == Path::N32 && h->has_k1sum && h->blksum.p) pp.bsum = h->blksum.as<uint32_t>();
+  const bool ub_ok = h->path == Path::N32 && pp.g.tab && !h->kbub_dirty && h->kbub.p;
+  if (ub_ok) pp.kbub = h->kbub.as<uint32_t>();
   if (h->perm_run()) {
     pp.ids = h->perm_ids.as<uint32_t>();
     if (pp.g.tab) pp.g.tab = h->gtab_p.as<uint32_t>();
     pp.bsum = h->blksum_p.p ? h->blksum_p.as<uint32_t>() : nullptr;
+    pp.kbub = ub_ok && h->kbub_p.p ? h->kbub_p.as<uint32_t>() : nullptr;
   }
   pp.mt = h->mem_ranks ? h->mt : MemTab{};
   return pp;
@@ -992,6 +1000,25 @@ int ensure_diskio_classes(yoda_t* h) {
   return YODA_OK;
 }
 
+// The K2 block bounds of both orders from the current K2 summaries and G tables.
+hipError_t build_block_ub(yoda_t* h) {
+  hipError_t e = hipSuccess;
+  if (!(h->path == Path::N32 && h->has_k2sum && h->gtab.p)) return e;
+  const size_t bytes = (size_t)std::max<uint32_t>((h->n_nodes + 63) / 64, 1) * kbub_stride(h->K);
+  e = h->kbub.ensure(bytes);
+  if (e == hipSuccess)
+    e = launch_block_ub(h->K, h->k2sum.as<uint32_t>(), h->gtab.as<uint32_t>(), h->n_nodes,
+                        h->kbub.as<uint32_t>(), h->stream);
+  if (e == hipSuccess && h->perm_on) {
+    e = h->kbub_p.ensure(bytes);
+    if (e == hipSuccess)
+      e = launch_block_ub(h->K, h->k2sum_p.as<uint32_t>(), h->gtab_p.as<uint32_t>(), h->n_nodes,
+                          h->kbub_p.as<uint32_t>(), h->stream);
+  }
+  if (e == hipSuccess) h->kbub_dirty = false;
+  return e;
+}
+
 // Inside a greedy batch: its node-state pushes leave the block summaries' bounds valid (the
 // atomics of k_set_static), so its windows do not tighten them; the next private run does.
 struct GreedyScope {
@@ -1169,6 +1196,9 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
                                best, idx, ties, low, h->stream));
     return YODA_OK;
   }
+  if (mode == YODA_MODE_SCV && !rows && h->kbub_dirty && h->path == Path::N32 && h->has_k2sum &&
+      h->g.tab)
+    HIP_TRY(h, build_block_ub(h));
   if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
   if (mode == YODA_MODE_DISKIO) {
     HIP_TRY(h, launch_k2_diskio(h->nodes_b.as<NodeRecB>(), h->n_nodes, h->chunk2, h->C2,
@@ -1947,6 +1977,8 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     }
     h->generic = path == Path::U64;
     h->mem_ranks = ranks;
+    h->kbub_dirty = true;
+    if (h->has_k2sum && h->g.tab && N > 0) HIP_TRY(h, build_block_ub(h));
     if (!ranks) h->mt = MemTab{};
     h->h_frees.swap(frees);
     h->has_nodes = true;
@@ -2621,7 +2653,7 @@ int yoda_class_stats_enable(yoda_t* h, int enable) {
 
 int yoda_class_stats_read(yoda_t* h, uint64_t* out) {
   if (!h || !out) return YODA_ERR_INVALID_ARG;
-  for (int i = 0; i < 16; ++i) out[i] = 0;
+  for (int i = 0; i < 18; ++i) out[i] = 0;
   if (!h->stats_dev.p) return YODA_OK;
   HIP_TRY(h, hipSetDevice(h->device));
   uint64_t d[16] = {};
@@ -2643,6 +2675,8 @@ int yoda_class_stats_read(yoda_t* h, uint64_t* out) {
   out[13] = d[10];                                                 // K1 (w, block)s all NONE
   out[14] = d[11];                                                 // K1 (w, block)s all ALL
   out[15] = d[12];                                                 // K1 (w, block)s
+  out[16] = d[13];                                                 // K2 (w, block)s pruned
+  out[17] = d[14];                                                 // K2 (w, block)s worked
   HIP_TRY(h, hipMemsetAsync(h->stats_dev.p, 0, 15 * 8, h->stream));
   h->stats_pairs1 = h->stats_pairs2 = 0;
   return YODA_OK;
@@ -2739,6 +2773,7 @@ struct GreedyState {
     const unsigned char* d = static_cast<const unsigned char*>(h->upd_stage.dp);
     const uint32_t stride = h->path == Path::N32 ? n32_stride(h->K) : node_stride(h->K);
     h->blksum_loose = true;  // (the atomics keep the block bounds valid, not tight)
+    h->kbub_dirty = true;     // (static scores change: the K2 block bounds are rebuilt)
     HIP_TRY(h, launch_set_static(h->nodes.as<unsigned char>(), stride,
                                  reinterpret_cast<const uint32_t*>(d),
                                  reinterpret_cast<const uint64_t*>(d + o_val),
@@ -3241,6 +3276,7 @@ int push_node_state(yoda_t* h, const std::vector<uint32_t>& loc, const std::vect
   unsigned char* d = h->upd_node.as<unsigned char>();
   const uint32_t stride = h->path == Path::N32 ? n32_stride(h->K) : node_stride(h->K);
   h->blksum_loose = true;  // (the atomics keep the block bounds valid, not tight)
+  h->kbub_dirty = true;     // (static scores change: the K2 block bounds are rebuilt)
   HIP_TRY(h, launch_set_static(h->nodes.as<unsigned char>(), stride,
                                reinterpret_cast<const uint32_t*>(d),
                                reinterpret_cast<const uint64_t*>(d + o_val),

@@ -1474,6 +1474,58 @@ __global__ __launch_bounds__(kBlock) void k_gtable(const uint32_t* __restrict__ 
   }
 }
 
+// K2 block bounds (yoda_layout.h kbub_*): one wave per 64-node block, lane = node.
+template <int K>
+__global__ __launch_bounds__(kWave) void k_block_ub(const uint32_t* __restrict__ sum2,
+                                                    const uint32_t* __restrict__ tab,
+                                                    uint32_t n_nodes, uint32_t* __restrict__ out) {
+  constexpr uint32_t S2 = k2sum_stride(K), GS = gtab_stride(K), BW = kbub_stride(K) / 4u;
+  const uint32_t b = blockIdx.x, n = b * 64u + threadIdx.x;
+  const bool v = n < n_nodes;
+  uint32_t* o = out + (size_t)b * BW;
+  double stat = -1.0;
+  uint32_t cnt = 0;
+  if (v) {
+    stat = __longlong_as_double((long long)((uint64_t)sum2[sum_index(n, kS2Static, S2)] |
+                                            ((uint64_t)sum2[sum_index(n, kS2Static + 1, S2)] << 32)));
+    cnt = (sum2[sum_index(n, kS2Meta, S2)] >> 8) & 0xffu;
+  }
+  uint32_t bq = 0;  // B_G[min(j, cnt)], j ascending
+#pragma unroll
+  for (int j = 0; j <= K; ++j) {
+    if (j > 0 && v && (uint32_t)j <= cnt) bq = tab[sum_index(n, (uint32_t)j - 1u, GS)];
+    double u = v ? stat + (double)bq : -1.0;  // exact: integers below 2^53
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) u = fmax(u, __shfl_xor(u, off, kWave));
+    if (threadIdx.x == 0) {
+      const uint64_t ub = (uint64_t)__double_as_longlong(u);
+      o[2 * j] = (uint32_t)ub;
+      o[2 * j + 1] = (uint32_t)(ub >> 32);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint32_t f = v ? sum2[sum_index(n, kS2Fs + (uint32_t)k, S2)] : 0u;
+    const uint32_t fm = wave_max_u32(f);
+    if (threadIdx.x == 0) o[kbub_fmax(K) + k] = fm;
+  }
+}
+
+hipError_t launch_block_ub(int K, const uint32_t* sum2, const uint32_t* tab, uint32_t n_nodes,
+                           uint32_t* out, hipStream_t s) {
+  if (n_nodes == 0) return hipSuccess;
+  const dim3 grid((n_nodes + 63) / 64);
+  switch (K) {
+    case 1: hipLaunchKernelGGL(k_block_ub<1>, grid, dim3(kWave), 0, s, sum2, tab, n_nodes, out); break;
+    case 2: hipLaunchKernelGGL(k_block_ub<2>, grid, dim3(kWave), 0, s, sum2, tab, n_nodes, out); break;
+    case 4: hipLaunchKernelGGL(k_block_ub<4>, grid, dim3(kWave), 0, s, sum2, tab, n_nodes, out); break;
+    case 8: hipLaunchKernelGGL(k_block_ub<8>, grid, dim3(kWave), 0, s, sum2, tab, n_nodes, out); break;
+    case 16: hipLaunchKernelGGL(k_block_ub<16>, grid, dim3(kWave), 0, s, sum2, tab, n_nodes, out); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_gtable(int K, const uint32_t* sum2, const uint32_t* mix, uint32_t n_nodes,
                          const uint64_t* g_max, uint32_t* tab, uint32_t* rcp_out, MemTab mt,
                          hipStream_t s) {
@@ -1505,6 +1557,7 @@ struct ScoreArgs {
   const uint32_t* mix = nullptr;  // per-card models in free order (yoda_layout.h MixWord)
   MemTab mt = {};                 // memory ranks (yoda_layout.h MemTab)
   const uint32_t* ids = nullptr;  // block-grouped node order: the local id of each position
+  const uint32_t* kbub = nullptr; // K2 block bounds (yoda_layout.h kbub_*): argmax pruning
 };
 
 template <Path P>
@@ -1885,6 +1938,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
                      u_free == args.g.r_free && u_tot == args.g.r_tot;
   const uint32_t m_max = wave_max_u32(act ? sc.m : 0u), m_min = wave_min_u32(act ? sc.m : ~0u);
   const uint32_t c_max = wave_max_u32(act ? sc.c : 0u), c_min = wave_min_u32(act ? sc.c : ~0u);
+  // Block pruning (argmax, G waves): a block whose bound -- the most any node of it can score
+  // for a pod with at most J qualifying cards, J from the block's largest frees and the wave's
+  // smallest scv/memory (kbub_*) -- is below every active lane's best so far cannot hold a
+  // pick or a tie of any of them.  thr: the min over active lanes of that best, refreshed
+  // after each block the wave works on (it only grows, so a stale value stays a lower bound).
+  const bool prune = !TOPK && args.kbub != nullptr && use_g;
+  constexpr uint32_t KBW = kbub_stride(K) / 4u;
+  double thr = -1.0;
 
   double ubest = -1.0;                      // node lane (U nodes)
   uint32_t uidx = 0xffffffffu, uties = 0;
@@ -1913,7 +1974,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   };
   // One block: the wave's mask of node nb + lane and its summary (kept for the per-pod pass,
   // read back with v_readlane), loaded together: one memory latency per block.
+  bool worked = false;  // the last block() call did the block's work (not pruned / empty)
   auto block = [&](uint32_t nb) {
+    worked = false;
+    if (prune) {
+      const uint32_t* U = args.kbub + (size_t)(nb >> 6) * KBW;
+      uint32_t J = 0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) J += U[kbub_fmax(K) + (uint32_t)k] >= m_min ? 1u : 0u;
+      const double ub =
+          __longlong_as_double((long long)((uint64_t)U[2 * J] | ((uint64_t)U[2 * J + 1] << 32)));
+      if (ub < thr) {
+        if (STATS && !trace && lane == 0) atomicAdd(stats + 13, 1ull);
+        return;
+      }
+    }
     const uint32_t n = nb + lane;
     const bool valid0 = n < n1;
     const uint32_t nid = (args.ids && valid0) ? args.ids[n] : n;
@@ -1952,6 +2027,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       for (int t = 0; t < K; ++t) ts.v[t] = s[64 * (kS2Fs + K + t)];
     }
     if (feas_b == 0) return;  // no pod of the wave can use any node of the block
+    worked = true;
+    if (STATS && !trace && lane == 0) atomicAdd(stats + 14, 1ull);
     uint64_t fast_b = 0, u_b = 0, rec_b = 0;
     // the clock the per-pod passes compare with the pods' scv/clock (algorithm.go:271): the
     // node's one model, or ~0 for a mixed-model node whose clock test is folded into its row
@@ -2323,6 +2400,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         const uint32_t j = (uint32_t)__builtin_ctzll(bits);
         bits &= bits - 1;
         block((base + j) << 6);
+        if (prune && worked) {  // every active lane's best so far: its nodes', the U nodes'
+          double wu = ubest;
+#pragma unroll
+          for (int o = kWave / 2; o > 0; o >>= 1) wu = fmax(wu, __shfl_xor(wu, o, kWave));
+          double lb = act ? fmax(rties > 0u ? (double)rbest : -1.0, wu) : HUGE_VAL;
+#pragma unroll
+          for (int o = kWave / 2; o > 0; o >>= 1) lb = fmin(lb, __shfl_xor(lb, o, kWave));
+          thr = __longlong_as_double((long long)uniform_u64((uint64_t)__double_as_longlong(lb)));
+        }
       }
     }
   } else {
@@ -3930,7 +4016,7 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
                               unsigned long long* stats, const uint32_t* counts, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g, pp.mix, pp.mt,
-                    pp.ids};
+                    pp.ids, OUT == OUT_ARGMAX ? pp.kbub : nullptr};
   const MaskSrc ms{bm, bs, bm_stride, bs_stride};
   switch (path) {
     case Path::N32:

@@ -138,6 +138,20 @@ __host__ __device__ constexpr uint32_t bsum_stride(int k) {
   return 4u * ((kBsT + 2u * (uint32_t)k + 3u) & ~3u);
 }
 
+// K2 block bounds (N32 path; waves whose reciprocals are the G table's): per 64-node block of a
+// summary order, u32 words (kbub_stride(K) bytes a block):
+//   ub[j]    (f64, words 2j, 2j + 1; j = 0..K)  the max over the block's real nodes of
+//            static + B_G[min(j, len(CardList))] -- no pod with at most j qualifying cards on
+//            every node of the block scores more there (basic <= B_G[nq], nq <= j)
+//   fmax[k]  (u32, from word 2K + 2; k < K)  the max over the nodes of fs[k] (K2 summary): a
+//            pod with scv/memory m qualifies at most #{k : fmax[k] >= m} cards on any of them
+// Built from the K2 summaries and the G table on the device (k_block_ub), again whenever the
+// static scores changed (k_set_static).
+__host__ __device__ constexpr uint32_t kbub_fmax(int k) { return 2u * (uint32_t)k + 2u; }
+__host__ __device__ constexpr uint32_t kbub_stride(int k) {
+  return (4u * (kbub_fmax(k) + (uint32_t)k) + 15u) & ~15u;
+}
+
 // Per-card GPU models of every node (N32 path), in the K2 summary's descending-free card order,
 // read with lane = node by the block kernels for the nodes whose cards are not all one model
 // (no kSumUni4): u32 words
@@ -326,6 +340,8 @@ struct PodParams {
   MemTab mt = {};
   // 64-node block summaries of the order the run visits (BlockSumWord; nullptr: none)
   const uint32_t* bsum = nullptr;
+  // K2 block bounds of that order (kbub_stride; nullptr: none -- the argmax K2 prunes with them)
+  const uint32_t* kbub = nullptr;
 };
 
 // Per-pod state produced between kernels (length P each unless noted).

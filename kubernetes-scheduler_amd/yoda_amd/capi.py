@@ -347,7 +347,7 @@ class Yoda:
             self._check(lib().yoda_class_stats_enable(self._h, 1 if enable else 0),
                         "yoda_class_stats_enable")
             return None
-        out = np.zeros(16, np.uint64)
+        out = np.zeros(18, np.uint64)
         self._check(lib().yoda_class_stats_read(self._h, _np_ptr(out)), "yoda_class_stats_read")
         v = [int(x) for x in out]
         pairs = max(v[9], 1)
@@ -359,6 +359,7 @@ class Yoda:
                 "k2_max_per_pod_nodes_wave_chunk": v[12],
                 "k1_blocks": {"none": v[13] / max(v[15], 1), "all": v[14] / max(v[15], 1),
                               "n": v[15]},
+                "k2_blocks": {"pruned": v[16], "worked": v[17]},
                 "wave_node_pairs": v[9]}
 
     def k2_trace(self, n_slots: int) -> np.ndarray:
