@@ -314,7 +314,7 @@ def row_latency(dev_index: int, node_counts=(5000, 100000), cycles: int = 60) ->
         dicts = pods_to_dicts(pods)
         for d in dicts[:3]:
             plugin.pre_filter(CycleState(), d)
-        t_plugin, t_abi = [], []
+        t_plugin, t_abi, t_b = [], [], []
         for p, d in enumerate(dicts):
             t0 = time.perf_counter()
             plugin.pre_filter(CycleState(), d)
@@ -324,10 +324,16 @@ def row_latency(dev_index: int, node_counts=(5000, 100000), cycles: int = 60) ->
             z.upload_pods(one)
             z.score_rows(MODE_SCV)
             t_abi.append((time.perf_counter() - t0) * 1e3)
+            # Mode B (BalancedCpuDiskIOPriority, what the shipped binary scores per cycle)
+            t0 = time.perf_counter()
+            z.upload_pods(one)
+            z.score_rows(MODE_DISKIO)
+            t_b.append((time.perf_counter() - t0) * 1e3)
         z.close()
         q = lambda v, x: float(np.percentile(v, x))  # noqa: E731
         out[str(n)] = {"prefilter_ms_p50": q(t_plugin, 50), "prefilter_ms_p99": q(t_plugin, 99),
                        "capi_ms_p50": q(t_abi, 50), "capi_ms_p99": q(t_abi, 99),
+                       "capi_diskio_ms_p50": q(t_b, 50), "capi_diskio_ms_p99": q(t_b, 99),
                        "cycles": cycles}
     return out
 

@@ -51,6 +51,8 @@ hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigne
                      const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
                      uint32_t bs_stride, const Partials& part, int64_t* rows,
                      unsigned long long* stats, const uint32_t* counts, hipStream_t s);
+hipError_t launch_k2b_rows(const NodeRecB* nodes, uint32_t n_nodes, const PodParams& pp,
+                           uint32_t n_pods, const Partials& part, int64_t* rows, hipStream_t s);
 hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
                             uint32_t C, const PodParams& pp, uint32_t n_pods, const Partials& part,
                             int64_t* rows, hipStream_t s);
@@ -1200,9 +1202,18 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
       h->g.tab)
     HIP_TRY(h, build_block_ub(h));
   if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
+  uint32_t C2 = h->C2;
   if (mode == YODA_MODE_DISKIO) {
-    HIP_TRY(h, launch_k2_diskio(h->nodes_b.as<NodeRecB>(), h->n_nodes, h->chunk2, h->C2,
-                                pod_params(h), P, part, rows, h->stream));
+    // score rows (the plugin's row per cycle, small P): lane = node over 256-node chunks
+    C2 = (h->n_nodes + kBlock - 1) / kBlock;
+    const size_t cp = (size_t)C2 * P;
+    HIP_TRY(h, h->p_best_f.ensure(cp * 8));
+    HIP_TRY(h, h->p_low_f.ensure(cp * 8));
+    HIP_TRY(h, h->p_idx.ensure(cp * 4));
+    HIP_TRY(h, h->p_ties.ensure(cp * 4));
+    part = partials(h);
+    HIP_TRY(h, launch_k2b_rows(h->nodes_b.as<NodeRecB>(), h->n_nodes, pod_params(h), P, part,
+                               rows, h->stream));
   } else {
     HIP_TRY(h, launch_k2(h->K, h->path, h->nodes.as<unsigned char>(),
                          h->has_k2sum ? (h->perm_run() ? h->k2sum_p : h->k2sum)
@@ -1226,7 +1237,7 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
   // merge reports each pod's best in their place
   Partials pr = part;
   if (mode == YODA_MODE_SCV && h->path == Path::N32 && h->has_k2sum && !rows) pr.low_f = nullptr;
-  HIP_TRY(h, launch_reduce2(pr, h->C2, P, is_f64, h->node_offset, best, idx, ties, low,
+  HIP_TRY(h, launch_reduce2(pr, C2, P, is_f64, h->node_offset, best, idx, ties, low,
                             h->stream));
   return YODA_OK;
 }

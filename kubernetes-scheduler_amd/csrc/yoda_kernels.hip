@@ -3252,6 +3252,73 @@ __global__ __launch_bounds__(kBlock) void k2_diskio(const NodeRecB* __restrict__
   plow[o] = low;
 }
 
+// K2B score rows (yoda_score_rows in Mode B, the plugin's per-cycle row): lane = node, one
+// 256-node chunk per workgroup, the pods of the (small) batch in turn -- every lane busy and
+// the row stores coalesced at P = 1, where the lane = pod kernel above runs one lane of 64.
+// Per pod the chunk's (best, lowest node, ties, lowest score) as k2_diskio's partials.
+__global__ __launch_bounds__(kBlock) void k2b_rows(const NodeRecB* __restrict__ nodes,
+                                                   uint32_t n_nodes,
+                                                   const double* __restrict__ alpha_in,
+                                                   const double* __restrict__ beta_in,
+                                                   uint32_t n_pods, double* __restrict__ pbest,
+                                                   uint32_t* __restrict__ pidx,
+                                                   uint32_t* __restrict__ pties,
+                                                   double* __restrict__ plow,
+                                                   int64_t* __restrict__ rows) {
+#pragma clang fp contract(off)
+  __shared__ double s_best[kBlock / kWave], s_low[kBlock / kWave];
+  __shared__ uint32_t s_idx[kBlock / kWave], s_ties[kBlock / kWave];
+  const uint32_t c = blockIdx.x, n = c * kBlock + threadIdx.x, w = threadIdx.x >> 6;
+  const bool v = n < n_nodes;
+  const NodeRecB r = v ? nodes[n] : NodeRecB{0.0, 0.0};
+  for (uint32_t p = 0; p < n_pods; ++p) {
+    const double alpha = alpha_in[p], beta = beta_in[p];
+    const double a = alpha * r.v;
+    const double b = beta * r.u;
+    const double l = fabs(a - b);  // algorithm.go:110
+    const double t = 10.0 * l;
+    const double sc = 10.0 - t;    // :111
+    // uint64(Si) on amd64 then Uint64ToInt64: trunc for Si >= 1, else 0 (NaN, negatives)
+    const double score = (sc >= 1.0) ? __builtin_trunc(sc) : 0.0;
+    if (v) rows[(size_t)n * n_pods + p] = (int64_t)score;
+    double best = v ? score : -1.0, low = v ? score : 1.0e300;
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      best = fmax(best, __shfl_xor(best, o, kWave));
+      low = fmin(low, __shfl_xor(low, o, kWave));
+    }
+    const bool at = v && score == best;
+    const uint64_t bb = ballot(at);
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+      s_best[w] = best;
+      s_low[w] = low;
+      s_idx[w] = bb ? (c * kBlock + w * kWave + (uint32_t)__builtin_ctzll(bb)) : 0xffffffffu;
+      s_ties[w] = (uint32_t)__builtin_popcountll(bb);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double B = -1.0, L = 1.0e300;
+      uint32_t I = 0xffffffffu, T = 0;
+      for (int k = 0; k < kBlock / kWave; ++k) {  // waves in node order: strict '>' keeps lowest
+        if (s_best[k] > B) {
+          B = s_best[k];
+          I = s_idx[k];
+          T = s_ties[k];
+        } else if (s_best[k] == B && s_ties[k]) {
+          T += s_ties[k];
+        }
+        L = fmin(L, s_low[k]);
+      }
+      const size_t o = (size_t)c * n_pods + p;
+      pbest[o] = B;
+      pidx[o] = I;
+      pties[o] = T;
+      plow[o] = L;
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // K2B batch path (Mode B): the same score over pod CLASSES -- the distinct
 // (alpha, beta) bit pairs of the batch (algorithm.go:105-106).  Pods of one class score every
@@ -4249,6 +4316,15 @@ hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigne
   return launch_k2_t<OUT_ARGMAX>(K, path, nodes, sum2, blk, blk_stride, n_nodes, chunk_nodes, C, pp, maxima, rcp,
                                  rcp32, n_pods, bm, bm_stride, bs, bs_stride, part, rows, nullptr,
                                  nullptr, stats, counts, s);
+}
+
+hipError_t launch_k2b_rows(const NodeRecB* nodes, uint32_t n_nodes, const PodParams& pp,
+                           uint32_t n_pods, const Partials& part, int64_t* rows, hipStream_t s) {
+  if (n_nodes == 0 || n_pods == 0) return hipSuccess;
+  hipLaunchKernelGGL(k2b_rows, dim3((n_nodes + kBlock - 1) / kBlock), dim3(kBlock), 0, s, nodes,
+                     n_nodes, pp.alpha, pp.beta, n_pods, part.best_f, part.idx, part.ties,
+                     part.low_f, rows);
+  return hipGetLastError();
 }
 
 hipError_t launch_k2_diskio(const NodeRecB* nodes, uint32_t n_nodes, uint32_t chunk_nodes,
