@@ -311,8 +311,9 @@ int yoda_profile_read(yoda_t* h, double* k1_ms, double* k2_ms, uint32_t* n_launc
  * read: {K1 ALL, K1 NONE, K1 PART, K2 U, K2 FAST, K2 EXACT, K2 skipped,
  * K2 (wave, chunk)s with uniform maxima, K2 (wave, chunk)s, (wave, node) pairs,
  * K2 FAST pairs served by node records, K2 per-pod pairs of non-uniform waves,
- * the most per-pod nodes of one (wave, chunk), K1 (wave, 64-node block)s whose every node is
- * NONE, ... every node ALL, K1 (wave, block)s, K2 (wave, block)s pruned by their bound,
+ * the most per-pod nodes of one (wave, chunk), K1 (wave, 64-node block)s the block summaries
+ * decide NONE, ... decide ALL, K1 (wave, block)s classified node by node, K2 (wave, block)s
+ * pruned by their bound,
  * K2 (wave, block)s worked on}: out[18]; resets them. */
 int yoda_class_stats_enable(yoda_t* h, int enable);
 int yoda_class_stats_read(yoda_t* h, uint64_t* out);

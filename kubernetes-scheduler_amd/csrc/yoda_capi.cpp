@@ -1804,9 +1804,10 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
         const uint32_t SW = (uint32_t)(sstride / 4);
         auto bsums = [&](const uint32_t* order) {
           const uint32_t nb = (N + 63) / 64, BW = bsum_stride(K) / 4;
-          std::vector<uint32_t> b((size_t)std::max<uint32_t>(nb, 1) * BW, 0u);
+          std::vector<uint32_t> b(sum_words(std::max<uint32_t>(nb, 1), bsum_stride(K)), 0u);
+          std::vector<uint32_t> o(BW);
           for (uint32_t blk = 0; blk < nb; ++blk) {
-            uint32_t* o = b.data() + (size_t)blk * BW;
+            std::fill(o.begin(), o.end(), 0u);
             uint64_t cmin = ~0ull, cmax = 0;
             uint32_t fl = kBsOneModel | kBsUni4, ckmin = ~0u, ckmax = 0, hmin = ~0u, hmax = 0;
             uint32_t nhmin = ~0u, nhmax = 0, mrmin = ~0u, mrmax = 0, nreal = 0, nzt = 0;
@@ -1852,8 +1853,8 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
               }
             }
             if (nreal == 0) continue;
-            std::memcpy(o + kBsCnMin, &cmin, 8);
-            std::memcpy(o + kBsCnMax, &cmax, 8);
+            o[kBsCnMin] = (uint32_t)std::min<uint64_t>(cmin, 0xffffffffull);
+            o[kBsCnMax] = (uint32_t)std::min<uint64_t>(cmax, 0xffffffffull);
             o[kBsFlags] = fl;
             o[kBsCkMin] = ckmin;
             o[kBsCkMax] = ckmax;
@@ -1874,6 +1875,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
               o[kBsT + t] = tmin[t];
               o[kBsT + K + t] = tmax[t];
             }
+            for (uint32_t w = 0; w < BW; ++w) b[sum_index(blk, w, bsum_stride(K))] = o[w];
           }
           return b;
         };

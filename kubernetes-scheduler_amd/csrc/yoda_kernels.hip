@@ -710,78 +710,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   // of the block's nodes against the wave's bounds prove every node NONE, or every node ALL
   // with one contribution (all qualifying: the block's maxima; none qualifying: nothing).
   // Sufficient conditions of the per-node tests below, so the outcome is the same.
-  constexpr uint32_t BSW = bsum_stride(K) / 4u;
+  constexpr uint32_t BST = bsum_stride(K);
   const uint32_t s_mpm_max = uniform_u32(mpm_max), s_mpm_min = uniform_u32(mpm_min);
   const uint32_t s_m_max = uniform_u32(m_max), s_m_min = uniform_u32(m_min);
   const uint32_t s_c_max = uniform_u32(c_max), s_c_min = uniform_u32(c_min);
   const uint32_t bs_tn = kBsT + (uint32_t)K + (hfs_none_ok && nm_min > 0u ? nm_min - 1u : 0u);
   const uint32_t bs_ta = kBsT + (any_pm && hfs_all_ok && nm_max > 0u ? nm_max - 1u : 0u);
-  for (uint32_t nb = n0; nb < n1; nb += kWave) {
-    if (bsm != nullptr) {
-      const uint32_t* B = bsm + (size_t)(nb >> 6) * BSW;
-      const uint64_t bcn_min = (uint64_t)B[kBsCnMin] | ((uint64_t)B[kBsCnMin + 1] << 32);
-      const uint64_t bcn_max = (uint64_t)B[kBsCnMax] | ((uint64_t)B[kBsCnMax + 1] << 32);
-      const uint32_t bfl = B[kBsFlags], ckmin = B[kBsCkMin], ckmax = B[kBsCkMax];
-      const uint32_t nreal = B[kBsNReal];
-      // every node NONE: PodFitsNumber, PodFitsMemory or PodFitsClock fails on all of them
-      bool bnone = num_min > bcn_max;
-      bnone = bnone || (all_pm && (!hfs_none_ok || B[bs_tn] <= s_mpm_min));
-      if (all_pc && c_uni) {
-        // no healthy card of the block has the wave's clock (hc = 0 < need), or one-model
-        // nodes of that clock with too few healthy cards
-        bnone = bnone || cpc_max < B[kBsHckMin] || cpc_max > B[kBsHckMax] ||
-                ((bfl & kBsUni4) && ckmin == ckmax && ckmin == cpc_max && B[kBsNhMax] < nc_min);
-      }
-      // every node ALL: feasible for every pod, one-model, and all or none qualifying
-      bool ball = (bfl & kBsOneModel) && num_max <= bcn_min;
-      ball = ball && (!any_pm || (hfs_all_ok && B[bs_ta] > s_mpm_max));
-      ball = ball && (!any_pc || (c_uni && ckmin == ckmax && ckmin == cpc_max &&
-                                  B[kBsNhMin] >= nc_max));
-      const bool allq = ckmin >= s_c_max && B[kBsMrfMin] > s_m_max;
-      const bool noq = ckmax < s_c_min || B[kBsMrfMax] <= s_m_min;
-      ball = ball && (allq || noq) && !bnone;
-      if (bnone || ball) {
-        const uint64_t vb = nreal >= 64u ? ~0ull : ((1ull << nreal) - 1ull);
-        if (STATS && !trace && lane == 0) {
-          atomicAdd(stats + (ball ? 0 : 1), (unsigned long long)nreal);
-          atomicAdd(stats + (ball ? 11 : 10), 1ull);
-          atomicAdd(stats + 12, 1ull);
-        }
-        if (lane == 0) bsw[nb >> 6] = ball ? BlockMask{vb, vb} : BlockMask{0ull, 0ull};
-        if (bnone) continue;
-        nf_all += nreal;
-        nz_all += B[kBsNzt];
-        if (allq) {
-          if constexpr (WIT) {  // one lane folds the block's witnesses (the reduce sums lanes)
-            if (lane == 0) {
-#pragma unroll
-              for (int f = 0; f < 6; ++f) {
-                const uint32_t v = B[kBsMx + f], cnt = B[kBsWc + f], low = nb + B[kBsWl + f];
-                const bool gt = v > aw[f], eq = v == aw[f];
-                ac[f] = gt ? cnt : ac[f] + (eq ? cnt : 0u);
-                al[f] = gt ? low : (eq ? min(al[f], low) : al[f]);
-                aw[f] = gt ? v : aw[f];
-              }
-            }
-          } else {
-            a_bw = max(a_bw, B[kBsMx + kMaxBw]);
-            a_ck = max(a_ck, B[kBsMx + kMaxClock]);
-            a_core = max(a_core, B[kBsMx + kMaxCore]);
-            a_free = max(a_free, B[kBsMx + kMaxFree]);
-            a_pw = max(a_pw, B[kBsMx + kMaxPower]);
-            a_tot = max(a_tot, B[kBsMx + kMaxTotal]);
-          }
-        }
-        const uint32_t bi = nb >> 6;
-        if ((bi >> 6) != blk_wi) {
-          blk_flush();
-          blk_wi = bi >> 6;
-          blk_bits = 0;
-        }
-        blk_bits |= 1ull << (bi & 63u);
-        continue;
-      }
-    }
+  // per-node classification of one 64-node block (below: only the blocks the block summaries
+  // leave undecided)
+  auto node_block = [&](uint32_t nb) {
     const uint32_t n = nb + lane;
     const bool valid = n < n1;
     // this block's tile of summaries (nb is a multiple of 64): word w at s[64 w]
@@ -928,12 +865,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     const uint64_t all_b = ballot(is_all), none_b = ballot(is_none);
     uint64_t part_b = ballot(valid) & ~all_b & ~none_b;
     if (STATS && !trace) {  // class counts of (wave, node) pairs: ALL, NONE; whole blocks
-      const uint64_t vb = ballot(valid);
       if (lane == 0) {
         atomicAdd(stats + 0, (unsigned long long)__builtin_popcountll(all_b));
         atomicAdd(stats + 1, (unsigned long long)__builtin_popcountll(none_b));
-        atomicAdd(stats + 10, none_b == vb ? 1ull : 0ull);
-        atomicAdd(stats + 11, all_b == vb ? 1ull : 0ull);
         atomicAdd(stats + 12, 1ull);
       }
     }
@@ -1064,7 +998,115 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
       }
       blk_bits |= 1ull << (bi & 63u);
     }
+  };
+  // ALL blocks' counts, lane = block (summed across the wave at the end)
+  uint32_t g_nf = 0, g_nz = 0;
+  if (bsm != nullptr) {
+    // Whole-block decisions from the block summaries (BlockSumWord), 64 blocks at a time,
+    // lane = block: the bounds of a block's nodes against the wave's bounds prove every node
+    // NONE, or every node ALL with one contribution (all qualifying: the block's maxima; none
+    // qualifying: nothing).  Sufficient conditions of node_block's per-node tests, so the
+    // outcome is the same; the undecided blocks then take node_block.
+    const uint32_t b0 = n0 >> 6, b1 = (n1 + 63u) >> 6;
+    for (uint32_t g = b0; g < b1; g += kWave) {
+      const uint32_t bi = g + lane;
+      const bool bv = bi < b1;
+      const uint32_t* B = bsm + sum_index(bv ? bi : b0, 0, BST);  // word w at B[64 w]
+      const uint32_t fl = B[64 * kBsFlags], ckmin = B[64 * kBsCkMin], ckmax = B[64 * kBsCkMax];
+      const uint32_t cn_min = B[64 * kBsCnMin], cn_max = B[64 * kBsCnMax];
+      const uint32_t nreal = bv ? B[64 * kBsNReal] : 0u;
+      // every node NONE: PodFitsNumber, PodFitsMemory or PodFitsClock fails on all of them
+      bool bnone = cn_max != 0xffffffffu && num_min > (uint64_t)cn_max;
+      bnone = bnone || (all_pm && (!hfs_none_ok || B[64 * bs_tn] <= s_mpm_min));
+      if (all_pc && c_uni) {
+        // no healthy card of the block has the wave's clock (hc = 0 < need), or one-model
+        // nodes of that clock with too few healthy cards
+        bnone = bnone || cpc_max < B[64 * kBsHckMin] || cpc_max > B[64 * kBsHckMax] ||
+                ((fl & kBsUni4) && ckmin == ckmax && ckmin == cpc_max &&
+                 B[64 * kBsNhMax] < nc_min);
+      }
+      // every node ALL: feasible for every pod, one-model, and all or none qualifying
+      bool ball = (fl & kBsOneModel) && num_max <= (uint64_t)cn_min;
+      ball = ball && (!any_pm || (hfs_all_ok && B[64 * bs_ta] > s_mpm_max));
+      ball = ball && (!any_pc || (c_uni && ckmin == ckmax && ckmin == cpc_max &&
+                                  B[64 * kBsNhMin] >= nc_max));
+      const bool allq = ckmin >= s_c_max && B[64 * kBsMrfMin] > s_m_max;
+      const bool noq = ckmax < s_c_min || B[64 * kBsMrfMax] <= s_m_min;
+      ball = ball && (allq || noq) && !bnone;
+      bnone = bnone && bv && nreal > 0u;
+      ball = ball && bv && nreal > 0u;
+      const uint64_t none_m = ballot(bnone), all_m = ballot(ball);
+      if (bnone || ball) {
+        const uint64_t vb = nreal >= 64u ? ~0ull : ((1ull << nreal) - 1ull);
+        bsw[bi] = ball ? BlockMask{vb, vb} : BlockMask{0ull, 0ull};
+      }
+      if (ball) {
+        g_nf += nreal;
+        g_nz += B[64 * kBsNzt];
+        if (allq) {
+          if constexpr (WIT) {  // (the same rule as a node's: larger replaces, equal adds)
+#pragma unroll
+            for (int f = 0; f < 6; ++f) {
+              const uint32_t v = B[64 * (kBsMx + f)], cnt = B[64 * (kBsWc + f)];
+              const uint32_t low = (bi << 6) + B[64 * (kBsWl + f)];
+              const bool gt = v > aw[f], eq = v == aw[f];
+              ac[f] = gt ? cnt : ac[f] + (eq ? cnt : 0u);
+              al[f] = gt ? low : (eq ? min(al[f], low) : al[f]);
+              aw[f] = gt ? v : aw[f];
+            }
+          } else {
+            a_bw = max(a_bw, B[64 * (kBsMx + kMaxBw)]);
+            a_ck = max(a_ck, B[64 * (kBsMx + kMaxClock)]);
+            a_core = max(a_core, B[64 * (kBsMx + kMaxCore)]);
+            a_free = max(a_free, B[64 * (kBsMx + kMaxFree)]);
+            a_pw = max(a_pw, B[64 * (kBsMx + kMaxPower)]);
+            a_tot = max(a_tot, B[64 * (kBsMx + kMaxTotal)]);
+          }
+        }
+      }
+      if (all_m != 0ull && lane == 0) {  // blocks g .. g + 63 -> their block-list words
+        const uint32_t sh = g & 63u;
+        atomicOr(reinterpret_cast<unsigned long long*>(blkw + (g >> 6)),
+                 (unsigned long long)(all_m << sh));
+        if (sh != 0u && (all_m >> (64u - sh)) != 0ull)
+          atomicOr(reinterpret_cast<unsigned long long*>(blkw + (g >> 6) + 1),
+                   (unsigned long long)(all_m >> (64u - sh)));
+      }
+      if (STATS && !trace && lane == 0) {
+        const uint64_t bvm = ballot(bv && nreal > 0u);
+        atomicAdd(stats + 10, (unsigned long long)__builtin_popcountll(none_m));
+        atomicAdd(stats + 11, (unsigned long long)__builtin_popcountll(all_m));
+        (void)bvm;
+      }
+      if (STATS && !trace) {  // (wave, node) pairs of the decided blocks
+        uint32_t na = ball ? nreal : 0u, nn = bnone ? nreal : 0u;
+#pragma unroll
+        for (int o = kWave / 2; o > 0; o >>= 1) {
+          na += (uint32_t)__shfl_xor((int)na, o, kWave);
+          nn += (uint32_t)__shfl_xor((int)nn, o, kWave);
+        }
+        if (lane == 0) {
+          atomicAdd(stats + 0, (unsigned long long)na);
+          atomicAdd(stats + 1, (unsigned long long)nn);
+        }
+      }
+      uint64_t und = ballot(bv && nreal > 0u) & ~(none_m | all_m);
+      while (und) {
+        const uint32_t j = (uint32_t)__builtin_ctzll(und);
+        und &= und - 1;
+        node_block((g + j) << 6);
+      }
+    }
+  } else {
+    for (uint32_t nb = n0; nb < n1; nb += kWave) node_block(nb);
   }
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    g_nf += (uint32_t)__shfl_xor((int)g_nf, o, kWave);
+    g_nz += (uint32_t)__shfl_xor((int)g_nz, o, kWave);
+  }
+  nf_all += g_nf;
+  nz_all += g_nz;
   blk_flush();
   if (trace && lane == 0) {
     unsigned long long* tr = stats + 16 + 4 * ((size_t)(p >> 6) * C + chunk);
@@ -2689,19 +2731,17 @@ __global__ __launch_bounds__(kBlock) void k_set_static(unsigned char* __restrict
     s2[sum_index(q, kS2Static + 1, sum2_stride)] = (uint32_t)(value[t] >> 32);
   }
   if (pc.bsum || pc.bsum_p) {  // widen the blocks' CardNumber bounds to the new value
-    const uint32_t bsw = pc.bsum_words;
-    const unsigned long long cn = (unsigned long long)card_number[t];
+    const uint32_t bst = 4u * pc.bsum_words;
+    const uint32_t cn = (uint32_t)min(card_number[t], (uint64_t)0xffffffffu);
     if (pc.bsum) {
-      unsigned long long* b = reinterpret_cast<unsigned long long*>(
-          pc.bsum + (size_t)(node[t] >> 6) * bsw);
-      atomicMin(b + kBsCnMin / 2, cn);
-      atomicMax(b + kBsCnMax / 2, cn);
+      const uint32_t b = node[t] >> 6;
+      atomicMin(pc.bsum + sum_index(b, kBsCnMin, bst), cn);
+      atomicMax(pc.bsum + sum_index(b, kBsCnMax, bst), cn);
     }
     if (pc.bsum_p) {
-      unsigned long long* b = reinterpret_cast<unsigned long long*>(
-          pc.bsum_p + (size_t)(pc.inv[node[t]] >> 6) * bsw);
-      atomicMin(b + kBsCnMin / 2, cn);
-      atomicMax(b + kBsCnMax / 2, cn);
+      const uint32_t b = pc.inv[node[t]] >> 6;
+      atomicMin(pc.bsum_p + sum_index(b, kBsCnMin, bst), cn);
+      atomicMax(pc.bsum_p + sum_index(b, kBsCnMax, bst), cn);
     }
   }
   uint64_t* hdr = reinterpret_cast<uint64_t*>(nodes + (size_t)node[t] * stride);
@@ -4241,9 +4281,8 @@ __global__ __launch_bounds__(kWave) void k_bsum_cn(const uint32_t* __restrict__ 
          ((uint64_t)sum[sum_index(n, kSumCnHi, sum_stride)] << 32);
   const uint64_t lo = wave_min_u64(v ? cn : ~0ull), hi = wave_max_u64(v ? cn : 0ull);
   if (threadIdx.x == 0) {
-    uint64_t* o = reinterpret_cast<uint64_t*>(bsum + (size_t)b * bsw);
-    o[kBsCnMin / 2] = lo;
-    o[kBsCnMax / 2] = hi;
+    bsum[sum_index(b, kBsCnMin, 4u * bsw)] = (uint32_t)min(lo, (uint64_t)0xffffffffu);
+    bsum[sum_index(b, kBsCnMax, 4u * bsw)] = (uint32_t)min(hi, (uint64_t)0xffffffffu);
   }
 }
 

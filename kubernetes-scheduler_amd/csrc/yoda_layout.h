@@ -112,11 +112,13 @@ enum K2SumWord { kS2Static = 0, kS2Clock = 2, kS2Meta = 3, kS2Bw = 4, kS2Core = 
 __host__ __device__ constexpr uint32_t k2sum_stride(int k) { return 32u + 8u * (uint32_t)k; }
 
 // Block summary (N32 path): bounds over the REAL nodes of one 64-node block of a summary
-// order (the snapshot order, or the block-grouped copy's), so that the block K1 can decide a
-// whole block for a wave from one scalar read -- every node NONE, or every node ALL with one
-// maxima contribution -- before any per-node work.  u32 words, bsum_stride(K) bytes a block:
-//   cn_min, cn_max (u64, words 0-3)   CardNumber bounds (k_set_static keeps them valid bounds
-//                                     with atomics; a recompute makes them tight again)
+// order (the snapshot order, or the block-grouped copy's), so that the block K1 can decide
+// whole blocks for a wave -- every node NONE, or every node ALL with one maxima contribution
+// -- before any per-node work, 64 blocks at a time (lane = block).  u32 words, stored in tiles
+// of 64 blocks word-major like the node summaries (sum_index(block, word, bsum_stride(K))):
+//   cn_min, cn_max      CardNumber bounds, saturated to 32 bits (0xFFFFFFFF: >= that);
+//                       k_set_static keeps them valid bounds with atomics, k_bsum_cn makes
+//                       them tight again
 //   flags    kBsOneModel: every node one GPU model with one TotalMemory (kSumUni4|UniTotal);
 //            kBsUni4: every node kSumUni4
 //   ck_min, ck_max      the nodes' clock (one-model nodes) / card clocks (others)
@@ -129,14 +131,12 @@ __host__ __device__ constexpr uint32_t k2sum_stride(int k) { return 32u + 8u * (
 //   wc[6]   nodes reaching mx[f];  wl[6]  the lowest of them (offset in the block)
 //   tmin[K], tmax[K]    bounds of hfs[k] (K1Sum: 1 + free of the k-th healthy card by free)
 enum BlockSumWord {
-  kBsCnMin = 0, kBsCnMax = 2, kBsFlags = 4, kBsCkMin = 5, kBsCkMax = 6, kBsHckMin = 7,
-  kBsHckMax = 8, kBsNhMin = 9, kBsNhMax = 10, kBsMrfMin = 11, kBsMrfMax = 12, kBsNReal = 13,
-  kBsNzt = 14, kBsMx = 16, kBsWc = 22, kBsWl = 28, kBsT = 34
+  kBsCnMin = 0, kBsCnMax = 1, kBsFlags = 2, kBsCkMin = 3, kBsCkMax = 4, kBsHckMin = 5,
+  kBsHckMax = 6, kBsNhMin = 7, kBsNhMax = 8, kBsMrfMin = 9, kBsMrfMax = 10, kBsNReal = 11,
+  kBsNzt = 12, kBsMx = 13, kBsWc = 19, kBsWl = 25, kBsT = 31
 };
 constexpr uint32_t kBsOneModel = 1u, kBsUni4 = 2u;
-__host__ __device__ constexpr uint32_t bsum_stride(int k) {
-  return 4u * ((kBsT + 2u * (uint32_t)k + 3u) & ~3u);
-}
+__host__ __device__ constexpr uint32_t bsum_stride(int k) { return 4u * (kBsT + 2u * (uint32_t)k); }
 
 // K2 block bounds (N32 path; waves whose reciprocals are the G table's): per 64-node block of a
 // summary order, u32 words (kbub_stride(K) bytes a block):

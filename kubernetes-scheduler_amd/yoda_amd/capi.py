@@ -357,8 +357,10 @@ class Yoda:
                 "k2_uniform_maxima_wave_chunks": v[7] / max(v[8], 1),
                 "k2_fast_records": v[10] / pairs, "k2_per_pod_nonuniform": v[11] / pairs,
                 "k2_max_per_pod_nodes_wave_chunk": v[12],
-                "k1_blocks": {"none": v[13] / max(v[15], 1), "all": v[14] / max(v[15], 1),
-                              "n": v[15]},
+                "k1_blocks": {"none": v[13] / max(v[13] + v[14] + v[15], 1),
+                              "all": v[14] / max(v[13] + v[14] + v[15], 1),
+                              "per_node": v[15] / max(v[13] + v[14] + v[15], 1),
+                              "n": v[13] + v[14] + v[15]},
                 "k2_blocks": {"pruned": v[16], "worked": v[17]},
                 "wave_node_pairs": v[9]}
 
