@@ -344,6 +344,9 @@ struct yoda_handle {
   // K2 block bounds (yoda_layout.h kbub_*) of both orders; dirty: static scores changed since
   DevBuf kbub, kbub_p;
   bool kbub_dirty = true;
+  // the top tenth of the blocks by bound (ub[K]) at upload, per order: K2 visits them first
+  DevBuf hot, hot_p;
+  bool hot_ok = false;
   PermCopy perm_copy() const {
     PermCopy pc;
     if (perm_on) {
@@ -477,7 +480,7 @@ struct yoda_handle {
   ~yoda_handle() {
     if (comm && rccl().ok) (void)rccl().comm_destroy(comm);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &k1sum_p,   &k2sum_p,   &gtab_p, &blksum, &blksum_p, &kbub, &kbub_p,    &perm_ids,  &perm_inv,    &pod_blob,   &maxima,       &counts,
+    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &k1sum_p,   &k2sum_p,   &gtab_p, &blksum, &blksum_p, &kbub, &kbub_p, &hot, &hot_p,    &perm_ids,  &perm_inv,    &pod_blob,   &maxima,       &counts,
                      &pod_sorted, &perm,     &order_scratch, &order_meta, &order_hist,
                      &order_bstart, &order_slot, &order_bkt,
                      &rcp,       &rcp32,     &best,       &idx,          &ties,
@@ -756,11 +759,13 @@ PodParams pod_params(yoda_t* h) {
   if (h->path == Path::N32 && h->has_k1sum && h->blksum.p) pp.bsum = h->blksum.as<uint32_t>();
   const bool ub_ok = h->path == Path::N32 && pp.g.tab && !h->kbub_dirty && h->kbub.p;
   if (ub_ok) pp.kbub = h->kbub.as<uint32_t>();
+  if (ub_ok && h->hot_ok) pp.hot = h->hot.as<uint64_t>();
   if (h->perm_run()) {
     pp.ids = h->perm_ids.as<uint32_t>();
     if (pp.g.tab) pp.g.tab = h->gtab_p.as<uint32_t>();
     pp.bsum = h->blksum_p.p ? h->blksum_p.as<uint32_t>() : nullptr;
     pp.kbub = ub_ok && h->kbub_p.p ? h->kbub_p.as<uint32_t>() : nullptr;
+    pp.hot = pp.kbub && h->hot_ok ? h->hot_p.as<uint64_t>() : nullptr;
   }
   pp.mt = h->mem_ranks ? h->mt : MemTab{};
   return pp;
@@ -1991,7 +1996,45 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     h->generic = path == Path::U64;
     h->mem_ranks = ranks;
     h->kbub_dirty = true;
-    if (h->has_k2sum && h->g.tab && N > 0) HIP_TRY(h, build_block_ub(h));
+    h->hot_ok = false;
+    if (h->has_k2sum && h->g.tab && N > 0) {
+      HIP_TRY(h, build_block_ub(h));
+      // the blocks whose bound with every card qualifying (ub[K]) is in the top tenth: a
+      // static visiting order hint for the argmax K2 (results do not depend on it)
+      const uint32_t nb = (N + 63) / 64, KW = kbub_stride(K) / 4;
+      std::vector<uint32_t> ubw((size_t)nb * KW);
+      std::vector<uint64_t> words((nb + 63) / 64), words_p((nb + 63) / 64);
+      auto hot_bits = [&](const DevBuf& src, std::vector<uint64_t>& out) -> int {
+        HIP_TRY(h, hipMemcpyAsync(ubw.data(), src.p, ubw.size() * 4, hipMemcpyDeviceToHost,
+                                  h->stream));
+        HIP_TRY(h, hipStreamSynchronize(h->stream));
+        std::vector<double> u(nb);
+        for (uint32_t b = 0; b < nb; ++b) {
+          const uint64_t bits = (uint64_t)ubw[(size_t)b * KW + 2 * K] |
+                                ((uint64_t)ubw[(size_t)b * KW + 2 * K + 1] << 32);
+          std::memcpy(&u[b], &bits, 8);
+        }
+        std::vector<double> srt(u);
+        const size_t q = srt.size() - 1 - srt.size() / 10;
+        std::nth_element(srt.begin(), srt.begin() + q, srt.end());
+        const double thr = srt[q];
+        std::fill(out.begin(), out.end(), 0ull);
+        for (uint32_t b = 0; b < nb; ++b)
+          if (u[b] >= thr) out[b >> 6] |= 1ull << (b & 63);
+        return YODA_OK;
+      };
+      int hr = hot_bits(h->kbub, words);
+      if (!hr && h->perm_on) hr = hot_bits(h->kbub_p, words_p);
+      if (hr) return hr;
+      HIP_TRY(h, h->hot.ensure(words.size() * 8));
+      HIP_TRY(h, hipMemcpy(h->hot.p, words.data(), words.size() * 8, hipMemcpyHostToDevice));
+      if (h->perm_on) {
+        HIP_TRY(h, h->hot_p.ensure(words_p.size() * 8));
+        HIP_TRY(h, hipMemcpy(h->hot_p.p, words_p.data(), words_p.size() * 8,
+                             hipMemcpyHostToDevice));
+      }
+      h->hot_ok = true;
+    }
     if (!ranks) h->mt = MemTab{};
     h->h_frees.swap(frees);
     h->has_nodes = true;

@@ -1600,6 +1600,8 @@ struct ScoreArgs {
   MemTab mt = {};                 // memory ranks (yoda_layout.h MemTab)
   const uint32_t* ids = nullptr;  // block-grouped node order: the local id of each position
   const uint32_t* kbub = nullptr; // K2 block bounds (yoda_layout.h kbub_*): argmax pruning
+  const uint64_t* hot = nullptr;  // blocks of the highest bounds (bit b % 64 of word b / 64):
+                                  // visited first, so that the best so far rises early
 };
 
 template <Path P>
@@ -2433,11 +2435,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     // only the blocks K1 found a feasible pod of this wave in (bit b of word b/64)
     const uint64_t* bw = blk + (size_t)uniform_u32(p >> 6) * blk_stride;
     const uint32_t b0 = n0 >> 6, b1 = (n1 + 63) >> 6;
+    // pruning: the chunk's high-bound blocks first (pass 0), then the rest (pass 1)
+    const int passes = prune && args.hot ? 2 : 1;
+    for (int pass = 0; pass < passes; ++pass)
     for (uint32_t wi = b0 >> 6; b0 < b1 && wi <= (b1 - 1) >> 6; ++wi) {
       uint64_t bits = bw[wi];
       const uint32_t base = wi << 6;
       if (b0 > base) bits &= ~0ull << (b0 - base);
       if (b1 < base + 64) bits &= (1ull << (b1 - base)) - 1ull;
+      if (passes == 2) bits &= pass == 0 ? args.hot[wi] : ~args.hot[wi];
       while (bits) {
         const uint32_t j = (uint32_t)__builtin_ctzll(bits);
         bits &= bits - 1;
@@ -4123,7 +4129,8 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
                               unsigned long long* stats, const uint32_t* counts, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g, pp.mix, pp.mt,
-                    pp.ids, OUT == OUT_ARGMAX ? pp.kbub : nullptr};
+                    pp.ids, OUT == OUT_ARGMAX ? pp.kbub : nullptr,
+                    OUT == OUT_ARGMAX ? pp.hot : nullptr};
   const MaskSrc ms{bm, bs, bm_stride, bs_stride};
   switch (path) {
     case Path::N32:

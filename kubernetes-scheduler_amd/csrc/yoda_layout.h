@@ -342,6 +342,8 @@ struct PodParams {
   const uint32_t* bsum = nullptr;
   // K2 block bounds of that order (kbub_stride; nullptr: none -- the argmax K2 prunes with them)
   const uint32_t* kbub = nullptr;
+  // the blocks of that order with the highest bounds (bit words, as the K1 block list)
+  const uint64_t* hot = nullptr;
 };
 
 // Per-pod state produced between kernels (length P each unless noted).
