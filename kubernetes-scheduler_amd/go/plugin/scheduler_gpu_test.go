@@ -81,3 +81,46 @@ func TestAllocatedFollowsGenerations(t *testing.T) {
 		t.Fatalf("after AddPod: alloc %v gens %v -> %v", after, gens, gens2)
 	}
 }
+
+// Mode B's node set (snapshotNodes): every node of the scheduler's snapshot, in name order,
+// NodeInfos without a Node skipped -- the nodes the reference's pass-through Filter hands to
+// PreScore (scheduler.go:96-99,122), uploaded with the advisor's metrics each cycle.
+func TestModeBSnapshotNodes(t *testing.T) {
+	orphan := framework.NewNodeInfo() // no Node set (a NodeInfo the cache holds pods for)
+	l := fakeLister{infos: map[string]*framework.NodeInfo{
+		"n2": nodeInfo("n2"), "n10": nodeInfo("n10"), "n1": nodeInfo("n1"), "x": orphan,
+	}}
+	y := &Yoda{handle: fakeHandle{l: l}}
+	names, err := y.snapshotNodes()
+	if err != nil {
+		t.Fatal(err)
+	}
+	want := []string{"n1", "n10", "n2"}
+	if fmt.Sprint(names) != fmt.Sprint(want) {
+		t.Fatalf("snapshotNodes = %v, want %v", names, want)
+	}
+}
+
+// Less keeps sort.go:8-18: higher scv/priority first; a missing or non-numeric label is 0
+// (Atoi error -> 0), a negative one stays negative.
+func TestLessFollowsScvPriority(t *testing.T) {
+	pod := func(p string) *framework.QueuedPodInfo {
+		labels := map[string]string{}
+		if p != "" {
+			labels["scv/priority"] = p
+		}
+		return &framework.QueuedPodInfo{PodInfo: framework.NewPodInfo(
+			&v1.Pod{ObjectMeta: metav1.ObjectMeta{Name: "p" + p, Labels: labels}})}
+	}
+	y := &Yoda{}
+	cases := []struct {
+		a, b string
+		less bool
+	}{{"5", "3", true}, {"3", "5", false}, {"1", "", true}, {"", "x", false}, {"-1", "", false},
+		{"", "-1", true}, {"7", "7", false}}
+	for _, c := range cases {
+		if got := y.Less(pod(c.a), pod(c.b)); got != c.less {
+			t.Errorf("Less(%q, %q) = %v, want %v", c.a, c.b, got, c.less)
+		}
+	}
+}
