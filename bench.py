@@ -175,7 +175,8 @@ def bench_greedy(args):
     feeds Allocate, algorithm.go:299-303); `capacity` = the same batch with the CardNumber
     decrement (YODA_GREEDY_CARD_CAPACITY, the build-defined extension BASELINE config 5 names).
     N=1: one handle (yoda_greedy); N>1: nodes sharded across ranks, windows merged over RCCL
-    (yoda_amd/dist.py sharded_greedy).  Rank 0 checks a queue-order prefix against the
+    by libyoda's own driver (yoda_comm_greedy; --greedy-driver python: yoda_amd/dist.py
+    sharded_greedy over torch.distributed).  Rank 0 checks a queue-order prefix against the
     sequential oracle (N=1), for both modes."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -217,20 +218,37 @@ def bench_greedy(args):
         red = Reducer()
         agree_on_path(red, [y], [shard], [lo], device)
         hs = [HandleShard(y, device)]
+        native = args.greedy_driver == "libyoda"
+        if native:  # libyoda's own RCCL communicator (yoda_comm_init), id broadcast by torch
+            from yoda_amd.dist import LibExchange
+            LibExchange(y, device)
+
+        def run_greedy(pd, flags, st=None):
+            if not native:
+                return sharded_greedy(hs, red, nodes, pd, flags, stats=st)
+            pk = y.comm_greedy(nodes, pd, MODE_SCV, flags)
+            if st is not None:
+                st.update(y.comm_greedy_stats())
+            return pk
+
         for flags in (0, 1):
-            sharded_greedy(hs, red, nodes, pods.slice(0, min(pods.n_pods, 4096)), flags)  # warm-up
+            run_greedy(pods.slice(0, min(pods.n_pods, 4096)), flags)  # warm-up
             dist.barrier()
             torch.cuda.synchronize(device)
             t0 = time.perf_counter()
             st = {}
-            picks = sharded_greedy(hs, red, nodes, pods, flags, stats=st)
+            picks = run_greedy(pods, flags, st)
             torch.cuda.synchronize(device)
             dt = time.perf_counter() - t0
             t = torch.tensor([dt], dtype=torch.float64, device=device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             runs[flags] = {"seconds": float(t.item()), "picks": picks, "windows": st["windows"],
+                           "driver": "yoda_comm_greedy" if native else "dist.sharded_greedy",
                            ("exact_fallback_pods" if flags == 0 else "window_restarts"):
-                           st["exact_pods"] if flags == 0 else st["restarts"]}
+                           st["exact_pods"] if flags == 0 else st["restarts"],
+                           "refreshes": st.get("refreshes", 0)}
+            if native:
+                runs[flags]["collectives"] = st["collectives"]
             if args.check and rank == 0:
                 full = Yoda(dev_index)
                 full.upload_nodes(nodes)
@@ -419,6 +437,9 @@ def disclosure(y, nodes, pods, step, barrier, args) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--greedy-driver", choices=("libyoda", "python"), default="libyoda",
+                    help="--workload greedy at N>1: libyoda's yoda_comm_greedy (RCCL inside "
+                         "libyoda) or the Python dist.sharded_greedy (torch.distributed)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=3)

@@ -147,3 +147,18 @@ def test_sharded_greedy_u64(flags):
     np.testing.assert_array_equal(got, want)
     for y in hs:
         y.close()
+
+
+@pytest.mark.parametrize("flags", [0, 1])
+def test_comm_greedy_local_windows_vs_oracle(flags):
+    """The config-5 generator at 14,000 pods x 8,000 nodes (several 6,144-pod windows, the
+    mid-window list refresh in flags 0, capacity restarts in flags 1) over three node shards
+    with libyoda's driver: every pick equals the sequential oracle's."""
+    nodes, pods = synth.make_config(5, pods=14_000, nodes=8_000)
+    hs = _shard_handles(nodes, 3)
+    got = comm_greedy_local(hs, nodes, pods, MODE_SCV, flags)
+    st = hs[0].comm_greedy_stats()
+    assert st["windows"] >= 3
+    np.testing.assert_array_equal(got, oracle.greedy_mt(nodes, pods, flags, threads=16)[0])
+    for y in hs:
+        y.close()
