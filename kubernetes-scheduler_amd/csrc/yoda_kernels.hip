@@ -1164,9 +1164,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   mx[kMaxTotal] = max(mx[kMaxTotal], a_tot);
   nf += nf_all;
   nz += nz_all;
-  uint32_t* pmax32 = reinterpret_cast<uint32_t*>(pmax);  // N32: u32 partials (k_reduce1<true>)
+  // N32: packed u32 partials (k_reduce1<true>), [kNarrowWords][C][P]: bandwidth | clock << 16,
+  // core | power << 16 (each <= 55738 on this path), FreeMemory, TotalMemory (u32 codes)
+  uint32_t* pmax32 = reinterpret_cast<uint32_t*>(pmax);
+  const uint32_t pw4[kNarrowWords] = {mx[kMaxBw] | (mx[kMaxClock] << 16),
+                                      mx[kMaxCore] | (mx[kMaxPower] << 16), mx[kMaxFree],
+                                      mx[kMaxTotal]};
 #pragma unroll
-  for (int f = 0; f < 6; ++f) pmax32[((size_t)f * C + chunk) * n_pods + p] = mx[f];
+  for (int f = 0; f < kNarrowWords; ++f) pmax32[((size_t)f * C + chunk) * n_pods + p] = pw4[f];
   pcnt[((size_t)0 * C + chunk) * n_pods + p] = nf;
   pcnt[((size_t)1 * C + chunk) * n_pods + p] = nz;
 }
@@ -1210,6 +1215,40 @@ __device__ __forceinline__ float ru32_100_over(double M);
 
 // rcp != nullptr (a single-handle run, whose maxima are final here): each maxima thread also
 // writes its field's reciprocals (k_prep2's, fused).
+// Packed N32 partial word w (k1_block_n32's epilogue) -> the MaxValue fields it holds:
+// w 0: bandwidth | clock << 16, w 1: core | power << 16 (per-half max), w 2: free, w 3: total.
+__device__ __forceinline__ uint32_t narrow_max(uint32_t a, uint32_t b, int w) {
+  return w < 2 ? max16x2(a, b) : max(a, b);
+}
+__device__ __forceinline__ void narrow_store(uint32_t v, int w, uint32_t n_pods, uint32_t p,
+                                            uint64_t* maxima, const MemTab& mt) {
+  auto put = [&](int f, uint64_t x) {
+    if (mt.vf && f == kMaxFree) x = rank_value(x, mt.vf);  // memory ranks -> values
+    if (mt.vf && f == kMaxTotal) x = rank_value(x, mt.vt);
+    maxima[(size_t)f * n_pods + p] = x;
+  };
+  if (w == 0) {
+    put(kMaxBw, v & 0xffffu);
+    put(kMaxClock, v >> 16);
+  } else if (w == 1) {
+    put(kMaxCore, v & 0xffffu);
+    put(kMaxPower, v >> 16);
+  } else {
+    put(w == 2 ? kMaxFree : kMaxTotal, v);
+  }
+}
+
+// rcp rows: bw, core, power, free, total (k_prep2's order); the clock has none
+__device__ __forceinline__ void store_rcp(int f, uint64_t mx, uint32_t n_pods, uint32_t p,
+                                          double* rcp, float* rcp32) {
+  const int k = f == kMaxBw ? 0 : f == kMaxCore ? 1 : f == kMaxPower ? 2 : f == kMaxFree ? 3
+              : f == kMaxTotal ? 4 : -1;
+  if (rcp && k >= 0) {
+    rcp[(size_t)k * n_pods + p] = ru_100_over((double)mx);
+    if (k < 3) rcp32[(size_t)k * n_pods + p] = ru32_100_over((double)mx);
+  }
+}
+
 template <bool NARROW>
 __global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__ pmax,
                                                     const uint32_t* __restrict__ pcnt, uint32_t C,
@@ -1219,37 +1258,38 @@ __global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__
                                                     double* __restrict__ rcp,
                                                     float* __restrict__ rcp32, MemTab mt) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t f = blockIdx.y;
+  const uint32_t f = blockIdx.y;  // NARROW: packed words 0..3, then the 2 counts
+  constexpr uint32_t NF = NARROW ? kNarrowWords : 6u;
   if (p >= n_pods) return;
-  if (f < 6) {
-    uint64_t mx = 1;
+  if (f < NF) {
     if constexpr (NARROW) {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(pmax) + (size_t)f * C * n_pods + p;
-      uint32_t m32 = 1;
+      uint32_t m32 = f < 2 ? 0x00010001u : 1u;  // floor 1 (collection.go:31-38), per half
 #pragma unroll 8
-      for (uint32_t c = 0; c < C; ++c) m32 = max(m32, src[(size_t)c * n_pods]);
-      mx = m32;
+      for (uint32_t c = 0; c < C; ++c) m32 = narrow_max(m32, src[(size_t)c * n_pods], (int)f);
+      narrow_store(m32, (int)f, n_pods, p, maxima, mt);
+      if (rcp) {
+        const int fa = f == 0 ? kMaxBw : f == 1 ? kMaxCore : f == 2 ? kMaxFree : kMaxTotal;
+        store_rcp(fa, maxima[(size_t)fa * n_pods + p], n_pods, p, rcp, rcp32);
+        if (f == 1) store_rcp(kMaxPower, maxima[(size_t)kMaxPower * n_pods + p], n_pods, p, rcp,
+                              rcp32);
+      }
     } else {
+      uint64_t mx = 1;
       const uint64_t* src = pmax + (size_t)f * C * n_pods + p;
 #pragma unroll 8
       for (uint32_t c = 0; c < C; ++c) mx = umax64(mx, src[(size_t)c * n_pods]);
-    }
-    if (mt.vf && f == kMaxFree) mx = rank_value(mx, mt.vf);  // memory ranks -> values
-    if (mt.vf && f == kMaxTotal) mx = rank_value(mx, mt.vt);
-    maxima[(size_t)f * n_pods + p] = mx;
-    // rcp rows: bw, core, power, free, total (k_prep2's order); the clock has none
-    const int k = f == kMaxBw ? 0 : f == kMaxCore ? 1 : f == kMaxPower ? 2 : f == kMaxFree ? 3
-                : f == kMaxTotal ? 4 : -1;
-    if (rcp && k >= 0) {
-      rcp[(size_t)k * n_pods + p] = ru_100_over((double)mx);
-      if (k < 3) rcp32[(size_t)k * n_pods + p] = ru32_100_over((double)mx);
+      if (mt.vf && f == kMaxFree) mx = rank_value(mx, mt.vf);  // memory ranks -> values
+      if (mt.vf && f == kMaxTotal) mx = rank_value(mx, mt.vt);
+      maxima[(size_t)f * n_pods + p] = mx;
+      store_rcp((int)f, mx, n_pods, p, rcp, rcp32);
     }
   } else {
-    const uint32_t* src = pcnt + (size_t)(f - 6) * C * n_pods + p;
+    const uint32_t* src = pcnt + (size_t)(f - NF) * C * n_pods + p;
     uint32_t s = 0;
 #pragma unroll 8
     for (uint32_t c = 0; c < C; ++c) s += src[(size_t)c * n_pods];
-    counts[(size_t)(f - 6) * n_pods + p] = s;
+    counts[(size_t)(f - NF) * n_pods + p] = s;
   }
 }
 
@@ -1263,16 +1303,25 @@ __global__ __launch_bounds__(kWave) void k_reduce1_wave(const uint64_t* __restri
                                                          uint32_t* __restrict__ counts,
                                                          MemTab mt) {
   const uint32_t p = blockIdx.x, lane = threadIdx.x;
-  for (int f = 0; f < 6; ++f) {
-    uint64_t mx = 1;
-    for (uint32_t c = lane; c < C; c += kWave) {
-      const size_t o = ((size_t)f * C + c) * n_pods + p;
-      mx = umax64(mx, NARROW ? (uint64_t)reinterpret_cast<const uint32_t*>(pmax)[o] : pmax[o]);
+  if constexpr (NARROW) {
+    for (int w = 0; w < (int)kNarrowWords; ++w) {
+      uint32_t m = w < 2 ? 0x00010001u : 1u;
+      for (uint32_t c = lane; c < C; c += kWave)
+        m = narrow_max(m, reinterpret_cast<const uint32_t*>(pmax)[((size_t)w * C + c) * n_pods + p],
+                       w);
+      for (int o = kWave / 2; o > 0; o >>= 1)
+        m = narrow_max(m, (uint32_t)__shfl_xor((int)m, o, kWave), w);
+      if (lane == 0) narrow_store(m, w, n_pods, p, maxima, mt);
     }
-    for (int o = kWave / 2; o > 0; o >>= 1) mx = umax64(mx, __shfl_xor(mx, o, kWave));
-    if (mt.vf && f == kMaxFree) mx = rank_value(mx, mt.vf);  // memory ranks -> values
-    if (mt.vf && f == kMaxTotal) mx = rank_value(mx, mt.vt);
-    if (lane == 0) maxima[(size_t)f * n_pods + p] = mx;
+  } else {
+    for (int f = 0; f < 6; ++f) {
+      uint64_t mx = 1;
+      for (uint32_t c = lane; c < C; c += kWave) mx = umax64(mx, pmax[((size_t)f * C + c) * n_pods + p]);
+      for (int o = kWave / 2; o > 0; o >>= 1) mx = umax64(mx, __shfl_xor(mx, o, kWave));
+      if (mt.vf && f == kMaxFree) mx = rank_value(mx, mt.vf);  // memory ranks -> values
+      if (mt.vf && f == kMaxTotal) mx = rank_value(mx, mt.vt);
+      if (lane == 0) maxima[(size_t)f * n_pods + p] = mx;
+    }
   }
   for (int f = 0; f < 2; ++f) {
     uint32_t sum = 0;
@@ -1293,31 +1342,43 @@ __global__ __launch_bounds__(kBlock) void k_reduce1_split(const uint64_t* __rest
                                                           uint64_t* __restrict__ maxima,
                                                           uint32_t* __restrict__ counts) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x, f = blockIdx.y;
-  if (p >= n_pods) return;
+  constexpr uint32_t NF = NARROW ? kNarrowWords : 6u;
+  if (p >= n_pods || f >= NF + 2u) return;
   const uint32_t S = gridDim.z, per = (C + S - 1) / S;
   const uint32_t c0 = blockIdx.z * per, c1 = min(C, c0 + per);
   if (c0 >= c1) return;
-  if (f < 6) {
-    uint64_t mx = 0;
+  auto amax = [&](int fo, uint64_t v) {
+    atomicMax(reinterpret_cast<unsigned long long*>(maxima + (size_t)fo * n_pods + p),
+              (unsigned long long)v);
+  };
+  if (f < NF) {
     if constexpr (NARROW) {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(pmax) + (size_t)f * C * n_pods + p;
       uint32_t m32 = 0;
 #pragma unroll 8
-      for (uint32_t c = c0; c < c1; ++c) m32 = max(m32, src[(size_t)c * n_pods]);
-      mx = m32;
+      for (uint32_t c = c0; c < c1; ++c) m32 = narrow_max(m32, src[(size_t)c * n_pods], (int)f);
+      if (f == 0) {
+        amax(kMaxBw, m32 & 0xffffu);
+        amax(kMaxClock, m32 >> 16);
+      } else if (f == 1) {
+        amax(kMaxCore, m32 & 0xffffu);
+        amax(kMaxPower, m32 >> 16);
+      } else {
+        amax(f == 2 ? kMaxFree : kMaxTotal, m32);
+      }
     } else {
       const uint64_t* src = pmax + (size_t)f * C * n_pods + p;
+      uint64_t mx = 0;
 #pragma unroll 8
       for (uint32_t c = c0; c < c1; ++c) mx = umax64(mx, src[(size_t)c * n_pods]);
+      amax((int)f, mx);
     }
-    atomicMax(reinterpret_cast<unsigned long long*>(maxima + (size_t)f * n_pods + p),
-              (unsigned long long)mx);
   } else {
-    const uint32_t* src = pcnt + (size_t)(f - 6) * C * n_pods + p;
+    const uint32_t* src = pcnt + (size_t)(f - NF) * C * n_pods + p;
     uint32_t sum = 0;
 #pragma unroll 8
     for (uint32_t c = c0; c < c1; ++c) sum += src[(size_t)c * n_pods];
-    atomicAdd(counts + (size_t)(f - 6) * n_pods + p, sum);
+    atomicAdd(counts + (size_t)(f - NF) * n_pods + p, sum);
   }
 }
 
@@ -4072,7 +4133,7 @@ hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, boo
     hipError_t e = hipMemsetAsync(maxima, 0, 6 * (size_t)n_pods * 8, s);
     if (e == hipSuccess) e = hipMemsetAsync(counts, 0, 2 * (size_t)n_pods * 4, s);
     if (e != hipSuccess) return e;
-    const dim3 grid(pb, 8, S);
+    const dim3 grid(pb, narrow ? kNarrowWords + 2u : 8u, S);
     if (narrow)
       hipLaunchKernelGGL(k_reduce1_split<true>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
                          n_pods, maxima, counts);
@@ -4091,7 +4152,7 @@ hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, boo
                          part.cnt, C, n_pods, maxima, counts, mt);
     if (rcp) return launch_prep2(maxima, n_pods, rcp, rcp32, s);
   } else {
-    const dim3 grid((n_pods + kBlock - 1) / kBlock, 8);
+    const dim3 grid((n_pods + kBlock - 1) / kBlock, narrow ? kNarrowWords + 2u : 8u);
     if (narrow)
       hipLaunchKernelGGL(k_reduce1<true>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
                          n_pods, maxima, counts, rcp, rcp32, mt);

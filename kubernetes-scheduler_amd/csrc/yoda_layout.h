@@ -365,7 +365,10 @@ struct PodState {
 // MaxValue field order (collection.go:14-21) used for the [6][P] maxima buffer.
 enum MaxField { kMaxBw = 0, kMaxClock = 1, kMaxCore = 2, kMaxFree = 3, kMaxPower = 4, kMaxTotal = 5 };
 
-// Chunk partials: [field][chunk][P].
+// Chunk partials: [field][chunk][P].  The block K1 (N32) writes its maxima packed into
+// kNarrowWords u32 words (bandwidth | clock << 16, core | power << 16, free, total: the four
+// small fields are <= 55738 on that path), read back by k_reduce1<true>.
+constexpr uint32_t kNarrowWords = 4;
 struct Partials {
   uint64_t* max_u;     // [6][C][P]
   uint32_t* cnt;       // [2][C][P]
