@@ -372,6 +372,9 @@ int yoda_greedy_refreshes(const yoda_t* h, uint32_t* refreshes);
  * no pod is evaluated one by one.  On the U64 path every pod is one exact sharded step
  * (yoda_shard_phase1 / phase2 / finalize over a one-pod batch) fed to yoda_gs_assign. */
 int yoda_topk_k(void);
+/* The capacity windows' list depth: yoda_shard_topk returns this many candidates per pod after
+ * yoda_shard_phase1_witness (yoda_topk_k() after yoda_shard_phase1). */
+int yoda_topk_k_capacity(void);
 /* Set the allocated memory (and CardNumber) of the listed nodes (GLOBAL ids; ids outside
  * this handle's shard are ignored) and refresh their static score on the device. */
 int yoda_set_node_state(yoda_t* h, uint32_t count, const uint32_t* nodes, const uint64_t* alloc,

@@ -437,6 +437,7 @@ struct yoda_handle {
   bool ran = false;
   bool ran_bitmask = false;
   bool phase1_done = false;
+  bool phase1_wit = false;  // the last shard phase 1 was the witness one (capacity windows)
 
   // class counters of the block kernels (yoda_class_stats_*): device [8] u64 + host totals
   bool class_stats = false;
@@ -2566,6 +2567,7 @@ int yoda_shard_phase1(yoda_t* h, int mode, uint64_t* d_maxima, uint32_t* d_count
     if ((rc = order_pods(h, mode))) return rc;
     if ((rc = phase1(h, mode, d_maxima, d_counts))) return rc;
     h->phase1_done = true;
+    h->phase1_wit = false;
     h->ran = false;
     return YODA_OK;
   } catch (...) {
@@ -3309,6 +3311,7 @@ int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks,
 // yoda_set_node_state on every shard).
 
 int yoda_topk_k(void) { return topk_k(); }
+int yoda_topk_k_capacity(void) { return topk_k_capacity(); }
 
 namespace {
 
@@ -3407,7 +3410,9 @@ int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_count
   if (!d_maxima || !d_counts || !counts || !top_score || !top_node)
     return fail(h, YODA_ERR_INVALID_ARG, "NULL buffer");
   try {
-    const uint32_t P = h->n_pods, N = h->n_nodes, KT = (uint32_t)topk_k();
+    // the capacity windows' deeper lists after the witness phase 1 (yoda_greedy's depths)
+    const uint32_t P = h->n_pods, N = h->n_nodes,
+                   KT = (uint32_t)(h->phase1_wit ? topk_k_capacity() : topk_k());
     h->h_pos.resize(P);
     for (uint32_t i = 0; i < P; ++i) h->h_pos[i] = i;
     h->topk_ready = false;
@@ -3462,6 +3467,7 @@ int yoda_shard_phase1_witness(yoda_t* h, uint64_t* d_maxima, uint32_t* d_counts,
     if ((rc = order_pods(h, YODA_MODE_SCV))) return rc;
     if ((rc = phase1_witness(h, d_maxima, d_counts, d_wit, h->node_offset))) return rc;
     h->phase1_done = true;
+    h->phase1_wit = true;
     h->ran = false;
     return YODA_OK;
   } catch (...) {
@@ -4752,7 +4758,8 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
       }
       return push(false);
     }
-    const uint32_t K = (uint32_t)topk_k(), W0 = std::min<uint32_t>(P, greedy_window());
+    const uint32_t K = (uint32_t)(capacity ? topk_k_capacity() : topk_k()),
+                   W0 = std::min<uint32_t>(P, greedy_window());
     std::vector<uint32_t> counts, ti, wit_h;
     std::vector<double> ts;
     std::vector<uint64_t> mx_h;

@@ -72,6 +72,7 @@ _SIGS = {
     "yoda_greedy_stats": ([_vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                            C.POINTER(C.c_double)], C.c_int),
     "yoda_topk_k": ([], C.c_int),
+    "yoda_topk_k_capacity": ([], C.c_int),
     "yoda_set_node_state": ([_vp, _u32, _vp, _vp, _vp], C.c_int),
     "yoda_shard_topk": ([_vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "yoda_shard_best_one": ([_vp, _u32, C.POINTER(C.c_double), C.POINTER(C.c_int32)], C.c_int),
@@ -412,9 +413,10 @@ class Yoda:
         self._check(lib().yoda_set_node_state(self._h, n.size, _np_ptr(n), _np_ptr(a),
                                               _np_ptr(c)), "yoda_set_node_state")
 
-    def shard_topk(self, d_maxima: int, d_counts: int):
-        """(counts [2, P], top_score [k, P], top_node [k, P]) of the uploaded batch."""
-        P, k = self.n_pods, topk_k()
+    def shard_topk(self, d_maxima: int, d_counts: int, k: int | None = None):
+        """(counts [2, P], top_score [k, P], top_node [k, P]) of the uploaded batch; k =
+        topk_k() after shard_phase1, topk_k_capacity() after shard_phase1_witness."""
+        P, k = self.n_pods, (topk_k() if k is None else k)
         counts = np.zeros((2, max(P, 1)), np.uint32)
         ts = np.zeros((k, max(P, 1)), np.float64)
         ti = np.zeros((k, max(P, 1)), np.uint32)
@@ -523,6 +525,11 @@ def comm_greedy_local(handles, all_nodes, pods, mode: int = 0, flags: int = 0) -
 def topk_k() -> int:
     """Candidates per pod in the greedy top-k lists (yoda_topk_k)."""
     return int(lib().yoda_topk_k())
+
+
+def topk_k_capacity() -> int:
+    """Candidates per pod in the capacity windows' lists (yoda_topk_k_capacity)."""
+    return int(lib().yoda_topk_k_capacity())
 
 
 def next_window(progress: int, wmax: int) -> int:

@@ -457,8 +457,8 @@ class HandleShard:
         """(maxima [6, P], wit [12, P]) after the merge and topk(), caller's pod order."""
         return self.h.shard_witness_download(self.bufs.maxima.data_ptr(), self.bufs.wit.data_ptr())
 
-    def topk(self):
-        return self.h.shard_topk(self.bufs.maxima.data_ptr(), self.bufs.counts.data_ptr())
+    def topk(self, k: int | None = None):
+        return self.h.shard_topk(self.bufs.maxima.data_ptr(), self.bufs.counts.data_ptr(), k)
 
     def best_one(self, i: int):
         return self.h.shard_best_one(i)
@@ -492,8 +492,9 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
     how far the last one got), as the single-handle yoda_greedy does.
     `shards`: this process's shards (HandleShard); `nodes`: the FULL snapshot.  The shards'
     node state is restored at the end."""
-    from .capi import GreedySession, next_window, topk_k
+    from .capi import GreedySession, next_window, topk_k, topk_k_capacity
     k = topk_k()
+    k_cap = topk_k_capacity()  # the capacity windows' lists (yoda_greedy's depth)
     gs = GreedySession(nodes, pods, flags)
     order = gs.queue_order()
     P = pods.n_pods
@@ -541,11 +542,11 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
                 bufs = [s.phase1_witness() for s in shards]
                 sb = dict(zip(map(id, bufs), shards))
                 merge_witness(reduce, bufs, lambda b: sb[id(b)].witness_prepare(b))
-                lists = [s.topk() for s in shards]
+                lists = [s.topk(k_cap) for s in shards]
                 g = reduce.gather([np.stack([ts, ti.astype(np.float64)]) for _, ts, ti in lists])
-                ts, ti = merge_topk([x[0] for x in g], [x[1].astype(np.uint64) for x in g], k)
+                ts, ti = merge_topk([x[0] for x in g], [x[1].astype(np.uint64) for x in g], k_cap)
                 mx, wit = shards[0].witness()
-                gs.begin_window(ws, k, lists[0][0], ts, ti)
+                gs.begin_window(ws, k_cap, lists[0][0], ts, ti)
                 gs.set_witness(mx, wit[:6], wit[6:])
                 nxt = gs.resolve()
                 windows += 1

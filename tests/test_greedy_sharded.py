@@ -72,8 +72,8 @@ class OracleShard:
                                             dtype=torch.int32))
         return self.bufs
 
-    def topk(self):
-        k, n = topk_k(), self.pods.n_pods
+    def topk(self, k=None):
+        k, n = (topk_k() if k is None else k), self.pods.n_pods
         ts = np.full((k, n), -1.0)
         ti = np.full((k, n), 0xFFFFFFFF, np.uint32)
         for p in range(n):
