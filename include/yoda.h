@@ -344,9 +344,9 @@ int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks,
  * stays 0); the YODA_GREEDY_FAIL_DIV environment knob re-enables one-by-one fallbacks for
  * A/B runs. */
 int yoda_greedy_restarts(const yoda_t* h, uint32_t* restarts);
-/* flags == 0: mid-window list refreshes of the last yoda_greedy (the window's top-k lists
- * recomputed against the current state once many of its remaining pods had gone uncertified;
- * DESIGN.md §5). */
+/* Mid-window list refreshes of the last yoda_greedy (the window's top-k lists recomputed
+ * against the current state: flags 0 once many of its remaining pods had gone uncertified,
+ * capacity mode at a failing pod with many window pods left). */
 int yoda_greedy_refreshes(const yoda_t* h, uint32_t* refreshes);
 
 /* ---- sharded greedy batch (node shards on several GPUs) ------------------------------
@@ -435,9 +435,10 @@ int yoda_gs_assign(yoda_gs_t* g, uint32_t queue_pos, int32_t pick);
 /* flags == 0: *count = window pods [from, from + scan) with >= 2 feasible nodes whose lists no
  * longer certify them (they stay so: scores only drop) -- the refresh trigger. */
 int yoda_gs_uncertified(const yoda_gs_t* g, uint32_t from, uint32_t scan, uint32_t* count);
-/* flags == 0: new candidate lists for window pods [from, wn) ([k][wn] in window order, as
- * yoda_gs_begin_window's, scored against the CURRENT node state): each list's threshold
- * becomes its refresh-time k-th score. */
+/* New candidate lists for window pods [from, wn) ([k][wn] in window order, as
+ * yoda_gs_begin_window's, scored against the CURRENT node state with the window's phase-1
+ * masks and maxima): each list's threshold becomes its refresh-time k-th score.  Capacity
+ * sessions keep judging feasibility and maxima against the window start. */
 int yoda_gs_refresh(yoda_gs_t* g, uint32_t from, const double* top_score,
                     const uint32_t* top_node);
 /* YODA_GREEDY_CARD_CAPACITY: the size of the window that a restart at window index `progress`

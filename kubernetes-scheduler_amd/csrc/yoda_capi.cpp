@@ -3823,11 +3823,9 @@ bool yoda_greedy_session::resolve_capacity(uint32_t i, uint32_t p, int32_t* pk) 
   if (!maxima_kept(i, q, lq, exact, lw)) return ++why[3], false;  // unlisted scores may move
   if (bi == 0xffffffffu) return ++why[4], false;       // every listed node lost
   if (!whole) {
-    // every unlisted node scored <= T at the window start (ties: higher index) and has
-    // only lost Allocate since, or feasibility
-    const double T = ts[(size_t)(len - 1) * wn + i];
-    const uint32_t tidx = ti[(size_t)(len - 1) * wn + i];
-    if (!(bs > T || (bs == T && bi <= tidx))) return ++why[5], false;
+    // every unlisted node scored <= T at the window start or the list's last refresh (ties:
+    // higher index) and has only lost Allocate since, or feasibility
+    if (!(bs > Tw[i] || (bs == Tw[i] && bi <= Tix[i]))) return ++why[5], false;
   }
   *pk = (int32_t)bi;
   return true;
@@ -4038,7 +4036,6 @@ int yoda_gs_uncertified(const yoda_gs_t* g, uint32_t from, uint32_t scan, uint32
 int yoda_gs_refresh(yoda_gs_t* g, uint32_t from, const double* top_score,
                     const uint32_t* top_node) {
   if (!g || !g->in_window || !top_score || !top_node || from > g->wn) return YODA_ERR_INVALID_ARG;
-  if (g->flags & YODA_GREEDY_CARD_CAPACITY) return YODA_ERR_STATE;
   const uint32_t wn = g->wn, k = g->k;
   for (uint32_t i = from; i < wn; ++i) {
     const uint32_t len = std::min<uint32_t>(g->counts[i], k);
@@ -4320,12 +4317,40 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
       return fail(h, rc, "greedy: session window");
     // resolve; an uncertified pod is scheduled exactly against the current state (k_one_*)
     // while such pods stay rare in the window, else it opens the next window
-    uint32_t next = 0, fails = 0;
+    uint32_t next = 0, fails = 0, refreshed_at = 0xffffffffu;
     double fb_ms = 0;
     uint64_t why0[6];
     std::copy(std::begin(g->why), std::end(g->why), why0);
+    // Mid-window list refresh (capacity mode): when a pod fails with many window pods left,
+    // the window's top-k K2 runs again against the current state on the window's own K1
+    // masks, maxima and reciprocals (the session keeps judging feasibility and maxima against
+    // the window start: lost nodes are skipped in the lists and counted as before, and a pod
+    // whose maxima may have moved stays uncertified); each list's threshold becomes its
+    // refresh-time k-th score.  A pod that still fails right after a refresh opens the next
+    // window.  YODA_GREEDY_CAP_REFRESH=0: off (A/B knob); _MIN: the pods left it needs.
+    static const bool cap_refresh = YODA_KNOB("YODA_GREEDY_CAP_REFRESH", 1) != 0;
+    static const uint32_t cap_refresh_min = YODA_KNOB("YODA_GREEDY_CAP_REFRESH_MIN", 256);
     for (;;) {
       if ((rc = yoda_gs_resolve(g, &next))) return fail(h, rc, "greedy: resolve");
+      if (next < wn && cap_refresh && N > 0 && wn - next >= cap_refresh_min &&
+          refreshed_at != next && !g->wrapped) {
+        refreshed_at = next;
+        if ((rc = push())) return rc;
+        const uint32_t off = h->node_offset;
+        h->node_offset = 0;
+        rc = topk_lists(h, wn, KT, h->counts.as<uint32_t>());
+        h->node_offset = off;
+        if (rc) return rc;
+        HIP_TRY(h, launch_window_out(h->counts.as<uint32_t>(), h->maxima.as<uint64_t>(),
+                                     h->wit.as<uint32_t>(), h->tk_s.as<double>(),
+                                     h->tk_i.as<uint32_t>(),
+                                     h->ordered ? h->perm.as<uint32_t>() : nullptr, wn, KT,
+                                     static_cast<unsigned char*>(h->win_stage.dp), h->stream));
+        HIP_TRY(h, hipStreamSynchronize(h->stream));
+        if ((rc = yoda_gs_refresh(g, next, ts_p, ti_p))) return fail(h, rc, "greedy: refresh");
+        ++h->greedy_refreshes;
+        continue;
+      }
       // YODA_GREEDY_FAIL_DIV (A/B knob): one exact evaluation allowed per that many resolved pods
       static const uint32_t rate = YODA_KNOB("YODA_GREEDY_FAIL_DIV", 0);
       // YODA_GREEDY_CAP_SCAN=<n> (A/B knob): fall back exactly (instead of restarting) when at
