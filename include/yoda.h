@@ -344,9 +344,9 @@ int yoda_greedy_stats(const yoda_t* h, uint32_t* windows, uint32_t* fallbacks,
  * stays 0); the YODA_GREEDY_FAIL_DIV environment knob re-enables one-by-one fallbacks for
  * A/B runs. */
 int yoda_greedy_restarts(const yoda_t* h, uint32_t* restarts);
-/* Mid-window list refreshes of the last yoda_greedy (the window's top-k lists recomputed
- * against the current state: flags 0 once many of its remaining pods had gone uncertified,
- * capacity mode at a failing pod with many window pods left). */
+/* flags == 0: mid-window list refreshes of the last yoda_greedy (the window's top-k lists
+ * recomputed against the current state once many of its remaining pods had gone uncertified;
+ * DESIGN.md §5). */
 int yoda_greedy_refreshes(const yoda_t* h, uint32_t* refreshes);
 
 /* ---- sharded greedy batch (node shards on several GPUs) ------------------------------

@@ -343,7 +343,13 @@ struct yoda_handle {
   bool greedy_active = false;  // inside a greedy batch (its pushes keep the bounds valid)
   // K2 block bounds (yoda_layout.h kbub_*) of both orders; dirty: static scores changed since
   DevBuf kbub, kbub_p;
-  bool kbub_dirty = true;
+  bool kbub_dirty = true;   // a static score rose above the bounds' own: rebuild before use
+  bool kbub_loose = false;  // static scores only fell since the build: valid, rebuilt for runs
+  std::vector<uint64_t> ub_stat;  // each node's static score when the bounds were built
+  // a pushed static score against the bounds: above -> dirty, else loose
+  void note_static(uint32_t n, uint64_t s) {
+    if (n < ub_stat.size() && s <= ub_stat[n]) kbub_loose = true; else kbub_dirty = true;
+  }
   // the top tenth of the blocks by bound (ub[K]) at upload, per order: K2 visits them first
   DevBuf hot, hot_p;
   bool hot_ok = false;
@@ -1023,7 +1029,19 @@ hipError_t build_block_ub(yoda_t* h) {
       e = launch_block_ub(h->K, h->k2sum_p.as<uint32_t>(), h->gtab_p.as<uint32_t>(), h->n_nodes,
                           h->kbub_p.as<uint32_t>(), h->stream);
   }
-  if (e == hipSuccess) h->kbub_dirty = false;
+  if (e == hipSuccess) {
+    h->kbub_dirty = h->kbub_loose = false;
+    // the static scores the bounds hold (the host copy of the K2 summaries' static words)
+    const uint32_t N = h->n_nodes, S2 = k2sum_stride(h->K);
+    h->ub_stat.resize(N);
+    for (uint32_t n = 0; n < N; ++n) {
+      const uint64_t b = (uint64_t)h->host_k2sum[sum_index(n, kS2Static, S2)] |
+                         ((uint64_t)h->host_k2sum[sum_index(n, kS2Static + 1, S2)] << 32);
+      double d;
+      std::memcpy(&d, &b, 8);
+      h->ub_stat[n] = (uint64_t)d;
+    }
+  }
   return e;
 }
 
@@ -1204,8 +1222,8 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
                                best, idx, ties, low, h->stream));
     return YODA_OK;
   }
-  if (mode == YODA_MODE_SCV && !rows && h->kbub_dirty && h->path == Path::N32 && h->has_k2sum &&
-      h->g.tab)
+  if (mode == YODA_MODE_SCV && !rows && (h->kbub_dirty || (h->kbub_loose && !h->greedy_active)) &&
+      h->path == Path::N32 && h->has_k2sum && h->g.tab)
     HIP_TRY(h, build_block_ub(h));
   if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
   uint32_t C2 = h->C2;
@@ -1997,6 +2015,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     h->generic = path == Path::U64;
     h->mem_ranks = ranks;
     h->kbub_dirty = true;
+    h->kbub_loose = false;
     h->hot_ok = false;
     if (h->has_k2sum && h->g.tab && N > 0) {
       HIP_TRY(h, build_block_ub(h));
@@ -2831,7 +2850,7 @@ struct GreedyState {
     const unsigned char* d = static_cast<const unsigned char*>(h->upd_stage.dp);
     const uint32_t stride = h->path == Path::N32 ? n32_stride(h->K) : node_stride(h->K);
     h->blksum_loose = true;  // (the atomics keep the block bounds valid, not tight)
-    h->kbub_dirty = true;     // (static scores change: the K2 block bounds are rebuilt)
+    for (uint32_t i = 0; i < cnt; ++i) h->note_static(list[i], stat[list[i]]);
     HIP_TRY(h, launch_set_static(h->nodes.as<unsigned char>(), stride,
                                  reinterpret_cast<const uint32_t*>(d),
                                  reinterpret_cast<const uint64_t*>(d + o_val),
@@ -3335,7 +3354,15 @@ int push_node_state(yoda_t* h, const std::vector<uint32_t>& loc, const std::vect
   unsigned char* d = h->upd_node.as<unsigned char>();
   const uint32_t stride = h->path == Path::N32 ? n32_stride(h->K) : node_stride(h->K);
   h->blksum_loose = true;  // (the atomics keep the block bounds valid, not tight)
-  h->kbub_dirty = true;     // (static scores change: the K2 block bounds are rebuilt)
+  for (uint32_t t = 0; t < cnt; ++t) {  // the K2 block bounds stay valid while scores only fall
+    uint64_t sv = val[t];
+    if (!h->generic) {
+      double d;
+      std::memcpy(&d, &val[t], 8);
+      sv = (uint64_t)d;
+    }
+    h->note_static(loc[t], sv);
+  }
   HIP_TRY(h, launch_set_static(h->nodes.as<unsigned char>(), stride,
                                reinterpret_cast<const uint32_t*>(d),
                                reinterpret_cast<const uint64_t*>(d + o_val),
@@ -4317,40 +4344,12 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
       return fail(h, rc, "greedy: session window");
     // resolve; an uncertified pod is scheduled exactly against the current state (k_one_*)
     // while such pods stay rare in the window, else it opens the next window
-    uint32_t next = 0, fails = 0, refreshed_at = 0xffffffffu;
+    uint32_t next = 0, fails = 0;
     double fb_ms = 0;
     uint64_t why0[6];
     std::copy(std::begin(g->why), std::end(g->why), why0);
-    // Mid-window list refresh (capacity mode): when a pod fails with many window pods left,
-    // the window's top-k K2 runs again against the current state on the window's own K1
-    // masks, maxima and reciprocals (the session keeps judging feasibility and maxima against
-    // the window start: lost nodes are skipped in the lists and counted as before, and a pod
-    // whose maxima may have moved stays uncertified); each list's threshold becomes its
-    // refresh-time k-th score.  A pod that still fails right after a refresh opens the next
-    // window.  YODA_GREEDY_CAP_REFRESH=0: off (A/B knob); _MIN: the pods left it needs.
-    static const bool cap_refresh = YODA_KNOB("YODA_GREEDY_CAP_REFRESH", 1) != 0;
-    static const uint32_t cap_refresh_min = YODA_KNOB("YODA_GREEDY_CAP_REFRESH_MIN", 256);
     for (;;) {
       if ((rc = yoda_gs_resolve(g, &next))) return fail(h, rc, "greedy: resolve");
-      if (next < wn && cap_refresh && N > 0 && wn - next >= cap_refresh_min &&
-          refreshed_at != next && !g->wrapped) {
-        refreshed_at = next;
-        if ((rc = push())) return rc;
-        const uint32_t off = h->node_offset;
-        h->node_offset = 0;
-        rc = topk_lists(h, wn, KT, h->counts.as<uint32_t>());
-        h->node_offset = off;
-        if (rc) return rc;
-        HIP_TRY(h, launch_window_out(h->counts.as<uint32_t>(), h->maxima.as<uint64_t>(),
-                                     h->wit.as<uint32_t>(), h->tk_s.as<double>(),
-                                     h->tk_i.as<uint32_t>(),
-                                     h->ordered ? h->perm.as<uint32_t>() : nullptr, wn, KT,
-                                     static_cast<unsigned char*>(h->win_stage.dp), h->stream));
-        HIP_TRY(h, hipStreamSynchronize(h->stream));
-        if ((rc = yoda_gs_refresh(g, next, ts_p, ti_p))) return fail(h, rc, "greedy: refresh");
-        ++h->greedy_refreshes;
-        continue;
-      }
       // YODA_GREEDY_FAIL_DIV (A/B knob): one exact evaluation allowed per that many resolved pods
       static const uint32_t rate = YODA_KNOB("YODA_GREEDY_FAIL_DIV", 0);
       // YODA_GREEDY_CAP_SCAN=<n> (A/B knob): fall back exactly (instead of restarting) when at

@@ -2048,9 +2048,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // smallest scv/memory (kbub_*) -- is below every active lane's best so far cannot hold a
   // pick or a tie of any of them.  thr: the min over active lanes of that best, refreshed
   // after each block the wave works on (it only grows, so a stale value stays a lower bound).
-  const bool prune = !TOPK && args.kbub != nullptr && use_g;
+  // TOPK (greedy windows): a block whose best possible key cannot beat any active lane's
+  // k-th key (thrk: the min over active lanes of their own and the U list's k-th) is skipped.
+  const bool prune = args.kbub != nullptr && use_g;
   constexpr uint32_t KBW = kbub_stride(K) / 4u;
   double thr = -1.0;
+  uint64_t thrk = 0ull;
 
   double ubest = -1.0;                      // node lane (U nodes)
   uint32_t uidx = 0xffffffffu, uties = 0;
@@ -2089,7 +2092,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       for (int k = 0; k < K; ++k) J += U[kbub_fmax(K) + (uint32_t)k] >= m_min ? 1u : 0u;
       const double ub =
           __longlong_as_double((long long)((uint64_t)U[2 * J] | ((uint64_t)U[2 * J + 1] << 32)));
-      if (ub < thr) {
+      bool skip;
+      if constexpr (TOPK) {  // (ub: an integer-valued double >= 0)
+        skip = ((((uint64_t)ub) << ib) | (uint64_t)imax) <= thrk;
+      } else {
+        skip = ub < thr;
+      }
+      if (skip) {
         if (STATS && !trace && lane == 0) atomicAdd(stats + 13, 1ull);
         return;
       }
@@ -2509,7 +2518,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         const uint32_t j = (uint32_t)__builtin_ctzll(bits);
         bits &= bits - 1;
         block((base + j) << 6);
-        if (prune && worked) {  // every active lane's best so far: its nodes', the U nodes'
+        if (prune && worked && TOPK) {  // every active lane's k-th key so far
+          const uint64_t kth = act ? (pl[TL - 1] > ul[TL - 1] ? pl[TL - 1] : ul[TL - 1]) : ~0ull;
+          thrk = wave_min_u64(kth);
+        } else if (prune && worked) {  // every active lane's best: its nodes', the U nodes'
           double wu = ubest;
 #pragma unroll
           for (int o = kWave / 2; o > 0; o >>= 1) wu = fmax(wu, __shfl_xor(wu, o, kWave));
@@ -4278,7 +4290,8 @@ hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigne
                                 uint32_t ib, int tk, hipStream_t s) {
   if ((tk != kTopK && tk != kTopKCap) || K > 8 || n_pods == 0) return hipErrorInvalidValue;
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
-  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g, pp.mix, pp.mt};
+  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g, pp.mix, pp.mt,
+                    nullptr, pp.kbub};
 #define YODA_TOPKB(TKV, RKV, MIXV)                                                              \
   YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false, TKV, RKV, MIXV>), grid,            \
                                       dim3(kBlock), 0, s, nodes, sum2, n_nodes, chunk_nodes, a,   \
