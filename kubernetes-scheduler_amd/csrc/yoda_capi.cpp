@@ -1018,7 +1018,8 @@ int ensure_diskio_classes(yoda_t* h) {
 hipError_t build_block_ub(yoda_t* h) {
   hipError_t e = hipSuccess;
   if (!(h->path == Path::N32 && h->has_k2sum && h->gtab.p)) return e;
-  const size_t bytes = (size_t)std::max<uint32_t>((h->n_nodes + 63) / 64, 1) * kbub_stride(h->K);
+  const size_t bytes = sum_words(std::max<uint32_t>((h->n_nodes + 63) / 64, 1),
+                                 kbub_stride(h->K)) * 4;  // tiles of 64 blocks
   e = h->kbub.ensure(bytes);
   if (e == hipSuccess)
     e = launch_block_ub(h->K, h->k2sum.as<uint32_t>(), h->gtab.as<uint32_t>(), h->n_nodes,
@@ -2021,8 +2022,8 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
       HIP_TRY(h, build_block_ub(h));
       // the blocks whose bound with every card qualifying (ub[K]) is in the top tenth: a
       // static visiting order hint for the argmax K2 (results do not depend on it)
-      const uint32_t nb = (N + 63) / 64, KW = kbub_stride(K) / 4;
-      std::vector<uint32_t> ubw((size_t)nb * KW);
+      const uint32_t nb = (N + 63) / 64, KST = kbub_stride(K);
+      std::vector<uint32_t> ubw(sum_words(nb, KST));
       std::vector<uint64_t> words((nb + 63) / 64), words_p((nb + 63) / 64);
       auto hot_bits = [&](const DevBuf& src, std::vector<uint64_t>& out) -> int {
         HIP_TRY(h, hipMemcpyAsync(ubw.data(), src.p, ubw.size() * 4, hipMemcpyDeviceToHost,
@@ -2030,8 +2031,8 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
         HIP_TRY(h, hipStreamSynchronize(h->stream));
         std::vector<double> u(nb);
         for (uint32_t b = 0; b < nb; ++b) {
-          const uint64_t bits = (uint64_t)ubw[(size_t)b * KW + 2 * K] |
-                                ((uint64_t)ubw[(size_t)b * KW + 2 * K + 1] << 32);
+          const uint64_t bits = (uint64_t)ubw[sum_index(b, 2 * K, KST)] |
+                                ((uint64_t)ubw[sum_index(b, 2 * K + 1, KST)] << 32);
           std::memcpy(&u[b], &bits, 8);
         }
         std::vector<double> srt(u);

@@ -1585,7 +1585,7 @@ __global__ __launch_bounds__(kWave) void k_block_ub(const uint32_t* __restrict__
   constexpr uint32_t S2 = k2sum_stride(K), GS = gtab_stride(K), BW = kbub_stride(K) / 4u;
   const uint32_t b = blockIdx.x, n = b * 64u + threadIdx.x;
   const bool v = n < n_nodes;
-  uint32_t* o = out + (size_t)b * BW;
+  auto o_at = [&](uint32_t w) -> uint32_t& { return out[sum_index(b, w, 4u * BW)]; };
   double stat = -1.0;
   uint32_t cnt = 0;
   if (v) {
@@ -1602,15 +1602,15 @@ __global__ __launch_bounds__(kWave) void k_block_ub(const uint32_t* __restrict__
     for (int off = 32; off > 0; off >>= 1) u = fmax(u, __shfl_xor(u, off, kWave));
     if (threadIdx.x == 0) {
       const uint64_t ub = (uint64_t)__double_as_longlong(u);
-      o[2 * j] = (uint32_t)ub;
-      o[2 * j + 1] = (uint32_t)(ub >> 32);
+      o_at(2 * j) = (uint32_t)ub;
+      o_at(2 * j + 1) = (uint32_t)(ub >> 32);
     }
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const uint32_t f = v ? sum2[sum_index(n, kS2Fs + (uint32_t)k, S2)] : 0u;
     const uint32_t fm = wave_max_u32(f);
-    if (threadIdx.x == 0) o[kbub_fmax(K) + k] = fm;
+    if (threadIdx.x == 0) o_at(kbub_fmax(K) + k) = fm;
   }
 }
 
@@ -2051,7 +2051,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // TOPK (greedy windows): a block whose best possible key cannot beat any active lane's
   // k-th key (thrk: the min over active lanes of their own and the U list's k-th) is skipped.
   const bool prune = args.kbub != nullptr && use_g;
-  constexpr uint32_t KBW = kbub_stride(K) / 4u;
+  constexpr uint32_t KBST = kbub_stride(K);
   double thr = -1.0;
   uint64_t thrk = 0ull;
 
@@ -2083,26 +2083,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // One block: the wave's mask of node nb + lane and its summary (kept for the per-pod pass,
   // read back with v_readlane), loaded together: one memory latency per block.
   bool worked = false;  // the last block() call did the block's work (not pruned / empty)
+  // a block's bound for this wave (kbub_*): J = the most cards any pod of the wave can
+  // qualify on any node of it (from the block's largest frees and the wave's smallest
+  // scv/memory), ub = static + B_G[J] maximised over the block's nodes
+  auto block_ub = [&](uint32_t b) -> double {
+    const uint32_t* U = args.kbub;
+    uint32_t J = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      J += U[sum_index(b, kbub_fmax(K) + (uint32_t)k, KBST)] >= m_min ? 1u : 0u;
+    return __longlong_as_double((long long)((uint64_t)U[sum_index(b, 2 * J, KBST)] |
+                                            ((uint64_t)U[sum_index(b, 2 * J + 1, KBST)] << 32)));
+  };
+  auto pruned = [&](double ub) -> bool {
+    if constexpr (TOPK) {  // (ub: an integer-valued double >= 0)
+      return ((((uint64_t)ub) << ib) | (uint64_t)imax) <= thrk;
+    } else {
+      return ub < thr;
+    }
+  };
   auto block = [&](uint32_t nb) {
     worked = false;
-    if (prune) {
-      const uint32_t* U = args.kbub + (size_t)(nb >> 6) * KBW;
-      uint32_t J = 0;
-#pragma unroll
-      for (int k = 0; k < K; ++k) J += U[kbub_fmax(K) + (uint32_t)k] >= m_min ? 1u : 0u;
-      const double ub =
-          __longlong_as_double((long long)((uint64_t)U[2 * J] | ((uint64_t)U[2 * J + 1] << 32)));
-      bool skip;
-      if constexpr (TOPK) {  // (ub: an integer-valued double >= 0)
-        skip = ((((uint64_t)ub) << ib) | (uint64_t)imax) <= thrk;
-      } else {
-        skip = ub < thr;
-      }
-      if (skip) {
-        if (STATS && !trace && lane == 0) atomicAdd(stats + 13, 1ull);
-        return;
-      }
-    }
     const uint32_t n = nb + lane;
     const bool valid0 = n < n1;
     const uint32_t nid = (args.ids && valid0) ? args.ids[n] : n;
@@ -2514,9 +2515,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       if (b0 > base) bits &= ~0ull << (b0 - base);
       if (b1 < base + 64) bits &= (1ull << (b1 - base)) - 1ull;
       if (passes == 2) bits &= pass == 0 ? args.hot[wi] : ~args.hot[wi];
+      // the bounds of the word's 64 blocks, lane = block (one coalesced pass; a block is
+      // then skipped on a v_readlane and a compare against the current threshold)
+      double ub_l = 0.0;
+      if (prune && bits != 0ull) ub_l = block_ub(min(base + lane, b1 - 1u));
       while (bits) {
         const uint32_t j = (uint32_t)__builtin_ctzll(bits);
         bits &= bits - 1;
+        if (prune) {
+          const uint64_t ubb = (uint64_t)__double_as_longlong(ub_l);
+          const double ub = __longlong_as_double(
+              (long long)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ubb >> 32), (int)j) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ubb, (int)j)));
+          if (pruned(ub)) {
+            if (STATS && !trace && lane == 0) atomicAdd(stats + 13, 1ull);
+            continue;
+          }
+        }
         block((base + j) << 6);
         if (prune && worked && TOPK) {  // every active lane's k-th key so far
           const uint64_t kth = act ? (pl[TL - 1] > ul[TL - 1] ? pl[TL - 1] : ul[TL - 1]) : ~0ull;

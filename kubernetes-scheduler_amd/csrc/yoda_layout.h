@@ -139,7 +139,8 @@ constexpr uint32_t kBsOneModel = 1u, kBsUni4 = 2u;
 __host__ __device__ constexpr uint32_t bsum_stride(int k) { return 4u * (kBsT + 2u * (uint32_t)k); }
 
 // K2 block bounds (N32 path; waves whose reciprocals are the G table's): per 64-node block of a
-// summary order, u32 words (kbub_stride(K) bytes a block):
+// summary order, u32 words (kbub_stride(K) bytes a block), in tiles of 64 blocks word-major
+// (sum_index(block, word, kbub_stride(K))) so that a wave reads 64 blocks' bounds coalesced:
 //   ub[j]    (f64, words 2j, 2j + 1; j = 0..K)  the max over the block's real nodes of
 //            static + B_G[min(j, len(CardList))] -- no pod with at most j qualifying cards on
 //            every node of the block scores more there (basic <= B_G[nq], nq <= j)
