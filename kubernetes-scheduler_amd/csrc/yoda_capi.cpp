@@ -33,7 +33,7 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                      uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                      uint32_t n_pods, const Partials& part, uint64_t* bm, uint32_t bm_stride,
                      BlockMask* bs, uint32_t bs_stride, uint64_t* blk, uint32_t blk_stride,
-                     unsigned long long* stats, hipStream_t s);
+                     unsigned long long* stats, hipStream_t s, uint32_t sub);
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool narrow,
                           uint64_t* maxima, uint32_t* counts, double* rcp, float* rcp32,
                           const MemTab& mt, hipStream_t s);
@@ -95,7 +95,8 @@ hipError_t launch_reduce3(const Partials& part, uint32_t C, const uint32_t* flag
                           const uint32_t* n_flagged, uint32_t max_flagged, uint32_t node_offset,
                           int32_t* pick, int32_t* status, uint32_t* ties, hipStream_t s);
 hipError_t launch_bitmask_transpose(const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
-                                    uint32_t bs_stride, uint32_t n_nodes,
+                                    uint32_t bs_stride, const uint64_t* blk, uint32_t blk_stride,
+                                    uint32_t n_nodes,
                                     uint32_t W, uint32_t n_pods, const uint32_t* perm,
                                     uint32_t* out, hipStream_t s);
 int kernel_capacity(int K, Path path, int which, int mode_diskio);
@@ -103,8 +104,9 @@ hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t
                           uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                           const double* rcp, const float* rcp32, uint32_t n_pods,
                           const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
-                          uint32_t bs_stride, const Partials& part,
-                          double* tk_s, uint32_t* tk_i, int tk, hipStream_t s);
+                          uint32_t bs_stride, const uint64_t* blk, uint32_t blk_stride,
+                          const Partials& part, double* tk_s, uint32_t* tk_i, int tk,
+                          hipStream_t s);
 hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t C,
                              uint32_t n_pods, uint32_t node_offset, double* out_s,
                              uint32_t* out_i, int tk, hipStream_t s);
@@ -136,8 +138,8 @@ hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes,
                              const unsigned char* sum2, uint32_t n_nodes,
                              const PodParams& pp, const double* rcp, const float* rcp32,
                              uint32_t n_pods, uint32_t s, const uint64_t* bm, uint32_t bm_stride,
-                             const BlockMask* bs, uint32_t bs_stride,
-                             double* part_s, uint32_t* part_i, uint32_t* done, uint32_t* out,
+                             const BlockMask* bs, uint32_t bs_stride, const uint64_t* blk,
+                             uint32_t blk_stride, double* part_s, uint32_t* part_i, uint32_t* done, uint32_t* out,
                              hipStream_t st);
 hipError_t launch_k1_witness(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                              uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
@@ -418,6 +420,9 @@ struct yoda_handle {
   DevBuf bsum;              // [wave][node block] BlockMask: the block K1's sparse masks
   bool bm_sparse = false;   // the last K1 wrote the sparse form (bsum + partial masks only)
   const BlockMask* bs_ptr() const { return bm_sparse ? bsum.as<BlockMask>() : nullptr; }
+  // the sparse masks' block list: a block whose bit is clear has no feasible pod of the wave
+  // and its BlockMask was not written this run
+  const uint64_t* blk_ptr() const { return bm_sparse ? blk.as<uint64_t>() : nullptr; }
   // greedy
   DevBuf tk_s_part, tk_i_part, tk_s, tk_i, upd_node, upd_val, upd_cn;
   DevBuf g1_part, g1_done;  // k_greedy_one partials + block counter (zeroed once)
@@ -436,7 +441,8 @@ struct yoda_handle {
   double greedy_prep_ms = 0;  // (YODA_GREEDY_DEBUG) the host part of the windows: state push,
                               // window gather + pod upload + order launches
   DevBuf p_max_u, p_cnt, p_best_f, p_best_i, p_idx, p_ties, p_low_f, p_low_i, p_err;
-  uint32_t C1 = 1, chunk1 = 32;  // K1 node chunking
+  uint32_t C1 = 1, chunk1 = 32;  // K1 node chunking (partial chunks; chunk1: nodes per K1 wave)
+  uint32_t k1_sub = 1;           // K1 waves per chunk (4: k1_block_n32's SUB, chunk1 = a quarter)
   uint32_t C2 = 1, chunk2 = 32;  // K2 / K3 node chunking
   int cap[2][3][2] = {};         // resident workgroups per (kernel, path, mode), cached
   int last_mode = -1;
@@ -704,11 +710,26 @@ void plan_chunks(yoda_t* h, int mode, uint32_t n_pods, uint32_t n_nodes) {
       h->C1 = (h->C1 + 7) / 8 * 8;
     }
   }
+  // YODA_K1_SUB=4 (A/B knob, off): the block K1 with SUB = 4 -- the same (pod wave, node range)
+  // tasks, the four waves of a workgroup on quarters of one chunk merging their partials in
+  // LDS: a quarter of the partial bytes, but K1 0.284-0.289 against 0.230-0.235 ms (the four
+  // waves no longer share the node tiles in L1).  C1 becomes the chunk count, chunk1 the quarter.
+  static const bool k1_split = YODA_KNOB("YODA_K1_SUB", 1) == 4;
+  h->k1_sub = 1;
+  if (k1_split && h->path == Path::N32 && h->has_k1sum && mode != YODA_MODE_DISKIO &&
+      h->C1 >= 4) {
+    uint32_t C = (h->C1 + 3) / 4;
+    if (C >= 8) C = (C + 7) / 8 * 8;
+    const uint32_t q = (n_nodes + 4 * C - 1) / (4 * C);
+    h->chunk1 = std::max<uint32_t>(kChunkAlign, (q + kChunkAlign - 1) / kChunkAlign * kChunkAlign);
+    h->C1 = C >= 8 ? C : std::max<uint32_t>(1, (n_nodes + 4 * h->chunk1 - 1) / (4 * h->chunk1));
+    h->k1_sub = 4;
+  }
   plan_chunks_for((uint32_t)capacity(h, 2, mode), r2, n_pods, n_nodes, &h->C2, &h->chunk2);
 }
 
 int ensure_state(yoda_t* h, uint32_t P) {
-  const size_t CP = (size_t)std::max(h->C1, h->C2) * P;
+  const size_t CP = (size_t)std::max(h->C1 * h->k1_sub, h->C2) * P;
   HIP_TRY(h, h->maxima.ensure(6 * (size_t)P * 8));
   HIP_TRY(h, h->counts.ensure(2 * (size_t)P * 4));
   HIP_TRY(h, h->rcp.ensure(5 * (size_t)P * 8));
@@ -1105,7 +1126,8 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_m
                        h->kmix.as<unsigned char>(), h->n_nodes,
                        h->chunk1, h->C1, pod_params(h), P, part, h->bitmask.as<uint64_t>(),
                        bm_row(h->n_nodes), h->bsum.as<BlockMask>(), bs_row(h->n_nodes),
-                       h->blk.as<uint64_t>(), blk_row(h->n_nodes), h->stats_ptr(), h->stream));
+                       h->blk.as<uint64_t>(), blk_row(h->n_nodes), h->stats_ptr(), h->stream,
+                       h->k1_sub));
   if (h->class_stats && h->has_k1sum) h->stats_pairs1 += (uint64_t)(P + 63) / 64 * h->n_nodes;
   if (e1) {
     HIP_TRY(h, hipEventRecord(e1, h->stream));
@@ -1140,10 +1162,11 @@ int phase1_witness(yoda_t* h, uint64_t* maxima, uint32_t* counts, uint32_t* wit,
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     return YODA_OK;
   }
-  HIP_TRY(h, h->p_wit.ensure(12 * (size_t)h->C1 * P * 4));
+  // (the witness K1s run one wave per node range: chunk1 nodes each, C1 * k1_sub of them)
+  uint32_t C = h->C1 * h->k1_sub;
+  HIP_TRY(h, h->p_wit.ensure(12 * (size_t)C * P * 4));
   Partials part = partials(h);
   static const bool block_wit = YODA_KNOB("YODA_BLOCK_WITNESS", 1) != 0;
-  uint32_t C = h->C1;
   if (block_wit && h->path == Path::N32 && h->has_k1sum && h->has_k2sum && h->all_one_model) {
     // block-classified, like phase 1's K1: sparse masks and the block list for the window's K2.
     // Its per-(wave, chunk) epilogue (18 wave reductions, 104 B of partials a pod) is the
@@ -1167,7 +1190,7 @@ int phase1_witness(yoda_t* h, uint64_t* maxima, uint32_t* counts, uint32_t* wit,
                                        h->bsum.as<BlockMask>(), bs_row(N), h->blk.as<uint64_t>(),
                                        blk_row(N), h->stream));
   } else {
-    HIP_TRY(h, launch_k1_witness(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk1, h->C1,
+    HIP_TRY(h, launch_k1_witness(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk1, C,
                                  pod_params(h), P, part.max_u, h->p_wit.as<uint32_t>(), part.cnt,
                                  h->bitmask.as<uint64_t>(), bm_row(N), h->stream));
   }
@@ -1385,7 +1408,7 @@ int topk_lists(yoda_t* h, uint32_t P, uint32_t KT, const uint32_t* d_counts) {
   HIP_TRY(h, launch_k2_topk(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk2, h->C2,
                             pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(), P,
                             h->bitmask.as<uint64_t>(), bm_row(N), h->bs_ptr(), bs_row(N),
-                            partials(h), h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),
+                            h->blk_ptr(), blk_row(N), partials(h), h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),
                             (int)KT, h->stream));
   HIP_TRY(h, launch_topk_merge(h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(), h->C2, P,
                                h->node_offset, h->tk_s.as<double>(), h->tk_i.as<uint32_t>(),
@@ -2483,7 +2506,8 @@ int yoda_download_bitmask(yoda_t* h, uint32_t* words, uint64_t n_words) {
   HIP_TRY(h, hipSetDevice(h->device));
   HIP_TRY(h, h->bitmask_t.ensure(need * 4));
   HIP_TRY(h, launch_bitmask_transpose(h->bitmask.as<uint64_t>(), bm_row(h->n_nodes), h->bs_ptr(),
-                                      bs_row(h->n_nodes), h->n_nodes,
+                                      bs_row(h->n_nodes), h->blk_ptr(), blk_row(h->n_nodes),
+                                      h->n_nodes,
                                       W, h->n_pods,
                                       h->ordered ? h->perm.as<uint32_t>() : nullptr,
                                       h->bitmask_t.as<uint32_t>(), h->stream));
@@ -2983,7 +3007,8 @@ int greedy_eval_fast(GreedyState& g, uint32_t s, int32_t* pick_out) {
                                h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr, h->n_nodes,
                                pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(),
                                h->n_pods, s, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
-                               h->bs_ptr(), bs_row(h->n_nodes), ps, pi, done,
+                               h->bs_ptr(), bs_row(h->n_nodes), h->blk_ptr(),
+                               blk_row(h->n_nodes), ps, pi, done,
                                static_cast<uint32_t*>(h->poll_stage.dp) + 1, h->stream));
   {
     const auto t0 = std::chrono::steady_clock::now();
@@ -3563,7 +3588,8 @@ int yoda_shard_best_one(yoda_t* h, uint32_t pod, double* score, int32_t* node) {
                                h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr, h->n_nodes,
                                pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(),
                                h->n_pods, s, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
-                               h->bs_ptr(), bs_row(h->n_nodes), ps, pi, done, done + 1, h->stream));
+                               h->bs_ptr(), bs_row(h->n_nodes), h->blk_ptr(),
+                               blk_row(h->n_nodes), ps, pi, done, done + 1, h->stream));
   HIP_TRY(h, h->pick_stage.ensure(16));
   HIP_TRY(h, hipMemcpyAsync(h->pick_stage.p, done, 16, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(h, hipStreamSynchronize(h->stream));

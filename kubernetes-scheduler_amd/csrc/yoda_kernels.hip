@@ -583,7 +583,17 @@ __global__ __launch_bounds__(kWave) void k_reduce_wit(const uint64_t* __restrict
 // WIT (capacity greedy windows, with MIX = false): also the witnesses of every maximum (how
 // many nodes reach it, the lowest one; k1_witness's outputs), in k1_witness's partial layout:
 // pmax [6][C][P] u64, pwit [2][6][C][P], pcnt [2][C][P].
-template <int K, bool STATS, bool MIX = true, bool WIT = false>
+// Packed N32 partial word w (k1_block_n32's epilogue) -> the MaxValue fields it holds:
+// w 0: bandwidth | clock << 16, w 1: core | power << 16 (per-half max), w 2: free, w 3: total.
+__device__ __forceinline__ uint32_t narrow_max(uint32_t a, uint32_t b, int w) {
+  return w < 2 ? max16x2(a, b) : max(a, b);
+}
+
+// SUB = 4 (the argmax runs): the workgroup's four waves hold the SAME 64 pods, each over its own
+// quarter of the chunk (chunk_nodes = the quarter), and merge their partials in LDS at the end:
+// a quarter of the partial bytes (and of k_reduce1's reads) for the same (wave, node-range)
+// tasks -- 24 B per (pod, chunk) written once per chunk instead of once per quarter.
+template <int K, bool STATS, bool MIX = true, bool WIT = false, int SUB = 1>
 #ifndef YODA_K1_WAVES
 #define YODA_K1_WAVES 7
 #endif
@@ -600,6 +610,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     unsigned long long* __restrict__ stats, uint32_t* __restrict__ pwit = nullptr,
     const uint32_t* __restrict__ bsm = nullptr) {
   static_assert(!(WIT && MIX), "the witness K1 serves one-model snapshots");
+  static_assert(SUB == 1 || (SUB == kBlock / kWave && !WIT), "SUB: 1, or one pod wave per workgroup");
   constexpr uint32_t SS = k1sum_stride(K);
   constexpr uint32_t NS = n32_stride(K);
   constexpr uint32_t S2 = k2sum_stride(K), MS = mix_stride(K), XS = x1_stride(K);
@@ -610,13 +621,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   uint32_t* lds = lds_all[threadIdx.x >> 6];
   const uint32_t lane = lane_id();
   const Tile tl = tile();
-  const uint32_t p = tl.pb * kBlock + threadIdx.x;
+  const uint32_t sub = SUB > 1 ? threadIdx.x >> 6 : 0u;
+  const uint32_t p = SUB > 1 ? tl.pb * kWave + lane : tl.pb * kBlock + threadIdx.x;
   const uint32_t chunk = tl.chunk, C = gridDim.y;
-  const uint32_t n0 = chunk * chunk_nodes;
+  const uint32_t n0 = (chunk * SUB + sub) * chunk_nodes;
   const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
   const bool live = p < n_pods;
   const uint64_t live_mask = ballot(live);
-  if (live_mask == 0) return;  // a wave past the batch: no bitmask row, no partials
+  // a wave past the batch: no bitmask row, no partials (SUB: the whole workgroup, together)
+  if (live_mask == 0) return;
   uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
   BlockMask* bsw = bs + (size_t)uniform_u32(p >> 6) * bs_stride;
   // STATS with stats[15] == 2: per-(wave, chunk) timing trace only (no counter atomics)
@@ -693,8 +706,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
 #ifndef YODA_K1_PF
 #define YODA_K1_PF 0
 #endif
-  // the summary words a block's classification reads (YODA_K1_PF: the next block's are loaded
-  // while this one is classified -- the loop is otherwise one memory latency per block)
+  // the summary words a block's classification reads (YODA_K1_PF = 1: the next block
+  // node_block visits is loaded while this one is classified; off: the extra live registers
+  // spill, K1 0.211-0.219 ms without against 0.230-0.235 with, same box)
   uint4 pf0 = make_uint4(0u, 0u, 0u, 0u), pf1 = pf0;
   uint32_t pf_pw = 0, pf_ta = 0, pf_tn = 0;
   auto load_sum = [&](uint32_t nb) {
@@ -705,7 +719,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     pf_ta = s[64 * hfs_all];
     pf_tn = s[64 * hfs_none];
   };
-  if (YODA_K1_PF && n0 < n1) load_sum(n0);
   // Whole-block decisions from the block summaries (BlockSumWord, scalar reads): the bounds
   // of the block's nodes against the wave's bounds prove every node NONE, or every node ALL
   // with one contribution (all qualifying: the block's maxima; none qualifying: nothing).
@@ -718,7 +731,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   const uint32_t bs_ta = kBsT + (any_pm && hfs_all_ok && nm_max > 0u ? nm_max - 1u : 0u);
   // per-node classification of one 64-node block (below: only the blocks the block summaries
   // leave undecided)
-  auto node_block = [&](uint32_t nb) {
+  // (nxt: the block node_block visits next, whose summary words are loaded here -- the
+  // caller loaded nb's before the first call; ~0u: none)
+  auto node_block = [&](uint32_t nb, uint32_t nxt) {
     const uint32_t n = nb + lane;
     const bool valid = n < n1;
     // this block's tile of summaries (nb is a multiple of 64): word w at s[64 w]
@@ -726,7 +741,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     if (!YODA_K1_PF) load_sum(nb);
     const uint4 w0 = pf0, w1 = pf1;
     const uint32_t pw0 = pf_pw, t_all = pf_ta, t_none = pf_tn;
-    if (YODA_K1_PF && nb + kWave < n1) load_sum(nb + kWave);
+    if (YODA_K1_PF && nxt != ~0u) load_sum(nxt);
     if (!need_uni) {  // the node's healthy frees for the per-pod pass: lds[node][need - 1] (slot K: 0)
 #pragma unroll
       for (int t = 0; t < K; ++t) lds[lane * HW + t] = s[64 * (kSumHfs + t)];
@@ -987,8 +1002,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     const uint64_t mine = ((uint64_t)hi << 32) | lo;
     const bool nzl = valid && mine != 0ull, fulll = nzl && mine == live_mask;
     const uint64_t nz_b = ballot(nzl), full_b = ballot(fulll);
+#ifndef YODA_ABL_K1_NOBM  // (write-traffic ablations: timing/counter builds only, wrong masks)
     if (nzl && !fulll) bmw[nb + lane] = mine;
-    if (lane == 0) bsw[nb >> 6] = BlockMask{nz_b, full_b};
+#endif
+#ifndef YODA_ABL_K1_NOBS
+    // (a block with no feasible pod stays out of the block list and its BlockMask unwritten:
+    // every reader checks the list first)
+    if (lane == 0 && nz_b != 0ull) bsw[nb >> 6] = BlockMask{nz_b, full_b};
+#endif
     if (nz_b != 0) {
       const uint32_t bi = nb >> 6;
       if ((bi >> 6) != blk_wi) {
@@ -1036,10 +1057,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
       bnone = bnone && bv && nreal > 0u;
       ball = ball && bv && nreal > 0u;
       const uint64_t none_m = ballot(bnone), all_m = ballot(ball);
-      if (bnone || ball) {
+#ifndef YODA_ABL_K1_NOBS
+      if (ball) {  // (NONE blocks: unlisted, unwritten)
         const uint64_t vb = nreal >= 64u ? ~0ull : ((1ull << nreal) - 1ull);
-        bsw[bi] = ball ? BlockMask{vb, vb} : BlockMask{0ull, 0ull};
+        bsw[bi] = BlockMask{vb, vb};
       }
+#endif
       if (ball) {
         g_nf += nreal;
         g_nz += B[64 * kBsNzt];
@@ -1091,14 +1114,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
         }
       }
       uint64_t und = ballot(bv && nreal > 0u) & ~(none_m | all_m);
+      if (YODA_K1_PF && und) load_sum((g + (uint32_t)__builtin_ctzll(und)) << 6);
       while (und) {
         const uint32_t j = (uint32_t)__builtin_ctzll(und);
         und &= und - 1;
-        node_block((g + j) << 6);
+        node_block((g + j) << 6, und ? (g + (uint32_t)__builtin_ctzll(und)) << 6 : ~0u);
       }
     }
   } else {
-    for (uint32_t nb = n0; nb < n1; nb += kWave) node_block(nb);
+    if (YODA_K1_PF && n0 < n1) load_sum(n0);
+    for (uint32_t nb = n0; nb < n1; nb += kWave) node_block(nb, nb + kWave < n1 ? nb + kWave : ~0u);
   }
 #pragma unroll
   for (int o = kWave / 2; o > 0; o >>= 1) {
@@ -1109,7 +1134,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   nz_all += g_nz;
   blk_flush();
   if (trace && lane == 0) {
-    unsigned long long* tr = stats + 16 + 4 * ((size_t)(p >> 6) * C + chunk);
+    unsigned long long* tr = stats + 16 + 4 * (((size_t)(p >> 6) * C + chunk) * SUB + sub);
     tr[0] = t_start;
     tr[1] = wall_clock64();
     tr[2] = npart;
@@ -1155,7 +1180,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   a_free = wave_max_u32(a_free);
   a_pw = wave_max_u32(a_pw);
   a_tot = wave_max_u32(a_tot);
-  if (!live) return;
+  if (SUB == 1 && !live) return;  // (lane 0 is live: the live lanes are a prefix)
   mx[kMaxBw] = max(mx[kMaxBw], a_bw);
   mx[kMaxClock] = max(mx[kMaxClock], a_ck);
   mx[kMaxCore] = max(mx[kMaxCore], a_core);
@@ -1167,14 +1192,37 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   // N32: packed u32 partials (k_reduce1<true>), [kNarrowWords][C][P]: bandwidth | clock << 16,
   // core | power << 16 (each <= 55738 on this path), FreeMemory, TotalMemory (u32 codes)
   uint32_t* pmax32 = reinterpret_cast<uint32_t*>(pmax);
-  const uint32_t pw4[kNarrowWords] = {mx[kMaxBw] | (mx[kMaxClock] << 16),
-                                      mx[kMaxCore] | (mx[kMaxPower] << 16), mx[kMaxFree],
-                                      mx[kMaxTotal]};
+  uint32_t pw4[kNarrowWords] = {mx[kMaxBw] | (mx[kMaxClock] << 16),
+                                mx[kMaxCore] | (mx[kMaxPower] << 16), mx[kMaxFree],
+                                mx[kMaxTotal]};
+  if constexpr (SUB > 1) {
+    // the quarters' partials through LDS (each wave's own region, free after its loop);
+    // wave 0 folds them and writes the chunk's
+    static_assert(RECS + kWave * REC >= (kNarrowWords + 2) * kWave, "LDS merge area");
+#pragma unroll
+    for (int f = 0; f < kNarrowWords; ++f) lds[f * kWave + lane] = pw4[f];
+    lds[kNarrowWords * kWave + lane] = nf;
+    lds[(kNarrowWords + 1) * kWave + lane] = nz;
+    __syncthreads();
+    if (sub != 0u || !live) return;
+#pragma unroll
+    for (int w = 1; w < SUB; ++w) {
+      const uint32_t* o = lds_all[w];
+#pragma unroll
+      for (int f = 0; f < kNarrowWords; ++f) pw4[f] = narrow_max(pw4[f], o[f * kWave + lane], f);
+      nf += o[kNarrowWords * kWave + lane];
+      nz += o[(kNarrowWords + 1) * kWave + lane];
+    }
+  }
+#ifdef YODA_ABL_K1_NOPART  // (write-traffic ablation: no partial stores)
+  return;
+#endif
 #pragma unroll
   for (int f = 0; f < kNarrowWords; ++f) pmax32[((size_t)f * C + chunk) * n_pods + p] = pw4[f];
   pcnt[((size_t)0 * C + chunk) * n_pods + p] = nf;
   pcnt[((size_t)1 * C + chunk) * n_pods + p] = nz;
 }
+
 
 // feasibility of (pod p, node n) in the [wave][node] bitmask
 __device__ __forceinline__ bool bm_bit(const uint64_t* __restrict__ bm, uint32_t bm_stride,
@@ -1194,12 +1242,19 @@ struct MaskSrc {
   const uint64_t* bm;
   const BlockMask* bs;
   uint32_t bm_stride, bs_stride;
+  const uint64_t* blk;  // with bs: the wave's block list (a clear bit: no feasible pod, and
+  uint32_t blk_stride;  // the block's BlockMask was not written this run)
 };
+__device__ __forceinline__ bool blk_listed(const uint64_t* blk, uint32_t blk_stride, uint32_t w,
+                                           uint32_t b) {
+  return (blk[(size_t)w * blk_stride + (b >> 6)] >> (b & 63u)) & 1ull;
+}
 
 // Mask of (wave w, node n) for a thread that reads single masks (not the hot kernels).
 __device__ __forceinline__ uint64_t mask_at(const MaskSrc& m, uint32_t w, uint32_t n,
                                             uint32_t n_pods) {
   if (!m.bs) return m.bm[(size_t)w * m.bm_stride + n];
+  if (!blk_listed(m.blk, m.blk_stride, w, n >> 6)) return 0ull;
   const BlockMask b = m.bs[(size_t)w * m.bs_stride + (n >> 6)];
   const uint32_t j = n & 63u;
   if ((b.full >> j) & 1ull) return wave_live(w, n_pods);
@@ -1214,12 +1269,7 @@ __device__ __forceinline__ double ru_100_over(double M);
 __device__ __forceinline__ float ru32_100_over(double M);
 
 // rcp != nullptr (a single-handle run, whose maxima are final here): each maxima thread also
-// writes its field's reciprocals (k_prep2's, fused).
-// Packed N32 partial word w (k1_block_n32's epilogue) -> the MaxValue fields it holds:
-// w 0: bandwidth | clock << 16, w 1: core | power << 16 (per-half max), w 2: free, w 3: total.
-__device__ __forceinline__ uint32_t narrow_max(uint32_t a, uint32_t b, int w) {
-  return w < 2 ? max16x2(a, b) : max(a, b);
-}
+// writes its field's reciprocals (k_prep2's, fused).  Packed partial words: narrow_max.
 __device__ __forceinline__ void narrow_store(uint32_t v, int w, uint32_t n_pods, uint32_t p,
                                             uint64_t* maxima, const MemTab& mt) {
   auto put = [&](int f, uint64_t x) {
@@ -1866,6 +1916,7 @@ __global__ __launch_bounds__(kBlock) void k2_score(
     // node's own mask is one more scalar load
     const BlockMask* bsw = ms.bs + (size_t)w * ms.bs_stride;
     for (uint32_t nb = n0; nb < n1; nb += kWave) {
+      if (!blk_listed(ms.blk, ms.blk_stride, w, nb >> 6)) continue;
       const BlockMask bk = bsw[nb >> 6];
       uint64_t bits = bk.nz;
       while (bits) {
@@ -4055,39 +4106,36 @@ __global__ __launch_bounds__(kBlock) void k_bitmask_transpose(const MaskSrc ms,
 
 
 
+// sub (block K1 only): 1, or 4 = one pod wave per workgroup over four quarters of each
+// chunk, chunk_nodes then being the quarter (k1_block_n32's SUB).
 hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigned char* sum,
                      const unsigned char* sum2, const unsigned char* mix, uint32_t n_nodes, uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                      uint32_t n_pods, const Partials& part, uint64_t* bm, uint32_t bm_stride,
                      BlockMask* bs, uint32_t bs_stride, uint64_t* blk, uint32_t blk_stride,
-                     unsigned long long* stats, hipStream_t s) {
+                     unsigned long long* stats, hipStream_t s, uint32_t sub) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   switch (path) {
     case Path::N32:
       if (sum) {
-        if (stats)
-          YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK, true>), grid, dim3(kBlock), 0, s,
-                                              nodes, sum, reinterpret_cast<const uint32_t*>(sum2),
-                                              reinterpret_cast<const uint32_t*>(mix), pp.x1, n_nodes,
-                                              chunk_nodes, pp.m_32, pp.c_32,
-                                              pp.number, pp.need_mem, pp.need_clk, n_pods,
-                                              part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,
-                                              blk, blk_stride, stats, nullptr, pp.bsum))
-        else if (pp.one_model)
-          YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK, false, false>), grid, dim3(kBlock), 0, s,
-                                              nodes, sum, reinterpret_cast<const uint32_t*>(sum2),
-                                              reinterpret_cast<const uint32_t*>(mix), pp.x1, n_nodes,
-                                              chunk_nodes, pp.m_32, pp.c_32,
-                                              pp.number, pp.need_mem, pp.need_clk, n_pods,
-                                              part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,
-                                              blk, blk_stride, stats, nullptr, pp.bsum))
-        else
-          YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<KK, false>), grid, dim3(kBlock), 0, s,
-                                              nodes, sum, reinterpret_cast<const uint32_t*>(sum2),
-                                              reinterpret_cast<const uint32_t*>(mix), pp.x1, n_nodes,
-                                              chunk_nodes, pp.m_32, pp.c_32,
-                                              pp.number, pp.need_mem, pp.need_clk, n_pods,
-                                              part.max_u, part.cnt, bm, bm_stride, bs, bs_stride,
-                                              blk, blk_stride, stats, nullptr, pp.bsum));
+        if (sub != 1u && sub != (uint32_t)(kBlock / kWave)) return hipErrorInvalidValue;
+        const dim3 g1 = sub == 1u ? grid : dim3((n_pods + kWave - 1) / kWave, C);
+#define YODA_K1B(...)                                                                          \
+  YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_block_n32<__VA_ARGS__>), g1, dim3(kBlock), 0, s, nodes, \
+                                      sum, reinterpret_cast<const uint32_t*>(sum2),            \
+                                      reinterpret_cast<const uint32_t*>(mix), pp.x1, n_nodes,  \
+                                      chunk_nodes, pp.m_32, pp.c_32, pp.number, pp.need_mem,   \
+                                      pp.need_clk, n_pods, part.max_u, part.cnt, bm, bm_stride, \
+                                      bs, bs_stride, blk, blk_stride, stats, nullptr, pp.bsum))
+        if (sub == 1u) {
+          if (stats) YODA_K1B(KK, true)
+          else if (pp.one_model) YODA_K1B(KK, false, false)
+          else YODA_K1B(KK, false)
+        } else {
+          if (stats) YODA_K1B(KK, true, true, false, kBlock / kWave)
+          else if (pp.one_model) YODA_K1B(KK, false, false, false, kBlock / kWave)
+          else YODA_K1B(KK, false, true, false, kBlock / kWave)
+        }
+#undef YODA_K1B
       } else {
         YODA_K_SWITCH(K, hipLaunchKernelGGL((k1_filter_maxima<KK, Path::N32>), grid, dim3(kBlock),
                                             0, s, nodes, n_nodes, chunk_nodes, pp.m_32, pp.c_32,
@@ -4219,7 +4267,8 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g, pp.mix, pp.mt,
                     pp.ids, OUT == OUT_ARGMAX ? pp.kbub : nullptr,
                     OUT == OUT_ARGMAX ? pp.hot : nullptr};
-  const MaskSrc ms{bm, bs, bm_stride, bs_stride};
+  const MaskSrc ms{bm, bs, bm_stride, bs_stride, blk, blk_stride};
+  if (bs && !blk) return hipErrorInvalidValue;  // sparse masks are read through their block list
   switch (path) {
     case Path::N32:
       if (OUT == OUT_ARGMAX && sum2) {
@@ -4269,12 +4318,14 @@ hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t
                           uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
                           const double* rcp, const float* rcp32, uint32_t n_pods,
                           const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
-                          uint32_t bs_stride, const Partials& part, double* tk_s,
-                          uint32_t* tk_i, int tk, hipStream_t s) {
+                          uint32_t bs_stride, const uint64_t* blk, uint32_t blk_stride,
+                          const Partials& part, double* tk_s, uint32_t* tk_i, int tk,
+                          hipStream_t s) {
   if (tk != kTopK && tk != kTopKCap) return hipErrorInvalidValue;
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
-  const MaskSrc ms{bm, bs, bm_stride, bs_stride};
+  const MaskSrc ms{bm, bs, bm_stride, bs_stride, blk, blk_stride};
+  if (bs && !blk) return hipErrorInvalidValue;  // sparse masks are read through their block list
 #define YODA_TOPK(PTH, TKV)                                                                      \
   YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_score<KK, PTH, OUT_TOPK, TKV>), grid, dim3(kBlock), 0, \
                                       s, nodes, n_nodes, chunk_nodes, a, n_pods, ms, part.best_f, \
@@ -4304,6 +4355,7 @@ hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigne
                                 uint32_t bs_stride, const uint32_t* counts, uint64_t* keys,
                                 uint32_t ib, int tk, hipStream_t s) {
   if ((tk != kTopK && tk != kTopKCap) || K > 8 || n_pods == 0) return hipErrorInvalidValue;
+  if (bs && !blk) return hipErrorInvalidValue;  // sparse masks are read through their block list
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g, pp.mix, pp.mt,
                     nullptr, pp.kbub};
@@ -4411,12 +4463,14 @@ hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes,
                              const unsigned char* sum2, uint32_t n_nodes,
                              const PodParams& pp, const double* rcp, const float* rcp32,
                              uint32_t n_pods, uint32_t s, const uint64_t* bm, uint32_t bm_stride,
-                             const BlockMask* bs, uint32_t bs_stride, double* part_s, uint32_t* part_i, uint32_t* done, uint32_t* out,
-                             hipStream_t st) {
+                             const BlockMask* bs, uint32_t bs_stride, const uint64_t* blk,
+                             uint32_t blk_stride, double* part_s, uint32_t* part_i,
+                             uint32_t* done, uint32_t* out, hipStream_t st) {
   ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
   a.g = pp.g;
   a.mt = pp.mt;
-  const MaskSrc ms{bm, bs, bm_stride, bs_stride};
+  const MaskSrc ms{bm, bs, bm_stride, bs_stride, blk, blk_stride};
+  if (bs && !blk) return hipErrorInvalidValue;  // sparse masks are read through their block list
   const uint32_t* s2 = reinterpret_cast<const uint32_t*>(sum2);
   const dim3 grid(std::max<uint32_t>(1, std::min<uint32_t>(kGreedyOneBlocks,
                                                            (n_nodes + kBlock - 1) / kBlock)));
@@ -4445,7 +4499,7 @@ hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigne
                      uint32_t bs_stride, const Partials& part, int64_t* rows,
                      unsigned long long* stats, const uint32_t* counts, hipStream_t s) {
   if (rows)
-    return launch_k2_t<OUT_ROWS>(K, path, nodes, nullptr, nullptr, 0, n_nodes, chunk_nodes, C, pp, maxima, rcp,
+    return launch_k2_t<OUT_ROWS>(K, path, nodes, nullptr, blk, blk_stride, n_nodes, chunk_nodes, C, pp, maxima, rcp,
                                  rcp32, n_pods, bm, bm_stride, bs, bs_stride, part, rows, nullptr,
                                  nullptr, stats, counts, s);
   return launch_k2_t<OUT_ARGMAX>(K, path, nodes, sum2, blk, blk_stride, n_nodes, chunk_nodes, C, pp, maxima, rcp,
@@ -4609,12 +4663,14 @@ hipError_t launch_reduce3(const Partials& part, uint32_t C, const uint32_t* flag
 }
 
 hipError_t launch_bitmask_transpose(const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
-                                    uint32_t bs_stride, uint32_t n_nodes,
+                                    uint32_t bs_stride, const uint64_t* blk, uint32_t blk_stride,
+                                    uint32_t n_nodes,
                                     uint32_t W, uint32_t n_pods, const uint32_t* perm,
                                     uint32_t* out, hipStream_t s) {
   const uint64_t total = (uint64_t)W * n_pods;
   dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
-  const MaskSrc ms{bm, bs, bm_stride, bs_stride};
+  const MaskSrc ms{bm, bs, bm_stride, bs_stride, blk, blk_stride};
+  if (bs && !blk) return hipErrorInvalidValue;  // sparse masks are read through their block list
   hipLaunchKernelGGL(k_bitmask_transpose, grid, dim3(kBlock), 0, s, ms, n_nodes, W,
                      n_pods, perm, out);
   return hipGetLastError();
