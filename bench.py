@@ -427,8 +427,9 @@ def disclosure(y, nodes, pods, step, barrier, args) -> dict:
     timed("per_pair_kernels", nodes, pods, MODE_SCV, dict(per_node_k1=True, per_node_k2=True), 3)
     variants["per_pair_kernels"]["desc"] = "config 3 on the per-pair kernels (no block classes)"
     for name, nd, pd, mode, kw in synth.variant_workloads(
-            ["mixed50", "bytes", "u64", "c4", "het100k", "diskio", "diskio_distinct"]):
-        timed(name, nd, pd, mode, kw, 3 if name == "u64" else 5)
+            ["mixed50", "bytes", "bw1000", "f64", "u64", "c4", "het100k", "diskio",
+             "diskio_distinct"]):
+        timed(name, nd, pd, mode, kw, 3 if name in ("u64", "f64") else 5)
     out["variants"] = variants
     out["plugin_row_latency"] = row_latency(dev_index)
     return out

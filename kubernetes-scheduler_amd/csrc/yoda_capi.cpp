@@ -34,12 +34,12 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                      uint32_t n_pods, const Partials& part, uint64_t* bm, uint32_t bm_stride,
                      BlockMask* bs, uint32_t bs_stride, uint64_t* blk, uint32_t blk_stride,
                      unsigned long long* stats, hipStream_t s, uint32_t sub);
-hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool narrow,
-                          uint64_t* maxima, uint32_t* counts, double* rcp, float* rcp32,
+hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uint32_t nw,
+                          uint64_t* maxima, uint32_t* counts, double* rcp,
                           const MemTab& mt, hipStream_t s);
 hipError_t launch_mem_rank(const uint64_t* m_u, uint32_t n_pods, const MemTab& mt, uint32_t* m32,
                            hipStream_t s);
-hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
+hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp,
                         hipStream_t s);
 hipError_t launch_window_out(const uint32_t* counts, const uint64_t* maxima, const uint32_t* wit,
                              const double* tk_s, const uint32_t* tk_i, const uint32_t* perm,
@@ -47,7 +47,7 @@ hipError_t launch_window_out(const uint32_t* counts, const uint64_t* maxima, con
 hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigned char* sum2,
                      const uint64_t* blk, uint32_t blk_stride, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
-                     const double* rcp, const float* rcp32, uint32_t n_pods,
+                     const double* rcp, uint32_t n_pods,
                      const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
                      uint32_t bs_stride, const Partials& part, int64_t* rows,
                      unsigned long long* stats, const uint32_t* counts, hipStream_t s);
@@ -102,7 +102,7 @@ hipError_t launch_bitmask_transpose(const uint64_t* bm, uint32_t bm_stride, cons
 int kernel_capacity(int K, Path path, int which, int mode_diskio);
 hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                           uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
-                          const double* rcp, const float* rcp32, uint32_t n_pods,
+                          const double* rcp, uint32_t n_pods,
                           const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
                           uint32_t bs_stride, const uint64_t* blk, uint32_t blk_stride,
                           const Partials& part, double* tk_s, uint32_t* tk_i, int tk,
@@ -113,7 +113,7 @@ hipError_t launch_topk_merge(const double* tk_s, const uint32_t* tk_i, uint32_t 
 hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigned char* sum2,
                                 const uint64_t* blk, uint32_t blk_stride, uint32_t n_nodes,
                                 uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
-                                const double* rcp, const float* rcp32, uint32_t n_pods,
+                                const double* rcp, uint32_t n_pods,
                                 const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
                                 uint32_t bs_stride, const uint32_t* counts, uint64_t* keys,
                                 uint32_t ib, int tk, hipStream_t s);
@@ -136,7 +136,7 @@ int topk_k_capacity();
 uint32_t greedy_one_blocks();
 hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes,
                              const unsigned char* sum2, uint32_t n_nodes,
-                             const PodParams& pp, const double* rcp, const float* rcp32,
+                             const PodParams& pp, const double* rcp,
                              uint32_t n_pods, uint32_t s, const uint64_t* bm, uint32_t bm_stride,
                              const BlockMask* bs, uint32_t bs_stride, const uint64_t* blk,
                              uint32_t blk_stride, double* part_s, uint32_t* part_i, uint32_t* done, uint32_t* out,
@@ -406,7 +406,7 @@ struct yoda_handle {
   size_t sorted_off[kPodArrays] = {};
 
   // state
-  DevBuf maxima, counts, rcp, rcp32, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
+  DevBuf maxima, counts, rcp, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
   // scatter targets of unpermute_outputs, swapped with the buffers above after each scatter
   DevBuf pick_alt, status_alt, ties_out_alt, counts_alt, best_alt, maxima_alt;
   DevBuf bitmask, bitmask_t, rows, rows_t, norm;
@@ -442,7 +442,9 @@ struct yoda_handle {
                               // window gather + pod upload + order launches
   DevBuf p_max_u, p_cnt, p_best_f, p_best_i, p_idx, p_ties, p_low_f, p_low_i, p_err;
   uint32_t C1 = 1, chunk1 = 32;  // K1 node chunking (partial chunks; chunk1: nodes per K1 wave)
-  uint32_t k1_sub = 1;           // K1 waves per chunk (4: k1_block_n32's SUB, chunk1 = a quarter)
+  uint32_t k1_sub = 1;
+  bool pack16 = true;            // N32: the small card fields fit 16 bits (packed K1 partials)
+  bool q32 = true;               // ... and <= kF32SmallMax (the block K2's f32 quotients)           // K1 waves per chunk (4: k1_block_n32's SUB, chunk1 = a quarter)
   uint32_t C2 = 1, chunk2 = 32;  // K2 / K3 node chunking
   int cap[2][3][2] = {};         // resident workgroups per (kernel, path, mode), cached
   int last_mode = -1;
@@ -496,7 +498,7 @@ struct yoda_handle {
     DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &k1sum_p,   &k2sum_p,   &gtab_p, &blksum, &blksum_p, &kbub, &kbub_p, &hot, &hot_p,    &perm_ids,  &perm_inv,    &pod_blob,   &maxima,       &counts,
                      &pod_sorted, &perm,     &order_scratch, &order_meta, &order_hist,
                      &order_bstart, &order_slot, &order_bkt,
-                     &rcp,       &rcp32,     &best,       &idx,          &ties,
+                     &rcp,       &best,       &idx,          &ties,
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
                      &n_flagged, &bitmask,   &bitmask_t,  &blk,  &bsum, &p_max_u,      &p_cnt,
                      &rows,      &rows_t,    &norm,      &tk_s_part,  &tk_i_part,    &tk_s,
@@ -733,7 +735,6 @@ int ensure_state(yoda_t* h, uint32_t P) {
   HIP_TRY(h, h->maxima.ensure(6 * (size_t)P * 8));
   HIP_TRY(h, h->counts.ensure(2 * (size_t)P * 4));
   HIP_TRY(h, h->rcp.ensure(5 * (size_t)P * 8));
-  HIP_TRY(h, h->rcp32.ensure(3 * (size_t)P * 4));
   HIP_TRY(h, h->best.ensure((size_t)P * 8));
   HIP_TRY(h, h->idx.ensure((size_t)P * 4));
   HIP_TRY(h, h->ties.ensure((size_t)P * 4));
@@ -761,8 +762,8 @@ int ensure_state(yoda_t* h, uint32_t P) {
   return YODA_OK;
 }
 
-// gtab_aux: [G maxima 6 x u64 | G reciprocals 8 x u32]
-constexpr size_t kGTabAuxBytes = 48 + 32;
+// gtab_aux: [G maxima 6 x u64 | G reciprocals 5 x f64]
+constexpr size_t kGTabAuxBytes = 48 + 40;
 
 PodParams pod_params(yoda_t* h) {
   unsigned char* b = (h->ordered ? h->pod_sorted : h->pod_blob).as<unsigned char>();
@@ -796,6 +797,8 @@ PodParams pod_params(yoda_t* h) {
     pp.hot = pp.kbub && h->hot_ok ? h->hot_p.as<uint64_t>() : nullptr;
   }
   pp.mt = h->mem_ranks ? h->mt : MemTab{};
+  pp.nwords = h->pack16 ? kNarrowWords : kWideWords;
+  pp.q32 = h->q32;
   return pp;
 }
 
@@ -1136,9 +1139,9 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_m
   // the block-classified K1 (N32) writes u32 maxima partials; a single-handle run's maxima
   // are final, so the reduce writes the reciprocals too (phase 2 then skips k_prep2)
   const bool rcp = final_maxima && !h->generic;
-  HIP_TRY(h, launch_reduce1(part, h->C1, P, h->has_k1sum, maxima, counts,
-                            rcp ? h->rcp.as<double>() : nullptr,
-                            rcp ? h->rcp32.as<float>() : nullptr, pod_params(h).mt, h->stream));
+  HIP_TRY(h, launch_reduce1(part, h->C1, P, h->has_k1sum ? pod_params(h).nwords : 0u, maxima,
+                            counts,
+                            rcp ? h->rcp.as<double>() : nullptr, pod_params(h).mt, h->stream));
   h->rcp_ready = rcp;
   return YODA_OK;
 }
@@ -1221,7 +1224,7 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
   hipEvent_t e0 = h->profiling ? h->next_event() : nullptr;
   hipEvent_t e1 = h->profiling ? h->next_event() : nullptr;
   if (mode == YODA_MODE_SCV && !h->generic && !h->rcp_ready)
-    HIP_TRY(h, launch_prep2(maxima, P, h->rcp.as<double>(), h->rcp32.as<float>(), h->stream));
+    HIP_TRY(h, launch_prep2(maxima, P, h->rcp.as<double>(),  h->stream));
   h->rcp_ready = false;
   if (mode == YODA_MODE_DISKIO && !rows) {
     // batch path: over the batch's pod classes, then each pod takes its class's outcome
@@ -1270,7 +1273,7 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
                          h->blk_valid ? h->blk.as<uint64_t>() : nullptr, blk_row(h->n_nodes),
                          h->n_nodes,
                          h->chunk2, h->C2, pod_params(h), maxima, h->rcp.as<double>(),
-                         h->rcp32.as<float>(), P, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
+                          P, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
                          h->bs_ptr(), bs_row(h->n_nodes), part, rows, h->stats_ptr(), counts,
                          h->stream));
     if (h->class_stats && h->has_k2sum && !rows)
@@ -1394,7 +1397,7 @@ int topk_lists(yoda_t* h, uint32_t P, uint32_t KT, const uint32_t* d_counts) {
                                     h->k2sum.as<unsigned char>(),
                                     h->blk_valid ? h->blk.as<uint64_t>() : nullptr, blk_row(N), N,
                                     cht, Ct, pod_params(h), h->rcp.as<double>(),
-                                    h->rcp32.as<float>(), P, h->bitmask.as<uint64_t>(), bm_row(N),
+                                     P, h->bitmask.as<uint64_t>(), bm_row(N),
                                     h->bs_ptr(), bs_row(N), d_counts,
                                     h->tk_s_part.as<uint64_t>(), ib, (int)KT, h->stream));
     HIP_TRY(h, launch_topk_merge_keys(h->tk_s_part.as<uint64_t>(), Ct, P, ib, h->node_offset,
@@ -1406,7 +1409,7 @@ int topk_lists(yoda_t* h, uint32_t P, uint32_t KT, const uint32_t* d_counts) {
   HIP_TRY(h, h->tk_s_part.ensure(CPk * 8));
   HIP_TRY(h, h->tk_i_part.ensure(CPk * 4));
   HIP_TRY(h, launch_k2_topk(h->K, h->path, h->nodes.as<unsigned char>(), N, h->chunk2, h->C2,
-                            pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(), P,
+                            pod_params(h), h->rcp.as<double>(),  P,
                             h->bitmask.as<uint64_t>(), bm_row(N), h->bs_ptr(), bs_row(N),
                             h->blk_ptr(), blk_row(N), partials(h), h->tk_s_part.as<double>(), h->tk_i_part.as<uint32_t>(),
                             (int)KT, h->stream));
@@ -1517,6 +1520,8 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     std::vector<uint64_t> stat(N);
     std::vector<uint8_t> zt(N);
     uint64_t max_field = 0, max_small = 0, max_clock = 0, max_static = 0, max_mem = 0;
+    uint64_t max_ckq = 0;  // the largest clock quotient a card can score
+    bool all_one = true;   // every node one GPU model with one TotalMemory
     for (uint32_t i = 0; i < N; ++i) {
       bool z = false;
       const uint64_t alloc = nd->alloc_memory ? nd->alloc_memory[i] : 0;
@@ -1532,7 +1537,21 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
                               nd->card_power[k], nd->card_clock[k]});
         max_mem = std::max({max_mem, nd->card_free_memory[k], nd->card_total_memory[k]});
         max_clock = std::max(max_clock, nd->card_clock[k]);
+        // clock / MaxBandwidth (algorithm.go:283): a scored card qualifies, so MaxBandwidth is
+        // at least its own bandwidth (and 1)
+        if (nd->card_clock[k] <= kN32FieldMax)
+          max_ckq = std::max(max_ckq, nd->card_clock[k] * 100u /
+                                          std::max<uint64_t>(1, nd->card_bandwidth[k]));
       }
+      // one GPU model with one TotalMemory (the mixed-model K1 tiles pack small fields in 16 bits)
+      const size_t a = (size_t)i * KS;
+      bool one = nd->card_count[i] > 0 && !(flags & YODA_UPLOAD_NO_UNIFORM);
+      for (uint32_t j = 1; j < nd->card_count[i] && one; ++j)
+        one = nd->card_clock[a + j] == nd->card_clock[a] &&
+              nd->card_bandwidth[a + j] == nd->card_bandwidth[a] &&
+              nd->card_core[a + j] == nd->card_core[a] && nd->card_power[a + j] == nd->card_power[a] &&
+              nd->card_total_memory[a + j] == nd->card_total_memory[a];
+      all_one = all_one && one;
     }
     // per-card score <= 800 + 100*clock (five quotients <= 100, clock/MaxBandwidth <= 100*clock)
     const long double score_bound =
@@ -1548,12 +1567,19 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
                             (long double)max_actual;
       h->score_bound = b < 9.0e18L ? (uint64_t)b + 1u : ~0ull;
     }
-    // bandwidth, clock, core and power <= 55738 on EVERY shard keeps 300 x + M < 2^24 for
-    // any maxima another shard contributes (all shards run one path: yoda_amd/dist.py).
-    // Memory fields beyond 32 bits (e.g. bytes) keep the N32 path with memory RANKS in the u32
-    // fields (yoda_layout.h MemTab): every compare and max is unchanged, the values come back
-    // for the quotients and the maxima (all <= 2^44: exact in f64).
-    const bool n32_ok = f64_ok && max_small <= kN32SmallFieldMax;
+    // N32: every small card field in u32, every quotient exact in f64 (x, M < 2^32: 300 x + M
+    // < 2^53) -- the block K2 keeps the small-field quotients in f32 while those fields are
+    // <= kF32SmallMax (q32) -- the card score summed in u32: per card at most 800 + the clock
+    // quotient.  Small fields beyond that need one-model nodes (the mixed-model K1 tiles pack
+    // them in 16 bits, and the f64 block K2 is instantiated without the mixed-model rows); beyond
+    // 16 bits the K1 writes unpacked partial words (kWideWords).  Memory fields beyond 32 bits (e.g.
+    // bytes) keep the N32 path with memory RANKS in the u32 fields (yoda_layout.h MemTab):
+    // every compare and max is unchanged, the values come back for the quotients and the
+    // maxima (all <= 2^44: exact in f64).
+    const bool pack16 = max_small <= kPack16Max;
+    const bool q32 = max_small <= kF32SmallMax;
+    const bool n32_ok = f64_ok && max_small <= kN32FieldMax && (q32 || all_one) &&
+                        (uint64_t)K * (800u + max_ckq) < (1ull << 32);
     Path path = n32_ok ? Path::N32 : (f64_ok ? Path::F64 : Path::U64);
     if ((flags & YODA_UPLOAD_FORCE_F64) && path == Path::N32) path = Path::F64;
     if (flags & YODA_UPLOAD_FORCE_GENERIC) path = Path::U64;
@@ -1585,7 +1611,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     std::vector<unsigned char> rec((size_t)std::max<uint32_t>(N, 1) * stride, 0);
     // K1 node summaries (N32 path): the facts the block-classified K1 reads per node
     const bool want_sum = path == Path::N32;
-    uint32_t g_rcp[8] = {};  // the G table's reciprocals, read back from the device
+    uint32_t g_rcp[10] = {};  // the G table's reciprocals, read back from the device
     const size_t sstride = k1sum_stride(K);
     std::vector<uint32_t> sum(want_sum ? (size_t)std::max<uint32_t>(N, 1) * sstride / 4 : 0, 0);
     const size_t s2stride = k2sum_stride(K);
@@ -1746,11 +1772,6 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
           for (int f = 0; f < kCardFields; ++f) u[f * K + j] = (uint32_t)v[f];
           u[kFree * K + j] = code_f(v[kFree]);
           u[kTotal * K + j] = code_t(v[kTotal]);
-          float* g = reinterpret_cast<float*>(r + n32_f32_off(0, K));
-          g[kF32Bandwidth * K + j] = (float)v[kBandwidth];
-          g[kF32Clock * K + j] = (float)v[kClock];
-          g[kF32Core * K + j] = (float)v[kCore];
-          g[kF32Power * K + j] = (float)v[kPower];
           double* d = reinterpret_cast<double*>(r + n32_f64_off(0, K));
           d[kF64Free * K + j] = (double)v[kFree];
           d[kF64Total * K + j] = (double)v[kTotal];
@@ -2030,14 +2051,24 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     static const bool no_gtab = YODA_KNOB("YODA_NO_GTAB", 0) != 0;  // A/B knob
     if (h->has_k2sum && N > 0 && !no_gtab && !(flags & YODA_UPLOAD_NO_GTAB)) {
       h->g.tab = h->gtab.as<uint32_t>();
-      std::memcpy(&h->g.r_bw, &g_rcp[0], 4);
-      std::memcpy(&h->g.r_core, &g_rcp[1], 4);
-      std::memcpy(&h->g.r_pow, &g_rcp[2], 4);
-      std::memcpy(&h->g.r_free, &g_rcp[4], 8);
-      std::memcpy(&h->g.r_tot, &g_rcp[6], 8);
+      std::memcpy(&h->g.r_bw, &g_rcp[0], 8);
+      std::memcpy(&h->g.r_core, &g_rcp[2], 8);
+      std::memcpy(&h->g.r_pow, &g_rcp[4], 8);
+      std::memcpy(&h->g.r_free, &g_rcp[6], 8);
+      std::memcpy(&h->g.r_tot, &g_rcp[8], 8);
+      auto ru32 = [](double r) {  // the smallest float >= r (yoda_kernels.hip ru32_of)
+        float f = (float)r;
+        if ((double)f < r) f = std::nextafter(f, INFINITY);
+        return f;
+      };
+      h->g.f_bw = ru32(h->g.r_bw);
+      h->g.f_core = ru32(h->g.r_core);
+      h->g.f_pow = ru32(h->g.r_pow);
     }
     h->generic = path == Path::U64;
     h->mem_ranks = ranks;
+    h->pack16 = pack16;
+    h->q32 = q32;
     h->kbub_dirty = true;
     h->kbub_loose = false;
     h->hot_ok = false;
@@ -3005,7 +3036,7 @@ int greedy_eval_fast(GreedyState& g, uint32_t s, int32_t* pick_out) {
   std::atomic_thread_fence(std::memory_order_seq_cst);
   HIP_TRY(h, launch_greedy_one(h->K, h->path, h->nodes.as<unsigned char>(),
                                h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr, h->n_nodes,
-                               pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(),
+                               pod_params(h), h->rcp.as<double>(), 
                                h->n_pods, s, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
                                h->bs_ptr(), bs_row(h->n_nodes), h->blk_ptr(),
                                blk_row(h->n_nodes), ps, pi, done,
@@ -3148,7 +3179,7 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
           if ((rc = phase1(h, YODA_MODE_SCV, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>())))
             return rc;
           HIP_TRY(h, launch_prep2(h->maxima.as<uint64_t>(), wn, h->rcp.as<double>(),
-                                  h->rcp32.as<float>(), h->stream));
+                                   h->stream));
           if ((rc = topk_lists(h, wn, KT, h->counts.as<uint32_t>()))) return rc;
           HIP_TRY(h, hipMemcpyAsync(counts.data(), h->counts.p, 2ull * wn * 4,
                                     hipMemcpyDeviceToHost, h->stream));
@@ -3478,7 +3509,7 @@ int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_count
                               h->stream));
     if (N > 0) {
       HIP_TRY(h, launch_prep2(h->maxima.as<uint64_t>(), P, h->rcp.as<double>(),
-                              h->rcp32.as<float>(), h->stream));
+                               h->stream));
       if ((rc = topk_lists(h, P, KT, d_counts))) return rc;
       HIP_TRY(h, hipMemcpyAsync(ts.data(), h->tk_s.p, (size_t)KT * P * 8, hipMemcpyDeviceToHost,
                                 h->stream));
@@ -3586,7 +3617,7 @@ int yoda_shard_best_one(yoda_t* h, uint32_t pod, double* score, int32_t* node) {
   uint32_t* done = h->g1_done.as<uint32_t>();
   HIP_TRY(h, launch_greedy_one(h->K, h->path, h->nodes.as<unsigned char>(),
                                h->has_k2sum ? h->k2sum.as<unsigned char>() : nullptr, h->n_nodes,
-                               pod_params(h), h->rcp.as<double>(), h->rcp32.as<float>(),
+                               pod_params(h), h->rcp.as<double>(), 
                                h->n_pods, s, h->bitmask.as<uint64_t>(), bm_row(h->n_nodes),
                                h->bs_ptr(), bs_row(h->n_nodes), h->blk_ptr(),
                                blk_row(h->n_nodes), ps, pi, done, done + 1, h->stream));
@@ -4329,7 +4360,7 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
     double t_issued, t_sync;
     if (N > 0) {
       HIP_TRY(h, launch_prep2(h->maxima.as<uint64_t>(), wn, h->rcp.as<double>(),
-                              h->rcp32.as<float>(), h->stream));
+                               h->stream));
       // (node ids local here: the session works on this handle's nodes)
       const uint32_t off = h->node_offset;
       h->node_offset = 0;

@@ -585,8 +585,14 @@ __global__ __launch_bounds__(kWave) void k_reduce_wit(const uint64_t* __restrict
 // pmax [6][C][P] u64, pwit [2][6][C][P], pcnt [2][C][P].
 // Packed N32 partial word w (k1_block_n32's epilogue) -> the MaxValue fields it holds:
 // w 0: bandwidth | clock << 16, w 1: core | power << 16 (per-half max), w 2: free, w 3: total.
-__device__ __forceinline__ uint32_t narrow_max(uint32_t a, uint32_t b, int w) {
-  return w < 2 ? max16x2(a, b) : max(a, b);
+// nw = kNarrowWords when the four small fields fit 16 bits (<= 65535); with a wider one the
+// partials hold one u32 word per MaxValue field, kMax* order (nw = kWideWords).
+__device__ __forceinline__ uint32_t narrow_max(uint32_t a, uint32_t b, int w,
+                                               uint32_t nw = kNarrowWords) {
+  return (nw == kNarrowWords && w < 2) ? max16x2(a, b) : max(a, b);
+}
+__device__ __forceinline__ uint32_t narrow_floor(int w, uint32_t nw) {  // floor 1 per field
+  return (nw == kNarrowWords && w < 2) ? 0x00010001u : 1u;
 }
 
 // SUB = 4 (the argmax runs): the workgroup's four waves hold the SAME 64 pods, each over its own
@@ -608,7 +614,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     uint64_t* __restrict__ bm, uint32_t bm_stride, BlockMask* __restrict__ bs,
     uint32_t bs_stride, uint64_t* __restrict__ blk, uint32_t blk_stride,
     unsigned long long* __restrict__ stats, uint32_t* __restrict__ pwit = nullptr,
-    const uint32_t* __restrict__ bsm = nullptr) {
+    const uint32_t* __restrict__ bsm = nullptr, uint32_t nwords = kNarrowWords) {
   static_assert(!(WIT && MIX), "the witness K1 serves one-model snapshots");
   static_assert(SUB == 1 || (SUB == kBlock / kWave && !WIT), "SUB: 1, or one pod wave per workgroup");
   constexpr uint32_t SS = k1sum_stride(K);
@@ -1189,36 +1195,52 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   mx[kMaxTotal] = max(mx[kMaxTotal], a_tot);
   nf += nf_all;
   nz += nz_all;
-  // N32: packed u32 partials (k_reduce1<true>), [kNarrowWords][C][P]: bandwidth | clock << 16,
-  // core | power << 16 (each <= 55738 on this path), FreeMemory, TotalMemory (u32 codes)
+  // N32: u32 partials (k_reduce1<true>), [nwords][C][P]: packed (nwords = kNarrowWords:
+  // bandwidth | clock << 16, core | power << 16 -- each <= 65535 -- FreeMemory, TotalMemory as
+  // u32 codes), or one word per field in kMax* order (kWideWords)
   uint32_t* pmax32 = reinterpret_cast<uint32_t*>(pmax);
-  uint32_t pw4[kNarrowWords] = {mx[kMaxBw] | (mx[kMaxClock] << 16),
-                                mx[kMaxCore] | (mx[kMaxPower] << 16), mx[kMaxFree],
-                                mx[kMaxTotal]};
+  uint32_t pw4[kWideWords];
+  if (nwords == kNarrowWords) {
+    pw4[0] = mx[kMaxBw] | (mx[kMaxClock] << 16);
+    pw4[1] = mx[kMaxCore] | (mx[kMaxPower] << 16);
+    pw4[2] = mx[kMaxFree];
+    pw4[3] = mx[kMaxTotal];
+    pw4[4] = pw4[5] = 0u;
+  } else {
+#pragma unroll
+    for (int f = 0; f < kWideWords; ++f) pw4[f] = mx[f];
+  }
   if constexpr (SUB > 1) {
     // the quarters' partials through LDS (each wave's own region, free after its loop);
     // wave 0 folds them and writes the chunk's
-    static_assert(RECS + kWave * REC >= (kNarrowWords + 2) * kWave, "LDS merge area");
+    static_assert(RECS + kWave * REC >= (kWideWords + 2) * kWave, "LDS merge area");
 #pragma unroll
-    for (int f = 0; f < kNarrowWords; ++f) lds[f * kWave + lane] = pw4[f];
-    lds[kNarrowWords * kWave + lane] = nf;
-    lds[(kNarrowWords + 1) * kWave + lane] = nz;
+    for (int f = 0; f < kWideWords; ++f) lds[f * kWave + lane] = pw4[f];
+    lds[kWideWords * kWave + lane] = nf;
+    lds[(kWideWords + 1) * kWave + lane] = nz;
     __syncthreads();
     if (sub != 0u || !live) return;
 #pragma unroll
     for (int w = 1; w < SUB; ++w) {
       const uint32_t* o = lds_all[w];
 #pragma unroll
-      for (int f = 0; f < kNarrowWords; ++f) pw4[f] = narrow_max(pw4[f], o[f * kWave + lane], f);
-      nf += o[kNarrowWords * kWave + lane];
-      nz += o[(kNarrowWords + 1) * kWave + lane];
+      for (int f = 0; f < kWideWords; ++f)
+        pw4[f] = narrow_max(pw4[f], o[f * kWave + lane], f, nwords);
+      nf += o[kWideWords * kWave + lane];
+      nz += o[(kWideWords + 1) * kWave + lane];
     }
   }
 #ifdef YODA_ABL_K1_NOPART  // (write-traffic ablation: no partial stores)
   return;
 #endif
-#pragma unroll
-  for (int f = 0; f < kNarrowWords; ++f) pmax32[((size_t)f * C + chunk) * n_pods + p] = pw4[f];
+  pmax32[((size_t)0 * C + chunk) * n_pods + p] = pw4[0];
+  pmax32[((size_t)1 * C + chunk) * n_pods + p] = pw4[1];
+  pmax32[((size_t)2 * C + chunk) * n_pods + p] = pw4[2];
+  pmax32[((size_t)3 * C + chunk) * n_pods + p] = pw4[3];
+  if (nwords != kNarrowWords) {
+    pmax32[((size_t)4 * C + chunk) * n_pods + p] = pw4[4];
+    pmax32[((size_t)5 * C + chunk) * n_pods + p] = pw4[5];
+  }
   pcnt[((size_t)0 * C + chunk) * n_pods + p] = nf;
   pcnt[((size_t)1 * C + chunk) * n_pods + p] = nz;
 }
@@ -1266,18 +1288,20 @@ __device__ __forceinline__ uint64_t mask_at(const MaskSrc& m, uint32_t w, uint32
 // (pod, field) (grid.y = the 6 maxima + 2 counts), chunk loads unrolled so each thread keeps
 // several in flight.  NARROW: u32 maxima partials (the N32 K1).
 __device__ __forceinline__ double ru_100_over(double M);
-__device__ __forceinline__ float ru32_100_over(double M);
 
 // rcp != nullptr (a single-handle run, whose maxima are final here): each maxima thread also
 // writes its field's reciprocals (k_prep2's, fused).  Packed partial words: narrow_max.
 __device__ __forceinline__ void narrow_store(uint32_t v, int w, uint32_t n_pods, uint32_t p,
-                                            uint64_t* maxima, const MemTab& mt) {
+                                            uint64_t* maxima, const MemTab& mt,
+                                            uint32_t nw = kNarrowWords) {
   auto put = [&](int f, uint64_t x) {
     if (mt.vf && f == kMaxFree) x = rank_value(x, mt.vf);  // memory ranks -> values
     if (mt.vf && f == kMaxTotal) x = rank_value(x, mt.vt);
     maxima[(size_t)f * n_pods + p] = x;
   };
-  if (w == 0) {
+  if (nw != kNarrowWords) {
+    put(w, v);
+  } else if (w == 0) {
     put(kMaxBw, v & 0xffffu);
     put(kMaxClock, v >> 16);
   } else if (w == 1) {
@@ -1290,13 +1314,10 @@ __device__ __forceinline__ void narrow_store(uint32_t v, int w, uint32_t n_pods,
 
 // rcp rows: bw, core, power, free, total (k_prep2's order); the clock has none
 __device__ __forceinline__ void store_rcp(int f, uint64_t mx, uint32_t n_pods, uint32_t p,
-                                          double* rcp, float* rcp32) {
+                                          double* rcp) {
   const int k = f == kMaxBw ? 0 : f == kMaxCore ? 1 : f == kMaxPower ? 2 : f == kMaxFree ? 3
               : f == kMaxTotal ? 4 : -1;
-  if (rcp && k >= 0) {
-    rcp[(size_t)k * n_pods + p] = ru_100_over((double)mx);
-    if (k < 3) rcp32[(size_t)k * n_pods + p] = ru32_100_over((double)mx);
-  }
+  if (rcp && k >= 0) rcp[(size_t)k * n_pods + p] = ru_100_over((double)mx);
 }
 
 template <bool NARROW>
@@ -1306,23 +1327,25 @@ __global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__
                                                     uint64_t* __restrict__ maxima,
                                                     uint32_t* __restrict__ counts,
                                                     double* __restrict__ rcp,
-                                                    float* __restrict__ rcp32, MemTab mt) {
+                                                    MemTab mt, uint32_t nw) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t f = blockIdx.y;  // NARROW: packed words 0..3, then the 2 counts
-  constexpr uint32_t NF = NARROW ? kNarrowWords : 6u;
+  const uint32_t f = blockIdx.y;  // NARROW: the nw partial words, then the 2 counts
+  const uint32_t NF = NARROW ? nw : 6u;
   if (p >= n_pods) return;
   if (f < NF) {
     if constexpr (NARROW) {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(pmax) + (size_t)f * C * n_pods + p;
-      uint32_t m32 = f < 2 ? 0x00010001u : 1u;  // floor 1 (collection.go:31-38), per half
+      uint32_t m32 = narrow_floor((int)f, nw);  // floor 1 (collection.go:31-38)
 #pragma unroll 8
-      for (uint32_t c = 0; c < C; ++c) m32 = narrow_max(m32, src[(size_t)c * n_pods], (int)f);
-      narrow_store(m32, (int)f, n_pods, p, maxima, mt);
-      if (rcp) {
+      for (uint32_t c = 0; c < C; ++c)
+        m32 = narrow_max(m32, src[(size_t)c * n_pods], (int)f, nw);
+      narrow_store(m32, (int)f, n_pods, p, maxima, mt, nw);
+      if (rcp && nw != kNarrowWords) {
+        store_rcp((int)f, maxima[(size_t)f * n_pods + p], n_pods, p, rcp);
+      } else if (rcp) {
         const int fa = f == 0 ? kMaxBw : f == 1 ? kMaxCore : f == 2 ? kMaxFree : kMaxTotal;
-        store_rcp(fa, maxima[(size_t)fa * n_pods + p], n_pods, p, rcp, rcp32);
-        if (f == 1) store_rcp(kMaxPower, maxima[(size_t)kMaxPower * n_pods + p], n_pods, p, rcp,
-                              rcp32);
+        store_rcp(fa, maxima[(size_t)fa * n_pods + p], n_pods, p, rcp);
+        if (f == 1) store_rcp(kMaxPower, maxima[(size_t)kMaxPower * n_pods + p], n_pods, p, rcp);
       }
     } else {
       uint64_t mx = 1;
@@ -1332,7 +1355,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__
       if (mt.vf && f == kMaxFree) mx = rank_value(mx, mt.vf);  // memory ranks -> values
       if (mt.vf && f == kMaxTotal) mx = rank_value(mx, mt.vt);
       maxima[(size_t)f * n_pods + p] = mx;
-      store_rcp((int)f, mx, n_pods, p, rcp, rcp32);
+      store_rcp((int)f, mx, n_pods, p, rcp);
     }
   } else {
     const uint32_t* src = pcnt + (size_t)(f - NF) * C * n_pods + p;
@@ -1351,17 +1374,17 @@ __global__ __launch_bounds__(kWave) void k_reduce1_wave(const uint64_t* __restri
                                                          uint32_t C, uint32_t n_pods,
                                                          uint64_t* __restrict__ maxima,
                                                          uint32_t* __restrict__ counts,
-                                                         MemTab mt) {
+                                                         MemTab mt, uint32_t nw) {
   const uint32_t p = blockIdx.x, lane = threadIdx.x;
   if constexpr (NARROW) {
-    for (int w = 0; w < (int)kNarrowWords; ++w) {
-      uint32_t m = w < 2 ? 0x00010001u : 1u;
+    for (int w = 0; w < (int)nw; ++w) {
+      uint32_t m = narrow_floor(w, nw);
       for (uint32_t c = lane; c < C; c += kWave)
         m = narrow_max(m, reinterpret_cast<const uint32_t*>(pmax)[((size_t)w * C + c) * n_pods + p],
-                       w);
+                       w, nw);
       for (int o = kWave / 2; o > 0; o >>= 1)
-        m = narrow_max(m, (uint32_t)__shfl_xor((int)m, o, kWave), w);
-      if (lane == 0) narrow_store(m, w, n_pods, p, maxima, mt);
+        m = narrow_max(m, (uint32_t)__shfl_xor((int)m, o, kWave), w, nw);
+      if (lane == 0) narrow_store(m, w, n_pods, p, maxima, mt, nw);
     }
   } else {
     for (int f = 0; f < 6; ++f) {
@@ -1390,9 +1413,10 @@ __global__ __launch_bounds__(kBlock) void k_reduce1_split(const uint64_t* __rest
                                                           const uint32_t* __restrict__ pcnt,
                                                           uint32_t C, uint32_t n_pods,
                                                           uint64_t* __restrict__ maxima,
-                                                          uint32_t* __restrict__ counts) {
+                                                          uint32_t* __restrict__ counts,
+                                                          uint32_t nw) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x, f = blockIdx.y;
-  constexpr uint32_t NF = NARROW ? kNarrowWords : 6u;
+  const uint32_t NF = NARROW ? nw : 6u;
   if (p >= n_pods || f >= NF + 2u) return;
   const uint32_t S = gridDim.z, per = (C + S - 1) / S;
   const uint32_t c0 = blockIdx.z * per, c1 = min(C, c0 + per);
@@ -1406,8 +1430,11 @@ __global__ __launch_bounds__(kBlock) void k_reduce1_split(const uint64_t* __rest
       const uint32_t* src = reinterpret_cast<const uint32_t*>(pmax) + (size_t)f * C * n_pods + p;
       uint32_t m32 = 0;
 #pragma unroll 8
-      for (uint32_t c = c0; c < c1; ++c) m32 = narrow_max(m32, src[(size_t)c * n_pods], (int)f);
-      if (f == 0) {
+      for (uint32_t c = c0; c < c1; ++c)
+        m32 = narrow_max(m32, src[(size_t)c * n_pods], (int)f, nw);
+      if (nw != kNarrowWords) {
+        amax((int)f, m32);
+      } else if (f == 0) {
         amax(kMaxBw, m32 & 0xffffu);
         amax(kMaxClock, m32 >> 16);
       } else if (f == 1) {
@@ -1482,20 +1509,10 @@ __device__ __forceinline__ double ru_100_over(double M) {
   return r;
 }
 
-// RU32(100 / M): the smallest float >= 100/M (M < 2^24, so (double)f * M is exact and the
-// fma's sign is exact).  floor(fl32(x * RU32(100/M))) == floor(100 x / M) whenever
-// 300 x + M < 2^24 (tools/check_div_lemma.c).
-__device__ __forceinline__ float ru32_100_over(double M) {
-  float f = (float)(100.0 / M);
-  if (__builtin_fma((double)f, M, -100.0) < 0.0) f = __int_as_float(__float_as_int(f) + 1);
-  return f;
-}
-
-// Per-pod reciprocals of the (all-reduced) maxima: f64 for all five divisors, f32 for the
-// small-field ones (bandwidth, core, power) used by the N32 path.
+// Per-pod reciprocals of the (all-reduced) maxima, f64 for all five divisors (every record
+// path).
 __global__ __launch_bounds__(kBlock) void k_prep2(const uint64_t* __restrict__ maxima,
-                                                  uint32_t n_pods, double* __restrict__ rcp,
-                                                  float* __restrict__ rcp32) {
+                                                  uint32_t n_pods, double* __restrict__ rcp) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (p >= n_pods) return;
   const int src[5] = {kMaxBw, kMaxCore, kMaxPower, kMaxFree, kMaxTotal};
@@ -1503,7 +1520,6 @@ __global__ __launch_bounds__(kBlock) void k_prep2(const uint64_t* __restrict__ m
   for (int k = 0; k < 5; ++k) {
     const double M = (double)maxima[(size_t)src[k] * n_pods + p];
     rcp[(size_t)k * n_pods + p] = ru_100_over(M);
-    if (k < 3) rcp32[(size_t)k * n_pods + p] = ru32_100_over(M);
   }
 }
 
@@ -1543,6 +1559,29 @@ __global__ __launch_bounds__(kBlock) void k_window_out(
   }
 }
 
+// CalculateCardScore's bandwidth, clock / MaxBandwidth (algorithm.go:283), 2 core and power
+// terms of a card (or of a one-model node's model) under the reciprocals r, as products of
+// the u32 fields in RS: f64 always exact (x, M < 2^32: 300 x + M < 2^53), f32 when every
+// small field is <= kF32SmallMax (300 x + M < 2^24) -- the quotient lemma, DESIGN.md §5.
+template <typename RS>
+__device__ __forceinline__ uint32_t card_shared_terms(uint32_t bw, uint32_t ck, uint32_t core,
+                                                      uint32_t pw, RS r_bw, RS r_core, RS r_pow) {
+  return (uint32_t)((RS)bw * r_bw) + (uint32_t)((RS)ck * r_bw) +
+         2u * (uint32_t)((RS)core * r_core) + (uint32_t)((RS)pw * r_pow);
+}
+// RU32(100 / M) from r = RU(100 / M) in f64: the smallest float >= r, which is the smallest
+// float >= 100 / M (a float in [100 / M, r) would be a double below r).
+__device__ __forceinline__ float ru32_of(double r) {
+  float f = (float)r;
+  if ((double)f < r) f = __int_as_float(__float_as_int(f) + 1);
+  return f;
+}
+template <typename RS>
+__device__ __forceinline__ RS rcp_as(double r) {
+  if constexpr (sizeof(RS) == 4) return ru32_of(r);
+  else return r;
+}
+
 // The "G table" (N32 block K2): for the snapshot-wide maxima G (per CalculateCardScore field,
 // the max over every real card, floor 1 -- the PreScore maxima of any pod whose feasible
 // nodes include the maximal cards, which is most pods of a large cluster) the per-node terms
@@ -1553,13 +1592,6 @@ __global__ __launch_bounds__(kBlock) void k_window_out(
 // reciprocals equal G's (compared bit for bit) reads them instead.
 // (struct GTab, gtab_stride: yoda_layout.h)
 
-// The terms of one one-model node under reciprocals r (the expressions of k2_block_n32).
-__device__ __forceinline__ uint32_t card_shared_terms(uint32_t bw, uint32_t ck, uint32_t core,
-                                                      uint32_t pw, float r_bw, float r_core,
-                                                      float r_pow) {
-  return (uint32_t)((float)bw * r_bw) + (uint32_t)((float)ck * r_bw) +
-         2u * (uint32_t)((float)core * r_core) + (uint32_t)((float)pw * r_pow);
-}
 __device__ __forceinline__ uint32_t card_mem_term(uint32_t f, uint32_t t, double r_free,
                                                   double r_tot) {
   return 3u * (uint32_t)((double)f * r_free) + (uint32_t)((double)t * r_tot);
@@ -1581,8 +1613,8 @@ __device__ __forceinline__ uint32_t card_mem_term(uint32_t f, uint32_t t, double
 }
 
 // Build the G table (GTab above) of the N32 snapshot: g_max = G per maxima field (kMax*
-// order); rcp_out <- G's reciprocals (f32 bw, core, power; f64 free, total) for the host to
-// hand to K2.  One thread per node, tile layout.
+// order); rcp_out <- G's reciprocals (f64 bw, core, power, free, total: 10 words) for the host
+// to hand to K2.  One thread per node, tile layout.
 template <int K>
 __global__ __launch_bounds__(kBlock) void k_gtable(const uint32_t* __restrict__ sum2,
                                                    const uint32_t* __restrict__ mix,
@@ -1590,21 +1622,19 @@ __global__ __launch_bounds__(kBlock) void k_gtable(const uint32_t* __restrict__ 
                                                    uint32_t* __restrict__ tab,
                                                    uint32_t* __restrict__ rcp_out, MemTab mt) {
   const uint32_t n = blockIdx.x * kBlock + threadIdx.x;
-  const float r_bw = ru32_100_over((double)g_max[kMaxBw]);
-  const float r_core = ru32_100_over((double)g_max[kMaxCore]);
-  const float r_pow = ru32_100_over((double)g_max[kMaxPower]);
+  const double r_bw = ru_100_over((double)g_max[kMaxBw]);
+  const double r_core = ru_100_over((double)g_max[kMaxCore]);
+  const double r_pow = ru_100_over((double)g_max[kMaxPower]);
   const double r_free = ru_100_over((double)g_max[kMaxFree]);
   const double r_tot = ru_100_over((double)g_max[kMaxTotal]);
   if (n == 0) {
-    rcp_out[0] = (uint32_t)__float_as_int(r_bw);
-    rcp_out[1] = (uint32_t)__float_as_int(r_core);
-    rcp_out[2] = (uint32_t)__float_as_int(r_pow);
-    const uint64_t f = (uint64_t)__double_as_longlong(r_free);
-    const uint64_t t = (uint64_t)__double_as_longlong(r_tot);
-    rcp_out[4] = (uint32_t)f;
-    rcp_out[5] = (uint32_t)(f >> 32);
-    rcp_out[6] = (uint32_t)t;
-    rcp_out[7] = (uint32_t)(t >> 32);
+    const double r[5] = {r_bw, r_core, r_pow, r_free, r_tot};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const uint64_t b = (uint64_t)__double_as_longlong(r[k]);
+      rcp_out[2 * k] = (uint32_t)b;
+      rcp_out[2 * k + 1] = (uint32_t)(b >> 32);
+    }
   }
   if (n >= ((n_nodes + 63u) & ~63u)) return;  // padded tail lanes: zero summaries
   constexpr uint32_t S2 = k2sum_stride(K), GS = gtab_stride(K), MS = mix_stride(K);
@@ -1704,7 +1734,6 @@ struct ScoreArgs {
   const uint32_t* m_32;
   const uint32_t* c_32;
   const double* rcp;    // [5][P] f64: bw, core, power, free, total
-  const float* rcp32;   // [3][P] f32: bw, core, power
   const uint32_t* cnt = nullptr;  // [P] feasible-node counts (phase 1), or none
   GTab g = {};                    // the snapshot-wide maxima's per-node terms (tab: none)
   const uint32_t* mix = nullptr;  // per-card models in free order (yoda_layout.h MixWord)
@@ -1717,6 +1746,7 @@ struct ScoreArgs {
 
 template <Path P>
 struct Scorer;
+
 
 // F64: every quotient in f64; each term is an exact integer < 2^52, so the sum is exact in
 // any order and the weights fold into FMAs.
@@ -1759,19 +1789,20 @@ struct Scorer<Path::F64> {
   }
 };
 
-// N32: the four small-field quotients in f32 (exact under the N32 bounds), the two memory
-// quotients in f64, the card score summed in u32 (< 2^27).
-template <>
-struct Scorer<Path::N32> {
+// N32: u32 card fields, the small-field quotients in RS (card_shared_terms: f64, or f32 where
+// its lemma holds -- the block K2's WQ = false), the memory quotients in f64, the card score
+// summed in u32 (the host bounds it: yoda_capi.cpp n32_ok).
+template <typename RS>
+struct ScorerN32 {
   uint32_t m = 0, c = 0;
-  float r_bw = 0, r_core = 0, r_pow = 0;
+  RS r_bw = 0, r_core = 0, r_pow = 0;
   double r_free = 0, r_tot = 0;
   __device__ void load(const ScoreArgs& a, uint32_t p, uint32_t n_pods) {
     m = a.m_32[p];
     c = a.c_32[p];
-    r_bw = a.rcp32[0 * (size_t)n_pods + p];
-    r_core = a.rcp32[1 * (size_t)n_pods + p];
-    r_pow = a.rcp32[2 * (size_t)n_pods + p];
+    r_bw = rcp_as<RS>(a.rcp[0 * (size_t)n_pods + p]);
+    r_core = rcp_as<RS>(a.rcp[1 * (size_t)n_pods + p]);
+    r_pow = rcp_as<RS>(a.rcp[2 * (size_t)n_pods + p]);
     r_free = a.rcp[3 * (size_t)n_pods + p];
     r_tot = a.rcp[4 * (size_t)n_pods + p];
   }
@@ -1784,14 +1815,12 @@ struct Scorer<Path::N32> {
       // real card, so the card-score sum factors into  nq * shared + sum(3 q_free + q_tot)
       // over the nq qualifying real cards — the same integers, added in another order.
       const Group<uint32_t, K> fr = load_group<uint32_t, K>(rec + n32_u32_off(kFree, K));
-      const uint32_t ck0 = reinterpret_cast<const uint32_t*>(rec + n32_u32_off(kClock, K))[0];
-      const float* f32 = reinterpret_cast<const float*>(rec + n32_f32_off(0, K));
+      auto u0 = [&](int f) { return reinterpret_cast<const uint32_t*>(rec + n32_u32_off(f, K))[0]; };
+      const uint32_t ck0 = u0(kClock);
       const Group<double, K> frd = load_group<double, K>(rec + n32_f64_off(kF64Free, K));
       const Group<double, K> tod = load_group<double, K>(rec + n32_f64_off(kF64Total, K));
-      uint32_t shared = (uint32_t)(f32[kF32Bandwidth * K] * r_bw) +
-                        (uint32_t)(f32[kF32Clock * K] * r_bw) +
-                        2u * (uint32_t)(f32[kF32Core * K] * r_core) +
-                        (uint32_t)(f32[kF32Power * K] * r_pow);
+      uint32_t shared = card_shared_terms(u0(kBandwidth), ck0, u0(kCore), u0(kPower), r_bw,
+                                          r_core, r_pow);
       uint32_t nq = 0, mem = 0;
       if (hd->flags & kNodeUniformTotal) {
         shared += (uint32_t)(tod.v[0] * r_tot);
@@ -1815,24 +1844,24 @@ struct Scorer<Path::N32> {
     }
     const Group<uint32_t, K> fr = load_group<uint32_t, K>(rec + n32_u32_off(kFree, K));
     const Group<uint32_t, K> ck = load_group<uint32_t, K>(rec + n32_u32_off(kClock, K));
-    const Group<float, K> bwf = load_group<float, K>(rec + n32_f32_off(kF32Bandwidth, K));
-    const Group<float, K> ckf = load_group<float, K>(rec + n32_f32_off(kF32Clock, K));
-    const Group<float, K> cof = load_group<float, K>(rec + n32_f32_off(kF32Core, K));
-    const Group<float, K> pwf = load_group<float, K>(rec + n32_f32_off(kF32Power, K));
+    const Group<uint32_t, K> bwu = load_group<uint32_t, K>(rec + n32_u32_off(kBandwidth, K));
+    const Group<uint32_t, K> cou = load_group<uint32_t, K>(rec + n32_u32_off(kCore, K));
+    const Group<uint32_t, K> pwu = load_group<uint32_t, K>(rec + n32_u32_off(kPower, K));
     const Group<double, K> frd = load_group<double, K>(rec + n32_f64_off(kF64Free, K));
     const Group<double, K> tod = load_group<double, K>(rec + n32_f64_off(kF64Total, K));
     uint32_t basic = 0;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       // CalculateCardScore (algorithm.go:280-291); clock / MaxBandwidth (:283)
-      uint32_t sc = (uint32_t)(bwf.v[j] * r_bw) + (uint32_t)(ckf.v[j] * r_bw) +
-                    (uint32_t)(pwf.v[j] * r_pow) + (uint32_t)(tod.v[j] * r_tot);
-      sc += 2u * (uint32_t)(cof.v[j] * r_core) + 3u * (uint32_t)(frd.v[j] * r_free);
+      uint32_t sc = card_shared_terms(bwu.v[j], ck.v[j], cou.v[j], pwu.v[j], r_bw, r_core, r_pow) +
+                    (uint32_t)(tod.v[j] * r_tot) + 3u * (uint32_t)(frd.v[j] * r_free);
       basic += ((fr.v[j] >= m) & (ck.v[j] >= c)) ? sc : 0u;  // algorithm.go:271
     }
     return (double)basic + stat;  // algorithm.go:96
   }
 };
+template <>
+struct Scorer<Path::N32> : ScorerN32<double> {};
 
 __device__ __forceinline__ uint32_t rec_stride(Path p, int K) {
   return p == Path::N32 ? n32_stride(K) : node_stride(K);
@@ -1987,7 +2016,9 @@ __global__ __launch_bounds__(kBlock) void k2_score(
 #endif
 // MIX = false: a snapshot whose every node is one GPU model (kSumUni4): no mixed-model rows
 // and no exact per-pod Scorer in the kernel.
-template <int K, bool STATS, int TKO = 0, bool RK = false, bool MIX = true>
+// Q32: the small-field quotients in f32 (host: every bandwidth / clock / core / power <=
+// kF32SmallMax, where the f32 quotient lemma holds; fewer registers than f64), else f64.
+template <int K, bool STATS, int TKO = 0, bool RK = false, bool MIX = true, bool Q32 = true>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ? (TKO == 0 ? YODA_K2_WAVES : (TKO <= 8 ? 4 : 3)) : 1))) void k2_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum2,
     uint32_t n_nodes, uint32_t chunk_nodes, ScoreArgs args, uint32_t n_pods,
@@ -2004,7 +2035,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // node records (below): 16 words -- 8 of header, then 4 basic scores (uniform maxima) or
   // the (basic at nq_lo, at nq_lo + 1) pair of each reciprocal set
   constexpr uint32_t kSets = 4, REC = 16;
-  // LDS per wave: prefix table | 64 node records | the sets' reciprocals (8 words each).
+  // LDS per wave: prefix table | 64 node records | the sets' reciprocals (5 f64, 16 words each).
   // No lowest score: on this path NormalizeScore cannot overflow, so the
   // lowest raw score is never read (the chunk merge reports the best in its place).
   // + the nodes' local ids of a block-grouped run (args.ids)
@@ -2013,7 +2044,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // table above, the others after the ids), so the per-pod pass reads a lane's basic score as
   // in a uniform wave instead of computing its card terms per node
   constexpr uint32_t TT = (TOPK && !RK) ? (TKO > 8 ? 3u : 2u) : 1u;
-  constexpr uint32_t RECS = TAB, RCPS = TAB + kWave * REC, IDW = RCPS + 8 * kSets,
+  constexpr uint32_t RECS = TAB, RCPS = TAB + kWave * REC, IDW = RCPS + 16 * kSets,
                      XTAB = IDW + kWave, LDSW = XTAB + (TT - 1) * TAB;
   auto row_base = [&](uint32_t q) -> uint32_t { return q == 0 ? 0u : XTAB + (q - 1u) * TAB; };
   __shared__ __attribute__((aligned(16))) uint32_t lds_all[kBlock / kWave][LDSW];
@@ -2032,7 +2063,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   const uint64_t t_start = STATS ? wall_clock64() : 0ull;
   const uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
   const BlockMask* bsw = bs ? bs + (size_t)uniform_u32(p >> 6) * bs_stride : nullptr;
-  Scorer<Path::N32> sc;
+  using RS = std::conditional_t<Q32, float, double>;  // small-field reciprocal type
+  ScorerN32<RS> sc;
   if (live) sc.load(args, p, n_pods);
   // A pod feasible on no node has no bit in any mask: it takes no part in the wave's bounds
   // and reciprocal sets, and its outputs stay "no node".
@@ -2040,9 +2072,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   const uint64_t act_mask = ballot(act);
   // Reciprocal sets: active lanes with the same (bw, core, power, free, total) reciprocals,
   // numbered in order of their first lane; up to kSets, any further lanes "overflow".
-  auto rl_f = [&](float x, int l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
-  };
   auto rl_d = [&](double x, int l) {
     const uint64_t b = (uint64_t)__double_as_longlong(x);
     return __longlong_as_double((long long)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
@@ -2052,11 +2081,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   uint32_t set = 0, nsets = 0;
   bool has_set = false;  // this lane is in one of the sets (else it overflowed them)
   uint64_t rem = act_mask;
-  float u_bw = 0.f, u_core = 0.f, u_pow = 0.f;  // set 0's reciprocals (wave-uniform)
+  auto rl_s = [&](RS x, int l) -> RS {
+    if constexpr (Q32) return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+    else return rl_d(x, l);
+  };
+  RS u_bw = 0, u_core = 0, u_pow = 0;  // set 0's reciprocals (wave-uniform)
   double u_free = 0.0, u_tot = 0.0;
   for (; rem != 0ull && nsets < kSets; ++nsets) {
     const int l = __builtin_ctzll(rem);
-    const float b_bw = rl_f(sc.r_bw, l), b_core = rl_f(sc.r_core, l), b_pow = rl_f(sc.r_pow, l);
+    const RS b_bw = rl_s(sc.r_bw, l), b_core = rl_s(sc.r_core, l), b_pow = rl_s(sc.r_pow, l);
     const double b_free = rl_d(sc.r_free, l), b_tot = rl_d(sc.r_tot, l);
     const bool in = act && sc.r_bw == b_bw && sc.r_core == b_core && sc.r_pow == b_pow &&
                     sc.r_free == b_free && sc.r_tot == b_tot;
@@ -2073,25 +2106,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       u_free = b_free;
       u_tot = b_tot;
     }
-    if (lane == (uint32_t)l) {
-      uint32_t* r = lds + RCPS + 8 * nsets;
-      r[0] = (uint32_t)__float_as_int(b_bw);
-      r[1] = (uint32_t)__float_as_int(b_core);
-      r[2] = (uint32_t)__float_as_int(b_pow);
-      const uint64_t f = (uint64_t)__double_as_longlong(b_free);
-      const uint64_t t = (uint64_t)__double_as_longlong(b_tot);
-      r[4] = (uint32_t)f;
-      r[5] = (uint32_t)(f >> 32);
-      r[6] = (uint32_t)t;
-      r[7] = (uint32_t)(t >> 32);
+    if (lane == (uint32_t)l) {  // (bw, core, power in RS at word 0; free, total at word 8)
+      RS* r = reinterpret_cast<RS*>(lds + RCPS + 16 * nsets);
+      r[0] = b_bw;
+      r[1] = b_core;
+      r[2] = b_pow;
+      double* d = reinterpret_cast<double*>(lds + RCPS + 16 * nsets + 8);
+      d[0] = b_free;
+      d[1] = b_tot;
     }
   }
   const bool uni_max = nsets <= 1u && rem == 0ull;  // "uniform maxima"
   const bool rec_ok = rem == 0ull;  // every active lane has a set: node records serve it
   // the wave's reciprocals are the snapshot-wide maxima's: the G table serves its terms
-  const bool use_g = uni_max && args.g.tab != nullptr && u_bw == args.g.r_bw &&
-                     u_core == args.g.r_core && u_pow == args.g.r_pow &&
-                     u_free == args.g.r_free && u_tot == args.g.r_tot;
+  RS g_bw, g_core, g_pow;
+  if constexpr (Q32) {
+    g_bw = args.g.f_bw;
+    g_core = args.g.f_core;
+    g_pow = args.g.f_pow;
+  } else {
+    g_bw = args.g.r_bw;
+    g_core = args.g.r_core;
+    g_pow = args.g.r_pow;
+  }
+  const bool use_g = uni_max && args.g.tab != nullptr && u_bw == g_bw && u_core == g_core &&
+                     u_pow == g_pow && u_free == args.g.r_free && u_tot == args.g.r_tot;
   const uint32_t m_max = wave_max_u32(act ? sc.m : 0u), m_min = wave_min_u32(act ? sc.m : ~0u);
   const uint32_t c_max = wave_max_u32(act ? sc.c : 0u), c_min = wave_min_u32(act ? sc.c : ~0u);
   // Block pruning (argmax, G waves): a block whose bound -- the most any node of it can score
@@ -2378,16 +2417,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
                                                             (uint32_t)(stat_u >> 32), 0u, 0u);
           }
           for (uint32_t q = 0; q < nsets; ++q) {
-            const uint32_t* r = lds + RCPS + 8 * q;  // the set's reciprocals (broadcast)
-            const float v_bw = __int_as_float((int)r[0]), v_core = __int_as_float((int)r[1]);
-            const float v_pow = __int_as_float((int)r[2]);
-            const double v_free =
-                __longlong_as_double((long long)((uint64_t)r[4] | ((uint64_t)r[5] << 32)));
-            const double v_tot =
-                __longlong_as_double((long long)((uint64_t)r[6] | ((uint64_t)r[7] << 32)));
-            const uint32_t shared = (uint32_t)((float)bw * v_bw) + (uint32_t)((float)ck * v_bw) +
-                                    2u * (uint32_t)((float)core * v_core) +
-                                    (uint32_t)((float)pw * v_pow);
+            // the set's reciprocals (broadcast)
+            const RS* r = reinterpret_cast<const RS*>(lds + RCPS + 16 * q);
+            const double* d = reinterpret_cast<const double*>(lds + RCPS + 16 * q + 8);
+            const double v_free = d[0], v_tot = d[1];
+            const uint32_t shared = card_shared_terms(bw, ck, core, pw, r[0], r[1], r[2]);
             uint32_t sel = 0, sel_hi = 0;
             // the set's prefix row of this node lane (TT > 1, the first TT sets)
             uint32_t* trow = lds + row_base(q < TT ? q : 0u) + lane * PSW;
@@ -2525,13 +2559,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
           basic = ckj >= sc.c ? tab[nq] : 0u;
         } else {
           // several reciprocal sets: Scorer<N32>'s one-model branch on the node lane's data,
-          // with its own reciprocals (shared quotients f32, memory quotients f64)
-          const Scorer<Path::N32>& own = sc;
-          const uint32_t shared =
-            (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.x, j) * own.r_bw) +
-            (uint32_t)((float)ckj * own.r_bw) +
-            2u * (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.y, j) * own.r_core) +
-            (uint32_t)((float)(uint32_t)__builtin_amdgcn_readlane((int)h1.z, j) * own.r_pow);
+          // with its own reciprocals
+          const auto& own = sc;
+          const uint32_t shared = card_shared_terms(
+              (uint32_t)__builtin_amdgcn_readlane((int)h1.x, j), ckj,
+              (uint32_t)__builtin_amdgcn_readlane((int)h1.y, j),
+              (uint32_t)__builtin_amdgcn_readlane((int)h1.z, j), own.r_bw, own.r_core, own.r_pow);
           uint32_t mem = 0;
           auto terms = [&](auto rk) {
 #pragma unroll
@@ -3182,7 +3215,6 @@ __global__ __launch_bounds__(kBlock) void k_one_filter(const unsigned char* __re
   for (int k = 0; k < 5; ++k) {
     const double M = (double)acc[src[k]];
     out->rcp[k] = ru_100_over(M);
-    if (k < 3) out->rcp32[k] = ru32_100_over(M);
   }
   *done = 0u;
 }
@@ -3201,16 +3233,13 @@ __global__ __launch_bounds__(kBlock) void k_one_score(const unsigned char* __res
   if constexpr (PATH == Path::N32) {
     sc.m = pod.m32;
     sc.c = pod.c32;
-    sc.r_bw = out->rcp32[0];
-    sc.r_core = out->rcp32[1];
-    sc.r_pow = out->rcp32[2];
   } else {
     sc.m = pod.mf;
     sc.c = pod.cf;
-    sc.r_bw = out->rcp[0];
-    sc.r_core = out->rcp[1];
-    sc.r_pow = out->rcp[2];
   }
+  sc.r_bw = out->rcp[0];
+  sc.r_core = out->rcp[1];
+  sc.r_pow = out->rcp[2];
   sc.r_free = out->rcp[3];
   sc.r_tot = out->rcp[4];
   constexpr uint32_t stride = PATH == Path::N32 ? n32_stride(K) : node_stride(K);
@@ -4125,7 +4154,8 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                                       reinterpret_cast<const uint32_t*>(mix), pp.x1, n_nodes,  \
                                       chunk_nodes, pp.m_32, pp.c_32, pp.number, pp.need_mem,   \
                                       pp.need_clk, n_pods, part.max_u, part.cnt, bm, bm_stride, \
-                                      bs, bs_stride, blk, blk_stride, stats, nullptr, pp.bsum))
+                                      bs, bs_stride, blk, blk_stride, stats, nullptr, pp.bsum,   \
+                                      pp.nwords))
         if (sub == 1u) {
           if (stats) YODA_K1B(KK, true)
           else if (pp.one_model) YODA_K1B(KK, false, false)
@@ -4194,12 +4224,13 @@ int kernel_capacity(int K, Path path, int which, int mode_diskio) {
 // chunks, one wave per pod (strided over chunks) when there are many.
 constexpr uint32_t kWaveReduceChunks = 48;
 
-hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
+hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp,
                         hipStream_t s);
 
-// rcp / rcp32 non-null: also the reciprocals (k_prep2 fused; the wave variant runs it after)
-hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, bool narrow,
-                          uint64_t* maxima, uint32_t* counts, double* rcp, float* rcp32,
+// rcp non-null: also the reciprocals (k_prep2 fused; the wave variant runs it after)
+// nw: the block K1's partial words (kNarrowWords / kWideWords), 0: u64 partials [6][C][P]
+hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uint32_t nw,
+                          uint64_t* maxima, uint32_t* counts, double* rcp,
                           const MemTab& mt, hipStream_t s) {
   if (C > kWaveReduceChunks && n_pods >= 2 * kBlock) {
     // split the chunks so that ~64k threads read the partials, then atomics
@@ -4208,39 +4239,39 @@ hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, boo
     hipError_t e = hipMemsetAsync(maxima, 0, 6 * (size_t)n_pods * 8, s);
     if (e == hipSuccess) e = hipMemsetAsync(counts, 0, 2 * (size_t)n_pods * 4, s);
     if (e != hipSuccess) return e;
-    const dim3 grid(pb, narrow ? kNarrowWords + 2u : 8u, S);
-    if (narrow)
+    const dim3 grid(pb, nw ? nw + 2u : 8u, S);
+    if (nw)
       hipLaunchKernelGGL(k_reduce1_split<true>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
-                         n_pods, maxima, counts);
+                         n_pods, maxima, counts, nw);
     else
       hipLaunchKernelGGL(k_reduce1_split<false>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt,
-                         C, n_pods, maxima, counts);
+                         C, n_pods, maxima, counts, 0u);
     if (mt.vf)  // the atomics ran in rank space
       hipLaunchKernelGGL(k_rank_maxima, pod_grid(n_pods), dim3(kBlock), 0, s, maxima, n_pods, mt);
-    if (rcp) return launch_prep2(maxima, n_pods, rcp, rcp32, s);
+    if (rcp) return launch_prep2(maxima, n_pods, rcp, s);
   } else if (C > kWaveReduceChunks) {
-    if (narrow)
+    if (nw)
       hipLaunchKernelGGL(k_reduce1_wave<true>, dim3(n_pods), dim3(kWave), 0, s, part.max_u,
-                         part.cnt, C, n_pods, maxima, counts, mt);
+                         part.cnt, C, n_pods, maxima, counts, mt, nw);
     else
       hipLaunchKernelGGL(k_reduce1_wave<false>, dim3(n_pods), dim3(kWave), 0, s, part.max_u,
-                         part.cnt, C, n_pods, maxima, counts, mt);
-    if (rcp) return launch_prep2(maxima, n_pods, rcp, rcp32, s);
+                         part.cnt, C, n_pods, maxima, counts, mt, 0u);
+    if (rcp) return launch_prep2(maxima, n_pods, rcp, s);
   } else {
-    const dim3 grid((n_pods + kBlock - 1) / kBlock, narrow ? kNarrowWords + 2u : 8u);
-    if (narrow)
+    const dim3 grid((n_pods + kBlock - 1) / kBlock, nw ? nw + 2u : 8u);
+    if (nw)
       hipLaunchKernelGGL(k_reduce1<true>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
-                         n_pods, maxima, counts, rcp, rcp32, mt);
+                         n_pods, maxima, counts, rcp, mt, nw);
     else
       hipLaunchKernelGGL(k_reduce1<false>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
-                         n_pods, maxima, counts, rcp, rcp32, mt);
+                         n_pods, maxima, counts, rcp, mt, 0u);
   }
   return hipGetLastError();
 }
 
-hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp, float* rcp32,
+hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp,
                         hipStream_t s) {
-  hipLaunchKernelGGL(k_prep2, pod_grid(n_pods), dim3(kBlock), 0, s, maxima, n_pods, rcp, rcp32);
+  hipLaunchKernelGGL(k_prep2, pod_grid(n_pods), dim3(kBlock), 0, s, maxima, n_pods, rcp);
   return hipGetLastError();
 }
 
@@ -4258,13 +4289,13 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
                               const unsigned char* sum2, const uint64_t* blk, uint32_t blk_stride,
                               uint32_t n_nodes,
                               uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
-                              const uint64_t* maxima, const double* rcp, const float* rcp32,
+                              const uint64_t* maxima, const double* rcp,
                               uint32_t n_pods, const uint64_t* bm, uint32_t bm_stride,
                               const BlockMask* bs, uint32_t bs_stride, const Partials& part,
                               int64_t* rows, double* tk_s, uint32_t* tk_i,
                               unsigned long long* stats, const uint32_t* counts, hipStream_t s) {
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
-  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g, pp.mix, pp.mt,
+  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, counts, pp.g, pp.mix, pp.mt,
                     pp.ids, OUT == OUT_ARGMAX ? pp.kbub : nullptr,
                     OUT == OUT_ARGMAX ? pp.hot : nullptr};
   const MaskSrc ms{bm, bs, bm_stride, bs_stride, blk, blk_stride};
@@ -4272,22 +4303,29 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
   switch (path) {
     case Path::N32:
       if (OUT == OUT_ARGMAX && sum2) {
-#define YODA_K2B(ST, RKV)                                                                        \
-  YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, ST, 0, RKV>), grid, dim3(kBlock), 0, s,  \
-                                      nodes, sum2, n_nodes, chunk_nodes, a, n_pods, bm, bm_stride, \
-                                      bs, bs_stride, blk, blk_stride, part.best_f, part.idx,      \
-                                      part.ties, part.low_f, stats, nullptr, 0u))
-        // memory ranks: the kernel of its own (RK = true)
-        if (stats) {
-          if (a.mt.vf) YODA_K2B(true, true) else YODA_K2B(true, false);
+#define YODA_K2B(ST, RKV, MIXV, Q32V)                                                           \
+  YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, ST, 0, RKV, MIXV, Q32V>), grid,          \
+                                      dim3(kBlock), 0, s, nodes, sum2, n_nodes, chunk_nodes, a,   \
+                                      n_pods, bm, bm_stride, bs, bs_stride, blk, blk_stride,      \
+                                      part.best_f, part.idx, part.ties, part.low_f, stats,        \
+                                      nullptr, 0u))
+        // memory ranks: the kernel of its own (RK = true); small fields beyond kF32SmallMax
+        // (one-model snapshots only, yoda_capi.cpp n32_ok): the f64-quotient kernels
+        if (!pp.q32) {
+          if (stats) {
+            if (a.mt.vf) YODA_K2B(true, true, true, false) else YODA_K2B(true, false, true, false);
+          } else if (a.mt.vf) {
+            YODA_K2B(false, true, true, false);
+          } else {
+            if (!pp.all_uni4) return hipErrorInvalidValue;
+            YODA_K2B(false, false, false, false);
+          }
+        } else if (stats) {
+          if (a.mt.vf) YODA_K2B(true, true, true, true) else YODA_K2B(true, false, true, true);
         } else if (pp.all_uni4 && !a.mt.vf) {
-          YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false, 0, false, false>), grid,
-                                              dim3(kBlock), 0, s, nodes, sum2, n_nodes,
-                                              chunk_nodes, a, n_pods, bm, bm_stride, bs,
-                                              bs_stride, blk, blk_stride, part.best_f, part.idx,
-                                              part.ties, part.low_f, stats, nullptr, 0u));
+          YODA_K2B(false, false, false, true);
         } else {
-          if (a.mt.vf) YODA_K2B(false, true) else YODA_K2B(false, false);
+          if (a.mt.vf) YODA_K2B(false, true, true, true) else YODA_K2B(false, false, true, true);
         }
 #undef YODA_K2B
         break;
@@ -4316,14 +4354,14 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
 
 hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t n_nodes,
                           uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
-                          const double* rcp, const float* rcp32, uint32_t n_pods,
+                          const double* rcp, uint32_t n_pods,
                           const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
                           uint32_t bs_stride, const uint64_t* blk, uint32_t blk_stride,
                           const Partials& part, double* tk_s, uint32_t* tk_i, int tk,
                           hipStream_t s) {
   if (tk != kTopK && tk != kTopKCap) return hipErrorInvalidValue;
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
-  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
+  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp};
   const MaskSrc ms{bm, bs, bm_stride, bs_stride, blk, blk_stride};
   if (bs && !blk) return hipErrorInvalidValue;  // sparse masks are read through their block list
 #define YODA_TOPK(PTH, TKV)                                                                      \
@@ -4350,30 +4388,37 @@ hipError_t launch_k2_topk(int K, Path path, const unsigned char* nodes, uint32_t
 hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigned char* sum2,
                                 const uint64_t* blk, uint32_t blk_stride, uint32_t n_nodes,
                                 uint32_t chunk_nodes, uint32_t C, const PodParams& pp,
-                                const double* rcp, const float* rcp32, uint32_t n_pods,
+                                const double* rcp, uint32_t n_pods,
                                 const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
                                 uint32_t bs_stride, const uint32_t* counts, uint64_t* keys,
                                 uint32_t ib, int tk, hipStream_t s) {
   if ((tk != kTopK && tk != kTopKCap) || K > 8 || n_pods == 0) return hipErrorInvalidValue;
   if (bs && !blk) return hipErrorInvalidValue;  // sparse masks are read through their block list
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
-  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32, counts, pp.g, pp.mix, pp.mt,
+  const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, counts, pp.g, pp.mix, pp.mt,
                     nullptr, pp.kbub};
-#define YODA_TOPKB(TKV, RKV, MIXV)                                                              \
-  YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false, TKV, RKV, MIXV>), grid,            \
+#define YODA_TOPKB(TKV, RKV, MIXV, Q32V)                                                        \
+  YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false, TKV, RKV, MIXV, Q32V>), grid,      \
                                       dim3(kBlock), 0, s, nodes, sum2, n_nodes, chunk_nodes, a,   \
                                       n_pods, bm, bm_stride, bs, bs_stride, blk, blk_stride,      \
                                       nullptr, nullptr, nullptr, nullptr, nullptr, keys, ib))
-  // one-model snapshots without memory ranks: the kernel without the mixed-model rows
+  // one-model snapshots without memory ranks: the kernel without the mixed-model rows;
+  // small fields beyond kF32SmallMax (one-model snapshots only): the f64-quotient kernels
   const bool lean = pp.all_uni4 && !a.mt.vf;
+  if (!pp.q32 && !a.mt.vf && !lean) return hipErrorInvalidValue;
   if (tk == kTopK) {
-    if (a.mt.vf) YODA_TOPKB(kTopK, true, true)
-    else if (lean) YODA_TOPKB(kTopK, false, false)
-    else YODA_TOPKB(kTopK, false, true);
+    if (!pp.q32) {
+      if (a.mt.vf) YODA_TOPKB(kTopK, true, true, false) else YODA_TOPKB(kTopK, false, false, false);
+    } else if (a.mt.vf) YODA_TOPKB(kTopK, true, true, true)
+    else if (lean) YODA_TOPKB(kTopK, false, false, true)
+    else YODA_TOPKB(kTopK, false, true, true);
   } else {
-    if (a.mt.vf) YODA_TOPKB(kTopKCap, true, true)
-    else if (lean) YODA_TOPKB(kTopKCap, false, false)
-    else YODA_TOPKB(kTopKCap, false, true);
+    if (!pp.q32) {
+      if (a.mt.vf) YODA_TOPKB(kTopKCap, true, true, false)
+      else YODA_TOPKB(kTopKCap, false, false, false);
+    } else if (a.mt.vf) YODA_TOPKB(kTopKCap, true, true, true)
+    else if (lean) YODA_TOPKB(kTopKCap, false, false, true)
+    else YODA_TOPKB(kTopKCap, false, true, true);
   }
 #undef YODA_TOPKB
   return hipGetLastError();
@@ -4461,12 +4506,12 @@ uint32_t greedy_one_blocks() { return kGreedyOneBlocks; }
 
 hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes,
                              const unsigned char* sum2, uint32_t n_nodes,
-                             const PodParams& pp, const double* rcp, const float* rcp32,
+                             const PodParams& pp, const double* rcp,
                              uint32_t n_pods, uint32_t s, const uint64_t* bm, uint32_t bm_stride,
                              const BlockMask* bs, uint32_t bs_stride, const uint64_t* blk,
                              uint32_t blk_stride, double* part_s, uint32_t* part_i,
                              uint32_t* done, uint32_t* out, hipStream_t st) {
-  ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, rcp32};
+  ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp};
   a.g = pp.g;
   a.mt = pp.mt;
   const MaskSrc ms{bm, bs, bm_stride, bs_stride, blk, blk_stride};
@@ -4494,16 +4539,14 @@ hipError_t launch_greedy_one(int K, Path path, const unsigned char* nodes,
 hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigned char* sum2,
                      const uint64_t* blk, uint32_t blk_stride, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
-                     const double* rcp, const float* rcp32, uint32_t n_pods,
+                     const double* rcp, uint32_t n_pods,
                      const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
                      uint32_t bs_stride, const Partials& part, int64_t* rows,
                      unsigned long long* stats, const uint32_t* counts, hipStream_t s) {
   if (rows)
-    return launch_k2_t<OUT_ROWS>(K, path, nodes, nullptr, blk, blk_stride, n_nodes, chunk_nodes, C, pp, maxima, rcp,
-                                 rcp32, n_pods, bm, bm_stride, bs, bs_stride, part, rows, nullptr,
+    return launch_k2_t<OUT_ROWS>(K, path, nodes, nullptr, blk, blk_stride, n_nodes, chunk_nodes, C, pp, maxima, rcp, n_pods, bm, bm_stride, bs, bs_stride, part, rows, nullptr,
                                  nullptr, stats, counts, s);
-  return launch_k2_t<OUT_ARGMAX>(K, path, nodes, sum2, blk, blk_stride, n_nodes, chunk_nodes, C, pp, maxima, rcp,
-                                 rcp32, n_pods, bm, bm_stride, bs, bs_stride, part, rows, nullptr,
+  return launch_k2_t<OUT_ARGMAX>(K, path, nodes, sum2, blk, blk_stride, n_nodes, chunk_nodes, C, pp, maxima, rcp, n_pods, bm, bm_stride, bs, bs_stride, part, rows, nullptr,
                                  nullptr, stats, counts, s);
 }
 

@@ -15,17 +15,17 @@ constexpr int kWave = 64;
 constexpr uint32_t kChunkAlign = 64;    // node-chunk granularity (one K1 node block)
 
 // Three exact record formats, chosen per snapshot by the host:
-//   N32  every card field <= 0xFFFFFFFE and bandwidth/clock/core/power <= 55738
-//        (so 300 x + M < 2^24 for every f32 quotient): K1 runs on u32, K2's bandwidth/clock/core/
-//        power quotients in f32 (proof + exhaustive check: tools/check_div_lemma.c), the
-//        memory quotients in f64, the card score accumulates in u32.
+//   N32  every card field <= 0xFFFFFFFE (memory beyond that: ranks, MemTab) and the card score
+//        below 2^32 / K: K1 runs on u32, every K2 quotient in f64 (300 x + M < 2^53: the
+//        quotient lemma; tools/check_div_lemma.c), the card score accumulates in u32.
 //   F64  every card field <= 2^44 and every score < 2^52: everything in exact f64.
 //   U64  anything else: Go's uint64 wrap-around arithmetic verbatim.
 enum class Path : int { N32 = 0, F64 = 1, U64 = 2 };
 constexpr uint64_t kFastFieldMax = 1ull << 44;
 constexpr uint64_t kFastScoreMax = 1ull << 52;
 constexpr uint64_t kN32FieldMax = 0xFFFFFFFEull;
-constexpr uint64_t kN32SmallFieldMax = 55738;  // 301 * 55738 < 2^24
+// bandwidth, clock, core, power <= this: 301 * 55738 < 2^24, the f32 quotient lemma holds
+constexpr uint64_t kF32SmallMax = 55738;
 
 // Record header of the fast path (32 B).  Cards follow: 6 groups of K doubles:
 //   free[K], clock[K], total[K], bandwidth[K], core[K], power[K].
@@ -63,20 +63,16 @@ constexpr int kCardFields = 6;
 // F64 / U64 record: header + 6 groups of K 8-byte fields in CardField order.
 __host__ __device__ constexpr uint32_t node_stride(int k) { return 32u + 48u * (uint32_t)k; }
 
-// N32 record: header (NodeHdrF) + 6 groups of K u32 in CardField order (K1 + the K2 card
-// predicate) + 4 groups of K f32 {bandwidth, clock, core, power} + 2 groups of K f64
-// {free, total} (K2 quotients).
-__host__ __device__ constexpr uint32_t n32_stride(int k) { return 32u + 56u * (uint32_t)k; }
+// N32 record: header (NodeHdrF) + 6 groups of K u32 in CardField order (K1, the K2 card
+// predicate and the small-field quotients) + 2 groups of K f64 {free, total}: the memory
+// values (memory ranks: the u32 groups hold ranks) for the K2 quotients.
+__host__ __device__ constexpr uint32_t n32_stride(int k) { return 32u + 40u * (uint32_t)k; }
 __host__ __device__ constexpr uint32_t n32_u32_off(int field, int k) {
   return 32u + 4u * (uint32_t)(field * k);
 }
-enum N32F32 { kF32Bandwidth = 0, kF32Clock = 1, kF32Core = 2, kF32Power = 3 };
-__host__ __device__ constexpr uint32_t n32_f32_off(int g, int k) {
-  return 32u + 24u * (uint32_t)k + 4u * (uint32_t)(g * k);
-}
 enum N32F64 { kF64Free = 0, kF64Total = 1 };
 __host__ __device__ constexpr uint32_t n32_f64_off(int g, int k) {
-  return 32u + 40u * (uint32_t)k + 8u * (uint32_t)(g * k);
+  return 32u + 24u * (uint32_t)k + 8u * (uint32_t)(g * k);
 }
 
 // K1 node summary (N32 path): the Filter / PreScore facts of one node in a few u32 words,
@@ -174,7 +170,8 @@ __host__ __device__ constexpr uint32_t mix_stride(int k) { return 4u * (4u * (ui
 //   pm[q-1]  for q = 1..K, the maxima over the first q cards of (clock | bandwidth << 16)
 //            and (core | power << 16) per 16-bit half, and of TotalMemory (K2 summary code)
 //   cd[t]    card t's (clock | bandwidth << 16), (core | power << 16)
-// (N32: clock, bandwidth, core and power are <= 55738, so each fits 16 bits.)  Tile layout
+// (a snapshot with such nodes keeps clock, bandwidth, core and power <= 65535: yoda_capi.cpp
+// n32_ok.)  Tile layout
 // like the summaries (sum_index).
 enum K1MixWord { kX1Chg = 0, kX1Ch = 1, kX1Pm = 5 };
 __host__ __device__ constexpr uint32_t x1_pm(int q1, int f) { return kX1Pm + 3u * (uint32_t)q1 + (uint32_t)f; }
@@ -266,7 +263,6 @@ struct alignas(16) OneOut {
   uint64_t maxima[6];         // PreScore maxima, MaxValue order (floor 1)
   uint32_t nf, nz, first, pad;  // feasible nodes, of them TotalMemorySum == 0, lowest one
   double rcp[5];              // RU(100/M): bw, core, power, free, total
-  float rcp32[3], pad2;       // RU32(100/M): bw, core, power
   double best, low;           // highest / lowest raw score over the feasible nodes
   uint32_t idx, ties;         // lowest node reaching best, nodes reaching it
 };
@@ -287,11 +283,11 @@ struct PtrList {
 
 // Per-pod device parameters (struct of arrays, length P each).
 // The "G table" of an N32 snapshot (yoda_kernels.hip k_gtable / k2_block_n32): per-node terms
-// under the snapshot-wide maxima G, and G's reciprocals (f32 bw, core, power; f64 free, total).
+// under the snapshot-wide maxima G, and G's reciprocals (f64 bw, core, power, free, total).
 struct GTab {
   const uint32_t* tab;
-  float r_bw, r_core, r_pow;
-  double r_free, r_tot;
+  double r_bw, r_core, r_pow, r_free, r_tot;
+  float f_bw, f_core, f_pow;  // RU32 of r_bw, r_core, r_pow (the f32-quotient block K2's)
 };
 __host__ __device__ constexpr uint32_t gtab_stride(int k) { return 4u * (uint32_t)k; }
 
@@ -345,6 +341,10 @@ struct PodParams {
   const uint32_t* kbub = nullptr;
   // the blocks of that order with the highest bounds (bit words, as the K1 block list)
   const uint64_t* hot = nullptr;
+  // the block K1's partial words: kNarrowWords (small fields <= kPack16Max) or kWideWords
+  uint32_t nwords = 4;
+  // the block K2's small-field quotients in f32 (every small field <= kF32SmallMax), else f64
+  bool q32 = true;
 };
 
 // Per-pod state produced between kernels (length P each unless noted).
@@ -352,7 +352,6 @@ struct PodState {
   uint64_t* maxima;    // [6][P] MaxValue in collection.go field order (see kMax* below)
   uint32_t* counts;    // [2][P] n_feasible, n_zero_total
   double* rcp;         // [5][P] RU(100 / M) for bw, core, power, free, total (f64)
-  float* rcp32;        // [3][P] RU32(100 / M) for bw, core, power (narrow path)
   int64_t* best;       // [P] highest raw score over feasible nodes (-1: none)
   uint32_t* idx;       // [P] lowest global node index reaching it
   uint32_t* ties;      // [P] nodes reaching it
@@ -366,10 +365,12 @@ struct PodState {
 // MaxValue field order (collection.go:14-21) used for the [6][P] maxima buffer.
 enum MaxField { kMaxBw = 0, kMaxClock = 1, kMaxCore = 2, kMaxFree = 3, kMaxPower = 4, kMaxTotal = 5 };
 
-// Chunk partials: [field][chunk][P].  The block K1 (N32) writes its maxima packed into
-// kNarrowWords u32 words (bandwidth | clock << 16, core | power << 16, free, total: the four
-// small fields are <= 55738 on that path), read back by k_reduce1<true>.
+// Chunk partials: [field][chunk][P].  The block K1 (N32) writes its maxima as u32 words, read
+// back by k_reduce1<true>: packed into kNarrowWords (bandwidth | clock << 16, core | power << 16,
+// free, total) when the four small fields are <= 65535, else kWideWords (one per field).
 constexpr uint32_t kNarrowWords = 4;
+constexpr uint32_t kWideWords = 6;
+constexpr uint64_t kPack16Max = 0xFFFF;
 struct Partials {
   uint64_t* max_u;     // [6][C][P]
   uint32_t* cnt;       // [2][C][P]

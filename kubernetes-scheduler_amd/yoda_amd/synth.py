@@ -141,6 +141,16 @@ def memory_in_bytes(nodes: NodeSoA, pods: PodSoA):
     return n.normalized(), p.normalized()
 
 
+def wide_fields(nodes: NodeSoA, fields=("bandwidth",), factor: int = 1000) -> NodeSoA:
+    """The same fleet with small card fields scaled (e.g. bandwidth in MB/s instead of GB/s):
+    beyond 16 bits, the N32 kernels with unpacked K1 partials and f64 quotients.
+    Scale the pods' scv/clock labels with the clock, or the Filter changes."""
+    n = _copy(nodes)
+    for f in fields:
+        setattr(n, "card_" + f, getattr(n, "card_" + f) * np.uint64(factor))
+    return n.normalized()
+
+
 def distinct_diskio(pods: PodSoA, seed: int = 11) -> PodSoA:
     """The same pods with a distinct Mode-B request each: diskIO annotation U(0.5, 100) and a
     CPU request U{50..4000} millicores, so no two pods share (alpha, beta) and the Mode-B batch
@@ -182,6 +192,8 @@ VARIANTS = {
     "mixed100": "config 3 with every node holding mixed GPU models",
     "bytes": "config 3 with memory in bytes instead of MiB (fields above 2^32: memory ranks)",
     "u64": "config 3 forced onto the U64 record path (the reference's uint64 arithmetic)",
+    "f64": "config 3 forced onto the F64 record path (per-pair kernels, fields <= 2^44)",
+    "bw1000": "config 3 with bandwidth x 1000 (small fields beyond 16 bits: N32, f64 quotients)",
     "c4": "config 4 at its declared size (10k pods x 20k nodes, heterogeneous fleet)",
     "het100k": "config-4 generator at 100k pods x 100k nodes",
     "diskio": "config 3, Mode B (BalancedCpuDiskIOPriority), pods as generated (one spec)",
@@ -219,6 +231,10 @@ def variant_workloads(names):
             n, p = memory_in_bytes(n, p)
         elif name == "u64":
             kw = {"force_generic": True}
+        elif name == "f64":
+            kw = {"force_f64": True}
+        elif name == "bw1000":
+            n = wide_fields(n, ("bandwidth",), 1000)
         elif name == "diskio_distinct":
             p = distinct_diskio(p)
         if name.startswith("diskio") or name == "c4diskio":

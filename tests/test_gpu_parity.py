@@ -91,7 +91,8 @@ def test_every_record_path(dev, path):
 
 def test_wide_memory_fields(dev):
     # free memory in bytes (> 2^32): the N32 kernels with memory ranks (yoda_layout.h MemTab);
-    # a wide small field (bandwidth > 55738) takes the F64 per-pair kernels instead
+    # a wide small field on a mixed-model node (bandwidth > 65535, one card) takes the F64
+    # per-pair kernels instead (tests/test_gpu_wide.py: one-model nodes stay on N32)
     nodes, pods = synth.make_config(2, pods=200, nodes=1500)
     nodes.card_free_memory[:] *= np.uint64(1 << 20)
     nodes.card_total_memory[:] *= np.uint64(1 << 20)
@@ -364,7 +365,7 @@ def test_sharded_paths_agree(dev):
     import torch
     from yoda_amd.dist import ShardExchange
     nodes, pods = synth.make_config(2, pods=300, nodes=2000)
-    nodes.card_bandwidth[1500, 0] = np.uint64(70000)   # > 55738: F64 on shard 1 only
+    nodes.card_bandwidth[1500, 0] = np.uint64(70000)   # > 16 bits, mixed model: F64 on shard 1 only
     want = oracle.schedule(nodes, pods, MODE_SCV, threads=8)
     shards = [nodes.slice(0, 1000), nodes.slice(1000, 2000)]
     handles = []
