@@ -161,12 +161,17 @@ int yoda_synchronize(yoda_t* h);
                                         node's card terms itself; tests, A/B)         */
 #define YODA_UPLOAD_MEM_RANKS 64u    /* N32: memory ranks even when every memory field
                                         fits 32 bits (tests, A/B)                     */
+#define YODA_UPLOAD_F64_QUOTIENTS 128u /* N32: small-field quotients in f64 even when
+                                        every bandwidth/clock/core/power <= 55738 --
+                                        for a node shard whose peers hold wider
+                                        fields (yoda_small_field_max); a shard with
+                                        mixed-model nodes then takes YODA_PATH_F64    */
 int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nodes, uint32_t node_offset,
                       uint32_t flags);
 /* 1 if the uploaded snapshot runs on the generic (u64) path, 0 on a fast path. */
 int yoda_uses_generic_path(const yoda_t* h);
-/* Record format of the uploaded snapshot: YODA_PATH_N32 (u32/f32 fields + f64 memory
- * quotients), YODA_PATH_F64 (exact f64) or YODA_PATH_U64 (exact uint64 wrap-around). */
+/* Record format of the uploaded snapshot: YODA_PATH_N32 (u32 fields; f32 or f64 quotients,
+ * DESIGN.md §5), YODA_PATH_F64 (exact f64) or YODA_PATH_U64 (exact uint64 wrap-around). */
 #define YODA_PATH_N32 0
 #define YODA_PATH_F64 1
 #define YODA_PATH_U64 2
@@ -176,6 +181,14 @@ int yoda_record_path(const yoda_t* h);
  * quotients and the maxima -- DESIGN.md §3), 0 if as values; -1 for a NULL handle.  The
  * PreScore maxima returned and exchanged are values either way. */
 int yoda_memory_ranks(const yoda_t* h);
+/* The largest bandwidth, clock, core or power of any card of the uploaded snapshot.  N32
+ * computes their quotients in f32 while every maximum it divides by is <= 55738 and in f64
+ * beyond (every bandwidth/clock/core/power up to 2^32 - 2 stays on N32 when every node holds
+ * one GPU model with one TotalMemory).  Node shards exchange maxima, so all shards must agree:
+ * when the MAX of this over the shards exceeds 55738, re-upload the others with
+ * YODA_UPLOAD_F64_QUOTIENTS (yoda_amd/dist.py agree_on_path) before agreeing on the record
+ * path.  0 for a NULL handle. */
+uint64_t yoda_small_field_max(const yoda_t* h);
 /* An upper bound on every raw Score of the uploaded snapshot whatever its allocated memory
  * (Basic at the largest clock + the largest Allocate 300 + Actual); ~0 when unbounded.  The
  * sharded merge packs (score, node) into one 64-bit key when it fits (yoda_amd/dist.py). */

@@ -444,7 +444,8 @@ struct yoda_handle {
   uint32_t C1 = 1, chunk1 = 32;  // K1 node chunking (partial chunks; chunk1: nodes per K1 wave)
   uint32_t k1_sub = 1;
   bool pack16 = true;            // N32: the small card fields fit 16 bits (packed K1 partials)
-  bool q32 = true;               // ... and <= kF32SmallMax (the block K2's f32 quotients)           // K1 waves per chunk (4: k1_block_n32's SUB, chunk1 = a quarter)
+  bool q32 = true;               // ... and <= kF32SmallMax (the block K2's f32 quotients)
+  uint64_t small_max = 0;        // the largest bandwidth / clock / core / power (any path)           // K1 waves per chunk (4: k1_block_n32's SUB, chunk1 = a quarter)
   uint32_t C2 = 1, chunk2 = 32;  // K2 / K3 node chunking
   int cap[2][3][2] = {};         // resident workgroups per (kernel, path, mode), cached
   int last_mode = -1;
@@ -1577,7 +1578,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     // every compare and max is unchanged, the values come back for the quotients and the
     // maxima (all <= 2^44: exact in f64).
     const bool pack16 = max_small <= kPack16Max;
-    const bool q32 = max_small <= kF32SmallMax;
+    const bool q32 = max_small <= kF32SmallMax && !(flags & YODA_UPLOAD_F64_QUOTIENTS);
     const bool n32_ok = f64_ok && max_small <= kN32FieldMax && (q32 || all_one) &&
                         (uint64_t)K * (800u + max_ckq) < (1ull << 32);
     Path path = n32_ok ? Path::N32 : (f64_ok ? Path::F64 : Path::U64);
@@ -2069,6 +2070,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     h->mem_ranks = ranks;
     h->pack16 = pack16;
     h->q32 = q32;
+    h->small_max = max_small;
     h->kbub_dirty = true;
     h->kbub_loose = false;
     h->hot_ok = false;
@@ -2137,6 +2139,7 @@ int yoda_uses_generic_path(const yoda_t* h) { return h ? (h->generic ? 1 : 0) : 
 int yoda_record_path(const yoda_t* h) { return h ? (int)h->path : -1; }
 
 int yoda_memory_ranks(const yoda_t* h) { return h ? (h->mem_ranks ? 1 : 0) : -1; }
+uint64_t yoda_small_field_max(const yoda_t* h) { return h ? h->small_max : 0; }
 
 uint64_t yoda_score_bound(const yoda_t* h) { return h && h->has_nodes ? h->score_bound : ~0ull; }
 

@@ -165,9 +165,34 @@ func (g *Handle) UploadNodes(names []string, scvs []*scv.Scv, allocMemory []uint
 }
 
 // UploadShard is UploadNodes for one node shard of a multi-GPU snapshot: offset is the global
-// index of names[0] (picks and node ids are global; see CommInit).
+// index of names[0] (picks and node ids are global; see CommInit).  Shards exchange maxima, so
+// they must agree on the record path and the N32 quotient type: exchange SmallFieldMax and
+// RecordPath out of band and, when another shard's SmallFieldMax exceeds 55738, upload again
+// with UploadShardFlags(..., UploadF64Quotients), then with UploadForceF64 where any shard
+// reports PathF64 (include/yoda.h yoda_small_field_max; yoda_amd/dist.py agree_on_path).
 func (g *Handle) UploadShard(names []string, scvs []*scv.Scv, allocMemory []uint64,
 	cpu, diskIO []float64, offset uint32) error {
+	return g.UploadShardFlags(names, scvs, allocMemory, cpu, diskIO, offset, 0)
+}
+
+// Upload flags (include/yoda.h YODA_UPLOAD_*) and record paths (YODA_PATH_*).
+const (
+	UploadForceF64     = uint32(C.YODA_UPLOAD_FORCE_F64)
+	UploadF64Quotients = uint32(C.YODA_UPLOAD_F64_QUOTIENTS)
+	PathN32            = int(C.YODA_PATH_N32)
+	PathF64            = int(C.YODA_PATH_F64)
+	PathU64            = int(C.YODA_PATH_U64)
+)
+
+// SmallFieldMax is the largest card bandwidth / clock / core / power of the uploaded snapshot.
+func (g *Handle) SmallFieldMax() uint64 { return uint64(C.yoda_small_field_max(g.h)) }
+
+// RecordPath is the uploaded snapshot's record format (PathN32, PathF64 or PathU64).
+func (g *Handle) RecordPath() int { return int(C.yoda_record_path(g.h)) }
+
+// UploadShardFlags is UploadShard with YODA_UPLOAD_* flags.
+func (g *Handle) UploadShardFlags(names []string, scvs []*scv.Scv, allocMemory []uint64,
+	cpu, diskIO []float64, offset uint32, flags uint32) error {
 	n := len(names)
 	if (scvs != nil && len(scvs) != n) || (allocMemory != nil && len(allocMemory) != n) {
 		return errors.New("yodagpu: names/allocMemory do not match the SCV list")
@@ -183,7 +208,7 @@ func (g *Handle) UploadShard(names []string, scvs []*scv.Scv, allocMemory []uint
 		return err
 	}
 	// &soa is a Go pointer to memory holding only C pointers: allowed
-	if err := check(g.h, C.yoda_upload_nodes(g.h, &soa, C.uint32_t(offset), 0),
+	if err := check(g.h, C.yoda_upload_nodes(g.h, &soa, C.uint32_t(offset), C.uint32_t(flags)),
 		"yoda_upload_nodes"); err != nil {
 		return err
 	}

@@ -40,6 +40,7 @@ _SIGS = {
     "yoda_uses_generic_path": ([_vp], C.c_int),
     "yoda_record_path": ([_vp], C.c_int),
     "yoda_memory_ranks": ([_vp], C.c_int),
+    "yoda_small_field_max": ([_vp], C.c_uint64),
     "yoda_score_bound": ([_vp], C.c_uint64),
     "yoda_update_alloc": ([_vp, C.POINTER(C.c_uint64)], C.c_int),
     "yoda_eval": ([_vp, C.POINTER(CPodSoA), C.c_int, C.POINTER(CEvalOut)], C.c_int),
@@ -188,12 +189,14 @@ class Yoda:
     def upload_nodes(self, nodes: NodeSoA, node_offset: int = 0, force_generic: bool = False,
                      force_f64: bool = False, no_uniform: bool = False,
                      per_node_k1: bool = False, per_node_k2: bool = False,
-                     no_gtab: bool = False, mem_ranks: bool = False):
+                     no_gtab: bool = False, mem_ranks: bool = False,
+                     f64_quotients: bool = False):
         self._nodes = nodes.normalized()
         cn = self._nodes.c()
         flags = ((1 if force_generic else 0) | (2 if force_f64 else 0) | (4 if no_uniform else 0)
                  | (8 if per_node_k1 else 0) | (16 if per_node_k2 else 0)
-                 | (32 if no_gtab else 0) | (64 if mem_ranks else 0))
+                 | (32 if no_gtab else 0) | (64 if mem_ranks else 0)
+                 | (128 if f64_quotients else 0))
         self._check(lib().yoda_upload_nodes(self._h, C.byref(cn), node_offset, flags),
                     "yoda_upload_nodes")
         self.n_nodes = self._nodes.n_nodes
@@ -207,6 +210,11 @@ class Yoda:
     def path_code(self) -> int:
         """0 = N32, 1 = F64, 2 = U64 (include/yoda.h YODA_PATH_*)."""
         return int(lib().yoda_record_path(self._h))
+
+    @property
+    def small_field_max(self) -> int:
+        """The largest card bandwidth / clock / core / power (yoda_small_field_max)."""
+        return int(lib().yoda_small_field_max(self._h))
 
     @property
     def memory_ranks(self) -> bool:

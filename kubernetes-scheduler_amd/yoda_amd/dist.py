@@ -214,17 +214,30 @@ def merge_witness(reduce: Reducer, bufs: List[ShardBuffers], prepare: Callable):
         b.wit[n:].copy_(b.wit_node64)
 
 
+F32_SMALL_MAX = 55738  # N32's f32 small-field quotients hold up to here (yoda_layout.h)
+
+
 def agree_on_path(reduce: Reducer, handles, shards, offsets, device):
     """Every shard must run the SAME record path: the exactness bounds of the fast paths
-    involve maxima contributed by other shards.  Take the widest path any
-    shard needs (N32 < F64 < U64) and re-upload the shards that chose a narrower one."""
+    involve maxima contributed by other shards.  First the N32 quotient
+    type: when any shard holds a bandwidth / clock / core / power beyond F32_SMALL_MAX, the
+    others re-upload with f64 quotients (yoda_small_field_max; a shard with mixed-model nodes
+    then takes F64).  Then the widest path any shard needs (N32 < F64 < U64): the shards that
+    chose a narrower one re-upload."""
+    small = [torch.tensor([h.small_field_max], dtype=torch.int64, device=device)
+             for h in handles]
+    reduce(small, "max")
+    wide = int(small[0].item()) > F32_SMALL_MAX
+    for h, nodes, off in zip(handles, shards, offsets):
+        if wide and h.path_code == 0 and h.small_field_max <= F32_SMALL_MAX:
+            h.upload_nodes(nodes, node_offset=off, f64_quotients=True)
     codes = [torch.tensor([h.path_code], dtype=torch.int64, device=device) for h in handles]
     reduce(codes, "max")
     target = int(codes[0].item())
     for h, nodes, off in zip(handles, shards, offsets):
         if h.path_code != target:
             h.upload_nodes(nodes, node_offset=off, force_generic=target == 2,
-                           force_f64=target == 1)
+                           force_f64=target == 1, f64_quotients=wide)
     return target
 
 

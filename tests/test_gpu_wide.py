@@ -123,3 +123,33 @@ def test_wide_fields_full_size_sample(dev):
 def _take(res, idx):
     return dataclasses.replace(res, **{f.name: getattr(res, f.name)[idx]
                                        for f in dataclasses.fields(res)})
+
+
+@pytest.mark.parametrize("mixed_narrow_shard", [False, True])
+def test_sharded_quotient_agreement(mixed_narrow_shard):
+    """Node shards exchange maxima: a narrow shard next to a wide one must not keep f32
+    quotients (their lemma needs every maximum <= 55,738).  dist.agree_on_path re-uploads it
+    with f64 quotients -- or, holding mixed-model nodes, on F64, and then every shard."""
+    import torch
+    from yoda_amd.dist import ShardExchange
+    nodes, pods = synth.make_config(3, pods=300, nodes=2000)
+    if mixed_narrow_shard:
+        part = synth.mixed_models(nodes.slice(0, 1000), 0.3)
+        for f in ("card_clock", "card_bandwidth", "card_core", "card_power"):
+            getattr(nodes, f)[:1000] = getattr(part, f)
+    nodes.card_bandwidth[1000:] = nodes.card_bandwidth[1000:] * np.uint64(1000)
+    want = oracle.schedule(nodes, pods, MODE_SCV, threads=8)
+    shards = [nodes.slice(0, 1000), nodes.slice(1000, 2000)]
+    handles = []
+    for i, sh in enumerate(shards):
+        y = Yoda(0)
+        y.upload_nodes(sh, node_offset=1000 * i)
+        y.upload_pods(pods)
+        handles.append(y)
+    assert handles[0].small_field_max <= 55738 < handles[1].small_field_max
+    assert [h.path for h in handles] == ["n32", "n32"]
+    ex = ShardExchange.local(handles, torch.device("cuda:0"), shards, [0, 1000])
+    assert [h.path for h in handles] == (["f64", "f64"] if mixed_narrow_shard else ["n32", "n32"])
+    assert_same(ex.run(MODE_SCV), want)
+    for y in handles:
+        y.close()
