@@ -4824,7 +4824,10 @@ hipError_t launch_reduce_wit(const uint64_t* pmax, const uint32_t* pwit, const u
                              uint32_t* counts, uint32_t* wcount, uint32_t* wnode, const MemTab& mt,
                              hipStream_t s) {
   if (n_pods == 0) return hipSuccess;
-  if (C > kWaveReduceChunks && n_pods >= kBlock) {
+  // many chunks (greedy windows: 64-node chunks): the chunk-split two-phase reduction, also
+  // for windows under 256 pods (the wave-per-pod kernel below read ~125 KB per pod there:
+  // ~88 us a window against ~30)
+  if (C > kWaveReduceChunks) {
     const uint32_t pb = (n_pods + kBlock - 1) / kBlock;
     const uint32_t S = std::max<uint32_t>(1, std::min<uint32_t>(C / 16, 256 / pb + 1));
     hipLaunchKernelGGL(k_init_wit, dim3((6 * n_pods + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
