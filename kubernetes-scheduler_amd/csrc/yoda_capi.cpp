@@ -36,7 +36,8 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                      unsigned long long* stats, hipStream_t s, uint32_t sub);
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uint32_t nw,
                           uint64_t* maxima, uint32_t* counts, double* rcp,
-                          const MemTab& mt, hipStream_t s);
+                          const MemTab& mt, hipStream_t s,
+                          uint32_t* lpt_w = nullptr, uint32_t* lpt_order = nullptr);
 hipError_t launch_mem_rank(const uint64_t* m_u, uint32_t n_pods, const MemTab& mt, uint32_t* m32,
                            hipStream_t s);
 hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp,
@@ -445,7 +446,11 @@ struct yoda_handle {
   uint32_t k1_sub = 1;
   bool pack16 = true;            // N32: the small card fields fit 16 bits (packed K1 partials)
   bool q32 = true;               // ... and <= kF32SmallMax (the block K2's f32 quotients)
-  uint64_t small_max = 0;        // the largest bandwidth / clock / core / power (any path)           // K1 waves per chunk (4: k1_block_n32's SUB, chunk1 = a quarter)
+  uint64_t small_max = 0;        // the largest bandwidth / clock / core / power (any path)
+  // heaviest-first pod blocks for the argmax block K2 (k_lpt_order): this run uses them,
+  // the per-wave weights K1 adds to (zero between runs), the order (valid once sorted)
+  bool lpt_active = false, lpt_sorted = false;
+  DevBuf lpt_w, lpt_order;           // K1 waves per chunk (4: k1_block_n32's SUB, chunk1 = a quarter)
   uint32_t C2 = 1, chunk2 = 32;  // K2 / K3 node chunking
   int cap[2][3][2] = {};         // resident workgroups per (kernel, path, mode), cached
   int last_mode = -1;
@@ -501,7 +506,7 @@ struct yoda_handle {
                      &order_bstart, &order_slot, &order_bkt,
                      &rcp,       &best,       &idx,          &ties,
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
-                     &n_flagged, &bitmask,   &bitmask_t,  &blk,  &bsum, &p_max_u,      &p_cnt,
+                     &n_flagged, &bitmask,   &bitmask_t,  &blk,  &bsum, &p_max_u,      &p_cnt, &lpt_w, &lpt_order,
                      &rows,      &rows_t,    &norm,      &tk_s_part,  &tk_i_part,    &tk_s,
                      &tk_i,      &upd_node,  &upd_val,    &upd_cn,    &g1_part,   &g1_done,
                      &p_best_f,  &p_best_i,  &p_idx,      &p_ties,       &p_low_f,
@@ -800,6 +805,10 @@ PodParams pod_params(yoda_t* h) {
   pp.mt = h->mem_ranks ? h->mt : MemTab{};
   pp.nwords = h->pack16 ? kNarrowWords : kWideWords;
   pp.q32 = h->q32;
+  if (h->lpt_active) {
+    pp.lpt_w = h->lpt_w.as<uint32_t>();
+    if (h->lpt_sorted) pp.lpt_order = h->lpt_order.as<uint32_t>();
+  }
   return pp;
 }
 
@@ -1142,7 +1151,10 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_m
   const bool rcp = final_maxima && !h->generic;
   HIP_TRY(h, launch_reduce1(part, h->C1, P, h->has_k1sum ? pod_params(h).nwords : 0u, maxima,
                             counts,
-                            rcp ? h->rcp.as<double>() : nullptr, pod_params(h).mt, h->stream));
+                            rcp ? h->rcp.as<double>() : nullptr, pod_params(h).mt, h->stream,
+                            h->lpt_active ? h->lpt_w.as<uint32_t>() : nullptr,
+                            h->lpt_active ? h->lpt_order.as<uint32_t>() : nullptr));
+  h->lpt_sorted = h->lpt_active;  // (the order of this run's pod blocks, for phase 2)
   h->rcp_ready = rcp;
   return YODA_OK;
 }
@@ -2445,6 +2457,20 @@ static int prepare_run(yoda_t* h, int mode, bool pad = false) {
                       (uint64_t)h->n_pad * 8 <= (uint64_t)h->n_pods * 9;
   h->n_work = padded ? h->n_pad : h->n_pods;
   plan_chunks(h, mode, h->n_work, h->n_nodes);
+  // a private argmax run on the block kernels visits its pod blocks heaviest first (the
+  // weights: K1's PART nodes per pod block; YODA_LPT=0: launch order)
+  static const bool lpt_env = YODA_KNOB("YODA_LPT", 1) != 0;
+  const uint32_t n_pb = (h->n_work + kBlock - 1) / kBlock;
+  h->lpt_sorted = false;
+  h->lpt_active = lpt_env && h->count_order && mode == YODA_MODE_SCV && h->path == Path::N32 &&
+                  h->has_k1sum && h->has_k2sum && n_pb >= 8 && n_pb <= 4096;
+  if (h->lpt_active) {
+    const size_t had = h->lpt_w.bytes;
+    HIP_TRY(h, h->lpt_w.ensure((size_t)((h->n_work + 63) / 64) * 4));
+    HIP_TRY(h, h->lpt_order.ensure((size_t)n_pb * 4));
+    if (h->lpt_w.bytes != had)  // fresh weights start at zero (k_lpt_order re-zeroes them)
+      HIP_TRY(h, hipMemsetAsync(h->lpt_w.p, 0, h->lpt_w.bytes, h->stream));
+  }
   return ensure_state(h, std::max<uint32_t>(h->n_work, 1));
 }
 

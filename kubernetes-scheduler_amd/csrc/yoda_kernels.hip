@@ -614,7 +614,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     uint64_t* __restrict__ bm, uint32_t bm_stride, BlockMask* __restrict__ bs,
     uint32_t bs_stride, uint64_t* __restrict__ blk, uint32_t blk_stride,
     unsigned long long* __restrict__ stats, uint32_t* __restrict__ pwit = nullptr,
-    const uint32_t* __restrict__ bsm = nullptr, uint32_t nwords = kNarrowWords) {
+    const uint32_t* __restrict__ bsm = nullptr, uint32_t nwords = kNarrowWords,
+    uint32_t* __restrict__ wts = nullptr) {
   static_assert(!(WIT && MIX), "the witness K1 serves one-model snapshots");
   static_assert(SUB == 1 || (SUB == kBlock / kWave && !WIT), "SUB: 1, or one pod wave per workgroup");
   constexpr uint32_t SS = k1sum_stride(K);
@@ -914,7 +915,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     }
     uint32_t lo = is_all ? (uint32_t)live_mask : 0u;
     uint32_t hi = is_all ? (uint32_t)(live_mask >> 32) : 0u;
-    if (STATS) npart += (uint32_t)__builtin_popcountll(part_b);
+    npart += (uint32_t)__builtin_popcountll(part_b);  // (STATS trace; wts)
     // One-model PART nodes: a record of the node's facts in LDS -- {CardNumber lo, hi,
     // clock, meta, max free + 1, hfs[need - 1], bandwidth, core, power, total} -- read by
     // the per-pod pass with broadcast loads, four nodes per trip, branch-free.
@@ -1139,6 +1140,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   nf_all += g_nf;
   nz_all += g_nz;
   blk_flush();
+  // the wave's weight for the K2's heaviest-first order (k_lpt_order): its PART nodes, summed
+  // over its chunks (one add per (wave, chunk); k_lpt_order reads and re-zeroes them)
+  if (wts != nullptr && lane == 0 && npart != 0u) atomicAdd(wts + (p >> 6), npart);
   if (trace && lane == 0) {
     unsigned long long* tr = stats + 16 + 4 * (((size_t)(p >> 6) * C + chunk) * SUB + sub);
     tr[0] = t_start;
@@ -1320,6 +1324,58 @@ __device__ __forceinline__ void store_rcp(int f, uint64_t mx, uint32_t n_pods, u
   if (rcp && k >= 0) rcp[(size_t)k * n_pods + p] = ru_100_over((double)mx);
 }
 
+// The block K2's pod-block order, heaviest first (longest processing time first: a heavy
+// pod block that starts late sets the kernel's tail).  Weight = the pod block's PART nodes in
+// K1 (wts [n_waves], summed over the chunks by k1_block_n32; zeroed here for the next run).
+// One workgroup: each pod block's rank = the blocks heavier than it (ties: lower index
+// first), counted over an LDS copy of the weights; n_pb <= kLptMax.
+constexpr uint32_t kLptMax = 4096;
+__device__ void lpt_order_body(uint32_t* __restrict__ wts, uint32_t n_waves, uint32_t n_pb,
+                               uint32_t* __restrict__ order, uint32_t* __restrict__ w) {
+  for (uint32_t i = threadIdx.x; i < n_pb; i += blockDim.x) {
+    uint32_t s = 0;
+    if (4 * i + 4 <= n_waves) {  // the block's four waves in one 16-byte load
+      const uint4 q = reinterpret_cast<const uint4*>(wts)[i];
+      reinterpret_cast<uint4*>(wts)[i] = make_uint4(0u, 0u, 0u, 0u);
+      s = q.x + q.y + q.z + q.w;
+    } else {
+      for (uint32_t v = 4 * i; v < n_waves; ++v) {
+        s += wts[v];
+        wts[v] = 0u;
+      }
+    }
+    w[i] = s;
+  }
+  const uint32_t n4 = (n_pb + 15u) & ~15u;  // zero padding (counts for no block)
+  for (uint32_t i = n_pb + threadIdx.x; i < n4; i += blockDim.x) w[i] = 0u;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n_pb; i += blockDim.x) {
+    const uint32_t wi = w[i];
+    uint32_t r = 0;
+    const uint4* w4 = reinterpret_cast<const uint4*>(w);
+    for (uint32_t j = 0; j < n4; j += 16) {  // four 16-byte LDS reads in flight per trip
+      uint4 q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q[k] = w4[(j >> 2) + (uint32_t)k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t b = j + 4u * (uint32_t)k;
+        r += (q[k].x > wi || (q[k].x == wi && b < i)) ? 1u : 0u;
+        r += (q[k].y > wi || (q[k].y == wi && b + 1u < i)) ? 1u : 0u;
+        r += (q[k].z > wi || (q[k].z == wi && b + 2u < i)) ? 1u : 0u;
+        r += (q[k].w > wi || (q[k].w == wi && b + 3u < i)) ? 1u : 0u;
+      }
+    }
+    order[r] = i;
+  }
+}
+__global__ __launch_bounds__(1024) void k_lpt_order(uint32_t* __restrict__ wts,
+                                                    uint32_t n_waves, uint32_t n_pb,
+                                                    uint32_t* __restrict__ order) {
+  __shared__ __attribute__((aligned(16))) uint32_t w[kLptMax];
+  lpt_order_body(wts, n_waves, n_pb, order, w);
+}
+
 template <bool NARROW>
 __global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__ pmax,
                                                     const uint32_t* __restrict__ pcnt, uint32_t C,
@@ -1327,7 +1383,16 @@ __global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__
                                                     uint64_t* __restrict__ maxima,
                                                     uint32_t* __restrict__ counts,
                                                     double* __restrict__ rcp,
-                                                    MemTab mt, uint32_t nw) {
+                                                    MemTab mt, uint32_t nw,
+                                                    uint32_t* __restrict__ lpt_w = nullptr,
+                                                    uint32_t* __restrict__ lpt_order = nullptr) {
+  if (lpt_w != nullptr && blockIdx.x == gridDim.x - 1) {  // the extra block: the K2's order
+    __shared__ __attribute__((aligned(16))) uint32_t w[kLptMax];
+    if (blockIdx.y == 0)
+      lpt_order_body(lpt_w, (n_pods + kWave - 1) / kWave, (n_pods + kBlock - 1) / kBlock,
+                     lpt_order, w);
+    return;
+  }
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t f = blockIdx.y;  // NARROW: the nw partial words, then the 2 counts
   const uint32_t NF = NARROW ? nw : 6u;
@@ -1657,6 +1722,13 @@ __global__ __launch_bounds__(kBlock) void k_gtable(const uint32_t* __restrict__ 
   }
 }
 
+hipError_t launch_lpt_order(uint32_t* wts, uint32_t n_pods, uint32_t* order, hipStream_t s) {
+  const uint32_t n_waves = (n_pods + kWave - 1) / kWave, n_pb = (n_pods + kBlock - 1) / kBlock;
+  if (n_pb == 0 || n_pb > kLptMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(1024), 0, s, wts, n_waves, n_pb, order);
+  return hipGetLastError();
+}
+
 // K2 block bounds (yoda_layout.h kbub_*): one wave per 64-node block, lane = node.
 template <int K>
 __global__ __launch_bounds__(kWave) void k_block_ub(const uint32_t* __restrict__ sum2,
@@ -1742,6 +1814,7 @@ struct ScoreArgs {
   const uint32_t* kbub = nullptr; // K2 block bounds (yoda_layout.h kbub_*): argmax pruning
   const uint64_t* hot = nullptr;  // blocks of the highest bounds (bit b % 64 of word b / 64):
                                   // visited first, so that the best so far rises early
+  const uint32_t* pb_order = nullptr;  // the block K2's pod-block visiting order (or none)
 };
 
 template <Path P>
@@ -2051,7 +2124,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   const uint32_t lane = lane_id();
   uint32_t* lds = lds_all[threadIdx.x >> 6];
   const Tile tl = tile();
-  const uint32_t p = tl.pb * kBlock + threadIdx.x;
+  // args.pb_order: the pod blocks heaviest first (k_lpt_order), so the long ones do not start last
+  const uint32_t pbk = args.pb_order ? args.pb_order[tl.pb] : tl.pb;
+  const uint32_t p = pbk * kBlock + threadIdx.x;
   const uint32_t chunk = tl.chunk;
   const uint32_t n0 = chunk * chunk_nodes;
   const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
@@ -4155,7 +4230,7 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                                       chunk_nodes, pp.m_32, pp.c_32, pp.number, pp.need_mem,   \
                                       pp.need_clk, n_pods, part.max_u, part.cnt, bm, bm_stride, \
                                       bs, bs_stride, blk, blk_stride, stats, nullptr, pp.bsum,   \
-                                      pp.nwords))
+                                      pp.nwords, pp.lpt_w))
         if (sub == 1u) {
           if (stats) YODA_K1B(KK, true)
           else if (pp.one_model) YODA_K1B(KK, false, false)
@@ -4229,9 +4304,18 @@ hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp,
 
 // rcp non-null: also the reciprocals (k_prep2 fused; the wave variant runs it after)
 // nw: the block K1's partial words (kNarrowWords / kWideWords), 0: u64 partials [6][C][P]
+// lpt_w / lpt_order non-null: also the block K2's heaviest-first pod-block order (k_lpt_order;
+// in k_reduce1's grid as one extra workgroup where that kernel runs)
+hipError_t launch_lpt_order(uint32_t* wts, uint32_t n_pods, uint32_t* order, hipStream_t s);
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uint32_t nw,
                           uint64_t* maxima, uint32_t* counts, double* rcp,
-                          const MemTab& mt, hipStream_t s) {
+                          const MemTab& mt, hipStream_t s, uint32_t* lpt_w,
+                          uint32_t* lpt_order) {
+  const bool lpt_apart = lpt_w != nullptr && (C > kWaveReduceChunks || !nw);
+  if (lpt_apart) {
+    const hipError_t e = launch_lpt_order(lpt_w, n_pods, lpt_order, s);
+    if (e != hipSuccess) return e;
+  }
   if (C > kWaveReduceChunks && n_pods >= 2 * kBlock) {
     // split the chunks so that ~64k threads read the partials, then atomics
     const uint32_t pb = (n_pods + kBlock - 1) / kBlock;
@@ -4258,10 +4342,12 @@ hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uin
                          part.cnt, C, n_pods, maxima, counts, mt, 0u);
     if (rcp) return launch_prep2(maxima, n_pods, rcp, s);
   } else {
-    const dim3 grid((n_pods + kBlock - 1) / kBlock, nw ? nw + 2u : 8u);
+    const bool lpt = lpt_w != nullptr && !lpt_apart;
+    const dim3 grid((n_pods + kBlock - 1) / kBlock + (lpt ? 1u : 0u), nw ? nw + 2u : 8u);
     if (nw)
       hipLaunchKernelGGL(k_reduce1<true>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
-                         n_pods, maxima, counts, rcp, mt, nw);
+                         n_pods, maxima, counts, rcp, mt, nw, lpt ? lpt_w : nullptr,
+                         lpt ? lpt_order : nullptr);
     else
       hipLaunchKernelGGL(k_reduce1<false>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
                          n_pods, maxima, counts, rcp, mt, 0u);
@@ -4297,7 +4383,7 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, counts, pp.g, pp.mix, pp.mt,
                     pp.ids, OUT == OUT_ARGMAX ? pp.kbub : nullptr,
-                    OUT == OUT_ARGMAX ? pp.hot : nullptr};
+                    OUT == OUT_ARGMAX ? pp.hot : nullptr, OUT == OUT_ARGMAX ? pp.lpt_order : nullptr};
   const MaskSrc ms{bm, bs, bm_stride, bs_stride, blk, blk_stride};
   if (bs && !blk) return hipErrorInvalidValue;  // sparse masks are read through their block list
   switch (path) {

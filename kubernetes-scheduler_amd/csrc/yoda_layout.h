@@ -345,6 +345,10 @@ struct PodParams {
   uint32_t nwords = 4;
   // the block K2's small-field quotients in f32 (every small field <= kF32SmallMax), else f64
   bool q32 = true;
+  // heaviest-first pod blocks: K1 adds per-wave weights into lpt_w, k_lpt_order sorts them into
+  // lpt_order, the argmax block K2 visits its pod blocks in that order (nullptr: none)
+  uint32_t* lpt_w = nullptr;
+  const uint32_t* lpt_order = nullptr;
 };
 
 // Per-pod state produced between kernels (length P each unless noted).
