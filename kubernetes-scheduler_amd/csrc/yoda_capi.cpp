@@ -2457,12 +2457,12 @@ static int prepare_run(yoda_t* h, int mode, bool pad = false) {
                       (uint64_t)h->n_pad * 8 <= (uint64_t)h->n_pods * 9;
   h->n_work = padded ? h->n_pad : h->n_pods;
   plan_chunks(h, mode, h->n_work, h->n_nodes);
-  // a private argmax run on the block kernels visits its pod blocks heaviest first (the
-  // weights: K1's PART nodes per pod block; YODA_LPT=0: launch order)
+  // a run on the block kernels (argmax, or the greedy windows' top-k) visits its pod blocks
+  // heaviest first (the weights: K1's PART nodes per pod block; YODA_LPT=0: launch order)
   static const bool lpt_env = YODA_KNOB("YODA_LPT", 1) != 0;
   const uint32_t n_pb = (h->n_work + kBlock - 1) / kBlock;
   h->lpt_sorted = false;
-  h->lpt_active = lpt_env && h->count_order && mode == YODA_MODE_SCV && h->path == Path::N32 &&
+  h->lpt_active = lpt_env && mode == YODA_MODE_SCV && h->path == Path::N32 &&
                   h->has_k1sum && h->has_k2sum && n_pb >= 8 && n_pb <= 4096;
   if (h->lpt_active) {
     const size_t had = h->lpt_w.bytes;

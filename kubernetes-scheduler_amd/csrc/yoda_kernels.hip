@@ -4482,7 +4482,7 @@ hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigne
   if (bs && !blk) return hipErrorInvalidValue;  // sparse masks are read through their block list
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, counts, pp.g, pp.mix, pp.mt,
-                    nullptr, pp.kbub};
+                    nullptr, pp.kbub, nullptr, pp.lpt_order};
 #define YODA_TOPKB(TKV, RKV, MIXV, Q32V)                                                        \
   YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false, TKV, RKV, MIXV, Q32V>), grid,      \
                                       dim3(kBlock), 0, s, nodes, sum2, n_nodes, chunk_nodes, a,   \
