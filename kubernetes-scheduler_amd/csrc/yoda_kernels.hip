@@ -1027,8 +1027,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
       blk_bits |= 1ull << (bi & 63u);
     }
   };
-  // ALL blocks' counts, lane = block (summed across the wave at the end)
-  uint32_t g_nf = 0, g_nz = 0;
+  // ALL blocks' counts, lane = block (summed across the wave at the end); g_nu: their nodes
+  // the K2 will likely score per pod (the K2 cost hint, wts)
+  uint32_t g_nf = 0, g_nz = 0, g_nu = 0;
   if (bsm != nullptr) {
     // Whole-block decisions from the block summaries (BlockSumWord), 64 blocks at a time,
     // lane = block: the bounds of a block's nodes against the wave's bounds prove every node
@@ -1073,6 +1074,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
       if (ball) {
         g_nf += nreal;
         g_nz += B[64 * kBsNzt];
+        if constexpr (!WIT) {
+          // K2 cost hint (wts): a block whose q-th healthy frees straddle the wave's memory
+          // range leaves the K2 counting qualifying cards per pod on its nodes
+          if (wts != nullptr && s_m_min != s_m_max) {
+            bool nu = false;
+#pragma unroll
+            for (int q = 0; q < K; ++q)
+              nu = nu || (B[64 * (kBsT + q)] <= s_m_max && B[64 * (kBsT + K + q)] > s_m_min);
+            g_nu += nu ? nreal : 0u;
+          }
+        }
         if (allq) {
           if constexpr (WIT) {  // (the same rule as a node's: larger replaces, equal adds)
 #pragma unroll
@@ -1140,9 +1152,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   nf_all += g_nf;
   nz_all += g_nz;
   blk_flush();
-  // the wave's weight for the K2's heaviest-first order (k_lpt_order): its PART nodes, summed
-  // over its chunks (one add per (wave, chunk); k_lpt_order reads and re-zeroes them)
-  if (wts != nullptr && lane == 0 && npart != 0u) atomicAdd(wts + (p >> 6), npart);
+  // the wave's weight for the K2's heaviest-first order (k_lpt_order): its PART nodes and the
+  // ALL nodes above, summed over its chunks (one add per (wave, chunk); k_lpt_order reads and
+  // re-zeroes them)
+  if (wts != nullptr) {
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) g_nu += (uint32_t)__shfl_xor((int)g_nu, o, kWave);
+    const uint32_t wgt = npart + g_nu;
+    if (lane == 0 && wgt != 0u) atomicAdd(wts + (p >> 6), wgt);
+  }
   if (trace && lane == 0) {
     unsigned long long* tr = stats + 16 + 4 * (((size_t)(p >> 6) * C + chunk) * SUB + sub);
     tr[0] = t_start;
