@@ -647,9 +647,12 @@ def main():
                    "node_bounds": [int(v) for v in b] if world > 1 and not pod_shard
                    else None},
         # dominant kernel K2: its algorithmic (unique) bytes per launch / its HIP-event launch
-        # time, against HBM peak; `traffic` = its measured HBM bytes per launch (PMC).  The
-        # kernels are bound by issue/latency, not bandwidth: the three fractions below say so.
-        "roofline": {"bound": "hbm", "kernel": names[1], "achieved": achieved,
+        # time, against HBM peak; `traffic` = its measured HBM bytes per launch (PMC).  What
+        # binds it is instruction issue / memory latency at its occupancy, not HBM bandwidth
+        # (DESIGN.md §4): `bound` says so, `frac` stays the HBM fraction, and `issue` carries
+        # the PMC issue utilisation and wait fractions beside it.
+        "roofline": {"bound": "issue/latency", "frac_of": "hbm", "kernel": names[1],
+                     "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": pmc.get("hbm_bytes_per_launch"),
                      "algo_bytes_per_launch": algo_bytes,

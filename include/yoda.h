@@ -55,6 +55,7 @@ extern "C" {
 #define YODA_ERR_RANGE -5         /* input outside what the library can represent       */
 #define YODA_ERR_NO_DEVICE -6     /* no HIP device / bad device ordinal                 */
 #define YODA_ERR_STATE -7         /* call out of sequence (e.g. phase2 before phase1)   */
+#define YODA_ERR_SAME_DEVICE -8   /* two ranks of one communicator on the same GPU      */
 
 /* ---- scoring modes ----------------------------------------------------------------- */
 /* Mode A: the SCV GPU path (filter.go + collection.go + algorithm.go:264-310 composed as
@@ -273,6 +274,15 @@ int yoda_shard_exact_merge(yoda_t* h, const void* d_all, int world);
 #define YODA_COMM_ID_BYTES 128
 int yoda_comm_unique_id(uint8_t* id);
 int yoda_comm_init(yoda_t* h, const uint8_t* id, int rank, int world);
+/* RCCL refuses two ranks on one GPU ("invalid usage").  Before yoda_comm_init every rank
+ * exchanges its device's PCI bus id (yoda_device_bus_id, YODA_BUS_ID_BYTES, NUL-terminated)
+ * along with the communicator id, and checks the gathered ids (rank-major, `stride` bytes
+ * apart): YODA_ERR_SAME_DEVICE when two ranks share one, with *rank_a < *rank_b the first such
+ * pair (either pointer may be NULL).  Host only: no HIP call. */
+#define YODA_BUS_ID_BYTES 32
+int yoda_device_bus_id(const yoda_t* h, char* out, int len);
+int yoda_comm_check_devices(const char* bus_ids, int world, int stride, int* rank_a,
+                            int* rank_b);
 int yoda_comm_run(yoda_t* h, int mode);
 int yoda_comm_run_local(yoda_t* const* handles, int world, int mode);
 /* The greedy batch (yoda_greedy's semantics) over the ranks' node shards, driven inside libyoda
@@ -392,10 +402,14 @@ int yoda_topk_k_capacity(void);
  * this handle's shard are ignored) and refresh their static score on the device. */
 int yoda_set_node_state(yoda_t* h, uint32_t count, const uint32_t* nodes, const uint64_t* alloc,
                         const uint64_t* card_number);
-/* After yoda_shard_phase1 and the caller's reduction of its buffers (d_maxima, d_counts as
- * there).  Host outputs: counts [2][P] (n_feasible, n_zero_total), top_score [k][P] (f64,
- * exact integers), top_node [k][P]. */
-int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_counts,
+/* After yoda_shard_phase1 (or _phase1_witness) and the caller's reduction of its buffers
+ * (d_maxima, d_counts as there).  k = the list depth of that phase 1, yoda_shard_topk_depth(h)
+ * (yoda_topk_k() after yoda_shard_phase1, yoda_topk_k_capacity() after the witness phase 1);
+ * any other k is rejected with YODA_ERR_INVALID_ARG, so the caller's buffers always match.
+ * Host outputs: counts [2][P] (n_feasible, n_zero_total), top_score [k][P] (f64, exact
+ * integers), top_node [k][P]. */
+int yoda_shard_topk_depth(const yoda_t* h);
+int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_counts, uint32_t k,
                     uint32_t* counts, double* top_score, uint32_t* top_node);
 /* Exact best node of pod `pod` (index in the batch of the last yoda_shard_topk) over this
  * shard against the CURRENT node state: *node = global id or -1 (no feasible node here),
@@ -408,7 +422,8 @@ int yoda_shard_best_one(yoda_t* h, uint32_t pod, double* score, int32_t* node);
  * maximum) and its lowest witness (GLOBAL id).  Exchange: keep a copy of the local d_maxima,
  * all-reduce d_maxima MAX and d_counts SUM, yoda_shard_witness_prepare(global, local, d_wit)
  * (clears the fields where this shard does not reach the global maximum), then SUM-reduce
- * d_wit[0, 6P) and MIN-reduce (unsigned) d_wit[6P, 12P).  yoda_shard_topk as usual; then
+ * d_wit[0, 6P) and MIN-reduce (unsigned) d_wit[6P, 12P).  yoda_shard_topk with
+ * k = yoda_topk_k_capacity() (the deeper lists of the capacity windows); then
  * yoda_shard_witness_download gives maxima [6][P] and wit [12][P] in the caller's pod order
  * for yoda_gs_set_witness.  A pod the session cannot certify starts the next window. */
 int yoda_shard_phase1_witness(yoda_t* h, uint64_t* d_maxima, uint32_t* d_counts,
@@ -446,12 +461,15 @@ int yoda_gs_set_witness(yoda_gs_t* g, const uint64_t* maxima, const uint32_t* wi
 int yoda_gs_resolve(yoda_gs_t* g, uint32_t* next);
 int yoda_gs_assign(yoda_gs_t* g, uint32_t queue_pos, int32_t pick);
 /* flags == 0: *count = window pods [from, from + scan) with >= 2 feasible nodes whose lists no
- * longer certify them (they stay so: scores only drop) -- the refresh trigger. */
+ * longer certify them (they stay so: scores only drop) -- the refresh trigger; 0 once some
+ * node's Allocate has wrapped (no list certifies then, so a refresh cannot help).
+ * YODA_ERR_STATE for capacity sessions. */
 int yoda_gs_uncertified(const yoda_gs_t* g, uint32_t from, uint32_t scan, uint32_t* count);
 /* New candidate lists for window pods [from, wn) ([k][wn] in window order, as
  * yoda_gs_begin_window's, scored against the CURRENT node state with the window's phase-1
- * masks and maxima): each list's threshold becomes its refresh-time k-th score.  Capacity
- * sessions keep judging feasibility and maxima against the window start. */
+ * masks and maxima): each list's threshold becomes its refresh-time k-th score.  Every listed
+ * node is validated first (YODA_ERR_RANGE leaves the session unchanged); capacity sessions
+ * restart windows instead and get YODA_ERR_STATE. */
 int yoda_gs_refresh(yoda_gs_t* g, uint32_t from, const double* top_score,
                     const uint32_t* top_node);
 /* YODA_GREEDY_CARD_CAPACITY: the size of the window that a restart at window index `progress`

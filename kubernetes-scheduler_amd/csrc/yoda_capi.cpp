@@ -2802,7 +2802,8 @@ int yoda_class_stats_enable(yoda_t* h, int enable) {
     HIP_TRY(h, h->stats_dev.ensure(bytes));
     HIP_TRY(h, hipMemsetAsync(h->stats_dev.p, 0, bytes, h->stream));
     if (tr) {  // YODA_K1_TRACE set: the K1 records it instead of the K2
-      const uint64_t one = diag_env("YODA_K1_TRACE", 0) ? 2 : 1;
+      // low byte: which kernel traces; above it the slot count (the kernels bound the index)
+      const uint64_t one = (diag_env("YODA_K1_TRACE", 0) ? 2 : 1) | ((uint64_t)tr << 8);
       HIP_TRY(h, hipMemcpyAsync(h->stats_dev.as<uint64_t>() + 15, &one, 8,
                                 hipMemcpyHostToDevice, h->stream));
       HIP_TRY(h, hipStreamSynchronize(h->stream));
@@ -3513,7 +3514,13 @@ int yoda_set_node_state(yoda_t* h, uint32_t count, const uint32_t* nodes, const 
   }
 }
 
-int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_counts,
+int yoda_shard_topk_depth(const yoda_t* h) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  // the capacity windows' deeper lists after the witness phase 1 (yoda_greedy's depths)
+  return h->phase1_wit ? topk_k_capacity() : topk_k();
+}
+
+int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_counts, uint32_t k,
                     uint32_t* counts, double* top_score, uint32_t* top_node) {
   int rc = check_ready(h, YODA_MODE_SCV);
   if (rc) return rc;
@@ -3522,10 +3529,13 @@ int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_count
     return fail(h, YODA_ERR_STATE, "top-k lists need a fast record path (N32 or F64)");
   if (!d_maxima || !d_counts || !counts || !top_score || !top_node)
     return fail(h, YODA_ERR_INVALID_ARG, "NULL buffer");
+  const uint32_t KT = (uint32_t)yoda_shard_topk_depth(h);
+  if (k != KT)
+    return fail(h, YODA_ERR_INVALID_ARG,
+                "yoda_shard_topk: k = " + std::to_string(k) + " but this phase 1 lists " +
+                    std::to_string(KT) + " candidates per pod (yoda_shard_topk_depth)");
   try {
-    // the capacity windows' deeper lists after the witness phase 1 (yoda_greedy's depths)
-    const uint32_t P = h->n_pods, N = h->n_nodes,
-                   KT = (uint32_t)(h->phase1_wit ? topk_k_capacity() : topk_k());
+    const uint32_t P = h->n_pods, N = h->n_nodes;
     h->h_pos.resize(P);
     for (uint32_t i = 0; i < P; ++i) h->h_pos[i] = i;
     h->topk_ready = false;
@@ -4140,6 +4150,12 @@ int yoda_gs_uncertified(const yoda_gs_t* g, uint32_t from, uint32_t scan, uint32
   if (!g || !count || !g->in_window) return YODA_ERR_INVALID_ARG;
   if (g->flags & YODA_GREEDY_CARD_CAPACITY) return YODA_ERR_STATE;
   uint32_t c = 0, bi;
+  // once Allocate has wrapped (alloc < before) no list certifies any more: a refresh cannot
+  // help, so report none (the one rule of yoda_greedy, yoda_comm_greedy and dist.sharded_greedy)
+  if (g->wrapped) {
+    *count = 0;
+    return YODA_OK;
+  }
   const uint32_t end = (uint32_t)std::min<uint64_t>(g->wn, (uint64_t)from + scan);
   for (uint32_t i = from; i < end; ++i)
     if (g->counts[i] >= 2 && g->counts[(size_t)g->wn + i] == 0 && !g->certify0(i, &bi)) ++c;
@@ -4150,13 +4166,21 @@ int yoda_gs_uncertified(const yoda_gs_t* g, uint32_t from, uint32_t scan, uint32
 int yoda_gs_refresh(yoda_gs_t* g, uint32_t from, const double* top_score,
                     const uint32_t* top_node) {
   if (!g || !g->in_window || !top_score || !top_node || from > g->wn) return YODA_ERR_INVALID_ARG;
+  // capacity sessions judge feasibility and maxima against the window start and restart
+  // instead of refreshing (as yoda_gs_uncertified)
+  if (g->flags & YODA_GREEDY_CARD_CAPACITY) return YODA_ERR_STATE;
   const uint32_t wn = g->wn, k = g->k;
+  // validate every listed node first: a bad id leaves the session unchanged
+  for (uint32_t i = from; i < wn; ++i) {
+    const uint32_t len = std::min<uint32_t>(g->counts[i], k);
+    for (uint32_t kk = 0; kk < len; ++kk)
+      if (top_node[(size_t)kk * wn + i] >= g->N) return YODA_ERR_RANGE;
+  }
   for (uint32_t i = from; i < wn; ++i) {
     const uint32_t len = std::min<uint32_t>(g->counts[i], k);
     for (uint32_t kk = 0; kk < len; ++kk) {
       const size_t o = (size_t)kk * wn + i;
       const uint32_t n = top_node[o];
-      if (n >= g->N) return YODA_ERR_RANGE;
       // stored so that the certificate's  stored - old static + current static  is its
       // current score (the refresh scored it with the current static)
       g->ti[o] = n;
@@ -4549,10 +4573,39 @@ static uint32_t bit_length(uint64_t v) {
   return b;
 }
 
+// The words every shard contributes to exchange 1 (MAX-reduced with the maxima):
+//   [0] score bits and [1] node-id bits this shard needs (the phase-2 form: packed key or
+//       records);
+//   [2] the shard's largest small card field (bandwidth / clock / core / power) and [3] 1 when
+//       the shard's block K2 computes its small-field quotients in f32 (N32 path, every small
+//       field <= kF32SmallMax).  The exchanged maxima are the GLOBAL ones, so an
+//       f32 shard is exact only while the global small-field max is <= kF32SmallMax too;
+//       otherwise the shards must re-upload with YODA_UPLOAD_F64_QUOTIENTS (dist.agree_on_path
+//       does) -- quotient_disagreement names that instead of returning inexact scores.
+constexpr int kAgreeWords = 4;
+constexpr size_t kAgreeBytes = 8 * kAgreeWords;
+
+static void agreement_words(const yoda_t* h, int mode, uint64_t* w) {
+  w[0] = h->generic && mode == YODA_MODE_SCV ? 64u : bit_length(h->score_bound);
+  w[1] = bit_length((uint64_t)h->node_offset + h->n_nodes + 1);
+  const bool f32q = mode == YODA_MODE_SCV && h->path == Path::N32 && h->q32;
+  w[2] = mode == YODA_MODE_SCV ? h->small_max : 0;
+  w[3] = f32q ? 1 : 0;
+}
+
+static const char* quotient_disagreement(uint64_t global_small_max, uint64_t any_f32) {
+  if (any_f32 && global_small_max > kF32SmallMax)
+    return "shards disagree on the quotient type: a shard computes f32 small-field quotients "
+           "but another shard holds a small card field beyond 55738, so the reduced maxima "
+           "break the f32 lemma; upload every shard with YODA_UPLOAD_F64_QUOTIENTS (see "
+           "yoda_small_field_max)";
+  return nullptr;
+}
+
 static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local) {
   yoda_t* h0 = hs[0];
   const uint32_t P = h0->n_pods;
-  const size_t n1 = 6 * (size_t)P + 2;  // maxima | agreement words
+  const size_t n1 = 6 * (size_t)P + kAgreeWords;  // maxima | agreement words
   for (int i = 0; i < n; ++i) {
     yoda_t* h = hs[i];
     if (h->n_pods != P) return fail(h0, YODA_ERR_INVALID_ARG, "shards hold different batches");
@@ -4565,15 +4618,16 @@ static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local) 
     if (P == 0) continue;
     uint64_t* ex = h->ex1.as<uint64_t>();
     if ((rc = phase1(h, mode, ex, h->counts.as<uint32_t>()))) return rc;
-    // agreement words: the score bits and node-id bits this shard needs (pinned staging,
-    // one slot per shard; the previous step's copies finished before its read-back below)
-    const uint64_t agree[2] = {h->generic && mode == YODA_MODE_SCV ? 64u
-                                                                    : bit_length(h->score_bound),
-                               bit_length((uint64_t)h->node_offset + h->n_nodes + 1)};
-    HIP_TRY(h0, h0->win_stage.ensure(16 * ((size_t)n + 1)));
-    unsigned char* slot = static_cast<unsigned char*>(h0->win_stage.p) + 16 * ((size_t)i + 1);
-    std::memcpy(slot, agree, 16);
-    HIP_TRY(h, hipMemcpyAsync(ex + 6 * (size_t)P, slot, 16, hipMemcpyHostToDevice, h->stream));
+    // agreement words (pinned staging, one slot per shard; the previous step's copies
+    // finished before its read-back below)
+    uint64_t agree[kAgreeWords];
+    agreement_words(h, mode, agree);
+    HIP_TRY(h0, h0->win_stage.ensure(kAgreeBytes * ((size_t)n + 1)));
+    unsigned char* slot =
+        static_cast<unsigned char*>(h0->win_stage.p) + kAgreeBytes * ((size_t)i + 1);
+    std::memcpy(slot, agree, kAgreeBytes);
+    HIP_TRY(h, hipMemcpyAsync(ex + 6 * (size_t)P, slot, kAgreeBytes, hipMemcpyHostToDevice,
+                              h->stream));
   }
   if (P == 0) {
     for (int i = 0; i < n; ++i) hs[i]->ran = true;
@@ -4609,11 +4663,14 @@ static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local) 
       return fail(h0, YODA_ERR_HIP, std::string("ncclAllReduce: ") + rccl().error_string(r));
   }
   // the agreed phase-2 form (every shard reads the same reduced words; one host wait per step)
-  uint64_t agreed[2] = {64, 64};
-  HIP_TRY(h0, hipMemcpyAsync(h0->win_stage.p, h0->ex1.as<uint64_t>() + 6 * (size_t)P, 16,
-                             hipMemcpyDeviceToHost, h0->stream));
+  uint64_t agreed[kAgreeWords] = {64, 64, 0, 0};
+  HIP_TRY(h0, hipMemcpyAsync(h0->win_stage.p, h0->ex1.as<uint64_t>() + 6 * (size_t)P,
+                             kAgreeBytes, hipMemcpyDeviceToHost, h0->stream));
   HIP_TRY(h0, hipStreamSynchronize(h0->stream));
-  std::memcpy(agreed, h0->win_stage.p, 16);
+  std::memcpy(agreed, h0->win_stage.p, kAgreeBytes);
+  // every rank reads the same reduced words, so every rank fails here together
+  if (const char* why = quotient_disagreement(agreed[2], agreed[3]))
+    return fail(h0, YODA_ERR_STATE, why);
   const uint32_t ib = (uint32_t)std::max<uint64_t>(1, agreed[1]);
   const bool packed = agreed[0] + ib <= 63 && ib <= 40;
   for (int i = 0; i < n; ++i) {
@@ -4727,15 +4784,31 @@ struct Coll {
   yoda_t* const* hs;
   int n, world;
   bool local;
-  uint32_t* calls = nullptr;  // collective calls made (yoda_comm_greedy_stats)
+  uint32_t* calls = nullptr;  // collective launches made (yoda_comm_greedy_stats): a group of
+                              // collectives (begin() .. end()) counts once
+  bool in_group = false;
   int nccl(ncclResult_t r, const char* what) const {
     if (r == ncclSuccess) return YODA_OK;
     return fail(hs[0], YODA_ERR_HIP, std::string(what) + ": " + rccl().error_string(r));
   }
+  void count() const {
+    if (calls && !in_group) ++*calls;
+  }
+  // ncclGroupStart / End: the collectives issued in between run as ONE launch (RCCL fuses
+  // them); the local transport runs each at once
+  void begin() {
+    if (!local) rccl().group_start();
+    in_group = true;
+  }
+  int end() {
+    in_group = false;
+    count();
+    return local ? YODA_OK : nccl(rccl().group_end(), "ncclGroupEnd");
+  }
   // in-place elementwise all-reduce of `count` u64 or u32 device words (MAX / SUM / MIN)
   int allreduce(const std::vector<void*>& bufs, size_t count, bool u64, ncclRedOp_t op) const {
     if (count == 0) return YODA_OK;
-    if (calls) ++*calls;
+    this->count();
     if (!local)
       return nccl(rccl().all_reduce(bufs[0], bufs[0], count, u64 ? ncclUint64 : ncclUint32, op,
                                     hs[0]->comm, hs[0]->stream),
@@ -4767,11 +4840,17 @@ struct Coll {
     return YODA_OK;
   }
   // all-gather of host blocks: out = the world's `bytes`-byte blocks in rank order (RCCL:
-  // staged through the first handle's device scratch)
+  // staged through the first handle's device scratch).  In a group: allgather_issue before
+  // end(), allgather_finish after it (the copies back must follow the collective's launch).
   int allgather(const std::vector<const void*>& in, size_t bytes,
                 std::vector<unsigned char>& out) const {
+    int rc = allgather_issue(in, bytes, out);
+    return rc ? rc : allgather_finish(bytes, out);
+  }
+  int allgather_issue(const std::vector<const void*>& in, size_t bytes,
+                      std::vector<unsigned char>& out) const {
     out.resize((size_t)world * bytes);
-    if (calls) ++*calls;
+    count();
     if (local) {
       for (int i = 0; i < n; ++i) std::memcpy(out.data() + (size_t)i * bytes, in[i], bytes);
       return YODA_OK;
@@ -4781,9 +4860,14 @@ struct Coll {
     HIP_TRY(h, h->cg_gather.ensure(b8 * ((size_t)world + 1)));
     unsigned char* d = h->cg_gather.as<unsigned char>();
     HIP_TRY(h, hipMemcpyAsync(d, in[0], bytes, hipMemcpyHostToDevice, h->stream));
-    int rc = nccl(rccl().all_gather(d, d + b8, b8 / 8, ncclUint64, h->comm, h->stream),
-                  "ncclAllGather");
-    if (rc) return rc;
+    return nccl(rccl().all_gather(d, d + b8, b8 / 8, ncclUint64, h->comm, h->stream),
+                "ncclAllGather");
+  }
+  int allgather_finish(size_t bytes, std::vector<unsigned char>& out) const {
+    if (local) return YODA_OK;
+    yoda_t* h = hs[0];
+    const size_t b8 = (bytes + 7) / 8 * 8;
+    unsigned char* d = h->cg_gather.as<unsigned char>();
     for (int r = 0; r < world; ++r)
       HIP_TRY(h, hipMemcpyAsync(out.data() + (size_t)r * bytes, d + b8 * ((size_t)r + 1), bytes,
                                 hipMemcpyDeviceToHost, h->stream));
@@ -4838,6 +4922,23 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
   for (int i = 0; i < n; ++i)
     if (hs[i]->generic != generic)
       return fail(h0, YODA_ERR_STATE, "shards on different record paths");
+  if (!generic) {  // the quotient type too (comm_step's agreement words [2], [3]), once per batch
+    std::vector<void*> bq;
+    std::vector<uint64_t> w((size_t)kAgreeWords * n);  // alive until the stream syncs below
+    for (int i = 0; i < n; ++i) {
+      uint64_t* wi = w.data() + (size_t)kAgreeWords * i;
+      agreement_words(hs[i], YODA_MODE_SCV, wi);
+      HIP_TRY(hs[i], hs[i]->cg_max.ensure(2 * 8));
+      HIP_TRY(hs[i], hipMemcpyAsync(hs[i]->cg_max.p, wi + 2, 16, hipMemcpyHostToDevice,
+                                    hs[i]->stream));
+      bq.push_back(hs[i]->cg_max.p);
+    }
+    if ((rc = co.allreduce(bq, 2, true, ncclMax))) return rc;
+    uint64_t q[2] = {0, 0};
+    HIP_TRY(h0, hipMemcpyAsync(q, h0->cg_max.p, 16, hipMemcpyDeviceToHost, h0->stream));
+    HIP_TRY(h0, hipStreamSynchronize(h0->stream));
+    if (const char* why = quotient_disagreement(q[0], q[1])) return fail(h0, YODA_ERR_STATE, why);
+  }
   std::vector<uint32_t> ids;
   std::vector<uint64_t> al, cn;
   auto push = [&](bool original) -> int {  // the session's node changes -> every shard
@@ -4903,14 +5004,12 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
         bwc.push_back(h->cg_wit.p);
         bwn.push_back(h->cg_wit.as<uint32_t>() + 6ull * wn);
       }
-      if (!local) rccl().group_start();
+      // window exchange 1 (one group): maxima MAX, counts SUM
+      co.begin();
       rc = co.allreduce(bmax, 6ull * wn, true, ncclMax);
       const int rc2 = co.allreduce(bcnt, 2ull * wn, false, ncclSum);
-      if (!local) {
-        const int rc3 = co.nccl(rccl().group_end(), "ncclGroupEnd");
-        if (!rc) rc = rc3;
-      }
-      if (rc || (rc = rc2)) return rc;
+      const int rc3 = co.end();
+      if (rc || (rc = rc2) || (rc = rc3)) return rc;
       if (capacity) {
         for (int i = 0; i < n; ++i) {
           uint64_t* dmax = hs[i]->cg_max.as<uint64_t>();
@@ -4918,27 +5017,31 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
                                                hs[i]->cg_wit.as<uint32_t>())))
             return rc;
         }
-        if ((rc = co.allreduce(bwc, 6ull * wn, false, ncclSum))) return rc;
-        if ((rc = co.allreduce(bwn, 6ull * wn, false, ncclMin))) return rc;
       }
       // the shards' candidate lists, all-gathered and merged: the first K of the union in
-      // (score desc, node asc) order contain the global top K (window pods [from, wn) only)
+      // (score desc, node asc) order contain the global top K (window pods [from, wn) only).
+      // Window exchange 2 (one group): the lists' all-gather and, in capacity mode, the
+      // witness counts SUM and lowest witnesses MIN (they need only exchange 1's maxima)
       counts.resize(2ull * wn);
-      auto merged_lists = [&](uint32_t from) -> int {
+      auto merged_lists = [&](uint32_t from, bool with_witness) -> int {
         const size_t lb = (size_t)K * wn * 12;  // per shard: K x wn scores (f64) + nodes (u32)
         mine.resize((size_t)n * lb);
         for (int i = 0; i < n; ++i) {
           unsigned char* m = mine.data() + (size_t)i * lb;
           int r = yoda_shard_topk(hs[i], hs[i]->cg_max.as<uint64_t>(),
-                                  hs[i]->cg_cnt.as<uint32_t>(), counts.data(),
+                                  hs[i]->cg_cnt.as<uint32_t>(), K, counts.data(),
                                   reinterpret_cast<double*>(m),
                                   reinterpret_cast<uint32_t*>(m + (size_t)K * wn * 8));
           if (r) return r;
         }
         std::vector<const void*> ins;
         for (int i = 0; i < n; ++i) ins.push_back(mine.data() + (size_t)i * lb);
-        int r = co.allgather(ins, lb, gathered);
-        if (r) return r;
+        co.begin();
+        int r = with_witness ? co.allreduce(bwc, 6ull * wn, false, ncclSum) : YODA_OK;
+        if (!r && with_witness) r = co.allreduce(bwn, 6ull * wn, false, ncclMin);
+        if (!r) r = co.allgather_issue(ins, lb, gathered);
+        const int re = co.end();
+        if (r || (r = re) || (r = co.allgather_finish(lb, gathered))) return r;
         ts.assign((size_t)K * wn, -1.0);
         ti.assign((size_t)K * wn, 0xffffffffu);
         for (uint32_t p = from; p < wn; ++p) {
@@ -4962,7 +5065,7 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
         }
         return YODA_OK;
       };
-      if ((rc = merged_lists(0))) return rc;
+      if ((rc = merged_lists(0, capacity))) return rc;
       if ((rc = yoda_gs_begin_window(g, ws, wn, K, counts.data(), ts.data(), ti.data())))
         return fail(h0, rc, "greedy: begin window");
       ++h0->greedy_windows;
@@ -5004,7 +5107,7 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
           if ((rc = yoda_gs_uncertified(g, nxt + 1, kScan, &unc))) return fail(h0, rc, "greedy");
           if (unc >= kScanMin) {
             if ((rc = push(false))) return rc;
-            if ((rc = merged_lists(nxt))) return rc;
+            if ((rc = merged_lists(nxt, false))) return rc;
             if ((rc = yoda_gs_refresh(g, nxt, ts.data(), ti.data())))
               return fail(h0, rc, "greedy: refresh");
             ++h0->greedy_refreshes;
@@ -5074,6 +5177,33 @@ int yoda_comm_unique_id(uint8_t* id) {
   return YODA_OK;
 }
 
+int yoda_device_bus_id(const yoda_t* h, char* out, int len) {
+  if (!h || !out || len < 2) return YODA_ERR_INVALID_ARG;
+  std::memset(out, 0, (size_t)len);
+  if (hipDeviceGetPCIBusId(out, len - 1, h->device) != hipSuccess) return YODA_ERR_HIP;
+  return YODA_OK;
+}
+
+int yoda_comm_check_devices(const char* bus_ids, int world, int stride, int* rank_a,
+                            int* rank_b) {
+  if (!bus_ids || world < 1 || stride < 1) return YODA_ERR_INVALID_ARG;
+  const auto id = [&](int r) {
+    const char* p = bus_ids + (size_t)r * stride;
+    return std::string(p, strnlen(p, (size_t)stride));
+  };
+  for (int a = 0; a < world; ++a) {
+    const std::string ia = id(a);
+    if (ia.empty()) return YODA_ERR_INVALID_ARG;
+    for (int b = a + 1; b < world; ++b)
+      if (ia == id(b)) {
+        if (rank_a) *rank_a = a;
+        if (rank_b) *rank_b = b;
+        return YODA_ERR_SAME_DEVICE;
+      }
+  }
+  return YODA_OK;
+}
+
 int yoda_comm_init(yoda_t* h, const uint8_t* id, int rank, int world) {
   if (!h) return YODA_ERR_INVALID_ARG;
   if (!id || world < 1 || rank < 0 || rank >= world)
@@ -5089,7 +5219,11 @@ int yoda_comm_init(yoda_t* h, const uint8_t* id, int rank, int world) {
   const ncclResult_t r = rccl().comm_init_rank(&h->comm, world, u, rank);
   if (r != ncclSuccess) {
     h->comm = nullptr;
-    return fail(h, YODA_ERR_HIP, std::string("ncclCommInitRank: ") + rccl().error_string(r));
+    std::string msg = std::string("ncclCommInitRank: ") + rccl().error_string(r);
+    if (r == ncclInvalidUsage)  // the usual cause: two ranks on one GPU
+      msg += " (RCCL refuses two ranks of one communicator on the same GPU: check the "
+             "ranks' devices with yoda_device_bus_id / yoda_comm_check_devices)";
+    return fail(h, YODA_ERR_HIP, msg);
   }
   h->comm_rank = rank;
   h->comm_world = world;

@@ -640,7 +640,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
   BlockMask* bsw = bs + (size_t)uniform_u32(p >> 6) * bs_stride;
   // STATS with stats[15] == 2: per-(wave, chunk) timing trace only (no counter atomics)
-  const bool trace = STATS && stats[15] == 2ull;
+  // (stats[15] >> 8 = the trace slots allocated: every slot index is bounded by it)
+  const bool trace = STATS && (stats[15] & 0xffull) == 2ull;
   const uint64_t t_start = STATS ? wall_clock64() : 0ull;
   uint32_t npart = 0;
 
@@ -1161,8 +1162,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     const uint32_t wgt = npart + g_nu;
     if (lane == 0 && wgt != 0u) atomicAdd(wts + (p >> 6), wgt);
   }
-  if (trace && lane == 0) {
-    unsigned long long* tr = stats + 16 + 4 * (((size_t)(p >> 6) * C + chunk) * SUB + sub);
+  const size_t slot1 = ((size_t)(p >> 6) * C + chunk) * SUB + sub;
+  if (trace && lane == 0 && slot1 < (size_t)(stats[15] >> 8)) {
+    unsigned long long* tr = stats + 16 + 4 * slot1;
     tr[0] = t_start;
     tr[1] = wall_clock64();
     tr[2] = npart;
@@ -2152,7 +2154,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   const uint64_t live_mask = ballot(live);
   if (live_mask == 0) return;  // a wave past the batch
   // STATS with stats[15] set: the timing trace only (no per-block counter atomics)
-  const bool trace = STATS && stats[15] == 1ull;
+  const bool trace = STATS && (stats[15] & 0xffull) == 1ull;
   const uint64_t t_start = STATS ? wall_clock64() : 0ull;
   const uint64_t* bmw = bm + (size_t)uniform_u32(p >> 6) * bm_stride;
   const BlockMask* bsw = bs ? bs + (size_t)uniform_u32(p >> 6) * bs_stride : nullptr;
@@ -2732,9 +2734,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     atomicAdd(stats + 6, 1ull);
     atomicMax(stats + 9, (unsigned long long)npart);
   }
-  if (trace && lane == 0) {
+  const size_t slot2 = (size_t)(p >> 6) * gridDim.y + chunk;
+  if (trace && lane == 0 && slot2 < (size_t)(stats[15] >> 8)) {
     {  // per-(wave, chunk) trace: start, end (100 MHz clock), per-pod nodes
-      unsigned long long* tr = stats + 16 + 4 * ((size_t)(p >> 6) * gridDim.y + chunk);
+      unsigned long long* tr = stats + 16 + 4 * slot2;
       tr[0] = t_start;
       tr[1] = wall_clock64();
       tr[2] = npart;

@@ -22,6 +22,7 @@ HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "
 ERRORS = {
     -1: "YODA_ERR_INVALID_ARG", -2: "YODA_ERR_HIP", -3: "YODA_ERR_NO_NODES",
     -4: "YODA_ERR_NO_PODS", -5: "YODA_ERR_RANGE", -6: "YODA_ERR_NO_DEVICE", -7: "YODA_ERR_STATE",
+    -8: "YODA_ERR_SAME_DEVICE",
 }
 
 _lib = None
@@ -75,7 +76,8 @@ _SIGS = {
     "yoda_topk_k": ([], C.c_int),
     "yoda_topk_k_capacity": ([], C.c_int),
     "yoda_set_node_state": ([_vp, _u32, _vp, _vp, _vp], C.c_int),
-    "yoda_shard_topk": ([_vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "yoda_shard_topk": ([_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp], C.c_int),
+    "yoda_shard_topk_depth": ([_vp], C.c_int),
     "yoda_shard_best_one": ([_vp, _u32, C.POINTER(C.c_double), C.POINTER(C.c_int32)], C.c_int),
     "yoda_shard_phase1_witness": ([_vp, _vp, _vp, _vp], C.c_int),
     "yoda_shard_witness_prepare": ([_vp, _vp, _vp, _vp], C.c_int),
@@ -87,6 +89,8 @@ _SIGS = {
     "yoda_greedy_refreshes": ([_vp, C.POINTER(C.c_uint32)], C.c_int),
     "yoda_comm_unique_id": ([_vp], C.c_int),
     "yoda_comm_init": ([_vp, _vp, C.c_int, C.c_int], C.c_int),
+    "yoda_device_bus_id": ([_vp, C.c_char_p, C.c_int], C.c_int),
+    "yoda_comm_check_devices": ([C.c_char_p, C.c_int, C.c_int, _vp, _vp], C.c_int),
     "yoda_comm_run": ([_vp, C.c_int], C.c_int),
     "yoda_comm_run_local": ([_vp, C.c_int, C.c_int], C.c_int),
     "yoda_gs_create": ([C.POINTER(CNodeSoA), C.POINTER(CPodSoA), _u32, C.POINTER(_vp)], C.c_int),
@@ -395,6 +399,12 @@ class Yoda:
         buf = (C.c_uint8 * 128).from_buffer_copy(comm_id)
         self._check(lib().yoda_comm_init(self._h, buf, rank, world), "yoda_comm_init")
 
+    def bus_id(self) -> str:
+        """PCI bus id of the handle's device (yoda_device_bus_id)."""
+        buf = C.create_string_buffer(BUS_ID_BYTES)
+        self._check(lib().yoda_device_bus_id(self._h, buf, BUS_ID_BYTES), "yoda_device_bus_id")
+        return buf.value.decode()
+
     def comm_run(self, mode: int = 0):
         """One sharded step with libyoda's own RCCL exchanges (yoda_comm_run)."""
         self._check(lib().yoda_comm_run(self._h, mode), "yoda_comm_run")
@@ -421,15 +431,25 @@ class Yoda:
         self._check(lib().yoda_set_node_state(self._h, n.size, _np_ptr(n), _np_ptr(a),
                                               _np_ptr(c)), "yoda_set_node_state")
 
+    def shard_topk_depth(self) -> int:
+        """Candidates per pod the next shard_topk lists (yoda_shard_topk_depth): topk_k() after
+        shard_phase1, topk_k_capacity() after shard_phase1_witness."""
+        k = int(lib().yoda_shard_topk_depth(self._h))
+        if k < 0:
+            self._check(k, "yoda_shard_topk_depth")
+        return k
+
     def shard_topk(self, d_maxima: int, d_counts: int, k: int | None = None):
-        """(counts [2, P], top_score [k, P], top_node [k, P]) of the uploaded batch; k =
-        topk_k() after shard_phase1, topk_k_capacity() after shard_phase1_witness."""
-        P, k = self.n_pods, (topk_k() if k is None else k)
+        """(counts [2, P], top_score [k, P], top_node [k, P]) of the uploaded batch; k defaults
+        to the handle's depth (shard_topk_depth); libyoda rejects any other k."""
+        P = self.n_pods
+        k = self.shard_topk_depth() if k is None else k
         counts = np.zeros((2, max(P, 1)), np.uint32)
         ts = np.zeros((k, max(P, 1)), np.float64)
         ti = np.zeros((k, max(P, 1)), np.uint32)
-        self._check(lib().yoda_shard_topk(self._h, _vp(d_maxima), _vp(d_counts), _np_ptr(counts),
-                                          _np_ptr(ts), _np_ptr(ti)), "yoda_shard_topk")
+        self._check(lib().yoda_shard_topk(self._h, _vp(d_maxima), _vp(d_counts), k,
+                                          _np_ptr(counts), _np_ptr(ts), _np_ptr(ti)),
+                    "yoda_shard_topk")
         return counts[:, :P], ts[:, :P], ti[:, :P]
 
     def shard_phase1_witness(self, d_maxima: int, d_counts: int, d_wit: int):
@@ -494,6 +514,24 @@ class Yoda:
         self._check(lib().yoda_shard_finalize(self._h, mode, _vp(d_counts), _vp(d_best),
                                               _vp(d_idx), _vp(d_ties), _vp(d_lowest)),
                     "yoda_shard_finalize")
+
+
+BUS_ID_BYTES = 32  # YODA_BUS_ID_BYTES
+
+
+def comm_check_devices(bus_ids) -> None:
+    """Raise YodaError (YODA_ERR_SAME_DEVICE) naming the first two ranks whose devices share a
+    PCI bus id (yoda_comm_check_devices; host only).  bus_ids: one str per rank."""
+    world = len(bus_ids)
+    raw = b"".join(b.encode()[:BUS_ID_BYTES - 1].ljust(BUS_ID_BYTES, b"\0") for b in bus_ids)
+    a, b = C.c_int(-1), C.c_int(-1)
+    rc = lib().yoda_comm_check_devices(raw, world, BUS_ID_BYTES, C.byref(a), C.byref(b))
+    if rc == -8:
+        raise YodaError(f"yoda_comm_check_devices: YODA_ERR_SAME_DEVICE: ranks {a.value} and "
+                        f"{b.value} are on the same GPU ({bus_ids[a.value]}); RCCL needs one "
+                        "GPU per rank")
+    if rc != 0:
+        raise YodaError(f"yoda_comm_check_devices: {ERRORS.get(rc, rc)}")
 
 
 def comm_unique_id() -> bytes:

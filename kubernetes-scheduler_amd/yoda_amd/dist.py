@@ -347,6 +347,8 @@ class LibExchange:
             agree_on_path(Reducer(group=group), [handle], [shard], [offset], device)
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         on_dev = dist.get_backend(group) == "nccl"
+        # one GPU per rank, or RCCL's init fails with a bare "invalid usage"
+        agree_on_devices(handle.bus_id(), device if on_dev else torch.device("cpu"), group)
         t = torch.zeros(128, dtype=torch.uint8, device=device if on_dev else "cpu")
         if rank == 0:
             t.copy_(torch.tensor(list(comm_unique_id()), dtype=torch.uint8))
@@ -358,6 +360,22 @@ class LibExchange:
 
     def step(self, mode: int):
         self.handle.comm_run(mode)
+
+
+def agree_on_devices(bus_id: str, device, group=None) -> list:
+    """All-gather every rank's PCI bus id and raise YodaError (YODA_ERR_SAME_DEVICE, naming the
+    ranks) when two ranks share a GPU -- before yoda_comm_init, whose RCCL init would fail on
+    it with "invalid usage".  Returns the ids in rank order."""
+    import torch.distributed as dist
+    from .capi import BUS_ID_BYTES, comm_check_devices
+    world = dist.get_world_size(group)
+    raw = bus_id.encode()[:BUS_ID_BYTES - 1].ljust(BUS_ID_BYTES, b"\0")
+    mine = torch.tensor(list(raw), dtype=torch.uint8, device=device)
+    every = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(every, mine, group=group)
+    ids = [bytes(t.cpu().numpy().tobytes()).rstrip(b"\0").decode() for t in every]
+    comm_check_devices(ids)
+    return ids
 
 
 def shard_bounds(n_nodes: int, world: int) -> np.ndarray:

@@ -45,27 +45,44 @@ def check_inputs(fx: dict, nodes, pods):
         f"({fx['inputs']}): numpy drift, not a kernel mismatch")
 
 
-def config3_mismatch(fx: dict, got, nodes, pods, oracle, threads: int = 16) -> str | None:
-    """None when every 1,024-pod block's digest matches; else a report on the first block
-    that differs, with the oracle re-run on that block."""
-    dg = mf.config3_digests(got, fx["block"])
-    bad = [b for b, (x, y) in enumerate(zip(dg, fx["digests"])) if x != y]
+def check_variant_inputs(fx: dict, nodes, pods):
+    got = mf.input_digest(nodes, pods, mode_b=fx.get("mode", 0) == 1)
+    assert got == fx["inputs"], (
+        f"the generator made different inputs here ({got}) than where the fixture was made "
+        f"({fx['inputs']}): numpy drift, not a kernel mismatch")
+
+
+def eval_mismatch(fx: dict, got, nodes, pods, oracle, threads: int = 16) -> str | None:
+    """None when every 1,024-pod block's digest matches (pick, status, feasible count, ties,
+    top score and, in Mode A, the maxima of EVERY pod); else a report on the first block that
+    differs, with the oracle re-run on that block."""
+    mode = fx.get("mode", 0)
+    dg = mf.eval_digests(got, fx["block"], mode)
     if len(dg) != len(fx["digests"]):
         return f"{len(dg)} blocks, fixture has {len(fx['digests'])}"
+    bad = [b for b, (x, y) in enumerate(zip(dg, fx["digests"])) if x != y]
     if not bad:
         return None
     b = bad[0]
     B = fx["block"]
     sel = np.arange(b * B, min(pods.n_pods, (b + 1) * B))
-    want = oracle.schedule(nodes, pods.take(sel), 0, threads=threads)
+    want = oracle.schedule(nodes, pods.take(sel), mode, threads=threads)
+    ok = want.status == 0
     diffs = []
-    for f in ("pick", "status", "n_feasible", "n_ties", "top_score"):
+    for f in ("pick", "status", "n_feasible", "n_ties", "top_score", "maxima"):
+        if f == "maxima" and mode != 0:
+            continue
         g, w = getattr(got, f)[sel], getattr(want, f)
-        d = np.nonzero(g != w)[0]
+        if f in ("n_ties", "top_score"):
+            g, w = np.where(ok, g, 0), np.where(ok, w, 0)
+        d = np.nonzero((g != w).reshape(len(sel), -1).any(axis=1))[0]
         if d.size:
             diffs.append(f"{f}: {d.size} pods, first pod {sel[d[0]]}: gpu {g[d[0]]} oracle {w[d[0]]}")
     return (f"{len(bad)} of {len(dg)} blocks differ; first block {b}: "
             + ("; ".join(diffs) or "oracle re-run agrees with the GPU (digest drift?)"))
+
+
+config3_mismatch = eval_mismatch
 
 
 def greedy_mismatch(fx: dict, pick, nodes, pods, order, oracle, threads: int = 16) -> str | None:

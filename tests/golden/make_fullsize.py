@@ -1,12 +1,20 @@
 #!/usr/bin/env python3
 """Full-size parity fixtures: per-block digests of the C oracle's outputs on BASELINE configs
-3 and 5 at their declared sizes (tests/golden/fullsize.json).
+3 and 5 at their declared sizes, and on every variant workload bench.py reports
+(tests/golden/fullsize.json).
 
-    python tests/golden/make_fullsize.py [config3] [config5_0] [config5_1] [--threads T]
+    python tests/golden/make_fullsize.py [config3] [variant_<name> ...] [config5_0] [config5_1]
+                                         [--threads T]
 
 * config 3 (100k pods x 100k nodes, seed 7): every pod is an independent cycle
   (scheduler.go:158-183 then selectHost) -> oracle_schedule over all 100k pods; one digest
-  per 1,024 pods (input order) over (pick, status, n_feasible, n_ties, top_score).
+  per 1,024 pods (input order) over (pick, status, n_feasible, n_ties, top_score, maxima) --
+  n_ties and top_score where the status is 0, the six CollectMaxValues maxima
+  (collection.go:30-76) of every pod.
+* variant_<name> (synth.VARIANTS: mixed50, bytes, bw1000, het100k, diskio, diskio_distinct):
+  the same per-1,024-pod digests of the oracle over every pod of the variant workload, built
+  by synth.variant_workloads exactly as bench.py's `extra.variants` builds it.  Mode B
+  (BalancedCpuDiskIOPriority, algorithm.go:99-119) has no maxima, so its digests omit them.
 * config 5 (1M pods x 100k nodes, seed 13, both greedy flags): the sequential greedy in
   sort.go:8-10 queue order with the algorithm.go:299-303 assume (and the CardNumber
   decrement under YODA_GREEDY_CARD_CAPACITY) -> oracle_greedy_mt (node-parallel cycles,
@@ -51,26 +59,47 @@ def digest(*arrays) -> str:
     return h.hexdigest()[:16]
 
 
-def input_digest(nodes, pods) -> str:
-    """Digest of the generated snapshot and batch (every SoA field the path reads)."""
+def input_digest(nodes, pods, mode_b: bool = False) -> str:
+    """Digest of the generated snapshot and batch (every SoA field the path reads; with
+    mode_b also the Mode-B node metrics and pod requests)."""
     nodes, pods = nodes.normalized(), pods.normalized()
     nf = [nodes.card_number, nodes.card_count, nodes.free_memory_sum, nodes.total_memory_sum,
           nodes.alloc_memory, nodes.card_free_memory, nodes.card_total_memory, nodes.card_clock,
           nodes.card_bandwidth, nodes.card_core, nodes.card_power, nodes.card_healthy]
     pf = [pods.has_number, pods.number, pods.has_memory, pods.memory, pods.has_clock,
           pods.clock, pods.priority]
+    if mode_b:
+        nf += [nodes.cpu, nodes.disk_io]
+        pf += [pods.rio, pods.rcpu]
     return digest(*[np.asarray(a) for a in nf + pf])
 
 
-def config3_digests(res, block=C3_BLOCK):
+def eval_digests(res, block=C3_BLOCK, mode: int = 0):
+    """One digest per `block` pods (input order) of an evaluation batch's outputs: pick,
+    status, n_feasible, n_ties and top_score (zero where the status is not 0: no pick, so no
+    score), and in Mode A the six maxima."""
     P = len(res.pick)
+    ok = np.asarray(res.status) == 0
+    ties = np.where(ok, res.n_ties, 0).astype(np.uint32)
+    top = np.where(ok, res.top_score, 0).astype(np.int64)
     out = []
     for b in range(0, P, block):
         s = slice(b, min(P, b + block))
-        out.append(digest(res.pick[s].astype(np.int32), res.status[s].astype(np.int32),
-                          res.n_feasible[s].astype(np.uint32), res.n_ties[s].astype(np.uint32),
-                          res.top_score[s].astype(np.int64)))
+        arrays = [res.pick[s].astype(np.int32), res.status[s].astype(np.int32),
+                  res.n_feasible[s].astype(np.uint32), ties[s], top[s]]
+        if mode == 0:
+            arrays.append(np.asarray(res.maxima[s], np.uint64))
+        out.append(digest(*arrays))
     return out
+
+
+config3_digests = eval_digests
+FIELDS_A = ("pick i32, status i32, n_feasible u32, n_ties u32 and top_score i64 (0 unless "
+            "status 0), maxima u64[6] (input order)")
+FIELDS_B = "pick i32, status i32, n_feasible u32, n_ties u32 and top_score i64 (0 unless status 0)"
+# the variant workloads bench.py reports (synth.VARIANTS) whose outputs differ from config 3's
+# (f64 / u64 / per-pair kernels compute config 3 itself and are checked against "config3")
+VARIANTS = ("mixed50", "bytes", "bw1000", "het100k", "diskio", "diskio_distinct")
 
 
 def greedy_window_digests(pick, order, window=C5_WINDOW):
@@ -99,10 +128,29 @@ def run_config3(threads):
     print(f"config3: oracle {time.time() - t:.0f} s", flush=True)
     os.makedirs(CACHE, exist_ok=True)
     np.savez(os.path.join(CACHE, "config3.npz"), pick=res.pick, status=res.status,
-             n_feasible=res.n_feasible, n_ties=res.n_ties, top_score=res.top_score)
+             n_feasible=res.n_feasible, n_ties=res.n_ties, top_score=res.top_score,
+             maxima=res.maxima)
     return {"inputs": input_digest(nodes, pods), "pods": pods.n_pods, "nodes": nodes.n_nodes,
-            "block": C3_BLOCK, "fields": "pick i32, status i32, n_feasible u32, n_ties u32, "
-            "top_score i64 (input order)", "digests": config3_digests(res)}
+            "mode": 0, "block": C3_BLOCK, "fields": FIELDS_A, "digests": eval_digests(res)}
+
+
+def variant_inputs(name):
+    """(nodes, pods, mode) of a bench variant, exactly as bench.py builds it."""
+    ((_, nodes, pods, mode, _kw),) = synth.variant_workloads([name])
+    return nodes, pods, mode
+
+
+def run_variant(name, threads):
+    import oracle
+    nodes, pods, mode = variant_inputs(name)
+    t = time.time()
+    res = oracle.schedule(nodes, pods, mode, threads=threads)
+    print(f"variant {name}: oracle {time.time() - t:.0f} s", flush=True)
+    return {"inputs": input_digest(nodes, pods, mode_b=mode == 1), "pods": pods.n_pods,
+            "nodes": nodes.n_nodes, "mode": mode, "block": C3_BLOCK,
+            "desc": synth.VARIANTS[name], "fields": FIELDS_A if mode == 0 else FIELDS_B,
+            "feasible_pairs": int(res.n_feasible.astype(np.int64).sum()),
+            "digests": eval_digests(res, C3_BLOCK, mode)}
 
 
 def run_config5(flags, threads):
@@ -150,13 +198,16 @@ def main(argv):
     if "--threads" in argv:
         threads = int(argv[argv.index("--threads") + 1])
     which = [a for a in argv if not a.startswith("--") and not a.isdigit()] or \
-        ["config3", "config5_0", "config5_1"]
+        ["config3"] + [f"variant_{v}" for v in VARIANTS] + ["config5_0", "config5_1"]
     fx = json.load(open(OUT)) if os.path.exists(OUT) else {}
-    fx["_about"] = ("C-oracle digests at BASELINE configs 3 and 5, full size "
-                    "(tests/golden/make_fullsize.py). Parity unpinned by reference vectors.")
+    fx["_about"] = ("C-oracle digests at BASELINE configs 3 and 5 and the bench's variant "
+                    "workloads, full size (tests/golden/make_fullsize.py). Parity unpinned by "
+                    "reference vectors.")
     for w in which:
         if w == "config3":
             fx["config3"] = run_config3(threads)
+        elif w.startswith("variant_"):
+            fx[w] = run_variant(w[len("variant_"):], threads)
         elif w.startswith("config5_"):
             fx[w] = run_config5(int(w[-1]), threads)
         else:

@@ -71,3 +71,18 @@ def test_release_library_ignores_ab_knobs():
     assert not found, f"release libyoda.so reads tuning knobs from the environment: {found}"
     # the diagnostics may (traces and counters, never results or policy)
     assert b"YODA_K2_TRACE" in data
+
+
+def test_comm_check_devices_names_shared_gpu():
+    """yoda_comm_check_devices (host only): two ranks on one GPU are named before RCCL's init
+    would fail on them with a bare "invalid usage" (the round-4 n2_libyoda failure)."""
+    import pytest
+    capi.comm_check_devices(["0000:05:00.0", "0000:15:00.0", "0000:65:00.0"])
+    capi.comm_check_devices(["0000:05:00.0"])
+    with pytest.raises(capi.YodaError, match=r"SAME_DEVICE: ranks 1 and 3 .*0000:15:00.0"):
+        capi.comm_check_devices(["0000:05:00.0", "0000:15:00.0", "0000:25:00.0",
+                                 "0000:15:00.0"])
+    L = capi.lib()
+    assert L.yoda_comm_check_devices(None, 2, 32, None, None) == -1
+    assert L.yoda_comm_check_devices(b"\0" * 64, 2, 32, None, None) == -1  # empty id
+    assert L.yoda_device_bus_id(None, None, 0) == -1

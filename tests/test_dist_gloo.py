@@ -197,3 +197,42 @@ def test_balanced_bounds():
     assert np.array_equal(balanced_bounds([0, 10], [3.0]), [0, 10])
     tight = balanced_bounds([0, 1, 2, 3], [100.0, 0.0, 0.0])
     assert np.array_equal(tight, [0, 1, 2, 3])
+
+
+def _devices_worker(rank, world, port, q, ids):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from yoda_amd.capi import YodaError
+        from yoda_amd.dist import agree_on_devices
+        try:
+            q.put((rank, agree_on_devices(ids[rank], torch.device("cpu"))))
+        except YodaError as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shared", [False, True])
+def test_gloo_agree_on_devices(shared):
+    """dist.agree_on_devices (LibExchange runs it before yoda_comm_init): the ranks all-gather
+    their PCI bus ids; two ranks on one GPU make EVERY rank raise YODA_ERR_SAME_DEVICE naming
+    them (so no rank goes on into RCCL's init alone)."""
+    world = 3
+    ids = ["0000:05:00.0", "0000:15:00.0", "0000:05:00.0" if shared else "0000:25:00.0"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_devices_worker, args=(r, world, port, q, ids))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        if shared:
+            assert "SAME_DEVICE: ranks 0 and 2" in outs[r], outs[r]
+        else:
+            assert outs[r] == ids

@@ -72,7 +72,7 @@ def test_fullsize_fixture_pins_the_oracle():
     for b in (0, nb - 1):
         sel = np.arange(b * B, min(pods.n_pods, (b + 1) * B))
         res = oracle.schedule(nodes, pods.take(sel), 0, threads=8)
-        assert fc.mf.config3_digests(res, B)[0] == fx["digests"][b], b
+        assert fc.mf.eval_digests(res, B, 0)[0] == fx["digests"][b], b
     for key in ("config5_0", "config5_1"):
         import json
         if key not in json.load(open(fc.FIXTURE)):
@@ -80,3 +80,19 @@ def test_fullsize_fixture_pins_the_oracle():
         g = fc.load(key)
         fc.check_inputs(g, *synth.make_config(5))
         assert len(g["digests"]) == -(-g["pods"] // g["window"])
+
+
+@pytest.mark.parametrize("name", ["mixed50", "bytes", "bw1000", "het100k", "diskio",
+                                  "diskio_distinct"])
+def test_variant_fixtures_pin_the_oracle(name):
+    """The every-pod digests of the bench's variant workloads (tests/golden/fullsize.json
+    variant_*): the generator still makes the same inputs, and the C oracle reproduces the
+    first 1,024-pod block here (maxima included in Mode A)."""
+    import fullsize_check as fc
+    fx = fc.load(f"variant_{name}")
+    nodes, pods, mode = fc.mf.variant_inputs(name)
+    fc.check_variant_inputs(fx, nodes, pods)
+    assert fx["mode"] == mode and len(fx["digests"]) == -(-pods.n_pods // fx["block"])
+    B = fx["block"]
+    res = oracle.schedule(nodes, pods.slice(0, B), mode, threads=8)
+    assert fc.mf.eval_digests(res, B, mode)[0] == fx["digests"][0]

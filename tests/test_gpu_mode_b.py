@@ -127,14 +127,5 @@ def test_repeated_classes_shuffled(dev):
     np.testing.assert_array_equal(got.pick[same], got2.pick[same])
 
 
-@pytest.mark.parametrize("distinct", [False, True])
-def test_config3_full_size_sampled(dev, distinct):
-    """100k pods x 100k nodes: as generated (one pod spec) and with a distinct diskIO
-    annotation per pod (every pod its own class); 256 pods against the oracle."""
-    nodes, pods = synth.make_config(3)
-    if distinct:
-        pods = synth.distinct_diskio(pods, seed=11)
-    sample = np.linspace(0, pods.n_pods - 1, 256).astype(np.int64)
-    got = check(dev, nodes, pods, sample=sample)
-    assert (got.status == 0).all()
-    assert (got.n_feasible == nodes.n_nodes).all()
+# Config 3 in Mode B at 100k x 100k (one pod class, and a distinct request per pod): every
+# pod in tests/test_gpu_fullsize.py (variants diskio, diskio_distinct).

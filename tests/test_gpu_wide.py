@@ -4,7 +4,6 @@ them in u32 with every quotient in f64 and, beyond 16 bits, unpa
 partial words; such snapshots must be one GPU model per node (else F64), and a clock quotient
 that could overflow the u32 card score sends them to F64 too.  Everything is compared with
 the C oracle (oracle/yoda_oracle.c)."""
-import dataclasses
 
 import numpy as np
 import pytest
@@ -107,22 +106,7 @@ def test_wide_fields_greedy(flags):
     y.close()
 
 
-def test_wide_fields_full_size_sample(dev):
-    """BASELINE config 3 at 100k x 100k with bandwidth x 1000: the N32 block kernels (not the
-    per-pair F64 ones), every output of a 1,024-pod sample against the oracle."""
-    nodes, pods = synth.make_config(3)
-    nodes.card_bandwidth[:] = nodes.card_bandwidth * np.uint64(1000)
-    dev.upload_nodes(nodes)
-    assert dev.path == "n32"
-    got = dev.eval(pods, MODE_SCV)
-    idx = np.random.default_rng(5).choice(pods.n_pods, 1024, replace=False)
-    want = oracle.schedule(nodes, pods.take(idx), MODE_SCV, threads=16)
-    assert_same(_take(got, idx), want)
-
-
-def _take(res, idx):
-    return dataclasses.replace(res, **{f.name: getattr(res, f.name)[idx]
-                                       for f in dataclasses.fields(res)})
+# bandwidth x 1000 at 100k x 100k: every pod in tests/test_gpu_fullsize.py (variant bw1000)
 
 
 @pytest.mark.parametrize("mixed_narrow_shard", [False, True])
