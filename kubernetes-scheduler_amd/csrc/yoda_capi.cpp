@@ -128,7 +128,7 @@ hipError_t launch_set_static(unsigned char* nodes, uint32_t stride, const uint32
 hipError_t launch_bsum_cn(const unsigned char* sum, uint32_t sum_stride, uint32_t n_nodes,
                           uint32_t* bsum, uint32_t bsw, hipStream_t s);
 hipError_t launch_block_ub(int K, const uint32_t* sum2, const uint32_t* tab, uint32_t n_nodes,
-                           uint32_t* out, hipStream_t s);
+                           uint32_t* out, const uint32_t* levels, hipStream_t s);
 hipError_t launch_gtable(int K, const uint32_t* sum2, const uint32_t* mix, uint32_t n_nodes,
                          const uint64_t* g_max,
                          uint32_t* tab, uint32_t* rcp_out, MemTab mt, hipStream_t s);
@@ -346,6 +346,9 @@ struct yoda_handle {
   bool greedy_active = false;  // inside a greedy batch (its pushes keep the bounds valid)
   // K2 block bounds (yoda_layout.h kbub_*) of both orders; dirty: static scores changed since
   DevBuf kbub, kbub_p;
+  DevBuf kb_levels;          // the free levels of kbub's lv[] bounds (kKbLevels u32)
+  bool seeds_valid = false;  // this run's block K1 cleared and writes the K2 pruning seeds
+  bool kb_levels_ok = false;  // built for the current snapshot
   bool kbub_dirty = true;   // a static score rose above the bounds' own: rebuild before use
   bool kbub_loose = false;  // static scores only fell since the build: valid, rebuilt for runs
   std::vector<uint64_t> ub_stat;  // each node's static score when the bounds were built
@@ -752,7 +755,8 @@ int ensure_state(yoda_t* h, uint32_t P) {
   HIP_TRY(h, h->n_flagged.ensure(16));
   // [wave][node] u64 masks (yoda_layout.h), +8 words: K2 reads masks in groups of 8
   HIP_TRY(h, h->bitmask.ensure(((size_t)(P + 63) / 64 * bm_row(h->n_nodes) + 8) * 8));
-  HIP_TRY(h, h->blk.ensure((size_t)(P + 63) / 64 * blk_row(h->n_nodes) * 8));
+  // the block list [waves][blk_row] then the K2 pruning seeds [waves] (PodParams::seed)
+  HIP_TRY(h, h->blk.ensure((size_t)(P + 63) / 64 * (blk_row(h->n_nodes) + 1) * 8));
   HIP_TRY(h, h->bsum.ensure((size_t)(P + 63) / 64 * bs_row(h->n_nodes) * sizeof(BlockMask)));
   HIP_TRY(h, h->p_max_u.ensure(6 * CP * 8));
   if (h->generic) {
@@ -794,6 +798,12 @@ PodParams pod_params(yoda_t* h) {
   if (h->path == Path::N32 && h->has_k1sum && h->blksum.p) pp.bsum = h->blksum.as<uint32_t>();
   const bool ub_ok = h->path == Path::N32 && pp.g.tab && !h->kbub_dirty && h->kbub.p;
   if (ub_ok) pp.kbub = h->kbub.as<uint32_t>();
+  pp.kbub_exact = ub_ok && !h->kbub_loose;
+  if (ub_ok && h->kb_levels_ok) pp.kb_levels = h->kb_levels.as<uint32_t>();
+  // the K2 pruning seeds live after the block list (cleared with it); the block K1 of this run
+  // writes them, the argmax K2 of the same run reads them
+  if (ub_ok && h->seeds_valid && h->blk_valid && h->bm_sparse && pp.g.tab)
+    pp.seed = h->blk.as<uint64_t>() + (size_t)((h->n_work + 63) / 64) * blk_row(h->n_nodes);
   if (ub_ok && h->hot_ok) pp.hot = h->hot.as<uint64_t>();
   if (h->perm_run()) {
     pp.ids = h->perm_ids.as<uint32_t>();
@@ -890,7 +900,7 @@ int order_pods(yoda_t* h, int mode) {
       }
     }
     // the K1 block list is cleared here rather than by a memset in phase 1
-    const uint32_t n_zero = h->has_k1sum ? (W + 63) / 64 * blk_row(h->n_nodes) : 0u;
+    const uint32_t n_zero = h->has_k1sum ? (W + 63) / 64 * (blk_row(h->n_nodes) + 1) : 0u;
     h->blk_zeroed = n_zero != 0;
     HIP_TRY(h, h->order_slot.ensure((size_t)P * 4));
     HIP_TRY(h, h->order_bkt.ensure((size_t)P * 4));
@@ -1048,21 +1058,53 @@ int ensure_diskio_classes(yoda_t* h) {
   return YODA_OK;
 }
 
+// The free levels t_0 = 0 < ... < t_{L-1} = 0xFFFFFFFF of the kbub lv[] bounds (yoda_layout.h):
+// the quantiles of the snapshot's real card frees (K2 summary words: values, or memory ranks),
+// so that a wave's scv/memory range falls between close levels wherever the cards are.
+hipError_t build_kb_levels(yoda_t* h) {
+  const uint32_t N = h->n_nodes, K = (uint32_t)h->K, S2 = k2sum_stride(h->K);
+  std::vector<uint32_t> f;
+  f.reserve((size_t)N * K);
+  for (uint32_t n = 0; n < N; ++n) {
+    const uint32_t cnt = std::min<uint32_t>((h->host_k2sum[sum_index(n, kS2Meta, S2)] >> 8) & 0xffu, K);
+    for (uint32_t t = 0; t < cnt; ++t) f.push_back(h->host_k2sum[sum_index(n, kS2Fs + t, S2)]);
+  }
+  std::vector<uint32_t> lv(kKbLevels, 0u);
+  lv[kKbLevels - 1] = 0xffffffffu;
+  if (!f.empty()) {
+    for (uint32_t l = 1; l + 1 < kKbLevels; ++l) {  // interior levels: quantiles l / (L - 1)
+      const size_t at = (size_t)((double)l / (kKbLevels - 1) * (double)(f.size() - 1));
+      std::nth_element(f.begin(), f.begin() + at, f.end());
+      lv[l] = f[at];
+    }
+    std::sort(lv.begin() + 1, lv.end() - 1);
+    for (uint32_t l = 1; l + 1 < kKbLevels; ++l)  // strictly increasing above t_0 = 0
+      lv[l] = std::max(lv[l], lv[l - 1] + 1u);
+  }
+  hipError_t e = h->kb_levels.ensure(kKbLevels * 4);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(h->kb_levels.p, lv.data(), kKbLevels * 4, hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);  // (lv goes out of scope)
+  if (e == hipSuccess) h->kb_levels_ok = true;
+  return e;
+}
+
 // The K2 block bounds of both orders from the current K2 summaries and G tables.
 hipError_t build_block_ub(yoda_t* h) {
   hipError_t e = hipSuccess;
   if (!(h->path == Path::N32 && h->has_k2sum && h->gtab.p)) return e;
+  if (!h->kb_levels_ok && (e = build_kb_levels(h)) != hipSuccess) return e;
   const size_t bytes = sum_words(std::max<uint32_t>((h->n_nodes + 63) / 64, 1),
                                  kbub_stride(h->K)) * 4;  // tiles of 64 blocks
   e = h->kbub.ensure(bytes);
   if (e == hipSuccess)
     e = launch_block_ub(h->K, h->k2sum.as<uint32_t>(), h->gtab.as<uint32_t>(), h->n_nodes,
-                        h->kbub.as<uint32_t>(), h->stream);
+                        h->kbub.as<uint32_t>(), h->kb_levels.as<uint32_t>(), h->stream);
   if (e == hipSuccess && h->perm_on) {
     e = h->kbub_p.ensure(bytes);
     if (e == hipSuccess)
       e = launch_block_ub(h->K, h->k2sum_p.as<uint32_t>(), h->gtab_p.as<uint32_t>(), h->n_nodes,
-                          h->kbub_p.as<uint32_t>(), h->stream);
+                          h->kbub_p.as<uint32_t>(), h->kb_levels.as<uint32_t>(), h->stream);
   }
   if (e == hipSuccess) {
     h->kbub_dirty = h->kbub_loose = false;
@@ -1106,6 +1148,7 @@ hipError_t tighten_block_sums(yoda_t* h) {
 // Phase 1: Filter + PreScore maxima (Mode A), or the all-feasible state (Mode B).
 // final_maxima: this handle's maxima are the run's (no exchange follows).
 int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_maxima = false) {
+  h->seeds_valid = false;  // (set again below when this run's block K1 writes them)
   h->rcp_ready = false;
   const uint32_t P = h->n_work;  // sorted positions of this run
   if (P == 0) return YODA_OK;
@@ -1127,11 +1170,17 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_m
   if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
   h->blk_valid = h->has_k1sum;
   h->bm_sparse = h->has_k1sum;  // the block K1 writes the sparse form
-  if (h->blk_valid && !h->blk_zeroed)
-    HIP_TRY(h, hipMemsetAsync(h->blk.p, 0, (size_t)(P + 63) / 64 * blk_row(h->n_nodes) * 8,
+  h->seeds_valid = h->has_k1sum && mode == YODA_MODE_SCV;
+  if (h->blk_valid && !h->blk_zeroed)  // (the list and the seeds after it)
+    HIP_TRY(h, hipMemsetAsync(h->blk.p, 0, (size_t)(P + 63) / 64 * (blk_row(h->n_nodes) + 1) * 8,
                               h->stream));
   h->blk_zeroed = false;
   const bool pr = h->perm_run();  // block-grouped node order (upload's node_perm)
+  // current block bounds for the K1's seeds (loose ones -- static scores fell since the build --
+  // are upper bounds only); outside greedy batches they are rebuilt here rather than in phase 2
+  if (mode == YODA_MODE_SCV && (h->kbub_dirty || (h->kbub_loose && !h->greedy_active)) &&
+      h->path == Path::N32 && h->has_k2sum && h->g.tab)
+    HIP_TRY(h, build_block_ub(h));
   if (h->blksum_loose && !h->greedy_active) HIP_TRY(h, tighten_block_sums(h));
   HIP_TRY(h, launch_k1(h->K, h->path, h->nodes.as<unsigned char>(),
                        h->has_k1sum ? (pr ? h->k1sum_p : h->k1sum).as<unsigned char>() : nullptr,
@@ -1168,6 +1217,7 @@ int phase1_witness(yoda_t* h, uint64_t* maxima, uint32_t* counts, uint32_t* wit,
   if (P == 0) return YODA_OK;
   h->bm_sparse = false;
   h->blk_valid = false;
+  h->seeds_valid = false;
   if (N == 0) {
     HIP_TRY(h, hipMemsetAsync(counts, 0, 2 * (size_t)P * 4, h->stream));
     HIP_TRY(h, hipMemsetAsync(wit, 0, 6 * (size_t)P * 4, h->stream));
@@ -2085,6 +2135,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     h->small_max = max_small;
     h->kbub_dirty = true;
     h->kbub_loose = false;
+    h->kb_levels_ok = false;
     h->hot_ok = false;
     if (h->has_k2sum && h->g.tab && N > 0) {
       HIP_TRY(h, build_block_ub(h));

@@ -615,7 +615,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     uint32_t bs_stride, uint64_t* __restrict__ blk, uint32_t blk_stride,
     unsigned long long* __restrict__ stats, uint32_t* __restrict__ pwit = nullptr,
     const uint32_t* __restrict__ bsm = nullptr, uint32_t nwords = kNarrowWords,
-    uint32_t* __restrict__ wts = nullptr) {
+    uint32_t* __restrict__ wts = nullptr, const uint32_t* __restrict__ gtab = nullptr,
+    const uint32_t* __restrict__ kbub = nullptr, const uint32_t* __restrict__ levels = nullptr,
+    unsigned long long* __restrict__ seed_out = nullptr) {
   static_assert(!(WIT && MIX), "the witness K1 serves one-model snapshots");
   static_assert(SUB == 1 || (SUB == kBlock / kWave && !WIT), "SUB: 1, or one pod wave per workgroup");
   constexpr uint32_t SS = k1sum_stride(K);
@@ -735,6 +737,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   const uint32_t s_mpm_max = uniform_u32(mpm_max), s_mpm_min = uniform_u32(mpm_min);
   const uint32_t s_m_max = uniform_u32(m_max), s_m_min = uniform_u32(m_min);
   const uint32_t s_c_max = uniform_u32(c_max), s_c_min = uniform_u32(c_min);
+  // K2 pruning seed (PodParams::seed): the most any node that EVERY live pod of the wave passes
+  // scores for all of them under the G maxima -- static + B_G[q], q = the cards that qualify
+  // for the wave's largest scv/memory (so for every pod: B_G is non-decreasing in q), one-model
+  // nodes only (a feasible one has the pods' scv/clock, so every card passes the clock test)
+  const bool seeding = !WIT && seed_out != nullptr && gtab != nullptr;
+  // (kept in LDS, one word per wave, max-updated by the lanes: no registers across the loops)
+  __shared__ unsigned long long lds_seed[kBlock / kWave];
+  unsigned long long* sdw = lds_seed + (threadIdx.x >> 6);
+  if (seeding && lane == 0) *sdw = 0ull;
+  // ALL blocks: kbub's lv[l_hi], l_hi = the smallest free level >= the wave's largest scv/memory
+  uint32_t l_hi = kKbLevels - 1u;
+  if (seeding && kbub != nullptr && levels != nullptr)
+    for (uint32_t l = kKbLevels - 1u; l-- > 0u;) l_hi = levels[l] >= s_m_max ? l : l_hi;
   const uint32_t bs_tn = kBsT + (uint32_t)K + (hfs_none_ok && nm_min > 0u ? nm_min - 1u : 0u);
   const uint32_t bs_ta = kBsT + (any_pm && hfs_all_ok && nm_max > 0u ? nm_max - 1u : 0u);
   // per-node classification of one 64-node block (below: only the blocks the block summaries
@@ -885,6 +900,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     }
     const bool is_none = valid && feas_none;
     const bool is_all = valid && !feas_none && feas_all && same;
+    if (seeding) {
+      const bool sdl = valid && feas_all && !feas_none && uni4;
+      if (ballot(sdl) != 0ull && sdl) {
+        uint32_t q = 0;  // healthy cards with free >= the largest m (<= the qualifying cards)
+#pragma unroll
+        for (int t = 0; t < K; ++t) q += s[64 * (kSumHfs + t)] > m_max ? 1u : 0u;
+        const uint32_t* s2 = sum2w + sum_index(nb, 0, k2sum_stride(K)) + lane;
+        const double st = __longlong_as_double(
+            (long long)((uint64_t)s2[64 * kS2Static] | ((uint64_t)s2[64 * (kS2Static + 1)] << 32)));
+        const uint32_t bq = q > 0u ? gtab[sum_index(nb + lane, q - 1u, gtab_stride(K))] : 0u;
+        atomicMax(sdw, (unsigned long long)((uint64_t)st + (uint64_t)bq));
+      }
+    }
     const uint64_t all_b = ballot(is_all), none_b = ballot(is_none);
     uint64_t part_b = ballot(valid) & ~all_b & ~none_b;
     if (STATS && !trace) {  // class counts of (wave, node) pairs: ALL, NONE; whole blocks
@@ -1075,6 +1103,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
       if (ball) {
         g_nf += nreal;
         g_nz += B[64 * kBsNzt];
+        if (seeding && kbub != nullptr) {  // the block's lv[l_hi]: a node every pod passes scores it
+          const uint32_t w = kbub_lvl(K) + 2u * l_hi;
+          const uint32_t* U = kbub + sum_index(bi, w, kbub_stride(K));
+          const double v = __longlong_as_double((long long)((uint64_t)U[0] | ((uint64_t)U[64] << 32)));
+          if (v > 0.0) atomicMax(sdw, (unsigned long long)v);
+        }
         if constexpr (!WIT) {
           // K2 cost hint (wts): a block whose q-th healthy frees straddle the wave's memory
           // range leaves the K2 counting qualifying cards per pod on its nodes
@@ -1153,6 +1187,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   nf_all += g_nf;
   nz_all += g_nz;
   blk_flush();
+  if (seeding && lane == 0) {  // this (wave, chunk)'s seed into the wave's (every chunk's; max)
+    const unsigned long long w = *sdw;
+    if (w != 0ull) atomicMax(seed_out + (p >> 6), w);
+  }
   // the wave's weight for the K2's heaviest-first order (k_lpt_order): its PART nodes and the
   // ALL nodes above, summed over its chunks (one add per (wave, chunk); k_lpt_order reads and
   // re-zeroes them)
@@ -1753,7 +1791,8 @@ hipError_t launch_lpt_order(uint32_t* wts, uint32_t n_pods, uint32_t* order, hip
 template <int K>
 __global__ __launch_bounds__(kWave) void k_block_ub(const uint32_t* __restrict__ sum2,
                                                     const uint32_t* __restrict__ tab,
-                                                    uint32_t n_nodes, uint32_t* __restrict__ out) {
+                                                    uint32_t n_nodes, uint32_t* __restrict__ out,
+                                                    const uint32_t* __restrict__ levels) {
   constexpr uint32_t S2 = k2sum_stride(K), GS = gtab_stride(K), BW = kbub_stride(K) / 4u;
   const uint32_t b = blockIdx.x, n = b * 64u + threadIdx.x;
   const bool v = n < n_nodes;
@@ -1778,24 +1817,42 @@ __global__ __launch_bounds__(kWave) void k_block_ub(const uint32_t* __restrict__
       o_at(2 * j + 1) = (uint32_t)(ub >> 32);
     }
   }
+  uint32_t fs[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const uint32_t f = v ? sum2[sum_index(n, kS2Fs + (uint32_t)k, S2)] : 0u;
-    const uint32_t fm = wave_max_u32(f);
+    fs[k] = v ? sum2[sum_index(n, kS2Fs + (uint32_t)k, S2)] : 0u;
+    const uint32_t fm = wave_max_u32(fs[k]);
     if (threadIdx.x == 0) o_at(kbub_fmax(K) + k) = fm;
+  }
+  // the level bounds lv[l]: static + B_G[nq(t_l)] maximised over the block's real nodes
+  for (uint32_t l = 0; l < kKbLevels; ++l) {
+    const uint32_t t = levels[l];
+    uint32_t q = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) q += fs[k] >= t ? 1u : 0u;
+    q = min(q, cnt);
+    const uint32_t bq2 = (v && q > 0u) ? tab[sum_index(n, q - 1u, GS)] : 0u;
+    double u = v ? stat + (double)bq2 : -1.0;  // exact: integers below 2^53
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) u = fmax(u, __shfl_xor(u, off, kWave));
+    if (threadIdx.x == 0) {
+      const uint64_t ub = (uint64_t)__double_as_longlong(u);
+      o_at(kbub_lvl(K) + 2u * l) = (uint32_t)ub;
+      o_at(kbub_lvl(K) + 2u * l + 1u) = (uint32_t)(ub >> 32);
+    }
   }
 }
 
 hipError_t launch_block_ub(int K, const uint32_t* sum2, const uint32_t* tab, uint32_t n_nodes,
-                           uint32_t* out, hipStream_t s) {
+                           uint32_t* out, const uint32_t* levels, hipStream_t s) {
   if (n_nodes == 0) return hipSuccess;
   const dim3 grid((n_nodes + 63) / 64);
   switch (K) {
-    case 1: hipLaunchKernelGGL(k_block_ub<1>, grid, dim3(kWave), 0, s, sum2, tab, n_nodes, out); break;
-    case 2: hipLaunchKernelGGL(k_block_ub<2>, grid, dim3(kWave), 0, s, sum2, tab, n_nodes, out); break;
-    case 4: hipLaunchKernelGGL(k_block_ub<4>, grid, dim3(kWave), 0, s, sum2, tab, n_nodes, out); break;
-    case 8: hipLaunchKernelGGL(k_block_ub<8>, grid, dim3(kWave), 0, s, sum2, tab, n_nodes, out); break;
-    case 16: hipLaunchKernelGGL(k_block_ub<16>, grid, dim3(kWave), 0, s, sum2, tab, n_nodes, out); break;
+    case 1: hipLaunchKernelGGL(k_block_ub<1>, grid, dim3(kWave), 0, s, sum2, tab, n_nodes, out, levels); break;
+    case 2: hipLaunchKernelGGL(k_block_ub<2>, grid, dim3(kWave), 0, s, sum2, tab, n_nodes, out, levels); break;
+    case 4: hipLaunchKernelGGL(k_block_ub<4>, grid, dim3(kWave), 0, s, sum2, tab, n_nodes, out, levels); break;
+    case 8: hipLaunchKernelGGL(k_block_ub<8>, grid, dim3(kWave), 0, s, sum2, tab, n_nodes, out, levels); break;
+    case 16: hipLaunchKernelGGL(k_block_ub<16>, grid, dim3(kWave), 0, s, sum2, tab, n_nodes, out, levels); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1835,6 +1892,10 @@ struct ScoreArgs {
   const uint64_t* hot = nullptr;  // blocks of the highest bounds (bit b % 64 of word b / 64):
                                   // visited first, so that the best so far rises early
   const uint32_t* pb_order = nullptr;  // the block K2's pod-block visiting order (or none)
+  // argmax pruning: the block K1's per-wave seeds (a lower bound on every live pod's best,
+  // PodParams::seed) and the free levels of kbub's lv[] bounds (nullptr: none)
+  const unsigned long long* seed = nullptr;
+  const uint32_t* levels = nullptr;
 };
 
 template <Path P>
@@ -2237,7 +2298,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // k-th key (thrk: the min over active lanes of their own and the U list's k-th) is skipped.
   const bool prune = args.kbub != nullptr && use_g;
   constexpr uint32_t KBST = kbub_stride(K);
+  // The block K1's seed: a score every live pod of the wave reaches on some node it passes (a
+  // G score, so valid exactly when the wave's maxima are G's, i.e. under `prune`): no pod's
+  // best -- nor a tie of it -- lies below, so thr starts there instead of at -1 and blocks
+  // whose bound is below it are skipped from the first one on.
   double thr = -1.0;
+  if (prune && !TOPK && args.seed != nullptr) {
+    const uint64_t sv = args.seed[uniform_u32(p >> 6)];
+    if (sv != 0ull) thr = (double)sv;  // (an integer below 2^53)
+  }
+  // the largest free level <= the wave's smallest scv/memory: every active pod qualifies at
+  // most nq(t) cards on every node, so kbub's lv[l_lo] bounds the block too (its word: lvw)
+  uint32_t lvw = 0;
+  if (prune && args.levels != nullptr) {
+    uint32_t l_lo = 0;
+    for (uint32_t l = 1; l < kKbLevels; ++l) l_lo = args.levels[l] <= m_min ? l : l_lo;
+    lvw = uniform_u32(kbub_lvl(K) + 2u * l_lo);
+  }
   uint64_t thrk = 0ull;
 
   double ubest = -1.0;                      // node lane (U nodes)
@@ -2277,8 +2354,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
 #pragma unroll
     for (int k = 0; k < K; ++k)
       J += U[sum_index(b, kbub_fmax(K) + (uint32_t)k, KBST)] >= m_min ? 1u : 0u;
-    return __longlong_as_double((long long)((uint64_t)U[sum_index(b, 2 * J, KBST)] |
-                                            ((uint64_t)U[sum_index(b, 2 * J + 1, KBST)] << 32)));
+    double ub = __longlong_as_double((long long)((uint64_t)U[sum_index(b, 2 * J, KBST)] |
+                                                 ((uint64_t)U[sum_index(b, 2 * J + 1, KBST)] << 32)));
+    if (lvw != 0u)
+      ub = fmin(ub, __longlong_as_double((long long)((uint64_t)U[sum_index(b, lvw, KBST)] |
+                                                     ((uint64_t)U[sum_index(b, lvw + 1u, KBST)] << 32))));
+    return ub;
   };
   auto pruned = [&](double ub) -> bool {
     if constexpr (TOPK) {  // (ub: an integer-valued double >= 0)
@@ -2722,7 +2803,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
           double lb = act ? fmax(rties > 0u ? (double)rbest : -1.0, wu) : HUGE_VAL;
 #pragma unroll
           for (int o = kWave / 2; o > 0; o >>= 1) lb = fmin(lb, __shfl_xor(lb, o, kWave));
-          thr = __longlong_as_double((long long)uniform_u64((uint64_t)__double_as_longlong(lb)));
+          // (lb only grows; max with the seed the threshold started at)
+          thr = fmax(thr, __longlong_as_double(
+                              (long long)uniform_u64((uint64_t)__double_as_longlong(lb))));
         }
       }
     }
@@ -4251,7 +4334,9 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                                       chunk_nodes, pp.m_32, pp.c_32, pp.number, pp.need_mem,   \
                                       pp.need_clk, n_pods, part.max_u, part.cnt, bm, bm_stride, \
                                       bs, bs_stride, blk, blk_stride, stats, nullptr, pp.bsum,   \
-                                      pp.nwords, pp.lpt_w))
+                                      pp.nwords, pp.lpt_w, pp.seed ? pp.g.tab : nullptr,         \
+                                      pp.kbub_exact ? pp.kbub : nullptr, pp.kb_levels,           \
+                                      reinterpret_cast<unsigned long long*>(pp.seed)))
         if (sub == 1u) {
           if (stats) YODA_K1B(KK, true)
           else if (pp.one_model) YODA_K1B(KK, false, false)
@@ -4404,7 +4489,9 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, counts, pp.g, pp.mix, pp.mt,
                     pp.ids, OUT == OUT_ARGMAX ? pp.kbub : nullptr,
-                    OUT == OUT_ARGMAX ? pp.hot : nullptr, OUT == OUT_ARGMAX ? pp.lpt_order : nullptr};
+                    OUT == OUT_ARGMAX ? pp.hot : nullptr, OUT == OUT_ARGMAX ? pp.lpt_order : nullptr,
+                    OUT == OUT_ARGMAX ? reinterpret_cast<const unsigned long long*>(pp.seed) : nullptr,
+                    OUT == OUT_ARGMAX && pp.kbub ? pp.kb_levels : nullptr};
   const MaskSrc ms{bm, bs, bm_stride, bs_stride, blk, blk_stride};
   if (bs && !blk) return hipErrorInvalidValue;  // sparse masks are read through their block list
   switch (path) {
@@ -4503,7 +4590,8 @@ hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigne
   if (bs && !blk) return hipErrorInvalidValue;  // sparse masks are read through their block list
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, counts, pp.g, pp.mix, pp.mt,
-                    nullptr, pp.kbub, nullptr, pp.lpt_order};
+                    nullptr, pp.kbub, nullptr, pp.lpt_order, nullptr,
+                    pp.kbub ? pp.kb_levels : nullptr};
 #define YODA_TOPKB(TKV, RKV, MIXV, Q32V)                                                        \
   YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false, TKV, RKV, MIXV, Q32V>), grid,      \
                                       dim3(kBlock), 0, s, nodes, sum2, n_nodes, chunk_nodes, a,   \

@@ -142,11 +142,21 @@ __host__ __device__ constexpr uint32_t bsum_stride(int k) { return 4u * (kBsT + 
 //            every node of the block scores more there (basic <= B_G[nq], nq <= j)
 //   fmax[k]  (u32, from word 2K + 2; k < K)  the max over the nodes of fs[k] (K2 summary): a
 //            pod with scv/memory m qualifies at most #{k : fmax[k] >= m} cards on any of them
+//   lv[l]    (f64, words kbub_lvl(K) + 2l, 2l + 1; l < kKbLevels)  the max over the block's real
+//            nodes of static + B_G[nq(t_l)], nq(t) = min(#{fs >= t}, len(CardList)), at the
+//            snapshot's free levels t_0 = 0 < t_1 < ... < t_{L-1} = 0xFFFFFFFF (kb_levels):
+//            - an UPPER bound for a wave whose smallest scv/memory is >= t_l (each pod qualifies
+//              at most nq(t_l) cards, B_G is non-decreasing in q): the argmax K2's pruning;
+//            - a LOWER bound on every pod's best score for a wave whose largest scv/memory is
+//              <= t_l when every node of the block is feasible for every pod of the wave (the
+//              maximising node scores at least that for each of them): the block K1's seed.
 // Built from the K2 summaries and the G table on the device (k_block_ub), again whenever the
 // static scores changed (k_set_static).
+constexpr uint32_t kKbLevels = 32;
 __host__ __device__ constexpr uint32_t kbub_fmax(int k) { return 2u * (uint32_t)k + 2u; }
+__host__ __device__ constexpr uint32_t kbub_lvl(int k) { return kbub_fmax(k) + (uint32_t)k; }
 __host__ __device__ constexpr uint32_t kbub_stride(int k) {
-  return (4u * (kbub_fmax(k) + (uint32_t)k) + 15u) & ~15u;
+  return (4u * (kbub_lvl(k) + 2u * kKbLevels) + 15u) & ~15u;
 }
 
 // Per-card GPU models of every node (N32 path), in the K2 summary's descending-free card order,
@@ -349,6 +359,14 @@ struct PodParams {
   // lpt_order, the argmax block K2 visits its pod blocks in that order (nullptr: none)
   uint32_t* lpt_w = nullptr;
   const uint32_t* lpt_order = nullptr;
+  // K2 pruning seeds [waves] u64 (zeroed with the block list before the block K1): a lower
+  // bound on every live pod's best raw score under the G maxima, found by the block K1 on the
+  // nodes every pod of the wave passes (nullptr: none); the snapshot's free levels kb_levels
+  // [kKbLevels] of the kbub lv[] bounds; kbub_exact: those bounds are current (not loose), so
+  // the block K1 may take seeds from them
+  uint64_t* seed = nullptr;
+  const uint32_t* kb_levels = nullptr;
+  bool kbub_exact = false;
 };
 
 // Per-pod state produced between kernels (length P each unless noted).
