@@ -129,6 +129,8 @@ hipError_t launch_bsum_cn(const unsigned char* sum, uint32_t sum_stride, uint32_
                           uint32_t* bsum, uint32_t bsw, hipStream_t s);
 hipError_t launch_block_ub(int K, const uint32_t* sum2, const uint32_t* tab, uint32_t n_nodes,
                            uint32_t* out, const uint32_t* levels, hipStream_t s);
+hipError_t launch_block_dec(int K, const uint32_t* sum2, uint32_t n_nodes, uint32_t* out,
+                            const uint32_t* levels, uint32_t ranks, hipStream_t s);
 hipError_t launch_gtable(int K, const uint32_t* sum2, const uint32_t* mix, uint32_t n_nodes,
                          const uint64_t* g_max,
                          uint32_t* tab, uint32_t* rcp_out, MemTab mt, hipStream_t s);
@@ -182,8 +184,8 @@ hipError_t launch_order_pods(const uint64_t* number, const uint64_t* m_u, const 
                              const uint32_t* need_mem, uint32_t n_pods, const uint32_t key_bits[3],
                              const uint64_t* groups, uint32_t n_groups, void* scratch,
                              size_t scratch_bytes, uint32_t* perm, const uint32_t* m32, hipStream_t s);
-hipError_t launch_order_count(const OrderMeta& o, const uint64_t* number, const uint64_t* m_u,
-                              const uint64_t* c_u, const uint32_t* need_mem, uint32_t n_pods,
+hipError_t launch_order_count(const OrderMeta& o, const uint64_t* number, const uint32_t* m32,
+                              const uint32_t* c32, const uint32_t* need_mem, uint32_t n_pods,
                               uint32_t* hist, uint32_t* bstart, uint32_t* slot, uint32_t* bkt,
                               const PermTable& t, const uint32_t* pad, uint32_t n_pad,
                               uint64_t* zero, uint32_t n_zero, uint32_t* perm, hipStream_t s);
@@ -301,6 +303,12 @@ enum PodArray {
   kPodM32, kPodC32, kPodNeedMem, kPodNeedClk, kPodArrays
 };
 constexpr size_t kPodArrayBytes[kPodArrays] = {8, 8, 8, 8, 8, 8, 8, 4, 4, 4, 4};
+// Placement in the uploaded blob: first the arrays a private run on the block kernels reads (the
+// counting order included), then the rest, whose copy waits for the first entry point that
+// needs it (pods_complete) -- after the kernels of such a run.
+constexpr int kPodCoreArrays = 5;
+constexpr int kPodPlace[kPodArrays] = {kPodM32, kPodC32, kPodNumber, kPodNeedMem, kPodNeedClk,
+                                       kPodMU, kPodCU, kPodMF, kPodCF, kPodAlpha, kPodBeta};
 
 }  // namespace
 
@@ -346,6 +354,7 @@ struct yoda_handle {
   bool greedy_active = false;  // inside a greedy batch (its pushes keep the bounds valid)
   // K2 block bounds (yoda_layout.h kbub_*) of both orders; dirty: static scores changed since
   DevBuf kbub, kbub_p;
+  DevBuf kbdec, kbdec_p;     // the non-G block bounds (yoda_layout.h kbdec_*) of both orders
   DevBuf kb_levels;          // the free levels of kbub's lv[] bounds (kKbLevels u32)
   bool seeds_valid = false;  // this run's block K1 cleared and writes the K2 pruning seeds
   bool kb_levels_ok = false;  // built for the current snapshot
@@ -389,6 +398,8 @@ struct yoda_handle {
   hipEvent_t switch_event = nullptr;  // yoda_set_stream: the old stream's work, waited on
   bool stage_pending = false;
   size_t pod_off[kPodArrays] = {};
+  size_t pod_rest_off = 0, pod_rest_bytes = 0;  // the blob's deferred part (pods_complete)
+  bool fast_run = false;  // inside a private block-kernel run: the deferred part may wait
   // batch ordering (yoda_order.hip): when `ordered`, the kernels of this run read the pods
   // from pod_sorted (sorted position i = original pod perm[i]); bitmask/rows stay in sorted
   // order and are un-permuted by their transposes, the per-pod outputs by finalize().
@@ -504,7 +515,7 @@ struct yoda_handle {
   ~yoda_handle() {
     if (comm && rccl().ok) (void)rccl().comm_destroy(comm);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &k1sum_p,   &k2sum_p,   &gtab_p, &blksum, &blksum_p, &kbub, &kbub_p, &hot, &hot_p,    &perm_ids,  &perm_inv,    &pod_blob,   &maxima,       &counts,
+    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &k1sum_p,   &k2sum_p,   &gtab_p, &blksum, &blksum_p, &kbub, &kbub_p, &kbdec, &kbdec_p, &kb_levels, &hot, &hot_p,    &perm_ids,  &perm_inv,    &pod_blob,   &maxima,       &counts,
                      &pod_sorted, &perm,     &order_scratch, &order_meta, &order_hist,
                      &order_bstart, &order_slot, &order_bkt,
                      &rcp,       &best,       &idx,          &ties,
@@ -739,6 +750,12 @@ void plan_chunks(yoda_t* h, int mode, uint32_t n_pods, uint32_t n_nodes) {
   plan_chunks_for((uint32_t)capacity(h, 2, mode), r2, n_pods, n_nodes, &h->C2, &h->chunk2);
 }
 
+// u64 words of the block-list buffer: the list, the seeds, the shared best (ensure_state)
+size_t blk_words(const yoda_t* h, uint32_t P) {
+  const size_t nw = (P + 63) / 64;
+  return nw * (blk_row(h->n_nodes) + 1) + P;
+}
+
 int ensure_state(yoda_t* h, uint32_t P) {
   const size_t CP = (size_t)std::max(h->C1 * h->k1_sub, h->C2) * P;
   HIP_TRY(h, h->maxima.ensure(6 * (size_t)P * 8));
@@ -755,8 +772,9 @@ int ensure_state(yoda_t* h, uint32_t P) {
   HIP_TRY(h, h->n_flagged.ensure(16));
   // [wave][node] u64 masks (yoda_layout.h), +8 words: K2 reads masks in groups of 8
   HIP_TRY(h, h->bitmask.ensure(((size_t)(P + 63) / 64 * bm_row(h->n_nodes) + 8) * 8));
-  // the block list [waves][blk_row] then the K2 pruning seeds [waves] (PodParams::seed)
-  HIP_TRY(h, h->blk.ensure((size_t)(P + 63) / 64 * (blk_row(h->n_nodes) + 1) * 8));
+  // the block list [waves][blk_row], the K2 pruning seeds [waves] (PodParams::seed), the shared
+  // per-pod best [P] (PodParams::gbest): blk_words(P) u64, all cleared before each block K1
+  HIP_TRY(h, h->blk.ensure(blk_words(h, P) * 8));
   HIP_TRY(h, h->bsum.ensure((size_t)(P + 63) / 64 * bs_row(h->n_nodes) * sizeof(BlockMask)));
   HIP_TRY(h, h->p_max_u.ensure(6 * CP * 8));
   if (h->generic) {
@@ -799,17 +817,28 @@ PodParams pod_params(yoda_t* h) {
   const bool ub_ok = h->path == Path::N32 && pp.g.tab && !h->kbub_dirty && h->kbub.p;
   if (ub_ok) pp.kbub = h->kbub.as<uint32_t>();
   pp.kbub_exact = ub_ok && !h->kbub_loose;
-  if (ub_ok && h->kb_levels_ok) pp.kb_levels = h->kb_levels.as<uint32_t>();
+  // (A/B knobs: YODA_KB_LEVELS=0 / YODA_SEEDS=0 turn the level bounds / the seeds off)
+  static const bool lv_env = YODA_KNOB("YODA_KB_LEVELS", 1) != 0;
+  static const bool seeds_env = YODA_KNOB("YODA_SEEDS", 1) != 0;
+  if (ub_ok && h->kb_levels_ok && lv_env) pp.kb_levels = h->kb_levels.as<uint32_t>();
   // the K2 pruning seeds live after the block list (cleared with it); the block K1 of this run
   // writes them, the argmax K2 of the same run reads them
-  if (ub_ok && h->seeds_valid && h->blk_valid && h->bm_sparse && pp.g.tab)
-    pp.seed = h->blk.as<uint64_t>() + (size_t)((h->n_work + 63) / 64) * blk_row(h->n_nodes);
+  // (A/B knobs: YODA_KB_DEC=0 / YODA_GBEST=0 turn the non-G bounds / the shared best off)
+  static const bool dec_env = YODA_KNOB("YODA_KB_DEC", 1) != 0;
+  static const bool gbest_env = YODA_KNOB("YODA_GBEST", 1) != 0;
+  if (ub_ok && dec_env && h->kbdec.p) pp.kbdec = h->kbdec.as<uint32_t>();
+  if (seeds_env && ub_ok && h->seeds_valid && h->blk_valid && h->bm_sparse && pp.g.tab) {
+    const size_t nw = (h->n_work + 63) / 64;
+    pp.seed = h->blk.as<uint64_t>() + nw * blk_row(h->n_nodes);
+    if (gbest_env) pp.gbest = pp.seed + nw;  // [n_work] after the seeds
+  }
   if (ub_ok && h->hot_ok) pp.hot = h->hot.as<uint64_t>();
   if (h->perm_run()) {
     pp.ids = h->perm_ids.as<uint32_t>();
     if (pp.g.tab) pp.g.tab = h->gtab_p.as<uint32_t>();
     pp.bsum = h->blksum_p.p ? h->blksum_p.as<uint32_t>() : nullptr;
     pp.kbub = ub_ok && h->kbub_p.p ? h->kbub_p.as<uint32_t>() : nullptr;
+    pp.kbdec = pp.kbub && dec_env && h->kbdec_p.p ? h->kbdec_p.as<uint32_t>() : nullptr;
     pp.hot = pp.kbub && h->hot_ok ? h->hot_p.as<uint64_t>() : nullptr;
   }
   pp.mt = h->mem_ranks ? h->mt : MemTab{};
@@ -836,6 +865,19 @@ Partials partials(yoda_t* h) {
   return p;
 }
 
+// The deferred part of the last pod upload (the arrays past kPodCoreArrays) to the device, on
+// the handle's stream, from the pinned staging copy (reused only after stage_event).
+int pods_complete(yoda_t* h) {
+  if (h->pod_rest_bytes == 0) return YODA_OK;
+  unsigned char* st = static_cast<unsigned char*>(h->pod_stage.p);
+  HIP_TRY(h, hipMemcpyAsync(h->pod_blob.as<unsigned char>() + h->pod_rest_off, st + h->pod_rest_off,
+                            h->pod_rest_bytes, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(h, hipEventRecord(h->stage_event, h->stream));
+  h->stage_pending = true;
+  h->pod_rest_bytes = 0;
+  return YODA_OK;
+}
+
 int check_ready(yoda_t* h, int mode) {
   if (!h) return YODA_ERR_INVALID_ARG;
   if (mode != YODA_MODE_SCV && mode != YODA_MODE_DISKIO)
@@ -845,7 +887,7 @@ int check_ready(yoda_t* h, int mode) {
   if (mode == YODA_MODE_DISKIO && !(h->nodes_diskio && h->pods_diskio))
     return fail(h, YODA_ERR_INVALID_ARG, "Mode B needs node cpu/disk_io and pod rio/rcpu");
   HIP_TRY(h, hipSetDevice(h->device));
-  return YODA_OK;
+  return h->fast_run ? YODA_OK : pods_complete(h);
 }
 
 // Batches above this size are sorted (below it a batch fills at most one wave).
@@ -900,7 +942,7 @@ int order_pods(yoda_t* h, int mode) {
       }
     }
     // the K1 block list is cleared here rather than by a memset in phase 1
-    const uint32_t n_zero = h->has_k1sum ? (W + 63) / 64 * (blk_row(h->n_nodes) + 1) : 0u;
+    const uint32_t n_zero = h->has_k1sum ? (uint32_t)blk_words(h, W) : 0u;
     h->blk_zeroed = n_zero != 0;
     HIP_TRY(h, h->order_slot.ensure((size_t)P * 4));
     HIP_TRY(h, h->order_bkt.ensure((size_t)P * 4));
@@ -919,8 +961,8 @@ int order_pods(yoda_t* h, int mode) {
       o.m32 = reinterpret_cast<const uint32_t*>(b + h->pod_off[kPodM32]);
     }
     HIP_TRY(h, launch_order_count(o, reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodNumber]),
-                                  reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodMU]),
-                                  reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodCU]),
+                                  reinterpret_cast<const uint32_t*>(b + h->pod_off[kPodM32]),
+                                  reinterpret_cast<const uint32_t*>(b + h->pod_off[kPodC32]),
                                   reinterpret_cast<const uint32_t*>(b + h->pod_off[kPodNeedMem]),
                                   P, h->order_hist.as<uint32_t>(), h->order_bstart.as<uint32_t>(),
                                   h->order_slot.as<uint32_t>(), h->order_bkt.as<uint32_t>(), t,
@@ -1096,15 +1138,26 @@ hipError_t build_block_ub(yoda_t* h) {
   if (!h->kb_levels_ok && (e = build_kb_levels(h)) != hipSuccess) return e;
   const size_t bytes = sum_words(std::max<uint32_t>((h->n_nodes + 63) / 64, 1),
                                  kbub_stride(h->K)) * 4;  // tiles of 64 blocks
+  const size_t dbytes = sum_words(std::max<uint32_t>((h->n_nodes + 63) / 64, 1),
+                                  kbdec_stride()) * 4;
+  const uint32_t ranks = h->mem_ranks ? 1u : 0u;
   e = h->kbub.ensure(bytes);
+  if (e == hipSuccess) e = h->kbdec.ensure(dbytes);
   if (e == hipSuccess)
     e = launch_block_ub(h->K, h->k2sum.as<uint32_t>(), h->gtab.as<uint32_t>(), h->n_nodes,
                         h->kbub.as<uint32_t>(), h->kb_levels.as<uint32_t>(), h->stream);
+  if (e == hipSuccess)
+    e = launch_block_dec(h->K, h->k2sum.as<uint32_t>(), h->n_nodes, h->kbdec.as<uint32_t>(),
+                         h->kb_levels.as<uint32_t>(), ranks, h->stream);
   if (e == hipSuccess && h->perm_on) {
     e = h->kbub_p.ensure(bytes);
+    if (e == hipSuccess) e = h->kbdec_p.ensure(dbytes);
     if (e == hipSuccess)
       e = launch_block_ub(h->K, h->k2sum_p.as<uint32_t>(), h->gtab_p.as<uint32_t>(), h->n_nodes,
                           h->kbub_p.as<uint32_t>(), h->kb_levels.as<uint32_t>(), h->stream);
+    if (e == hipSuccess)
+      e = launch_block_dec(h->K, h->k2sum_p.as<uint32_t>(), h->n_nodes, h->kbdec_p.as<uint32_t>(),
+                           h->kb_levels.as<uint32_t>(), ranks, h->stream);
   }
   if (e == hipSuccess) {
     h->kbub_dirty = h->kbub_loose = false;
@@ -1172,8 +1225,7 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_m
   h->bm_sparse = h->has_k1sum;  // the block K1 writes the sparse form
   h->seeds_valid = h->has_k1sum && mode == YODA_MODE_SCV;
   if (h->blk_valid && !h->blk_zeroed)  // (the list and the seeds after it)
-    HIP_TRY(h, hipMemsetAsync(h->blk.p, 0, (size_t)(P + 63) / 64 * (blk_row(h->n_nodes) + 1) * 8,
-                              h->stream));
+    HIP_TRY(h, hipMemsetAsync(h->blk.p, 0, blk_words(h, P) * 8, h->stream));
   h->blk_zeroed = false;
   const bool pr = h->perm_run();  // block-grouped node order (upload's node_perm)
   // current block bounds for the K1's seeds (loose ones -- static scores fell since the build --
@@ -2180,6 +2232,8 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
     h->has_nodes = true;
     // the uploaded pods' N32 memory thresholds follow the snapshot (ranks or the clamp)
     if (h->has_pods && path == Path::N32) {
+      int rc = pods_complete(h);  // (the rank kernel reads the 64-bit scv/memory)
+      if (rc) return rc;
       unsigned char* b = h->pod_blob.as<unsigned char>();
       HIP_TRY(h, launch_mem_rank(reinterpret_cast<const uint64_t*>(b + h->pod_off[kPodMU]),
                                  h->n_pods, pod_params(h).mt,
@@ -2240,12 +2294,16 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     h->topk_ready = false;
     h->b_cls_ready = false;
     HIP_TRY(h, hipSetDevice(h->device));
-    // One blob of per-pod arrays, staged in pinned memory and sent with ONE copy.
-    size_t off[kPodArrays], total = 0;
-    for (int a = 0; a < kPodArrays; ++a) {
+    // One blob of per-pod arrays, staged in pinned memory; the arrays a private block-kernel
+    // run reads go with one copy now, the rest (kPodPlace) when an entry point needs them.
+    size_t off[kPodArrays], total = 0, core_bytes = 0;
+    for (int i = 0; i < kPodArrays; ++i) {
+      const int a = kPodPlace[i];
       off[a] = total;
       total += ((size_t)std::max<uint32_t>(P, 1) * kPodArrayBytes[a] + 255) / 256 * 256;
+      if (i == kPodCoreArrays - 1) core_bytes = total;
     }
+    h->pod_rest_bytes = 0;  // (a deferred part of the previous batch is dropped)
     static const bool dbg = std::getenv("YODA_UPLOAD_DEBUG") != nullptr;
     auto now_ms = [] {
       return std::chrono::duration<double, std::milli>(
@@ -2394,7 +2452,10 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     std::vector<uint64_t>& gmin = all.mn;
     const size_t g_n = all.n;
     const double t_merged = dbg ? now_ms() : 0.0;
-    HIP_TRY(h, hipMemcpyAsync(h->pod_blob.p, st, total, hipMemcpyHostToDevice, h->stream));
+    // (memory ranks: the rank kernel below reads the 64-bit scv/memory now)
+    const bool defer = !(h->has_nodes && h->mem_ranks);
+    HIP_TRY(h, hipMemcpyAsync(h->pod_blob.p, st, defer ? core_bytes : total, hipMemcpyHostToDevice,
+                              h->stream));
     const double t_copied = dbg ? now_ms() : 0.0;
     if (h->has_nodes && h->mem_ranks)  // scv/memory -> its rank threshold, on the device
       HIP_TRY(h, launch_mem_rank(reinterpret_cast<const uint64_t*>(
@@ -2468,6 +2529,8 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     HIP_TRY(h, hipEventRecord(h->stage_event, h->stream));
     h->stage_pending = true;
     for (int a = 0; a < kPodArrays; ++a) h->pod_off[a] = off[a];
+    h->pod_rest_off = core_bytes;
+    h->pod_rest_bytes = defer ? total - core_bytes : 0;
     for (int f = 0; f < 3; ++f) {
       uint32_t bits = 0;
       while (bits < 64 && (key_or[f] >> bits)) ++bits;
@@ -2525,9 +2588,51 @@ static int prepare_run(yoda_t* h, int mode, bool pad = false) {
   return ensure_state(h, std::max<uint32_t>(h->n_work, 1));
 }
 
+// Diagnostic (YODA_SEED_DEBUG): how close the block K1's K2 pruning seeds came to each wave's
+// smallest best score (sorted order, before finalize), on stderr.  Never results or policy.
+static void seed_report(yoda_t* h) {
+  const uint32_t W = h->n_work, nw = (W + 63) / 64;
+  std::vector<uint64_t> sd(nw);
+  std::vector<int64_t> best(W);
+  std::vector<uint32_t> cnt(W);
+  const PodParams pp = pod_params(h);
+  if (hipMemcpyAsync(sd.data(), pp.seed, nw * 8ull, hipMemcpyDeviceToHost, h->stream) ||
+      hipMemcpyAsync(best.data(), h->best.p, W * 8ull, hipMemcpyDeviceToHost, h->stream) ||
+      hipMemcpyAsync(cnt.data(), h->counts.p, W * 4ull, hipMemcpyDeviceToHost, h->stream) ||
+      hipStreamSynchronize(h->stream))
+    return;
+  uint32_t zero = 0, bad = 0, act_w = 0, hist[6] = {};
+  double gap = 0;
+  for (uint32_t w = 0; w < nw; ++w) {
+    int64_t mb = INT64_MAX;
+    for (uint32_t l = 64 * w; l < std::min(W, 64 * w + 64); ++l)
+      if (cnt[l] && best[l] >= 0) mb = std::min(mb, best[l]);
+    if (mb == INT64_MAX) continue;
+    ++act_w;
+    if (sd[w] == 0) { ++zero; continue; }
+    if ((int64_t)sd[w] > mb) ++bad;
+    const double r = (double)sd[w] / (double)std::max<int64_t>(mb, 1);
+    hist[r >= 1.0 ? 5 : r >= 0.99 ? 4 : r >= 0.95 ? 3 : r >= 0.9 ? 2 : r >= 0.75 ? 1 : 0]++;
+    gap += (double)(mb - (int64_t)sd[w]);
+  }
+  std::fprintf(stderr, "seeds: %u waves with a best, %u without a seed, %u ABOVE the best (bug); "
+               "seed/best <.75 %u, <.9 %u, <.95 %u, <.99 %u, <1 %u, =1 %u; mean gap %.1f\n",
+               act_w, zero, bad, hist[0], hist[1], hist[2], hist[3], hist[4], hist[5],
+               gap / std::max<uint32_t>(1, act_w - zero));
+}
+
 int yoda_run(yoda_t* h, int mode, uint32_t flags) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  // a private run on the block kernels in the counting order reads only the pod arrays the
+  // upload copied first; the rest of the batch goes to the device after its kernels
+  const bool fast = mode == YODA_MODE_SCV && !(flags & YODA_RUN_BITMASK) &&
+                    h->path == Path::N32 && h->has_k1sum && h->has_k2sum && !h->mem_ranks;
+  h->fast_run = fast;
   int rc = prepare_run(h, mode, (flags & YODA_RUN_BITMASK) == 0);
+  h->fast_run = false;
   if (rc) return rc;
+  const bool defer = fast && h->count_order;
+  if (!defer && (rc = pods_complete(h))) return rc;
   try {
     if ((rc = order_pods(h, mode))) return rc;
     if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), true)))
@@ -2535,10 +2640,12 @@ int yoda_run(yoda_t* h, int mode, uint32_t flags) {
     if ((rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), h->best.as<int64_t>(),
                      h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>())))
       return rc;
+    if (diag_env("YODA_SEED_DEBUG", 0) && pod_params(h).seed) seed_report(h);
     if ((rc = finalize(h, mode, h->counts.as<uint32_t>(), h->best.as<int64_t>(),
                        h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(),
                        false)))
       return rc;
+    if (defer && (rc = pods_complete(h))) return rc;
     h->ran = true;
     h->ran_bitmask = mode == YODA_MODE_SCV && (flags & YODA_RUN_BITMASK);
     h->last_mode = mode;

@@ -287,6 +287,11 @@ __device__ __forceinline__ uint64_t wave_max_u64v(uint64_t v) {
   return v;
 }
 __device__ __forceinline__ uint64_t wave_min_u64v(uint64_t v) { return ~wave_max_u64v(~v); }
+__device__ __forceinline__ double wave_max_f64(double v) {
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
+  return v;
+}
 
 // Lane j of (lo, hi) := the 64-bit wave mask b (j wave-uniform).
 __device__ __forceinline__ void set_lane(uint32_t& lo, uint32_t& hi, uint64_t b, uint32_t j) {
@@ -740,8 +745,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   // K2 pruning seed (PodParams::seed): the most any node that EVERY live pod of the wave passes
   // scores for all of them under the G maxima -- static + B_G[q], q = the cards that qualify
   // for the wave's largest scv/memory (so for every pod: B_G is non-decreasing in q), one-model
-  // nodes only (a feasible one has the pods' scv/clock, so every card passes the clock test)
+  // nodes only (a feasible one has the pods' scv/clock, so every card passes the clock test).
+  // Taken over the ALL blocks (lane = block, kbub's lv[] at the wave's largest scv/memory);
+  // YODA_K1_NODE_SEEDS (A/B) adds the ALL nodes of the blocks classified node by node.
+#ifdef YODA_K1_NOSEED  // (A/B build: the seed code compiled out)
+  const bool seeding = false;
+#else
   const bool seeding = !WIT && seed_out != nullptr && gtab != nullptr;
+#endif
   // (kept in LDS, one word per wave, max-updated by the lanes: no registers across the loops)
   __shared__ unsigned long long lds_seed[kBlock / kWave];
   unsigned long long* sdw = lds_seed + (threadIdx.x >> 6);
@@ -900,6 +911,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     }
     const bool is_none = valid && feas_none;
     const bool is_all = valid && !feas_none && feas_all && same;
+#ifdef YODA_K1_NODE_SEEDS  // (A/B: per-node seeds too -- +35 % K1 time for little K2 gain)
     if (seeding) {
       const bool sdl = valid && feas_all && !feas_none && uni4;
       if (ballot(sdl) != 0ull && sdl) {
@@ -913,6 +925,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
         atomicMax(sdw, (unsigned long long)((uint64_t)st + (uint64_t)bq));
       }
     }
+#endif
     const uint64_t all_b = ballot(is_all), none_b = ballot(is_none);
     uint64_t part_b = ballot(valid) & ~all_b & ~none_b;
     if (STATS && !trace) {  // class counts of (wave, node) pairs: ALL, NONE; whole blocks
@@ -1843,6 +1856,90 @@ __global__ __launch_bounds__(kWave) void k_block_ub(const uint32_t* __restrict__
   }
 }
 
+// The non-G block bounds (yoda_layout.h kbdec_*): one wave per 64-node block, lane = node.
+// ranks: the summaries hold memory ranks (their sums mean nothing): every block "not ok".
+template <int K>
+__global__ __launch_bounds__(kWave) void k_block_dec(const uint32_t* __restrict__ sum2,
+                                                     uint32_t n_nodes, uint32_t* __restrict__ out,
+                                                     const uint32_t* __restrict__ levels,
+                                                     uint32_t ranks) {
+  constexpr uint32_t S2 = k2sum_stride(K), DS = kbdec_stride();
+  const uint32_t b = blockIdx.x, n = b * 64u + threadIdx.x;
+  const bool v = n < n_nodes;
+  auto o_at = [&](uint32_t w) -> uint32_t& { return out[sum_index(b, w, DS)]; };
+  auto put_d = [&](uint32_t w, double d) {
+    const uint64_t u = (uint64_t)__double_as_longlong(d);
+    o_at(w) = (uint32_t)u;
+    o_at(w + 1u) = (uint32_t)(u >> 32);
+  };
+  auto w2 = [&](uint32_t word) { return sum2[sum_index(n, word, S2)]; };
+  double stat = -1.0;
+  uint32_t cnt = 0, meta = 0, bw = 0, ck = 0, co = 0, pw = 0;
+  uint32_t fs[K], ts[K];
+  if (v) {
+    stat = __longlong_as_double((long long)((uint64_t)w2(kS2Static) |
+                                            ((uint64_t)w2(kS2Static + 1) << 32)));
+    meta = w2(kS2Meta);
+    cnt = (meta >> 8) & 0xffu;
+    bw = w2(kS2Bw);
+    ck = w2(kS2Clock);
+    co = w2(kS2Core);
+    pw = w2(kS2Power);
+  }
+#pragma unroll
+  for (int t = 0; t < K; ++t) {
+    const bool real = v && (uint32_t)t < cnt;
+    fs[t] = real ? w2(kS2Fs + (uint32_t)t) : 0u;
+    ts[t] = real ? w2(kS2Fs + (uint32_t)K + (uint32_t)t) : 0u;
+  }
+  const bool ok = ranks == 0u && ballot(v && (meta & kSumUni4) == 0u) == 0ull;
+  const double st = wave_max_f64(stat);
+  const uint32_t mbw = wave_max_u32(bw), mck = wave_max_u32(ck), mco = wave_max_u32(co),
+                 mpw = wave_max_u32(pw);
+  if (threadIdx.x == 0) {
+    o_at(kDecOk) = ok ? 1u : 0u;
+    o_at(kDecBw) = mbw;
+    o_at(kDecCk) = mck;
+    o_at(kDecCo) = mco;
+    o_at(kDecPw) = mpw;
+    put_d(kDecStat, st);
+  }
+  for (uint32_t l = 0; l < kKbLevels; ++l) {
+    const uint32_t t = levels[l];
+    uint32_t q = 0;
+    double f = 0.0, tt = 0.0;  // exact: sums of at most 16 u32
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const bool in = fs[k] >= t && (uint32_t)k < cnt;
+      q += in ? 1u : 0u;
+      f += in ? (double)fs[k] : 0.0;
+      tt += in ? (double)ts[k] : 0.0;
+    }
+    const uint32_t mq = wave_max_u32(q);
+    const double mf = wave_max_f64(f), mt = wave_max_f64(tt);
+    if (threadIdx.x == 0) {
+      o_at(kDecQl + l) = mq;
+      put_d(kbdec_fl(l), mf);
+      put_d(kbdec_tl(l), mt);
+    }
+  }
+}
+
+hipError_t launch_block_dec(int K, const uint32_t* sum2, uint32_t n_nodes, uint32_t* out,
+                            const uint32_t* levels, uint32_t ranks, hipStream_t s) {
+  if (n_nodes == 0) return hipSuccess;
+  const dim3 grid((n_nodes + 63) / 64);
+  switch (K) {
+    case 1: hipLaunchKernelGGL(k_block_dec<1>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, ranks); break;
+    case 2: hipLaunchKernelGGL(k_block_dec<2>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, ranks); break;
+    case 4: hipLaunchKernelGGL(k_block_dec<4>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, ranks); break;
+    case 8: hipLaunchKernelGGL(k_block_dec<8>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, ranks); break;
+    case 16: hipLaunchKernelGGL(k_block_dec<16>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, ranks); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_block_ub(int K, const uint32_t* sum2, const uint32_t* tab, uint32_t n_nodes,
                            uint32_t* out, const uint32_t* levels, hipStream_t s) {
   if (n_nodes == 0) return hipSuccess;
@@ -1896,6 +1993,9 @@ struct ScoreArgs {
   // PodParams::seed) and the free levels of kbub's lv[] bounds (nullptr: none)
   const unsigned long long* seed = nullptr;
   const uint32_t* levels = nullptr;
+  // the non-G block bounds (kbdec_*) and the per-pod best shared across the chunks (PodParams)
+  const uint32_t* kbdec = nullptr;
+  unsigned long long* gbest = nullptr;
 };
 
 template <Path P>
@@ -2296,12 +2396,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // after each block the wave works on (it only grows, so a stale value stays a lower bound).
   // TOPK (greedy windows): a block whose best possible key cannot beat any active lane's
   // k-th key (thrk: the min over active lanes of their own and the U list's k-th) is skipped.
-  const bool prune = args.kbub != nullptr && use_g;
+  // Non-G uniform waves (one reciprocal set, not G's -- e.g. clock-labelled pods, whose feasible
+  // nodes are one GPU model): the decoupled bounds kbdec_* (argmax, no memory ranks).
+  const bool dec = !TOPK && !RK && args.kbdec != nullptr && uni_max && !use_g;
+  const bool prune = args.kbub != nullptr && (use_g || dec);
   constexpr uint32_t KBST = kbub_stride(K);
-  // The block K1's seed: a score every live pod of the wave reaches on some node it passes (a
-  // G score, so valid exactly when the wave's maxima are G's, i.e. under `prune`): no pod's
-  // best -- nor a tie of it -- lies below, so thr starts there instead of at -1 and blocks
-  // whose bound is below it are skipped from the first one on.
+  // The block K1's seed: a score every live pod of the wave reaches on some node it passes,
+  // under the G maxima; a pod's own maxima are never above G's (a max over fewer cards), so
+  // its score there is at least the seed whatever its maxima: no pod's best -- nor a tie of
+  // it -- lies below, and thr starts there instead of at -1.
   double thr = -1.0;
   if (prune && !TOPK && args.seed != nullptr) {
     const uint64_t sv = args.seed[uniform_u32(p >> 6)];
@@ -2309,11 +2412,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   }
   // the largest free level <= the wave's smallest scv/memory: every active pod qualifies at
   // most nq(t) cards on every node, so kbub's lv[l_lo] bounds the block too (its word: lvw)
-  uint32_t lvw = 0;
+  uint32_t lvw = 0, l_lo = 0;
   if (prune && args.levels != nullptr) {
-    uint32_t l_lo = 0;
     for (uint32_t l = 1; l < kKbLevels; ++l) l_lo = args.levels[l] <= m_min ? l : l_lo;
-    lvw = uniform_u32(kbub_lvl(K) + 2u * l_lo);
+    l_lo = uniform_u32(l_lo);
+    lvw = kbub_lvl(K) + 2u * l_lo;
   }
   uint64_t thrk = 0ull;
 
@@ -2349,6 +2452,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // qualify on any node of it (from the block's largest frees and the wave's smallest
   // scv/memory), ub = static + B_G[J] maximised over the block's nodes
   auto block_ub = [&](uint32_t b) -> double {
+    if (dec) {  // static + nq shared + 3 r_free F + r_total T, each maximised over the block
+      constexpr uint32_t DS = kbdec_stride();
+      const uint32_t* D = args.kbdec;
+      if (args.levels == nullptr || D[sum_index(b, kDecOk, DS)] == 0u) return HUGE_VAL;
+      auto d64 = [&](uint32_t w) {
+        return __longlong_as_double((long long)((uint64_t)D[sum_index(b, w, DS)] |
+                                                ((uint64_t)D[sum_index(b, w + 1u, DS)] << 32)));
+      };
+      const uint32_t sh = card_shared_terms(D[sum_index(b, kDecBw, DS)], D[sum_index(b, kDecCk, DS)],
+                                            D[sum_index(b, kDecCo, DS)], D[sum_index(b, kDecPw, DS)],
+                                            u_bw, u_core, u_pow);
+      const double q = (double)D[sum_index(b, kDecQl + l_lo, DS)];
+      // (+1: the f64 rounding of the products; the scores are integers)
+      return d64(kDecStat) + q * (double)sh + 3.0 * u_free * d64(kbdec_fl(l_lo)) +
+             u_tot * d64(kbdec_tl(l_lo)) + 1.0;
+    }
     const uint32_t* U = args.kbub;
     uint32_t J = 0;
 #pragma unroll
@@ -2762,6 +2881,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       take_r(((mj >> lane) & 1ull) != 0ull, to_u(raw), nn);
     }
   };
+  // thr := max(thr, the min over active lanes of their best so far -- this chunk's nodes', the
+  // U nodes', and (gbest) every other chunk's, which this one publishes its own to); each
+  // value is a score the lane reaches on a feasible node, so thr stays below every lane's best
+  auto refresh_thr = [&]() {
+    double wu = ubest;
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) wu = fmax(wu, __shfl_xor(wu, o, kWave));
+    double lb = act ? fmax(rties > 0u ? (double)rbest : -1.0, wu) : HUGE_VAL;
+    if (args.gbest != nullptr && act) {  // (score + 1; 0: none yet)
+      const unsigned long long g = args.gbest[p];
+      const unsigned long long mine = lb >= 0.0 ? (unsigned long long)lb + 1ull : 0ull;
+      if (mine > g) atomicMax(args.gbest + p, mine);
+      lb = fmax(lb, (double)g - 1.0);
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) lb = fmin(lb, __shfl_xor(lb, o, kWave));
+    thr = fmax(thr, __longlong_as_double(
+                        (long long)uniform_u64((uint64_t)__double_as_longlong(lb))));
+  };
   if (blk) {
     // only the blocks K1 found a feasible pod of this wave in (bit b of word b/64)
     const uint64_t* bw = blk + (size_t)uniform_u32(p >> 6) * blk_stride;
@@ -2778,7 +2916,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       // the bounds of the word's 64 blocks, lane = block (one coalesced pass; a block is
       // then skipped on a v_readlane and a compare against the current threshold)
       double ub_l = 0.0;
-      if (prune && bits != 0ull) ub_l = block_ub(min(base + lane, b1 - 1u));
+      if (prune && bits != 0ull) {
+        ub_l = block_ub(min(base + lane, b1 - 1u));
+        if (!TOPK && args.gbest != nullptr) refresh_thr();  // (the other chunks' progress)
+      }
       while (bits) {
         const uint32_t j = (uint32_t)__builtin_ctzll(bits);
         bits &= bits - 1;
@@ -2796,16 +2937,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         if (prune && worked && TOPK) {  // every active lane's k-th key so far
           const uint64_t kth = act ? (pl[TL - 1] > ul[TL - 1] ? pl[TL - 1] : ul[TL - 1]) : ~0ull;
           thrk = wave_min_u64(kth);
-        } else if (prune && worked) {  // every active lane's best: its nodes', the U nodes'
-          double wu = ubest;
-#pragma unroll
-          for (int o = kWave / 2; o > 0; o >>= 1) wu = fmax(wu, __shfl_xor(wu, o, kWave));
-          double lb = act ? fmax(rties > 0u ? (double)rbest : -1.0, wu) : HUGE_VAL;
-#pragma unroll
-          for (int o = kWave / 2; o > 0; o >>= 1) lb = fmin(lb, __shfl_xor(lb, o, kWave));
-          // (lb only grows; max with the seed the threshold started at)
-          thr = fmax(thr, __longlong_as_double(
-                              (long long)uniform_u64((uint64_t)__double_as_longlong(lb))));
+        } else if (prune && worked) {
+          refresh_thr();
         }
       }
     }
@@ -4491,7 +4624,9 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
                     pp.ids, OUT == OUT_ARGMAX ? pp.kbub : nullptr,
                     OUT == OUT_ARGMAX ? pp.hot : nullptr, OUT == OUT_ARGMAX ? pp.lpt_order : nullptr,
                     OUT == OUT_ARGMAX ? reinterpret_cast<const unsigned long long*>(pp.seed) : nullptr,
-                    OUT == OUT_ARGMAX && pp.kbub ? pp.kb_levels : nullptr};
+                    OUT == OUT_ARGMAX && pp.kbub ? pp.kb_levels : nullptr,
+                    OUT == OUT_ARGMAX && pp.kbub ? pp.kbdec : nullptr,
+                    OUT == OUT_ARGMAX ? reinterpret_cast<unsigned long long*>(pp.gbest) : nullptr};
   const MaskSrc ms{bm, bs, bm_stride, bs_stride, blk, blk_stride};
   if (bs && !blk) return hipErrorInvalidValue;  // sparse masks are read through their block list
   switch (path) {

@@ -159,6 +159,28 @@ __host__ __device__ constexpr uint32_t kbub_stride(int k) {
   return (4u * (kbub_lvl(k) + 2u * kKbLevels) + 15u) & ~15u;
 }
 
+// K2 block bounds for waves whose maxima M are NOT the G maxima (N32 path, one reciprocal set;
+// e.g. clock-labelled pods, whose feasible nodes are one GPU model): B_M has no table, so the
+// bound decouples the basic score per card (algorithm.go:280-291) into its model part and its
+// memory part, each bounded over the block's real nodes independently:
+//   basic_M(n, q) <= q shared_M(n) + (300 / M_free) F_n[q] + (100 / M_total) T_n[q]
+// (floor(x 100 / M) <= x r with r = RU(100 / M)), F / T the sums of free / total over the q
+// cards of largest free.  u32 words, tiles of 64 blocks (sum_index(block, word, kbdec_stride)):
+//   ok            1: every real node of the block is one GPU model (kSumUni4), values, not ranks
+//   bw, ck, co, pw   the max over the block's nodes of the model values (shared_M is monotone)
+//   stat (f64)    the max static score
+//   ql[l]         the max over the nodes of nq(t_l) (kb_levels, as kbub's lv[])
+//   fl[l] (f64)   the max over the nodes of the sum of the frees >= t_l
+//   tl[l] (f64)   the max over the nodes of the sum of the totals of those cards
+// so that static + nq shared + 3 r_free F + r_total T <= stat + ql shared(bw, ck, co, pw) +
+// 3 r_free fl + r_total tl for every pod whose smallest scv/memory is >= t_l.
+enum KbDecWord { kDecOk = 0, kDecBw = 1, kDecCk = 2, kDecCo = 3, kDecPw = 4, kDecStat = 5, kDecQl = 7 };
+__host__ __device__ constexpr uint32_t kbdec_fl(uint32_t l) { return kDecQl + kKbLevels + 2u * l; }
+__host__ __device__ constexpr uint32_t kbdec_tl(uint32_t l) { return kDecQl + 3u * kKbLevels + 2u * l; }
+__host__ __device__ constexpr uint32_t kbdec_stride() {
+  return (4u * (kDecQl + 5u * kKbLevels) + 15u) & ~15u;
+}
+
 // Per-card GPU models of every node (N32 path), in the K2 summary's descending-free card order,
 // read with lane = node by the block kernels for the nodes whose cards are not all one model
 // (no kSumUni4): u32 words
@@ -367,6 +389,11 @@ struct PodParams {
   uint64_t* seed = nullptr;
   const uint32_t* kb_levels = nullptr;
   bool kbub_exact = false;
+  // the non-G block bounds (kbdec_*) of the order the run visits (nullptr: none), and the
+  // argmax K2's per-pod best so far shared across its node chunks ([P] u64: score + 1, zeroed
+  // with the block list; nullptr: none)
+  const uint32_t* kbdec = nullptr;
+  uint64_t* gbest = nullptr;
 };
 
 // Per-pod state produced between kernels (length P each unless noted).

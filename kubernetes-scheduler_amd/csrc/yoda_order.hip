@@ -180,10 +180,12 @@ hipError_t launch_permute(const PermTable& t, const uint32_t* perm, uint32_t n_p
 // (a sorted position that maps to the same caller pod: identical inputs, identical
 // results, written back twice), so no wave mixes two groups -- a mixed wave leaves the
 // block kernels nothing but per-pod work on every node.
+// (m32 / c32: scv/memory / scv/clock clamped to 32 bits -- or the memory rank -- whose 32- and
+// 24-bit clamps below equal those of the 64-bit labels: the counting order reads only the pod
+// arrays the block kernels read)
 __device__ __forceinline__ uint32_t order_bucket(const OrderMeta& o, uint64_t number,
-                                                 uint64_t m_u, uint64_t c_u, uint32_t need_mem,
-                                                 uint32_t p) {
-  const uint64_t c = c_u < 0xffffffull ? c_u : 0xffffffull;
+                                                 uint32_t m32, uint32_t c32, uint32_t need_mem) {
+  const uint64_t c = c32 < 0xffffffu ? c32 : 0xffffffu;
   const uint64_t n = number < 0xffull ? number : 0xffull;
   const uint64_t key = (c << 9) | (n << 1) | (need_mem != 0u ? 1ull : 0ull);
   uint32_t lo = 0, hi = o.n_groups;  // lower_bound: the group's rank (the key is present)
@@ -191,8 +193,8 @@ __device__ __forceinline__ uint32_t order_bucket(const OrderMeta& o, uint64_t nu
     const uint32_t mid = (lo + hi) >> 1;
     if (o.groups[mid] < key) lo = mid + 1; else hi = mid;
   }
-  // memory ranks: the rank thresholds (monotone in scv/memory) instead of the 32-bit clamp
-  const uint64_t m = o.m32 ? (uint64_t)o.m32[p] : (m_u < 0xffffffffull ? m_u : 0xffffffffull);
+  // (memory ranks: the rank thresholds, monotone in scv/memory)
+  const uint64_t m = m32;
   const uint32_t nb = 1u << o.nb_log2;
   uint32_t b = (uint32_t)(m >> o.m_shift);
   b = b < nb ? b : nb - 1u;
@@ -203,8 +205,8 @@ __device__ __forceinline__ uint32_t order_bucket(const OrderMeta& o, uint64_t nu
 // Per workgroup: an LDS histogram of the buckets (each pod's rank inside its workgroup's
 // share of the bucket), then one global atomic per (workgroup, bucket): the share's base.
 __global__ __launch_bounds__(1024) void k_order_hist(OrderMeta o, const uint64_t* __restrict__ number,
-                                                     const uint64_t* __restrict__ m_u,
-                                                     const uint64_t* __restrict__ c_u,
+                                                     const uint32_t* __restrict__ m32,
+                                                     const uint32_t* __restrict__ c32,
                                                      const uint32_t* __restrict__ need_mem,
                                                      uint32_t n_pods, uint32_t* __restrict__ hist,
                                                      uint32_t* __restrict__ slot,
@@ -216,7 +218,7 @@ __global__ __launch_bounds__(1024) void k_order_hist(OrderMeta o, const uint64_t
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t b = 0, local = 0;
   if (p < n_pods) {
-    b = order_bucket(o, number[p], m_u[p], c_u[p], need_mem[p], p);
+    b = order_bucket(o, number[p], m32[p], c32[p], need_mem[p]);
     local = atomicAdd(&lh[b], 1u);
   }
   __syncthreads();
@@ -301,15 +303,15 @@ __global__ __launch_bounds__(kBlock) void k_order_scatter(PermTable t,
 }
 
 // t: the pod arrays (src = caller order, dst = sorted order); scratch: slot, bkt [P] u32.
-hipError_t launch_order_count(const OrderMeta& o, const uint64_t* number, const uint64_t* m_u,
-                              const uint64_t* c_u, const uint32_t* need_mem, uint32_t n_pods,
+hipError_t launch_order_count(const OrderMeta& o, const uint64_t* number, const uint32_t* m32,
+                              const uint32_t* c32, const uint32_t* need_mem, uint32_t n_pods,
                               uint32_t* hist, uint32_t* bstart, uint32_t* slot, uint32_t* bkt,
                               const PermTable& t, const uint32_t* pad, uint32_t n_pad,
                               uint64_t* zero, uint32_t n_zero, uint32_t* perm, hipStream_t s) {
   const uint32_t nbk = o.n_groups << o.nb_log2;
   if (o.nb_log2 > 10 || nbk > 16u * 1024u) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_order_hist, dim3((n_pods + 1023) / 1024), dim3(1024), nbk * 4, s, o,
-                     number, m_u, c_u, need_mem, n_pods, hist, slot, bkt);
+                     number, m32, c32, need_mem, n_pods, hist, slot, bkt);
   hipLaunchKernelGGL(k_order_scan, dim3(o.n_groups), dim3(1u << o.nb_log2), 0, s, o, hist,
                      bstart);
   hipLaunchKernelGGL(k_order_scatter, dim3((n_pods + n_pad + kBlock - 1) / kBlock), dim3(kBlock),
