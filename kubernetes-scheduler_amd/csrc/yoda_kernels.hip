@@ -2298,7 +2298,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // table above, the others after the ids), so the per-pod pass reads a lane's basic score as
   // in a uniform wave instead of computing its card terms per node
   constexpr uint32_t TT = (TOPK && !RK) ? (TKO > 8 ? 3u : 2u) : 1u;
-  constexpr uint32_t RECS = TAB, RCPS = TAB + kWave * REC, IDW = RCPS + 16 * kSets,
+  // (RCPS: the sets' reciprocals, then one more slot: the decoupled bound's, below)
+  constexpr uint32_t RECS = TAB, RCPS = TAB + kWave * REC, IDW = RCPS + 16 * (kSets + 1),
                      XTAB = IDW + kWave, LDSW = XTAB + (TT - 1) * TAB;
   auto row_base = [&](uint32_t q) -> uint32_t { return q == 0 ? 0u : XTAB + (q - 1u) * TAB; };
   __shared__ __attribute__((aligned(16))) uint32_t lds_all[kBlock / kWave][LDSW];
@@ -2398,8 +2399,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // k-th key (thrk: the min over active lanes of their own and the U list's k-th) is skipped.
   // Non-G uniform waves (one reciprocal set, not G's -- e.g. clock-labelled pods, whose feasible
   // nodes are one GPU model): the decoupled bounds kbdec_* (argmax, no memory ranks).
-  const bool dec = !TOPK && !RK && args.kbdec != nullptr && uni_max && !use_g;
+  // Several reciprocal sets: the largest reciprocal of each field over the active lanes (the
+  // smallest maxima) gives the highest score any of them can make, so the bound holds for all.
+  const bool dec = !TOPK && !RK && args.kbdec != nullptr && !use_g && act_mask != 0ull;
   const bool prune = args.kbub != nullptr && (use_g || dec);
+  if (dec) {  // the bound's reciprocals into the extra RCPS slot (RS at word 0, f64 at word 8)
+    RS d_bw = act ? sc.r_bw : (RS)0, d_core = act ? sc.r_core : (RS)0, d_pow = act ? sc.r_pow : (RS)0;
+    double d_free = act ? sc.r_free : 0.0, d_tot = act ? sc.r_tot : 0.0;
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      d_bw = fmax(d_bw, __shfl_xor(d_bw, o, kWave));
+      d_core = fmax(d_core, __shfl_xor(d_core, o, kWave));
+      d_pow = fmax(d_pow, __shfl_xor(d_pow, o, kWave));
+      d_free = fmax(d_free, __shfl_xor(d_free, o, kWave));
+      d_tot = fmax(d_tot, __shfl_xor(d_tot, o, kWave));
+    }
+    if (lane == 0) {
+      RS* r = reinterpret_cast<RS*>(lds + RCPS + 16 * kSets);
+      r[0] = d_bw;
+      r[1] = d_core;
+      r[2] = d_pow;
+      double* d = reinterpret_cast<double*>(lds + RCPS + 16 * kSets + 8);
+      d[0] = d_free;
+      d[1] = d_tot;
+    }
+  }
   constexpr uint32_t KBST = kbub_stride(K);
   // The block K1's seed: a score every live pod of the wave reaches on some node it passes,
   // under the G maxima; a pod's own maxima are never above G's (a max over fewer cards), so
@@ -2460,13 +2484,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         return __longlong_as_double((long long)((uint64_t)D[sum_index(b, w, DS)] |
                                                 ((uint64_t)D[sum_index(b, w + 1u, DS)] << 32)));
       };
+      const RS* r = reinterpret_cast<const RS*>(lds + RCPS + 16 * kSets);
+      const double* rd = reinterpret_cast<const double*>(lds + RCPS + 16 * kSets + 8);
       const uint32_t sh = card_shared_terms(D[sum_index(b, kDecBw, DS)], D[sum_index(b, kDecCk, DS)],
                                             D[sum_index(b, kDecCo, DS)], D[sum_index(b, kDecPw, DS)],
-                                            u_bw, u_core, u_pow);
+                                            r[0], r[1], r[2]);
       const double q = (double)D[sum_index(b, kDecQl + l_lo, DS)];
       // (+1: the f64 rounding of the products; the scores are integers)
-      return d64(kDecStat) + q * (double)sh + 3.0 * u_free * d64(kbdec_fl(l_lo)) +
-             u_tot * d64(kbdec_tl(l_lo)) + 1.0;
+      return d64(kDecStat) + q * (double)sh + 3.0 * rd[0] * d64(kbdec_fl(l_lo)) +
+             rd[1] * d64(kbdec_tl(l_lo)) + 1.0;
     }
     const uint32_t* U = args.kbub;
     uint32_t J = 0;
@@ -2957,7 +2983,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       tr[0] = t_start;
       tr[1] = wall_clock64();
       tr[2] = npart;
-      tr[3] = uni_max ? 1ull : 0ull;
+      // uniform maxima | G's << 1 | decoupled bounds << 2 | reciprocal sets << 4
+      tr[3] = (uni_max ? 1ull : 0ull) | (use_g ? 2ull : 0ull) | (dec ? 4ull : 0ull) |
+              ((unsigned long long)nsets << 4);
     }
   }
   if constexpr (TOPK) {

@@ -52,5 +52,13 @@ if os.environ.get("YODA_K2_TRACE"):
     print("heavy: npart mean", t[heavy, 2].mean(), "uni frac", t[heavy, 3].mean(),
           "start us", np.percentile((t[heavy, 0] - t0) * 10e-3, [0, 50, 100]))
     print("corr(dur, npart)", np.corrcoef(dur, t[:, 2])[0, 1])
+    cls = t[:, 3]
+    for name, sel in (("G", (cls & 2) != 0), ("dec uniform", ((cls & 4) != 0) & ((cls & 1) != 0)),
+                      ("dec several sets", ((cls & 4) != 0) & ((cls & 1) == 0)),
+                      ("unpruned", (cls & 6) == 0)):
+        if sel.any():
+            d = dur[sel]
+            print(f"{name}: {sel.sum()} wave-chunks, dur mean {d.mean():.1f} p99 {np.percentile(d, 99):.1f} "
+                  f"max {d.max():.1f} us, sum {d.sum():.0f} us, npart mean {t[sel, 2].mean():.1f}")
     ends = np.sort((t[:, 1] - t0) * 10e-3)
     print("end-time percentiles us", [round(float(np.percentile(ends, q)), 1) for q in (50, 90, 99, 99.9, 100)])
