@@ -1937,7 +1937,55 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
           if (ok) grp[g].push_back(i);
         }
         const size_t G = grp.size();
-        if (ok && G >= 2) {
+        // Inside a clock group the nodes go into blocks by their healthy frees: sorted on a
+        // Z-order key of hfs[0], hfs[1], hfs[3], hfs[7] (the frees that PodFitsMemory compares
+        // for 1, 2, 4, 8 GPUs; hfs[15] too at K = 16), so that a block's nodes are alike and its
+        // bounds decide it for a whole wave (tools: 16 % of (wave, block)s undecided on config 3
+        // with the blocks as uploaded, 4 % sorted); the sorted blocks are then taken in
+        // bit-reversed order, so that any run of consecutive blocks -- a node chunk -- still
+        // samples every free level (the chunks stay even).
+        static const bool zorder_env = YODA_KNOB("YODA_NODE_ZORDER", 1) != 0;  // A/B knob
+        if (ok && zorder_env) {
+          std::vector<uint32_t> hix;
+          for (uint32_t t = 1; t <= (uint32_t)K; t <<= 1) hix.push_back(t - 1);
+          const uint32_t nc = (uint32_t)hix.size(), bits = 64 / nc > 16 ? 16 : 64 / nc;
+          std::vector<std::pair<uint64_t, uint32_t>> zk;
+          for (auto& g : grp) {
+            uint32_t mx[8] = {};
+            for (uint32_t i : g)
+              for (uint32_t c = 0; c < nc; ++c)
+                mx[c] = std::max(mx[c], sum[(size_t)i * SW + kSumHfs + hix[c]]);
+            zk.clear();
+            for (uint32_t i : g) {
+              uint64_t z = 0;
+              for (uint32_t c = 0; c < nc; ++c) {
+                const uint64_t v = sum[(size_t)i * SW + kSumHfs + hix[c]];
+                const uint64_t qv = mx[c] ? std::min<uint64_t>((v << bits) / ((uint64_t)mx[c] + 1),
+                                                               (1ull << bits) - 1) : 0;
+                for (uint32_t b = 0; b < bits; ++b) z |= ((qv >> b) & 1ull) << (b * nc + c);
+              }
+              zk.emplace_back(z, i);
+            }
+            std::stable_sort(zk.begin(), zk.end(), [](const std::pair<uint64_t, uint32_t>& a,
+                                                      const std::pair<uint64_t, uint32_t>& b) {
+              return a.first < b.first;
+            });
+            const size_t nbg = g.size() / 64;
+            size_t lg = 0;
+            while (((size_t)1 << lg) < nbg) ++lg;
+            std::vector<uint32_t> out;
+            out.reserve(g.size());
+            for (size_t j = 0; j < ((size_t)1 << lg); ++j) {  // bit-reversed block order
+              size_t r = 0;
+              for (size_t b = 0; b < lg; ++b) r |= ((j >> b) & 1u) << (lg - 1 - b);
+              if (r < nbg)
+                for (size_t k = 0; k < 64; ++k) out.push_back(zk[r * 64 + k].second);
+            }
+            for (size_t k = nbg * 64; k < g.size(); ++k) out.push_back(zk[k].second);
+            g.swap(out);
+          }
+        }
+        if (ok && G >= 1) {
           std::vector<size_t> nb(G), done(G, 0);
           size_t total = 0;
           for (size_t g = 0; g < G; ++g) total += (nb[g] = grp[g].size() / 64);
