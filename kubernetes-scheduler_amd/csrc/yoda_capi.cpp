@@ -357,6 +357,7 @@ struct yoda_handle {
   DevBuf kbdec, kbdec_p;     // the non-G block bounds (yoda_layout.h kbdec_*) of both orders
   DevBuf kb_levels;          // the free levels of kbub's lv[] bounds (kKbLevels u32)
   bool seeds_valid = false;  // this run's block K1 cleared and writes the K2 pruning seeds
+  bool blk_fresh = false;    // this run cleared the whole block-list buffer (list, seeds, gbest)
   bool kb_levels_ok = false;  // built for the current snapshot
   bool kbub_dirty = true;   // a static score rose above the bounds' own: rebuild before use
   bool kbub_loose = false;  // static scores only fell since the build: valid, rebuilt for runs
@@ -827,10 +828,12 @@ PodParams pod_params(yoda_t* h) {
   static const bool dec_env = YODA_KNOB("YODA_KB_DEC", 1) != 0;
   static const bool gbest_env = YODA_KNOB("YODA_GBEST", 1) != 0;
   if (ub_ok && dec_env && h->kbdec.p) pp.kbdec = h->kbdec.as<uint32_t>();
-  if (seeds_env && ub_ok && h->seeds_valid && h->blk_valid && h->bm_sparse && pp.g.tab) {
+  {
     const size_t nw = (h->n_work + 63) / 64;
-    pp.seed = h->blk.as<uint64_t>() + nw * blk_row(h->n_nodes);
-    if (gbest_env) pp.gbest = pp.seed + nw;  // [n_work] after the seeds
+    uint64_t* sd = h->blk.as<uint64_t>() + nw * blk_row(h->n_nodes);
+    if (seeds_env && ub_ok && h->seeds_valid && h->blk_valid && h->bm_sparse && pp.g.tab)
+      pp.seed = sd;
+    if (gbest_env && ub_ok && h->blk_fresh) pp.gbest = sd + nw;  // [n_work] after the seeds
   }
   if (ub_ok && h->hot_ok) pp.hot = h->hot.as<uint64_t>();
   if (h->perm_run()) {
@@ -1224,6 +1227,7 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_m
   h->blk_valid = h->has_k1sum;
   h->bm_sparse = h->has_k1sum;  // the block K1 writes the sparse form
   h->seeds_valid = h->has_k1sum && mode == YODA_MODE_SCV;
+  h->blk_fresh = h->has_k1sum;  // (the memset below or the order scatter clears it whole)
   if (h->blk_valid && !h->blk_zeroed)  // (the list and the seeds after it)
     HIP_TRY(h, hipMemsetAsync(h->blk.p, 0, blk_words(h, P) * 8, h->stream));
   h->blk_zeroed = false;
@@ -1270,6 +1274,7 @@ int phase1_witness(yoda_t* h, uint64_t* maxima, uint32_t* counts, uint32_t* wit,
   h->bm_sparse = false;
   h->blk_valid = false;
   h->seeds_valid = false;
+  h->blk_fresh = false;
   if (N == 0) {
     HIP_TRY(h, hipMemsetAsync(counts, 0, 2 * (size_t)P * 4, h->stream));
     HIP_TRY(h, hipMemsetAsync(wit, 0, 6 * (size_t)P * 4, h->stream));
@@ -1299,7 +1304,8 @@ int phase1_witness(yoda_t* h, uint64_t* maxima, uint32_t* counts, uint32_t* wit,
     }
     h->bm_sparse = true;
     h->blk_valid = true;
-    HIP_TRY(h, hipMemsetAsync(h->blk.p, 0, (size_t)(P + 63) / 64 * blk_row(N) * 8, h->stream));
+    h->blk_fresh = true;
+    HIP_TRY(h, hipMemsetAsync(h->blk.p, 0, blk_words(h, P) * 8, h->stream));
     HIP_TRY(h, launch_k1_block_witness(h->K, h->nodes.as<unsigned char>(),
                                        h->k1sum.as<unsigned char>(), h->k2sum.as<unsigned char>(),
                                        h->kmix.as<unsigned char>(), N, chunk, C,
@@ -1508,10 +1514,14 @@ int topk_lists(yoda_t* h, uint32_t P, uint32_t KT, const uint32_t* d_counts) {
       if (Ct >= 8) Ct = (Ct + 7) / 8 * 8;
     }
     HIP_TRY(h, h->tk_s_part.ensure((size_t)Ct * P * KT * 8));
+    // the chunks' shared k-th keys start empty at every list pass (a mid-window refresh scores
+    // a later node state, whose keys are lower: the last pass's would be too high)
+    const PodParams pp = pod_params(h);
+    if (pp.gbest) HIP_TRY(h, hipMemsetAsync(pp.gbest, 0, (size_t)P * 8, h->stream));
     HIP_TRY(h, launch_k2_topk_block(h->K, h->nodes.as<unsigned char>(),
                                     h->k2sum.as<unsigned char>(),
                                     h->blk_valid ? h->blk.as<uint64_t>() : nullptr, blk_row(N), N,
-                                    cht, Ct, pod_params(h), h->rcp.as<double>(),
+                                    cht, Ct, pp, h->rcp.as<double>(),
                                      P, h->bitmask.as<uint64_t>(), bm_row(N),
                                     h->bs_ptr(), bs_row(N), d_counts,
                                     h->tk_s_part.as<uint64_t>(), ib, (int)KT, h->stream));

@@ -2401,7 +2401,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // nodes are one GPU model): the decoupled bounds kbdec_* (argmax, no memory ranks).
   // Several reciprocal sets: the largest reciprocal of each field over the active lanes (the
   // smallest maxima) gives the highest score any of them can make, so the bound holds for all.
-  const bool dec = !TOPK && !RK && args.kbdec != nullptr && !use_g && act_mask != 0ull;
+  const bool dec = !RK && args.kbdec != nullptr && !use_g && act_mask != 0ull;
   const bool prune = args.kbub != nullptr && (use_g || dec);
   if (dec) {  // the bound's reciprocals into the extra RCPS slot (RS at word 0, f64 at word 8)
     RS d_bw = act ? sc.r_bw : (RS)0, d_core = act ? sc.r_core : (RS)0, d_pow = act ? sc.r_pow : (RS)0;
@@ -2507,7 +2507,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     return ub;
   };
   auto pruned = [&](double ub) -> bool {
-    if constexpr (TOPK) {  // (ub: an integer-valued double >= 0)
+    if constexpr (TOPK) {  // (ub >= 0; a score is an integer <= floor(ub); beyond 2^52: none)
+      if (!(ub < 4503599627370496.0)) return false;
       return ((((uint64_t)ub) << ib) | (uint64_t)imax) <= thrk;
     } else {
       return ub < thr;
@@ -2926,6 +2927,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     thr = fmax(thr, __longlong_as_double(
                         (long long)uniform_u64((uint64_t)__double_as_longlong(lb))));
   };
+  // TOPK: thrk := the min over active lanes of their k-th key so far (own list or the U list:
+  // the merged list's k-th is at least either) -- and (gbest) the largest k-th key any chunk
+  // has published for the lane: a chunk whose own list has k keys >= x proves the lane's global
+  // k-th key >= x, so a block that cannot beat it holds none of the lane's top k
+  auto refresh_thrk = [&]() {
+    uint64_t kth = act ? (pl[TL - 1] > ul[TL - 1] ? pl[TL - 1] : ul[TL - 1]) : ~0ull;
+    if (args.gbest != nullptr && act) {
+      const unsigned long long g = args.gbest[p];
+      if (kth > g) atomicMax(args.gbest + p, (unsigned long long)kth);
+      kth = kth > g ? kth : g;
+    }
+    thrk = wave_min_u64(kth);
+  };
   if (blk) {
     // only the blocks K1 found a feasible pod of this wave in (bit b of word b/64)
     const uint64_t* bw = blk + (size_t)uniform_u32(p >> 6) * blk_stride;
@@ -2944,7 +2958,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       double ub_l = 0.0;
       if (prune && bits != 0ull) {
         ub_l = block_ub(min(base + lane, b1 - 1u));
-        if (!TOPK && args.gbest != nullptr) refresh_thr();  // (the other chunks' progress)
+        if (args.gbest != nullptr) {  // (the other chunks' progress)
+          if constexpr (TOPK) refresh_thrk(); else refresh_thr();
+        }
       }
       while (bits) {
         const uint32_t j = (uint32_t)__builtin_ctzll(bits);
@@ -2960,9 +2976,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
           }
         }
         block((base + j) << 6);
-        if (prune && worked && TOPK) {  // every active lane's k-th key so far
-          const uint64_t kth = act ? (pl[TL - 1] > ul[TL - 1] ? pl[TL - 1] : ul[TL - 1]) : ~0ull;
-          thrk = wave_min_u64(kth);
+        if (prune && worked && TOPK) {
+          refresh_thrk();
         } else if (prune && worked) {
           refresh_thr();
         }
@@ -4754,7 +4769,8 @@ hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigne
   dim3 grid((n_pods + kBlock - 1) / kBlock, C);
   const ScoreArgs a{pp.m_f, pp.c_f, pp.m_32, pp.c_32, rcp, counts, pp.g, pp.mix, pp.mt,
                     nullptr, pp.kbub, nullptr, pp.lpt_order, nullptr,
-                    pp.kbub ? pp.kb_levels : nullptr};
+                    pp.kbub ? pp.kb_levels : nullptr, pp.kbub ? pp.kbdec : nullptr,
+                    reinterpret_cast<unsigned long long*>(pp.gbest)};
 #define YODA_TOPKB(TKV, RKV, MIXV, Q32V)                                                        \
   YODA_K_SWITCH(K, hipLaunchKernelGGL((k2_block_n32<KK, false, TKV, RKV, MIXV, Q32V>), grid,      \
                                       dim3(kBlock), 0, s, nodes, sum2, n_nodes, chunk_nodes, a,   \
