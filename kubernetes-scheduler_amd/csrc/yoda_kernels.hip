@@ -2961,6 +2961,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
         if (args.gbest != nullptr) {  // (the other chunks' progress)
           if constexpr (TOPK) refresh_thrk(); else refresh_thr();
         }
+        // every listed block of the word below the threshold: skipped at once
+        const double wmax = wave_max_f64(((bits >> lane) & 1ull) ? ub_l : -1.0);
+        if (pruned(wmax)) {
+          if (STATS && !trace && lane == 0)
+            atomicAdd(stats + 13, (unsigned long long)__builtin_popcountll(bits));
+          bits = 0ull;
+        }
       }
       while (bits) {
         const uint32_t j = (uint32_t)__builtin_ctzll(bits);

@@ -6,3 +6,5 @@ timeout -k 10 600 bash tools/ab_run.sh 3 "r8|abl/cur.so|" "r4|abl/cur.so|YODA_CH
 cat $O/ab.txt
 timeout -k 10 400 python bench.py --workload greedy > $O/bench_greedy.json 2> $O/bench_greedy.err || { tail -20 $O/bench_greedy.err; exit 1; }
 cut -c1-1200 $O/bench_greedy.json
+timeout -k 10 450 bash tools/greedy_rank_probe.sh $O/rank8 0 1 || { tail -5 $O/rank8/rehearsal.err; exit 1; }
+cut -c1-400 $O/rank8/rehearsal.jsonl
