@@ -1516,7 +1516,13 @@ int topk_lists(yoda_t* h, uint32_t P, uint32_t KT, const uint32_t* d_counts) {
     HIP_TRY(h, h->tk_s_part.ensure((size_t)Ct * P * KT * 8));
     // the chunks' shared k-th keys start empty at every list pass (a mid-window refresh scores
     // a later node state, whose keys are lower: the last pass's would be too high)
-    const PodParams pp = pod_params(h);
+    PodParams pp = pod_params(h);
+    // (A/B knobs: YODA_TOPK_GBEST=0 / YODA_TOPK_DEC=0 -- the shared k-th keys / the non-G
+    // bounds in the list passes)
+    static const bool tk_gbest = YODA_KNOB("YODA_TOPK_GBEST", 1) != 0;
+    static const bool tk_dec = YODA_KNOB("YODA_TOPK_DEC", 1) != 0;
+    if (!tk_gbest) pp.gbest = nullptr;
+    if (!tk_dec) pp.kbdec = nullptr;
     if (pp.gbest) HIP_TRY(h, hipMemsetAsync(pp.gbest, 0, (size_t)P * 8, h->stream));
     HIP_TRY(h, launch_k2_topk_block(h->K, h->nodes.as<unsigned char>(),
                                     h->k2sum.as<unsigned char>(),

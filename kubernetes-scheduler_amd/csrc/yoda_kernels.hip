@@ -2962,8 +2962,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
           if constexpr (TOPK) refresh_thrk(); else refresh_thr();
         }
         // every listed block of the word below the threshold: skipped at once
+#ifndef YODA_K2_NO_WORDSKIP
         const double wmax = wave_max_f64(((bits >> lane) & 1ull) ? ub_l : -1.0);
         if (pruned(wmax)) {
+#else
+        if (false) {
+#endif
           if (STATS && !trace && lane == 0)
             atomicAdd(stats + 13, (unsigned long long)__builtin_popcountll(bits));
           bits = 0ull;
