@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <string>
 #include <vector>
@@ -1233,9 +1234,10 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_m
   h->blk_zeroed = false;
   const bool pr = h->perm_run();  // block-grouped node order (upload's node_perm)
   // current block bounds for the K1's seeds (loose ones -- static scores fell since the build --
-  // are upper bounds only); outside greedy batches they are rebuilt here rather than in phase 2
-  if (mode == YODA_MODE_SCV && (h->kbub_dirty || (h->kbub_loose && !h->greedy_active)) &&
-      h->path == Path::N32 && h->has_k2sum && h->g.tab)
+  // are upper bounds only): a private run (yoda_run) rebuilds them here rather than in phase 2;
+  // the other entry points (shards, greedy windows) keep phase 2's rule
+  if (mode == YODA_MODE_SCV && h->count_order && !h->greedy_active &&
+      (h->kbub_dirty || h->kbub_loose) && h->path == Path::N32 && h->has_k2sum && h->g.tab)
     HIP_TRY(h, build_block_ub(h));
   if (h->blksum_loose && !h->greedy_active) HIP_TRY(h, tighten_block_sums(h));
   HIP_TRY(h, launch_k1(h->K, h->path, h->nodes.as<unsigned char>(),
@@ -1519,8 +1521,10 @@ int topk_lists(yoda_t* h, uint32_t P, uint32_t KT, const uint32_t* d_counts) {
     PodParams pp = pod_params(h);
     // (A/B knobs: YODA_TOPK_GBEST=0 / YODA_TOPK_DEC=0 -- the shared k-th keys / the non-G
     // bounds in the list passes)
-    static const bool tk_gbest = YODA_KNOB("YODA_TOPK_GBEST", 1) != 0;
-    static const bool tk_dec = YODA_KNOB("YODA_TOPK_DEC", 1) != 0;
+    // (both off by default: the capacity windows ran 1.51 s without them, 1.58 s with them,
+    // profiles/r05/g)
+    static const bool tk_gbest = YODA_KNOB("YODA_TOPK_GBEST", 0) != 0;
+    static const bool tk_dec = YODA_KNOB("YODA_TOPK_DEC", 0) != 0;
     if (!tk_gbest) pp.gbest = nullptr;
     if (!tk_dec) pp.kbdec = nullptr;
     if (pp.gbest) HIP_TRY(h, hipMemsetAsync(pp.gbest, 0, (size_t)P * 8, h->stream));
@@ -5375,7 +5379,11 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
     return push(false);
   };
   h0->greedy_windows = h0->greedy_fallbacks = h0->greedy_restarts = h0->greedy_refreshes = 0;
-  rc = run();
+  {  // a greedy batch on every shard: its pushes keep the block bounds valid (no rebuilds)
+    std::vector<std::unique_ptr<GreedyScope>> scopes;
+    for (int i = 0; i < n; ++i) scopes.emplace_back(new GreedyScope(hs[i]));
+    rc = run();
+  }
   const int rr = push(true);  // restore the shards' original node state
   if (rc) return rc;
   if (rr) return rr;

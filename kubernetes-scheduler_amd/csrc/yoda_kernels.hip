@@ -2962,7 +2962,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
           if constexpr (TOPK) refresh_thrk(); else refresh_thr();
         }
         // every listed block of the word below the threshold: skipped at once
-#ifndef YODA_K2_NO_WORDSKIP
+#ifdef YODA_K2_WORDSKIP  // (A/B: off -- K2 0.218 vs 0.205 ms without, profiles/r05/g)
         const double wmax = wave_max_f64(((bits >> lane) & 1ull) ? ub_l : -1.0);
         if (pruned(wmax)) {
 #else
