@@ -38,7 +38,8 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uint32_t nw,
                           uint64_t* maxima, uint32_t* counts, double* rcp,
                           const MemTab& mt, hipStream_t s,
-                          uint32_t* lpt_w = nullptr, uint32_t* lpt_order = nullptr);
+                          uint32_t* lpt_w = nullptr, uint32_t* lpt_order = nullptr,
+                          const uint64_t* cmask = nullptr);
 hipError_t launch_mem_rank(const uint64_t* m_u, uint32_t n_pods, const MemTab& mt, uint32_t* m32,
                            hipStream_t s);
 hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp,
@@ -71,7 +72,7 @@ hipError_t launch_rows_transpose(const int64_t* in, uint32_t n_nodes, uint32_t n
                                  int64_t* out, hipStream_t s);
 hipError_t launch_reduce2(const Partials& part, uint32_t C, uint32_t n_pods, bool is_f64,
                           uint32_t node_offset, int64_t* best, uint32_t* idx, uint32_t* ties,
-                          int64_t* low, hipStream_t s);
+                          int64_t* low, hipStream_t s, const uint64_t* cmask = nullptr);
 hipError_t launch_merge_prepare(const int64_t* best_global, const int64_t* best_local,
                                 uint32_t n_pods, uint32_t* idx, uint32_t* ties, hipStream_t s);
 hipError_t launch_fill_diskio_state(uint32_t n_pods, uint32_t n_nodes, uint64_t* maxima,
@@ -682,6 +683,9 @@ static uint32_t diag_env(const char* name, uint32_t dflt) {
 }
 
 constexpr uint32_t kMinChunkNodes = 1536;
+// the reduces read the chunk partials one thread per pod up to this many chunks (the chunk
+// masks' limit too); beyond, one wave per pod (yoda_kernels.hip kWaveReduceChunks)
+constexpr uint32_t kPlainReduceChunks = 48;
 
 void plan_chunks_for(uint32_t cap, uint32_t rounds, uint32_t n_pods, uint32_t n_nodes,
                      uint32_t* C_out, uint32_t* chunk_out) {
@@ -755,7 +759,7 @@ void plan_chunks(yoda_t* h, int mode, uint32_t n_pods, uint32_t n_nodes) {
 // u64 words of the block-list buffer: the list, the seeds, the shared best (ensure_state)
 size_t blk_words(const yoda_t* h, uint32_t P) {
   const size_t nw = (P + 63) / 64;
-  return nw * (blk_row(h->n_nodes) + 1) + P;
+  return nw * (blk_row(h->n_nodes) + 1) + P + 2 * nw;  // + the two chunk masks per wave
 }
 
 int ensure_state(yoda_t* h, uint32_t P) {
@@ -835,6 +839,13 @@ PodParams pod_params(yoda_t* h) {
     if (seeds_env && ub_ok && h->seeds_valid && h->blk_valid && h->bm_sparse && pp.g.tab)
       pp.seed = sd;
     if (gbest_env && ub_ok && h->blk_fresh) pp.gbest = sd + nw;  // [n_work] after the seeds
+    // the chunk masks after the shared best (A/B knob YODA_CMASK=0: every chunk writes)
+    static const bool cmask_env = YODA_KNOB("YODA_CMASK", 1) != 0;
+    uint64_t* cm = sd + nw + h->n_work;
+    if (cmask_env && h->blk_fresh && h->path == Path::N32) {
+      if (h->has_k1sum && h->C1 <= kPlainReduceChunks && h->k1_sub == 1) pp.cmask1 = cm;
+      if (h->has_k2sum && h->C2 <= kPlainReduceChunks) pp.cmask2 = cm + nw;
+    }
   }
   if (ub_ok && h->hot_ok) pp.hot = h->hot.as<uint64_t>();
   if (h->perm_run()) {
@@ -1260,7 +1271,8 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_m
                             counts,
                             rcp ? h->rcp.as<double>() : nullptr, pod_params(h).mt, h->stream,
                             h->lpt_active ? h->lpt_w.as<uint32_t>() : nullptr,
-                            h->lpt_active ? h->lpt_order.as<uint32_t>() : nullptr));
+                            h->lpt_active ? h->lpt_order.as<uint32_t>() : nullptr,
+                            h->has_k1sum ? pod_params(h).cmask1 : nullptr));
   h->lpt_sorted = h->lpt_active;  // (the order of this run's pod blocks, for phase 2)
   h->rcp_ready = rcp;
   return YODA_OK;
@@ -1332,6 +1344,7 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
            uint32_t* idx, uint32_t* ties, int64_t* low, int64_t* rows = nullptr) {
   const uint32_t P = h->n_work;  // sorted positions of this run
   if (P == 0) return YODA_OK;
+  const uint64_t* cmask2 = nullptr;
   if (h->n_nodes == 0) {
     std::vector<int64_t> neg(P, -1), big(P, INT64_MAX);
     std::vector<uint32_t> none(P, 0xffffffffu);
@@ -1389,6 +1402,8 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
     HIP_TRY(h, launch_k2b_rows(h->nodes_b.as<NodeRecB>(), h->n_nodes, pod_params(h), P, part,
                                rows, h->stream));
   } else {
+    // the block argmax K2 (N32 with summaries) marks the chunks it wrote (PodParams::cmask2)
+    if (h->path == Path::N32 && h->has_k2sum && !rows) cmask2 = pod_params(h).cmask2;
     HIP_TRY(h, launch_k2(h->K, h->path, h->nodes.as<unsigned char>(),
                          h->has_k2sum ? (h->perm_run() ? h->k2sum_p : h->k2sum)
                                             .as<unsigned char>()
@@ -1402,6 +1417,9 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
     if (h->class_stats && h->has_k2sum && !rows)
       h->stats_pairs2 += (uint64_t)(P + 63) / 64 * h->n_nodes;
     is_f64 = !h->generic;
+    // the shared best and the chunk masks hold this K2's scores: a later phase 2 on the same
+    // phase 1 (other maxima) must not read them
+    if (!rows) h->blk_fresh = false;
   }
   if (e1) {
     HIP_TRY(h, hipEventRecord(e1, h->stream));
@@ -1412,7 +1430,7 @@ int phase2(yoda_t* h, int mode, const uint64_t* maxima, const uint32_t* counts, 
   Partials pr = part;
   if (mode == YODA_MODE_SCV && h->path == Path::N32 && h->has_k2sum && !rows) pr.low_f = nullptr;
   HIP_TRY(h, launch_reduce2(pr, C2, P, is_f64, h->node_offset, best, idx, ties, low,
-                            h->stream));
+                            h->stream, cmask2));
   return YODA_OK;
 }
 

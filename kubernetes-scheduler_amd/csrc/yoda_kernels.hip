@@ -622,7 +622,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     const uint32_t* __restrict__ bsm = nullptr, uint32_t nwords = kNarrowWords,
     uint32_t* __restrict__ wts = nullptr, const uint32_t* __restrict__ gtab = nullptr,
     const uint32_t* __restrict__ kbub = nullptr, const uint32_t* __restrict__ levels = nullptr,
-    unsigned long long* __restrict__ seed_out = nullptr) {
+    unsigned long long* __restrict__ seed_out = nullptr,
+    unsigned long long* __restrict__ cmask = nullptr) {
   static_assert(!(WIT && MIX), "the witness K1 serves one-model snapshots");
   static_assert(SUB == 1 || (SUB == kBlock / kWave && !WIT), "SUB: 1, or one pod wave per workgroup");
   constexpr uint32_t SS = k1sum_stride(K);
@@ -1261,6 +1262,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   a_free = wave_max_u32(a_free);
   a_pw = wave_max_u32(a_pw);
   a_tot = wave_max_u32(a_tot);
+  if (SUB == 1 && cmask != nullptr) {
+    // no pod of the wave has a feasible node in the chunk: its partials are the identity
+    // (maxima at the floor, counts 0) -- nothing written, and k_reduce1 skips the chunk
+    if (ballot(live && nf + nf_all != 0u) == 0ull) return;
+    if (lane == 0) atomicOr(cmask + (p >> 6), 1ull << chunk);
+  }
   if (SUB == 1 && !live) return;  // (lane 0 is live: the live lanes are a prefix)
   mx[kMaxBw] = max(mx[kMaxBw], a_bw);
   mx[kMaxClock] = max(mx[kMaxClock], a_ck);
@@ -1456,7 +1463,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__
                                                     double* __restrict__ rcp,
                                                     MemTab mt, uint32_t nw,
                                                     uint32_t* __restrict__ lpt_w = nullptr,
-                                                    uint32_t* __restrict__ lpt_order = nullptr) {
+                                                    uint32_t* __restrict__ lpt_order = nullptr,
+                                                    const unsigned long long* __restrict__ cmask = nullptr) {
   if (lpt_w != nullptr && blockIdx.x == gridDim.x - 1) {  // the extra block: the K2's order
     __shared__ __attribute__((aligned(16))) uint32_t w[kLptMax];
     if (blockIdx.y == 0)
@@ -1472,9 +1480,14 @@ __global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__
     if constexpr (NARROW) {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(pmax) + (size_t)f * C * n_pods + p;
       uint32_t m32 = narrow_floor((int)f, nw);  // floor 1 (collection.go:31-38)
+      if (cmask != nullptr) {  // only the chunks that wrote (the wave's bits; uniform loop)
+        for (uint64_t bits = cmask[p >> 6]; bits != 0ull; bits &= bits - 1ull)
+          m32 = narrow_max(m32, src[(size_t)__builtin_ctzll(bits) * n_pods], (int)f, nw);
+      } else {
 #pragma unroll 8
-      for (uint32_t c = 0; c < C; ++c)
-        m32 = narrow_max(m32, src[(size_t)c * n_pods], (int)f, nw);
+        for (uint32_t c = 0; c < C; ++c)
+          m32 = narrow_max(m32, src[(size_t)c * n_pods], (int)f, nw);
+      }
       narrow_store(m32, (int)f, n_pods, p, maxima, mt, nw);
       if (rcp && nw != kNarrowWords) {
         store_rcp((int)f, maxima[(size_t)f * n_pods + p], n_pods, p, rcp);
@@ -1496,8 +1509,13 @@ __global__ __launch_bounds__(kBlock) void k_reduce1(const uint64_t* __restrict__
   } else {
     const uint32_t* src = pcnt + (size_t)(f - NF) * C * n_pods + p;
     uint32_t s = 0;
+    if (cmask != nullptr) {
+      for (uint64_t bits = cmask[p >> 6]; bits != 0ull; bits &= bits - 1ull)
+        s += src[(size_t)__builtin_ctzll(bits) * n_pods];
+    } else {
 #pragma unroll 8
-    for (uint32_t c = 0; c < C; ++c) s += src[(size_t)c * n_pods];
+      for (uint32_t c = 0; c < C; ++c) s += src[(size_t)c * n_pods];
+    }
     counts[(size_t)(f - NF) * n_pods + p] = s;
   }
 }
@@ -1996,6 +2014,8 @@ struct ScoreArgs {
   // the non-G block bounds (kbdec_*) and the per-pod best shared across the chunks (PodParams)
   const uint32_t* kbdec = nullptr;
   unsigned long long* gbest = nullptr;
+  // the argmax block K2's chunk mask (PodParams::cmask2; nullptr: every chunk writes)
+  unsigned long long* cmask = nullptr;
 };
 
 template <Path P>
@@ -3042,7 +3062,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     wi = min(wi, (uint32_t)__shfl_xor((int)wi, o, kWave));
     wt += (uint32_t)__shfl_xor((int)wt, o, kWave);
   }
-  if (!live) return;
   // the per-pod nodes' state (exact: every score < 2^53), then the U nodes
   double best = rties > 0 ? (double)rbest : -1.0;
   uint32_t idx = ridx, ties = rties;
@@ -3056,6 +3075,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       ties += wt;
     }
   }
+  if (args.cmask != nullptr) {
+    // no pod of the wave has a node here that can be its pick or a tie (none at all, or below
+    // a score another chunk already reached: gbest): nothing written, k_reduce2 skips the chunk
+    bool useful = live && act && best >= 0.0;
+    if (useful && args.gbest != nullptr)
+      useful = (unsigned long long)best + 1ull >= args.gbest[p];
+    if (ballot(useful) == 0ull) return;
+    if (lane == 0) atomicOr(args.cmask + (p >> 6), 1ull << chunk);
+  }
+  if (!live) return;
   const size_t o = (size_t)chunk * n_pods + p;
   pbest[o] = best;
   pidx[o] = idx;
@@ -4111,15 +4140,24 @@ __global__ __launch_bounds__(kBlock) void k_reduce2(const double* __restrict__ p
                                                     int64_t* __restrict__ best_out,
                                                     uint32_t* __restrict__ idx_out,
                                                     uint32_t* __restrict__ ties_out,
-                                                    int64_t* __restrict__ low_out) {
+                                                    int64_t* __restrict__ low_out,
+                                                    const unsigned long long* __restrict__ cmask = nullptr) {
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (p >= n_pods) return;
   int64_t best = -1, low = kI64Max;
   uint32_t idx = 0xffffffffu, ties = 0;
+  // (cmask: only the chunks whose bit is set wrote this run -- the wave's bits, a uniform loop)
+  uint64_t bits = cmask != nullptr ? cmask[p >> 6] : 0ull;
+  const uint32_t CN = cmask != nullptr ? (uint32_t)__builtin_popcountll(bits) : C;
   // branch-free, unrolled: every chunk's four words are loaded up front (several chunks in
   // flight), then folded with selects; equal bests keep the earlier chunk's (lower) index
 #pragma unroll 4
-  for (uint32_t c = 0; c < C; ++c) {
+  for (uint32_t k = 0; k < CN; ++k) {
+    uint32_t c = k;
+    if (cmask != nullptr) {
+      c = (uint32_t)__builtin_ctzll(bits);
+      bits &= bits - 1ull;
+    }
     const size_t o = (size_t)c * n_pods + p;
     int64_t b, l;
     if (is_f64) {
@@ -4523,7 +4561,8 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                                       bs, bs_stride, blk, blk_stride, stats, nullptr, pp.bsum,   \
                                       pp.nwords, pp.lpt_w, pp.seed ? pp.g.tab : nullptr,         \
                                       pp.kbub_exact ? pp.kbub : nullptr, pp.kb_levels,           \
-                                      reinterpret_cast<unsigned long long*>(pp.seed)))
+                                      reinterpret_cast<unsigned long long*>(pp.seed),          \
+                                      reinterpret_cast<unsigned long long*>(pp.cmask1)))
         if (sub == 1u) {
           if (stats) YODA_K1B(KK, true)
           else if (pp.one_model) YODA_K1B(KK, false, false)
@@ -4603,7 +4642,8 @@ hipError_t launch_lpt_order(uint32_t* wts, uint32_t n_pods, uint32_t* order, hip
 hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uint32_t nw,
                           uint64_t* maxima, uint32_t* counts, double* rcp,
                           const MemTab& mt, hipStream_t s, uint32_t* lpt_w,
-                          uint32_t* lpt_order) {
+                          uint32_t* lpt_order, const uint64_t* cmask) {
+  if (cmask != nullptr && (C > kWaveReduceChunks || !nw)) return hipErrorInvalidValue;
   const bool lpt_apart = lpt_w != nullptr && (C > kWaveReduceChunks || !nw);
   if (lpt_apart) {
     const hipError_t e = launch_lpt_order(lpt_w, n_pods, lpt_order, s);
@@ -4640,7 +4680,8 @@ hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uin
     if (nw)
       hipLaunchKernelGGL(k_reduce1<true>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
                          n_pods, maxima, counts, rcp, mt, nw, lpt ? lpt_w : nullptr,
-                         lpt ? lpt_order : nullptr);
+                         lpt ? lpt_order : nullptr,
+                         reinterpret_cast<const unsigned long long*>(cmask));
     else
       hipLaunchKernelGGL(k_reduce1<false>, grid, dim3(kBlock), 0, s, part.max_u, part.cnt, C,
                          n_pods, maxima, counts, rcp, mt, 0u);
@@ -4680,7 +4721,9 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
                     OUT == OUT_ARGMAX ? reinterpret_cast<const unsigned long long*>(pp.seed) : nullptr,
                     OUT == OUT_ARGMAX && pp.kbub ? pp.kb_levels : nullptr,
                     OUT == OUT_ARGMAX && pp.kbub ? pp.kbdec : nullptr,
-                    OUT == OUT_ARGMAX ? reinterpret_cast<unsigned long long*>(pp.gbest) : nullptr};
+                    OUT == OUT_ARGMAX ? reinterpret_cast<unsigned long long*>(pp.gbest) : nullptr,
+                    OUT == OUT_ARGMAX && sum2 ? reinterpret_cast<unsigned long long*>(pp.cmask2)
+                                              : nullptr};
   const MaskSrc ms{bm, bs, bm_stride, bs_stride, blk, blk_stride};
   if (bs && !blk) return hipErrorInvalidValue;  // sparse masks are read through their block list
   switch (path) {
@@ -5029,7 +5072,8 @@ hipError_t launch_rows_transpose(const int64_t* in, uint32_t n_nodes, uint32_t n
 
 hipError_t launch_reduce2(const Partials& part, uint32_t C, uint32_t n_pods, bool is_f64,
                           uint32_t node_offset, int64_t* best, uint32_t* idx, uint32_t* ties,
-                          int64_t* low, hipStream_t s) {
+                          int64_t* low, hipStream_t s, const uint64_t* cmask) {
+  if (cmask != nullptr && C > kWaveReduceChunks) return hipErrorInvalidValue;
   if (C > kWaveReduceChunks) {
     hipLaunchKernelGGL(k_reduce2_wave, dim3(n_pods), dim3(kWave), 0, s, part.best_f, part.best_i,
                        part.idx, part.ties, part.low_f, part.low_i, C, n_pods, is_f64 ? 1 : 0,
@@ -5038,7 +5082,8 @@ hipError_t launch_reduce2(const Partials& part, uint32_t C, uint32_t n_pods, boo
   }
   hipLaunchKernelGGL(k_reduce2, pod_grid(n_pods), dim3(kBlock), 0, s, part.best_f, part.best_i,
                      part.idx, part.ties, part.low_f, part.low_i, C, n_pods, is_f64 ? 1 : 0,
-                     node_offset, best, idx, ties, low);
+                     node_offset, best, idx, ties, low,
+                     reinterpret_cast<const unsigned long long*>(cmask));
   return hipGetLastError();
 }
 

@@ -394,6 +394,11 @@ struct PodParams {
   // with the block list; nullptr: none)
   const uint32_t* kbdec = nullptr;
   uint64_t* gbest = nullptr;
+  // per pod wave a bit per node chunk that wrote its partials (K1: some pod has a feasible
+  // node there; the argmax K2: some pod may hold its pick or a tie there): the reduces read
+  // only those chunks (<= 48 chunks, the plain reduces; nullptr: every chunk writes)
+  uint64_t* cmask1 = nullptr;
+  uint64_t* cmask2 = nullptr;
 };
 
 // Per-pod state produced between kernels (length P each unless noted).
