@@ -606,7 +606,7 @@ __device__ __forceinline__ uint32_t narrow_floor(int w, uint32_t nw) {  // floor
 // tasks -- 24 B per (pod, chunk) written once per chunk instead of once per quarter.
 template <int K, bool STATS, bool MIX = true, bool WIT = false, int SUB = 1>
 #ifndef YODA_K1_WAVES
-#define YODA_K1_WAVES 7
+#define YODA_K1_WAVES 6  // (7: 9 VGPRs spilled, ~90 MB of scratch writes per launch; r05j)
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 : (K >= 16 ? 5 : YODA_K1_WAVES)))) void k1_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum,
@@ -2931,6 +2931,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // thr := max(thr, the min over active lanes of their best so far -- this chunk's nodes', the
   // U nodes', and (gbest) every other chunk's, which this one publishes its own to); each
   // value is a score the lane reaches on a feasible node, so thr stays below every lane's best
+  unsigned long long gpub = 0ull;  // the largest value this lane published to gbest
   auto refresh_thr = [&]() {
     double wu = ubest;
 #pragma unroll
@@ -2939,7 +2940,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     if (args.gbest != nullptr && act) {  // (score + 1; 0: none yet)
       const unsigned long long g = args.gbest[p];
       const unsigned long long mine = lb >= 0.0 ? (unsigned long long)lb + 1ull : 0ull;
+      // (published once per value: the load may see a stale line, not this lane's own atomic)
+#ifndef YODA_GBEST_REPUB
+      if (mine > g && mine > gpub) {
+        atomicMax(args.gbest + p, mine);
+        gpub = mine;
+      }
+#else
       if (mine > g) atomicMax(args.gbest + p, mine);
+#endif
       lb = fmax(lb, (double)g - 1.0);
     }
 #pragma unroll
