@@ -398,6 +398,11 @@ struct yoda_handle {
   DevBuf pod_blob;
   PinnedBuf pod_stage;
   hipEvent_t stage_event = nullptr;
+  // the deferred pod arrays' copy of a private run goes on a copy stream of its own, alongside
+  // the run's kernels (pods_complete_async); rest_event joins it back into `stream`
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t core_event = nullptr, rest_event = nullptr;
+  bool rest_join = false;
   hipEvent_t switch_event = nullptr;  // yoda_set_stream: the old stream's work, waited on
   bool stage_pending = false;
   size_t pod_off[kPodArrays] = {};
@@ -541,6 +546,9 @@ struct yoda_handle {
     if (stage_event) (void)hipEventDestroy(stage_event);
     if (switch_event) (void)hipEventDestroy(switch_event);
     if (upd_event) (void)hipEventDestroy(upd_event);
+    if (core_event) (void)hipEventDestroy(core_event);
+    if (rest_event) (void)hipEventDestroy(rest_event);
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 };
@@ -882,7 +890,39 @@ Partials partials(yoda_t* h) {
 
 // The deferred part of the last pod upload (the arrays past kPodCoreArrays) to the device, on
 // the handle's stream, from the pinned staging copy (reused only after stage_event).
+// Make `stream` wait for a copy pods_complete_async issued (every reader of the deferred
+// arrays comes through pods_complete).
+int pods_join(yoda_t* h) {
+  if (!h->rest_join) return YODA_OK;
+  h->rest_join = false;
+  HIP_TRY(h, hipStreamWaitEvent(h->stream, h->rest_event, 0));
+  return YODA_OK;
+}
+
+// The deferred part on the copy stream, after what `stream` holds so far (the core copy of
+// the upload: the run's kernels do not wait for it); pods_join after the run's launches.
+int pods_complete_async(yoda_t* h) {
+  if (h->pod_rest_bytes == 0) return YODA_OK;
+  if (!h->copy_stream) {
+    HIP_TRY(h, hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
+    HIP_TRY(h, hipEventCreateWithFlags(&h->core_event, hipEventDisableTiming));
+    HIP_TRY(h, hipEventCreateWithFlags(&h->rest_event, hipEventDisableTiming));
+  }
+  unsigned char* st = static_cast<unsigned char*>(h->pod_stage.p);
+  HIP_TRY(h, hipEventRecord(h->core_event, h->stream));
+  HIP_TRY(h, hipStreamWaitEvent(h->copy_stream, h->core_event, 0));
+  HIP_TRY(h, hipMemcpyAsync(h->pod_blob.as<unsigned char>() + h->pod_rest_off, st + h->pod_rest_off,
+                            h->pod_rest_bytes, hipMemcpyHostToDevice, h->copy_stream));
+  HIP_TRY(h, hipEventRecord(h->stage_event, h->copy_stream));
+  HIP_TRY(h, hipEventRecord(h->rest_event, h->copy_stream));
+  h->stage_pending = true;
+  h->rest_join = true;
+  h->pod_rest_bytes = 0;
+  return YODA_OK;
+}
+
 int pods_complete(yoda_t* h) {
+  if (int rc = pods_join(h)) return rc;
   if (h->pod_rest_bytes == 0) return YODA_OK;
   unsigned char* st = static_cast<unsigned char*>(h->pod_stage.p);
   HIP_TRY(h, hipMemcpyAsync(h->pod_blob.as<unsigned char>() + h->pod_rest_off, st + h->pod_rest_off,
@@ -2719,6 +2759,9 @@ int yoda_run(yoda_t* h, int mode, uint32_t flags) {
   if (rc) return rc;
   const bool defer = fast && h->count_order;
   if (!defer && (rc = pods_complete(h))) return rc;
+  // (YODA_SIDE_COPY=0, A/B knob: the deferred copy on the run's stream after its kernels)
+  static const bool side = YODA_KNOB("YODA_SIDE_COPY", 1) != 0;
+  if (defer && side && (rc = pods_complete_async(h))) return rc;
   try {
     if ((rc = order_pods(h, mode))) return rc;
     if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), true)))
@@ -2731,7 +2774,7 @@ int yoda_run(yoda_t* h, int mode, uint32_t flags) {
                        h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(),
                        false)))
       return rc;
-    if (defer && (rc = pods_complete(h))) return rc;
+    if (defer && (rc = pods_complete(h))) return rc;  // (side copy: the join)
     h->ran = true;
     h->ran_bitmask = mode == YODA_MODE_SCV && (flags & YODA_RUN_BITMASK);
     h->last_mode = mode;
