@@ -420,6 +420,42 @@ func CommUniqueID() ([]byte, error) {
 	return id, nil
 }
 
+// DeviceBusID is the PCI bus id of this handle's GPU (yoda_device_bus_id).  Ranks exchange
+// it with the communicator id, out of band, and call CheckDevices before CommInit.
+func (g *Handle) DeviceBusID() (string, error) {
+	buf := make([]byte, C.YODA_BUS_ID_BYTES)
+	if err := check(g.h, C.yoda_device_bus_id(g.h, (*C.char)(unsafe.Pointer(&buf[0])),
+		C.int(len(buf))), "yoda_device_bus_id"); err != nil {
+		return "", err
+	}
+	return C.GoString((*C.char)(unsafe.Pointer(&buf[0]))), nil
+}
+
+// CheckDevices takes every rank's DeviceBusID (rank order) and fails, naming the first pair,
+// when two ranks would share one GPU (YODA_ERR_SAME_DEVICE: RCCL itself only reports an
+// "invalid usage").  Host only.
+func CheckDevices(busIDs []string) error {
+	if len(busIDs) == 0 {
+		return nil
+	}
+	stride := int(C.YODA_BUS_ID_BYTES)
+	flat := make([]byte, stride*len(busIDs))
+	for r, id := range busIDs {
+		if len(id) >= stride {
+			return fmt.Errorf("yodagpu: bus id of rank %d too long", r)
+		}
+		copy(flat[r*stride:], id)
+	}
+	var a, b C.int
+	rc := C.yoda_comm_check_devices((*C.char)(unsafe.Pointer(&flat[0])), C.int(len(busIDs)),
+		C.int(stride), &a, &b)
+	if rc == C.YODA_ERR_SAME_DEVICE {
+		return fmt.Errorf("yodagpu: ranks %d and %d are on the same GPU (%s)", int(a), int(b),
+			busIDs[a])
+	}
+	return check(nil, rc, "yoda_comm_check_devices")
+}
+
 // CommInit joins this handle (one GPU holding the node shard uploaded with UploadShard) to the
 // communicator of `world` ranks; collective: every rank calls it.
 func (g *Handle) CommInit(id []byte, rank, world int) error {
