@@ -403,6 +403,9 @@ struct yoda_handle {
   hipStream_t copy_stream = nullptr;
   hipEvent_t core_event = nullptr, rest_event = nullptr;
   bool rest_join = false;
+  // the staged f64 thresholds and Mode B weights of the last upload are still to be written
+  // (pods_pack_rest: derived from the staged u64 ones, after a run's kernel launches)
+  bool rest_lazy = false;
   hipEvent_t switch_event = nullptr;  // yoda_set_stream: the old stream's work, waited on
   bool stage_pending = false;
   size_t pod_off[kPodArrays] = {};
@@ -890,6 +893,34 @@ Partials partials(yoda_t* h) {
 
 // The deferred part of the last pod upload (the arrays past kPodCoreArrays) to the device, on
 // the handle's stream, from the pinned staging copy (reused only after stage_event).
+constexpr uint64_t kPodF64Clamp = 1ull << 53;  // > every F64-path card field (<= 2^44)
+
+// The staged arrays an upload left for later (rest_lazy): mf / cf from the staged mu / cu,
+// alpha = beta = 0 (a batch without Mode B inputs).  Host work on the pool; a private run
+// does it after launching its kernels.
+void pods_pack_rest(yoda_t* h) {
+  if (!h->rest_lazy) return;
+  h->rest_lazy = false;
+  const uint32_t P = h->n_pods;
+  unsigned char* st = static_cast<unsigned char*>(h->pod_stage.p);
+  const uint64_t* mu = reinterpret_cast<const uint64_t*>(st + h->pod_off[kPodMU]);
+  const uint64_t* cu = reinterpret_cast<const uint64_t*>(st + h->pod_off[kPodCU]);
+  double* mf = reinterpret_cast<double*>(st + h->pod_off[kPodMF]);
+  double* cf = reinterpret_cast<double*>(st + h->pod_off[kPodCF]);
+  double* al = reinterpret_cast<double*>(st + h->pod_off[kPodAlpha]);
+  double* be = reinterpret_cast<double*>(st + h->pod_off[kPodBeta]);
+  const uint32_t n_thr = std::min<uint32_t>(HostPool::get().size(), std::max(1u, P / 4096));
+  const uint32_t per = (P + n_thr - 1) / n_thr;
+  auto range = [&](uint32_t t) {
+    for (uint32_t p = std::min(P, t * per), e = std::min(P, (t + 1) * per); p < e; ++p) {
+      mf[p] = (double)std::min(mu[p], kPodF64Clamp);
+      cf[p] = (double)std::min(cu[p], kPodF64Clamp);
+      al[p] = be[p] = 0.0;
+    }
+  };
+  if (n_thr > 1) HostPool::get().run(n_thr, range); else range(0);
+}
+
 // Make `stream` wait for a copy pods_complete_async issued (every reader of the deferred
 // arrays comes through pods_complete).
 int pods_join(yoda_t* h) {
@@ -901,15 +932,20 @@ int pods_join(yoda_t* h) {
 
 // The deferred part on the copy stream, after what `stream` holds so far (the core copy of
 // the upload: the run's kernels do not wait for it); pods_join after the run's launches.
+int ensure_copy_stream(yoda_t* h) {
+  if (h->copy_stream) return YODA_OK;
+  HIP_TRY(h, hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
+  HIP_TRY(h, hipEventCreateWithFlags(&h->core_event, hipEventDisableTiming));
+  HIP_TRY(h, hipEventCreateWithFlags(&h->rest_event, hipEventDisableTiming));
+  return YODA_OK;
+}
+
 int pods_complete_async(yoda_t* h) {
   if (h->pod_rest_bytes == 0) return YODA_OK;
-  if (!h->copy_stream) {
-    HIP_TRY(h, hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
-    HIP_TRY(h, hipEventCreateWithFlags(&h->core_event, hipEventDisableTiming));
-    HIP_TRY(h, hipEventCreateWithFlags(&h->rest_event, hipEventDisableTiming));
-  }
+  if (!h->copy_stream) return fail(h, YODA_ERR_STATE, "pods_complete_async: no copy stream");
+  pods_pack_rest(h);
   unsigned char* st = static_cast<unsigned char*>(h->pod_stage.p);
-  HIP_TRY(h, hipEventRecord(h->core_event, h->stream));
+  // (core_event: recorded after the upload's copy -- the run's kernels are queued since)
   HIP_TRY(h, hipStreamWaitEvent(h->copy_stream, h->core_event, 0));
   HIP_TRY(h, hipMemcpyAsync(h->pod_blob.as<unsigned char>() + h->pod_rest_off, st + h->pod_rest_off,
                             h->pod_rest_bytes, hipMemcpyHostToDevice, h->copy_stream));
@@ -924,6 +960,7 @@ int pods_complete_async(yoda_t* h) {
 int pods_complete(yoda_t* h) {
   if (int rc = pods_join(h)) return rc;
   if (h->pod_rest_bytes == 0) return YODA_OK;
+  pods_pack_rest(h);
   unsigned char* st = static_cast<unsigned char*>(h->pod_stage.p);
   HIP_TRY(h, hipMemcpyAsync(h->pod_blob.as<unsigned char>() + h->pod_rest_off, st + h->pod_rest_off,
                             h->pod_rest_bytes, hipMemcpyHostToDevice, h->stream));
@@ -1119,6 +1156,7 @@ static const DiskLevels& diskio_levels() {
 // bit-identical (alpha, beta) score every node alike (algorithm.go:105-111).
 int ensure_diskio_classes(yoda_t* h) {
   if (h->b_cls_ready) return YODA_OK;
+  pods_pack_rest(h);
   const uint32_t P = h->n_pods;
   const unsigned char* st = static_cast<const unsigned char*>(h->pod_stage.p);
   const uint64_t* al = reinterpret_cast<const uint64_t*>(st + h->pod_off[kPodAlpha]);
@@ -2430,6 +2468,12 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
       if (i == kPodCoreArrays - 1) core_bytes = total;
     }
     h->pod_rest_bytes = 0;  // (a deferred part of the previous batch is dropped)
+    h->rest_lazy = false;
+    // (memory ranks: the rank kernel below reads the 64-bit scv/memory now)
+    const bool defer = !(h->has_nodes && h->mem_ranks);
+    // the f64 thresholds and the Mode B weights (zero without rio / rcpu) are written later,
+    // off the upload's critical path (pods_pack_rest)
+    const bool lazy = defer && !(pd->rio && pd->rcpu);
     static const bool dbg = std::getenv("YODA_UPLOAD_DEBUG") != nullptr;
     auto now_ms = [] {
       return std::chrono::duration<double, std::milli>(
@@ -2451,7 +2495,7 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     uint32_t* c32 = reinterpret_cast<uint32_t*>(st + off[kPodC32]);
     uint32_t* nm = reinterpret_cast<uint32_t*>(st + off[kPodNeedMem]);
     uint32_t* nc = reinterpret_cast<uint32_t*>(st + off[kPodNeedClk]);
-    const uint64_t kClamp = 1ull << 53;  // > every F64-path card field (<= 2^44)
+    const uint64_t kClamp = kPodF64Clamp;
     uint64_t key_or[3] = {0, 0, 0};       // OR of the sort key's clamped fields (c, n, m)
     // distinct (clock, number, has-memory) groups with their pod counts and, per group, its
     // pods of the largest and of the smallest memory (the padding copies) as (m << 32 | pod)
@@ -2513,8 +2557,10 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
         nc[p] = pd->has_clock[p] ? need : 0;
         mu[p] = m;
         cu[p] = c;
-        mf[p] = (double)std::min(m, kClamp);
-        cf[p] = (double)std::min(c, kClamp);
+        if (!lazy) {
+          mf[p] = (double)std::min(m, kClamp);
+          cf[p] = (double)std::min(c, kClamp);
+        }
         m32[p] = (uint32_t)std::min<uint64_t>(m, 0xffffffffull);  // > every N32 field
         c32[p] = (uint32_t)std::min<uint64_t>(c, 0xffffffffull);
         kor[0] |= std::min<uint64_t>(c, 0xffffffull);  // the clamps of k_order_keys
@@ -2533,7 +2579,7 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
         const uint64_t mp = (std::min<uint64_t>(m, 0xffffffffull) << 32) | p;
         r_max = std::max(r_max, mp);
         r_min = std::min(r_min, mp);
-        al[p] = be[p] = 0.0;
+        if (!lazy) al[p] = be[p] = 0.0;
         if (pd->rio && pd->rcpu) {  // algorithm.go:105-106
           const double beta = 1.0 / (1.0 + (double)pd->rcpu[p] / pd->rio[p]);
           be[p] = beta;
@@ -2578,10 +2624,12 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     std::vector<uint64_t>& gmin = all.mn;
     const size_t g_n = all.n;
     const double t_merged = dbg ? now_ms() : 0.0;
-    // (memory ranks: the rank kernel below reads the 64-bit scv/memory now)
-    const bool defer = !(h->has_nodes && h->mem_ranks);
     HIP_TRY(h, hipMemcpyAsync(h->pod_blob.p, st, defer ? core_bytes : total, hipMemcpyHostToDevice,
                               h->stream));
+    if (defer) {  // (the deferred copy of a private run starts from here: pods_complete_async)
+      if (int rc = ensure_copy_stream(h)) return rc;
+      HIP_TRY(h, hipEventRecord(h->core_event, h->stream));
+    }
     const double t_copied = dbg ? now_ms() : 0.0;
     if (h->has_nodes && h->mem_ranks)  // scv/memory -> its rank threshold, on the device
       HIP_TRY(h, launch_mem_rank(reinterpret_cast<const uint64_t*>(
@@ -2657,6 +2705,7 @@ int yoda_upload_pods(yoda_t* h, const yoda_pod_soa* pd) {
     for (int a = 0; a < kPodArrays; ++a) h->pod_off[a] = off[a];
     h->pod_rest_off = core_bytes;
     h->pod_rest_bytes = defer ? total - core_bytes : 0;
+    h->rest_lazy = lazy;
     for (int f = 0; f < 3; ++f) {
       uint32_t bits = 0;
       while (bits < 64 && (key_or[f] >> bits)) ++bits;
@@ -2761,7 +2810,6 @@ int yoda_run(yoda_t* h, int mode, uint32_t flags) {
   if (!defer && (rc = pods_complete(h))) return rc;
   // (YODA_SIDE_COPY=0, A/B knob: the deferred copy on the run's stream after its kernels)
   static const bool side = YODA_KNOB("YODA_SIDE_COPY", 1) != 0;
-  if (defer && side && (rc = pods_complete_async(h))) return rc;
   try {
     if ((rc = order_pods(h, mode))) return rc;
     if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), true)))
@@ -2774,7 +2822,10 @@ int yoda_run(yoda_t* h, int mode, uint32_t flags) {
                        h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(),
                        false)))
       return rc;
-    if (defer && (rc = pods_complete(h))) return rc;  // (side copy: the join)
+    // the deferred arrays: packed on the host while the kernels run, copied on the side stream
+    // (from the upload's core copy on, so alongside the kernels), joined into the stream
+    if (defer && side && h->copy_stream && (rc = pods_complete_async(h))) return rc;
+    if (defer && (rc = pods_complete(h))) return rc;
     h->ran = true;
     h->ran_bitmask = mode == YODA_MODE_SCV && (flags & YODA_RUN_BITMASK);
     h->last_mode = mode;
