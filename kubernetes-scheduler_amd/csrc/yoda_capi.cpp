@@ -120,6 +120,9 @@ hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigne
                                 const uint64_t* bm, uint32_t bm_stride, const BlockMask* bs,
                                 uint32_t bs_stride, const uint32_t* counts, uint64_t* keys,
                                 uint32_t ib, int tk, hipStream_t s);
+hipError_t launch_topk_merge_deep(const uint64_t* keys, uint32_t C, uint32_t n_pods, uint32_t ib,
+                                  uint32_t node_offset, double* out_s, uint32_t* out_i, int ko,
+                                  hipStream_t s);
 hipError_t launch_topk_merge_keys(const uint64_t* keys, uint32_t C, uint32_t n_pods, uint32_t ib,
                                   uint32_t node_offset, double* out_s, uint32_t* out_i, int tk,
                                   hipStream_t s);
@@ -435,6 +438,7 @@ struct yoda_handle {
   DevBuf maxima, counts, rcp, best, idx, ties, lowest, pick, status, ties_out, flagged, n_flagged;
   // scatter targets of unpermute_outputs, swapped with the buffers above after each scatter
   DevBuf pick_alt, status_alt, ties_out_alt, counts_alt, best_alt, maxima_alt;
+  DevBuf win_dev;  // a capacity window's outputs on the device, then one DMA copy to win_stage
   DevBuf bitmask, bitmask_t, rows, rows_t, norm;
   DevBuf blk;               // [wave][node block / 64] u64: blocks with a feasible pod (K1 -> K2)
   bool blk_valid = false;   // the last K1 wrote blk (block-classified K1 on this batch)
@@ -539,7 +543,7 @@ struct yoda_handle {
                      &p_wit,     &wit,       &stats_dev, &one_feas,  &one_part,  &one_done,
                      &ex1,       &rec,       &rec_all,   &cg_max,    &cg_cnt,    &cg_wit,    &cg_gather, &k3rec,     &k3all,
                      &one_out,   &b_cab,     &b_cls,     &b_part,
-                     &counts_alt, &best_alt, &maxima_alt};
+                     &counts_alt, &best_alt, &maxima_alt, &win_dev};
     for (DevBuf* b : all) b->release();
     pod_stage.release();
     upd_stage.release();
@@ -1585,10 +1589,16 @@ int finalize(yoda_t* h, int mode, const uint32_t* counts, const int64_t* best,
 // path and the score bound allow it (its own chunking: one round of workgroups, so that the
 // [C][P][KT] lists stay small); else the per-pair K2 (k2_score OUT_TOPK).
 // YODA_TOPK_PER_PAIR=1 forces the per-pair kernels (A/B, tests).
-int topk_lists(yoda_t* h, uint32_t P, uint32_t KT, const uint32_t* d_counts) {
+// deep > KT (the capacity windows, block kernels only): the chunks' KT-deep lists merged into
+// `deep`-deep lists exact as far as they reach (k_topk_merge_deep; entries past that empty);
+// *depth_out: the depth written (deep, or KT where the block kernels do not run).
+int topk_lists(yoda_t* h, uint32_t P, uint32_t KT, const uint32_t* d_counts, uint32_t deep = 0,
+               uint32_t* depth_out = nullptr) {
   const uint32_t N = h->n_nodes;
-  HIP_TRY(h, h->tk_s.ensure((size_t)KT * P * 8));
-  HIP_TRY(h, h->tk_i.ensure((size_t)KT * P * 4));
+  if (depth_out) *depth_out = KT;
+  const uint32_t KD = std::max(KT, deep);
+  HIP_TRY(h, h->tk_s.ensure((size_t)KD * P * 8));
+  HIP_TRY(h, h->tk_i.ensure((size_t)KD * P * 4));
   if (P == 0 || N == 0) return YODA_OK;
   uint32_t ib = 1;
   while ((1ull << ib) <= N) ++ib;  // node ids < 2^ib - 1: a real key is never 0
@@ -1631,6 +1641,13 @@ int topk_lists(yoda_t* h, uint32_t P, uint32_t KT, const uint32_t* d_counts) {
                                      P, h->bitmask.as<uint64_t>(), bm_row(N),
                                     h->bs_ptr(), bs_row(N), d_counts,
                                     h->tk_s_part.as<uint64_t>(), ib, (int)KT, h->stream));
+    if (deep > KT && KT == (uint32_t)topk_k_capacity()) {
+      HIP_TRY(h, launch_topk_merge_deep(h->tk_s_part.as<uint64_t>(), Ct, P, ib, h->node_offset,
+                                        h->tk_s.as<double>(), h->tk_i.as<uint32_t>(), (int)deep,
+                                        h->stream));
+      if (depth_out) *depth_out = deep;
+      return YODA_OK;
+    }
     HIP_TRY(h, launch_topk_merge_keys(h->tk_s_part.as<uint64_t>(), Ct, P, ib, h->node_offset,
                                       h->tk_s.as<double>(), h->tk_i.as<uint32_t>(), (int)KT,
                                       h->stream));
@@ -4035,11 +4052,17 @@ struct yoda_greedy_session {
   // current window (queue positions [ws, ws + wn)), inputs in window order
   uint32_t ws = 0, wn = 0, k = 0, next = 0, resolved = 0, assigned = 0, refreshes = 0;
   bool in_window = false, wrapped = false;
+  // some node's static score rose within the window (never, short of a wrap: Allocate only
+  // grows): a listed node's current score may then exceed its window-start one
+  bool stat_rose = false;
   std::vector<uint32_t> counts, ti;
   std::vector<double> ts;
   // each list's certificate threshold (flags 0): its last entry's window-start -- or, after a
   // mid-window refresh (yoda_gs_refresh), refresh-time -- score and node
   std::vector<double> Tw;
+  // entries of each list before its first empty one (a deep merge stops where it is no longer
+  // exact, k_topk_merge_deep): the list holds every feasible node only when that is nf
+  std::vector<uint32_t> vlen;
   std::vector<uint32_t> Tix;
   // YODA_GREEDY_CARD_CAPACITY (greedy): cross[q] = window-touched nodes whose
   // CardNumber has dropped from >= q (window start) to < q, i.e. nodes a pod needing q cards
@@ -4082,7 +4105,9 @@ struct yoda_greedy_session {
       }
     }
     bool z;
+    const int64_t before_stat = stat[n];
     stat[n] = static_score(free_sum[n], total_sum[n], alloc[n], &z);
+    if (stat[n] > before_stat) stat_rose = true;
   }
   // PodFitsNumber operand of pod p (filter.go:11-16): the label, or 1 (CardNumber > 0)
   uint64_t need_cards(uint32_t p) const { return has_number[p] ? number[p] : 1; }
@@ -4112,6 +4137,9 @@ struct yoda_greedy_session {
   }
   // Node n's contribution to pod p's maxima (ProcessMaxValueWithCard over the cards with
   // FreeMemory >= m and Clock >= c, collection.go:46-76), MaxValue field order.
+  // per node (MaxValue order) the largest value over its real cards: no pod's contrib() from
+  // the node exceeds it (scan_lost skips nodes that cannot be a witness)
+  std::vector<uint64_t> nodemax;
   bool contrib(uint32_t n, uint32_t p, uint64_t v[6]) const {
     const uint64_t* c = cards.data() + (size_t)n * 6 * K;
     const uint64_t m = has_memory[p] ? memory[p] : 0, ck = has_clock[p] ? clock[p] : 0;
@@ -4136,13 +4164,35 @@ struct yoda_greedy_session {
   // those had TotalMemorySum == 0 (lz), and how many were witnesses of each of its maxima
   // (lw).  False (nothing computed) without the cards or when too many nodes were lost.
   static constexpr uint64_t kExactLost = 512;
+  // witness_only: the caller needs lw only (nf0 >= 2 + lq and no zero-total node at the window
+  // start: lf and lz cannot change its outcome) -- and only for the fields whose witnesses lq
+  // lost nodes could all be (wcnt <= lq); a node below every such maximum is skipped unvisited
+  // (lf / lz then count only the visited nodes)
   bool scan_lost(uint32_t i, uint32_t p, uint64_t q, uint64_t lq, uint64_t* lf, uint64_t* lz,
-                 uint64_t lw[6]) const {
+                 uint64_t lw[6], bool witness_only = false) const {
     *lf = *lz = 0;
     for (int f = 0; f < 6; ++f) lw[f] = 0;
     if (lq == 0) return true;
     if (cards.empty() || lq > kExactLost) return false;
+    ++n_scan;
+    uint32_t fmask = 0x3fu;
+    if (witness_only && has_wit) {
+      fmask = 0;
+      for (int f = 0; f < 6; ++f) {
+        const size_t o = (size_t)f * wn + i;
+        if (wmax[o] > 1 && wcnt[o] <= lq) fmask |= 1u << f;
+      }
+      if (fmask == 0) return true;
+    }
     auto visit = [&](uint32_t x) {
+      if (witness_only && has_wit) {
+        const uint64_t* nm = nodemax.data() + (size_t)x * 6;
+        bool maybe = false;
+        for (int f = 0; f < 6 && !maybe; ++f)
+          maybe = ((fmask >> f) & 1u) && nm[f] >= wmax[(size_t)f * wn + i];
+        if (!maybe) return;
+      }
+      ++n_scan_nodes;
       if (!fit_ws(x, p, q)) return;
       ++*lf;
       *lz += total_sum[x] == 0 ? 1 : 0;
@@ -4198,16 +4248,19 @@ struct yoda_greedy_session {
       }
     }
     *best = bi;
-    return nf <= k || bs > Tw[i] || (bs == Tw[i] && bi <= Tix[i]);
+    return (nf <= k && vlen[i] >= nf) || bs > Tw[i] || (bs == Tw[i] && bi <= Tix[i]);
   }
   // why capacity certificates failed: wrap, few feasible left, zero-total, maxima, list
   // exhausted, below the threshold
   uint64_t why[6] = {};
+  // (diagnostics, YODA_GREEDY_DEBUG) capacity resolves, lost-node scans and nodes they visited
+  mutable uint64_t n_resolve = 0, n_scan = 0, n_scan_nodes = 0;
 };
 
 bool yoda_greedy_session::resolve_capacity(uint32_t i, uint32_t p, int32_t* pk) {
   const uint32_t KT = k;
   const uint32_t nf0 = counts[i], nz0 = counts[(size_t)wn + i];
+  ++n_resolve;
   if (nf0 == 0) {  // feasibility only shrinks: still no node
     *pk = YODA_PICK_NONE;
     return true;
@@ -4215,24 +4268,37 @@ bool yoda_greedy_session::resolve_capacity(uint32_t i, uint32_t p, int32_t* pk) 
   if (wrapped) return ++why[0], false;
   const uint64_t q = need_cards(p);
   const uint32_t len = std::min<uint32_t>(nf0, KT);
-  const bool whole = nf0 <= KT;  // the list holds every feasible node of the window start
+  // the list holds every feasible node of the window start
+  const bool whole = nf0 <= KT && vlen[i] >= nf0;
   const uint64_t lq = lost(q);
   uint32_t alive = 0, first = 0xffffffffu, alive_zero = 0;
   double bs = -1.0;
   uint32_t bi = 0xffffffffu;
-  for (uint32_t kk = 0; kk < len; ++kk) {
-    const uint32_t n = ti[(size_t)kk * wn + i];
-    if (n >= N || removed(n, q)) continue;
-    ++alive;
-    if (first == 0xffffffffu) first = n;
-    alive_zero += total_sum[n] == 0 ? 1u : 0u;
-    double cur = ts[(size_t)kk * wn + i];
-    if (touched_w[n]) cur = cur - (double)stat_w[n] + (double)stat[n];
-    if (cur > bs || (cur == bs && n < bi)) {
-      bs = cur;
-      bi = n;
+  // the list's best current candidate; alive / first / alive_zero too on a full scan.  A
+  // partial scan stops at the first entry whose window-start score is below the best so far:
+  // the list is in descending window-start order and a score only falls in a window (deep
+  // lists, k_topk_merge_deep, make the full scan the resolve's main cost)
+  auto scan = [&](bool full) {
+    alive = 0, first = 0xffffffffu, alive_zero = 0;
+    bs = -1.0, bi = 0xffffffffu;
+    for (uint32_t kk = 0; kk < len; ++kk) {
+      const size_t o = (size_t)kk * wn + i;
+      if (!full && ts[o] < bs) break;
+      const uint32_t n = ti[o];
+      if (n >= N || removed(n, q)) continue;
+      ++alive;
+      if (first == 0xffffffffu) first = n;
+      alive_zero += total_sum[n] == 0 ? 1u : 0u;
+      double cur = ts[o];
+      if (touched_w[n]) cur = cur - (double)stat_w[n] + (double)stat[n];
+      if (cur > bs || (cur == bs && n < bi)) {
+        bs = cur;
+        bi = n;
+      }
     }
-  }
+  };
+  const bool full_scan = whole || stat_rose;
+  scan(full_scan);
   uint64_t lf = 0, lz = 0, lw[6] = {};
   // The bounds-only certificate first (no card scan): whatever it certifies, the exact one
   // certifies with the same outcome (nf0 >= 2 + lq leaves >= 2 feasible nodes; a field with
@@ -4243,7 +4309,7 @@ bool yoda_greedy_session::resolve_capacity(uint32_t i, uint32_t p, int32_t* pk) 
       maxima_kept(i, q, lq, false, lw)) {
     // (falls through to the list certificate below with exact == false)
   } else {
-    exact = scan_lost(i, p, q, lq, &lf, &lz, lw);
+    exact = scan_lost(i, p, q, lq, &lf, &lz, lw, nf0 >= 2 + lq && nz0 == 0);
   }
   if (whole) {
     if (alive == 0) {
@@ -4266,6 +4332,7 @@ bool yoda_greedy_session::resolve_capacity(uint32_t i, uint32_t p, int32_t* pk) 
       return true;
     }
     if (nf == 1) {  // the only feasible node: listed and alive, or somewhere unlisted
+      if (!full_scan) scan(true);
       if (alive != 1) return ++why[1], false;
       *pk = (int32_t)first;
       return true;
@@ -4360,6 +4427,21 @@ int yoda_gs_create(const yoda_node_soa* nodes, const yoda_pod_soa* pods, uint32_
           if (nodes->card_healthy[k]) g->hmask[n] |= 1u << j;
         }
       }
+      // each node's largest contribution to any pod's maxima (contrib() over every real card)
+      g->nodemax.assign((size_t)N * 6, 0);
+      for (uint32_t n = 0; n < N; ++n) {
+        uint64_t* v = g->nodemax.data() + (size_t)n * 6;
+        const uint64_t* c = g->cards.data() + (size_t)n * 6 * K;
+        for (uint32_t j = 0; j < K; ++j) {
+          if (!((g->rmask[n] >> j) & 1u)) continue;
+          v[0] = std::max(v[0], c[3 * K + j]);
+          v[1] = std::max(v[1], c[1 * K + j]);
+          v[2] = std::max(v[2], c[4 * K + j]);
+          v[3] = std::max(v[3], c[0 * K + j]);
+          v[4] = std::max(v[4], c[5 * K + j]);
+          v[5] = std::max(v[5], c[2 * K + j]);
+        }
+      }
     }
     g->pick.assign(P, YODA_PICK_NONE);
     // queue order: sort.Less (sort.go:8-10), scv/priority descending, then input index
@@ -4396,6 +4478,7 @@ int yoda_gs_begin_window(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
     g->ws = ws, g->wn = wn, g->k = k, g->next = 0;
     g->in_window = true;
     g->wrapped = false;
+    g->stat_rose = false;
     std::fill(std::begin(g->cross), std::end(g->cross), 0u);
     for (auto& l : g->cross_list) l.clear();
     g->has_wit = false;
@@ -4404,8 +4487,13 @@ int yoda_gs_begin_window(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
     g->ti.assign(top_node, top_node + (size_t)k * wn);
     g->Tw.resize(wn);
     g->Tix.resize(wn);
+    g->vlen.resize(wn);
     for (uint32_t i = 0; i < wn; ++i) {
-      const uint32_t len = std::max<uint32_t>(1, std::min<uint32_t>(counts[i], k));
+      const uint32_t cap = std::min<uint32_t>(counts[i], k);
+      uint32_t v = 0;
+      while (v < cap && top_node[(size_t)v * wn + i] != 0xffffffffu) ++v;
+      g->vlen[i] = v;
+      const uint32_t len = std::max<uint32_t>(1, v);  // (threshold: the last entry listed)
       g->Tw[i] = top_score[(size_t)(len - 1) * wn + i];
       g->Tix[i] = top_node[(size_t)(len - 1) * wn + i];
     }
@@ -4525,6 +4613,7 @@ int yoda_gs_refresh(yoda_gs_t* g, uint32_t from, const double* top_score,
       g->ts[o] = g->touched_w[n] ? top_score[o] + (double)g->stat_w[n] - (double)g->stat[n]
                                  : top_score[o];
     }
+    g->vlen[i] = len;  // (a refresh's lists are whole: every id validated above)
     if (len) {
       g->Tw[i] = top_score[(size_t)(len - 1) * wn + i];
       g->Tix[i] = top_node[(size_t)(len - 1) * wn + i];
@@ -4738,11 +4827,20 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
     if ((rc = phase1_witness(h, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(),
                              h->wit.as<uint32_t>(), 0)))
       return rc;
+    // the lists' depth: KT from the chunks, merged deeper where the block kernels run
+    // (k_topk_merge_deep: exact as far as they reach; YODA_GREEDY_CAP_DEPTH, A/B knob: 32 /
+    // 64 / 128, 0 = KT)
+    static const uint32_t cap_depth = YODA_KNOB("YODA_GREEDY_CAP_DEPTH", 64);
+    uint32_t KD = KT;
     // pinned staging of the window's outputs, in window order (k_window_out writes them there
     // from the sorted order in one launch): counts | maxima | wit | top scores | top nodes
-    const size_t o_cnt = 0, o_mx = o_cnt + 8 * (size_t)wn, o_wit = o_mx + 48 * (size_t)wn,
-                 o_ts = o_wit + 48 * (size_t)wn, o_ti = o_ts + 8 * (size_t)KT * wn,
-                 total = o_ti + 4 * (size_t)KT * wn;
+    size_t o_cnt = 0, o_mx = 0, o_wit = 0, o_ts = 0, o_ti = 0, total = 0;
+    auto layout = [&](uint32_t kd) {
+      o_cnt = 0, o_mx = o_cnt + 8 * (size_t)wn, o_wit = o_mx + 48 * (size_t)wn,
+      o_ts = o_wit + 48 * (size_t)wn, o_ti = o_ts + 8 * (size_t)kd * wn,
+      total = o_ti + 4 * (size_t)kd * wn;
+    };
+    layout(std::max(KT, cap_depth));
     HIP_TRY(h, h->win_stage.ensure(total));
     unsigned char* st = static_cast<unsigned char*>(h->win_stage.p);
     const uint32_t *cnt_p, *wc_p, *ti_p;
@@ -4755,14 +4853,23 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
       // (node ids local here: the session works on this handle's nodes)
       const uint32_t off = h->node_offset;
       h->node_offset = 0;
-      rc = topk_lists(h, wn, KT, h->counts.as<uint32_t>());
+      rc = topk_lists(h, wn, KT, h->counts.as<uint32_t>(), cap_depth, &KD);
       h->node_offset = off;
       if (rc) return rc;
+      layout(KD);
+      // (YODA_WIN_DMA=0, A/B knob: k_window_out writes the pinned pages directly)
+      static const bool win_dma = YODA_KNOB("YODA_WIN_DMA", 1) != 0;
+      if (win_dma) HIP_TRY(h, h->win_dev.ensure(total));
       HIP_TRY(h, launch_window_out(h->counts.as<uint32_t>(), h->maxima.as<uint64_t>(),
                                    h->wit.as<uint32_t>(), h->tk_s.as<double>(),
                                    h->tk_i.as<uint32_t>(),
-                                   h->ordered ? h->perm.as<uint32_t>() : nullptr, wn, KT,
-                                   static_cast<unsigned char*>(h->win_stage.dp), h->stream));
+                                   h->ordered ? h->perm.as<uint32_t>() : nullptr, wn, KD,
+                                   win_dma ? h->win_dev.as<unsigned char>()
+                                           : static_cast<unsigned char*>(h->win_stage.dp),
+                                   h->stream));
+      if (win_dma)
+        HIP_TRY(h, hipMemcpyAsync(h->win_stage.p, h->win_dev.p, total, hipMemcpyDeviceToHost,
+                                  h->stream));
       t_issued = ms_since(tw);
       HIP_TRY(h, hipStreamSynchronize(h->stream));
       t_sync = ms_since(tw);
@@ -4779,8 +4886,8 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
       mx_w.assign(6 * (size_t)wn, 1ull);
       wc_w.assign(12 * (size_t)wn, 0u);
       for (size_t t = 6 * (size_t)wn; t < 12 * (size_t)wn; ++t) wc_w[t] = 0xffffffffu;
-      ts_w.assign((size_t)KT * wn, -1.0);
-      ti_w.assign((size_t)KT * wn, 0xffffffffu);
+      ts_w.assign((size_t)KD * wn, -1.0);
+      ti_w.assign((size_t)KD * wn, 0xffffffffu);
       cnt_p = cnt_w.data(), mx_p = mx_w.data(), wc_p = wc_w.data();
       ts_p = ts_w.data(), ti_p = ti_w.data();
     }
@@ -4788,7 +4895,7 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
     const double t_win = ms_since(tw);
     h->greedy_window_ms += t_win;
     const auto tr = Clock::now();
-    if ((rc = yoda_gs_begin_window(g, ws, wn, KT, cnt_p, ts_p, ti_p)) ||
+    if ((rc = yoda_gs_begin_window(g, ws, wn, KD, cnt_p, ts_p, ti_p)) ||
         (rc = yoda_gs_set_witness(g, mx_p, wc_p, wc_p + 6 * (size_t)wn)))
       return fail(h, rc, "greedy: session window");
     // resolve; an uncertified pod is scheduled exactly against the current state (k_one_*)
@@ -4870,11 +4977,13 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
   if (std::getenv("YODA_GREEDY_DEBUG"))
     std::fprintf(stderr,
                  "greedy capacity: windows %u restarts %u; failed certificates: wrap %llu, "
-                 "few-left %llu, zero-total %llu, maxima %llu, list-lost %llu, threshold %llu\n",
+                 "few-left %llu, zero-total %llu, maxima %llu, list-lost %llu, threshold %llu; "
+                 "resolves %llu, lost-node scans %llu visiting %llu nodes\n",
                  h->greedy_windows, h->greedy_restarts, (unsigned long long)g->why[0],
                  (unsigned long long)g->why[1], (unsigned long long)g->why[2],
                  (unsigned long long)g->why[3], (unsigned long long)g->why[4],
-                 (unsigned long long)g->why[5]);
+                 (unsigned long long)g->why[5], (unsigned long long)g->n_resolve,
+                 (unsigned long long)g->n_scan, (unsigned long long)g->n_scan_nodes);
   for (uint32_t p = 0; p < P; ++p)
     if (pick[p] >= 0) pick[p] += (int32_t)h->node_offset;
   // leave the uploaded snapshot as it was

@@ -3290,6 +3290,82 @@ __global__ __launch_bounds__(kBlock) void k_topk_merge_keys(const uint64_t* __re
       mine ? (uint32_t)(imask - (mine & imask)) + node_offset : 0xffffffffu;
 }
 
+// Deeper lists from the same chunk lists (the capacity windows' certificates):
+// the merged top KO of every chunk's top TK, kept as far as it is exact.  A node missing from
+// its chunk's list (or from the list a thread folds its chunks into) is at most that list's
+// TK-th key, so with M = the largest such key over the full lists, every candidate above M is
+// in place; the global top TK always is (each of them is within its chunk's and its thread's
+// top TK).  Output entries 0..L-1, L = max(TK, #candidates > M) capped at KO; the rest empty
+// (-1, 0xffffffff): every node left out is at most entry L-1 in (score desc, node asc).
+template <int TK, int KO>
+__global__ __launch_bounds__(kWave) void k_topk_merge_deep(const uint64_t* __restrict__ keys,
+                                                           uint32_t C, uint32_t n_pods,
+                                                           uint32_t ib, uint32_t node_offset,
+                                                           double* __restrict__ out_s,
+                                                           uint32_t* __restrict__ out_i) {
+  // one wave per pod: each lane folds every 64th chunk's list into its own top TK, then KO
+  // rounds take the largest lane head (the lane holding it moves on)
+  static_assert(KO % kWave == 0 || KO < kWave, "whole output rows per lane");
+  constexpr uint32_t PER = KO >= kWave ? KO / kWave : 1;  // output keys a lane holds
+  const uint32_t p = blockIdx.x, lane = threadIdx.x;
+  if (p >= n_pods) return;  // workgroup-uniform
+  uint64_t pl[TK];
+#pragma unroll
+  for (int k = 0; k < TK; ++k) pl[k] = 0ull;
+  uint64_t mbound = 0ull;  // the largest TK-th key of a full chunk list or of this lane's
+  for (uint32_t c = lane; c < C; c += kWave) {
+    const ulonglong2* l = reinterpret_cast<const ulonglong2*>(keys + ((size_t)c * n_pods + p) * TK);
+    uint64_t v[TK];
+#pragma unroll
+    for (int k = 0; k < TK / 2; ++k) {
+      const ulonglong2 t = l[k];
+      v[2 * k] = t.x;
+      v[2 * k + 1] = t.y;
+    }
+    mbound = max(mbound, v[TK - 1]);  // (0 unless the chunk's list is full)
+#pragma unroll
+    for (int k = 0; k < TK; ++k) {
+      if (!(v[k] > pl[TK - 1])) break;  // the list is sorted: nothing further enters
+      uint64_t x = v[k];
+#pragma unroll
+      for (int j = 0; j < TK; ++j) {
+        const uint64_t o = pl[j];
+        const bool gt = x > o;
+        pl[j] = gt ? x : o;
+        x = gt ? o : x;
+      }
+    }
+  }
+  mbound = max(mbound, pl[TK - 1]);  // (what this lane's folding dropped is below it)
+  const uint64_t M = wave_max_u64v(mbound);
+  uint64_t out[PER];
+#pragma unroll
+  for (uint32_t r = 0; r < PER; ++r) out[r] = 0ull;
+  uint32_t L = 0;
+  for (int k = 0; k < KO; ++k) {
+    const uint64_t m = wave_max_u64v(pl[0]);
+    if (m == 0ull) break;                // (uniform)
+    if (k >= TK && !(m > M)) break;      // no longer certain to be in place
+#pragma unroll
+    for (uint32_t r = 0; r < PER; ++r) out[r] = (uint32_t)k == r * kWave + lane ? m : out[r];
+    if (pl[0] == m) {
+#pragma unroll
+      for (int j = 0; j + 1 < TK; ++j) pl[j] = pl[j + 1];
+      pl[TK - 1] = 0ull;
+    }
+    ++L;
+  }
+  const uint64_t imask = (1ull << ib) - 1ull;
+#pragma unroll
+  for (uint32_t r = 0; r < PER; ++r) {
+    const uint32_t k = r * kWave + lane;
+    if (k >= (uint32_t)KO) continue;
+    const uint64_t x = k < L ? out[r] : 0ull;
+    out_s[(size_t)k * n_pods + p] = x ? (double)(x >> ib) : -1.0;
+    out_i[(size_t)k * n_pods + p] = x ? (uint32_t)(imask - (x & imask)) + node_offset : 0xffffffffu;
+  }
+}
+
 // Greedy: overwrite the static score (record header offset 0) of a few nodes.
 __global__ __launch_bounds__(kBlock) void k_set_static(unsigned char* __restrict__ nodes,
                                                        uint32_t stride,
@@ -4858,6 +4934,31 @@ hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigne
     else YODA_TOPKB(kTopKCap, false, true, true);
   }
 #undef YODA_TOPKB
+  return hipGetLastError();
+}
+
+// The 16-deep chunk lists merged into ko-deep exact-prefix lists (k_topk_merge_deep).
+hipError_t launch_topk_merge_deep(const uint64_t* keys, uint32_t C, uint32_t n_pods, uint32_t ib,
+                                  uint32_t node_offset, double* out_s, uint32_t* out_i, int ko,
+                                  hipStream_t s) {
+  if (n_pods == 0) return hipSuccess;
+  const dim3 grid(n_pods);
+  switch (ko) {
+    case 32:
+      hipLaunchKernelGGL((k_topk_merge_deep<kTopKCap, 32>), grid, dim3(kWave), 0, s, keys, C,
+                         n_pods, ib, node_offset, out_s, out_i);
+      break;
+    case 64:
+      hipLaunchKernelGGL((k_topk_merge_deep<kTopKCap, 64>), grid, dim3(kWave), 0, s, keys, C,
+                         n_pods, ib, node_offset, out_s, out_i);
+      break;
+    case 128:
+      hipLaunchKernelGGL((k_topk_merge_deep<kTopKCap, 128>), grid, dim3(kWave), 0, s, keys, C,
+                         n_pods, ib, node_offset, out_s, out_i);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
