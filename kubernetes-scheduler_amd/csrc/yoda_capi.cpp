@@ -121,8 +121,8 @@ hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigne
                                 uint32_t bs_stride, const uint32_t* counts, uint64_t* keys,
                                 uint32_t ib, int tk, hipStream_t s);
 hipError_t launch_topk_merge_deep(const uint64_t* keys, uint32_t C, uint32_t n_pods, uint32_t ib,
-                                  uint32_t node_offset, double* out_s, uint32_t* out_i, int ko,
-                                  hipStream_t s);
+                                  uint32_t node_offset, double* out_s, uint32_t* out_i, int tk,
+                                  int ko, hipStream_t s);
 hipError_t launch_topk_merge_keys(const uint64_t* keys, uint32_t C, uint32_t n_pods, uint32_t ib,
                                   uint32_t node_offset, double* out_s, uint32_t* out_i, int tk,
                                   hipStream_t s);
@@ -1589,6 +1589,15 @@ int finalize(yoda_t* h, int mode, const uint32_t* counts, const int64_t* best,
 // path and the score bound allow it (its own chunking: one round of workgroups, so that the
 // [C][P][KT] lists stay small); else the per-pair K2 (k2_score OUT_TOPK).
 // YODA_TOPK_PER_PAIR=1 forces the per-pair kernels (A/B, tests).
+// The block-classified top-k K2 with packed keys serves this snapshot (else the per-pair one).
+bool topk_block_ok(const yoda_t* h) {
+  static const bool per_pair = YODA_KNOB("YODA_TOPK_PER_PAIR", 0) == 1;
+  uint32_t ib = 1;
+  while ((1ull << ib) <= h->n_nodes) ++ib;
+  return !per_pair && h->path == Path::N32 && h->has_k2sum && h->K <= 8 && ib <= 40 &&
+         h->score_bound < (1ull << (64 - ib));
+}
+
 // deep > KT (the capacity windows, block kernels only): the chunks' KT-deep lists merged into
 // `deep`-deep lists exact as far as they reach (k_topk_merge_deep; entries past that empty);
 // *depth_out: the depth written (deep, or KT where the block kernels do not run).
@@ -1602,9 +1611,7 @@ int topk_lists(yoda_t* h, uint32_t P, uint32_t KT, const uint32_t* d_counts, uin
   if (P == 0 || N == 0) return YODA_OK;
   uint32_t ib = 1;
   while ((1ull << ib) <= N) ++ib;  // node ids < 2^ib - 1: a real key is never 0
-  static const bool per_pair = YODA_KNOB("YODA_TOPK_PER_PAIR", 0) == 1;
-  const bool block = !per_pair && h->path == Path::N32 && h->has_k2sum && h->K <= 8 &&
-                     ib <= 40 && h->score_bound < (1ull << (64 - ib));
+  const bool block = topk_block_ok(h);
   if (block) {
     uint32_t Ct = 1, cht = 64;
     // rounds of resident workgroups: 4 for window-sized batches (more, shorter per-(wave,
@@ -1641,10 +1648,10 @@ int topk_lists(yoda_t* h, uint32_t P, uint32_t KT, const uint32_t* d_counts, uin
                                      P, h->bitmask.as<uint64_t>(), bm_row(N),
                                     h->bs_ptr(), bs_row(N), d_counts,
                                     h->tk_s_part.as<uint64_t>(), ib, (int)KT, h->stream));
-    if (deep > KT && KT == (uint32_t)topk_k_capacity()) {
+    if (deep > KT) {
       HIP_TRY(h, launch_topk_merge_deep(h->tk_s_part.as<uint64_t>(), Ct, P, ib, h->node_offset,
-                                        h->tk_s.as<double>(), h->tk_i.as<uint32_t>(), (int)deep,
-                                        h->stream));
+                                        h->tk_s.as<double>(), h->tk_i.as<uint32_t>(), (int)KT,
+                                        (int)deep, h->stream));
       if (depth_out) *depth_out = deep;
       return YODA_OK;
     }
@@ -4055,8 +4062,12 @@ struct yoda_greedy_session {
   // some node's static score rose within the window (never, short of a wrap: Allocate only
   // grows): a listed node's current score may then exceed its window-start one
   bool stat_rose = false;
-  std::vector<uint32_t> counts, ti;
-  std::vector<double> ts;
+  std::vector<uint32_t> counts, ti_own;
+  std::vector<double> ts_own;
+  // the window's lists [k][wn]: the session's copies, or (greedy_capacity, gs_begin_window_at)
+  // the caller's staging, valid until the window ends
+  double* ts = nullptr;
+  uint32_t* ti = nullptr;
   // each list's certificate threshold (flags 0): its last entry's window-start -- or, after a
   // mid-window refresh (yoda_gs_refresh), refresh-time -- score and node
   std::vector<double> Tw;
@@ -4465,13 +4476,30 @@ int yoda_gs_queue_order(const yoda_gs_t* g, uint32_t* order) {
   return YODA_OK;
 }
 
+namespace {
+// yoda_gs_begin_window without copying the lists: the session reads (and, on a refresh,
+// writes) top_score / top_node in place until the window ends (greedy_capacity's staging)
+int gs_begin_window_at(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
+                       const uint32_t* counts, double* top_score, uint32_t* top_node,
+                       bool borrow);
+}  // namespace
+
 int yoda_gs_begin_window(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
                          const uint32_t* counts, const double* top_score,
                          const uint32_t* top_node) {
+  return gs_begin_window_at(g, ws, wn, k, counts, const_cast<double*>(top_score),
+                            const_cast<uint32_t*>(top_node), false);
+}
+
+namespace {
+int gs_begin_window_at(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
+                       const uint32_t* counts, double* top_score, uint32_t* top_node,
+                       bool borrow) {
   if (!g || ws > g->P || wn > g->P - ws || k == 0 || !counts || !top_score || !top_node)
     return YODA_ERR_INVALID_ARG;
-  for (uint32_t i = 0; i < (uint32_t)k * wn; ++i)
-    if (top_node[i] != 0xffffffffu && top_node[i] >= g->N) return YODA_ERR_RANGE;
+  if (!borrow)  // (the borrowed lists are libyoda's own kernel output)
+    for (uint32_t i = 0; i < (uint32_t)k * wn; ++i)
+      if (top_node[i] != 0xffffffffu && top_node[i] >= g->N) return YODA_ERR_RANGE;
   try {
     for (uint32_t n : g->touched_list) g->touched_w[n] = 0;
     g->touched_list.clear();
@@ -4483,8 +4511,15 @@ int yoda_gs_begin_window(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
     for (auto& l : g->cross_list) l.clear();
     g->has_wit = false;
     g->counts.assign(counts, counts + 2 * (size_t)wn);
-    g->ts.assign(top_score, top_score + (size_t)k * wn);
-    g->ti.assign(top_node, top_node + (size_t)k * wn);
+    if (borrow) {
+      g->ts = top_score;
+      g->ti = top_node;
+    } else {
+      g->ts_own.assign(top_score, top_score + (size_t)k * wn);
+      g->ti_own.assign(top_node, top_node + (size_t)k * wn);
+      g->ts = g->ts_own.data();
+      g->ti = g->ti_own.data();
+    }
     g->Tw.resize(wn);
     g->Tix.resize(wn);
     g->vlen.resize(wn);
@@ -4502,6 +4537,7 @@ int yoda_gs_begin_window(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
     return YODA_ERR_INVALID_ARG;
   }
 }
+}  // namespace
 
 int yoda_gs_set_witness(yoda_gs_t* g, const uint64_t* maxima, const uint32_t* wit_count,
                         const uint32_t* wit_node) {
@@ -4742,10 +4778,13 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
   auto ms_since = [](Clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
   };
-  // YODA_GREEDY_CAP_TOPK=8 (A/B knob): the shorter lists of the flags-0 mode
-  static const uint32_t kt_cap =
-      YODA_KNOB("YODA_GREEDY_CAP_TOPK", 0) == (uint32_t)topk_k() ? (uint32_t)topk_k()
-                                                               : (uint32_t)topk_k_capacity();
+  // the chunks' list depth: 8 where the lists are merged deeper (k_topk_merge_deep: the same
+  // 64-deep lists as from 16, and a cheaper K2 -- 1.00-1.02 vs 1.07-1.09 s,
+  // profiles/r05/pqr/tk_ab.txt), else 16; YODA_GREEDY_CAP_TOPK=16 (A/B knob): 16 always
+  static const uint32_t kt_knob = YODA_KNOB("YODA_GREEDY_CAP_TOPK", 0);
+  const uint32_t kt_cap = kt_knob == (uint32_t)topk_k_capacity() || !topk_block_ok(h)
+                              ? (uint32_t)topk_k_capacity()
+                              : (uint32_t)topk_k();
   const uint32_t P = pods->n_pods, N = h->n_nodes, KT = kt_cap;
   yoda_node_soa nv{};
   nv.n_nodes = N;
@@ -4895,7 +4934,8 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
     const double t_win = ms_since(tw);
     h->greedy_window_ms += t_win;
     const auto tr = Clock::now();
-    if ((rc = yoda_gs_begin_window(g, ws, wn, KD, cnt_p, ts_p, ti_p)) ||
+    if ((rc = gs_begin_window_at(g, ws, wn, KD, cnt_p, const_cast<double*>(ts_p),
+                                 const_cast<uint32_t*>(ti_p), true)) ||
         (rc = yoda_gs_set_witness(g, mx_p, wc_p, wc_p + 6 * (size_t)wn)))
       return fail(h, rc, "greedy: session window");
     // resolve; an uncertified pod is scheduled exactly against the current state (k_one_*)

@@ -4939,26 +4939,28 @@ hipError_t launch_k2_topk_block(int K, const unsigned char* nodes, const unsigne
 
 // The 16-deep chunk lists merged into ko-deep exact-prefix lists (k_topk_merge_deep).
 hipError_t launch_topk_merge_deep(const uint64_t* keys, uint32_t C, uint32_t n_pods, uint32_t ib,
-                                  uint32_t node_offset, double* out_s, uint32_t* out_i, int ko,
-                                  hipStream_t s) {
+                                  uint32_t node_offset, double* out_s, uint32_t* out_i, int tk,
+                                  int ko, hipStream_t s) {
   if (n_pods == 0) return hipSuccess;
+  if (tk != kTopK && tk != kTopKCap) return hipErrorInvalidValue;
   const dim3 grid(n_pods);
+#define YODA_DEEP(TKV, KOV)                                                                     \
+  hipLaunchKernelGGL((k_topk_merge_deep<TKV, KOV>), grid, dim3(kWave), 0, s, keys, C, n_pods, ib, \
+                     node_offset, out_s, out_i)
   switch (ko) {
     case 32:
-      hipLaunchKernelGGL((k_topk_merge_deep<kTopKCap, 32>), grid, dim3(kWave), 0, s, keys, C,
-                         n_pods, ib, node_offset, out_s, out_i);
+      if (tk == kTopK) YODA_DEEP(kTopK, 32); else YODA_DEEP(kTopKCap, 32);
       break;
     case 64:
-      hipLaunchKernelGGL((k_topk_merge_deep<kTopKCap, 64>), grid, dim3(kWave), 0, s, keys, C,
-                         n_pods, ib, node_offset, out_s, out_i);
+      if (tk == kTopK) YODA_DEEP(kTopK, 64); else YODA_DEEP(kTopKCap, 64);
       break;
     case 128:
-      hipLaunchKernelGGL((k_topk_merge_deep<kTopKCap, 128>), grid, dim3(kWave), 0, s, keys, C,
-                         n_pods, ib, node_offset, out_s, out_i);
+      if (tk == kTopK) YODA_DEEP(kTopK, 128); else YODA_DEEP(kTopKCap, 128);
       break;
     default:
       return hipErrorInvalidValue;
   }
+#undef YODA_DEEP
   return hipGetLastError();
 }
 
