@@ -46,7 +46,8 @@ hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp,
                         hipStream_t s);
 hipError_t launch_window_out(const uint32_t* counts, const uint64_t* maxima, const uint32_t* wit,
                              const double* tk_s, const uint32_t* tk_i, const uint32_t* perm,
-                             uint32_t wn, uint32_t kt, unsigned char* out, hipStream_t s);
+                             uint32_t wn, uint32_t kt, bool lists_row_major, unsigned char* out,
+                             hipStream_t s);
 hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigned char* sum2,
                      const uint64_t* blk, uint32_t blk_stride, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
@@ -4068,6 +4069,12 @@ struct yoda_greedy_session {
   // the caller's staging, valid until the window ends
   double* ts = nullptr;
   uint32_t* ti = nullptr;
+  // entry kk of window pod i: [k][wn] (the API's layout), or [wn][k] (row_major: a pod's list
+  // contiguous, as k_window_out writes the capacity windows' staging)
+  bool row_major = false;
+  size_t at(uint32_t i, uint32_t kk) const {
+    return row_major ? (size_t)i * k + kk : (size_t)kk * wn + i;
+  }
   // each list's certificate threshold (flags 0): its last entry's window-start -- or, after a
   // mid-window refresh (yoda_gs_refresh), refresh-time -- score and node
   std::vector<double> Tw;
@@ -4250,8 +4257,8 @@ struct yoda_greedy_session {
     double bs = -1.0;
     uint32_t bi = 0xffffffffu;
     for (uint32_t kk = 0; kk < len; ++kk) {
-      const uint32_t n = ti[(size_t)kk * wn + i];
-      double cur = ts[(size_t)kk * wn + i];
+      const uint32_t n = ti[at(i, kk)];
+      double cur = ts[at(i, kk)];
       if (touched_w[n]) cur = cur - (double)stat_w[n] + (double)stat[n];
       if (cur > bs || (cur == bs && n < bi)) {
         bs = cur;
@@ -4293,7 +4300,7 @@ bool yoda_greedy_session::resolve_capacity(uint32_t i, uint32_t p, int32_t* pk) 
     alive = 0, first = 0xffffffffu, alive_zero = 0;
     bs = -1.0, bi = 0xffffffffu;
     for (uint32_t kk = 0; kk < len; ++kk) {
-      const size_t o = (size_t)kk * wn + i;
+      const size_t o = at(i, kk);
       if (!full && ts[o] < bs) break;
       const uint32_t n = ti[o];
       if (n >= N || removed(n, q)) continue;
@@ -4481,20 +4488,21 @@ namespace {
 // writes) top_score / top_node in place until the window ends (greedy_capacity's staging)
 int gs_begin_window_at(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
                        const uint32_t* counts, double* top_score, uint32_t* top_node,
-                       bool borrow);
+                       bool borrow, bool row_major = false);
 }  // namespace
 
 int yoda_gs_begin_window(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
                          const uint32_t* counts, const double* top_score,
                          const uint32_t* top_node) {
   return gs_begin_window_at(g, ws, wn, k, counts, const_cast<double*>(top_score),
-                            const_cast<uint32_t*>(top_node), false);
+                            const_cast<uint32_t*>(top_node), false, false);
 }
 
 namespace {
 int gs_begin_window_at(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
                        const uint32_t* counts, double* top_score, uint32_t* top_node,
-                       bool borrow) {
+                       bool borrow, bool row_major) {
+  if (row_major && !borrow) return YODA_ERR_INVALID_ARG;
   if (!g || ws > g->P || wn > g->P - ws || k == 0 || !counts || !top_score || !top_node)
     return YODA_ERR_INVALID_ARG;
   if (!borrow)  // (the borrowed lists are libyoda's own kernel output)
@@ -4504,6 +4512,7 @@ int gs_begin_window_at(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
     for (uint32_t n : g->touched_list) g->touched_w[n] = 0;
     g->touched_list.clear();
     g->ws = ws, g->wn = wn, g->k = k, g->next = 0;
+    g->row_major = row_major;
     g->in_window = true;
     g->wrapped = false;
     g->stat_rose = false;
@@ -4526,11 +4535,11 @@ int gs_begin_window_at(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
     for (uint32_t i = 0; i < wn; ++i) {
       const uint32_t cap = std::min<uint32_t>(counts[i], k);
       uint32_t v = 0;
-      while (v < cap && top_node[(size_t)v * wn + i] != 0xffffffffu) ++v;
+      while (v < cap && top_node[g->at(i, v)] != 0xffffffffu) ++v;
       g->vlen[i] = v;
       const uint32_t len = std::max<uint32_t>(1, v);  // (threshold: the last entry listed)
-      g->Tw[i] = top_score[(size_t)(len - 1) * wn + i];
-      g->Tix[i] = top_node[(size_t)(len - 1) * wn + i];
+      g->Tw[i] = top_score[g->at(i, len - 1)];
+      g->Tix[i] = top_node[g->at(i, len - 1)];
     }
     return YODA_OK;
   } catch (...) {
@@ -4573,7 +4582,7 @@ int yoda_gs_resolve(yoda_gs_t* g, uint32_t* next) {
     } else if (nf >= 2 && nz > 0) {
       pk = YODA_PICK_ERROR;  // Score would divide by TotalMemorySum == 0
     } else if (nf == 1) {
-      pk = (int32_t)g->ti[i];  // the only feasible node, returned without scoring
+      pk = (int32_t)g->ti[g->at(i, 0)];  // the only feasible node, returned without scoring
     } else if (g->wrapped) {
       break;
     } else {
@@ -4645,8 +4654,8 @@ int yoda_gs_refresh(yoda_gs_t* g, uint32_t from, const double* top_score,
       const uint32_t n = top_node[o];
       // stored so that the certificate's  stored - old static + current static  is its
       // current score (the refresh scored it with the current static)
-      g->ti[o] = n;
-      g->ts[o] = g->touched_w[n] ? top_score[o] + (double)g->stat_w[n] - (double)g->stat[n]
+      g->ti[g->at(i, kk)] = n;
+      g->ts[g->at(i, kk)] = g->touched_w[n] ? top_score[o] + (double)g->stat_w[n] - (double)g->stat[n]
                                  : top_score[o];
     }
     g->vlen[i] = len;  // (a refresh's lists are whole: every id validated above)
@@ -4902,7 +4911,7 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
       HIP_TRY(h, launch_window_out(h->counts.as<uint32_t>(), h->maxima.as<uint64_t>(),
                                    h->wit.as<uint32_t>(), h->tk_s.as<double>(),
                                    h->tk_i.as<uint32_t>(),
-                                   h->ordered ? h->perm.as<uint32_t>() : nullptr, wn, KD,
+                                   h->ordered ? h->perm.as<uint32_t>() : nullptr, wn, KD, true,
                                    win_dma ? h->win_dev.as<unsigned char>()
                                            : static_cast<unsigned char*>(h->win_stage.dp),
                                    h->stream));
@@ -4935,7 +4944,7 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
     h->greedy_window_ms += t_win;
     const auto tr = Clock::now();
     if ((rc = gs_begin_window_at(g, ws, wn, KD, cnt_p, const_cast<double*>(ts_p),
-                                 const_cast<uint32_t*>(ti_p), true)) ||
+                                 const_cast<uint32_t*>(ti_p), true, N > 0)) ||
         (rc = yoda_gs_set_witness(g, mx_p, wc_p, wc_p + 6 * (size_t)wn)))
       return fail(h, rc, "greedy: session window");
     // resolve; an uncertified pod is scheduled exactly against the current state (k_one_*)

@@ -1687,7 +1687,7 @@ __global__ __launch_bounds__(kBlock) void k_window_out(
     const uint32_t* __restrict__ counts, const uint64_t* __restrict__ maxima,
     const uint32_t* __restrict__ wit, const double* __restrict__ tk_s,
     const uint32_t* __restrict__ tk_i, const uint32_t* __restrict__ perm, uint32_t wn,
-    uint32_t kt, unsigned char* __restrict__ out) {
+    uint32_t kt, int row_major, unsigned char* __restrict__ out) {
   __shared__ uint32_t inv[kBlock];
   const uint32_t w0 = blockIdx.x * kBlock, w = w0 + threadIdx.x;
   if (perm) {
@@ -1707,9 +1707,11 @@ __global__ __launch_bounds__(kBlock) void k_window_out(
   for (uint32_t f = 0; f < 2; ++f) o_cnt[(size_t)f * wn + w] = counts[(size_t)f * wn + q];
   for (uint32_t f = 0; f < 6; ++f) o_mx[(size_t)f * wn + w] = maxima[(size_t)f * wn + q];
   for (uint32_t f = 0; f < 12; ++f) o_wit[(size_t)f * wn + w] = wit[(size_t)f * wn + q];
+  // the lists [k][wn], or [wn][k] (row_major: each pod's list contiguous for the host's scan)
   for (uint32_t k = 0; k < kt; ++k) {
-    o_ts[(size_t)k * wn + w] = tk_s[(size_t)k * wn + q];
-    o_ti[(size_t)k * wn + w] = tk_i[(size_t)k * wn + q];
+    const size_t o = row_major ? (size_t)w * kt + k : (size_t)k * wn + w;
+    o_ts[o] = tk_s[(size_t)k * wn + q];
+    o_ti[o] = tk_i[(size_t)k * wn + q];
   }
 }
 
@@ -4782,10 +4784,11 @@ hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp,
 
 hipError_t launch_window_out(const uint32_t* counts, const uint64_t* maxima, const uint32_t* wit,
                              const double* tk_s, const uint32_t* tk_i, const uint32_t* perm,
-                             uint32_t wn, uint32_t kt, unsigned char* out, hipStream_t s) {
+                             uint32_t wn, uint32_t kt, bool lists_row_major, unsigned char* out,
+                             hipStream_t s) {
   if (wn == 0) return hipSuccess;
   hipLaunchKernelGGL(k_window_out, pod_grid(wn), dim3(kBlock), 0, s, counts, maxima, wit, tk_s,
-                     tk_i, perm, wn, kt, out);
+                     tk_i, perm, wn, kt, lists_row_major ? 1 : 0, out);
   return hipGetLastError();
 }
 
