@@ -848,7 +848,11 @@ PodParams pod_params(yoda_t* h) {
   // (A/B knobs: YODA_KB_DEC=0 / YODA_GBEST=0 turn the non-G bounds / the shared best off)
   static const bool dec_env = YODA_KNOB("YODA_KB_DEC", 1) != 0;
   static const bool gbest_env = YODA_KNOB("YODA_GBEST", 1) != 0;
-  if (ub_ok && dec_env && h->kbdec.p) pp.kbdec = h->kbdec.as<uint32_t>();
+  // (the non-G bounds pay on one-model snapshots at K <= 8: config 3's K2 0.32 -> 0.21 ms;
+  // on mixed-model nodes and at K = 16 their per-block cost exceeds what they prune -- mixed50
+  // K2 1.52 vs 1.29 ms, the config-4 generator 0.64 vs 0.48 ms, profiles/r05/y/ab.txt)
+  if (ub_ok && dec_env && h->kbdec.p && h->K <= 8 && h->all_one_model)
+    pp.kbdec = h->kbdec.as<uint32_t>();
   {
     const size_t nw = (h->n_work + 63) / 64;
     uint64_t* sd = h->blk.as<uint64_t>() + nw * blk_row(h->n_nodes);
@@ -2085,8 +2089,10 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
         // with the blocks as uploaded, 4 % sorted); the sorted blocks are then taken in
         // bit-reversed order, so that any run of consecutive blocks -- a node chunk -- still
         // samples every free level (the chunks stay even).
+        // Not with memory ranks: there the rank-space K2 ran slower on the sorted blocks
+        // (memory in bytes: 1.91 vs 1.80 ms, profiles/r05/y/ab.txt).
         static const bool zorder_env = YODA_KNOB("YODA_NODE_ZORDER", 1) != 0;  // A/B knob
-        if (ok && zorder_env) {
+        if (ok && zorder_env && !ranks) {
           std::vector<uint32_t> hix;
           for (uint32_t t = 1; t <= (uint32_t)K; t <<= 1) hix.push_back(t - 1);
           const uint32_t nc = (uint32_t)hix.size(), bits = 64 / nc > 16 ? 16 : 64 / nc;

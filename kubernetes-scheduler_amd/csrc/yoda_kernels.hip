@@ -608,7 +608,9 @@ template <int K, bool STATS, bool MIX = true, bool WIT = false, int SUB = 1>
 #ifndef YODA_K1_WAVES
 #define YODA_K1_WAVES 6  // (7: 9 VGPRs spilled, ~90 MB of scratch writes per launch; r05j)
 #endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 : (K >= 16 ? 5 : YODA_K1_WAVES)))) void k1_block_n32(
+// (waves per SIMD: 6 for one-model tiles -- no VGPR spills; 7 with the mixed-model tiles, whose
+// loop is faster there despite spilling: mixed50 K1 1.56 vs 1.71 ms, profiles/r05/y/ab.txt)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 : (K >= 16 ? 5 : (MIX ? 7 : YODA_K1_WAVES))))) void k1_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum,
     const uint32_t* __restrict__ sum2w, const uint32_t* __restrict__ mixw,
     const uint32_t* __restrict__ x1w,
@@ -4696,7 +4698,8 @@ int kernel_capacity(int K, Path path, int which, int mode_diskio) {
     YODA_FN(&k2_diskio<false>);
   } else if (which == 1) {
     switch (path) {
-      case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k1_block_n32<KK, false>))); break;
+      // (the one-model tiles' kernel: the chunk plan of config 3 as measured)
+      case Path::N32: YODA_K_SWITCH(K, YODA_FN((&k1_block_n32<KK, false, false>))); break;
       case Path::F64: YODA_K_SWITCH(K, YODA_FN((&k1_filter_maxima<KK, Path::F64>))); break;
       case Path::U64: YODA_K_SWITCH(K, YODA_FN((&k1_filter_maxima<KK, Path::U64>))); break;
     }
