@@ -4259,10 +4259,10 @@ struct yoda_greedy_session {
   // static) and whether the list certifies it: every unlisted node scored <= T at the window
   // start or last refresh (ties: higher index) and its score can only have dropped since
   bool certify0(uint32_t i, uint32_t* best) const {
-    const uint32_t nf = counts[i], len = std::min<uint32_t>(nf, k);
+    const uint32_t nf = counts[i], len = std::min<uint32_t>(nf, vlen[i]);
     double bs = -1.0;
     uint32_t bi = 0xffffffffu;
-    for (uint32_t kk = 0; kk < len; ++kk) {
+    for (uint32_t kk = 0; kk < len; ++kk) {  // (the listed entries: none empty, every id < N)
       const uint32_t n = ti[at(i, kk)];
       double cur = ts[at(i, kk)];
       if (touched_w[n]) cur = cur - (double)stat_w[n] + (double)stat[n];
@@ -4272,6 +4272,7 @@ struct yoda_greedy_session {
       }
     }
     *best = bi;
+    if (bi == 0xffffffffu) return false;  // nothing listed
     return (nf <= k && vlen[i] >= nf) || bs > Tw[i] || (bs == Tw[i] && bi <= Tix[i]);
   }
   // why capacity certificates failed: wrap, few feasible left, zero-total, maxima, list
@@ -4588,6 +4589,7 @@ int yoda_gs_resolve(yoda_gs_t* g, uint32_t* next) {
     } else if (nf >= 2 && nz > 0) {
       pk = YODA_PICK_ERROR;  // Score would divide by TotalMemorySum == 0
     } else if (nf == 1) {
+      if (g->vlen[i] == 0) break;  // (not listed: the caller evaluates it)
       pk = (int32_t)g->ti[g->at(i, 0)];  // the only feasible node, returned without scoring
     } else if (g->wrapped) {
       break;
