@@ -442,7 +442,11 @@ int yoda_gs_create(const yoda_node_soa* nodes, const yoda_pod_soa* pods, uint32_
 int yoda_gs_destroy(yoda_gs_t* g);
 /* order[q] = input index of the pod at queue position q (sort.go:8-10). */
 int yoda_gs_queue_order(const yoda_gs_t* g, uint32_t* order);
-/* Window = queue positions [ws, ws + wn); arrays in window order as yoda_shard_topk's. */
+/* Window = queue positions [ws, ws + wn); arrays in window order as yoda_shard_topk's.  A
+ * pod's list may end (0xFFFFFFFF entries) before min(counts[i], k) entries: it then holds its
+ * best nodes only down to its last entry (every unlisted node scored at most that, in score
+ * desc / node asc order), which becomes the pod's threshold, and is never taken for the whole
+ * feasible set (libyoda's own capacity windows pass such lists, merged deeper than exact). */
 int yoda_gs_begin_window(yoda_gs_t* g, uint32_t ws, uint32_t wn, uint32_t k,
                          const uint32_t* counts, const double* top_score,
                          const uint32_t* top_node);
