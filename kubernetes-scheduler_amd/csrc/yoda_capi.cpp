@@ -3889,8 +3889,22 @@ int yoda_shard_topk_depth(const yoda_t* h) {
   return h->phase1_wit ? topk_k_capacity() : topk_k();
 }
 
+namespace {
+int shard_topk_impl(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_counts, uint32_t k,
+                    uint32_t deep, uint32_t* counts, double* top_score, uint32_t* top_node);
+}  // namespace
+
 int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_counts, uint32_t k,
                     uint32_t* counts, double* top_score, uint32_t* top_node) {
+  return shard_topk_impl(h, d_maxima, d_counts, k, 0, counts, top_score, top_node);
+}
+
+namespace {
+// deep > 0 (libyoda's sharded capacity windows): lists `deep` long, exact down to their last
+// entry and empty past it -- the 8-deep chunk lists merged deeper where the block kernels run
+// (k_topk_merge_deep), else the k-deep lists padded -- whatever this shard's kernels.
+int shard_topk_impl(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_counts, uint32_t k,
+                    uint32_t deep, uint32_t* counts, double* top_score, uint32_t* top_node) {
   int rc = check_ready(h, YODA_MODE_SCV);
   if (rc) return rc;
   if (!h->phase1_done) return fail(h, YODA_ERR_STATE, "yoda_shard_topk before yoda_shard_phase1");
@@ -3909,8 +3923,10 @@ int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_count
     for (uint32_t i = 0; i < P; ++i) h->h_pos[i] = i;
     h->topk_ready = false;
     if (P == 0) return YODA_OK;
-    std::vector<uint32_t> cnt(2 * (size_t)P), ti((size_t)KT * P, 0xffffffffu), perm(P);
-    std::vector<double> ts((size_t)KT * P, -1.0);
+    const uint32_t KO = std::max(KT, deep);  // the depth written to the caller
+    std::vector<uint32_t> cnt(2 * (size_t)P), ti((size_t)KO * P, 0xffffffffu), perm(P);
+    std::vector<double> ts((size_t)KO * P, -1.0);
+    uint32_t KD = KT;  // the depth the device lists hold
     HIP_TRY(h, hipMemcpyAsync(h->maxima.p, d_maxima, 6ull * P * 8, hipMemcpyDeviceToDevice,
                               h->stream));
     HIP_TRY(h, hipMemcpyAsync(cnt.data(), d_counts, 2ull * P * 4, hipMemcpyDeviceToHost,
@@ -3918,10 +3934,14 @@ int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_count
     if (N > 0) {
       HIP_TRY(h, launch_prep2(h->maxima.as<uint64_t>(), P, h->rcp.as<double>(),
                                h->stream));
-      if ((rc = topk_lists(h, P, KT, d_counts))) return rc;
-      HIP_TRY(h, hipMemcpyAsync(ts.data(), h->tk_s.p, (size_t)KT * P * 8, hipMemcpyDeviceToHost,
+      if (deep > KT && topk_block_ok(h)) {
+        if ((rc = topk_lists(h, P, (uint32_t)topk_k(), d_counts, deep, &KD))) return rc;
+      } else if ((rc = topk_lists(h, P, KT, d_counts))) {
+        return rc;
+      }
+      HIP_TRY(h, hipMemcpyAsync(ts.data(), h->tk_s.p, (size_t)KD * P * 8, hipMemcpyDeviceToHost,
                                 h->stream));
-      HIP_TRY(h, hipMemcpyAsync(ti.data(), h->tk_i.p, (size_t)KT * P * 4, hipMemcpyDeviceToHost,
+      HIP_TRY(h, hipMemcpyAsync(ti.data(), h->tk_i.p, (size_t)KD * P * 4, hipMemcpyDeviceToHost,
                                 h->stream));
     }
     if (h->ordered)
@@ -3934,9 +3954,9 @@ int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_count
       const uint32_t q = h->h_pos[i];
       counts[i] = cnt[q];
       counts[(size_t)P + i] = cnt[(size_t)P + q];
-      for (uint32_t k = 0; k < KT; ++k) {
-        top_score[(size_t)k * P + i] = ts[(size_t)k * P + q];
-        top_node[(size_t)k * P + i] = ti[(size_t)k * P + q];
+      for (uint32_t k = 0; k < KO; ++k) {
+        top_score[(size_t)k * P + i] = k < KD ? ts[(size_t)k * P + q] : -1.0;
+        top_node[(size_t)k * P + i] = k < KD ? ti[(size_t)k * P + q] : 0xffffffffu;
       }
     }
     h->topk_ready = true;
@@ -3947,6 +3967,7 @@ int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_count
     return fail(h, YODA_ERR_INVALID_ARG, "unexpected exception");
   }
 }
+}  // namespace
 
 int yoda_shard_phase1_witness(yoda_t* h, uint64_t* d_maxima, uint32_t* d_counts,
                               uint32_t* d_wit) {
@@ -5476,6 +5497,11 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
     }
     const uint32_t K = (uint32_t)(capacity ? topk_k_capacity() : topk_k()),
                    W0 = std::min<uint32_t>(P, greedy_window());
+    // capacity windows: each shard's lists merged deeper (shard_topk_impl, exact down to their
+    // last entry), the union cut where a shard's unlisted nodes could enter (below); the same
+    // depth on every rank (YODA_GREEDY_CAP_DEPTH, as yoda_greedy's; 0: K)
+    static const uint32_t cap_depth = YODA_KNOB("YODA_GREEDY_CAP_DEPTH", 64);
+    const uint32_t KL = capacity && cap_depth > K ? cap_depth : K;
     std::vector<uint32_t> counts, ti, wit_h;
     std::vector<double> ts;
     std::vector<uint64_t> mx_h;
@@ -5528,14 +5554,14 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
       // witness counts SUM and lowest witnesses MIN (they need only exchange 1's maxima)
       counts.resize(2ull * wn);
       auto merged_lists = [&](uint32_t from, bool with_witness) -> int {
-        const size_t lb = (size_t)K * wn * 12;  // per shard: K x wn scores (f64) + nodes (u32)
+        const size_t lb = (size_t)KL * wn * 12;  // per shard: KL x wn scores (f64) + nodes (u32)
         mine.resize((size_t)n * lb);
         for (int i = 0; i < n; ++i) {
           unsigned char* m = mine.data() + (size_t)i * lb;
-          int r = yoda_shard_topk(hs[i], hs[i]->cg_max.as<uint64_t>(),
-                                  hs[i]->cg_cnt.as<uint32_t>(), K, counts.data(),
-                                  reinterpret_cast<double*>(m),
-                                  reinterpret_cast<uint32_t*>(m + (size_t)K * wn * 8));
+          int r = shard_topk_impl(hs[i], hs[i]->cg_max.as<uint64_t>(),
+                                  hs[i]->cg_cnt.as<uint32_t>(), K, KL > K ? KL : 0u,
+                                  counts.data(), reinterpret_cast<double*>(m),
+                                  reinterpret_cast<uint32_t*>(m + (size_t)KL * wn * 8));
           if (r) return r;
         }
         std::vector<const void*> ins;
@@ -5546,31 +5572,59 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
         if (!r) r = co.allgather_issue(ins, lb, gathered);
         const int re = co.end();
         if (r || (r = re) || (r = co.allgather_finish(lb, gathered))) return r;
-        ts.assign((size_t)K * wn, -1.0);
-        ti.assign((size_t)K * wn, 0xffffffffu);
+        ts.assign((size_t)KL * wn, -1.0);
+        ti.assign((size_t)KL * wn, 0xffffffffu);
+        auto before = [](const std::pair<double, uint32_t>& a,
+                         const std::pair<double, uint32_t>& b) {
+          return a.first > b.first || (a.first == b.first && a.second < b.second);
+        };
+        // each shard's list is sorted: a world-way merge of the heads, stopping after KL
+        // entries.  Deep lists: every node a shard left out is at most the shard's last entry,
+        // so the union is certain only above the latest of those (and for its first topk_k():
+        // the global best few are within their shards' exact prefixes)
+        std::vector<const double*> sc(world);
+        std::vector<const uint32_t*> nd(world);
+        std::vector<uint32_t> head(world), len(world);
+        for (int rk = 0; rk < world; ++rk) {
+          const unsigned char* b = gathered.data() + (size_t)rk * lb;
+          sc[rk] = reinterpret_cast<const double*>(b);
+          nd[rk] = reinterpret_cast<const uint32_t*>(b + (size_t)KL * wn * 8);
+        }
         for (uint32_t p = from; p < wn; ++p) {
-          cand.clear();
+          bool any_last = false;
+          std::pair<double, uint32_t> last_max{-1.0, 0xffffffffu};
           for (int rk = 0; rk < world; ++rk) {
-            const unsigned char* b = gathered.data() + (size_t)rk * lb;
-            const double* sc = reinterpret_cast<const double*>(b);
-            const uint32_t* nd = reinterpret_cast<const uint32_t*>(b + (size_t)K * wn * 8);
-            for (uint32_t k = 0; k < K; ++k)
-              if (nd[(size_t)k * wn + p] != 0xffffffffu)
-                cand.emplace_back(sc[(size_t)k * wn + p], nd[(size_t)k * wn + p]);
+            uint32_t l = 0;
+            while (l < KL && nd[rk][(size_t)l * wn + p] != 0xffffffffu) ++l;
+            len[rk] = l;
+            head[rk] = 0;
+            if (KL > K && l > 0) {
+              const std::pair<double, uint32_t> last{sc[rk][(size_t)(l - 1) * wn + p],
+                                                     nd[rk][(size_t)(l - 1) * wn + p]};
+              if (!any_last || before(last_max, last)) last_max = last;
+              any_last = true;
+            }
           }
-          std::sort(cand.begin(), cand.end(), [](const std::pair<double, uint32_t>& a,
-                                                 const std::pair<double, uint32_t>& b) {
-            return a.first > b.first || (a.first == b.first && a.second < b.second);
-          });
-          for (uint32_t k = 0; k < K && k < cand.size(); ++k) {
-            ts[(size_t)k * wn + p] = cand[k].first;
-            ti[(size_t)k * wn + p] = cand[k].second;
+          for (uint32_t k = 0; k < KL; ++k) {
+            int best = -1;
+            std::pair<double, uint32_t> bv{-1.0, 0xffffffffu};
+            for (int rk = 0; rk < world; ++rk) {
+              if (head[rk] >= len[rk]) continue;
+              const size_t o = (size_t)head[rk] * wn + p;
+              const std::pair<double, uint32_t> v{sc[rk][o], nd[rk][o]};
+              if (best < 0 || before(v, bv)) best = rk, bv = v;
+            }
+            if (best < 0) break;
+            if (any_last && k >= (uint32_t)topk_k() && !before(bv, last_max)) break;
+            ++head[best];
+            ts[(size_t)k * wn + p] = bv.first;
+            ti[(size_t)k * wn + p] = bv.second;
           }
         }
         return YODA_OK;
       };
       if ((rc = merged_lists(0, capacity))) return rc;
-      if ((rc = yoda_gs_begin_window(g, ws, wn, K, counts.data(), ts.data(), ti.data())))
+      if ((rc = yoda_gs_begin_window(g, ws, wn, KL, counts.data(), ts.data(), ti.data())))
         return fail(h0, rc, "greedy: begin window");
       ++h0->greedy_windows;
       ++st[0];
