@@ -292,7 +292,9 @@ int yoda_comm_run_local(yoda_t* const* handles, int world, int mode);
  * lists all-gathered; an uncertified pod is scored on every shard and the (score, node)
  * candidates all-gathered.  U64 snapshots: every pod one sharded exact step.  pick [P]: global
  * node ids in input order.  The shards' node state is restored at the end.  The C/cgo twin of
- * the Python driver dist.sharded_greedy (the Go plugin's ShardedGreedy calls it).
+ * the Python driver dist.sharded_greedy (the Go plugin's ShardedGreedy calls it); the same
+ * picks, but its capacity windows take yoda_greedy's deeper lists (each shard's merged to 64,
+ * the union cut where it stops being certain), so it runs fewer windows than the Python driver.
  * _local: the same over `world` handles of this process on one device (tests). */
 int yoda_comm_greedy(yoda_t* h, const yoda_node_soa* all_nodes, const yoda_pod_soa* pods,
                      int mode, uint32_t flags, int32_t* pick);
