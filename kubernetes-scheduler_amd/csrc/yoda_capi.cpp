@@ -604,6 +604,10 @@ uint64_t static_score(uint64_t free_sum, uint64_t total_sum, uint64_t alloc, boo
 // parked on a condition variable between calls -- spawning 15 threads per upload cost more
 // than the packing itself.  run(n, fn) calls fn(0..n-1) once each, the caller taking part;
 // calls are serialised (one batch at a time).
+uint32_t pool_spin_us();  // (below, after the knobs)
+
+// After a batch the workers spin for a short while before parking: a scheduler uploads its
+// batches back to back, and a parked thread's wake-up is what a late range costs the pack.
 class HostPool {
  public:
   static HostPool& get() {
@@ -624,7 +628,7 @@ class HostPool {
       n_ = n;
       next_.store(0);
       left_ = n;
-      ++gen_;
+      gen_.fetch_add(1);  // (after the batch's fields: a spinning worker reads them next)
     }
     cv_.notify_all();
     work();
@@ -635,8 +639,8 @@ class HostPool {
   ~HostPool() {
     {
       std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-      ++gen_;
+      stop_.store(true);
+      gen_.fetch_add(1);
     }
     cv_.notify_all();
     for (auto& t : threads_) t.join();
@@ -659,12 +663,22 @@ class HostPool {
   }
   void loop() {
     uint64_t seen = 0;
+    const uint32_t spin_us = pool_spin_us();
     for (;;) {
+      if (spin_us) {
+        const auto t0 = std::chrono::steady_clock::now();
+        uint32_t it = 0;
+        while (gen_.load() == seen && !stop_.load()) {
+          if ((++it & 255u) == 0u &&
+              std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us))
+            break;
+        }
+      }
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-        if (stop_) return;
-        seen = gen_;
+        cv_.wait(lk, [&] { return stop_.load() || gen_.load() != seen; });
+        if (stop_.load()) return;
+        seen = gen_.load();
       }
       work();
     }
@@ -675,8 +689,8 @@ class HostPool {
   const std::function<void(uint32_t)>* fn_ = nullptr;
   uint32_t n_ = 0, left_ = 0;
   std::atomic<uint32_t> next_{0};
-  uint64_t gen_ = 0;
-  bool stop_ = false;
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<bool> stop_{false};
 };
 
 // Tuning knobs of the A/B harness (tools/ab_lib.sh).  Only the A/B build reads them from
@@ -692,6 +706,12 @@ static uint32_t knob_env(const char* name, uint32_t dflt) {
 #else
 #define YODA_KNOB(name, dflt) ((uint32_t)(dflt))
 #endif
+uint32_t pool_spin_us() {
+  // how long a HostPool worker spins for the next batch before parking (YODA_POOL_SPIN_US,
+  // A/B knob; 0 parks at once)
+  static const uint32_t v = YODA_KNOB("YODA_POOL_SPIN_US", 2000);
+  return v;
+}
 // Diagnostics (*_TRACE, *_DEBUG): counters, timings and traces only, never results or policy.
 static uint32_t diag_env(const char* name, uint32_t dflt) {
   const char* s = std::getenv(name);

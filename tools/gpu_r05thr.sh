@@ -1,0 +1,9 @@
+#!/bin/bash
+# e2e A/B on one box: upload pack threads (YODA_UPLOAD_THREADS 16 / 8 / 4).
+set -o pipefail
+O=gpurun_out/r05thr; rm -rf $O; mkdir -p $O
+for r in 1 2 3; do
+  for v in 16 8 4; do
+    echo "thr$v $(YODA_UPLOAD_THREADS=$v YODA_UPLOAD_DEBUG=1 YODA_LIB_PATH=$(realpath abl/cur.so) timeout -k 10 200 python3 tools/dbg/e2e_split.py 2>&1 | tail -2 | tr '\n' ' ')" | tee -a $O/e2e_ab.txt
+  done
+done
