@@ -5526,7 +5526,6 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
     std::vector<double> ts;
     std::vector<uint64_t> mx_h;
     std::vector<unsigned char> gathered, mine, one;
-    std::vector<std::pair<double, uint32_t>> cand;
     uint32_t ws = 0, W = W0;
     while (ws < P) {
       const uint32_t wn = std::min(W, P - ws);
