@@ -59,6 +59,24 @@ def k2_unique_bytes(P: int, N: int, k: int, path: str, mode: int) -> int:
     return N * (rec + summ) + P * (36 + 24)
 
 
+def k1_unique_bytes(P: int, N: int, k: int, path: str, mode: int) -> int:
+    """Algorithmic bytes of ONE K1 launch (Filter + PreScore maxima): per node
+    its K1 summary (N32: 48 + 4K B rounded to 16; F64/U64: the record, 32 + 48K B), per
+    64-node block its bound summary (N32: 4 (31 + 2K) B), per pod the five Filter inputs it
+    reads (scv/memory and scv/clock as u32, scv/number u64, need-memory and need-clock flags
+    u32: 24 B) and the stage's outputs (6 u64 maxima + feasible and zero-total counts: 56 B).
+    The chunk partials, masks and block lists K1 writes for k_reduce1 / K2 are intermediates
+    (they show in the counter traffic, not here)."""
+    if mode == MODE_DISKIO:  # the all-feasible state: outputs only
+        return P * 56
+    if path == "n32":
+        per_node = (48 + 4 * k + 15) // 16 * 16
+        blocks = (N + 63) // 64 * 4 * (31 + 2 * k)
+    else:
+        per_node, blocks = 32 + 48 * k, 0
+    return N * per_node + blocks + P * (24 + 56)
+
+
 def step_unique_bytes(P: int, N: int, k: int, path: str, mode: int) -> int:
     """Algorithmic bytes of one whole step: node records + both summaries (K1: 48 + 4K B,
     K2: 32 + 8K B), the pod blob (68 B) and the per-pod outputs (pick, status, ties,
@@ -197,17 +215,7 @@ def bench_greedy(args):
     runs = {}
     if world == 1:
         y.upload_nodes(nodes)
-        for flags in (0, 1):
-            y.greedy(pods.slice(0, min(pods.n_pods, 4096)), MODE_SCV, flags)  # warm-up
-            torch.cuda.synchronize(device)
-            t0 = time.perf_counter()
-            picks = y.greedy(pods, MODE_SCV, flags)
-            dt = time.perf_counter() - t0
-            windows, fallbacks, times = y.greedy_stats(times=True)
-            runs[flags] = {"seconds": dt, "picks": picks, "windows": windows,
-                           "exact_fallback_pods": fallbacks, "host_times_ms": times}
-            if flags:
-                runs[flags]["window_restarts"] = y.greedy_restarts()
+        runs = greedy_runs(y, pods, device)
     else:
         import torch.distributed as dist
         from yoda_amd.dist import HandleShard, Reducer, agree_on_path, shard_bounds, sharded_greedy
@@ -304,6 +312,46 @@ def bench_greedy(args):
                                    "sample_picks_match_gpu": bool(np.array_equal(got, want))}
     print(json.dumps(out), flush=True)
     y.close()
+
+
+def greedy_runs(y, pods, device) -> dict:
+    """Config 5 on one handle (nodes uploaded): flags 0 (reference-faithful assume) and 1 (the
+    card-capacity decrement), each after a 4096-pod warm-up batch; seconds host to host."""
+    runs = {}
+    for flags in (0, 1):
+        y.greedy(pods.slice(0, min(pods.n_pods, 4096)), MODE_SCV, flags)  # warm-up
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        picks = y.greedy(pods, MODE_SCV, flags)
+        dt = time.perf_counter() - t0
+        windows, fallbacks, times = y.greedy_stats(times=True)
+        runs[flags] = {"seconds": dt, "picks": picks, "windows": windows,
+                       "exact_fallback_pods": fallbacks, "host_times_ms": times}
+        if flags:
+            runs[flags]["window_restarts"] = y.greedy_restarts()
+    return runs
+
+
+def greedy_leg(dev_index: int) -> dict:
+    """extra.greedy: config 5 at full size (1M pods x 100k nodes, sort.Less queue order,
+    sequential assume) on this GPU, both flags -- the driver-observed config-5 seconds.  Every
+    pick of both runs is checked against the oracle's per-window digests in the GPU suite
+    (tests/test_gpu_greedy_config5.py); here the picks are summarised by a SHA-256 digest."""
+    import hashlib
+    device = torch.device("cuda", dev_index)
+    nodes, pods = synth.make_config(5)
+    z = Yoda(dev_index)
+    z.upload_nodes(nodes)
+    runs = greedy_runs(z, pods, device)
+    z.close()
+    out = {"workload": f"config5: {pods.n_pods} pods x {nodes.n_nodes} nodes greedy"}
+    for flags, key in ((0, "flags0"), (1, "capacity")):
+        r = runs[flags]
+        out[key] = {k: v for k, v in r.items() if k != "picks"}
+        out[key]["assigned"] = int((r["picks"] >= 0).sum())
+        out[key]["picks_sha256"] = hashlib.sha256(r["picks"].astype(np.int32).tobytes()).hexdigest()
+    out["seconds"] = out["flags0"]["seconds"]
+    return out
 
 
 def _timed_steps(step, barrier, n: int) -> float:
@@ -432,6 +480,8 @@ def disclosure(y, nodes, pods, step, barrier, args) -> dict:
         timed(name, nd, pd, mode, kw, 3 if name in ("u64", "f64") else 5)
     out["variants"] = variants
     out["plugin_row_latency"] = row_latency(dev_index)
+    if not args.no_greedy:
+        out["greedy"] = greedy_leg(dev_index)
     return out
 
 
@@ -453,6 +503,8 @@ def main():
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the disclosure runs (work classes, per-pair path, mixed-model "
                          "and F64 variants) after the timed region")
+    ap.add_argument("--no-greedy", action="store_true",
+                    help="skip the config-5 greedy leg of the disclosure runs (extra.greedy)")
     ap.add_argument("--check", action="store_true",
                     help="N>1: rank 0 re-evaluates the batch on one unsharded handle and "
                          "asserts identical picks / statuses / ties (rehearsal)")
@@ -607,16 +659,39 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = P * N / (elapsed / args.steps)
     n_local = hi - lo
-    # dominant kernel of this rank: K2 (score) unless K1 takes longer
+    p_local = my_pods.n_pods
+    # Per kernel (K1 = Filter + maxima, K2 = score + argmax): its algorithmic bytes per launch
+    # over its HIP-event launch time (events on the launch stream), the PMC counter bytes and
+    # issue figures of the committed rocprofv3 summary; the line's roofline is the DOMINANT
+    # kernel's (the longer average launch), whichever it is.
     k1_avg = k1_ms / max(launches, 1)
     k2_avg = k2_ms / max(launches, 1)
     names = kernel_names(y.path, mode)
-    dom, dom_ms = (names[1], k2_avg) if k2_avg >= k1_avg else (names[0], k1_avg)
-    p_local = my_pods.n_pods
-    algo_bytes = k2_unique_bytes(p_local, n_local, k_slots, y.path, mode)
-    achieved = algo_bytes / (k2_avg / 1e3) / 1e9 if k2_avg > 0 else 0.0
-    pmc = committed_pmc(names[1], P, N, world)
-    pmc1 = committed_pmc(names[0], P, N, world)
+    per_kernel = {}
+    for tag, name, avg, algo in (
+            ("k1", names[0], k1_avg, k1_unique_bytes(p_local, n_local, k_slots, y.path, mode)),
+            ("k2", names[1], k2_avg, k2_unique_bytes(p_local, n_local, k_slots, y.path, mode))):
+        pmc = committed_pmc(name, P, N, world)
+        ach = algo / (avg / 1e3) / 1e9 if avg > 0 else 0.0
+        tr = pmc.get("hbm_bytes_per_launch")
+        per_kernel[tag] = {
+            "kernel": name, "avg_launch_ms": avg, "algo_bytes_per_launch": algo,
+            "achieved": ach, "frac": ach / HBM_PEAK_GBS,
+            "traffic": tr,
+            # counter bytes over the committed profile's own launch time, against peak
+            "traffic_frac": (tr / (pmc["avg_ns"] / 1e9) / 1e9 / HBM_PEAK_GBS
+                             if tr and pmc.get("avg_ns") else None),
+            "traffic_over_algo": tr / algo if tr and algo else None,
+            "write_bytes": pmc.get("hbm_write_bytes"),
+            "pmc_avg_ms": pmc["avg_ns"] / 1e6 if pmc.get("avg_ns") else None,
+            # the issue roofline (what binds these kernels): VALU and SALU issue
+            # cycles / available cycles, and the share of wave-cycles waiting on memory
+            "issue": {k: pmc[k] for k in ("valu_issue_util", "salu_issue_util",
+                                          "wave_frac_waitcnt", "wave_frac_issue_stall",
+                                          "wave_frac_issuing") if k in pmc}}
+    dom_tag = "k2" if k2_avg >= k1_avg else "k1"
+    dom = per_kernel[dom_tag]
+    pmc_src = committed_pmc(dom["kernel"], P, N, world).get("_source")
     step_traffic = committed_step_traffic(P, N, world)
     step_bytes = step_unique_bytes(p_local, n_local, k_slots, y.path, mode)
 
@@ -648,39 +723,29 @@ def main():
                                         " (RCCL all-reduce merge)") if world > 1 else "")),
                    "node_bounds": [int(v) for v in b] if world > 1 and not pod_shard
                    else None},
-        # dominant kernel K2: its algorithmic (unique) bytes per launch / its HIP-event launch
+        # the dominant kernel's algorithmic (unique) bytes per launch / its HIP-event launch
         # time, against HBM peak; `traffic` = its measured HBM bytes per launch (PMC).  What
         # binds it is instruction issue / memory latency at its occupancy, not HBM bandwidth
         # (DESIGN.md §4): `bound` says so, `frac` stays the HBM fraction, and `issue` carries
-        # the PMC issue utilisation and wait fractions beside it.
-        "roofline": {"bound": "issue/latency", "frac_of": "hbm", "kernel": names[1],
-                     "achieved": achieved,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": pmc.get("hbm_bytes_per_launch"),
-                     "algo_bytes_per_launch": algo_bytes,
-                     "avg_launch_ms": k2_avg, "k1_avg_ms": k1_avg, "k2_avg_ms": k2_avg,
-                     "dominant_by_time": dom,
+        # the PMC issue utilisation and wait fractions beside it; `per_kernel` holds both.
+        "roofline": {"bound": "issue/latency", "frac_of": "hbm", "kernel": dom["kernel"],
+                     "dominant_by_time": dom["kernel"],
+                     "achieved": dom["achieved"],
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dom["frac"],
+                     "traffic": dom["traffic"],
+                     "algo_bytes_per_launch": dom["algo_bytes_per_launch"],
+                     "avg_launch_ms": dom["avg_launch_ms"], "k1_avg_ms": k1_avg,
+                     "k2_avg_ms": k2_avg,
+                     "issue": dom["issue"],
+                     "per_kernel": per_kernel,
                      "fractions": {
-                         # counter HBM bytes of K2 per launch / launch time / peak
-                         "counter_hbm": (pmc["hbm_bytes_per_launch"] / (k2_avg / 1e3) / 1e9
-                                         / HBM_PEAK_GBS
-                                         if pmc.get("hbm_bytes_per_launch") and k2_avg > 0
-                                         else None),
                          # the whole step's algorithmic bytes / step time / peak
                          "unique_bytes_step": step_bytes / (ms_per_step / 1e3) / 1e9
-                         / HBM_PEAK_GBS,
-                         # VALU issue utilisation of K2 and K1 (PMC)
-                         "valu_issue_k2": pmc.get("valu_issue_util"),
-                         "valu_issue_k1": pmc1.get("valu_issue_util")},
+                         / HBM_PEAK_GBS},
                      "step_traffic_bytes": step_traffic,
                      "step_unique_bytes": step_bytes,
-                     "k1_traffic": pmc1.get("hbm_bytes_per_launch"),
-                     "issue": {k: pmc[k] for k in ("valu_issue_util", "salu_issue_util",
-                                                   "wave_frac_waitcnt",
-                                                   "wave_frac_issue_stall",
-                                                   "wave_frac_issuing") if k in pmc},
                      "per_pair_model_bytes": bytes_per_pair(k_slots, mode),
-                     "pmc_source": pmc.get("_source")},
+                     "pmc_source": pmc_src},
         "e2e_ms": e2e_ms,
         "status_counts": {str(s): int((res.status == s).sum()) for s in np.unique(res.status)},
     }

@@ -275,12 +275,15 @@ int yoda_shard_exact_merge(yoda_t* h, const void* d_all, int world);
 int yoda_comm_unique_id(uint8_t* id);
 int yoda_comm_init(yoda_t* h, const uint8_t* id, int rank, int world);
 /* RCCL refuses two ranks on one GPU ("invalid usage").  Before yoda_comm_init every rank
- * exchanges its device's PCI bus id (yoda_device_bus_id, YODA_BUS_ID_BYTES, NUL-terminated)
- * along with the communicator id, and checks the gathered ids (rank-major, `stride` bytes
- * apart): YODA_ERR_SAME_DEVICE when two ranks share one, with *rank_a < *rank_b the first such
- * pair (either pointer may be NULL).  Host only: no HIP call. */
+ * exchanges its device key (yoda_device_key, YODA_DEVICE_KEY_BYTES, NUL-terminated: a 16-hex
+ * hash of the hostname and boot id, '/', the PCI bus id of yoda_device_bus_id -- bus ids alone
+ * repeat across identical servers) along with the communicator id, and checks the gathered keys
+ * (rank-major, `stride` bytes apart): YODA_ERR_SAME_DEVICE when two ranks share one, with
+ * *rank_a < *rank_b the first such pair (either pointer may be NULL).  Host only: no HIP call. */
 #define YODA_BUS_ID_BYTES 32
+#define YODA_DEVICE_KEY_BYTES 64
 int yoda_device_bus_id(const yoda_t* h, char* out, int len);
+int yoda_device_key(const yoda_t* h, char* out, int len);
 int yoda_comm_check_devices(const char* bus_ids, int world, int stride, int* rank_a,
                             int* rank_b);
 int yoda_comm_run(yoda_t* h, int mode);

@@ -4,6 +4,7 @@
 // the exact-f64 fast path or the exact-u64 generic path, and sequences the kernels of
 // yoda_kernels.hip on the handle's stream.  No exception crosses the C boundary.
 #include <dlfcn.h>
+#include <unistd.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>  // types only: librccl is opened at yoda_comm_init (dlopen)
 
@@ -415,6 +416,10 @@ struct yoda_handle {
   size_t pod_off[kPodArrays] = {};
   size_t pod_rest_off = 0, pod_rest_bytes = 0;  // the blob's deferred part (pods_complete)
   bool fast_run = false;  // inside a private block-kernel run: the deferred part may wait
+  // a deferred private run's kernels are in flight before the non-core pod arrays (m_f, c_f,
+  // m_u, c_u, alpha, beta) reach the device: pod_params hands out null pointers for them, so a
+  // kernel that read them there would fault instead of reading the last batch's values
+  bool core_only = false;
   // batch ordering (yoda_order.hip): when `ordered`, the kernels of this run read the pods
   // from pod_sorted (sorted position i = original pod perm[i]); bitmask/rows stay in sorted
   // order and are un-permuted by their transposes, the per-pod outputs by finalize().
@@ -626,6 +631,7 @@ class HostPool {
       std::lock_guard<std::mutex> lk(mu_);
       fn_ = &fn;
       n_ = n;
+      last_n_.store(n, std::memory_order_relaxed);
       next_.store(0);
       left_ = n;
       gen_.fetch_add(1);  // (after the batch's fields: a spinning worker reads them next)
@@ -650,7 +656,7 @@ class HostPool {
   HostPool() {
     const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
     const uint32_t n = std::min(16u, hw) - 1u;  // + the calling thread
-    for (uint32_t i = 0; i < n; ++i) threads_.emplace_back([this] { loop(); });
+    for (uint32_t i = 0; i < n; ++i) threads_.emplace_back([this, i] { loop(i); });
   }
   void work() {
     for (;;) {
@@ -661,15 +667,18 @@ class HostPool {
       if (--left_ == 0) done_cv_.notify_one();
     }
   }
-  void loop() {
+  void loop(uint32_t self) {
     uint64_t seen = 0;
     const uint32_t spin_us = pool_spin_us();
     for (;;) {
-      if (spin_us) {
+      // only the workers the last batch used spin (a small batch leaves the rest parked), and
+      // they pause between polls so a sibling hyperthread keeps its issue slots
+      if (spin_us && self + 1u < last_n_.load(std::memory_order_relaxed)) {
         const auto t0 = std::chrono::steady_clock::now();
         uint32_t it = 0;
         while (gen_.load() == seen && !stop_.load()) {
-          if ((++it & 255u) == 0u &&
+          __builtin_ia32_pause();
+          if ((++it & 63u) == 0u &&
               std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us))
             break;
         }
@@ -688,7 +697,7 @@ class HostPool {
   std::condition_variable cv_, done_cv_;
   const std::function<void(uint32_t)>* fn_ = nullptr;
   uint32_t n_ = 0, left_ = 0;
-  std::atomic<uint32_t> next_{0};
+  std::atomic<uint32_t> next_{0}, last_n_{0};
   std::atomic<uint64_t> gen_{0};
   std::atomic<bool> stop_{false};
 };
@@ -708,8 +717,9 @@ static uint32_t knob_env(const char* name, uint32_t dflt) {
 #endif
 uint32_t pool_spin_us() {
   // how long a HostPool worker spins for the next batch before parking (YODA_POOL_SPIN_US,
-  // A/B knob; 0 parks at once)
-  static const uint32_t v = YODA_KNOB("YODA_POOL_SPIN_US", 2000);
+  // A/B knob; 0 parks at once).  1 ms covers a batch-to-batch gap of the e2e loop (~0.9 ms);
+  // a scheduler that uploads less often parks its workers after that.
+  static const uint32_t v = YODA_KNOB("YODA_POOL_SPIN_US", 1000);
   return v;
 }
 // Diagnostics (*_TRACE, *_DEBUG): counters, timings and traces only, never results or policy.
@@ -850,6 +860,7 @@ PodParams pod_params(yoda_t* h) {
   pp.need_clk = reinterpret_cast<uint32_t*>(b + off[kPodNeedClk]);
   pp.alpha = reinterpret_cast<double*>(b + off[kPodAlpha]);
   pp.beta = reinterpret_cast<double*>(b + off[kPodBeta]);
+  if (h->core_only) pp.m_f = pp.c_f = pp.alpha = pp.beta = nullptr, pp.m_u = pp.c_u = nullptr;
   pp.g = h->has_k2sum ? h->g : GTab{};
   pp.mix = h->path == Path::N32 ? h->kmix.as<uint32_t>() : nullptr;
   pp.x1 = h->path == Path::N32 ? h->kx1.as<uint32_t>() : nullptr;
@@ -1320,9 +1331,20 @@ hipError_t tighten_block_sums(yoda_t* h) {
   return e;
 }
 
+// Whose PreScore maxima a phase 1 produces.  (The K2 pruning seeds are scores under this
+// handle's G table, lower bounds only for pods whose maxima are at most G's: exchanged maxima
+// can exceed a shard's G, so the argmax K2 checks each wave's reciprocals against G's before
+// it takes a seed -- tests/test_gpu_shard_seeds.py.)
+enum class Maxima {
+  Exchanged,  // a node shard: the maxima are reduced across shards after this phase
+  Own,        // this handle's maxima are the run's (score rows, greedy windows)
+  OwnFinal,   // ... and the reduce writes the reciprocals too (yoda_run)
+};
+
 // Phase 1: Filter + PreScore maxima (Mode A), or the all-feasible state (Mode B).
-// final_maxima: this handle's maxima are the run's (no exchange follows).
-int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts, bool final_maxima = false) {
+int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts,
+           Maxima whose = Maxima::Exchanged) {
+  const bool final_maxima = whose == Maxima::OwnFinal;
   h->seeds_valid = false;  // (set again below when this run's block K1 writes them)
   h->rcp_ready = false;
   const uint32_t P = h->n_work;  // sorted positions of this run
@@ -2861,9 +2883,15 @@ int yoda_run(yoda_t* h, int mode, uint32_t flags) {
   if (!defer && (rc = pods_complete(h))) return rc;
   // (YODA_SIDE_COPY=0, A/B knob: the deferred copy on the run's stream after its kernels)
   static const bool side = YODA_KNOB("YODA_SIDE_COPY", 1) != 0;
+  h->core_only = defer;
   try {
+    struct Clear {
+      bool& f;
+      ~Clear() { f = false; }
+    } clear{h->core_only};
     if ((rc = order_pods(h, mode))) return rc;
-    if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), true)))
+    if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(),
+                     Maxima::OwnFinal)))
       return rc;
     if ((rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), h->best.as<int64_t>(),
                      h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>())))
@@ -2875,6 +2903,7 @@ int yoda_run(yoda_t* h, int mode, uint32_t flags) {
       return rc;
     // the deferred arrays: packed on the host while the kernels run, copied on the side stream
     // (from the upload's core copy on, so alongside the kernels), joined into the stream
+    h->core_only = false;
     if (defer && side && h->copy_stream && (rc = pods_complete_async(h))) return rc;
     if (defer && (rc = pods_complete(h))) return rc;
     h->ran = true;
@@ -2995,7 +3024,8 @@ int yoda_score_rows_norm(yoda_t* h, int mode, uint32_t* bitmask_out, uint64_t n_
       rows = h->rows.as<int64_t>();
     }
     if ((rc = order_pods(h, mode))) return rc;
-    if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>()))) return rc;
+    if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), Maxima::Own)))
+      return rc;
     if ((rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), h->best.as<int64_t>(),
                      h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(),
                      rows)))
@@ -3595,7 +3625,8 @@ int yoda_greedy(yoda_t* h, const yoda_pod_soa* pods, int mode, uint32_t flags, i
         if ((rc = order_pods(h, YODA_MODE_SCV))) return rc;
         h->greedy_prep_ms += ms_since(tw);
         if (N > 0) {
-          if ((rc = phase1(h, YODA_MODE_SCV, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>())))
+          if ((rc = phase1(h, YODA_MODE_SCV, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(),
+                           Maxima::Own)))
             return rc;
           HIP_TRY(h, launch_prep2(h->maxima.as<uint64_t>(), wn, h->rcp.as<double>(),
                                    h->stream));
@@ -5763,6 +5794,34 @@ int yoda_device_bus_id(const yoda_t* h, char* out, int len) {
   std::memset(out, 0, (size_t)len);
   if (hipDeviceGetPCIBusId(out, len - 1, h->device) != hipSuccess) return YODA_ERR_HIP;
   return YODA_OK;
+}
+
+// The host's identity for the device check: FNV-1a 64 of the hostname and the kernel's boot id
+// (what NCCL's hostHash takes), so identical servers -- equal PCI bus ids -- still differ.
+static uint64_t host_hash() {
+  uint64_t x = 1469598103934665603ull;
+  const auto mix = [&](const char* s, size_t n) {
+    for (size_t i = 0; i < n; ++i) x = (x ^ (unsigned char)s[i]) * 1099511628211ull;
+  };
+  char name[256] = {0};
+  gethostname(name, sizeof(name) - 1);
+  mix(name, strnlen(name, sizeof(name)));
+  if (FILE* f = std::fopen("/proc/sys/kernel/random/boot_id", "r")) {
+    char b[64] = {0};
+    const size_t n = std::fread(b, 1, sizeof(b) - 1, f);
+    std::fclose(f);
+    mix(b, n);
+  }
+  return x;
+}
+
+int yoda_device_key(const yoda_t* h, char* out, int len) {
+  if (!h || !out || len < 32) return YODA_ERR_INVALID_ARG;
+  char bus[YODA_BUS_ID_BYTES];
+  int rc = yoda_device_bus_id(h, bus, sizeof(bus));
+  if (rc) return rc;
+  const int n = std::snprintf(out, (size_t)len, "%016llx/%s", (unsigned long long)host_hash(), bus);
+  return n > 0 && n < len ? YODA_OK : YODA_ERR_INVALID_ARG;
 }
 
 int yoda_comm_check_devices(const char* bus_ids, int world, int stride, int* rank_a,

@@ -21,6 +21,15 @@
 
 #include "yoda_layout.h"
 
+// The YODA_ABL_* ablations remove work whose results the path needs (written masks, summaries,
+// whole classes): counter and timing builds only.  They compile only beside the A/B knobs
+// (tools/build_ab.sh), never into a release libyoda.
+#if !defined(YODA_AB_KNOBS) &&                                                         \
+    (defined(YODA_ABL_K1_NOGEN) || defined(YODA_ABL_K1_NOHC) || defined(YODA_ABL_K1_NOPART) || \
+     defined(YODA_ABL_K1_NOBS) || defined(YODA_ABL_K1_NOBM) || defined(YODA_ABL_K1_NOLEAN))
+#error "YODA_ABL_* ablations give wrong results: build them with -DYODA_AB_KNOBS (tools/build_ab.sh)"
+#endif
+
 #pragma clang fp contract(off)
 
 namespace yoda {
@@ -253,45 +262,87 @@ __device__ __forceinline__ Tile tile() {
   return {i % PB, (i / PB) * 8u + (L & 7u)};
 }
 
-// Wave-wide reductions (every lane gets the result; once per workgroup chunk, not hot).
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+// Wave-wide reductions (every lane gets the result).  The block kernels run them in every
+// (wave, chunk) task's set-up and epilogue -- ~20 per task, which at config 3's ~38k tasks per
+// launch made them a large part of the fixed per-task cost -- so with the whole wave active
+// they take no LDS round trip: the cross-row steps are the CDNA4 half/row swaps
+// (v_permlane32_swap, v_permlane16_swap), the in-row steps DPP moves (row_ror:8,
+// row_half_mirror, quad_perm), ~2 VALU each instead of a dependent ds_bpermute.  Step s pairs
+// lane l with l ^ {32, 16, 8, 7, 2, 1}[s]: the six masks span the six lane bits, so after all
+// six every lane holds the reduction over the wave, for any commutative, associative op.
+// A wave with lanes switched off (exec partial: a DPP / permlane read of an off lane is not
+// its value) takes the ds_bpermute butterfly instead.
+__device__ __forceinline__ bool exec_full() { return __builtin_amdgcn_read_exec() == ~0ull; }
+template <int S>
+__device__ __forceinline__ uint32_t xlane_u32(uint32_t v) {
+  if constexpr (S == 0) {  // l ^ 32
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (threadIdx.x & 32u) ? r[0] : r[1];
+  } else if constexpr (S == 1) {  // l ^ 16
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (threadIdx.x & 16u) ? r[0] : r[1];
+  } else if constexpr (S == 2) {  // l ^ 8: rotate the 16-lane row by 8
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);
+  } else if constexpr (S == 3) {  // l ^ 7: mirror within each 8-lane half row
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false);
+  } else if constexpr (S == 4) {  // l ^ 2: quad_perm [2, 3, 0, 1]
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);
+  } else {  // l ^ 1: quad_perm [1, 0, 3, 2]
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);
+  }
+}
+template <int S>
+__device__ __forceinline__ uint64_t xlane_u64(uint64_t v) {
+  return (uint64_t)xlane_u32<S>((uint32_t)v) | ((uint64_t)xlane_u32<S>((uint32_t)(v >> 32)) << 32);
+}
+// op(v, partner) over the six steps (whole wave active), else the xor butterfly
+template <class T, class Op>
+__device__ __forceinline__ T wave_allreduce(T v, Op op) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit lanes");
+  using U = std::conditional_t<sizeof(T) == 4, uint32_t, uint64_t>;
+  auto x = [](T a, auto step) -> T {
+    constexpr int S = decltype(step)::value;
+    if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, xlane_u32<S>(__builtin_bit_cast(U, a)));
+    else return __builtin_bit_cast(T, xlane_u64<S>(__builtin_bit_cast(U, a)));
+  };
+  if (exec_full()) {
+    v = op(v, x(v, std::integral_constant<int, 0>{}));
+    v = op(v, x(v, std::integral_constant<int, 1>{}));
+    v = op(v, x(v, std::integral_constant<int, 2>{}));
+    v = op(v, x(v, std::integral_constant<int, 3>{}));
+    v = op(v, x(v, std::integral_constant<int, 4>{}));
+    v = op(v, x(v, std::integral_constant<int, 5>{}));
+    return v;
+  }
 #pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, kWave));
-  return uniform_u32(v);
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    const U u = (U)__shfl_xor(__builtin_bit_cast(std::conditional_t<sizeof(T) == 4, int, long long>, v), o, kWave);
+    v = op(v, __builtin_bit_cast(T, u));
+  }
+  return v;
+}
+struct OpMaxU32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return max(a, b); } };
+struct OpMaxU64 { __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return a > b ? a : b; } };
+struct OpSumU32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; } };
+struct OpMaxF64 { __device__ double operator()(double a, double b) const { return fmax(a, b); } };
+struct OpMaxF32 { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  return uniform_u32(wave_allreduce(v, OpMaxU32{}));
 }
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) { return ~wave_max_u32(~v); }
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) {
-    const uint64_t u = (uint64_t)__shfl_xor((unsigned long long)v, o, kWave);
-    v = v > u ? v : u;
-  }
-  return uniform_u64(v);
+  return uniform_u64(wave_allreduce(v, OpMaxU64{}));
 }
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) { return ~wave_max_u64(~v); }
 // The same reductions left in VGPRs (every lane holds the result; the compiler does not know
 // it is uniform): for wave bounds that are only VALU operands, so that a kernel with many of
 // them does not run out of SGPRs (spills, lower occupancy).
-__device__ __forceinline__ uint32_t wave_max_u32v(uint32_t v) {
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, kWave));
-  return v;
-}
+__device__ __forceinline__ uint32_t wave_max_u32v(uint32_t v) { return wave_allreduce(v, OpMaxU32{}); }
 __device__ __forceinline__ uint32_t wave_min_u32v(uint32_t v) { return ~wave_max_u32v(~v); }
-__device__ __forceinline__ uint64_t wave_max_u64v(uint64_t v) {
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) {
-    const uint64_t u = (uint64_t)__shfl_xor((unsigned long long)v, o, kWave);
-    v = v > u ? v : u;
-  }
-  return v;
-}
+__device__ __forceinline__ uint64_t wave_max_u64v(uint64_t v) { return wave_allreduce(v, OpMaxU64{}); }
 __device__ __forceinline__ uint64_t wave_min_u64v(uint64_t v) { return ~wave_max_u64v(~v); }
-__device__ __forceinline__ double wave_max_f64(double v) {
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
-  return v;
-}
+__device__ __forceinline__ double wave_max_f64(double v) { return wave_allreduce(v, OpMaxF64{}); }
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) { return wave_allreduce(v, OpSumU32{}); }
 
 // Lane j of (lo, hi) := the 64-bit wave mask b (j wave-uniform).
 __device__ __forceinline__ void set_lane(uint32_t& lo, uint32_t& hi, uint64_t b, uint32_t j) {
@@ -1195,11 +1246,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     if (YODA_K1_PF && n0 < n1) load_sum(n0);
     for (uint32_t nb = n0; nb < n1; nb += kWave) node_block(nb, nb + kWave < n1 ? nb + kWave : ~0u);
   }
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) {
-    g_nf += (uint32_t)__shfl_xor((int)g_nf, o, kWave);
-    g_nz += (uint32_t)__shfl_xor((int)g_nz, o, kWave);
-  }
+  g_nf = wave_sum_u32(g_nf);
+  g_nz = wave_sum_u32(g_nz);
   nf_all += g_nf;
   nz_all += g_nz;
   blk_flush();
@@ -1211,8 +1259,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   // ALL nodes above, summed over its chunks (one add per (wave, chunk); k_lpt_order reads and
   // re-zeroes them)
   if (wts != nullptr) {
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) g_nu += (uint32_t)__shfl_xor((int)g_nu, o, kWave);
+    g_nu = wave_sum_u32(g_nu);
     const uint32_t wgt = npart + g_nu;
     if (lane == 0 && wgt != 0u) atomicAdd(wts + (p >> 6), wgt);
   }
@@ -2351,6 +2398,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // and reciprocal sets, and its outputs stay "no node".
   const bool act = live && (args.cnt == nullptr || args.cnt[p] != 0u);
   const uint64_t act_mask = ballot(act);
+  // every active lane's maxima are at most G's (its reciprocals at least G's): the K1 seed, a
+  // score under G, is then a lower bound of the wave's scores (thr below)
+  bool seed_le_g = false;
+  if constexpr (!TOPK) {
+    if (args.seed != nullptr && args.g.tab != nullptr) {
+      bool le;
+      if constexpr (Q32)
+        le = sc.r_bw >= args.g.f_bw && sc.r_core >= args.g.f_core && sc.r_pow >= args.g.f_pow;
+      else
+        le = sc.r_bw >= args.g.r_bw && sc.r_core >= args.g.r_core && sc.r_pow >= args.g.r_pow;
+      le = le && sc.r_free >= args.g.r_free && sc.r_tot >= args.g.r_tot;
+      seed_le_g = (ballot(act && !le) == 0ull);
+    }
+  }
   // Reciprocal sets: active lanes with the same (bw, core, power, free, total) reciprocals,
   // numbered in order of their first lane; up to kSets, any further lanes "overflow".
   auto rl_d = [&](double x, int l) {
@@ -2430,14 +2491,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   if (dec) {  // the bound's reciprocals into the extra RCPS slot (RS at word 0, f64 at word 8)
     RS d_bw = act ? sc.r_bw : (RS)0, d_core = act ? sc.r_core : (RS)0, d_pow = act ? sc.r_pow : (RS)0;
     double d_free = act ? sc.r_free : 0.0, d_tot = act ? sc.r_tot : 0.0;
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) {
-      d_bw = fmax(d_bw, __shfl_xor(d_bw, o, kWave));
-      d_core = fmax(d_core, __shfl_xor(d_core, o, kWave));
-      d_pow = fmax(d_pow, __shfl_xor(d_pow, o, kWave));
-      d_free = fmax(d_free, __shfl_xor(d_free, o, kWave));
-      d_tot = fmax(d_tot, __shfl_xor(d_tot, o, kWave));
+    if constexpr (Q32) {
+      d_bw = wave_allreduce(d_bw, OpMaxF32{});
+      d_core = wave_allreduce(d_core, OpMaxF32{});
+      d_pow = wave_allreduce(d_pow, OpMaxF32{});
+    } else {
+      d_bw = wave_allreduce(d_bw, OpMaxF64{});
+      d_core = wave_allreduce(d_core, OpMaxF64{});
+      d_pow = wave_allreduce(d_pow, OpMaxF64{});
     }
+    d_free = wave_allreduce(d_free, OpMaxF64{});
+    d_tot = wave_allreduce(d_tot, OpMaxF64{});
     if (lane == 0) {
       RS* r = reinterpret_cast<RS*>(lds + RCPS + 16 * kSets);
       r[0] = d_bw;
@@ -2450,13 +2514,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   }
   constexpr uint32_t KBST = kbub_stride(K);
   // The block K1's seed: a score every live pod of the wave reaches on some node it passes,
-  // under the G maxima; a pod's own maxima are never above G's (a max over fewer cards), so
-  // its score there is at least the seed whatever its maxima: no pod's best -- nor a tie of
-  // it -- lies below, and thr starts there instead of at -1.
+  // under the G maxima.  A pod whose maxima are at most G's field by field (reciprocals at
+  // least G's) scores at least as much under its own, so no pod's best -- nor a tie of it --
+  // lies below, and thr starts there instead of at -1.  On one handle that always holds (a
+  // max over fewer cards); on a node shard the exchanged maxima can exceed this shard's G
+  // (another shard holds a faster model), so the wave checks it (tests/test_gpu_shard_seeds.py).
   double thr = -1.0;
   if (prune && !TOPK && args.seed != nullptr) {
     const uint64_t sv = args.seed[uniform_u32(p >> 6)];
-    if (sv != 0ull) thr = (double)sv;  // (an integer below 2^53)
+    if (sv != 0ull && (use_g || seed_le_g)) thr = (double)sv;  // (an integer below 2^53)
   }
   // the largest free level <= the wave's smallest scv/memory: every active pod qualifies at
   // most nq(t) cards on every node, so kbub's lv[l_lo] bounds the block too (its word: lvw)

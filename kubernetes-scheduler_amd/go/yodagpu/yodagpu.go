@@ -420,8 +420,19 @@ func CommUniqueID() ([]byte, error) {
 	return id, nil
 }
 
-// DeviceBusID is the PCI bus id of this handle's GPU (yoda_device_bus_id).  Ranks exchange
-// it with the communicator id, out of band, and call CheckDevices before CommInit.
+// DeviceKey identifies this handle's GPU across hosts (yoda_device_key: a hash of the hostname
+// and boot id, '/', the PCI bus id -- bus ids alone repeat on identical servers).  Ranks
+// exchange it with the communicator id, out of band, and call CheckDevices before CommInit.
+func (g *Handle) DeviceKey() (string, error) {
+	buf := make([]byte, C.YODA_DEVICE_KEY_BYTES)
+	if err := check(g.h, C.yoda_device_key(g.h, (*C.char)(unsafe.Pointer(&buf[0])),
+		C.int(len(buf))), "yoda_device_key"); err != nil {
+		return "", err
+	}
+	return C.GoString((*C.char)(unsafe.Pointer(&buf[0]))), nil
+}
+
+// DeviceBusID is the PCI bus id of this handle's GPU (yoda_device_bus_id).
 func (g *Handle) DeviceBusID() (string, error) {
 	buf := make([]byte, C.YODA_BUS_ID_BYTES)
 	if err := check(g.h, C.yoda_device_bus_id(g.h, (*C.char)(unsafe.Pointer(&buf[0])),
@@ -431,18 +442,18 @@ func (g *Handle) DeviceBusID() (string, error) {
 	return C.GoString((*C.char)(unsafe.Pointer(&buf[0]))), nil
 }
 
-// CheckDevices takes every rank's DeviceBusID (rank order) and fails, naming the first pair,
+// CheckDevices takes every rank's DeviceKey (rank order) and fails, naming the first pair,
 // when two ranks would share one GPU (YODA_ERR_SAME_DEVICE: RCCL itself only reports an
 // "invalid usage").  Host only.
 func CheckDevices(busIDs []string) error {
 	if len(busIDs) == 0 {
 		return nil
 	}
-	stride := int(C.YODA_BUS_ID_BYTES)
+	stride := int(C.YODA_DEVICE_KEY_BYTES)
 	flat := make([]byte, stride*len(busIDs))
 	for r, id := range busIDs {
 		if len(id) >= stride {
-			return fmt.Errorf("yodagpu: bus id of rank %d too long", r)
+			return fmt.Errorf("yodagpu: device key of rank %d too long", r)
 		}
 		copy(flat[r*stride:], id)
 	}

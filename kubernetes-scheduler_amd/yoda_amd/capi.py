@@ -90,6 +90,7 @@ _SIGS = {
     "yoda_comm_unique_id": ([_vp], C.c_int),
     "yoda_comm_init": ([_vp, _vp, C.c_int, C.c_int], C.c_int),
     "yoda_device_bus_id": ([_vp, C.c_char_p, C.c_int], C.c_int),
+    "yoda_device_key": ([_vp, C.c_char_p, C.c_int], C.c_int),
     "yoda_comm_check_devices": ([C.c_char_p, C.c_int, C.c_int, _vp, _vp], C.c_int),
     "yoda_comm_run": ([_vp, C.c_int], C.c_int),
     "yoda_comm_run_local": ([_vp, C.c_int, C.c_int], C.c_int),
@@ -405,6 +406,13 @@ class Yoda:
         self._check(lib().yoda_device_bus_id(self._h, buf, BUS_ID_BYTES), "yoda_device_bus_id")
         return buf.value.decode()
 
+    def device_key(self) -> str:
+        """Host hash + '/' + PCI bus id of the handle's device (yoda_device_key): unique across
+        the hosts of a multi-node job, unlike the bus id alone."""
+        buf = C.create_string_buffer(DEVICE_KEY_BYTES)
+        self._check(lib().yoda_device_key(self._h, buf, DEVICE_KEY_BYTES), "yoda_device_key")
+        return buf.value.decode()
+
     def comm_run(self, mode: int = 0):
         """One sharded step with libyoda's own RCCL exchanges (yoda_comm_run)."""
         self._check(lib().yoda_comm_run(self._h, mode), "yoda_comm_run")
@@ -517,15 +525,18 @@ class Yoda:
 
 
 BUS_ID_BYTES = 32  # YODA_BUS_ID_BYTES
+DEVICE_KEY_BYTES = 64  # YODA_DEVICE_KEY_BYTES
 
 
 def comm_check_devices(bus_ids) -> None:
-    """Raise YodaError (YODA_ERR_SAME_DEVICE) naming the first two ranks whose devices share a
-    PCI bus id (yoda_comm_check_devices; host only).  bus_ids: one str per rank."""
+    """Raise YodaError (YODA_ERR_SAME_DEVICE) naming the first two ranks whose device keys
+    (yoda_device_key: host hash / PCI bus id) are equal (yoda_comm_check_devices; host only).
+    bus_ids: one str per rank."""
     world = len(bus_ids)
-    raw = b"".join(b.encode()[:BUS_ID_BYTES - 1].ljust(BUS_ID_BYTES, b"\0") for b in bus_ids)
+    raw = b"".join(b.encode()[:DEVICE_KEY_BYTES - 1].ljust(DEVICE_KEY_BYTES, b"\0")
+                   for b in bus_ids)
     a, b = C.c_int(-1), C.c_int(-1)
-    rc = lib().yoda_comm_check_devices(raw, world, BUS_ID_BYTES, C.byref(a), C.byref(b))
+    rc = lib().yoda_comm_check_devices(raw, world, DEVICE_KEY_BYTES, C.byref(a), C.byref(b))
     if rc == -8:
         raise YodaError(f"yoda_comm_check_devices: YODA_ERR_SAME_DEVICE: ranks {a.value} and "
                         f"{b.value} are on the same GPU ({bus_ids[a.value]}); RCCL needs one "

@@ -347,8 +347,9 @@ class LibExchange:
             agree_on_path(Reducer(group=group), [handle], [shard], [offset], device)
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         on_dev = dist.get_backend(group) == "nccl"
-        # one GPU per rank, or RCCL's init fails with a bare "invalid usage"
-        agree_on_devices(handle.bus_id(), device if on_dev else torch.device("cpu"), group)
+        # one GPU per rank, or RCCL's init fails with a bare "invalid usage" (keys: host hash
+        # and PCI bus id, so identical servers of a multi-node job do not collide)
+        agree_on_devices(handle.device_key(), device if on_dev else torch.device("cpu"), group)
         t = torch.zeros(128, dtype=torch.uint8, device=device if on_dev else "cpu")
         if rank == 0:
             t.copy_(torch.tensor(list(comm_unique_id()), dtype=torch.uint8))
@@ -362,14 +363,15 @@ class LibExchange:
         self.handle.comm_run(mode)
 
 
-def agree_on_devices(bus_id: str, device, group=None) -> list:
-    """All-gather every rank's PCI bus id and raise YodaError (YODA_ERR_SAME_DEVICE, naming the
-    ranks) when two ranks share a GPU -- before yoda_comm_init, whose RCCL init would fail on
-    it with "invalid usage".  Returns the ids in rank order."""
+def agree_on_devices(key: str, device, group=None) -> list:
+    """All-gather every rank's device key (Yoda.device_key: host hash / PCI bus id) and raise
+    YodaError (YODA_ERR_SAME_DEVICE, naming the ranks) when two ranks share a GPU -- before
+    yoda_comm_init, whose RCCL init would fail on it with "invalid usage".  Returns the keys in
+    rank order."""
     import torch.distributed as dist
-    from .capi import BUS_ID_BYTES, comm_check_devices
+    from .capi import DEVICE_KEY_BYTES, comm_check_devices
     world = dist.get_world_size(group)
-    raw = bus_id.encode()[:BUS_ID_BYTES - 1].ljust(BUS_ID_BYTES, b"\0")
+    raw = key.encode()[:DEVICE_KEY_BYTES - 1].ljust(DEVICE_KEY_BYTES, b"\0")
     mine = torch.tensor(list(raw), dtype=torch.uint8, device=device)
     every = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(every, mine, group=group)

@@ -86,3 +86,15 @@ def test_comm_check_devices_names_shared_gpu():
     assert L.yoda_comm_check_devices(None, 2, 32, None, None) == -1
     assert L.yoda_comm_check_devices(b"\0" * 64, 2, 32, None, None) == -1  # empty id
     assert L.yoda_device_bus_id(None, None, 0) == -1
+    assert L.yoda_device_key(None, None, 0) == -1
+
+
+def test_comm_check_devices_multi_host_keys():
+    """PCI bus ids repeat across identical servers, so the check compares device
+    keys (yoda_device_key: host hash / bus id) -- the same bus id on two hosts passes, the same
+    (host, bus id) pair is still refused."""
+    import pytest
+    a, b = "0123456789abcdef/0000:c1:00.0", "fedcba9876543210/0000:c1:00.0"
+    capi.comm_check_devices([a, b])
+    with pytest.raises(capi.YodaError, match=r"SAME_DEVICE: ranks 0 and 2"):
+        capi.comm_check_devices([a, b, a])

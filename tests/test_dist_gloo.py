@@ -213,13 +213,18 @@ def _devices_worker(rank, world, port, q, ids):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("shared", [False, True])
+@pytest.mark.parametrize("shared", ["no", "yes", "other_host"])
 def test_gloo_agree_on_devices(shared):
     """dist.agree_on_devices (LibExchange runs it before yoda_comm_init): the ranks all-gather
-    their PCI bus ids; two ranks on one GPU make EVERY rank raise YODA_ERR_SAME_DEVICE naming
-    them (so no rank goes on into RCCL's init alone)."""
+    their device keys (host hash / PCI bus id); two ranks on one GPU make EVERY rank raise
+    YODA_ERR_SAME_DEVICE naming them (so no rank goes on into RCCL's init alone), while the
+    same bus id on another host (identical servers of a multi-node job) passes."""
     world = 3
-    ids = ["0000:05:00.0", "0000:15:00.0", "0000:05:00.0" if shared else "0000:25:00.0"]
+    h0, h1 = "00000000000000aa/", "00000000000000bb/"
+    third = {"no": h0 + "0000:25:00.0", "yes": h0 + "0000:05:00.0",
+             "other_host": h1 + "0000:05:00.0"}[shared]
+    ids = [h0 + "0000:05:00.0", h0 + "0000:15:00.0", third]
+    shared = shared == "yes"
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

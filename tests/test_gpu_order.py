@@ -102,3 +102,28 @@ def test_repeated_runs_identical(dev):
         again = dev.eval(pods, MODE_SCV)
         for f in ("pick", "status", "n_feasible", "n_ties", "top_score", "maxima"):
             np.testing.assert_array_equal(getattr(first, f), getattr(again, f), err_msg=f)
+
+
+def test_deferred_upload_alternating_batches(dev):
+    """a fast private run reads only the 5 core pod arrays; the rest of the batch
+    (f64 / u64 thresholds, Mode-B weights) reaches the device after its kernels.  Alternate two
+    different batches through yoda_run, then read the deferred arrays through entry points that
+    need them (Mode B, the U64-path score rows): every result == the oracle's for its batch."""
+    nodes, pods_a = synth.make_config(3, pods=6000, nodes=3000)
+    pods_b = synth.distinct_diskio(synth.make_pods(5000, seed=77))
+    dev.upload_nodes(nodes)
+    want = {k: oracle.schedule(nodes, p, MODE_SCV, threads=8)
+            for k, p in (("a", pods_a), ("b", pods_b))}
+    for k in ("a", "b", "a", "b"):
+        pods = pods_a if k == "a" else pods_b
+        assert_same(dev.eval(pods, MODE_SCV), want[k])
+    # batch b uploaded once: a fast Mode-A run, then on the same upload a Mode-B run (alpha /
+    # beta) and a bitmask run (not a fast run: the F64 thresholds), each against the oracle
+    dev.upload_pods(pods_b)
+    dev.run(MODE_SCV)
+    assert_same(dev.download(), want["b"])
+    dev.run(1)
+    assert_same(dev.download(), oracle.schedule(nodes, pods_b, 1, threads=8), 1)
+    dev.run(MODE_SCV, bitmask=True)
+    assert_same(dev.download(), want["b"])
+    assert_same(dev.eval(pods_a, MODE_SCV), want["a"])

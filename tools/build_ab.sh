@@ -9,7 +9,7 @@ NAME=$1; shift
 mkdir -p $ROOT/abl
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize"
 T=$(mktemp -d)
-/opt/rocm/bin/hipcc $F "$@" -c -o $T/k.o $SRC/yoda_kernels.hip
+/opt/rocm/bin/hipcc $F -DYODA_AB_KNOBS "$@" -c -o $T/k.o $SRC/yoda_kernels.hip
 /opt/rocm/bin/hipcc $F -c -o $T/o.o $SRC/yoda_order.hip
 /opt/rocm/bin/hipcc $F -DYODA_AB_KNOBS -c -o $T/c.o $SRC/yoda_capi.cpp
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/abl/$NAME.so $T/k.o $T/o.o $T/c.o
