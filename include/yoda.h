@@ -237,6 +237,13 @@ int yoda_score_rows_norm(yoda_t* h, int mode, uint32_t* bitmask, uint64_t n_bitm
  *            u32, d_lowest [P] i64 (MIN)
  *   prepare_merge (reads reduced d_best) -> masks d_idx (MIN) and d_ties (SUM) in place
  *   finalize (reads reduced buffers) -> picks into the handle, then yoda_download. */
+/* yoda_shard_exchange_order(h, 1): the exchange buffers above are in the CALLER's pod order
+ * (the order of yoda_upload_pods), so each shard sorts its pods and nodes privately -- the
+ * padded counting order and block-grouped node order of yoda_run -- instead of the
+ * reproducible radix order all shards must otherwise share (one shard of config 3: 5.7x
+ * faster).  Every shard of a batch must use the same setting.  Evaluation batches only (the
+ * greedy-window entry points below refuse it); the U64 record path ignores it.  Default 0. */
+int yoda_shard_exchange_order(yoda_t* h, int caller_order);
 int yoda_shard_phase1(yoda_t* h, int mode, uint64_t* d_maxima, uint32_t* d_counts);
 int yoda_shard_phase2(yoda_t* h, int mode, const uint64_t* d_maxima, const uint32_t* d_counts,
                       int64_t* d_best, uint32_t* d_idx, uint32_t* d_ties, int64_t* d_lowest);

@@ -505,6 +505,14 @@ struct yoda_handle {
   ncclComm_t comm = nullptr;
   int comm_rank = 0, comm_world = 1;
   DevBuf ex1, rec, rec_all;  // [maxima 6P | count slots world x P] u64; ShardRec [P], [world][P]
+  // Caller-order exchange (xo): a node-shard evaluation whose exchanged buffers are in the
+  // caller's pod order, so that each shard runs its private order -- the padded counting sort
+  // and the block-grouped node order of yoda_run -- instead of the reproducible radix order
+  // every shard must otherwise share (5.7x slower at one shard of config 3: no node grouping,
+  // no padded waves).  yoda_comm_run does it on the fast record paths; the yoda_shard_* calls
+  // after yoda_shard_exchange_order(h, 1).  xcnt, xbest, ... : the caller-order copies.
+  bool xo_enabled = false, xo = false;
+  DevBuf xcnt, xbest, xidx, xties, xlow;
   DevBuf cg_max, cg_cnt, cg_wit, cg_gather;  // yoda_comm_greedy: exchange buffers
   uint32_t comm_greedy_stats[5] = {};          // yoda_comm_greedy_stats
   // sharded exact normalize (K3 over a shard): per-pod records of the flagged pods, pending
@@ -549,7 +557,8 @@ struct yoda_handle {
                      &p_wit,     &wit,       &stats_dev, &one_feas,  &one_part,  &one_done,
                      &ex1,       &rec,       &rec_all,   &cg_max,    &cg_cnt,    &cg_wit,    &cg_gather, &k3rec,     &k3all,
                      &one_out,   &b_cab,     &b_cls,     &b_part,
-                     &counts_alt, &best_alt, &maxima_alt, &win_dev};
+                     &counts_alt, &best_alt, &maxima_alt, &win_dev,
+                     &xcnt,      &xbest,     &xidx,      &xties,     &xlow};
     for (DevBuf* b : all) b->release();
     pod_stage.release();
     upd_stage.release();
@@ -1159,6 +1168,53 @@ int unpermute_outputs(yoda_t* h) {
   }
   HIP_TRY(h, launch_permute(t, h->perm.as<uint32_t>(), W, true, h->stream));
   for (const Arr& a : arrs) std::swap(*a.buf, *a.alt);
+  return YODA_OK;
+}
+
+// Caller-order exchange (yoda_t::xo): rows of a run's sorted-order arrays (n_work positions)
+// to the caller's pod order (n_pods) or back.  A sorted position that pads a group is a copy
+// of its pod (the same values), so the scatter writes some caller slots twice, identically.
+// A run left unordered is already in caller order: plain copies.
+struct XArr {
+  void* sorted;  // [rows][n_work]
+  void* caller;  // [rows][n_pods]
+  uint32_t rows, bytes;
+};
+int xfer(yoda_t* h, bool to_caller, std::initializer_list<XArr> arrs) {
+  const uint32_t P = h->n_pods, W = h->n_work;
+  if (P == 0) return YODA_OK;
+  PermTable t{};
+  for (const XArr& a : arrs)
+    for (uint32_t r = 0; r < a.rows; ++r) {
+      unsigned char* sp = static_cast<unsigned char*>(a.sorted) + (size_t)r * W * a.bytes;
+      unsigned char* cp = static_cast<unsigned char*>(a.caller) + (size_t)r * P * a.bytes;
+      if (!h->ordered) {
+        if (sp != cp)
+          HIP_TRY(h, hipMemcpyAsync(to_caller ? cp : sp, to_caller ? sp : cp, (size_t)P * a.bytes,
+                                    hipMemcpyDeviceToDevice, h->stream));
+        continue;
+      }
+      if (t.n == kPermArrays) {
+        HIP_TRY(h, launch_permute(t, h->perm.as<uint32_t>(), W, to_caller, h->stream));
+        t = PermTable{};
+      }
+      t.src[t.n] = to_caller ? sp : cp;
+      t.dst[t.n] = to_caller ? cp : sp;
+      t.bytes[t.n] = a.bytes;
+      ++t.n;
+    }
+  if (t.n) HIP_TRY(h, launch_permute(t, h->perm.as<uint32_t>(), W, to_caller, h->stream));
+  return YODA_OK;
+}
+
+int xo_ensure(yoda_t* h) {
+  if (!h->xo) return YODA_OK;
+  const size_t P = std::max<uint32_t>(h->n_pods, 1);
+  HIP_TRY(h, h->xcnt.ensure(2 * P * 4));
+  HIP_TRY(h, h->xbest.ensure(P * 8));
+  HIP_TRY(h, h->xidx.ensure(P * 4));
+  HIP_TRY(h, h->xties.ensure(P * 4));
+  HIP_TRY(h, h->xlow.ensure(P * 8));
   return YODA_OK;
 }
 
@@ -3082,13 +3138,29 @@ int yoda_eval(yoda_t* h, const yoda_pod_soa* pods, int mode, yoda_eval_out* out)
 }
 
 // ---- sharded entry points -------------------------------------------------------------
+int yoda_shard_exchange_order(yoda_t* h, int caller_order) {
+  if (!h || (caller_order != 0 && caller_order != 1)) return YODA_ERR_INVALID_ARG;
+  h->xo_enabled = caller_order == 1;
+  return YODA_OK;
+}
+
 int yoda_shard_phase1(yoda_t* h, int mode, uint64_t* d_maxima, uint32_t* d_counts) {
-  int rc = prepare_run(h, mode);
+  if (!h) return YODA_ERR_INVALID_ARG;
+  // caller-order exchange (yoda_shard_exchange_order): each shard its private order; not on the
+  // U64 path (its exact-normalize records are per sorted position)
+  h->xo = h->xo_enabled && !h->generic;
+  int rc = prepare_run(h, mode, h->xo);
   if (rc) return rc;
   if (!d_maxima || !d_counts) return fail(h, YODA_ERR_INVALID_ARG, "NULL exchange buffer");
   try {
     if ((rc = order_pods(h, mode))) return rc;
-    if ((rc = phase1(h, mode, d_maxima, d_counts))) return rc;
+    if (h->xo) {
+      if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>()))) return rc;
+      if ((rc = xfer(h, true, {{h->maxima.p, d_maxima, 6, 8}, {h->counts.p, d_counts, 2, 4}})))
+        return rc;
+    } else if ((rc = phase1(h, mode, d_maxima, d_counts))) {
+      return rc;
+    }
     h->phase1_done = true;
     h->phase1_wit = false;
     h->ran = false;
@@ -3107,6 +3179,17 @@ int yoda_shard_phase2(yoda_t* h, int mode, const uint64_t* d_maxima, const uint3
     return fail(h, YODA_ERR_INVALID_ARG, "NULL exchange buffer");
   try {
     const uint32_t P = h->n_pods;
+    if (h->xo) {  // the reduced caller-order buffers into this run's order, and back
+      int rc2 = xfer(h, false, {{h->maxima.p, const_cast<uint64_t*>(d_maxima), 6, 8},
+                                {h->counts.p, const_cast<uint32_t*>(d_counts), 2, 4}});
+      if (rc2) return rc2;
+      if ((rc2 = phase2(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(),
+                        h->best.as<int64_t>(), h->idx.as<uint32_t>(), h->ties.as<uint32_t>(),
+                        h->lowest.as<int64_t>())))
+        return rc2;
+      return xfer(h, true, {{h->best.p, d_best, 1, 8}, {h->idx.p, d_idx, 1, 4},
+                            {h->ties.p, d_ties, 1, 4}, {h->lowest.p, d_lowest, 1, 8}});
+    }
     // keep the reduced maxima for download and the generic exact-normalize pass
     if (P) HIP_TRY(h, hipMemcpyAsync(h->maxima.p, d_maxima, 6ull * P * 8, hipMemcpyDeviceToDevice,
                                      h->stream));
@@ -3136,14 +3219,27 @@ int yoda_shard_finalize(yoda_t* h, int mode, const uint32_t* d_counts, const int
     return fail(h, YODA_ERR_INVALID_ARG, "NULL exchange buffer");
   try {
     const uint32_t P = h->n_pods;
-    if (P) {
-      HIP_TRY(h, hipMemcpyAsync(h->counts.p, d_counts, 2ull * P * 4, hipMemcpyDeviceToDevice,
-                                h->stream));
-      HIP_TRY(h, hipMemcpyAsync(h->best.p, d_best, P * 8ull, hipMemcpyDeviceToDevice, h->stream));
+    if (h->xo) {  // the merged caller-order buffers into this run's order
+      if ((rc = xfer(h, false, {{h->counts.p, const_cast<uint32_t*>(d_counts), 2, 4},
+                                {h->best.p, const_cast<int64_t*>(d_best), 1, 8},
+                                {h->idx.p, const_cast<uint32_t*>(d_idx), 1, 4},
+                                {h->ties.p, const_cast<uint32_t*>(d_ties), 1, 4},
+                                {h->lowest.p, const_cast<int64_t*>(d_lowest), 1, 8}})))
+        return rc;
+      if ((rc = finalize(h, mode, h->counts.as<uint32_t>(), h->best.as<int64_t>(),
+                         h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(),
+                         true)))
+        return rc;
+    } else {
+      if (P) {
+        HIP_TRY(h, hipMemcpyAsync(h->counts.p, d_counts, 2ull * P * 4, hipMemcpyDeviceToDevice,
+                                  h->stream));
+        HIP_TRY(h, hipMemcpyAsync(h->best.p, d_best, P * 8ull, hipMemcpyDeviceToDevice, h->stream));
+      }
+      if ((rc = finalize(h, mode, h->counts.as<uint32_t>(), h->best.as<int64_t>(), d_idx, d_ties,
+                         d_lowest, true)))
+        return rc;
     }
-    if ((rc = finalize(h, mode, h->counts.as<uint32_t>(), h->best.as<int64_t>(), d_idx, d_ties,
-                       d_lowest, true)))
-      return rc;
     h->ran = true;
     h->ran_bitmask = false;
     h->last_mode = mode;
@@ -3958,6 +4054,9 @@ int shard_topk_impl(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_count
                     uint32_t deep, uint32_t* counts, double* top_score, uint32_t* top_node) {
   int rc = check_ready(h, YODA_MODE_SCV);
   if (rc) return rc;
+  if (h->xo)  // (the window top-k reads the shared radix order's buffers)
+    return fail(h, YODA_ERR_STATE, "yoda_shard_topk after a caller-order phase 1: turn "
+                                   "yoda_shard_exchange_order off for greedy windows");
   if (!h->phase1_done) return fail(h, YODA_ERR_STATE, "yoda_shard_topk before yoda_shard_phase1");
   if (h->generic)
     return fail(h, YODA_ERR_STATE, "top-k lists need a fast record path (N32 or F64)");
@@ -4022,6 +4121,8 @@ int shard_topk_impl(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_count
 
 int yoda_shard_phase1_witness(yoda_t* h, uint64_t* d_maxima, uint32_t* d_counts,
                               uint32_t* d_wit) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  h->xo = false;  // (greedy windows: the shared radix order)
   int rc = prepare_run(h, YODA_MODE_SCV);
   if (rc) return rc;
   if (h->generic)
@@ -5185,15 +5286,26 @@ static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local) 
   for (int i = 0; i < n; ++i) {
     yoda_t* h = hs[i];
     if (h->n_pods != P) return fail(h0, YODA_ERR_INVALID_ARG, "shards hold different batches");
-    int rc = prepare_run(h, mode);
+    // the fast record paths exchange in the caller's pod order, so each shard runs its private
+    // order (padded counting sort, block-grouped nodes: xfer); the U64 path, whose exact-
+    // normalize records go per sorted position, keeps the radix order all shards share
+    h->xo = !h->generic;
+    int rc = prepare_run(h, mode, h->xo);
     if (rc) return rc;
     if ((rc = order_pods(h, mode))) return rc;
     HIP_TRY(h, h->ex1.ensure(n1 * 8));
     HIP_TRY(h, h->rec.ensure((size_t)std::max<uint32_t>(P, 1) * sizeof(ShardRec)));
     HIP_TRY(h, h->rec_all.ensure((size_t)world * std::max<uint32_t>(P, 1) * sizeof(ShardRec)));
+    if ((rc = xo_ensure(h))) return rc;
     if (P == 0) continue;
     uint64_t* ex = h->ex1.as<uint64_t>();
-    if ((rc = phase1(h, mode, ex, h->counts.as<uint32_t>()))) return rc;
+    if (h->xo) {
+      if ((rc = phase1(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>()))) return rc;
+      if ((rc = xfer(h, true, {{h->maxima.p, ex, 6, 8}, {h->counts.p, h->xcnt.p, 2, 4}})))
+        return rc;
+    } else if ((rc = phase1(h, mode, ex, h->counts.as<uint32_t>()))) {
+      return rc;
+    }
     // agreement words (pinned staging, one slot per shard; the previous step's copies
     // finished before its read-back below)
     uint64_t agree[kAgreeWords];
@@ -5209,11 +5321,17 @@ static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local) 
     for (int i = 0; i < n; ++i) hs[i]->ran = true;
     return YODA_OK;
   }
+  // the caller-order views of the exchanged buffers (the handle's own ones on the U64 path)
+  auto cnt_x = [](yoda_t* h) { return h->xo ? h->xcnt.as<uint32_t>() : h->counts.as<uint32_t>(); };
+  auto best_x = [](yoda_t* h) { return h->xo ? h->xbest.as<int64_t>() : h->best.as<int64_t>(); };
+  auto idx_x = [](yoda_t* h) { return h->xo ? h->xidx.as<uint32_t>() : h->idx.as<uint32_t>(); };
+  auto ties_x = [](yoda_t* h) { return h->xo ? h->xties.as<uint32_t>() : h->ties.as<uint32_t>(); };
+  auto low_x = [](yoda_t* h) { return h->xo ? h->xlow.as<int64_t>() : h->lowest.as<int64_t>(); };
   if (local) {  // exchange 1: elementwise MAX / SUM over the shards, back to each
     PtrList l{}, c{};
     for (int i = 0; i < n; ++i) {
       l.p[i] = hs[i]->ex1.p;
-      c.p[i] = hs[i]->counts.p;
+      c.p[i] = cnt_x(hs[i]);
     }
     HIP_TRY(h0, h0->rec.ensure(std::max<size_t>(2 * (size_t)P * 4, (size_t)P * sizeof(ShardRec))));
     HIP_TRY(h0, launch_max_multi(l, (uint32_t)n, n1, h0->ex1.as<uint64_t>(), h0->stream));
@@ -5223,14 +5341,14 @@ static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local) 
       if (i > 0)
         HIP_TRY(h0, hipMemcpyAsync(hs[i]->ex1.p, h0->ex1.p, n1 * 8, hipMemcpyDeviceToDevice,
                                    h0->stream));
-      HIP_TRY(h0, hipMemcpyAsync(hs[i]->counts.p, h0->rec.p, 2 * (size_t)P * 4,
+      HIP_TRY(h0, hipMemcpyAsync(cnt_x(hs[i]), h0->rec.p, 2 * (size_t)P * 4,
                                  hipMemcpyDeviceToDevice, h0->stream));
     }
   } else {
     rccl().group_start();
     ncclResult_t r = rccl().all_reduce(h0->ex1.p, h0->ex1.p, n1, ncclUint64, ncclMax, h0->comm,
                                        h0->stream);
-    const ncclResult_t r2 = rccl().all_reduce(h0->counts.p, h0->counts.p, 2 * (size_t)P,
+    const ncclResult_t r2 = rccl().all_reduce(cnt_x(h0), cnt_x(h0), 2 * (size_t)P,
                                               ncclUint32, ncclSum, h0->comm, h0->stream);
     const ncclResult_t r3 = rccl().group_end();
     if (r == ncclSuccess) r = r2;
@@ -5252,17 +5370,25 @@ static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local) 
   for (int i = 0; i < n; ++i) {
     yoda_t* h = hs[i];
     uint64_t* ex = h->ex1.as<uint64_t>();
-    HIP_TRY(h, hipMemcpyAsync(h->maxima.p, ex, 6 * (size_t)P * 8, hipMemcpyDeviceToDevice,
-                              h->stream));
-    int rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), h->best.as<int64_t>(),
-                    h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>());
+    int rc;
+    if (h->xo) {
+      if ((rc = xfer(h, false, {{h->maxima.p, ex, 6, 8}, {h->counts.p, h->xcnt.p, 2, 4}})))
+        return rc;
+    } else {
+      HIP_TRY(h, hipMemcpyAsync(h->maxima.p, ex, 6 * (size_t)P * 8, hipMemcpyDeviceToDevice,
+                                h->stream));
+    }
+    rc = phase2(h, mode, h->maxima.as<uint64_t>(), h->counts.as<uint32_t>(), h->best.as<int64_t>(),
+                h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>());
     if (rc) return rc;
+    if (h->xo && (rc = xfer(h, true, {{h->best.p, h->xbest.p, 1, 8}, {h->idx.p, h->xidx.p, 1, 4},
+                                      {h->ties.p, h->xties.p, 1, 4},
+                                      {h->lowest.p, h->xlow.p, 1, 8}})))
+      return rc;
     if (packed)
-      HIP_TRY(h, launch_pack_key(h->best.as<int64_t>(), h->idx.as<uint32_t>(), P, ib,
-                                 h->rec.as<uint64_t>(), h->stream));
+      HIP_TRY(h, launch_pack_key(best_x(h), idx_x(h), P, ib, h->rec.as<uint64_t>(), h->stream));
     else
-      HIP_TRY(h, launch_pack_rec(h->best.as<int64_t>(), h->idx.as<uint32_t>(),
-                                 h->ties.as<uint32_t>(), h->lowest.as<int64_t>(), P,
+      HIP_TRY(h, launch_pack_rec(best_x(h), idx_x(h), ties_x(h), low_x(h), P,
                                  h->rec.as<ShardRec>(), h->stream));
   }
   if (packed) {  // exchange 2: MAX of the keys, then SUM of the winners' ties
@@ -5281,19 +5407,18 @@ static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local) 
     }
     for (int i = 0; i < n; ++i) {
       yoda_t* h = hs[i];
-      HIP_TRY(h, launch_unpack_key(h->rec.as<uint64_t>(), P, ib, h->best.as<int64_t>(),
-                                   h->idx.as<uint32_t>(), h->ties.as<uint32_t>(),
-                                   h->lowest.as<int64_t>(), h->stream));
+      HIP_TRY(h, launch_unpack_key(h->rec.as<uint64_t>(), P, ib, best_x(h), idx_x(h), ties_x(h),
+                                   low_x(h), h->stream));
     }
     if (local) {
       PtrList t{};
-      for (int i = 0; i < n; ++i) t.p[i] = hs[i]->ties.p;
+      for (int i = 0; i < n; ++i) t.p[i] = ties_x(hs[i]);
       HIP_TRY(h0, launch_sum_multi_u32(t, (uint32_t)n, P, h0->rec_all.as<uint32_t>(), h0->stream));
       for (int i = 0; i < n; ++i)
-        HIP_TRY(h0, hipMemcpyAsync(hs[i]->ties.p, h0->rec_all.p, (size_t)P * 4,
+        HIP_TRY(h0, hipMemcpyAsync(ties_x(hs[i]), h0->rec_all.p, (size_t)P * 4,
                                    hipMemcpyDeviceToDevice, h0->stream));
     } else {
-      const ncclResult_t r = rccl().all_reduce(h0->ties.p, h0->ties.p, P, ncclUint32, ncclSum,
+      const ncclResult_t r = rccl().all_reduce(ties_x(h0), ties_x(h0), P, ncclUint32, ncclSum,
                                                h0->comm, h0->stream);
       if (r != ncclSuccess)
         return fail(h0, YODA_ERR_HIP, std::string("ncclAllReduce: ") + rccl().error_string(r));
@@ -5313,16 +5438,19 @@ static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local) 
     }
     for (int i = 0; i < n; ++i) {
       yoda_t* h = hs[i];
-      HIP_TRY(h, launch_merge_rec(h->rec_all.as<ShardRec>(), P, (uint32_t)world,
-                                  h->best.as<int64_t>(), h->idx.as<uint32_t>(),
-                                  h->ties.as<uint32_t>(), h->lowest.as<int64_t>(), h->stream));
+      HIP_TRY(h, launch_merge_rec(h->rec_all.as<ShardRec>(), P, (uint32_t)world, best_x(h),
+                                  idx_x(h), ties_x(h), low_x(h), h->stream));
     }
   }
   for (int i = 0; i < n; ++i) {
     yoda_t* h = hs[i];
-    int rc = finalize(h, mode, h->counts.as<uint32_t>(), h->best.as<int64_t>(),
-                      h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(),
-                      true);
+    int rc;
+    if (h->xo && (rc = xfer(h, false, {{h->best.p, h->xbest.p, 1, 8}, {h->idx.p, h->xidx.p, 1, 4},
+                                       {h->ties.p, h->xties.p, 1, 4},
+                                       {h->lowest.p, h->xlow.p, 1, 8}})))
+      return rc;
+    rc = finalize(h, mode, h->counts.as<uint32_t>(), h->best.as<int64_t>(),
+                  h->idx.as<uint32_t>(), h->ties.as<uint32_t>(), h->lowest.as<int64_t>(), true);
     if (rc) return rc;
     h->ran = true;
     h->ran_bitmask = false;

@@ -53,6 +53,7 @@ _SIGS = {
                              C.c_int),
     "yoda_score_rows": ([_vp, C.c_int, C.POINTER(C.c_uint32), C.c_uint64,
                          C.POINTER(C.c_int64), C.c_uint64], C.c_int),
+    "yoda_shard_exchange_order": ([_vp, C.c_int], C.c_int),
     "yoda_shard_phase1": ([_vp, C.c_int, _vp, _vp], C.c_int),
     "yoda_shard_phase2": ([_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "yoda_shard_prepare_merge": ([_vp, _vp, _vp, _vp, _vp], C.c_int),
@@ -416,6 +417,12 @@ class Yoda:
     def comm_run(self, mode: int = 0):
         """One sharded step with libyoda's own RCCL exchanges (yoda_comm_run)."""
         self._check(lib().yoda_comm_run(self._h, mode), "yoda_comm_run")
+
+    def shard_exchange_order(self, caller_order: bool):
+        """Exchange buffers of the yoda_shard_* evaluation in the caller's pod order, each shard
+        sorting privately (yoda_shard_exchange_order; evaluation batches only)."""
+        self._check(lib().yoda_shard_exchange_order(self._h, 1 if caller_order else 0),
+                    "yoda_shard_exchange_order")
 
     def shard_phase1(self, mode: int, d_maxima: int, d_counts: int):
         self._check(lib().yoda_shard_phase1(self._h, mode, _vp(d_maxima), _vp(d_counts)),

@@ -244,7 +244,8 @@ def agree_on_path(reduce: Reducer, handles, shards, offsets, device):
 class ShardExchange:
     """Drives libyoda handles (one per shard) through the sharded entry points."""
 
-    def __init__(self, handles, reducer: Reducer, device, path_code=None, compact: bool = True):
+    def __init__(self, handles, reducer: Reducer, device, path_code=None, compact: bool = True,
+                 caller_order: bool = True):
         self.handles = list(handles)
         self.reduce = reducer
         self.device = device
@@ -269,16 +270,20 @@ class ShardExchange:
         stream = torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0
         for h in self.handles:
             h.set_stream(stream)
+            # the exchanged buffers in the caller's pod order: each shard sorts its pods and
+            # nodes privately, as yoda_run does (the U64 path keeps the shared radix order)
+            h.shard_exchange_order(caller_order)
 
     @classmethod
-    def local(cls, handles, device, shards=None, offsets=None, compact: bool = True):
+    def local(cls, handles, device, shards=None, offsets=None, compact: bool = True,
+              caller_order: bool = True):
         """Several shards in one process (single-GPU testing).  Pass the node shards to
         enforce a common record path."""
         red = Reducer(local=True)
         path = None
         if shards is not None:
             path = agree_on_path(red, handles, shards, offsets, device)
-        return cls(handles, red, device, path, compact=compact)
+        return cls(handles, red, device, path, compact=compact, caller_order=caller_order)
 
     @classmethod
     def distributed(cls, handle, device, shard=None, offset=0, group=None):

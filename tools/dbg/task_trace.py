@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Per-(wave, chunk) task durations of the block K1 or K2 on one batch (GPU box).
+
+The kernels stamp each task's start / end with s_memrealtime (100 MHz) when YODA_K2_TRACE=<slots>
+is set (YODA_K1_TRACE=1: the K1 records instead of the K2).  Prints the task count, the duration
+distribution, the kernel's span, the mean concurrency (sum of task durations / span) and the
+durations split by per-pod work (npart = 0: the task's fixed cost plus its lane = block pass).
+
+    YODA_K2_TRACE=200000 [YODA_K1_TRACE=1] python tools/dbg/task_trace.py [--pods P] [--nodes N]
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(REPO, "kubernetes-scheduler_amd"))
+import numpy as np  # noqa: E402
+
+from yoda_amd import synth  # noqa: E402
+from yoda_amd.capi import Yoda  # noqa: E402
+from yoda_amd.soa import MODE_SCV  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--pods", type=int, default=None)
+ap.add_argument("--nodes", type=int, default=None)
+ap.add_argument("--variant", default=None, help="a synth.VARIANTS name instead of config 3")
+a = ap.parse_args()
+slots = int(os.environ.get("YODA_K2_TRACE", "0"))
+if slots <= 0:
+    raise SystemExit("set YODA_K2_TRACE=<slots> (and YODA_K1_TRACE=1 for K1)")
+kern = "k1" if os.environ.get("YODA_K1_TRACE") else "k2"
+if a.variant:
+    _, nodes, pods, _, kw = next(synth.variant_workloads([a.variant]))
+else:
+    nodes, pods = synth.make_config(3, pods=a.pods, nodes=a.nodes)
+    kw = {}
+y = Yoda(0)
+y.upload_nodes(nodes, **kw)
+y.upload_pods(pods)
+y.run(MODE_SCV)
+y.run(MODE_SCV)
+y.class_stats(True)
+y.run(MODE_SCV)
+y.class_stats(False)
+tr = y.k2_trace(slots)
+y.close()
+used = tr[:, 1] > 0
+t = tr[used].astype(np.int64)
+dur = (t[:, 1] - t[:, 0]) / 100.0  # us at 100 MHz
+span = (t[:, 1].max() - t[:, 0].min()) / 100.0
+npart = t[:, 2]
+q = lambda v, x: float(np.percentile(v, x)) if len(v) else None  # noqa: E731
+out = {"kernel": kern, "tasks": int(used.sum()), "span_us": span,
+       "mean_concurrency": float(dur.sum() / span) if span > 0 else None,
+       "dur_us": {"mean": float(dur.mean()), "p10": q(dur, 10), "p50": q(dur, 50),
+                  "p90": q(dur, 90), "p99": q(dur, 99), "max": float(dur.max())},
+       "npart0": {"tasks": int((npart == 0).sum()), "mean_us": float(dur[npart == 0].mean())
+                  if (npart == 0).any() else None},
+       "npart_pos": {"tasks": int((npart > 0).sum()), "mean_us": float(dur[npart > 0].mean())
+                     if (npart > 0).any() else None, "mean_npart": float(npart[npart > 0].mean())
+                     if (npart > 0).any() else None},
+       "corr_dur_npart": float(np.corrcoef(dur, npart)[0, 1]) if len(dur) > 2 else None}
+# start-time profile: how many tasks start in each tenth of the span
+st = (t[:, 0] - t[:, 0].min()) / 100.0
+out["starts_by_tenth"] = np.histogram(st, bins=10, range=(0, span))[0].tolist()
+out["ends_by_tenth"] = np.histogram((t[:, 1] - t[:, 0].min()) / 100.0, bins=10, range=(0, span))[0].tolist()
+print(json.dumps(out), flush=True)
