@@ -6,9 +6,9 @@ bit-exact picks.  One step = feasibility + PreScore maxima + score + NormalizeSc
 ALL P pods over ALL N nodes (percentageOfNodesToScore 100), node snapshot and pods already
 resident in HBM, picks left in device memory.  Workload: BASELINE config 3 (100k pods x 100k
 nodes, K=8, seed 7; synthetic data).  --gpus N (strong scaling: total work fixed): by
-default the nodes are sharded across ranks and the per-pod results merged with RCCL
-all-reduces (yoda_amd/dist.py); --shard pods gives each rank a pod slice and the whole node
-snapshot instead, with no collective (dist.pod_partition).
+default each rank evaluates a pod slice against the whole node snapshot, with no collective
+(dist.pod_partition); --shard nodes shards the nodes instead and merges the per-pod results
+with RCCL all-reduces (libyoda's yoda_comm_run, or yoda_amd/dist.py over torch).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -508,16 +508,21 @@ def main():
     ap.add_argument("--check", action="store_true",
                     help="N>1: rank 0 re-evaluates the batch on one unsharded handle and "
                          "asserts identical picks / statuses / ties (rehearsal)")
-    ap.add_argument("--shard", choices=["nodes", "pods"], default="nodes",
-                    help="--gpus N > 1: nodes = node blocks merged by RCCL all-reduces "
-                         "(yoda_amd/dist.py); pods = each rank evaluates a pod slice against "
-                         "the whole node snapshot, no collective (dist.pod_partition; slower "
-                         "per rank on one MI355X, profiles/r01/current/shard_timing.txt)")
-    ap.add_argument("--exchange", choices=["torch", "libyoda"], default="torch",
-                    help="--shard nodes: torch = RCCL all-reduces through torch.distributed "
-                         "(yoda_amd/dist.py ShardExchange: int32 maxima MAX + counts SUM, the "
-                         "packed (score, node) key MAX + ties SUM; 4.4 MB at 100k pods); libyoda = "
-                         "libyoda's own RCCL exchanges (yoda_comm_run, 2 collectives per step)")
+    ap.add_argument("--shard", choices=["nodes", "pods"], default="pods",
+                    help="--gpus N > 1: pods (default) = each rank evaluates a pod slice "
+                         "against the whole node snapshot, no collective (dist.pod_partition); "
+                         "nodes = node blocks merged by RCCL all-reduces, the north_star's "
+                         "packed-key merge (yoda_amd/dist.py).  Default from the one-GPU rank "
+                         "probes of tools/rank_probe.py (DESIGN.md §7, profiles/r06/rank8/): "
+                         "at 8 ranks the slowest pod rank takes 0.36 ms, a node rank 0.35 ms "
+                         "before its three collectives")
+    ap.add_argument("--exchange", choices=["torch", "libyoda"], default="libyoda",
+                    help="--shard nodes: libyoda (default) = libyoda's own RCCL exchanges "
+                         "(yoda_comm_run: maxima MAX + counts SUM in one group, the packed "
+                         "(score, node) key MAX, the winners' ties SUM; fused pack/unpack "
+                         "kernels); torch = the same merge through torch.distributed "
+                         "(yoda_amd/dist.py ShardExchange, elementwise torch ops around it: "
+                         "0.43 vs 0.35 ms per 8-way rank on the probe)")
     ap.add_argument("--no-balance", action="store_true",
                     help="--shard nodes: keep equal node blocks (default: re-cut them once "
                          "after warm-up so every rank's measured K1 + K2 time is equal)")

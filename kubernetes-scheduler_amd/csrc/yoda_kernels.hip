@@ -325,6 +325,7 @@ struct OpMaxU32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const {
 struct OpMaxU64 { __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return a > b ? a : b; } };
 struct OpSumU32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; } };
 struct OpMaxF64 { __device__ double operator()(double a, double b) const { return fmax(a, b); } };
+struct OpMinF64 { __device__ double operator()(double a, double b) const { return fmin(a, b); } };
 struct OpMaxF32 { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return uniform_u32(wave_allreduce(v, OpMaxU32{}));
@@ -744,6 +745,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   // node lane (t_all) instead of an LDS row of all K, and the rows are not staged at all.
   const bool need_uni = uniform_u32(!any_pm || (all_pm && nm_min == nm_max)) != 0u;
 
+  // (trace: the end of the set-up, the end of the block pass)
+  const uint64_t t_setup = STATS ? wall_clock64() : 0ull;
   uint32_t mx[6];
 #pragma unroll
   for (int f = 0; f < 6; ++f) mx[f] = 1u;  // floor 1 (collection.go:31-38)
@@ -1246,6 +1249,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     if (YODA_K1_PF && n0 < n1) load_sum(n0);
     for (uint32_t nb = n0; nb < n1; nb += kWave) node_block(nb, nb + kWave < n1 ? nb + kWave : ~0u);
   }
+  const uint64_t t_pass = STATS ? wall_clock64() : 0ull;
   g_nf = wave_sum_u32(g_nf);
   g_nz = wave_sum_u32(g_nz);
   nf_all += g_nf;
@@ -1269,7 +1273,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     tr[0] = t_start;
     tr[1] = wall_clock64();
     tr[2] = npart;
-    tr[3] = 0ull;
+    tr[3] = (t_setup - t_start) | ((t_pass - t_start) << 32);
   }
   if constexpr (WIT) {
     // the ALL nodes' maxima, witness counts and lowest witnesses, folded into every pod lane
@@ -3003,9 +3007,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // value is a score the lane reaches on a feasible node, so thr stays below every lane's best
   unsigned long long gpub = 0ull;  // the largest value this lane published to gbest
   auto refresh_thr = [&]() {
-    double wu = ubest;
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) wu = fmax(wu, __shfl_xor(wu, o, kWave));
+    const double wu = wave_allreduce(ubest, OpMaxF64{});
     double lb = act ? fmax(rties > 0u ? (double)rbest : -1.0, wu) : HUGE_VAL;
     if (args.gbest != nullptr && act) {  // (score + 1; 0: none yet)
       const unsigned long long g = args.gbest[p];
@@ -3021,8 +3023,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
 #endif
       lb = fmax(lb, (double)g - 1.0);
     }
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) lb = fmin(lb, __shfl_xor(lb, o, kWave));
+    lb = wave_allreduce(lb, OpMinF64{});
     thr = fmax(thr, __longlong_as_double(
                         (long long)uniform_u64((uint64_t)__double_as_longlong(lb))));
   };
@@ -3039,6 +3040,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     }
     thrk = wave_min_u64(kth);
   };
+  const uint64_t t_setup = STATS ? wall_clock64() : 0ull;
   if (blk) {
     // only the blocks K1 found a feasible pod of this wave in (bit b of word b/64)
     const uint64_t* bw = blk + (size_t)uniform_u32(p >> 6) * blk_stride;
@@ -3096,6 +3098,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   } else {
     for (uint32_t nb = n0; nb < n1; nb += kWave) block(nb);
   }
+  const uint64_t t_pass = STATS ? wall_clock64() : 0ull;
   if (STATS && !trace && lane == 0) {  // (wave, chunk)s with uniform maxima / all
     atomicAdd(stats + 5, uni_max ? 1ull : 0ull);
     atomicAdd(stats + 6, 1ull);
@@ -3109,8 +3112,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
       tr[1] = wall_clock64();
       tr[2] = npart;
       // uniform maxima | G's << 1 | decoupled bounds << 2 | reciprocal sets << 4
+      // | set-up end << 16 | block-list walk end << 40 (ticks after the start)
       tr[3] = (uni_max ? 1ull : 0ull) | (use_g ? 2ull : 0ull) | (dec ? 4ull : 0ull) |
-              ((unsigned long long)nsets << 4);
+              ((unsigned long long)nsets << 4) |
+              ((unsigned long long)min((unsigned long long)(t_setup - t_start), 0xffffffull) << 16) |
+              ((unsigned long long)min((unsigned long long)(t_pass - t_start), 0xffffffull) << 40);
     }
   }
   if constexpr (TOPK) {

@@ -241,3 +241,46 @@ def test_gloo_agree_on_devices(shared):
             assert "SAME_DEVICE: ranks 0 and 2" in outs[r], outs[r]
         else:
             assert outs[r] == ids
+
+
+def _pod_worker(rank, world, port, q):
+    """bench.py --gpus N's default (pod sharding): rank r evaluates dist.pod_partition's part r
+    against the WHOLE snapshot (the oracle standing in for libyoda on CPU), with nothing
+    exchanged but bench.py's max-over-ranks elapsed time; rank 0 gathers the picks only to
+    check them."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from yoda_amd.dist import pod_partition
+        nodes, pods = synth.make_config(2, pods=300, nodes=400)
+        part = pod_partition(pods, world, block=16)[rank]
+        res = oracle.schedule(nodes, pods.take(part), MODE_SCV)
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # bench.py: elapsed = max over ranks
+        q.put((rank, part, res.pick.copy(), res.status.copy(), res.n_ties.copy(), float(t.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_pod_shards_union(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pod_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nodes, pods = synth.make_config(2, pods=300, nodes=400)
+    want = oracle.schedule(nodes, pods, MODE_SCV)
+    seen = np.zeros(pods.n_pods, int)
+    for rank, part, pick, status, ties, tmax in outs:
+        assert tmax == float(world)
+        seen[part] += 1
+        np.testing.assert_array_equal(pick, want.pick[part])
+        np.testing.assert_array_equal(status, want.status[part])
+        np.testing.assert_array_equal(ties, want.n_ties[part])
+    assert (seen == 1).all()

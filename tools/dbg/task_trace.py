@@ -61,6 +61,22 @@ out = {"kernel": kern, "tasks": int(used.sum()), "span_us": span,
                      if (npart > 0).any() else None, "mean_npart": float(npart[npart > 0].mean())
                      if (npart > 0).any() else None},
        "corr_dur_npart": float(np.corrcoef(dur, npart)[0, 1]) if len(dur) > 2 else None}
+# phases (the trace's word 3): K1 set-up end | block-pass end << 32; K2 flags | set-up end << 16 |
+# block-list walk end << 40 (ticks after the task's start)
+w3 = tr[used][:, 3].astype(np.uint64)
+if kern == "k1":
+    t_set = (w3 & np.uint64(0xffffffff)).astype(np.int64) / 100.0
+    t_pass = (w3 >> np.uint64(32)).astype(np.int64) / 100.0
+else:
+    t_set = ((w3 >> np.uint64(16)) & np.uint64(0xffffff)).astype(np.int64) / 100.0
+    t_pass = ((w3 >> np.uint64(40)) & np.uint64(0xffffff)).astype(np.int64) / 100.0
+out["phase_us_mean"] = {"setup": float(t_set.mean()), "pass": float((t_pass - t_set).mean()),
+                        "epilogue": float((dur - t_pass).mean())}
+z = npart == 0
+if z.any():
+    out["phase_us_mean_npart0"] = {"setup": float(t_set[z].mean()),
+                                   "pass": float((t_pass[z] - t_set[z]).mean()),
+                                   "epilogue": float((dur[z] - t_pass[z]).mean())}
 # start-time profile: how many tasks start in each tenth of the span
 st = (t[:, 0] - t[:, 0].min()) / 100.0
 out["starts_by_tenth"] = np.histogram(st, bins=10, range=(0, span))[0].tolist()

@@ -8,7 +8,9 @@ model in DESIGN.md §7 adds it):
   nodes  (bench.py --shard nodes, the north_star's RCCL merge): all 100k pods and node block r
          of dist.shard_bounds through the torch-driven shard step (dist.ShardExchange: shard
          phase 1, the maxima/count merge, shard phase 2, the packed-key merge, finalize), with
-         the one-rank local reducer standing in for the all-reduces.
+         the one-rank local reducer standing in for the all-reduces;
+  nodes_lib  the same through libyoda's own exchange (yoda_comm_run_local with one handle:
+         device copies in place of the RCCL collectives, bench.py --exchange libyoda).
 One JSON line per (kind, W): per-rank ms/step (wall, HIP-synchronised), per-rank K1 / K2
 HIP-event ms, and the predicted whole-job pairs/s at max over ranks.
 
@@ -51,7 +53,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--worlds", default="1,2,4,8")
-    ap.add_argument("--kinds", default="pods,nodes")
+    ap.add_argument("--kinds", default="pods,nodes,nodes_lib")
     args = ap.parse_args()
     nodes, pods = synth.make_config(3)
     P, N = pods.n_pods, nodes.n_nodes
@@ -70,6 +72,19 @@ def main():
                 rows.append(timed(y, lambda: y.run(MODE_SCV), dev, args.steps))
             y.close()
             emit("pods", W, P, N, rows)
+        if "nodes_lib" in kinds:  # the same shard step through libyoda's own exchange
+            from yoda_amd.capi import comm_run_local
+            b = shard_bounds(N, W)
+            rows = []
+            for r in range(W):
+                lo, hi = int(b[r]), int(b[r + 1])
+                y = Yoda(0)
+                y.upload_nodes(nodes.slice(lo, hi), node_offset=lo)
+                y.upload_pods(pods)
+                y.set_stream(stream)
+                rows.append(timed(y, lambda: comm_run_local([y], MODE_SCV), dev, args.steps))
+                y.close()
+            emit("nodes_lib", W, P, N, rows)
         if "nodes" in kinds:
             b = shard_bounds(N, W)
             rows = []
