@@ -137,7 +137,7 @@ hipError_t launch_bsum_cn(const unsigned char* sum, uint32_t sum_stride, uint32_
 hipError_t launch_block_ub(int K, const uint32_t* sum2, const uint32_t* tab, uint32_t n_nodes,
                            uint32_t* out, const uint32_t* levels, hipStream_t s);
 hipError_t launch_block_dec(int K, const uint32_t* sum2, uint32_t n_nodes, uint32_t* out,
-                            const uint32_t* levels, uint32_t ranks, hipStream_t s);
+                            const uint32_t* levels, MemTab mt, hipStream_t s);
 hipError_t launch_gtable(int K, const uint32_t* sum2, const uint32_t* mix, uint32_t n_nodes,
                          const uint64_t* g_max,
                          uint32_t* tab, uint32_t* rcp_out, MemTab mt, hipStream_t s);
@@ -1329,7 +1329,7 @@ hipError_t build_block_ub(yoda_t* h) {
                                  kbub_stride(h->K)) * 4;  // tiles of 64 blocks
   const size_t dbytes = sum_words(std::max<uint32_t>((h->n_nodes + 63) / 64, 1),
                                   kbdec_stride()) * 4;
-  const uint32_t ranks = h->mem_ranks ? 1u : 0u;
+  const MemTab mt = h->mem_ranks ? h->mt : MemTab{};
   e = h->kbub.ensure(bytes);
   if (e == hipSuccess) e = h->kbdec.ensure(dbytes);
   if (e == hipSuccess)
@@ -1337,7 +1337,7 @@ hipError_t build_block_ub(yoda_t* h) {
                         h->kbub.as<uint32_t>(), h->kb_levels.as<uint32_t>(), h->stream);
   if (e == hipSuccess)
     e = launch_block_dec(h->K, h->k2sum.as<uint32_t>(), h->n_nodes, h->kbdec.as<uint32_t>(),
-                         h->kb_levels.as<uint32_t>(), ranks, h->stream);
+                         h->kb_levels.as<uint32_t>(), mt, h->stream);
   if (e == hipSuccess && h->perm_on) {
     e = h->kbub_p.ensure(bytes);
     if (e == hipSuccess) e = h->kbdec_p.ensure(dbytes);
@@ -1346,7 +1346,7 @@ hipError_t build_block_ub(yoda_t* h) {
                           h->kbub_p.as<uint32_t>(), h->kb_levels.as<uint32_t>(), h->stream);
     if (e == hipSuccess)
       e = launch_block_dec(h->K, h->k2sum_p.as<uint32_t>(), h->n_nodes, h->kbdec_p.as<uint32_t>(),
-                           h->kb_levels.as<uint32_t>(), ranks, h->stream);
+                           h->kb_levels.as<uint32_t>(), mt, h->stream);
   }
   if (e == hipSuccess) {
     h->kbub_dirty = h->kbub_loose = false;
@@ -2190,7 +2190,9 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
         // Not with memory ranks: there the rank-space K2 ran slower on the sorted blocks
         // (memory in bytes: 1.91 vs 1.80 ms, profiles/r05/y/ab.txt).
         static const bool zorder_env = YODA_KNOB("YODA_NODE_ZORDER", 1) != 0;  // A/B knob
-        if (ok && zorder_env && !ranks) {
+        // (YODA_ZORDER_RANKS=1, A/B knob: with memory ranks too)
+        static const bool zorder_ranks = YODA_KNOB("YODA_ZORDER_RANKS", 0) != 0;
+        if (ok && zorder_env && (!ranks || zorder_ranks)) {
           std::vector<uint32_t> hix;
           for (uint32_t t = 1; t <= (uint32_t)K; t <<= 1) hix.push_back(t - 1);
           const uint32_t nc = (uint32_t)hix.size(), bits = 64 / nc > 16 ? 16 : 64 / nc;

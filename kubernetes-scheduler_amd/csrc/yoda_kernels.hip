@@ -1930,12 +1930,14 @@ __global__ __launch_bounds__(kWave) void k_block_ub(const uint32_t* __restrict__
 }
 
 // The non-G block bounds (yoda_layout.h kbdec_*): one wave per 64-node block, lane = node.
-// ranks: the summaries hold memory ranks (their sums mean nothing): every block "not ok".
+// Memory ranks (mt.vf): the summaries' free / total words are ranks, compared with the levels
+// as they are (the same order) and summed as their VALUES (the tables), which is what the
+// bound's reciprocals multiply.
 template <int K>
 __global__ __launch_bounds__(kWave) void k_block_dec(const uint32_t* __restrict__ sum2,
                                                      uint32_t n_nodes, uint32_t* __restrict__ out,
                                                      const uint32_t* __restrict__ levels,
-                                                     uint32_t ranks) {
+                                                     MemTab mt) {
   constexpr uint32_t S2 = k2sum_stride(K), DS = kbdec_stride();
   const uint32_t b = blockIdx.x, n = b * 64u + threadIdx.x;
   const bool v = n < n_nodes;
@@ -1965,7 +1967,7 @@ __global__ __launch_bounds__(kWave) void k_block_dec(const uint32_t* __restrict_
     fs[t] = real ? w2(kS2Fs + (uint32_t)t) : 0u;
     ts[t] = real ? w2(kS2Fs + (uint32_t)K + (uint32_t)t) : 0u;
   }
-  const bool ok = ranks == 0u && ballot(v && (meta & kSumUni4) == 0u) == 0ull;
+  const bool ok = ballot(v && (meta & kSumUni4) == 0u) == 0ull;
   const double st = wave_max_f64(stat);
   const uint32_t mbw = wave_max_u32(bw), mck = wave_max_u32(ck), mco = wave_max_u32(co),
                  mpw = wave_max_u32(pw);
@@ -1980,13 +1982,13 @@ __global__ __launch_bounds__(kWave) void k_block_dec(const uint32_t* __restrict_
   for (uint32_t l = 0; l < kKbLevels; ++l) {
     const uint32_t t = levels[l];
     uint32_t q = 0;
-    double f = 0.0, tt = 0.0;  // exact: sums of at most 16 u32
+    double f = 0.0, tt = 0.0;  // exact: sums of at most 16 values below 2^44
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const bool in = fs[k] >= t && (uint32_t)k < cnt;
       q += in ? 1u : 0u;
-      f += in ? (double)fs[k] : 0.0;
-      tt += in ? (double)ts[k] : 0.0;
+      f += in ? (mt.vf ? mt.vf[fs[k]] : (double)fs[k]) : 0.0;
+      tt += in ? (mt.vt ? mt.vt[ts[k]] : (double)ts[k]) : 0.0;
     }
     const uint32_t mq = wave_max_u32(q);
     const double mf = wave_max_f64(f), mt = wave_max_f64(tt);
@@ -1999,15 +2001,15 @@ __global__ __launch_bounds__(kWave) void k_block_dec(const uint32_t* __restrict_
 }
 
 hipError_t launch_block_dec(int K, const uint32_t* sum2, uint32_t n_nodes, uint32_t* out,
-                            const uint32_t* levels, uint32_t ranks, hipStream_t s) {
+                            const uint32_t* levels, MemTab mt, hipStream_t s) {
   if (n_nodes == 0) return hipSuccess;
   const dim3 grid((n_nodes + 63) / 64);
   switch (K) {
-    case 1: hipLaunchKernelGGL(k_block_dec<1>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, ranks); break;
-    case 2: hipLaunchKernelGGL(k_block_dec<2>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, ranks); break;
-    case 4: hipLaunchKernelGGL(k_block_dec<4>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, ranks); break;
-    case 8: hipLaunchKernelGGL(k_block_dec<8>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, ranks); break;
-    case 16: hipLaunchKernelGGL(k_block_dec<16>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, ranks); break;
+    case 1: hipLaunchKernelGGL(k_block_dec<1>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, mt); break;
+    case 2: hipLaunchKernelGGL(k_block_dec<2>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, mt); break;
+    case 4: hipLaunchKernelGGL(k_block_dec<4>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, mt); break;
+    case 8: hipLaunchKernelGGL(k_block_dec<8>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, mt); break;
+    case 16: hipLaunchKernelGGL(k_block_dec<16>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, mt); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -2490,7 +2492,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
   // nodes are one GPU model): the decoupled bounds kbdec_* (argmax, no memory ranks).
   // Several reciprocal sets: the largest reciprocal of each field over the active lanes (the
   // smallest maxima) gives the highest score any of them can make, so the bound holds for all.
-  const bool dec = !RK && args.kbdec != nullptr && !use_g && act_mask != 0ull;
+  const bool dec = args.kbdec != nullptr && !use_g && act_mask != 0ull;
   const bool prune = args.kbub != nullptr && (use_g || dec);
   if (dec) {  // the bound's reciprocals into the extra RCPS slot (RS at word 0, f64 at word 8)
     RS d_bw = act ? sc.r_bw : (RS)0, d_core = act ? sc.r_core : (RS)0, d_pow = act ? sc.r_pow : (RS)0;
@@ -4913,6 +4915,8 @@ static hipError_t launch_k2_t(int K, Path path, const unsigned char* nodes,
           if (a.mt.vf) YODA_K2B(true, true, true, true) else YODA_K2B(true, false, true, true);
         } else if (pp.all_uni4 && !a.mt.vf) {
           YODA_K2B(false, false, false, true);
+        } else if (pp.all_uni4) {  // memory ranks on one-model nodes (e.g. memory in bytes)
+          YODA_K2B(false, true, false, true);
         } else {
           if (a.mt.vf) YODA_K2B(false, true, true, true) else YODA_K2B(false, false, true, true);
         }
