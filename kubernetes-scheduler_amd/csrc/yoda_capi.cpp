@@ -353,6 +353,7 @@ struct yoda_handle {
   // node's position (k_set_static keeps the copies current)
   bool perm_on = false;
   DevBuf k1sum_p, k2sum_p, gtab_p, perm_ids, perm_inv;
+  DevBuf kx1_p, kmix_p;  // the mixed-model tiles in that order (immutable card data)
   // 64-node block summaries (yoda_layout.h BlockSumWord) of the snapshot order and of the
   // block-grouped copy's; loose: node-state pushes left their CardNumber bounds valid but not
   // tight (k_set_static's atomics), recomputed before the next private run
@@ -544,7 +545,7 @@ struct yoda_handle {
   ~yoda_handle() {
     if (comm && rccl().ok) (void)rccl().comm_destroy(comm);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &k1sum_p,   &k2sum_p,   &gtab_p, &blksum, &blksum_p, &kbub, &kbub_p, &kbdec, &kbdec_p, &kb_levels, &hot, &hot_p,    &perm_ids,  &perm_inv,    &pod_blob,   &maxima,       &counts,
+    DevBuf* all[] = {&kx1_p, &kmix_p, &nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &k1sum_p,   &k2sum_p,   &gtab_p, &blksum, &blksum_p, &kbub, &kbub_p, &kbdec, &kbdec_p, &kb_levels, &hot, &hot_p,    &perm_ids,  &perm_inv,    &pod_blob,   &maxima,       &counts,
                      &pod_sorted, &perm,     &order_scratch, &order_meta, &order_hist,
                      &order_bstart, &order_slot, &order_bkt,
                      &rcp,       &best,       &idx,          &ties,
@@ -910,6 +911,8 @@ PodParams pod_params(yoda_t* h) {
   if (ub_ok && h->hot_ok) pp.hot = h->hot.as<uint64_t>();
   if (h->perm_run()) {
     pp.ids = h->perm_ids.as<uint32_t>();
+    pp.mix = h->kmix_p.as<uint32_t>();
+    pp.x1 = h->kx1_p.as<uint32_t>();
     if (pp.g.tab) pp.g.tab = h->gtab_p.as<uint32_t>();
     pp.bsum = h->blksum_p.p ? h->blksum_p.as<uint32_t>() : nullptr;
     pp.kbub = ub_ok && h->kbub_p.p ? h->kbub_p.as<uint32_t>() : nullptr;
@@ -1439,7 +1442,7 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts,
   HIP_TRY(h, launch_k1(h->K, h->path, h->nodes.as<unsigned char>(),
                        h->has_k1sum ? (pr ? h->k1sum_p : h->k1sum).as<unsigned char>() : nullptr,
                        (pr ? h->k2sum_p : h->k2sum).as<unsigned char>(),
-                       h->kmix.as<unsigned char>(), h->n_nodes,
+                       (pr ? h->kmix_p : h->kmix).as<unsigned char>(), h->n_nodes,
                        h->chunk1, h->C1, pod_params(h), P, part, h->bitmask.as<uint64_t>(),
                        bm_row(h->n_nodes), h->bsum.as<BlockMask>(), bs_row(h->n_nodes),
                        h->blk.as<uint64_t>(), blk_row(h->n_nodes), h->stats_ptr(), h->stream,
@@ -2162,14 +2165,21 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
       h->perm_on = false;
       static const bool perm_env = YODA_KNOB("YODA_NODE_PERM", 1) != 0;
       std::vector<uint32_t> nperm;
-      if (perm_env && path == Path::N32 && n_one_model == N && N >= 4096 &&
+      // Mixed-model nodes (cards of several GPU models) form a group of their own, so that
+      // the one-model nodes still fill one-model blocks, which the block summaries decide
+      // whole (50 % mixed-model nodes: every block mixed without it).  YODA_NODE_PERM_MIXED=0
+      // (A/B knob): one-model snapshots only, as in round 5.
+      static const bool perm_mixed = YODA_KNOB("YODA_NODE_PERM_MIXED", 1) != 0;
+      if (perm_env && path == Path::N32 && (n_one_model == N || perm_mixed) && N >= 4096 &&
           !(flags & YODA_UPLOAD_PER_NODE_K1) && !(flags & YODA_UPLOAD_PER_NODE_K2)) {
         const uint32_t SW = (uint32_t)(sstride / 4);
         std::vector<uint32_t> keys;
         std::vector<std::vector<uint32_t>> grp;
         bool ok = true;
         for (uint32_t i = 0; i < N && ok; ++i) {
-          const uint32_t ck = sum[(size_t)i * SW + kSumClock];
+          // (a mixed-model node's kSumClock is its first card's: the key of its group is ~0)
+          const uint32_t ck = (sum[(size_t)i * SW + kSumMeta] & kSumUni4)
+                                  ? sum[(size_t)i * SW + kSumClock] : 0xffffffffu;
           size_t g = 0;
           while (g < keys.size() && keys[g] != ck) ++g;
           if (g == keys.size()) {
@@ -2256,14 +2266,26 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
       if (h->perm_on) {
         const uint32_t SW = (uint32_t)(sstride / 4), S2W = (uint32_t)(s2stride / 4);
         std::vector<uint32_t> sp((size_t)N * SW), s2p((size_t)N * S2W), inv(N);
+        const uint32_t MW = (uint32_t)(mstride / 4), XW = (uint32_t)(xstride / 4);
+        std::vector<uint32_t> mp((size_t)N * MW), xp((size_t)N * XW);
         for (uint32_t q = 0; q < N; ++q) {
           const uint32_t i = nperm[q];
           std::memcpy(sp.data() + (size_t)q * SW, sum.data() + (size_t)i * SW, SW * 4);
           std::memcpy(s2p.data() + (size_t)q * S2W, sum2.data() + (size_t)i * S2W, S2W * 4);
+          std::memcpy(mp.data() + (size_t)q * MW, mix.data() + (size_t)i * MW, MW * 4);
+          std::memcpy(xp.data() + (size_t)q * XW, x1m.data() + (size_t)i * XW, XW * 4);
           inv[i] = q;
         }
         sp = tiles(sp, (uint32_t)sstride);
         s2p = tiles(s2p, (uint32_t)s2stride);
+        mp = tiles(mp, (uint32_t)mstride);
+        xp = tiles(xp, (uint32_t)xstride);
+        HIP_TRY(h, h->kmix_p.ensure(mp.size() * 4));
+        HIP_TRY(h, h->kx1_p.ensure(xp.size() * 4));
+        HIP_TRY(h, hipMemcpyAsync(h->kmix_p.p, mp.data(), mp.size() * 4, hipMemcpyHostToDevice,
+                                  h->stream));
+        HIP_TRY(h, hipMemcpyAsync(h->kx1_p.p, xp.data(), xp.size() * 4, hipMemcpyHostToDevice,
+                                  h->stream));
         HIP_TRY(h, h->k1sum_p.ensure(sp.size() * 4));
         HIP_TRY(h, h->k2sum_p.ensure(s2p.size() * 4));
         HIP_TRY(h, h->perm_ids.ensure((size_t)N * 4));
@@ -2422,7 +2444,7 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
                                h->gtab.as<uint32_t>(), rcp_dev, mt, h->stream));
       if (h->perm_on) {  // the G table of the block-grouped copy (the same rows, reordered)
         HIP_TRY(h, h->gtab_p.ensure(sum_words(std::max<uint32_t>(N, 1), gtab_stride(K)) * 4));
-        HIP_TRY(h, launch_gtable(K, h->k2sum_p.as<uint32_t>(), h->kmix.as<uint32_t>(), N,
+        HIP_TRY(h, launch_gtable(K, h->k2sum_p.as<uint32_t>(), h->kmix_p.as<uint32_t>(), N,
                                  h->gtab_aux.as<uint64_t>(), h->gtab_p.as<uint32_t>(), rcp_dev,
                                  mt, h->stream));
       }

@@ -677,7 +677,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     uint32_t* __restrict__ wts = nullptr, const uint32_t* __restrict__ gtab = nullptr,
     const uint32_t* __restrict__ kbub = nullptr, const uint32_t* __restrict__ levels = nullptr,
     unsigned long long* __restrict__ seed_out = nullptr,
-    unsigned long long* __restrict__ cmask = nullptr) {
+    unsigned long long* __restrict__ cmask = nullptr,
+    const uint32_t* __restrict__ ids = nullptr) {
   static_assert(!(WIT && MIX), "the witness K1 serves one-model snapshots");
   static_assert(SUB == 1 || (SUB == kBlock / kWave && !WIT), "SUB: 1, or one pod wave per workgroup");
   constexpr uint32_t SS = k1sum_stride(K);
@@ -1097,7 +1098,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
 #ifdef YODA_ABL_K1_NOLEAN
       const bool f = false;
 #else
-      const bool f = k1_node_lean<K>(nodes + (size_t)(nb + (uint32_t)j) * NS, m, c, number,
+      // (the record by the node's local id: a block-grouped run reads positions, ids)
+      const uint32_t rid = ids ? ids[nb + (uint32_t)j] : nb + (uint32_t)j;
+      const bool f = k1_node_lean<K>(nodes + (size_t)rid * NS, m, c, number,
                                      need_mem, need_clk, mx, nf, nz) && live;
 #endif
       const uint64_t b = ballot(f);
@@ -4725,7 +4728,7 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                                       pp.nwords, pp.lpt_w, pp.seed ? pp.g.tab : nullptr,         \
                                       pp.kbub_exact ? pp.kbub : nullptr, pp.kb_levels,           \
                                       reinterpret_cast<unsigned long long*>(pp.seed),          \
-                                      reinterpret_cast<unsigned long long*>(pp.cmask1)))
+                                      reinterpret_cast<unsigned long long*>(pp.cmask1), pp.ids))
         if (sub == 1u) {
           if (stats) YODA_K1B(KK, true)
           else if (pp.one_model) YODA_K1B(KK, false, false)
