@@ -892,8 +892,13 @@ PodParams pod_params(yoda_t* h) {
   // (the non-G bounds pay on one-model snapshots at K <= 8: config 3's K2 0.32 -> 0.21 ms;
   // on mixed-model nodes and at K = 16 their per-block cost exceeds what they prune -- mixed50
   // K2 1.52 vs 1.29 ms, the config-4 generator 0.64 vs 0.48 ms, profiles/r05/y/ab.txt)
-  if (ub_ok && dec_env && h->kbdec.p && h->K <= 8 && h->all_one_model)
-    pp.kbdec = h->kbdec.as<uint32_t>();
+  // (YODA_KB_DEC_GROUPED, A/B knob: 1 = also on mixed fleets in the block-grouped order, whose
+  // one-model blocks are whole again; 2 = there at K = 16 too)
+  static const uint32_t dec_grouped = YODA_KNOB("YODA_KB_DEC_GROUPED", 1);
+  const bool dec_ok = dec_env && (h->all_one_model ? h->K <= 8
+                                                    : h->perm_run() && dec_grouped != 0 &&
+                                                          (h->K <= 8 || dec_grouped == 2));
+  if (ub_ok && dec_ok && h->kbdec.p) pp.kbdec = h->kbdec.as<uint32_t>();
   {
     const size_t nw = (h->n_work + 63) / 64;
     uint64_t* sd = h->blk.as<uint64_t>() + nw * blk_row(h->n_nodes);
@@ -916,7 +921,7 @@ PodParams pod_params(yoda_t* h) {
     if (pp.g.tab) pp.g.tab = h->gtab_p.as<uint32_t>();
     pp.bsum = h->blksum_p.p ? h->blksum_p.as<uint32_t>() : nullptr;
     pp.kbub = ub_ok && h->kbub_p.p ? h->kbub_p.as<uint32_t>() : nullptr;
-    pp.kbdec = pp.kbub && dec_env && h->kbdec_p.p ? h->kbdec_p.as<uint32_t>() : nullptr;
+    pp.kbdec = pp.kbub && dec_ok && h->kbdec_p.p ? h->kbdec_p.as<uint32_t>() : nullptr;
     pp.hot = pp.kbub && h->hot_ok ? h->hot_p.as<uint64_t>() : nullptr;
   }
   pp.mt = h->mem_ranks ? h->mt : MemTab{};
