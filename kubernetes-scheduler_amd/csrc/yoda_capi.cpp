@@ -389,7 +389,16 @@ struct yoda_handle {
     pc.bsum_words = bsum_stride(K) / 4u;
     return pc;
   }
-  bool perm_run() const { return perm_on && count_order; }  // this run is block-grouped
+  // this run is block-grouped.  On a snapshot with mixed-model nodes (or per-card TotalMemory)
+  // only a large batch takes the grouped order: grouping gathers the nodes that need the
+  // per-card pass into a few blocks, so a few (wave, chunk) tasks carry all of it -- on a
+  // small batch (config 4: 10k pods x 20k nodes, K1 88 -> 143 us, the last tasks alone)
+  // that tail outweighs the whole-block decisions, which win from 32k pods on (the config-4
+  // generator at 100k x 100k: K1 0.52 -> 0.20 ms)
+  bool perm_run() const {
+    return perm_on && count_order && (all_one_model || n_work >= kGroupedMixedMinPods);
+  }
+  static constexpr uint32_t kGroupedMixedMinPods = 32768;
   bool all_uni4 = false;       // every node: one GPU model (kNodeUniform4)
   std::vector<unsigned char> host_records;  // kept for alloc updates (greedy)
   std::vector<uint32_t> host_k2sum;         // idem (its static score words)
