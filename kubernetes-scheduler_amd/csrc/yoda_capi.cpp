@@ -48,7 +48,7 @@ hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp,
 hipError_t launch_window_out(const uint32_t* counts, const uint64_t* maxima, const uint32_t* wit,
                              const double* tk_s, const uint32_t* tk_i, const uint32_t* perm,
                              uint32_t wn, uint32_t kt, bool lists_row_major, unsigned char* out,
-                             hipStream_t s);
+                             uint32_t* inv_scratch, hipStream_t s);
 hipError_t launch_k2(int K, Path path, const unsigned char* nodes, const unsigned char* sum2,
                      const uint64_t* blk, uint32_t blk_stride, uint32_t n_nodes,
                      uint32_t chunk_nodes, uint32_t C, const PodParams& pp, const uint64_t* maxima,
@@ -354,6 +354,7 @@ struct yoda_handle {
   bool perm_on = false;
   DevBuf k1sum_p, k2sum_p, gtab_p, perm_ids, perm_inv;
   DevBuf kx1_p, kmix_p;  // the mixed-model tiles in that order (immutable card data)
+  DevBuf win_inv;        // capacity windows: each window slot's sorted position (k_window_out)
   // 64-node block summaries (yoda_layout.h BlockSumWord) of the snapshot order and of the
   // block-grouped copy's; loose: node-state pushes left their CardNumber bounds valid but not
   // tight (k_set_static's atomics), recomputed before the next private run
@@ -554,7 +555,7 @@ struct yoda_handle {
   ~yoda_handle() {
     if (comm && rccl().ok) (void)rccl().comm_destroy(comm);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-    DevBuf* all[] = {&kx1_p, &kmix_p, &nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &k1sum_p,   &k2sum_p,   &gtab_p, &blksum, &blksum_p, &kbub, &kbub_p, &kbdec, &kbdec_p, &kb_levels, &hot, &hot_p,    &perm_ids,  &perm_inv,    &pod_blob,   &maxima,       &counts,
+    DevBuf* all[] = {&kx1_p, &kmix_p, &win_inv, &nodes,     &nodes_b,   &k1sum,     &k2sum,    &kmix,    &kx1,     &memtab,    &k1sum_p,   &k2sum_p,   &gtab_p, &blksum, &blksum_p, &kbub, &kbub_p, &kbdec, &kbdec_p, &kb_levels, &hot, &hot_p,    &perm_ids,  &perm_inv,    &pod_blob,   &maxima,       &counts,
                      &pod_sorted, &perm,     &order_scratch, &order_meta, &order_hist,
                      &order_bstart, &order_slot, &order_bkt,
                      &rcp,       &best,       &idx,          &ties,
@@ -5127,13 +5128,14 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
       // (YODA_WIN_DMA=0, A/B knob: k_window_out writes the pinned pages directly)
       static const bool win_dma = YODA_KNOB("YODA_WIN_DMA", 1) != 0;
       if (win_dma) HIP_TRY(h, h->win_dev.ensure(total));
+      HIP_TRY(h, h->win_inv.ensure((size_t)wn * 4));
       HIP_TRY(h, launch_window_out(h->counts.as<uint32_t>(), h->maxima.as<uint64_t>(),
                                    h->wit.as<uint32_t>(), h->tk_s.as<double>(),
                                    h->tk_i.as<uint32_t>(),
                                    h->ordered ? h->perm.as<uint32_t>() : nullptr, wn, KD, true,
                                    win_dma ? h->win_dev.as<unsigned char>()
                                            : static_cast<unsigned char*>(h->win_stage.dp),
-                                   h->stream));
+                                   h->win_inv.as<uint32_t>(), h->stream));
       if (win_dma)
         HIP_TRY(h, hipMemcpyAsync(h->win_stage.p, h->win_dev.p, total, hipMemcpyDeviceToHost,
                                   h->stream));

@@ -1743,7 +1743,7 @@ __global__ __launch_bounds__(kBlock) void k_window_out(
     const uint32_t* __restrict__ counts, const uint64_t* __restrict__ maxima,
     const uint32_t* __restrict__ wit, const double* __restrict__ tk_s,
     const uint32_t* __restrict__ tk_i, const uint32_t* __restrict__ perm, uint32_t wn,
-    uint32_t kt, int row_major, unsigned char* __restrict__ out) {
+    uint32_t kt, int row_major, unsigned char* __restrict__ out, uint32_t* __restrict__ inv_out) {
   __shared__ uint32_t inv[kBlock];
   const uint32_t w0 = blockIdx.x * kBlock, w = w0 + threadIdx.x;
   if (perm) {
@@ -1763,12 +1763,35 @@ __global__ __launch_bounds__(kBlock) void k_window_out(
   for (uint32_t f = 0; f < 2; ++f) o_cnt[(size_t)f * wn + w] = counts[(size_t)f * wn + q];
   for (uint32_t f = 0; f < 6; ++f) o_mx[(size_t)f * wn + w] = maxima[(size_t)f * wn + q];
   for (uint32_t f = 0; f < 12; ++f) o_wit[(size_t)f * wn + w] = wit[(size_t)f * wn + q];
+  if (inv_out) {  // the lists: k_window_lists, one thread per (pod, entry)
+    inv_out[w] = q;
+    return;
+  }
   // the lists [k][wn], or [wn][k] (row_major: each pod's list contiguous for the host's scan)
   for (uint32_t k = 0; k < kt; ++k) {
     const size_t o = row_major ? (size_t)w * kt + k : (size_t)k * wn + w;
     o_ts[o] = tk_s[(size_t)k * wn + q];
     o_ti[o] = tk_i[(size_t)k * wn + q];
   }
+}
+
+// The window's candidate lists into the staging layout of k_window_out, one thread per (pod,
+// entry) -- consecutive threads write consecutive entries (row_major: one pod's list) -- from
+// the sorted positions inv[w] that k_window_out found.  (One thread per pod looping over a
+// 64-deep list took 36-49 us per capacity window: 3 workgroups on the device.)
+__global__ __launch_bounds__(kBlock) void k_window_lists(
+    const double* __restrict__ tk_s, const uint32_t* __restrict__ tk_i,
+    const uint32_t* __restrict__ inv, uint32_t wn, uint32_t kt, int row_major,
+    unsigned char* __restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= (size_t)wn * kt) return;
+  double* o_ts = reinterpret_cast<double*>(out + 104 * (size_t)wn);
+  uint32_t* o_ti = reinterpret_cast<uint32_t*>(out + (104 + 8 * (size_t)kt) * wn);
+  const uint32_t w = row_major ? (uint32_t)(t / kt) : (uint32_t)(t % wn);
+  const uint32_t k = row_major ? (uint32_t)(t - (size_t)w * kt) : (uint32_t)(t / wn);
+  const uint32_t q = inv[w];
+  o_ts[t] = tk_s[(size_t)k * wn + q];
+  o_ti[t] = tk_i[(size_t)k * wn + q];
 }
 
 // CalculateCardScore's bandwidth, clock / MaxBandwidth (algorithm.go:283), 2 core and power
@@ -4865,10 +4888,15 @@ hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp,
 hipError_t launch_window_out(const uint32_t* counts, const uint64_t* maxima, const uint32_t* wit,
                              const double* tk_s, const uint32_t* tk_i, const uint32_t* perm,
                              uint32_t wn, uint32_t kt, bool lists_row_major, unsigned char* out,
-                             hipStream_t s) {
+                             uint32_t* inv_scratch, hipStream_t s) {
   if (wn == 0) return hipSuccess;
   hipLaunchKernelGGL(k_window_out, pod_grid(wn), dim3(kBlock), 0, s, counts, maxima, wit, tk_s,
-                     tk_i, perm, wn, kt, lists_row_major ? 1 : 0, out);
+                     tk_i, perm, wn, kt, lists_row_major ? 1 : 0, out, inv_scratch);
+  if (inv_scratch && kt > 0) {
+    const size_t n = (size_t)wn * kt;
+    hipLaunchKernelGGL(k_window_lists, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock),
+                       0, s, tk_s, tk_i, inv_scratch, wn, kt, lists_row_major ? 1 : 0, out);
+  }
   return hipGetLastError();
 }
 
