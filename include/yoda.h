@@ -423,6 +423,24 @@ int yoda_set_node_state(yoda_t* h, uint32_t count, const uint32_t* nodes, const 
 int yoda_shard_topk_depth(const yoda_t* h);
 int yoda_shard_topk(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_counts, uint32_t k,
                     uint32_t* counts, double* top_score, uint32_t* top_node);
+/* Capacity windows across shards (the window sequence of yoda_comm_greedy and yoda_greedy):
+ * yoda_shard_topk after yoda_shard_phase1_witness, but the lists are `deep` long
+ * (yoda_greedy_cap_depth()) -- the chunks' lists merged deeper, exact down to their last entry
+ * and 0xFFFFFFFF-ended past it; top_score / top_node are [deep][P]. */
+int yoda_greedy_cap_depth(void);
+int yoda_shard_topk_deep(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_counts,
+                         uint32_t k, uint32_t deep, uint32_t* counts, double* top_score,
+                         uint32_t* top_node);
+/* The shards' list merge of the sharded greedy (host only, no handle): scores / nodes are the
+ * world's gathered lists, [world][kl][wn] in shard order (yoda_shard_topk[_deep]'s layout);
+ * out_score / out_node [kl][wn] get, for window pods [from, wn), the first kl of the union in
+ * (score desc, node asc) order, -1.0 / 0xFFFFFFFF past its end.  Deep lists (kl >
+ * yoda_topk_k_capacity()) are cut where a node some shard left unlisted could enter (after the
+ * first yoda_topk_k(), at the latest of the shards' last entries).  yoda_comm_greedy merges
+ * with this same function. */
+int yoda_merge_shard_lists(uint32_t world, uint32_t wn, uint32_t kl, uint32_t from,
+                           const double* scores, const uint32_t* nodes, double* out_score,
+                           uint32_t* out_node);
 /* Exact best node of pod `pod` (index in the batch of the last yoda_shard_topk) over this
  * shard against the CURRENT node state: *node = global id or -1 (no feasible node here),
  * *score = its raw score (lowest node among equal scores). */

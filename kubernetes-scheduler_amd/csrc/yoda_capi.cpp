@@ -5622,6 +5622,59 @@ struct Coll {
 
 static int comm_step(yoda_t* const* hs, int n, int world, int mode, bool local);
 
+// The sharded greedy's list merge (window exchange 2), shared by comm_greedy and the caller-
+// driven protocol (yoda_merge_shard_lists, dist.sharded_greedy): shard rk's list of window pod
+// p is (sc[rk][l*wn + p], nd[rk][l*wn + p]), l < kl, sorted score desc / node asc and ended by
+// a 0xFFFFFFFF node.  ts/ti [kl][wn] receive the first kl of the union in that order (pods
+// [from, wn) only).  Deep lists (exact down to their last entry only): every node a shard left
+// out scores at most the shard's last entry, so the union is certain only above the latest of
+// those -- and for its first topk_k(), which lie within their shards' exact prefixes.
+static void merge_shard_lists(int world, uint32_t wn, uint32_t kl, bool deep, uint32_t from,
+                              const double* const* sc, const uint32_t* const* nd, double* ts,
+                              uint32_t* ti) {
+  auto before = [](const std::pair<double, uint32_t>& a, const std::pair<double, uint32_t>& b) {
+    return a.first > b.first || (a.first == b.first && a.second < b.second);
+  };
+  std::vector<uint32_t> head(world), len(world);
+  for (uint32_t p = from; p < wn; ++p) {
+    bool any_last = false;
+    std::pair<double, uint32_t> last_max{-1.0, 0xffffffffu};
+    for (int rk = 0; rk < world; ++rk) {
+      uint32_t l = 0;
+      while (l < kl && nd[rk][(size_t)l * wn + p] != 0xffffffffu) ++l;
+      len[rk] = l;
+      head[rk] = 0;
+      if (deep && l > 0) {
+        const std::pair<double, uint32_t> last{sc[rk][(size_t)(l - 1) * wn + p],
+                                               nd[rk][(size_t)(l - 1) * wn + p]};
+        if (!any_last || before(last_max, last)) last_max = last;
+        any_last = true;
+      }
+    }
+    for (uint32_t k = 0; k < kl; ++k) {
+      int best = -1;
+      std::pair<double, uint32_t> bv{-1.0, 0xffffffffu};
+      for (int rk = 0; rk < world; ++rk) {
+        if (head[rk] >= len[rk]) continue;
+        const size_t o = (size_t)head[rk] * wn + p;
+        const std::pair<double, uint32_t> v{sc[rk][o], nd[rk][o]};
+        if (best < 0 || before(v, bv)) best = rk, bv = v;
+      }
+      if (best < 0) break;
+      if (any_last && k >= (uint32_t)topk_k() && !before(bv, last_max)) break;
+      ++head[best];
+      ts[(size_t)k * wn + p] = bv.first;
+      ti[(size_t)k * wn + p] = bv.second;
+    }
+  }
+}
+
+// the capacity windows' list depth across shards (YODA_GREEDY_CAP_DEPTH, as yoda_greedy's)
+static uint32_t greedy_cap_depth() {
+  static const uint32_t d = YODA_KNOB("YODA_GREEDY_CAP_DEPTH", 64);
+  return std::max<uint32_t>(d, (uint32_t)topk_k_capacity());
+}
+
 // Greedy batch over node shards, inside libyoda ("Across GPUs"): the protocol of
 // dist.sharded_greedy with RCCL (or the in-process transport): per window, K1 on every shard,
 // maxima MAX / counts SUM (capacity mode: + the witnesses), the shards' candidate lists
@@ -5717,10 +5770,9 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
     const uint32_t K = (uint32_t)(capacity ? topk_k_capacity() : topk_k()),
                    W0 = std::min<uint32_t>(P, greedy_window());
     // capacity windows: each shard's lists merged deeper (shard_topk_impl, exact down to their
-    // last entry), the union cut where a shard's unlisted nodes could enter (below); the same
-    // depth on every rank (YODA_GREEDY_CAP_DEPTH, as yoda_greedy's; 0: K)
-    static const uint32_t cap_depth = YODA_KNOB("YODA_GREEDY_CAP_DEPTH", 64);
-    const uint32_t KL = capacity && cap_depth > K ? cap_depth : K;
+    // last entry), the union cut where a shard's unlisted nodes could enter (merge_shard_lists);
+    // the same depth on every rank
+    const uint32_t KL = capacity ? greedy_cap_depth() : K;
     std::vector<uint32_t> counts, ti, wit_h;
     std::vector<double> ts;
     std::vector<uint64_t> mx_h;
@@ -5792,53 +5844,15 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
         if (r || (r = re) || (r = co.allgather_finish(lb, gathered))) return r;
         ts.assign((size_t)KL * wn, -1.0);
         ti.assign((size_t)KL * wn, 0xffffffffu);
-        auto before = [](const std::pair<double, uint32_t>& a,
-                         const std::pair<double, uint32_t>& b) {
-          return a.first > b.first || (a.first == b.first && a.second < b.second);
-        };
-        // each shard's list is sorted: a world-way merge of the heads, stopping after KL
-        // entries.  Deep lists: every node a shard left out is at most the shard's last entry,
-        // so the union is certain only above the latest of those (and for its first topk_k():
-        // the global best few are within their shards' exact prefixes)
         std::vector<const double*> sc(world);
         std::vector<const uint32_t*> nd(world);
-        std::vector<uint32_t> head(world), len(world);
         for (int rk = 0; rk < world; ++rk) {
           const unsigned char* b = gathered.data() + (size_t)rk * lb;
           sc[rk] = reinterpret_cast<const double*>(b);
           nd[rk] = reinterpret_cast<const uint32_t*>(b + (size_t)KL * wn * 8);
         }
-        for (uint32_t p = from; p < wn; ++p) {
-          bool any_last = false;
-          std::pair<double, uint32_t> last_max{-1.0, 0xffffffffu};
-          for (int rk = 0; rk < world; ++rk) {
-            uint32_t l = 0;
-            while (l < KL && nd[rk][(size_t)l * wn + p] != 0xffffffffu) ++l;
-            len[rk] = l;
-            head[rk] = 0;
-            if (KL > K && l > 0) {
-              const std::pair<double, uint32_t> last{sc[rk][(size_t)(l - 1) * wn + p],
-                                                     nd[rk][(size_t)(l - 1) * wn + p]};
-              if (!any_last || before(last_max, last)) last_max = last;
-              any_last = true;
-            }
-          }
-          for (uint32_t k = 0; k < KL; ++k) {
-            int best = -1;
-            std::pair<double, uint32_t> bv{-1.0, 0xffffffffu};
-            for (int rk = 0; rk < world; ++rk) {
-              if (head[rk] >= len[rk]) continue;
-              const size_t o = (size_t)head[rk] * wn + p;
-              const std::pair<double, uint32_t> v{sc[rk][o], nd[rk][o]};
-              if (best < 0 || before(v, bv)) best = rk, bv = v;
-            }
-            if (best < 0) break;
-            if (any_last && k >= (uint32_t)topk_k() && !before(bv, last_max)) break;
-            ++head[best];
-            ts[(size_t)k * wn + p] = bv.first;
-            ti[(size_t)k * wn + p] = bv.second;
-          }
-        }
+        merge_shard_lists(world, wn, KL, KL > K, from, sc.data(), nd.data(), ts.data(),
+                          ti.data());
         return YODA_OK;
       };
       if ((rc = merged_lists(0, capacity))) return rc;
@@ -5942,6 +5956,41 @@ static int comm_greedy(yoda_t* const* hs, int n, int world, bool local, const yo
 }
 
 extern "C" {
+int yoda_greedy_cap_depth(void) { return (int)greedy_cap_depth(); }
+
+int yoda_shard_topk_deep(yoda_t* h, const uint64_t* d_maxima, const uint32_t* d_counts,
+                         uint32_t k, uint32_t deep, uint32_t* counts, double* top_score,
+                         uint32_t* top_node) {
+  if (!h) return YODA_ERR_INVALID_ARG;
+  if (deep > 1024) return fail(h, YODA_ERR_INVALID_ARG, "yoda_shard_topk_deep: deep > 1024");
+  return shard_topk_impl(h, d_maxima, d_counts, k, deep, counts, top_score, top_node);
+}
+
+int yoda_merge_shard_lists(uint32_t world, uint32_t wn, uint32_t kl, uint32_t from,
+                           const double* scores, const uint32_t* nodes, double* out_score,
+                           uint32_t* out_node) {
+  if (world < 1 || kl < 1 || from > wn || !scores || !nodes || !out_score || !out_node)
+    return YODA_ERR_INVALID_ARG;
+  try {
+    std::vector<const double*> sc(world);
+    std::vector<const uint32_t*> nd(world);
+    for (uint32_t rk = 0; rk < world; ++rk) {
+      sc[rk] = scores + (size_t)rk * kl * wn;
+      nd[rk] = nodes + (size_t)rk * kl * wn;
+    }
+    for (uint32_t k = 0; k < kl; ++k)
+      for (uint32_t p = from; p < wn; ++p) {
+        out_score[(size_t)k * wn + p] = -1.0;
+        out_node[(size_t)k * wn + p] = 0xffffffffu;
+      }
+    merge_shard_lists((int)world, wn, kl, kl > (uint32_t)topk_k_capacity(), from, sc.data(),
+                      nd.data(), out_score, out_node);
+    return YODA_OK;
+  } catch (...) {
+    return YODA_ERR_INVALID_ARG;
+  }
+}
+
 int yoda_comm_greedy_stats(const yoda_t* h, uint32_t* out) {
   if (!h || !out) return YODA_ERR_INVALID_ARG;
   std::copy(h->comm_greedy_stats, h->comm_greedy_stats + 5, out);

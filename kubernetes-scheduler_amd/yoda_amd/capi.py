@@ -79,6 +79,9 @@ _SIGS = {
     "yoda_set_node_state": ([_vp, _u32, _vp, _vp, _vp], C.c_int),
     "yoda_shard_topk": ([_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp], C.c_int),
     "yoda_shard_topk_depth": ([_vp], C.c_int),
+    "yoda_greedy_cap_depth": ([], C.c_int),
+    "yoda_shard_topk_deep": ([_vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp, _vp, _vp], C.c_int),
+    "yoda_merge_shard_lists": ([_u32, _u32, _u32, _u32, _vp, _vp, _vp, _vp], C.c_int),
     "yoda_shard_best_one": ([_vp, _u32, C.POINTER(C.c_double), C.POINTER(C.c_int32)], C.c_int),
     "yoda_shard_phase1_witness": ([_vp, _vp, _vp, _vp], C.c_int),
     "yoda_shard_witness_prepare": ([_vp, _vp, _vp, _vp], C.c_int),
@@ -454,17 +457,24 @@ class Yoda:
             self._check(k, "yoda_shard_topk_depth")
         return k
 
-    def shard_topk(self, d_maxima: int, d_counts: int, k: int | None = None):
-        """(counts [2, P], top_score [k, P], top_node [k, P]) of the uploaded batch; k defaults
-        to the handle's depth (shard_topk_depth); libyoda rejects any other k."""
+    def shard_topk(self, d_maxima: int, d_counts: int, k: int | None = None, deep: int = 0):
+        """(counts [2, P], top_score [d, P], top_node [d, P]) of the uploaded batch; k defaults
+        to the handle's depth (shard_topk_depth); libyoda rejects any other k.  deep > k
+        (capacity windows, yoda_shard_topk_deep): d = deep lists, exact down to their last
+        entry and 0xFFFFFFFF-ended past it; else d = k."""
         P = self.n_pods
         k = self.shard_topk_depth() if k is None else k
+        d = max(k, deep)
         counts = np.zeros((2, max(P, 1)), np.uint32)
-        ts = np.zeros((k, max(P, 1)), np.float64)
-        ti = np.zeros((k, max(P, 1)), np.uint32)
-        self._check(lib().yoda_shard_topk(self._h, _vp(d_maxima), _vp(d_counts), k,
-                                          _np_ptr(counts), _np_ptr(ts), _np_ptr(ti)),
-                    "yoda_shard_topk")
+        ts = np.zeros((d, max(P, 1)), np.float64)
+        ti = np.zeros((d, max(P, 1)), np.uint32)
+        if deep > k:
+            rc = lib().yoda_shard_topk_deep(self._h, _vp(d_maxima), _vp(d_counts), k, deep,
+                                            _np_ptr(counts), _np_ptr(ts), _np_ptr(ti))
+        else:
+            rc = lib().yoda_shard_topk(self._h, _vp(d_maxima), _vp(d_counts), k,
+                                       _np_ptr(counts), _np_ptr(ts), _np_ptr(ti))
+        self._check(rc, "yoda_shard_topk")
         return counts[:, :P], ts[:, :P], ti[:, :P]
 
     def shard_phase1_witness(self, d_maxima: int, d_counts: int, d_wit: int):
@@ -594,6 +604,31 @@ def topk_k() -> int:
 def topk_k_capacity() -> int:
     """Candidates per pod in the capacity windows' lists (yoda_topk_k_capacity)."""
     return int(lib().yoda_topk_k_capacity())
+
+
+def greedy_cap_depth() -> int:
+    """The sharded capacity windows' list depth (yoda_greedy_cap_depth)."""
+    return int(lib().yoda_greedy_cap_depth())
+
+
+def merge_shard_lists(scores, nodes, from_: int = 0):
+    """libyoda's list merge of the sharded greedy (yoda_merge_shard_lists, the one
+    yoda_comm_greedy runs): scores f64 / nodes u32 [world, kl, wn], each shard's lists sorted
+    score desc / node asc; returns ([kl, wn] scores, [kl, wn] nodes) of the union for window
+    pods [from_, wn), deep lists cut where an unlisted node could enter."""
+    S = np.ascontiguousarray(scores, np.float64)
+    I = np.ascontiguousarray(nodes, np.uint32)
+    if S.ndim != 3 or S.shape != I.shape:
+        raise ValueError("merge_shard_lists: scores and nodes must both be [world, kl, wn]")
+    world, kl, wn = S.shape
+    ts = np.full((kl, max(wn, 1)), -1.0, np.float64)
+    ti = np.full((kl, max(wn, 1)), 0xFFFFFFFF, np.uint32)
+    if wn:
+        rc = lib().yoda_merge_shard_lists(world, wn, kl, from_, _np_ptr(S), _np_ptr(I),
+                                          _np_ptr(ts), _np_ptr(ti))
+        if rc != 0:
+            raise YodaError(f"yoda_merge_shard_lists: {ERRORS.get(rc, rc)}")
+    return ts[:, :wn], ti[:, :wn]
 
 
 def next_window(progress: int, wmax: int) -> int:

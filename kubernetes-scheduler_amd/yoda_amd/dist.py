@@ -495,8 +495,9 @@ class HandleShard:
         """(maxima [6, P], wit [12, P]) after the merge and topk(), caller's pod order."""
         return self.h.shard_witness_download(self.bufs.maxima.data_ptr(), self.bufs.wit.data_ptr())
 
-    def topk(self, k: int | None = None):
-        return self.h.shard_topk(self.bufs.maxima.data_ptr(), self.bufs.counts.data_ptr(), k)
+    def topk(self, k: int | None = None, deep: int = 0):
+        return self.h.shard_topk(self.bufs.maxima.data_ptr(), self.bufs.counts.data_ptr(), k,
+                                 deep)
 
     def best_one(self, i: int):
         return self.h.shard_best_one(i)
@@ -508,12 +509,23 @@ class HandleShard:
 def merge_topk(ts_list: Sequence[np.ndarray], ti_list: Sequence[np.ndarray], k: int):
     """The first k of the union of the shards' candidate lists ([k, P] each), in the lists'
     order (score desc, node asc; padding -1.0 / 0xFFFFFFFF sorts last).  The global top-k is
-    contained in the union of the shards' top-k, so this is exact."""
+    contained in the union of the shards' top-k, so this is exact.  (A numpy restatement of
+    libyoda's merge for exact lists; the drivers call merge_gathered.)"""
     S = np.concatenate([np.asarray(t, np.float64) for t in ts_list], axis=0)
     I = np.concatenate([np.asarray(t).astype(np.uint64) for t in ti_list], axis=0)
     o = np.lexsort((I, -S), axis=0)[:k]
     return (np.take_along_axis(S, o, axis=0),
             np.take_along_axis(I, o, axis=0).astype(np.uint32))
+
+
+def merge_gathered(gathered) -> tuple:
+    """The world's gathered [2, d, P] lists (scores; nodes as f64) merged by libyoda's
+    yoda_merge_shard_lists -- the merge yoda_comm_greedy runs, so both drivers take the same
+    lists (deep capacity lists cut where an unlisted node could enter)."""
+    from .capi import merge_shard_lists
+    S = np.stack([np.asarray(x[0], np.float64) for x in gathered])
+    I = np.stack([np.asarray(x[1]).astype(np.uint32) for x in gathered])
+    return merge_shard_lists(S, I)
 
 
 def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window: int = 6144,
@@ -530,9 +542,10 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
     how far the last one got), as the single-handle yoda_greedy does.
     `shards`: this process's shards (HandleShard); `nodes`: the FULL snapshot.  The shards'
     node state is restored at the end."""
-    from .capi import GreedySession, next_window, topk_k, topk_k_capacity
+    from .capi import GreedySession, greedy_cap_depth, next_window, topk_k, topk_k_capacity
     k = topk_k()
-    k_cap = topk_k_capacity()  # the capacity windows' lists (yoda_greedy's depth)
+    k_cap = topk_k_capacity()  # the capacity windows' phase-1 depth
+    k_deep = greedy_cap_depth()  # their lists merged deeper (yoda_comm_greedy's window sequence)
     gs = GreedySession(nodes, pods, flags)
     order = gs.queue_order()
     P = pods.n_pods
@@ -550,7 +563,7 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
     def merged_lists():
         lists = [s.topk() for s in shards]
         g = reduce.gather([np.stack([ts, ti.astype(np.float64)]) for _, ts, ti in lists])
-        ts, ti = merge_topk([x[0] for x in g], [x[1].astype(np.uint64) for x in g], k)
+        ts, ti = merge_gathered(g)
         return lists[0][0], ts, ti
     generic = any(s.generic for s in shards)
     try:
@@ -580,11 +593,11 @@ def sharded_greedy(shards, reduce: Reducer, nodes, pods, flags: int = 0, window:
                 bufs = [s.phase1_witness() for s in shards]
                 sb = dict(zip(map(id, bufs), shards))
                 merge_witness(reduce, bufs, lambda b: sb[id(b)].witness_prepare(b))
-                lists = [s.topk(k_cap) for s in shards]
+                lists = [s.topk(k_cap, k_deep) for s in shards]
                 g = reduce.gather([np.stack([ts, ti.astype(np.float64)]) for _, ts, ti in lists])
-                ts, ti = merge_topk([x[0] for x in g], [x[1].astype(np.uint64) for x in g], k_cap)
+                ts, ti = merge_gathered(g)
                 mx, wit = shards[0].witness()
-                gs.begin_window(ws, k_cap, lists[0][0], ts, ti)
+                gs.begin_window(ws, ts.shape[0], lists[0][0], ts, ti)
                 gs.set_witness(mx, wit[:6], wit[6:])
                 nxt = gs.resolve()
                 windows += 1

@@ -59,6 +59,27 @@ def test_sharded_greedy_card_capacity():
         h.close()
 
 
+def test_sharded_greedy_drivers_same_windows():
+    """Capacity windows: dist.sharded_greedy (torch-side driver) and yoda_comm_greedy_local
+    (libyoda's own) take the same deep lists through the same merge (yoda_shard_topk_deep,
+    yoda_merge_shard_lists), so they run the same window sequence -- equal window and restart
+    counts -- and both equal the oracle."""
+    from yoda_amd.capi import comm_greedy_local
+    from yoda_amd.dist import sharded_greedy
+    nodes, pods = synth.make_config(5, pods=4000, nodes=3000)
+    want, _ = oracle.greedy(nodes, pods, MODE_SCV, 1)
+    handles, shards, red = _shards(nodes, 3, "n32")
+    stats = {}
+    got = sharded_greedy(shards, red, nodes, pods, 1, stats=stats)
+    np.testing.assert_array_equal(got, want)
+    lib_pick = comm_greedy_local(handles, nodes, pods, MODE_SCV, 1)
+    np.testing.assert_array_equal(lib_pick, want)
+    st = handles[0].comm_greedy_stats()
+    assert (stats["windows"], stats["restarts"]) == (st["windows"], st["restarts"]), (stats, st)
+    for h in handles:
+        h.close()
+
+
 def test_sharded_greedy_equals_single_handle():
     from yoda_amd.dist import sharded_greedy
     nodes, pods = synth.make_config(5, pods=6000, nodes=900)

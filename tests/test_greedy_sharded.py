@@ -16,16 +16,21 @@ import torch.multiprocessing as mp
 
 import oracle
 from yoda_amd import synth
-from yoda_amd.capi import topk_k
-from yoda_amd.dist import Reducer, ShardBuffers, shard_bounds, sharded_greedy
+from yoda_amd.capi import merge_shard_lists, topk_k, topk_k_capacity
+from yoda_amd.dist import Reducer, ShardBuffers, merge_topk, shard_bounds, sharded_greedy
 from yoda_amd.soa import MODE_SCV
 
 P, N = 60, 40
 
 
+# contended clusters hold more nodes per shard than the capacity windows' deep lists
+# (yoda_greedy_cap_depth, 64), so those lists end before the feasible set and windows restart
+N_CONTENDED, P_CONTENDED = 240, 200
+
+
 def _cluster(contended=False, seed=5):
-    nodes = synth.make_nodes(N, seed=seed)
-    pods = synth.make_pods(P, seed=seed + 1, priorities=True)
+    nodes = synth.make_nodes(N_CONTENDED if contended else N, seed=seed)
+    pods = synth.make_pods(P_CONTENDED if contended else P, seed=seed + 1, priorities=True)
     if not contended:
         nodes.total_memory_sum[3] = 0  # a zero-total node: the Error status
         return nodes.normalized(), pods.normalized()
@@ -72,8 +77,10 @@ class OracleShard:
                                             dtype=torch.int32))
         return self.bufs
 
-    def topk(self, k=None):
-        k, n = (topk_k() if k is None else k), self.pods.n_pods
+    def topk(self, k=None, deep=0):
+        # deep lists (capacity windows): the exact first `deep` -- exact down to their end, as
+        # libyoda's merged ones are
+        k, n = max(topk_k() if k is None else k, deep), self.pods.n_pods
         ts = np.full((k, n), -1.0)
         ti = np.full((k, n), 0xFFFFFFFF, np.uint32)
         for p in range(n):
@@ -147,7 +154,7 @@ def _want(nodes, pods, flags):
 @pytest.mark.parametrize("flags,window", [(0, 7), (0, 4096), (1, 4096), (1, 5)])
 def test_sharded_greedy_local(flags, window, contended):
     nodes, pods = _cluster(contended)
-    b = shard_bounds(N, 3)
+    b = shard_bounds(nodes.n_nodes, 3)
     shards = [OracleShard(nodes, int(b[r]), int(b[r + 1])) for r in range(3)]
     stats = {}
     got = sharded_greedy(shards, Reducer(local=True), nodes, pods, flags, window, stats)
@@ -166,7 +173,7 @@ def _worker(rank, world, port, flags, contended, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         nodes, pods = _cluster(contended)
-        b = shard_bounds(N, world)
+        b = shard_bounds(nodes.n_nodes, world)
         shard = OracleShard(nodes, int(b[rank]), int(b[rank + 1]))
         q.put((rank, sharded_greedy([shard], Reducer(), nodes, pods, flags, 16)))
     finally:
@@ -224,3 +231,58 @@ def test_sharded_greedy_refresh():
     got = sharded_greedy(shards, Reducer(local=True), nodes, pods, 0, 4096, stats)
     np.testing.assert_array_equal(got, _want(nodes, pods, 0))
     assert stats["refreshes"] > 0 and stats["exact_pods"] > 0, stats
+
+
+def _merge_restated(S, I, k_exact):
+    """yoda_merge_shard_lists restated: the union in (score desc, node asc) order, cut -- for
+    deep lists -- after the first k_exact at the first entry not above every shard's last."""
+    world, kl, wn = S.shape
+    ts = np.full((kl, wn), -1.0)
+    ti = np.full((kl, wn), 0xFFFFFFFF, np.uint32)
+    deep = kl > topk_k_capacity()
+    for p in range(wn):
+        ent, lasts = [], []
+        for r in range(world):
+            ln = 0
+            while ln < kl and I[r, ln, p] != 0xFFFFFFFF:
+                ln += 1
+            ent += [(-S[r, j, p], int(I[r, j, p])) for j in range(ln)]
+            if ln:
+                lasts.append((-S[r, ln - 1, p], int(I[r, ln - 1, p])))
+        ent.sort()
+        cut = max(lasts) if deep and lasts else None
+        for j, e in enumerate(ent[:kl]):
+            if cut is not None and j >= topk_k() and not e < cut:
+                break
+            ts[j, p], ti[j, p] = -e[0], e[1]
+    return ts, ti
+
+
+@pytest.mark.parametrize("kl", [8, 16, 64])
+def test_merge_shard_lists(kl):
+    """The list merge both sharded greedy drivers call (yoda_merge_shard_lists): exact lists
+    equal merge_topk's union; deep lists (kl > topk_k_capacity) end where a node a shard left
+    unlisted could enter."""
+    rng = np.random.default_rng(kl)
+    world, wn = 3, 40
+    S = np.full((world, kl, wn), -1.0)
+    I = np.full((world, kl, wn), 0xFFFFFFFF, np.uint32)
+    for r in range(world):
+        for p in range(wn):
+            ln = int(rng.integers(0, kl + 1))  # short (ended) and full lists
+            sc = np.sort(rng.integers(0, 30, ln).astype(np.float64))[::-1]  # ties across shards
+            nd = np.sort(rng.choice(np.arange(r * 1000, r * 1000 + 500), ln, replace=False))
+            o = np.lexsort((nd, -sc))
+            S[r, :ln, p], I[r, :ln, p] = sc[o], nd[o]
+    ts, ti = merge_shard_lists(S, I)
+    want_s, want_i = _merge_restated(S, I, topk_k())
+    np.testing.assert_array_equal(ts, want_s)
+    np.testing.assert_array_equal(ti, want_i)
+    if kl <= topk_k_capacity():  # exact lists: the plain union
+        ms, mi = merge_topk(list(S), list(I), kl)
+        np.testing.assert_array_equal(ti, mi)
+        np.testing.assert_array_equal(ts, np.where(mi == 0xFFFFFFFF, -1.0, ms))
+    # pods before `from` are left as initialised
+    ts2, ti2 = merge_shard_lists(S, I, from_=wn // 2)
+    np.testing.assert_array_equal(ti2[:, :wn // 2], 0xFFFFFFFF)
+    np.testing.assert_array_equal(ti2[:, wn // 2:], ti[:, wn // 2:])
