@@ -835,8 +835,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     const uint32_t pw0 = pf_pw, t_all = pf_ta, t_none = pf_tn;
     if (YODA_K1_PF && nxt != ~0u) load_sum(nxt);
     if (!need_uni) {  // the node's healthy frees for the per-pod pass: lds[node][need - 1] (slot K: 0)
+      // (all K loads in flight before the first LDS write: one round trip, not K / 2)
+      uint32_t hv[K];
 #pragma unroll
-      for (int t = 0; t < K; ++t) lds[lane * HW + t] = s[64 * (kSumHfs + t)];
+      for (int t = 0; t < K; ++t) hv[t] = s[64 * (kSumHfs + t)];
+#pragma unroll
+      for (int t = 0; t < K; ++t) lds[lane * HW + t] = hv[t];
       lds[lane * HW + K] = 0u;
     }
     const uint64_t cn = (uint64_t)w0.x | ((uint64_t)w0.y << 32);
@@ -1143,55 +1147,66 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
       const uint32_t bi = g + lane;
       const bool bv = bi < b1;
       const uint32_t* B = bsm + sum_index(bv ? bi : b0, 0, BST);  // word w at B[64 w]
+      // Every word the decisions read, loaded up front and tested bitwise: one memory round
+      // trip per 64 blocks.  (As short-circuit tests each load was issued only once the test
+      // before it had its answer: ~10 dependent round trips per 64 blocks, up to 16 more in the
+      // K2 cost hint's loop below -- most of a no-PART task's block pass.)
       const uint32_t fl = B[64 * kBsFlags], ckmin = B[64 * kBsCkMin], ckmax = B[64 * kBsCkMax];
       const uint32_t cn_min = B[64 * kBsCnMin], cn_max = B[64 * kBsCnMax];
-      const uint32_t nreal = bv ? B[64 * kBsNReal] : 0u;
+      const uint32_t nreal_w = B[64 * kBsNReal], t_none = B[64 * bs_tn], t_all = B[64 * bs_ta];
+      const uint32_t hck_min = B[64 * kBsHckMin], hck_max = B[64 * kBsHckMax];
+      const uint32_t nh_min = B[64 * kBsNhMin], nh_max = B[64 * kBsNhMax];
+      const uint32_t mrf_min = B[64 * kBsMrfMin], mrf_max = B[64 * kBsMrfMax];
+      const uint32_t nreal = bv ? nreal_w : 0u;
       // every node NONE: PodFitsNumber, PodFitsMemory or PodFitsClock fails on all of them
-      bool bnone = cn_max != 0xffffffffu && num_min > (uint64_t)cn_max;
-      bnone = bnone || (all_pm && (!hfs_none_ok || B[64 * bs_tn] <= s_mpm_min));
+      bool bnone = (cn_max != 0xffffffffu) & (num_min > (uint64_t)cn_max);
+      bnone |= all_pm & (!hfs_none_ok | (t_none <= s_mpm_min));
       if (all_pc && c_uni) {
         // no healthy card of the block has the wave's clock (hc = 0 < need), or one-model
         // nodes of that clock with too few healthy cards
-        bnone = bnone || cpc_max < B[64 * kBsHckMin] || cpc_max > B[64 * kBsHckMax] ||
-                ((fl & kBsUni4) && ckmin == ckmax && ckmin == cpc_max &&
-                 B[64 * kBsNhMax] < nc_min);
+        bnone |= (cpc_max < hck_min) | (cpc_max > hck_max) |
+                 (((fl & kBsUni4) != 0u) & (ckmin == ckmax) & (ckmin == cpc_max) &
+                  (nh_max < nc_min));
       }
       // every node ALL: feasible for every pod, one-model, and all or none qualifying
-      bool ball = (fl & kBsOneModel) && num_max <= (uint64_t)cn_min;
-      ball = ball && (!any_pm || (hfs_all_ok && B[64 * bs_ta] > s_mpm_max));
-      ball = ball && (!any_pc || (c_uni && ckmin == ckmax && ckmin == cpc_max &&
-                                  B[64 * kBsNhMin] >= nc_max));
-      const bool allq = ckmin >= s_c_max && B[64 * kBsMrfMin] > s_m_max;
-      const bool noq = ckmax < s_c_min || B[64 * kBsMrfMax] <= s_m_min;
-      ball = ball && (allq || noq) && !bnone;
-      bnone = bnone && bv && nreal > 0u;
-      ball = ball && bv && nreal > 0u;
+      bool ball = ((fl & kBsOneModel) != 0u) & (num_max <= (uint64_t)cn_min);
+      ball &= !any_pm | (hfs_all_ok & (t_all > s_mpm_max));
+      ball &= !any_pc | (c_uni & (ckmin == ckmax) & (ckmin == cpc_max) & (nh_min >= nc_max));
+      const bool allq = (ckmin >= s_c_max) & (mrf_min > s_m_max);
+      const bool noq = (ckmax < s_c_min) | (mrf_max <= s_m_min);
+      ball &= (allq | noq) & !bnone;
+      bnone &= bv & (nreal > 0u);
+      ball &= bv & (nreal > 0u);
       const uint64_t none_m = ballot(bnone), all_m = ballot(ball);
-#ifndef YODA_ABL_K1_NOBS
-      if (ball) {  // (NONE blocks: unlisted, unwritten)
+      if (ball) {
+#ifndef YODA_ABL_K1_NOBS  // (NONE blocks: unlisted, unwritten)
         const uint64_t vb = nreal >= 64u ? ~0ull : ((1ull << nreal) - 1ull);
         bsw[bi] = BlockMask{vb, vb};
-      }
 #endif
-      if (ball) {
-        g_nf += nreal;
-        g_nz += B[64 * kBsNzt];
-        if (seeding && kbub != nullptr) {  // the block's lv[l_hi]: a node every pod passes scores it
-          const uint32_t w = kbub_lvl(K) + 2u * l_hi;
-          const uint32_t* U = kbub + sum_index(bi, w, kbub_stride(K));
-          const double v = __longlong_as_double((long long)((uint64_t)U[0] | ((uint64_t)U[64] << 32)));
-          if (v > 0.0) atomicMax(sdw, (unsigned long long)v);
-        }
-        if constexpr (!WIT) {
-          // K2 cost hint (wts): a block whose q-th healthy frees straddle the wave's memory
-          // range leaves the K2 counting qualifying cards per pod on its nodes
-          if (wts != nullptr && s_m_min != s_m_max) {
-            bool nu = false;
+        // the words an ALL block folds in, issued together (one more round trip)
+        const uint32_t nzt = B[64 * kBsNzt];
+        uint32_t bmx[6];
 #pragma unroll
-            for (int q = 0; q < K; ++q)
-              nu = nu || (B[64 * (kBsT + q)] <= s_m_max && B[64 * (kBsT + K + q)] > s_m_min);
-            g_nu += nu ? nreal : 0u;
-          }
+        for (int f = 0; f < 6; ++f) bmx[f] = WIT ? 0u : B[64 * (kBsMx + f)];
+        uint64_t lv = 0ull;  // the block's lv[l_hi]: a node every pod passes scores it
+        if (seeding && kbub != nullptr) {
+          const uint32_t* U = kbub + sum_index(bi, kbub_lvl(K) + 2u * l_hi, kbub_stride(K));
+          lv = (uint64_t)U[0] | ((uint64_t)U[64] << 32);
+        }
+        // K2 cost hint (wts): a block whose q-th healthy frees straddle the wave's memory
+        // range leaves the K2 counting qualifying cards per pod on its nodes
+        bool nu = false;
+        if (!WIT && wts != nullptr && s_m_min != s_m_max) {
+#pragma unroll
+          for (int q = 0; q < K; ++q)
+            nu |= (B[64 * (kBsT + q)] <= s_m_max) & (B[64 * (kBsT + K + q)] > s_m_min);
+        }
+        g_nf += nreal;
+        g_nz += nzt;
+        g_nu += nu ? nreal : 0u;
+        if (seeding && kbub != nullptr) {
+          const double v = __longlong_as_double((long long)lv);
+          if (v > 0.0) atomicMax(sdw, (unsigned long long)v);
         }
         if (allq) {
           if constexpr (WIT) {  // (the same rule as a node's: larger replaces, equal adds)
@@ -1205,12 +1220,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
               aw[f] = gt ? v : aw[f];
             }
           } else {
-            a_bw = max(a_bw, B[64 * (kBsMx + kMaxBw)]);
-            a_ck = max(a_ck, B[64 * (kBsMx + kMaxClock)]);
-            a_core = max(a_core, B[64 * (kBsMx + kMaxCore)]);
-            a_free = max(a_free, B[64 * (kBsMx + kMaxFree)]);
-            a_pw = max(a_pw, B[64 * (kBsMx + kMaxPower)]);
-            a_tot = max(a_tot, B[64 * (kBsMx + kMaxTotal)]);
+            a_bw = max(a_bw, bmx[kMaxBw]);
+            a_ck = max(a_ck, bmx[kMaxClock]);
+            a_core = max(a_core, bmx[kMaxCore]);
+            a_free = max(a_free, bmx[kMaxFree]);
+            a_pw = max(a_pw, bmx[kMaxPower]);
+            a_tot = max(a_tot, bmx[kMaxTotal]);
           }
         }
       }

@@ -82,3 +82,8 @@ st = (t[:, 0] - t[:, 0].min()) / 100.0
 out["starts_by_tenth"] = np.histogram(st, bins=10, range=(0, span))[0].tolist()
 out["ends_by_tenth"] = np.histogram((t[:, 1] - t[:, 0].min()) / 100.0, bins=10, range=(0, span))[0].tolist()
 print(json.dumps(out), flush=True)
+# raw records for offline analysis (TASK_TRACE_DUMP=<path.npz>): slot (= wave * chunks + chunk),
+# start, end, npart, word 3
+dump = os.environ.get("TASK_TRACE_DUMP")
+if dump:
+    np.savez_compressed(dump, slot=np.nonzero(used)[0], rec=tr[used])
