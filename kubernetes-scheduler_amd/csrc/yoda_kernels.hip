@@ -2616,31 +2616,47 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     if (dec) {  // static + nq shared + 3 r_free F + r_total T, each maximised over the block
       constexpr uint32_t DS = kbdec_stride();
       const uint32_t* D = args.kbdec;
-      if (args.levels == nullptr || D[sum_index(b, kDecOk, DS)] == 0u) return HUGE_VAL;
-      auto d64 = [&](uint32_t w) {
-        return __longlong_as_double((long long)((uint64_t)D[sum_index(b, w, DS)] |
-                                                ((uint64_t)D[sum_index(b, w + 1u, DS)] << 32)));
+      if (args.levels == nullptr) return HUGE_VAL;
+      // every word loaded before the first test (one round trip; the ok flag gated them before)
+      const uint32_t ok = D[sum_index(b, kDecOk, DS)];
+      const uint32_t wbw = D[sum_index(b, kDecBw, DS)], wck = D[sum_index(b, kDecCk, DS)];
+      const uint32_t wco = D[sum_index(b, kDecCo, DS)], wpw = D[sum_index(b, kDecPw, DS)];
+      const uint32_t wq = D[sum_index(b, kDecQl + l_lo, DS)];
+      uint32_t w2[6];
+      const uint32_t wsrc[3] = {kDecStat, kbdec_fl(l_lo), kbdec_tl(l_lo)};
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        w2[2 * i] = D[sum_index(b, wsrc[i], DS)];
+        w2[2 * i + 1] = D[sum_index(b, wsrc[i] + 1u, DS)];
+      }
+      __builtin_amdgcn_sched_group_barrier(0x0020, 12, 0);  // (the VMEM reads above, grouped)
+      auto d64 = [&](int i) {
+        return __longlong_as_double((long long)((uint64_t)w2[2 * i] | ((uint64_t)w2[2 * i + 1] << 32)));
       };
       const RS* r = reinterpret_cast<const RS*>(lds + RCPS + 16 * kSets);
       const double* rd = reinterpret_cast<const double*>(lds + RCPS + 16 * kSets + 8);
-      const uint32_t sh = card_shared_terms(D[sum_index(b, kDecBw, DS)], D[sum_index(b, kDecCk, DS)],
-                                            D[sum_index(b, kDecCo, DS)], D[sum_index(b, kDecPw, DS)],
-                                            r[0], r[1], r[2]);
-      const double q = (double)D[sum_index(b, kDecQl + l_lo, DS)];
+      const uint32_t sh = card_shared_terms(wbw, wck, wco, wpw, r[0], r[1], r[2]);
+      const double q = (double)wq;
       // (+1: the f64 rounding of the products; the scores are integers)
-      return d64(kDecStat) + q * (double)sh + 3.0 * rd[0] * d64(kbdec_fl(l_lo)) +
-             rd[1] * d64(kbdec_tl(l_lo)) + 1.0;
+      const double ub = d64(0) + q * (double)sh + 3.0 * rd[0] * d64(1) + rd[1] * d64(2) + 1.0;
+      return ok == 0u ? HUGE_VAL : ub;
     }
     const uint32_t* U = args.kbub;
+    // the block's K largest frees and its level bound, all in flight together (the level
+    // words do not depend on J); then the J-indexed bound: two round trips
+    uint32_t fm[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) fm[k] = U[sum_index(b, kbub_fmax(K) + (uint32_t)k, KBST)];
+    // (lvw == 0: no level bound -- words 0 and 1 read and ignored, so no branch splits the group)
+    const uint32_t lv_lo = U[sum_index(b, lvw, KBST)], lv_hi = U[sum_index(b, lvw + 1u, KBST)];
+    __builtin_amdgcn_sched_group_barrier(0x0020, K + 2, 0);  // (the VMEM reads above, grouped)
     uint32_t J = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k)
-      J += U[sum_index(b, kbub_fmax(K) + (uint32_t)k, KBST)] >= m_min ? 1u : 0u;
+    for (int k = 0; k < K; ++k) J += fm[k] >= m_min ? 1u : 0u;
     double ub = __longlong_as_double((long long)((uint64_t)U[sum_index(b, 2 * J, KBST)] |
                                                  ((uint64_t)U[sum_index(b, 2 * J + 1, KBST)] << 32)));
     if (lvw != 0u)
-      ub = fmin(ub, __longlong_as_double((long long)((uint64_t)U[sum_index(b, lvw, KBST)] |
-                                                     ((uint64_t)U[sum_index(b, lvw + 1u, KBST)] << 32))));
+      ub = fmin(ub, __longlong_as_double((long long)((uint64_t)lv_lo | ((uint64_t)lv_hi << 32))));
     return ub;
   };
   auto pruned = [&](double ub) -> bool {
@@ -2658,18 +2674,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     const uint32_t nid = (args.ids && valid0) ? args.ids[n] : n;
     if (args.ids) lds[IDW + lane] = nid;
     const bool valid = n < n1;
-    // the wave's mask of node n: from the block's (nz, full) words, and a load of its own
-    // only for a partial node (sparse form); or the dense [wave][node] array
-    uint64_t mask, feas_b;
-    if (bsw) {
-      const BlockMask bk = bsw[nb >> 6];
-      mask = ((bk.full >> lane) & 1ull) ? live_mask : 0ull;
-      if (((bk.nz & ~bk.full) >> lane) & 1ull) mask = bmw[n];
-      feas_b = bk.nz;
-    } else {
-      mask = valid ? bmw[n] : 0ull;
-      feas_b = ballot(mask != 0ull);
-    }
+    // the block's (nz, full) mask words and its summaries, loaded together (before the branch
+    // to a partial node's own mask: one round trip for both, not two)
+    BlockMask bk{0ull, 0ull};
+    if (bsw) bk = bsw[nb >> 6];
     // this block's tile of summaries (nb is a multiple of 64): word w at s[64 w]
     const uint32_t* s = reinterpret_cast<const uint32_t*>(sum2) + sum_index(nb, 0, S2) + lane;
     const uint4 h0 = make_uint4(s[64 * kS2Static], s[64 * (kS2Static + 1)], s[64 * kS2Clock],
@@ -2689,6 +2697,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(K <= 8 ?
     } else {
 #pragma unroll
       for (int t = 0; t < K; ++t) ts.v[t] = s[64 * (kS2Fs + K + t)];
+    }
+    // the wave's mask of node n: from the block's (nz, full) words, and a load of its own
+    // only for a partial node (sparse form); or the dense [wave][node] array
+    uint64_t mask, feas_b;
+    if (bsw) {
+      mask = ((bk.full >> lane) & 1ull) ? live_mask : 0ull;
+      if (((bk.nz & ~bk.full) >> lane) & 1ull) mask = bmw[n];
+      feas_b = bk.nz;
+    } else {
+      mask = valid ? bmw[n] : 0ull;
+      feas_b = ballot(mask != 0ull);
     }
     if (feas_b == 0) return;  // no pod of the wave can use any node of the block
     worked = true;
