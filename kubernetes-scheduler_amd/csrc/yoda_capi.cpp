@@ -41,6 +41,8 @@ hipError_t launch_reduce1(const Partials& part, uint32_t C, uint32_t n_pods, uin
                           const MemTab& mt, hipStream_t s,
                           uint32_t* lpt_w = nullptr, uint32_t* lpt_order = nullptr,
                           const uint64_t* cmask = nullptr);
+hipError_t launch_k1_order(int K, const PodParams& pp, uint32_t n_pods, uint32_t n_nodes,
+                           uint32_t* wts, uint32_t* order, hipStream_t s);
 hipError_t launch_mem_rank(const uint64_t* m_u, uint32_t n_pods, const MemTab& mt, uint32_t* m32,
                            hipStream_t s);
 hipError_t launch_prep2(const uint64_t* maxima, uint32_t n_pods, double* rcp,
@@ -497,6 +499,10 @@ struct yoda_handle {
   // the per-wave weights K1 adds to (zero between runs), the order (valid once sorted)
   bool lpt_active = false, lpt_sorted = false;
   DevBuf lpt_w, lpt_order;           // K1 waves per chunk (4: k1_block_n32's SUB, chunk1 = a quarter)
+  // the block K1's own heaviest-first order (k1_probe's weights, ranked before the K1): valid
+  // for this run once k1_sorted
+  bool k1_sorted = false;
+  DevBuf k1_w, k1_order;
   uint32_t C2 = 1, chunk2 = 32;  // K2 / K3 node chunking
   int cap[2][3][2] = {};         // resident workgroups per (kernel, path, mode), cached
   int last_mode = -1;
@@ -560,7 +566,7 @@ struct yoda_handle {
                      &order_bstart, &order_slot, &order_bkt,
                      &rcp,       &best,       &idx,          &ties,
                      &lowest,    &pick,      &status,     &ties_out,     &flagged,
-                     &n_flagged, &bitmask,   &bitmask_t,  &blk,  &bsum, &p_max_u,      &p_cnt, &lpt_w, &lpt_order,
+                     &n_flagged, &bitmask,   &bitmask_t,  &blk,  &bsum, &p_max_u,      &p_cnt, &lpt_w, &lpt_order, &k1_w, &k1_order,
                      &rows,      &rows_t,    &norm,      &tk_s_part,  &tk_i_part,    &tk_s,
                      &tk_i,      &upd_node,  &upd_val,    &upd_cn,    &g1_part,   &g1_done,
                      &p_best_f,  &p_best_i,  &p_idx,      &p_ties,       &p_low_f,
@@ -940,6 +946,7 @@ PodParams pod_params(yoda_t* h) {
   if (h->lpt_active) {
     pp.lpt_w = h->lpt_w.as<uint32_t>();
     if (h->lpt_sorted) pp.lpt_order = h->lpt_order.as<uint32_t>();
+    if (h->k1_sorted) pp.k1_order = h->k1_order.as<uint32_t>();
   }
   return pp;
 }
@@ -1438,7 +1445,6 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts,
   Partials part = partials(h);
   hipEvent_t e0 = h->profiling ? h->next_event() : nullptr;
   hipEvent_t e1 = h->profiling ? h->next_event() : nullptr;
-  if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
   h->blk_valid = h->has_k1sum;
   h->bm_sparse = h->has_k1sum;  // the block K1 writes the sparse form
   h->seeds_valid = h->has_k1sum && mode == YODA_MODE_SCV;
@@ -1454,6 +1460,23 @@ int phase1(yoda_t* h, int mode, uint64_t* maxima, uint32_t* counts,
       (h->kbub_dirty || h->kbub_loose) && h->path == Path::N32 && h->has_k2sum && h->g.tab)
     HIP_TRY(h, build_block_ub(h));
   if (h->blksum_loose && !h->greedy_active) HIP_TRY(h, tighten_block_sums(h));
+  // the block K1 visits its pod blocks heaviest first too (k1_probe: the per-node work its
+  // whole-block decisions leave each wave on a sample of blocks; YODA_K1_LPT=0: launch order)
+  static const bool k1_lpt_env = YODA_KNOB("YODA_K1_LPT", 1) != 0;
+  h->k1_sorted = false;
+  if (k1_lpt_env && h->lpt_active && h->k1_sub == 1u && mode == YODA_MODE_SCV) {
+    const PodParams pp0 = pod_params(h);
+    if (pp0.bsum != nullptr) {
+      const uint32_t n_pb = (P + kBlock - 1) / kBlock;
+      HIP_TRY(h, h->k1_w.ensure((size_t)((P + 63) / 64) * 4));
+      HIP_TRY(h, h->k1_order.ensure((size_t)n_pb * 4));
+      HIP_TRY(h, launch_k1_order(h->K, pp0, P, h->n_nodes, h->k1_w.as<uint32_t>(),
+                                 h->k1_order.as<uint32_t>(), h->stream));
+      h->k1_sorted = true;
+    }
+  }
+  // (the K1 profile events bracket the K1 launch alone, as rocprofv3's kernel trace does)
+  if (e0) HIP_TRY(h, hipEventRecord(e0, h->stream));
   HIP_TRY(h, launch_k1(h->K, h->path, h->nodes.as<unsigned char>(),
                        h->has_k1sum ? (pr ? h->k1sum_p : h->k1sum).as<unsigned char>() : nullptr,
                        (pr ? h->k2sum_p : h->k2sum).as<unsigned char>(),

@@ -656,6 +656,58 @@ __device__ __forceinline__ uint32_t narrow_floor(int w, uint32_t nw) {  // floor
 // quarter of the chunk (chunk_nodes = the quarter), and merge their partials in LDS at the end:
 // a quarter of the partial bytes (and of k_reduce1's reads) for the same (wave, node-range)
 // tasks -- 24 B per (pod, chunk) written once per chunk instead of once per quarter.
+// The wave bounds K1's whole-block decisions compare against (k1_block_class), from the wave's
+// pods: scv/number, scv/memory (m, the need in cards), scv/clock (c, the need in cards).
+struct K1Wave {
+  uint64_t num_min, num_max;
+  uint32_t mpm_min, mpm_max;  // m over the pods with the scv/memory label
+  uint32_t m_min, m_max, c_min, c_max;
+  uint32_t cpc_max, nc_min, nc_max;  // c and the need over the pods with the scv/clock label
+  uint32_t bs_tn, bs_ta;  // BlockSumWord words: the q-th healthy free's min / max for the needs
+  bool any_pm, all_pm, any_pc, all_pc, c_uni, hfs_all_ok, hfs_none_ok;
+};
+// K1's whole-block decision for a block (its BlockSumWord words at B[64 w]): every node NONE
+// (PodFitsNumber, PodFitsMemory or PodFitsClock fails for every pod of the wave), or every node
+// ALL (one-model, feasible for every pod, its cards all qualifying -- allq -- or none).  Every
+// word is loaded up front and tested bitwise: one memory round trip per 64 blocks.  (As short-
+// circuit tests each load was issued only once the test before it had its answer: ~10 dependent
+// round trips per 64 blocks -- most of a K1 task's block pass.)  Shared by the block K1 and its
+// cost probe (k1_probe), so both classify alike.  Sufficient conditions of the per-node tests.
+struct K1BlockClass {
+  bool none, all, allq;
+  uint32_t nreal;  // the block's real nodes (0 for an invalid lane)
+};
+__device__ __forceinline__ K1BlockClass k1_block_class(const uint32_t* B, bool bv,
+                                                       const K1Wave& w) {
+  const uint32_t fl = B[64 * kBsFlags], ckmin = B[64 * kBsCkMin], ckmax = B[64 * kBsCkMax];
+  const uint32_t cn_min = B[64 * kBsCnMin], cn_max = B[64 * kBsCnMax];
+  const uint32_t nreal_w = B[64 * kBsNReal], t_none = B[64 * w.bs_tn], t_all = B[64 * w.bs_ta];
+  const uint32_t hck_min = B[64 * kBsHckMin], hck_max = B[64 * kBsHckMax];
+  const uint32_t nh_min = B[64 * kBsNhMin], nh_max = B[64 * kBsNhMax];
+  const uint32_t mrf_min = B[64 * kBsMrfMin], mrf_max = B[64 * kBsMrfMax];
+  K1BlockClass r;
+  r.nreal = bv ? nreal_w : 0u;
+  bool bnone = (cn_max != 0xffffffffu) & (w.num_min > (uint64_t)cn_max);
+  bnone |= w.all_pm & (!w.hfs_none_ok | (t_none <= w.mpm_min));
+  if (w.all_pc && w.c_uni) {
+    // no healthy card of the block has the wave's clock (hc = 0 < need), or one-model nodes
+    // of that clock with too few healthy cards
+    bnone |= (w.cpc_max < hck_min) | (w.cpc_max > hck_max) |
+             (((fl & kBsUni4) != 0u) & (ckmin == ckmax) & (ckmin == w.cpc_max) &
+              (nh_max < w.nc_min));
+  }
+  bool ball = ((fl & kBsOneModel) != 0u) & (w.num_max <= (uint64_t)cn_min);
+  ball &= !w.any_pm | (w.hfs_all_ok & (t_all > w.mpm_max));
+  ball &= !w.any_pc |
+          (w.c_uni & (ckmin == ckmax) & (ckmin == w.cpc_max) & (nh_min >= w.nc_max));
+  r.allq = (ckmin >= w.c_max) & (mrf_min > w.m_max);
+  const bool noq = (ckmax < w.c_min) | (mrf_max <= w.m_min);
+  ball &= (r.allq | noq) & !bnone;
+  r.none = bnone & bv & (r.nreal > 0u);
+  r.all = ball & bv & (r.nreal > 0u);
+  return r;
+}
+
 template <int K, bool STATS, bool MIX = true, bool WIT = false, int SUB = 1>
 #ifndef YODA_K1_WAVES
 #define YODA_K1_WAVES 6  // (7: 9 VGPRs spilled, ~90 MB of scratch writes per launch; r05j)
@@ -678,7 +730,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     const uint32_t* __restrict__ kbub = nullptr, const uint32_t* __restrict__ levels = nullptr,
     unsigned long long* __restrict__ seed_out = nullptr,
     unsigned long long* __restrict__ cmask = nullptr,
-    const uint32_t* __restrict__ ids = nullptr) {
+    const uint32_t* __restrict__ ids = nullptr,
+    const uint32_t* __restrict__ pb_order = nullptr) {
   static_assert(!(WIT && MIX), "the witness K1 serves one-model snapshots");
   static_assert(SUB == 1 || (SUB == kBlock / kWave && !WIT), "SUB: 1, or one pod wave per workgroup");
   constexpr uint32_t SS = k1sum_stride(K);
@@ -692,7 +745,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   const uint32_t lane = lane_id();
   const Tile tl = tile();
   const uint32_t sub = SUB > 1 ? threadIdx.x >> 6 : 0u;
-  const uint32_t p = SUB > 1 ? tl.pb * kWave + lane : tl.pb * kBlock + threadIdx.x;
+  // pb_order: the pod blocks heaviest first (k1_probe + k_lpt_order), so the long tasks do not
+  // start last (SUB = 1)
+  const uint32_t pbk = (SUB == 1 && pb_order != nullptr) ? pb_order[tl.pb] : tl.pb;
+  const uint32_t p = SUB > 1 ? tl.pb * kWave + lane : pbk * kBlock + threadIdx.x;
   const uint32_t chunk = tl.chunk, C = gridDim.y;
   const uint32_t n0 = (chunk * SUB + sub) * chunk_nodes;
   const uint32_t n1 = min(n0 + chunk_nodes, n_nodes);
@@ -821,6 +877,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     for (uint32_t l = kKbLevels - 1u; l-- > 0u;) l_hi = levels[l] >= s_m_max ? l : l_hi;
   const uint32_t bs_tn = kBsT + (uint32_t)K + (hfs_none_ok && nm_min > 0u ? nm_min - 1u : 0u);
   const uint32_t bs_ta = kBsT + (any_pm && hfs_all_ok && nm_max > 0u ? nm_max - 1u : 0u);
+  const K1Wave kw{num_min, num_max, s_mpm_min, s_mpm_max, s_m_min, s_m_max, s_c_min, s_c_max,
+                  cpc_max, nc_min, nc_max, bs_tn, bs_ta, any_pm, all_pm, any_pc, all_pc, c_uni,
+                  hfs_all_ok, hfs_none_ok};
   // per-node classification of one 64-node block (below: only the blocks the block summaries
   // leave undecided)
   // (nxt: the block node_block visits next, whose summary words are loaded here -- the
@@ -1147,36 +1206,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
       const uint32_t bi = g + lane;
       const bool bv = bi < b1;
       const uint32_t* B = bsm + sum_index(bv ? bi : b0, 0, BST);  // word w at B[64 w]
-      // Every word the decisions read, loaded up front and tested bitwise: one memory round
-      // trip per 64 blocks.  (As short-circuit tests each load was issued only once the test
-      // before it had its answer: ~10 dependent round trips per 64 blocks, up to 16 more in the
-      // K2 cost hint's loop below -- most of a no-PART task's block pass.)
-      const uint32_t fl = B[64 * kBsFlags], ckmin = B[64 * kBsCkMin], ckmax = B[64 * kBsCkMax];
-      const uint32_t cn_min = B[64 * kBsCnMin], cn_max = B[64 * kBsCnMax];
-      const uint32_t nreal_w = B[64 * kBsNReal], t_none = B[64 * bs_tn], t_all = B[64 * bs_ta];
-      const uint32_t hck_min = B[64 * kBsHckMin], hck_max = B[64 * kBsHckMax];
-      const uint32_t nh_min = B[64 * kBsNhMin], nh_max = B[64 * kBsNhMax];
-      const uint32_t mrf_min = B[64 * kBsMrfMin], mrf_max = B[64 * kBsMrfMax];
-      const uint32_t nreal = bv ? nreal_w : 0u;
-      // every node NONE: PodFitsNumber, PodFitsMemory or PodFitsClock fails on all of them
-      bool bnone = (cn_max != 0xffffffffu) & (num_min > (uint64_t)cn_max);
-      bnone |= all_pm & (!hfs_none_ok | (t_none <= s_mpm_min));
-      if (all_pc && c_uni) {
-        // no healthy card of the block has the wave's clock (hc = 0 < need), or one-model
-        // nodes of that clock with too few healthy cards
-        bnone |= (cpc_max < hck_min) | (cpc_max > hck_max) |
-                 (((fl & kBsUni4) != 0u) & (ckmin == ckmax) & (ckmin == cpc_max) &
-                  (nh_max < nc_min));
-      }
-      // every node ALL: feasible for every pod, one-model, and all or none qualifying
-      bool ball = ((fl & kBsOneModel) != 0u) & (num_max <= (uint64_t)cn_min);
-      ball &= !any_pm | (hfs_all_ok & (t_all > s_mpm_max));
-      ball &= !any_pc | (c_uni & (ckmin == ckmax) & (ckmin == cpc_max) & (nh_min >= nc_max));
-      const bool allq = (ckmin >= s_c_max) & (mrf_min > s_m_max);
-      const bool noq = (ckmax < s_c_min) | (mrf_max <= s_m_min);
-      ball &= (allq | noq) & !bnone;
-      bnone &= bv & (nreal > 0u);
-      ball &= bv & (nreal > 0u);
+      const K1BlockClass cls = k1_block_class(B, bv, kw);
+      const bool bnone = cls.none, ball = cls.all, allq = cls.allq;
+      const uint32_t nreal = cls.nreal;
       const uint64_t none_m = ballot(bnone), all_m = ballot(ball);
       if (ball) {
 #ifndef YODA_ABL_K1_NOBS  // (NONE blocks: unlisted, unwritten)
@@ -1518,6 +1550,69 @@ __device__ void lpt_order_body(uint32_t* __restrict__ wts, uint32_t n_waves, uin
     order[r] = i;
   }
 }
+// Cost probe of the block K1, for its heaviest-first pod-block order (k1_order): per pod wave,
+// how many of 64 blocks sampled evenly across the snapshot the wave's whole-block decisions
+// (k1_block_class, the block K1's) leave to the per-node pass.  The node order deals every free
+// level into any run of blocks, so the sample stands for the wave's chunks, and a
+// wave's per-node work sets its tasks' length: in a K1 trace the wave explains 91 % of the task-
+// time variance, and list scheduling the pod blocks heaviest first shortens the launch by a
+// fifth (the tail of late long tasks).  wts[wave] = 1 + that count (k_lpt_order ranks them).
+// Grid: one 256-pod block of the sorted batch per workgroup, one pod wave per wave.
+__global__ __launch_bounds__(kBlock) void k1_probe(
+    const uint32_t* __restrict__ m_in, const uint32_t* __restrict__ c_in,
+    const uint64_t* __restrict__ number_in, const uint32_t* __restrict__ need_mem_in,
+    const uint32_t* __restrict__ need_clk_in, uint32_t n_pods, uint32_t n_nodes,
+    const uint32_t* __restrict__ bsm, uint32_t bst, uint32_t K, uint32_t* __restrict__ wts) {
+  const uint32_t lane = lane_id();
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  const bool live = p < n_pods;
+  const uint64_t live_mask = ballot(live);
+  if (live_mask == 0ull) return;
+  uint32_t m = 0, c = 0, need_mem = 0, need_clk = 0;
+  uint64_t number = ~0ull;
+  if (live) {
+    m = m_in[p];
+    c = c_in[p];
+    number = number_in[p];
+    need_mem = need_mem_in[p];
+    need_clk = need_clk_in[p];
+  }
+  // the block K1's wave bounds (k1_block_n32's set-up)
+  const bool pm = live && need_mem > 0, pc = live && need_clk > 0;
+  const uint64_t pm_mask = ballot(pm), pc_mask = ballot(pc);
+  K1Wave w;
+  w.any_pm = pm_mask != 0ull;
+  w.all_pm = pm_mask == live_mask;
+  w.any_pc = pc_mask != 0ull;
+  w.all_pc = pc_mask == live_mask;
+  w.num_max = wave_max_u64(live ? number : 0ull);
+  w.num_min = wave_min_u64(live ? number : ~0ull);
+  const uint32_t nm_max = wave_max_u32(pm ? need_mem : 0u);
+  const uint32_t nm_min = wave_min_u32(pm ? need_mem : ~0u);
+  w.mpm_max = wave_max_u32(pm ? m : 0u);
+  w.mpm_min = wave_min_u32(pm ? m : ~0u);
+  w.nc_max = wave_max_u32(pc ? need_clk : 0u);
+  w.nc_min = wave_min_u32(pc ? need_clk : ~0u);
+  w.cpc_max = wave_max_u32(pc ? c : 0u);
+  const uint32_t cpc_min = wave_min_u32(pc ? c : ~0u);
+  w.m_max = wave_max_u32(live ? m : 0u);
+  w.m_min = wave_min_u32(live ? m : ~0u);
+  w.c_max = wave_max_u32(live ? c : 0u);
+  w.c_min = wave_min_u32(live ? c : ~0u);
+  w.c_uni = cpc_min == w.cpc_max;
+  w.hfs_all_ok = nm_max <= K;
+  w.hfs_none_ok = nm_min <= K;
+  w.bs_tn = kBsT + K + (w.hfs_none_ok && nm_min > 0u ? nm_min - 1u : 0u);
+  w.bs_ta = kBsT + (w.any_pm && w.hfs_all_ok && nm_max > 0u ? nm_max - 1u : 0u);
+  // 64 blocks spread over the snapshot, lane = block
+  const uint32_t nb = (n_nodes + kWave - 1) / kWave;
+  const uint32_t bi = nb >= kWave ? (uint32_t)(((uint64_t)lane * nb) / kWave) : lane;
+  const bool bv = bi < nb;
+  const K1BlockClass cls = k1_block_class(bsm + sum_index(bv ? bi : 0u, 0, bst), bv, w);
+  const uint64_t und = ballot(bv && cls.nreal > 0u && !cls.none && !cls.all);
+  if (lane == 0) wts[p >> 6] = 1u + (uint32_t)__builtin_popcountll(und);
+}
+
 __global__ __launch_bounds__(1024) void k_lpt_order(uint32_t* __restrict__ wts,
                                                     uint32_t n_waves, uint32_t n_pb,
                                                     uint32_t* __restrict__ order) {
@@ -1912,6 +2007,20 @@ hipError_t launch_lpt_order(uint32_t* wts, uint32_t n_pods, uint32_t* order, hip
   if (n_pb == 0 || n_pb > kLptMax) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(1024), 0, s, wts, n_waves, n_pb, order);
   return hipGetLastError();
+}
+
+// The block K1's heaviest-first pod-block order: k1_probe's per-wave weights into wts, ranked by
+// k_lpt_order into order (n_pb entries).
+hipError_t launch_k1_order(int K, const PodParams& pp, uint32_t n_pods, uint32_t n_nodes,
+                           uint32_t* wts, uint32_t* order, hipStream_t s) {
+  const uint32_t n_pb = (n_pods + kBlock - 1) / kBlock;
+  if (n_pb == 0 || n_pb > kLptMax || pp.bsum == nullptr || K < 1 || K > 16)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k1_probe, dim3(n_pb), dim3(kBlock), 0, s, pp.m_32, pp.c_32, pp.number,
+                     pp.need_mem, pp.need_clk, n_pods, n_nodes, pp.bsum, bsum_stride(K),
+                     (uint32_t)K, wts);
+  const hipError_t e = hipGetLastError();
+  return e != hipSuccess ? e : launch_lpt_order(wts, n_pods, order, s);
 }
 
 // K2 block bounds (yoda_layout.h kbub_*): one wave per 64-node block, lane = node.
@@ -4785,7 +4894,8 @@ hipError_t launch_k1(int K, Path path, const unsigned char* nodes, const unsigne
                                       pp.nwords, pp.lpt_w, pp.seed ? pp.g.tab : nullptr,         \
                                       pp.kbub_exact ? pp.kbub : nullptr, pp.kb_levels,           \
                                       reinterpret_cast<unsigned long long*>(pp.seed),          \
-                                      reinterpret_cast<unsigned long long*>(pp.cmask1), pp.ids))
+                                      reinterpret_cast<unsigned long long*>(pp.cmask1), pp.ids, \
+                                      pp.k1_order))
         if (sub == 1u) {
           if (stats) YODA_K1B(KK, true)
           else if (pp.one_model) YODA_K1B(KK, false, false)

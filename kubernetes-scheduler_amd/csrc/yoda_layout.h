@@ -381,6 +381,8 @@ struct PodParams {
   // lpt_order, the argmax block K2 visits its pod blocks in that order (nullptr: none)
   uint32_t* lpt_w = nullptr;
   const uint32_t* lpt_order = nullptr;
+  // the block K1's heaviest-first pod blocks (k1_probe + k_lpt_order; nullptr: launch order)
+  const uint32_t* k1_order = nullptr;
   // K2 pruning seeds [waves] u64 (zeroed with the block list before the block K1): a lower
   // bound on every live pod's best raw score under the G maxima, found by the block K1 on the
   // nodes every pod of the wave passes (nullptr: none); the snapshot's free levels kb_levels
