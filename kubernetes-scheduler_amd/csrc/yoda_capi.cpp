@@ -138,8 +138,8 @@ hipError_t launch_bsum_cn(const unsigned char* sum, uint32_t sum_stride, uint32_
                           uint32_t* bsum, uint32_t bsw, hipStream_t s);
 hipError_t launch_block_ub(int K, const uint32_t* sum2, const uint32_t* tab, uint32_t n_nodes,
                            uint32_t* out, const uint32_t* levels, hipStream_t s);
-hipError_t launch_block_dec(int K, const uint32_t* sum2, uint32_t n_nodes, uint32_t* out,
-                            const uint32_t* levels, MemTab mt, hipStream_t s);
+hipError_t launch_block_dec(int K, const uint32_t* sum2, const uint32_t* mix, uint32_t n_nodes,
+                            uint32_t* out, const uint32_t* levels, MemTab mt, hipStream_t s);
 hipError_t launch_gtable(int K, const uint32_t* sum2, const uint32_t* mix, uint32_t n_nodes,
                          const uint64_t* g_max,
                          uint32_t* tab, uint32_t* rcp_out, MemTab mt, hipStream_t s);
@@ -1361,7 +1361,8 @@ hipError_t build_block_ub(yoda_t* h) {
     e = launch_block_ub(h->K, h->k2sum.as<uint32_t>(), h->gtab.as<uint32_t>(), h->n_nodes,
                         h->kbub.as<uint32_t>(), h->kb_levels.as<uint32_t>(), h->stream);
   if (e == hipSuccess)
-    e = launch_block_dec(h->K, h->k2sum.as<uint32_t>(), h->n_nodes, h->kbdec.as<uint32_t>(),
+    e = launch_block_dec(h->K, h->k2sum.as<uint32_t>(), h->kmix.as<uint32_t>(), h->n_nodes,
+                         h->kbdec.as<uint32_t>(),
                          h->kb_levels.as<uint32_t>(), mt, h->stream);
   if (e == hipSuccess && h->perm_on) {
     e = h->kbub_p.ensure(bytes);
@@ -1370,7 +1371,8 @@ hipError_t build_block_ub(yoda_t* h) {
       e = launch_block_ub(h->K, h->k2sum_p.as<uint32_t>(), h->gtab_p.as<uint32_t>(), h->n_nodes,
                           h->kbub_p.as<uint32_t>(), h->kb_levels.as<uint32_t>(), h->stream);
     if (e == hipSuccess)
-      e = launch_block_dec(h->K, h->k2sum_p.as<uint32_t>(), h->n_nodes, h->kbdec_p.as<uint32_t>(),
+      e = launch_block_dec(h->K, h->k2sum_p.as<uint32_t>(), h->kmix_p.as<uint32_t>(), h->n_nodes,
+                           h->kbdec_p.as<uint32_t>(),
                            h->kb_levels.as<uint32_t>(), mt, h->stream);
   }
   if (e == hipSuccess) {
@@ -2354,12 +2356,56 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
             uint32_t wl[6] = {~0u, ~0u, ~0u, ~0u, ~0u, ~0u};
             uint32_t tmin[YODA_MAX_CARDS], tmax[YODA_MAX_CARDS];
             for (int t = 0; t < K; ++t) tmin[t] = ~0u, tmax[t] = 0;
+            uint32_t sat = ~0u;
+            // the healthy-card clocks of the block's nodes: clock, min / max count over the
+            // nodes seen so far (a node without the clock counts 0: hc_seen tracks it)
+            uint32_t hc_clk[4] = {0, 0, 0, 0}, hc_lo[4] = {0, 0, 0, 0}, hc_hi[4] = {0, 0, 0, 0};
+            uint32_t n_hc = 0;
+            bool hc_ok = true;
             for (uint32_t l = 0; l < 64 && blk * 64 + l < N; ++l) {
               const uint32_t i = order ? order[blk * 64 + l] : blk * 64 + l;
               const uint32_t* w = sum.data() + (size_t)i * SW;
               const uint64_t cn = (uint64_t)w[kSumCnLo] | ((uint64_t)w[kSumCnHi] << 32);
               const uint32_t meta = w[kSumMeta], nh = (meta >> 8) & 0xffu;
               const uint32_t* cr = clk_rng.data() + 4 * (size_t)i;
+              const uint32_t* s2n = sum2.data() + (size_t)i * (s2stride / 4);
+              const uint32_t* xn = x1m.data() + (size_t)i * (xstride / 4);
+              const uint32_t cnt = (s2n[kS2Meta] >> 8) & 0xffu;
+              const bool one = (meta & kSumUni4) && (meta & kSumUniTotal);
+              // saturation: 1 + the free of the last card (free order) where a prefix maximum
+              // changes (K1MixWord chg bits 1..K); one-model nodes of one total: card 0
+              uint32_t sat1 = w[kSumMrf1];
+              if (!one && cnt > 0) {
+                const uint32_t chg = xn[kX1Chg] & ((2u << K) - 2u);
+                const uint32_t jl = chg ? 30u - (uint32_t)__builtin_clz(chg) : 0u;  // bit jl+1
+                sat1 = s2n[kS2Fs + jl] + 1u;
+              }
+              sat = std::min(sat, sat1);
+              // healthy cards per clock (K1MixWord ch; more than 4 clocks or a clock beyond 16
+              // bits: no table)
+              if ((xn[kX1Chg] & kX1ChgMany) || (nh > 0 && cr[3] > 0xffffu)) hc_ok = false;
+              if (hc_ok) {
+                uint32_t mine[4] = {0, 0, 0, 0};  // this node's count per table entry
+                for (uint32_t e = 0; e < 4; ++e) {
+                  const uint32_t xw = xn[kX1Ch + e];
+                  if ((xw >> 16) == 0u) continue;
+                  const uint32_t ck = xw & 0xffffu;
+                  uint32_t k = 0;
+                  while (k < n_hc && hc_clk[k] != ck) ++k;
+                  if (k == n_hc) {
+                    if (n_hc == 4) { hc_ok = false; break; }
+                    hc_clk[k] = ck;
+                    hc_lo[k] = nreal == 0 ? ~0u : 0u;  // the nodes before lacked it
+                    hc_hi[k] = 0u;
+                    ++n_hc;
+                  }
+                  mine[k] = xw >> 16;
+                }
+                for (uint32_t k = 0; k < n_hc; ++k) {
+                  hc_lo[k] = std::min(hc_lo[k], mine[k]);
+                  hc_hi[k] = std::max(hc_hi[k], mine[k]);
+                }
+              }
               ++nreal;
               cmin = std::min(cmin, cn);
               cmax = std::max(cmax, cn);
@@ -2375,8 +2421,18 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
               mrmin = std::min(mrmin, w[kSumMrf1]);
               mrmax = std::max(mrmax, w[kSumMrf1]);
               const uint32_t mr = w[kSumMrf1];
-              const uint32_t v[6] = {w[kSumBw], w[kSumClock], w[kSumCore], mr - (mr != 0u ? 1u : 0u),
-                                     w[kSumPower], w[kSumTotal]};  // kMax* order
+              uint32_t v[6] = {w[kSumBw], w[kSumClock], w[kSumCore], mr - (mr != 0u ? 1u : 0u),
+                               w[kSumPower], w[kSumTotal]};  // kMax* order
+              if (!one && cnt > 0) {  // the all-card maxima (K1MixWord pm over every card)
+                const uint32_t a = xn[x1_pm((int)cnt - 1, 0)], b = xn[x1_pm((int)cnt - 1, 1)];
+                if (!(meta & kSumUni4)) {  // (16-bit halves: such snapshots keep them <= 65535)
+                  v[kMaxBw] = a >> 16;
+                  v[kMaxClock] = a & 0xffffu;
+                  v[kMaxCore] = b & 0xffffu;
+                  v[kMaxPower] = b >> 16;
+                }
+                v[kMaxTotal] = xn[x1_pm((int)cnt - 1, 2)];
+              }
               for (int f = 0; f < 6; ++f) {
                 if (wc[f] == 0 || v[f] > mx[f]) {
                   mx[f] = v[f];
@@ -2405,6 +2461,12 @@ int yoda_upload_nodes(yoda_t* h, const yoda_node_soa* nd, uint32_t node_offset, 
             o[kBsMrfMax] = mrmax;
             o[kBsNReal] = nreal;
             o[kBsNzt] = nzt;
+            o[kBsSat] = sat;
+            if (hc_ok) {
+              o[kBsFlags] |= kBsHcTab | (n_hc << 8);
+              for (uint32_t k = 0; k < n_hc; ++k)
+                o[kBsHc + k] = hc_clk[k] | (hc_lo[k] << 16) | (hc_hi[k] << 24);
+            }
             for (int f = 0; f < 6; ++f) {
               o[kBsMx + f] = mx[f];
               o[kBsWc + f] = wc[f];

@@ -677,32 +677,59 @@ struct K1BlockClass {
   bool none, all, allq;
   uint32_t nreal;  // the block's real nodes (0 for an invalid lane)
 };
+// mix_all = false: whole-block ALL for one-model blocks only (k1_probe's cost weights: with the
+// other blocks' ALL counted as per-node work the heaviest-first order comes out better --
+// mixed50 K1 0.91 vs 1.10 ms; the blocks they decide are not what makes a wave long)
 __device__ __forceinline__ K1BlockClass k1_block_class(const uint32_t* B, bool bv,
-                                                       const K1Wave& w) {
+                                                       const K1Wave& w, bool mix_all = true) {
   const uint32_t fl = B[64 * kBsFlags], ckmin = B[64 * kBsCkMin], ckmax = B[64 * kBsCkMax];
   const uint32_t cn_min = B[64 * kBsCnMin], cn_max = B[64 * kBsCnMax];
   const uint32_t nreal_w = B[64 * kBsNReal], t_none = B[64 * w.bs_tn], t_all = B[64 * w.bs_ta];
   const uint32_t hck_min = B[64 * kBsHckMin], hck_max = B[64 * kBsHckMax];
   const uint32_t nh_min = B[64 * kBsNhMin], nh_max = B[64 * kBsNhMax];
   const uint32_t mrf_min = B[64 * kBsMrfMin], mrf_max = B[64 * kBsMrfMax];
+  const uint32_t sat = B[64 * kBsSat];
+  uint32_t hcw[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) hcw[e] = B[64 * (kBsHc + e)];
   K1BlockClass r;
   r.nreal = bv ? nreal_w : 0u;
+  // the block's healthy cards of the wave's one scv/clock per node, min / max (hc table)
+  const bool tab = (fl & kBsHcTab) != 0u;
+  const uint32_t n_hc = (fl >> 8) & 7u;
+  uint32_t hc_lo = 0u, hc_hi = 0u;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const bool hit = ((uint32_t)e < n_hc) & ((hcw[e] & 0xffffu) == w.cpc_max);
+    hc_lo = hit ? (hcw[e] >> 16) & 0xffu : hc_lo;
+    hc_hi = hit ? hcw[e] >> 24 : hc_hi;
+  }
+  const bool one = (fl & kBsOneModel) != 0u;
   bool bnone = (cn_max != 0xffffffffu) & (w.num_min > (uint64_t)cn_max);
   bnone |= w.all_pm & (!w.hfs_none_ok | (t_none <= w.mpm_min));
   if (w.all_pc && w.c_uni) {
     // no healthy card of the block has the wave's clock (hc = 0 < need), or one-model nodes
-    // of that clock with too few healthy cards
+    // of that clock with too few healthy cards, or no node with enough of them (hc table)
     bnone |= (w.cpc_max < hck_min) | (w.cpc_max > hck_max) |
              (((fl & kBsUni4) != 0u) & (ckmin == ckmax) & (ckmin == w.cpc_max) &
-              (nh_max < w.nc_min));
+              (nh_max < w.nc_min)) |
+             (tab & (hc_hi < w.nc_min));
   }
-  bool ball = ((fl & kBsOneModel) != 0u) & (w.num_max <= (uint64_t)cn_min);
+  bool ball = (w.num_max <= (uint64_t)cn_min);
   ball &= !w.any_pm | (w.hfs_all_ok & (t_all > w.mpm_max));
   ball &= !w.any_pc |
-          (w.c_uni & (ckmin == ckmax) & (ckmin == w.cpc_max) & (nh_min >= w.nc_max));
-  r.allq = (ckmin >= w.c_max) & (mrf_min > w.m_max);
+          (w.c_uni & (one ? (ckmin == ckmax) & (ckmin == w.cpc_max) & (nh_min >= w.nc_max)
+                          : tab & (hc_lo >= w.nc_max)));
+  // every pod's qualifying cards (collection.go:46) reach each node's all-card maxima: every
+  // card passes the clock test and the scv/memory is below the saturation free (one-model
+  // nodes of one total: sat = mrf, the old rule)
+  r.allq = (ckmin >= w.c_max) & (sat > w.m_max);
   const bool noq = (ckmax < w.c_min) | (mrf_max <= w.m_min);
-  ball &= (r.allq | noq) & !bnone;
+  // (other blocks: no clock-only noq -- the seed's level bound assumes every card passes)
+  ball &= (r.allq | (one ? noq : mrf_max <= w.m_min)) & !bnone & (one | mix_all);
+#ifdef YODA_AB_NO_MIXALL  // (A/B build: whole-block ALL for one-model blocks only, as round 5)
+  ball &= one;
+#endif
   r.none = bnone & bv & (r.nreal > 0u);
   r.all = ball & bv & (r.nreal > 0u);
   return r;
@@ -762,7 +789,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   // (stats[15] >> 8 = the trace slots allocated: every slot index is bounded by it)
   const bool trace = STATS && (stats[15] & 0xffull) == 2ull;
   const uint64_t t_start = STATS ? wall_clock64() : 0ull;
-  uint32_t npart = 0;
+  uint32_t npart = 0, nblk = 0;  // (trace: PART nodes, blocks classified node by node)
 
   uint32_t m = 0, c = 0, need_mem = 0, need_clk = 0;
   uint64_t number = ~0ull;
@@ -885,6 +912,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
   // (nxt: the block node_block visits next, whose summary words are loaded here -- the
   // caller loaded nb's before the first call; ~0u: none)
   auto node_block = [&](uint32_t nb, uint32_t nxt) {
+    if (STATS) ++nblk;
     const uint32_t n = nb + lane;
     const bool valid = n < n1;
     // this block's tile of summaries (nb is a multiple of 64): word w at s[64 w]
@@ -1322,7 +1350,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
     unsigned long long* tr = stats + 16 + 4 * slot1;
     tr[0] = t_start;
     tr[1] = wall_clock64();
-    tr[2] = npart;
+    tr[2] = npart | ((unsigned long long)nblk << 32);
     tr[3] = (t_setup - t_start) | ((t_pass - t_start) << 32);
   }
   if constexpr (WIT) {
@@ -1608,7 +1636,7 @@ __global__ __launch_bounds__(kBlock) void k1_probe(
   const uint32_t nb = (n_nodes + kWave - 1) / kWave;
   const uint32_t bi = nb >= kWave ? (uint32_t)(((uint64_t)lane * nb) / kWave) : lane;
   const bool bv = bi < nb;
-  const K1BlockClass cls = k1_block_class(bsm + sum_index(bv ? bi : 0u, 0, bst), bv, w);
+  const K1BlockClass cls = k1_block_class(bsm + sum_index(bv ? bi : 0u, 0, bst), bv, w, false);
   const uint64_t und = ballot(bv && cls.nreal > 0u && !cls.none && !cls.all);
   if (lane == 0) wts[p >> 6] = 1u + (uint32_t)__builtin_popcountll(und);
 }
@@ -2085,6 +2113,7 @@ __global__ __launch_bounds__(kWave) void k_block_ub(const uint32_t* __restrict__
 // bound's reciprocals multiply.
 template <int K>
 __global__ __launch_bounds__(kWave) void k_block_dec(const uint32_t* __restrict__ sum2,
+                                                     const uint32_t* __restrict__ mix,
                                                      uint32_t n_nodes, uint32_t* __restrict__ out,
                                                      const uint32_t* __restrict__ levels,
                                                      MemTab mt) {
@@ -2111,13 +2140,31 @@ __global__ __launch_bounds__(kWave) void k_block_dec(const uint32_t* __restrict_
     co = w2(kS2Core);
     pw = w2(kS2Power);
   }
+  // A node of several GPU models (no kSumUni4): each card's model terms are at most those of
+  // the node's largest card values (shared_M is non-decreasing in each), so the bound holds
+  // with them; its qualifying cards for a pod are a subset of the cards with free >= the pod's
+  // scv/memory (collection.go:46 adds the clock test), so ql / fl / tl bound them as well.
+  const bool mixed = v && (meta & kSumUni4) == 0u;
+  if (mixed && mix != nullptr) {
+    const uint32_t MS = mix_stride(K);
+    auto x = [&](uint32_t word) { return mix[sum_index(n, word, MS)]; };
+    bw = ck = co = pw = 0u;
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const bool real = (uint32_t)t < cnt;
+      bw = max(bw, real ? x(mix_word(kMixBw, t, K)) : 0u);
+      ck = max(ck, real ? x(mix_word(kMixCk, t, K)) : 0u);
+      co = max(co, real ? x(mix_word(kMixCo, t, K)) : 0u);
+      pw = max(pw, real ? x(mix_word(kMixPw, t, K)) : 0u);
+    }
+  }
 #pragma unroll
   for (int t = 0; t < K; ++t) {
     const bool real = v && (uint32_t)t < cnt;
     fs[t] = real ? w2(kS2Fs + (uint32_t)t) : 0u;
     ts[t] = real ? w2(kS2Fs + (uint32_t)K + (uint32_t)t) : 0u;
   }
-  const bool ok = ballot(v && (meta & kSumUni4) == 0u) == 0ull;
+  const bool ok = ballot(mixed && mix == nullptr) == 0ull;
   const double st = wave_max_f64(stat);
   const uint32_t mbw = wave_max_u32(bw), mck = wave_max_u32(ck), mco = wave_max_u32(co),
                  mpw = wave_max_u32(pw);
@@ -2150,16 +2197,16 @@ __global__ __launch_bounds__(kWave) void k_block_dec(const uint32_t* __restrict_
   }
 }
 
-hipError_t launch_block_dec(int K, const uint32_t* sum2, uint32_t n_nodes, uint32_t* out,
-                            const uint32_t* levels, MemTab mt, hipStream_t s) {
+hipError_t launch_block_dec(int K, const uint32_t* sum2, const uint32_t* mix, uint32_t n_nodes,
+                            uint32_t* out, const uint32_t* levels, MemTab mt, hipStream_t s) {
   if (n_nodes == 0) return hipSuccess;
   const dim3 grid((n_nodes + 63) / 64);
   switch (K) {
-    case 1: hipLaunchKernelGGL(k_block_dec<1>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, mt); break;
-    case 2: hipLaunchKernelGGL(k_block_dec<2>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, mt); break;
-    case 4: hipLaunchKernelGGL(k_block_dec<4>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, mt); break;
-    case 8: hipLaunchKernelGGL(k_block_dec<8>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, mt); break;
-    case 16: hipLaunchKernelGGL(k_block_dec<16>, grid, dim3(kWave), 0, s, sum2, n_nodes, out, levels, mt); break;
+    case 1: hipLaunchKernelGGL(k_block_dec<1>, grid, dim3(kWave), 0, s, sum2, mix, n_nodes, out, levels, mt); break;
+    case 2: hipLaunchKernelGGL(k_block_dec<2>, grid, dim3(kWave), 0, s, sum2, mix, n_nodes, out, levels, mt); break;
+    case 4: hipLaunchKernelGGL(k_block_dec<4>, grid, dim3(kWave), 0, s, sum2, mix, n_nodes, out, levels, mt); break;
+    case 8: hipLaunchKernelGGL(k_block_dec<8>, grid, dim3(kWave), 0, s, sum2, mix, n_nodes, out, levels, mt); break;
+    case 16: hipLaunchKernelGGL(k_block_dec<16>, grid, dim3(kWave), 0, s, sum2, mix, n_nodes, out, levels, mt); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

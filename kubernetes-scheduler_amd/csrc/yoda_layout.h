@@ -125,13 +125,21 @@ __host__ __device__ constexpr uint32_t k2sum_stride(int k) { return 32u + 8u * (
 //   mx[6]   per MaxValue field (kMax* order) the max over the nodes of the contribution a
 //           one-model node makes when some card qualifies (its model values, max free)
 //   wc[6]   nodes reaching mx[f];  wl[6]  the lowest of them (offset in the block)
+//   sat      the min over the nodes of 1 + the free of the card (in descending free order)
+//            where the prefix maxima of the six MaxValue fields reach the node's all-card
+//            maxima: a pod with scv/memory m < sat (and scv/clock <= every card's clock)
+//            qualifies that prefix, so every node contributes its all-card maxima (one-model
+//            nodes of one TotalMemory: 1 + max free, as mrf)
+//   hc[4]    per distinct HEALTHY-card clock of the block (flags: kBsHcTab, entries << 8):
+//            clock | (min over the nodes of their healthy cards of that clock << 16) | (max << 24)
 //   tmin[K], tmax[K]    bounds of hfs[k] (K1Sum: 1 + free of the k-th healthy card by free)
+// mx[6] of a node that is not one model with one TotalMemory: its all-card maxima.
 enum BlockSumWord {
   kBsCnMin = 0, kBsCnMax = 1, kBsFlags = 2, kBsCkMin = 3, kBsCkMax = 4, kBsHckMin = 5,
   kBsHckMax = 6, kBsNhMin = 7, kBsNhMax = 8, kBsMrfMin = 9, kBsMrfMax = 10, kBsNReal = 11,
-  kBsNzt = 12, kBsMx = 13, kBsWc = 19, kBsWl = 25, kBsT = 31
+  kBsNzt = 12, kBsMx = 13, kBsWc = 19, kBsWl = 25, kBsSat = 31, kBsHc = 32, kBsT = 36
 };
-constexpr uint32_t kBsOneModel = 1u, kBsUni4 = 2u;
+constexpr uint32_t kBsOneModel = 1u, kBsUni4 = 2u, kBsHcTab = 4u;
 __host__ __device__ constexpr uint32_t bsum_stride(int k) { return 4u * (kBsT + 2u * (uint32_t)k); }
 
 // K2 block bounds (N32 path; waves whose reciprocals are the G table's): per 64-node block of a

@@ -49,7 +49,8 @@ used = tr[:, 1] > 0
 t = tr[used].astype(np.int64)
 dur = (t[:, 1] - t[:, 0]) / 100.0  # us at 100 MHz
 span = (t[:, 1].max() - t[:, 0].min()) / 100.0
-npart = t[:, 2]
+npart = t[:, 2] & 0xffffffff
+nblk = t[:, 2] >> 32  # K1: blocks classified node by node
 q = lambda v, x: float(np.percentile(v, x)) if len(v) else None  # noqa: E731
 out = {"kernel": kern, "tasks": int(used.sum()), "span_us": span,
        "mean_concurrency": float(dur.sum() / span) if span > 0 else None,
@@ -61,6 +62,16 @@ out = {"kernel": kern, "tasks": int(used.sum()), "span_us": span,
                      if (npart > 0).any() else None, "mean_npart": float(npart[npart > 0].mean())
                      if (npart > 0).any() else None},
        "corr_dur_npart": float(np.corrcoef(dur, npart)[0, 1]) if len(dur) > 2 else None}
+if kern == "k1" and len(dur) > 3:
+    # least squares: task duration ~ a + b * node-by-node blocks + c * PART nodes
+    A = np.stack([np.ones(len(dur)), nblk, npart], axis=1).astype(np.float64)
+    coef = np.linalg.lstsq(A, dur, rcond=None)[0]
+    out["fit_us"] = {"base": float(coef[0]), "per_node_block": float(coef[1]),
+                     "per_part_node": float(coef[2])}
+    out["node_blocks"] = {"mean": float(nblk.mean()), "sum": int(nblk.sum())}
+    out["span_share"] = {"base": float(coef[0] * len(dur) / dur.sum()),
+                         "node_blocks": float(coef[1] * nblk.sum() / dur.sum()),
+                         "part": float(coef[2] * npart.sum() / dur.sum())}
 # phases (the trace's word 3): K1 set-up end | block-pass end << 32; K2 flags | set-up end << 16 |
 # block-list walk end << 40 (ticks after the task's start)
 w3 = tr[used][:, 3].astype(np.uint64)
@@ -77,6 +88,13 @@ if z.any():
     out["phase_us_mean_npart0"] = {"setup": float(t_set[z].mean()),
                                    "pass": float((t_pass[z] - t_set[z]).mean()),
                                    "epilogue": float((dur[z] - t_pass[z]).mean())}
+if kern == "k2":  # task time by wave kind: G waves, decoupled-bound (non-G) waves, others
+    fl = w3 & np.uint64(0xffff)
+    for name, sel in (("g", (fl & np.uint64(2)) != 0), ("dec", (fl & np.uint64(4)) != 0),
+                      ("other", (fl & np.uint64(6)) == 0)):
+        out["by_kind_" + name] = {"tasks": int(sel.sum()), "dur_sum_us": float(dur[sel].sum()),
+                                  "mean_us": float(dur[sel].mean()) if sel.any() else None,
+                                  "npart_sum": int(npart[sel].sum())}
 # start-time profile: how many tasks start in each tenth of the span
 st = (t[:, 0] - t[:, 0].min()) / 100.0
 out["starts_by_tenth"] = np.histogram(st, bins=10, range=(0, span))[0].tolist()
