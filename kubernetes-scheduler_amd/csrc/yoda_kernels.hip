@@ -26,7 +26,7 @@
 // (tools/build_ab.sh), never into a release libyoda.
 #if !defined(YODA_AB_KNOBS) &&                                                         \
     (defined(YODA_ABL_K1_NOGEN) || defined(YODA_ABL_K1_NOHC) || defined(YODA_ABL_K1_NOPART) || \
-     defined(YODA_ABL_K1_NOBS) || defined(YODA_ABL_K1_NOBM) || defined(YODA_ABL_K1_NOLEAN))
+     defined(YODA_ABL_K1_NOBS) || defined(YODA_ABL_K1_NOBM))
 #error "YODA_ABL_* ablations give wrong results: build them with -DYODA_AB_KNOBS (tools/build_ab.sh)"
 #endif
 
@@ -739,9 +739,13 @@ template <int K, bool STATS, bool MIX = true, bool WIT = false, int SUB = 1>
 #ifndef YODA_K1_WAVES
 #define YODA_K1_WAVES 6  // (7: 9 VGPRs spilled, ~90 MB of scratch writes per launch; r05j)
 #endif
-// (waves per SIMD: 6 for one-model tiles -- no VGPR spills; 7 with the mixed-model tiles, whose
-// loop is faster there despite spilling: mixed50 K1 1.56 vs 1.71 ms, profiles/r05/y/ab.txt)
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 : (K >= 16 ? 5 : (MIX ? 7 : YODA_K1_WAVES))))) void k1_block_n32(
+// (waves per SIMD: 6 for one-model tiles -- no VGPR spills; 6 with the mixed-model tiles too
+// since their PART nodes are staged in LDS (round 6): mixed50 K1 0.75 vs 0.80 ms at 7 waves,
+// profiles/r06/mixed/ab_staged.txt; 7 paid while the per-node loop was a chain of scalar loads)
+#ifndef YODA_K1_MIX_WAVES
+#define YODA_K1_MIX_WAVES 6
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 : (K >= 16 ? 5 : (MIX ? YODA_K1_MIX_WAVES : YODA_K1_WAVES))))) void k1_block_n32(
     const unsigned char* __restrict__ nodes, const unsigned char* __restrict__ sum,
     const uint32_t* __restrict__ sum2w, const uint32_t* __restrict__ mixw,
     const uint32_t* __restrict__ x1w,
@@ -1183,20 +1187,92 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIT ? 4 
       }
     }
     part_b &= ~rec_b;
+#ifndef YODA_K1_LEAN_GLOBAL
+    // Other PART nodes (several GPU models, or several TotalMemory values): their cards staged
+    // in LDS, lane = node, from the block's tiles (K2 summary frees / totals in free order,
+    // K1MixWord cards, the health bits) -- one memory round trip per batch of nodes -- then
+    // read by the per-pod pass with broadcast ds_read_b128s.  (Before: k1_node_lean's per-card
+    // loop over the node record, ~2K dependent scalar loads per node: mixed50 K1 0.88 ms.)
+    // The area is the rows / records above, free again here.  Per node: {CardNumber lo, hi,
+    // health bits | zero-total << 31, 0}, then per card {free, clock | bw << 16, total,
+    // core | power << 16} (16-bit halves: such snapshots keep those fields <= 55738).
+    if constexpr (MIX) {
+      constexpr uint32_t XN = 4u * (uint32_t)K + 4u;
+      constexpr uint32_t NBAT = (RECS + kWave * REC) / XN;
+      static_assert(NBAT >= 1u, "LDS area");
+      while (part_b) {
+        uint64_t bat = part_b;
+        if ((uint32_t)__builtin_popcountll(bat) > NBAT) {  // the lowest NBAT nodes
+          uint64_t t = bat;
+          for (uint32_t k = 0; k < NBAT; ++k) t &= t - 1;
+          bat &= ~t;
+        }
+        part_b &= ~bat;
+        if ((bat >> lane) & 1ull) {
+          const uint32_t slot = (uint32_t)__builtin_popcountll(bat & ((1ull << lane) - 1ull));
+          uint32_t* r = lds + slot * XN;
+          const uint32_t* s2 = sum2w + sum_index(nb, 0, S2) + lane;
+          const uint32_t hm = mixw[sum_index(nb, 0, MS) + lane + 64u * mix_hm(K)];
+          *reinterpret_cast<uint4*>(r) =
+              make_uint4(w0.x, w0.y, hm | ((meta & kSumZeroTotal) ? 0x80000000u : 0u), 0u);
+          // (two cards' words in flight per step: more would spill -- the kernel runs at its
+          // VGPR budget)
+#pragma unroll 2
+          for (int t = 0; t < K; ++t)
+            *reinterpret_cast<uint4*>(r + 4 + 4 * t) =
+                make_uint4(s2[64 * (kS2Fs + t)], xw[64 * x1_cd(t, 0, K)],
+                           s2[64 * (kS2Fs + K + t)], xw[64 * x1_cd(t, 1, K)]);
+        }
+        uint32_t slot = 0;
+        while (bat) {
+          const uint32_t j = (uint32_t)__builtin_ctzll(bat);
+          bat &= bat - 1;
+          const uint32_t* r = lds + (slot++) * XN;
+          const uint4 h = *reinterpret_cast<const uint4*>(r);
+          // PodFitsMemory / PodFitsClock counts (filter.go:52-58) from {free, clock | bw}
+          uint32_t cm = 0, cc = 0;
+#pragma unroll 4
+          for (int t = 0; t < K; ++t) {
+            const uint2 fa = *reinterpret_cast<const uint2*>(r + 4 + 4 * t);
+            const uint32_t ht = (h.z >> t) & 1u;
+            cm += (uint32_t)(fa.x >= m) & ht;
+            cc += (uint32_t)((fa.y & 0xffffu) == c) & ht;
+          }
+          const uint64_t cnj = (uint64_t)h.x | ((uint64_t)h.y << 32);
+          const bool f = live & (number <= cnj) & (cm >= need_mem) & (cc >= need_clk);
+          nf += f ? 1u : 0u;
+          nz += (f & ((h.z >> 31) != 0u)) ? 1u : 0u;
+          const uint64_t b = ballot(f);
+          if (b != 0ull) {  // the maxima over the qualifying cards (collection.go:46: no health
+                            // check, clock >= the pod's), feasible lanes only
+#pragma unroll 2
+            for (int t = 0; t < K; ++t) {
+              const uint4 cd = *reinterpret_cast<const uint4*>(r + 4 + 4 * t);
+              const bool q = f & (cd.x >= m) & ((cd.y & 0xffffu) >= c);
+              mx[kMaxBw] = max(mx[kMaxBw], q ? cd.y >> 16 : 0u);
+              mx[kMaxClock] = max(mx[kMaxClock], q ? cd.y & 0xffffu : 0u);
+              mx[kMaxCore] = max(mx[kMaxCore], q ? cd.w & 0xffffu : 0u);
+              mx[kMaxPower] = max(mx[kMaxPower], q ? cd.w >> 16 : 0u);
+              mx[kMaxFree] = max(mx[kMaxFree], q ? cd.x : 0u);
+              mx[kMaxTotal] = max(mx[kMaxTotal], q ? cd.z : 0u);
+            }
+          }
+          set_lane(lo, hi, b, j);
+        }
+      }
+    }
+#else
     while (MIX && part_b) {  // mixed-model nodes: the exact per-card predicates from the record
       const int j = __builtin_ctzll(part_b);
       part_b &= part_b - 1;
-#ifdef YODA_ABL_K1_NOLEAN
-      const bool f = false;
-#else
       // (the record by the node's local id: a block-grouped run reads positions, ids)
       const uint32_t rid = ids ? ids[nb + (uint32_t)j] : nb + (uint32_t)j;
       const bool f = k1_node_lean<K>(nodes + (size_t)rid * NS, m, c, number,
                                      need_mem, need_clk, mx, nf, nz) && live;
-#endif
       const uint64_t b = ballot(f);
       set_lane(lo, hi, b, (uint32_t)j);
     }
+#endif
     // sparse masks: the block's (nz, full) words always, a node's own mask only when it is
     // neither empty nor the wave's live mask (the ALL / NONE nodes cost no mask traffic)
     const uint64_t mine = ((uint64_t)hi << 32) | lo;

@@ -166,3 +166,48 @@ def test_config4_declared_size(dev, mode):
     got = dev.eval(pods, mode)
     want = oracle.schedule(nodes, pods, mode, threads=16)
     assert_same(got, want, mode)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_mixed_block_rules(dev, seed):
+    """The whole-block rules for blocks of mixed-model nodes (k1_block_class: ALL past the
+    prefix-maxima saturation, NONE / ALL from the per-clock healthy counts; the decoupled K2
+    bounds from each node's largest card values) on the cases that must keep them off:
+    blocks with more than 4 healthy-card clocks (no table), clocks beyond 16 bits on one-model
+    nodes, nodes without cards, scv/number "0" with a clock label no card has, pods without
+    scv/memory (every card qualifies), every pod against the oracle."""
+    rng = np.random.default_rng(7300 + seed)
+    n, p = 4096, 2400
+    nodes = synth.make_nodes(n, int(rng.integers(1 << 30)))
+    nodes = synth.mixed_models(nodes, 0.7, seed=int(rng.integers(1 << 30)))
+    clocks6 = np.array([1200, 1300, 1410, 1500, 1600, 1755], dtype=np.uint64)
+    real = np.arange(8)[None, :] < nodes.card_count[:, None]
+    six = np.arange(n) < 1024  # the first 16 blocks: six clocks among their cards
+    nodes.card_clock[six] = np.where(real[six], clocks6[rng.integers(0, 6, size=(1024, 8))], 0)
+    empty = rng.random(n) < 0.02  # CardList empty, CardNumber kept
+    for a in (nodes.card_free_memory, nodes.card_total_memory, nodes.card_clock,
+              nodes.card_bandwidth, nodes.card_core, nodes.card_power, nodes.card_healthy):
+        a[empty] = 0
+    nodes.card_count[empty] = 0
+    nodes = nodes.normalized()
+    pods = synth.make_pods(p, int(rng.integers(1 << 30)))
+    pods.has_memory[rng.random(p) < 0.4] = 0
+    pods.memory[pods.has_memory == 0] = 0
+    zero = rng.random(p) < 0.1  # scv/number "0"
+    pods.has_number[zero] = 1
+    pods.number[zero] = 0
+    odd = rng.random(p) < 0.1  # a clock label no card has
+    pods.has_clock[odd] = 1
+    pods.clock[odd] = 1999
+    pods = pods.normalized()
+    want = oracle.schedule(nodes, pods, MODE_SCV, threads=8)
+    dev.upload_nodes(nodes)
+    assert dev.path == "n32"
+    assert_same(dev.eval(pods, MODE_SCV), want)
+    # a one-model fleet whose clocks exceed 16 bits (no per-clock table) beside it
+    big, bpods = synth.make_config(2, pods=1200, nodes=3000)
+    big.card_clock[:] = np.where(big.card_clock > 0, big.card_clock * 100, 0)
+    bpods.clock[:] = np.where(bpods.has_clock == 1, bpods.clock * 100, 0)
+    big, bpods = big.normalized(), bpods.normalized()
+    dev.upload_nodes(big)
+    assert_same(dev.eval(bpods, MODE_SCV), oracle.schedule(big, bpods, MODE_SCV, threads=8))
