@@ -62,7 +62,7 @@ def k2_unique_bytes(P: int, N: int, k: int, path: str, mode: int) -> int:
 def k1_unique_bytes(P: int, N: int, k: int, path: str, mode: int) -> int:
     """Algorithmic bytes of ONE K1 launch (Filter + PreScore maxima): per node
     its K1 summary (N32: 48 + 4K B rounded to 16; F64/U64: the record, 32 + 48K B), per
-    64-node block its bound summary (N32: 4 (31 + 2K) B), per pod the five Filter inputs it
+    64-node block its bound summary (N32: 4 (36 + 2K) B), per pod the five Filter inputs it
     reads (scv/memory and scv/clock as u32, scv/number u64, need-memory and need-clock flags
     u32: 24 B) and the stage's outputs (6 u64 maxima + feasible and zero-total counts: 56 B).
     The chunk partials, masks and block lists K1 writes for k_reduce1 / K2 are intermediates
@@ -71,7 +71,7 @@ def k1_unique_bytes(P: int, N: int, k: int, path: str, mode: int) -> int:
         return P * 56
     if path == "n32":
         per_node = (48 + 4 * k + 15) // 16 * 16
-        blocks = (N + 63) // 64 * 4 * (31 + 2 * k)
+        blocks = (N + 63) // 64 * 4 * (36 + 2 * k)
     else:
         per_node, blocks = 32 + 48 * k, 0
     return N * per_node + blocks + P * (24 + 56)
