@@ -211,3 +211,24 @@ def test_mixed_block_rules(dev, seed):
     big, bpods = big.normalized(), bpods.normalized()
     dev.upload_nodes(big)
     assert_same(dev.eval(bpods, MODE_SCV), oracle.schedule(big, bpods, MODE_SCV, threads=8))
+
+
+def test_consecutive_runs_deferred_pod_arrays(dev):
+    """yoda_run's fast path uploads only the pod arrays its kernels read first and copies the
+    rest after them (pods_complete): consecutive runs on different batches, a bitmask run and a
+    Mode-B run in between (both read the deferred arrays) and a repeated batch must each match
+    the oracle (no stale deferred arrays)."""
+    nodes, _ = synth.make_config(2, pods=10, nodes=4000)
+    dev.upload_nodes(nodes)
+    batches = [synth.make_pods(n, s) for n, s in ((3000, 41), (1700, 42), (4100, 43))]
+    want = [oracle.schedule(nodes, b, MODE_SCV, threads=8) for b in batches]
+    for i in (0, 1, 2, 0, 2):
+        dev.upload_pods(batches[i])
+        dev.run(MODE_SCV)
+        assert_same(dev.download(), want[i])
+        if i == 1:  # paths that read the deferred arrays, between two fast runs
+            dev.run(MODE_SCV, bitmask=True)
+            assert_same(dev.download(), want[i])
+            dev.run(MODE_DISKIO)
+            assert_same(dev.download(), oracle.schedule(nodes, batches[i], MODE_DISKIO, threads=8),
+                        MODE_DISKIO)

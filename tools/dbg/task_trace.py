@@ -46,6 +46,11 @@ y.class_stats(False)
 tr = y.k2_trace(slots)
 y.close()
 used = tr[:, 1] > 0
+# slots another launch of the batch wrote and the last one did not (a different grid shape):
+# keep the tasks of the last launch only (those that started within 5 ms of the last start)
+if used.any():
+    t0_last = tr[used][:, 0].astype(np.int64).max()
+    used &= tr[:, 0].astype(np.int64) >= t0_last - 500000
 t = tr[used].astype(np.int64)
 dur = (t[:, 1] - t[:, 0]) / 100.0  # us at 100 MHz
 span = (t[:, 1].max() - t[:, 0].min()) / 100.0
