@@ -794,9 +794,12 @@ int capacity(yoda_t* h, int which, int mode) {
 }
 
 void plan_chunks(yoda_t* h, int mode, uint32_t n_pods, uint32_t n_nodes) {
-  // K1's partials are 32 B a (pod, chunk) and its reduce reads them all: fewer rounds
+  // K1's partials are 24 B a (pod, chunk) and its reduce reads them all, but with the
+  // heaviest-first pod blocks and the lane = block pass a K1 task is short and the tail is
+  // set by the task size: 8 rounds (config 3 K1 0.199 -> 0.182 ms, mixed50 / bytes / greedy
+  // neutral or better; 10: 0.185, 12: 0.201, 16: 0.241 ms; profiles/r06/rounds1/)
   static const uint32_t r1 = std::max<uint32_t>(1, YODA_KNOB("YODA_CHUNK_ROUNDS1",
-                                                           YODA_KNOB("YODA_CHUNK_ROUNDS", 6)));
+                                                           YODA_KNOB("YODA_CHUNK_ROUNDS", 8)));
   static const uint32_t r2 = std::max<uint32_t>(1, YODA_KNOB("YODA_CHUNK_ROUNDS2",
                                                            YODA_KNOB("YODA_CHUNK_ROUNDS", 8)));
   plan_chunks_for((uint32_t)capacity(h, 1, mode), r1, n_pods, n_nodes, &h->C1, &h->chunk1);
