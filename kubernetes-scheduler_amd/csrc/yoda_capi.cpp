@@ -796,13 +796,18 @@ int capacity(yoda_t* h, int which, int mode) {
 void plan_chunks(yoda_t* h, int mode, uint32_t n_pods, uint32_t n_nodes) {
   // K1's partials are 24 B a (pod, chunk) and its reduce reads them all, but with the
   // heaviest-first pod blocks and the lane = block pass a K1 task is short and the tail is
-  // set by the task size: 8 rounds (config 3 K1 0.199 -> 0.182 ms, mixed50 / bytes / greedy
-  // neutral or better; 10: 0.185, 12: 0.201, 16: 0.241 ms; profiles/r06/rounds1/)
-  static const uint32_t r1 = std::max<uint32_t>(1, YODA_KNOB("YODA_CHUNK_ROUNDS1",
-                                                           YODA_KNOB("YODA_CHUNK_ROUNDS", 8)));
+  // set by the task size: 8 rounds while the chunks stay few enough for the chunk masks
+  // (C1 <= kPlainReduceChunks; config 3 K1 0.199 -> 0.182 ms, mixed50 / bytes / greedy neutral
+  // or better; 10: 0.185, 12: 0.201, 16: 0.241 ms), else 6 (a 50k / 25k / 12.5k-pod batch,
+  // one pod-sharded rank: K1 0.137 / 0.139 / 0.138 ms at 6 against 0.155 / 0.140 / 0.157 at
+  // 8); profiles/r06/rounds1/.  YODA_CHUNK_ROUNDS1 (A/B knob) fixes the rounds.
+  static const uint32_t r1_knob = YODA_KNOB("YODA_CHUNK_ROUNDS1", YODA_KNOB("YODA_CHUNK_ROUNDS", 0));
   static const uint32_t r2 = std::max<uint32_t>(1, YODA_KNOB("YODA_CHUNK_ROUNDS2",
                                                            YODA_KNOB("YODA_CHUNK_ROUNDS", 8)));
-  plan_chunks_for((uint32_t)capacity(h, 1, mode), r1, n_pods, n_nodes, &h->C1, &h->chunk1);
+  const uint32_t cap1 = (uint32_t)capacity(h, 1, mode);
+  plan_chunks_for(cap1, r1_knob ? r1_knob : 8u, n_pods, n_nodes, &h->C1, &h->chunk1);
+  if (!r1_knob && h->C1 > kPlainReduceChunks)
+    plan_chunks_for(cap1, 6u, n_pods, n_nodes, &h->C1, &h->chunk1);
   // YODA_K1_MAX_CHUNKS (A/B knob, default off): at most that many K1 chunks, so that small
   // batches keep their partials (and k_reduce1's reads) few
   static const uint32_t c1_max = YODA_KNOB("YODA_K1_MAX_CHUNKS", 0);
