@@ -5190,8 +5190,10 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
       return rc;
     // the lists' depth: KT from the chunks, merged deeper where the block kernels run
     // (k_topk_merge_deep: exact as far as they reach; YODA_GREEDY_CAP_DEPTH, A/B knob: 32 /
-    // 64 / 128, 0 = KT)
-    static const uint32_t cap_depth = YODA_KNOB("YODA_GREEDY_CAP_DEPTH", 64);
+    // 64 / 128, 0 = KT).  128 with the exact-fallback scan below (windows 1558 -> 822,
+    // capacity 0.97 -> 0.89-0.90 s; 128 alone 0.98 s, the scan alone 0.92-0.93 s;
+    // profiles/r06/greedy_scan/)
+    static const uint32_t cap_depth = YODA_KNOB("YODA_GREEDY_CAP_DEPTH", 128);
     uint32_t KD = KT;
     // pinned staging of the window's outputs, in window order (k_window_out writes them there
     // from the sorted order in one launch): counts | maxima | wit | top scores | top nodes
@@ -5271,9 +5273,12 @@ static int greedy_capacity(yoda_t* h, const yoda_pod_soa* pods, int32_t* pick) {
       if ((rc = yoda_gs_resolve(g, &next))) return fail(h, rc, "greedy: resolve");
       // YODA_GREEDY_FAIL_DIV (A/B knob): one exact evaluation allowed per that many resolved pods
       static const uint32_t rate = YODA_KNOB("YODA_GREEDY_FAIL_DIV", 0);
-      // YODA_GREEDY_CAP_SCAN=<n> (A/B knob): fall back exactly (instead of restarting) when at
-      // most YODA_GREEDY_CAP_SCAN_MAX of the next n window pods are uncertified already
-      static const uint32_t scan_n = YODA_KNOB("YODA_GREEDY_CAP_SCAN", 0);
+      // fall back exactly (instead of restarting the window) when at most
+      // YODA_GREEDY_CAP_SCAN_MAX of the next YODA_GREEDY_CAP_SCAN window pods are uncertified
+      // already (A/B knobs; 64 / 1: a restart re-runs the window's kernels for one pod whose
+      // witness was lost while its successors still hold theirs; 32 / 128 / 256: 0.97 / 0.92 /
+      // 0.91 s, 0: 0.97 s)
+      static const uint32_t scan_n = YODA_KNOB("YODA_GREEDY_CAP_SCAN", 64);
       static const uint32_t scan_max = YODA_KNOB("YODA_GREEDY_CAP_SCAN_MAX", 1);
       if (next >= wn) break;
       bool fallback = false;
